@@ -1,0 +1,329 @@
+#!/usr/bin/env python3
+"""Benchmark of the hot path: batched IFOPT eval_g + eval_jac_g of CentroidalPlanner instances.
+
+One step = one pass of the hot path over one batch resident in HBM: the eval kernel (values +
+CSR Jacobian values of every instance) plus the per-shard residual norms; with N > 1 ranks the
+norms are all-gathered over RCCL (asynchronously, on the collective stream).  Instances shard
+across ranks with no data-path exchange: per-rank batch is fixed -> weak scaling.
+
+Default workload = BASELINE.json configs[1]: 4-contact Ground env, batch 65,536 per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config ground4|sq8|mixed16|ground4_1m|none4]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Rank 0 prints one JSON line.  Fields beyond the driver contract:
+  roofline      dominant kernel (cpl_eval_kernel): algorithmic bytes per launch / mean launch
+                duration from HIP events on the launch stream; traffic = HBM bytes per launch from
+                rocprofv3 PMC passes (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE)
+  cpu_baseline  the oracle (CPU restatement, "port") on the host cores, bounded sample
+  target_1m     the north-star point (1,048,576 x 4 contacts, Ground) on the same GPU
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "NLP eval_g+eval_jac_g throughput (rows/sec) at batch*contacts; HBM GB/s vs peak"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+KERNEL_NAME = "cpl_eval_kernel"
+
+
+def algorithmic_bytes(N, env, outputs=("g", "jac"), with_mass=True):
+    """Per instance: read x (3+9N) [+ mass]; write g (m) + jac (nnz) [+ f + grad (n)]."""
+    has_env = env != "none"
+    n = 3 + 9 * N
+    m = 6 + (6 if has_env else 2) * N
+    nnz = 6 + 15 * N + (27 if has_env else 12) * N
+    b = n + (1 if with_mass else 0)
+    if "g" in outputs:
+        b += m
+    if "jac" in outputs:
+        b += nnz
+    if "f" in outputs:
+        b += 1
+    if "grad" in outputs:
+        b += n
+    return 8 * b, m
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="ground4")
+    ap.add_argument("--batch", type=int, default=0, help="override per-GPU batch")
+    ap.add_argument("--no-pmc", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-target", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--pmc-child", default="", help=argparse.SUPPRESS)
+    return ap.parse_args()
+
+
+# ------------------------------------------------------------------------------------------
+# PMC traffic (child processes under rocprofv3; run before this process touches the GPU)
+# ------------------------------------------------------------------------------------------
+def pmc_child(args):
+    """Runs the eval kernel a few times; executed under rocprofv3 --pmc."""
+    import torch
+    from centroidalplanner_amd.workload import CONFIGS, config_inputs
+
+    cfg = CONFIGS[args.config]
+    prob, x, mass, tag = config_inputs(cfg, args.batch or cfg.batch)
+    dev = torch.device("cuda:0")
+    xt, mt = torch.tensor(x, device=dev), torch.tensor(mass, device=dev)
+    tt = None if tag is None else torch.tensor(tag, device=dev)
+    out = prob.eval_batch(xt, mt, tt, outputs=("g", "jac"))
+    for _ in range(5):
+        prob.eval_batch(xt, mt, tt, outputs=("g", "jac"), out=out)
+    torch.cuda.synchronize()
+
+
+def collect_pmc(args, timeout=240):
+    rocprof = "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(rocprof):
+        return None, "rocprofv3 not found"
+    vals = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="cpl_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+        cmd = [rocprof, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
+               sys.executable, os.path.join(ROOT, "bench.py"), "--pmc-child", "1", "--config", args.config]
+        if args.batch:
+            cmd += ["--batch", str(args.batch)]
+        try:
+            subprocess.run(cmd, check=True, timeout=timeout, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                           cwd=ROOT)
+        except Exception as e:  # noqa: BLE001
+            return None, f"rocprofv3 {counter} pass failed: {e}"
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        if not files:
+            return None, f"no counter csv for {counter}"
+        import csv
+
+        per = []
+        with open(files[0]) as fh:
+            for row in csv.DictReader(fh):
+                if KERNEL_NAME in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                    per.append(float(row["Counter_Value"]))
+        if not per:
+            return None, f"no {counter} rows for {KERNEL_NAME}"
+        vals[counter] = sum(per) / len(per)  # KB per dispatch
+    # gfx950: FETCH_SIZE reads 1/2 of a wide coalesced stream's bytes (MI355X_MICROARCH.md §HBM)
+    traffic = (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
+    return traffic, vals
+
+
+# ------------------------------------------------------------------------------------------
+# CPU baseline: the oracle (CPU restatement of the reference path) on the host cores
+# ------------------------------------------------------------------------------------------
+def cpu_baseline(cfg, seconds):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from centroidalplanner_amd.workload import config_inputs
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+    B = 2048
+    while True:  # calibrate on a sample long enough to amortise thread start-up
+        prob, x, mass, tag = config_inputs(cfg, B)
+        t = pyoracle.time_eval_batch(prob.desc(), x, mass, tag, outputs=("g", "jac"), nthreads=threads, reps=1)
+        if t > 0.25 or B >= 1 << 20:
+            break
+        B *= 4
+    per_inst = t / x.shape[0]
+    B = int(min(max(seconds / max(per_inst, 1e-9), 2048), 4_000_000))
+    prob, x, mass, tag = config_inputs(cfg, B)
+    t = pyoracle.time_eval_batch(prob.desc(), x, mass, tag, outputs=("g", "jac"), nthreads=threads, reps=1)
+    _, m = algorithmic_bytes(cfg.n_contacts, cfg.env)
+    return {
+        "value": B * m / t,
+        "unit": "rows/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{B} instances of '{cfg.name}' (g+jac, IFOPT-order assembly) in {t:.2f} s on {threads} threads",
+        "instances_per_s": B / t,
+    }
+
+
+# ------------------------------------------------------------------------------------------
+def main():
+    args = parse()
+    if args.pmc_child:
+        pmc_child(args)
+        return
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    from centroidalplanner_amd.workload import CONFIGS
+
+    cfg = CONFIGS[args.config]
+    batch = args.batch or cfg.batch
+    if cfg.config_id == 4 and not args.batch:
+        batch = cfg.batch // max(world, 1)  # config 4 is quoted as 1,048,576 over the node
+
+    traffic, pmc_info = None, None
+    if world == 1 and not args.no_pmc:
+        traffic, pmc_info = collect_pmc(args)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        try:
+            cpu = cpu_baseline(cfg, args.cpu_seconds)
+        except Exception as e:  # noqa: BLE001
+            cpu = {"error": str(e)}
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    from centroidalplanner_amd import _abi
+    from centroidalplanner_amd.workload import generate, make_problem
+
+    prob = make_problem(cfg.n_contacts, cfg.env)
+    x, mass, tag = generate(cfg.n_contacts, cfg.env, batch, 0xC910 + cfg.config_id + 7919 * rank)
+    xt = torch.tensor(x, device=dev)
+    mt = torch.tensor(mass, device=dev)
+    tt = None if tag is None else torch.tensor(tag, device=dev)
+    del x, mass, tag
+    out = prob.eval_batch(xt, mt, tt, outputs=("g", "jac"))
+    stream = torch.cuda.current_stream(dev)
+    K, W = args.steps, args.warmup
+    norms = [torch.zeros(2, dtype=torch.float64, device=dev) for _ in range(max(K, 1))]
+    gathered = [torch.zeros(2 * world, dtype=torch.float64, device=dev) for _ in range(max(K, 1))]
+
+    import ctypes
+
+    def step(i):
+        prob.eval_batch(xt, mt, tt, outputs=("g", "jac"), out=out, stream=stream)
+        nb = norms[i % len(norms)]
+        _abi.check(_abi.lib.cpl_residual_norms(ctypes.byref(prob.desc()), batch, out["g"].data_ptr(), nb.data_ptr(),
+                                               stream.cuda_stream))
+        if world > 1:
+            return dist.all_gather_into_tensor(gathered[i % len(gathered)], nb, async_op=True)
+        return None
+
+    for i in range(W):
+        w = step(i)
+        if w is not None:
+            w.wait()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    works = [step(i) for i in range(K)]
+    for w in works:
+        if w is not None:
+            w.wait()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tdt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tdt, op=dist.ReduceOp.MAX)
+        dt = float(tdt.item())
+
+    # live kernel timing: HIP events on the launch stream around back-to-back eval launches only
+    ms = ctypes.c_double()
+    reps = max(K, 20)
+
+    def p(t):
+        return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+    _abi.check(_abi.lib.cpl_time_eval_batch(ctypes.byref(prob.desc()), batch, p(xt), p(mt), p(tt), p(out["g"]), p(out["jac"]),
+                                            None, None, ctypes.c_void_p(stream.cuda_stream), reps, ctypes.byref(ms)))
+    kernel_ms = ms.value
+
+    bytes_inst, m = algorithmic_bytes(cfg.n_contacts, cfg.env)
+    alg_bytes = bytes_inst * batch
+    rows_total = batch * m * world * K
+    value = rows_total / dt
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+
+    target = None
+    if rank == 0 and world == 1 and not args.no_target and args.config == "ground4":
+        del out
+        torch.cuda.empty_cache()
+        tcfg = CONFIGS["ground4_1m"]
+        tb = tcfg.batch
+        tp = make_problem(tcfg.n_contacts, tcfg.env)
+        x1, m1, _ = generate(tcfg.n_contacts, tcfg.env, tb, 0xC910 + tcfg.config_id)
+        x1t, m1t = torch.tensor(x1, device=dev), torch.tensor(m1, device=dev)
+        del x1, m1
+        o1 = tp.eval_batch(x1t, m1t, outputs=("g", "jac"))
+        _abi.check(_abi.lib.cpl_time_eval_batch(ctypes.byref(tp.desc()), tb, p(x1t), p(m1t), None, p(o1["g"]), p(o1["jac"]), None,
+                                                None, ctypes.c_void_p(stream.cuda_stream), 20, ctypes.byref(ms)))
+        tbytes, tm = algorithmic_bytes(4, "ground")
+        target = {
+            "workload": tcfg.name,
+            "kernel_ms": ms.value,
+            "rows_per_s": tb * tm / (ms.value * 1e-3),
+            "hbm_gbps": tbytes * tb / (ms.value * 1e-3) / 1e9,
+            "frac_of_peak": tbytes * tb / (ms.value * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+        }
+
+    if rank == 0:
+        res = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": dt / K * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded SURVEY.md §8(d) instances; no published reference number)",
+            "config": {
+                "workload": cfg.name,
+                "contacts": cfg.n_contacts,
+                "environment": cfg.env,
+                "batch_per_gpu": batch,
+                "outputs": "g + jac (IFOPT CSR values), per-shard residual norms",
+                "parallelism": f"instance-sharded x{world}" + (" + RCCL all-gather of residual norms" if world > 1 else ""),
+            },
+            "instances_per_s": batch * world * K / dt,
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBPS,
+                "traffic": traffic,
+                "kernel": KERNEL_NAME,
+                "kernel_ms": kernel_ms,
+                "algorithmic_bytes_per_launch": alg_bytes,
+                "bytes_per_instance": bytes_inst,
+                "pmc": pmc_info,
+            },
+            "cpu_baseline": cpu,
+        }
+        if target:
+            res["target_1m"] = target
+        print(json.dumps(res), flush=True)
+
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

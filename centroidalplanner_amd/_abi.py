@@ -1,0 +1,156 @@
+"""ctypes view of the C-ABI declared in include/cpl_mi355x.h.
+
+Loads ``centroidalplanner_amd/libcpl_mi355x.so`` (built in-tree by ``centroidalplanner_amd.build``).
+There is no fallback: if the library is missing the import of this module raises, so nothing can
+silently run on a CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_int32, c_int64, c_size_t, c_uint8, c_void_p
+
+MAX_CONTACTS = 32
+ABI_VERSION = 1
+
+ENV_NONE = 0
+ENV_GROUND = 1
+ENV_SUPERQUADRIC = 2
+ENV_MIXED = 3
+
+OK = 0
+ERR_INVALID_ARGUMENT = 1
+ERR_OUT_OF_RANGE = 2
+ERR_RUNTIME = 3
+ERR_HIP = 4
+ERR_UNSUPPORTED = 5
+
+INF = 1.0e20
+
+LIB_NAME = "libcpl_mi355x.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+_V3 = c_double * 3
+_V3N = _V3 * MAX_CONTACTS
+
+
+class ProblemDesc(ctypes.Structure):
+    """Mirror of ``cpl_problem_desc`` (field order and types must match the header)."""
+
+    _fields_ = [
+        ("abi_version", c_int32),
+        ("n_contacts", c_int32),
+        ("env_kind", c_int32),
+        ("reserved0", c_int32),
+        ("map_order", c_int32 * MAX_CONTACTS),
+        ("mass", c_double),
+        ("gravity", c_double * 3),
+        ("wrench", c_double * 6),
+        ("mu", c_double),
+        ("ground_z", c_double),
+        ("sq_C", c_double * 3),
+        ("sq_R", c_double * 3),
+        ("sq_P", c_double * 3),
+        ("F_thr", c_double * MAX_CONTACTS),
+        ("W_com", c_double),
+        ("com_ref", c_double * 3),
+        ("W_p", c_double * MAX_CONTACTS),
+        ("W_F", c_double * MAX_CONTACTS),
+        ("p_ref", _V3N),
+        ("F_ref", _V3N),
+        ("com_lb", c_double * 3),
+        ("com_ub", c_double * 3),
+        ("F_lb", _V3N),
+        ("F_ub", _V3N),
+        ("p_lb", _V3N),
+        ("p_ub", _V3N),
+        ("n_lb", _V3N),
+        ("n_ub", _V3N),
+    ]
+
+
+# every symbol include/cpl_mi355x.h declares, with its ctypes signature
+_DESC_P = POINTER(ProblemDesc)
+_DP = POINTER(c_double)
+_IP = POINTER(c_int32)
+SIGNATURES = {
+    "cpl_abi_version": (c_int32, []),
+    "cpl_desc_sizeof": (c_size_t, []),
+    "cpl_last_error": (c_char_p, []),
+    "cpl_status_string": (c_char_p, [c_int32]),
+    "cpl_desc_init": (c_int32, [_DESC_P, c_int32, c_int32, c_double]),
+    "cpl_desc_set_contact_names": (c_int32, [_DESC_P, POINTER(c_char_p), c_int32]),
+    "cpl_desc_set_mu": (c_int32, [_DESC_P, c_double]),
+    "cpl_desc_set_superquadric": (c_int32, [_DESC_P, _DP, _DP, _DP]),
+    "cpl_desc_set_bounds": (c_int32, [_DESC_P, c_int32, c_int32, _DP, _DP]),
+    "cpl_dims": (c_int32, [_DESC_P, _IP, _IP, _IP]),
+    "cpl_structure": (c_int32, [_DESC_P, _IP, _IP, _IP]),
+    "cpl_bounds": (c_int32, [_DESC_P, _DP, _DP, _DP, _DP]),
+    "cpl_eval_batch": (
+        c_int32,
+        [_DESC_P, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
+    "cpl_residual_norms": (c_int32, [_DESC_P, c_int64, c_void_p, c_void_p, c_void_p]),
+    "cpl_time_eval_batch": (
+        c_int32,
+        [_DESC_P, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_int32, _DP],
+    ),
+}
+
+
+class CplError(RuntimeError):
+    """A non-zero status from the C-ABI."""
+
+    def __init__(self, status: int, message: str):
+        super().__init__(f"{message} (status {status})")
+        self.status = status
+        self.message = message
+
+
+class InvalidArgument(CplError, ValueError):
+    """Reference: std::invalid_argument."""
+
+
+class OutOfRange(CplError, IndexError):
+    """Reference: std::out_of_range."""
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build the HIP extension first "
+            "(python -c 'import __graft_entry__ as g; g.build()')"
+        )
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(status: int) -> None:
+    if status == OK:
+        return
+    msg = lib.cpl_last_error().decode(errors="replace")
+    if status == ERR_INVALID_ARGUMENT:
+        raise InvalidArgument(status, msg)
+    if status == ERR_OUT_OF_RANGE:
+        raise OutOfRange(status, msg)
+    raise CplError(status, msg)
+
+
+def dptr(a) -> ctypes.POINTER(c_double):
+    return a.ctypes.data_as(POINTER(c_double))
+
+
+def iptr(a) -> ctypes.POINTER(c_int32):
+    return a.ctypes.data_as(POINTER(c_int32))
+
+
+if lib.cpl_desc_sizeof() != ctypes.sizeof(ProblemDesc):  # pragma: no cover - layout guard
+    raise ImportError("cpl_problem_desc layout mismatch between header and ctypes mirror")

@@ -1,0 +1,73 @@
+"""In-tree build of the HIP extension (gfx950) and of the oracle checker.
+
+``python -m centroidalplanner_amd.build`` compiles ``csrc/*`` with hipcc into
+``centroidalplanner_amd/libcpl_mi355x.so``.  The arithmetic contract needs
+``-ffp-contract=off`` (no FMA contraction: the reference's x86-64 build has none) and no
+fast-math.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libcpl_mi355x.so")
+
+SOURCES = ["cpl_host.cpp", "cpl_kernels.hip"]
+HEADERS = ["cpl_layout.hpp", "cpl_status.hpp"]
+
+HIPCC_FLAGS = [
+    "--offload-arch=gfx950",
+    "-O3",
+    "-ffp-contract=off",
+    "-fno-fast-math",
+    "-std=c++17",
+    "-fPIC",
+    "-shared",
+    "-Wall",
+    "-Wno-unused-result",
+]
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the HIP extension cannot be built")
+
+
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_extension(force: bool = False, verbose: bool = False) -> str:
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "cpl_mi355x.h")]
+    if not force and not _stale(LIB, deps):
+        return LIB
+    cmd = [_hipcc()] + HIPCC_FLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", LIB + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+def build_oracle(verbose: bool = False) -> str:
+    """Build the CPU restatement (test infrastructure) with its own Makefile."""
+    odir = os.path.join(ROOT, "oracle")
+    cmd = ["make", "-s", "-C", odir]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    return os.path.join(odir, "_build", "libcpl_oracle.so")
+
+
+if __name__ == "__main__":
+    print(build_extension(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,178 @@
+/*
+ * cpl_mi355x.h — C-ABI of the MI355X-native batched NLP-callback engine for
+ * CentroidalPlanner's IFOPT evaluation path.
+ *
+ * One "instance" is one CentroidalPlanner problem (reference: cpl::solver::CplProblem,
+ * /root/reference/src/CplProblem.cpp:6-82).  A batch is B independent instances that share
+ * one problem template (contact set, environment, weights, bounds) and differ in their
+ * decision vector x (and optionally mass and environment kind).
+ *
+ * Layout contract (IFOPT order, reference CplProblem ctor):
+ *   x  (n = 3+9N)  : [CoM(3) | for i in contact_names order: F_i(3) p_i(3) n_i(3)]
+ *                    (/root/reference/src/CplProblem.cpp:17-34)
+ *   g  (m)         : [statics(6) | for k in std::map (lexicographic) order:
+ *                     env(1) normal(3) cone(2)]            m = 6+6N   (with environment)
+ *                    [statics(6) | for k in map order: cone(2)]  m = 6+2N (no environment,
+ *                     the CoMPlanner path)                 (/root/reference/src/CplProblem.cpp:37-75)
+ *   jac (nnz)      : values of the RowMajor CSR Jacobian IFOPT hands to IPOPT, explicit zeros
+ *                    kept, columns ascending within a row. nnz = 6+42N (env) / 6+27N (none).
+ *   f, grad (n)    : cost value and dense cost gradient (IpoptAdapter::eval_f / eval_grad_f).
+ * Batched buffers are instance-major: instance b's record starts at b*n (x, grad), b*m (g),
+ * b*nnz (jac), b (f, mass, env_tag).
+ *
+ * Conventions: every function returns CPL_OK (0) or a CPL_ERR_* status; nothing throws across
+ * this boundary.  The reference's std::invalid_argument / std::out_of_range / std::runtime_error
+ * map to CPL_ERR_INVALID_ARGUMENT / CPL_ERR_OUT_OF_RANGE / CPL_ERR_RUNTIME; the message of the
+ * last failure on the calling thread is available from cpl_last_error().
+ * Device pointers are caller-owned HIP allocations; `stream` is a hipStream_t (NULL = default).
+ */
+#ifndef CPL_MI355X_H
+#define CPL_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CPL_ABI_VERSION 1
+#define CPL_MAX_CONTACTS 32
+
+/* environment kinds (reference: cpl::env::EnvironmentClass subclasses,
+ * /root/reference/include/CentroidalPlanner/Environment/Environment.h:13-48) */
+#define CPL_ENV_NONE 0          /* CoMPlanner path: FrictionCone only, mu from a private Ground */
+#define CPL_ENV_GROUND 1        /* cpl::env::Ground       (/root/reference/src/Ground.cpp) */
+#define CPL_ENV_SUPERQUADRIC 2  /* cpl::env::Superquadric (/root/reference/src/Superquadric.cpp) */
+#define CPL_ENV_MIXED 3         /* per-instance tag array selects GROUND (1) / SUPERQUADRIC (2) */
+
+#define CPL_OK 0
+#define CPL_ERR_INVALID_ARGUMENT 1 /* reference: std::invalid_argument */
+#define CPL_ERR_OUT_OF_RANGE 2     /* reference: std::out_of_range (std::map::at) */
+#define CPL_ERR_RUNTIME 3          /* reference: std::runtime_error */
+#define CPL_ERR_HIP 4              /* a HIP runtime call failed */
+#define CPL_ERR_UNSUPPORTED 5
+
+/* IFOPT's infinity for one-sided bounds (ifopt::inf = 1.0e20; BoundSmallerZero = [-inf, 0]) */
+#define CPL_INF 1.0e20
+
+/*
+ * The shared problem template.  Plain data: fill it with cpl_desc_init() and the setters below
+ * (which validate exactly like the reference setters), or directly.
+ * Per-contact arrays are indexed by the contact's position in contact_names (vector order).
+ */
+typedef struct cpl_problem_desc {
+  int32_t abi_version;  /* = CPL_ABI_VERSION */
+  int32_t n_contacts;   /* N, 1..CPL_MAX_CONTACTS */
+  int32_t env_kind;     /* CPL_ENV_* */
+  int32_t reserved0;
+  /* map_order[k] = vector index of the k-th contact in std::map<std::string,...> order.
+   * reference: constraints are added in map order (src/CplProblem.cpp:42), variables in vector
+   * order (src/CplProblem.cpp:21).  They differ e.g. for "contact10" < "contact2". */
+  int32_t map_order[CPL_MAX_CONTACTS];
+
+  double mass;        /* default robot mass when no per-instance mass array is given
+                         (CentroidalStatics::SetMass, src/Constraints/CentroidalStatics.cpp:20) */
+  double gravity[3];  /* (0,0,-9.81), src/Constraints/CentroidalStatics.cpp:15 */
+  double wrench[6];   /* manipulation wrench, default 0 (src/Constraints/CentroidalStatics.cpp:12) */
+  double mu;          /* friction coefficient, default 1.0 (Environment.h:46) */
+  double ground_z;    /* Ground level, default 0 (src/Ground.cpp:7) */
+  double sq_C[3];     /* Superquadric centre, default (0,0,10) (src/Superquadric.cpp:7) */
+  double sq_R[3];     /* radii, default (10,10,10) */
+  double sq_P[3];     /* curvatures, default (10,10,10) */
+
+  double F_thr[CPL_MAX_CONTACTS]; /* FrictionCone force threshold, default 0 (FrictionCone.cpp:14) */
+
+  /* cost (MinimizeCentroidalVariables, src/MinimizeCentroidalVariables.cpp:5-27) */
+  double W_com;                       /* default 1 */
+  double com_ref[3];                  /* default (0,0,1) */
+  double W_p[CPL_MAX_CONTACTS];       /* default 1 */
+  double W_F[CPL_MAX_CONTACTS];       /* default 1 */
+  double p_ref[CPL_MAX_CONTACTS][3];  /* default 0 */
+  double F_ref[CPL_MAX_CONTACTS][3];  /* default 0 */
+
+  /* variable bounds (Variable3D, src/Variable3D.cpp:12-13: default [-1000, 1000]) */
+  double com_lb[3], com_ub[3];
+  double F_lb[CPL_MAX_CONTACTS][3], F_ub[CPL_MAX_CONTACTS][3];
+  double p_lb[CPL_MAX_CONTACTS][3], p_ub[CPL_MAX_CONTACTS][3];
+  double n_lb[CPL_MAX_CONTACTS][3], n_ub[CPL_MAX_CONTACTS][3];
+} cpl_problem_desc;
+
+/* ---- library / diagnostics ------------------------------------------------------------ */
+int32_t cpl_abi_version(void);
+size_t cpl_desc_sizeof(void);          /* sizeof(cpl_problem_desc), for FFI layout checks */
+const char* cpl_last_error(void);      /* message of the last failing call on this thread */
+const char* cpl_status_string(int32_t status);
+
+/* ---- problem template (host only) ----------------------------------------------------- */
+/* Defaults of the reference constructors for N contacts named "contact1".."contactN"
+ * (map order computed from those names).  Replaces CplProblem::CplProblem
+ * (src/CplProblem.cpp:6-82) + CentroidalPlanner ctor mass check (src/CentroidalPlanner.cpp:12-15). */
+int32_t cpl_desc_init(cpl_problem_desc* d, int32_t n_contacts, int32_t env_kind, double mass);
+/* Recompute map_order from the contact names (vector order).  Duplicate or empty names are
+ * rejected (the reference would silently alias them in its std::map). */
+int32_t cpl_desc_set_contact_names(cpl_problem_desc* d, const char* const* names, int32_t n);
+/* Validating setters (same checks as the reference):
+ *   EnvironmentClass::SetMu        include/CentroidalPlanner/Environment/Environment.h:19-26
+ *   Superquadric::SetParameters    src/Superquadric.cpp:12-29
+ *   Variable3D::SetBounds          src/Variable3D.cpp:28-40  (var: 0=CoM,1=F,2=p,3=n) */
+int32_t cpl_desc_set_mu(cpl_problem_desc* d, double mu);
+int32_t cpl_desc_set_superquadric(cpl_problem_desc* d, const double C[3], const double R[3],
+                                  const double P[3]);
+int32_t cpl_desc_set_bounds(cpl_problem_desc* d, int32_t var, int32_t contact,
+                            const double lb[3], const double ub[3]);
+
+/* IpoptAdapter::get_nlp_info [IFOPT-ext]: n, m, nnz_jac_g. */
+int32_t cpl_dims(const cpl_problem_desc* d, int32_t* n, int32_t* m, int32_t* nnz);
+/* IpoptAdapter::eval_jac_g(values == NULL) [IFOPT-ext]: (iRow, jCol) of every stored entry in
+ * RowMajor-CSR order.  Either pointer may be NULL.  Additionally `row_ptr` (m+1, may be NULL). */
+int32_t cpl_structure(const cpl_problem_desc* d, int32_t* iRow, int32_t* jCol, int32_t* row_ptr);
+/* IpoptAdapter::get_bounds_info [IFOPT-ext] over Variable3D::GetBounds (src/Variable3D.cpp:54-65)
+ * and the ConstraintSet GetBounds overrides (CentroidalStatics.cpp:64-73, FrictionCone.cpp:48-58,
+ * EnvironmentConstraint.cpp:31-40, EnvironmentNormal.cpp:36-50).  Any pointer may be NULL. */
+int32_t cpl_bounds(const cpl_problem_desc* d, double* x_l, double* x_u, double* g_l, double* g_u);
+
+/* ---- the hot path (device) ------------------------------------------------------------ */
+/*
+ * Evaluate `batch` instances in one launch.  Replaces, per instance, IpoptAdapter::eval_g,
+ * eval_jac_g(values != NULL), eval_f and eval_grad_f [IFOPT-ext], i.e. the IFOPT walk over
+ *   CentroidalStatics::GetValues / FillJacobianBlock  src/Constraints/CentroidalStatics.cpp:37-137
+ *   EnvironmentConstraint::GetValues / FillJacobianBlock src/Constraints/EnvironmentConstraint.cpp:16-61
+ *   EnvironmentNormal::GetValues / FillJacobianBlock  src/Constraints/EnvironmentNormal.cpp:16-87
+ *   FrictionCone::GetValues / FillJacobianBlock       src/Constraints/FrictionCone.cpp:30-103
+ *   MinimizeCentroidalVariables::GetCost / FillJacobianBlock src/MinimizeCentroidalVariables.cpp:124-192
+ * and the Ground / Superquadric environment functions they call.
+ *   d_x       [batch*n]   device, required
+ *   d_mass    [batch]     device or NULL (then d->mass for every instance)
+ *   d_env_tag [batch]     device uint8 (CPL_ENV_GROUND / CPL_ENV_SUPERQUADRIC); required iff
+ *                         env_kind == CPL_ENV_MIXED, ignored otherwise
+ *   d_g [batch*m], d_jac [batch*nnz], d_f [batch], d_grad [batch*n]: device outputs, any may be
+ *   NULL (that output is skipped).
+ * Asynchronous on `stream`; returns after the launch is enqueued.
+ */
+int32_t cpl_eval_batch(const cpl_problem_desc* d, int64_t batch, const double* d_x,
+                       const double* d_mass, const uint8_t* d_env_tag, double* d_g,
+                       double* d_jac, double* d_f, double* d_grad, void* stream);
+
+/*
+ * Per-shard residual norms of g against the constraint bounds (the per-shard figure the
+ * multi-GPU path all-gathers): d_out[0] = max_b max_r viol(b,r), d_out[1] = sum_b sum_r viol^2,
+ * where viol = max(g_l - g, g - g_u, 0) and NaN counts as +inf.  d_g is [batch*m] from
+ * cpl_eval_batch.  Device output, 2 doubles.  Asynchronous on `stream`.
+ */
+int32_t cpl_residual_norms(const cpl_problem_desc* d, int64_t batch, const double* d_g,
+                           double* d_out, void* stream);
+
+/* Kernel timing helper for the bench: launches cpl_eval_batch `reps` times on `stream`
+ * bracketed by HIP events recorded on that same stream and returns the mean milliseconds per
+ * launch in *ms_per_launch (synchronises the stream). */
+int32_t cpl_time_eval_batch(const cpl_problem_desc* d, int64_t batch, const double* d_x,
+                            const double* d_mass, const uint8_t* d_env_tag, double* d_g,
+                            double* d_jac, double* d_f, double* d_grad, void* stream,
+                            int32_t reps, double* ms_per_launch);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CPL_MI355X_H */

@@ -1,0 +1,90 @@
+"""Comparison policy of the GPU path against the oracle (test infrastructure).
+
+Policy:
+  * every entry that does not depend on a data-dependent pow (statics, friction cone, Ground,
+    cost) must be bit-identical (+0.0 == -0.0), NaN positions identical;
+  * Superquadric entries (environment value / Jacobian / normal value / normal Jacobian) go through
+    pow, where the GPU uses a correctly rounded double-double power and glibc misrounds ~0.1 % of
+    calls by one ulp.  They must satisfy |gpu - ref| <= RTOL * scale with RTOL = 1e-10 (the
+    north-star tolerance), where scale = |ref| for every entry except the three normal-Jacobian
+    diagonals, whose expanded (C-p)^2 numerator cancels catastrophically
+    (src/Superquadric.cpp:98-100, 152-154, 206-208): there scale is the magnitude of the
+    un-cancelled terms, |lead / S^1.5| * sum|E terms|, evaluated in float64 from the same inputs.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+RTOL = 1e-10
+
+SQ = np.array([0.0, 0.0, 1.0]), np.array([0.3, 0.3, 10.0]), np.array([10.0, 10.0, 10.0])
+
+
+def contact_offsets(N, has_env, map_order):
+    """jac offset of the per-contact block of map position k, and g offset."""
+    statics = 6 + 15 * N
+    cj = 27 if has_env else 12
+    cg = 6 if has_env else 2
+    return [(statics + cj * k, 6 + cg * k, map_order[k]) for k in range(N)]
+
+
+def sq_entry_mask(N, map_order, nnz, m, sq_instances):
+    """Boolean masks [B, nnz] / [B, m] of the pow-bearing entries of Superquadric instances."""
+    jm = np.zeros(nnz, dtype=bool)
+    gm = np.zeros(m, dtype=bool)
+    for jo, go, _ in contact_offsets(N, True, map_order):
+        jm[jo: jo + 15] = True      # env row (3) + normal rows (12)
+        gm[go: go + 4] = True       # env value + normal value
+    B = len(sq_instances)
+    return np.where(sq_instances[:, None], jm[None, :], False), np.where(sq_instances[:, None], gm[None, :], False)
+
+
+def diag_scale(x, N, map_order, C, R, P):
+    """[B, N, 3] conditioning scale of the normal-Jacobian diagonals (per contact, map order)."""
+    B = x.shape[0]
+    out = np.zeros((B, N, 3))
+    with np.errstate(all="ignore"):
+        for k in range(N):
+            i = map_order[k]
+            p = x[:, 6 + 9 * i: 9 + 9 * i]
+            d = p - C
+            inv = 1.0 / (d * d)
+            p2P = np.abs(d) ** (2 * P)
+            Rm2 = R ** (-(2 * P))
+            Rp2 = R ** (2 * P)
+            T = Rm2 * inv * P * P * p2P
+            Dg = P * P * R ** (-2 * P) * p2P * inv
+            for a in range(3):
+                b, c = [q for q in range(3) if q != a]
+                lead = P[a] * R[a] ** (-P[a]) * np.abs(d[:, a]) ** P[a] * (P[a] - 1.0)
+                for q in range(3):
+                    lead = lead * (1.0 if q == a else Rm2[q]) * inv[:, q]
+                S = T[:, b] + T[:, c] + Dg[:, a]
+                terms = (np.abs(C[b] * C[b]) + p[:, b] ** 2 + 2 * np.abs(C[b] * p[:, b])) * P[c] ** 2 * p2P[:, c] * Rp2[b] \
+                    + (np.abs(C[c] * C[c]) + p[:, c] ** 2 + 2 * np.abs(C[c] * p[:, c])) * P[b] ** 2 * p2P[:, b] * Rp2[c]
+                out[:, k, a] = np.abs(lead / S ** 1.5) * terms
+    return out
+
+
+def compare(got, want, exact_mask=None, scale=None, rtol=RTOL):
+    """Returns (ok, stats).  exact_mask: entries that must be bit-identical (default: all)."""
+    got = np.asarray(got)
+    want = np.asarray(want)
+    nan_g, nan_w = np.isnan(got), np.isnan(want)
+    stats = {"n": got.size, "nan_mismatch": int((nan_g != nan_w).sum())}
+    both = ~(nan_g | nan_w)
+    eq = (got == want) | (nan_g & nan_w)
+    stats["bitwise_frac"] = float(eq.mean()) if got.size else 1.0
+    if exact_mask is None:
+        exact_mask = np.ones(got.shape, dtype=bool)
+    bad_exact = exact_mask & ~eq
+    stats["exact_violations"] = int(bad_exact.sum())
+    tol_mask = ~exact_mask & both
+    if scale is None:
+        scale = np.abs(want)
+    err = np.where(tol_mask, np.abs(got - want), 0.0)
+    with np.errstate(all="ignore"):
+        rel = np.where(tol_mask & (scale > 0), err / np.where(scale > 0, scale, 1.0), np.where(err > 0, np.inf, 0.0))
+    stats["max_scaled_err"] = float(rel.max()) if rel.size else 0.0
+    ok = stats["nan_mismatch"] == 0 and stats["exact_violations"] == 0 and stats["max_scaled_err"] <= rtol
+    return ok, stats

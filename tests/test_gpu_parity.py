@@ -1,0 +1,166 @@
+"""GPU parity: the HIP path (through the C-ABI) against the oracle on the same seeded inputs.
+
+Bit-exact for every entry that carries no data-dependent pow; within 1e-10 (conditioning-aware for
+the normal-Jacobian diagonals) for Superquadric pow-bearing entries — see tests/parity_util.py.
+"""
+import numpy as np
+import pytest
+
+import pyoracle
+from parity_util import SQ, compare, contact_offsets, diag_scale, sq_entry_mask
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+OUTPUTS = ("g", "jac", "f", "grad")
+
+
+def _run(prob, x, mass=None, tag=None, outputs=OUTPUTS):
+    from centroidalplanner_amd import ENV_SUPERQUADRIC
+
+    dev = torch.device("cuda:0")
+    xt = torch.tensor(x, device=dev)
+    mt = None if mass is None else torch.tensor(mass, device=dev)
+    tt = None if tag is None else torch.tensor(tag, device=dev)
+    out = prob.eval_batch(xt, mt, tt, outputs=outputs)
+    torch.cuda.synchronize()
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    ref = pyoracle.eval_batch(prob.desc(), x, mass, tag, outputs=outputs)
+    return got, ref
+
+
+def _check(prob, env, x, got, ref, tag=None):
+    from centroidalplanner_amd import ENV_SUPERQUADRIC
+
+    N = len(prob.contact_names)
+    n, m, nnz = prob.get_nlp_info()
+    B = x.shape[0]
+    if env == "superquadric":
+        sq_inst = np.ones(B, dtype=bool)
+    elif env == "mixed":
+        sq_inst = tag == ENV_SUPERQUADRIC
+    else:
+        sq_inst = np.zeros(B, dtype=bool)
+    jm, gm = sq_entry_mask(N, prob.map_order, nnz, m, sq_inst)
+    report = {}
+    for k in got:
+        if k == "jac":
+            scale = np.abs(ref[k]).copy()
+            if sq_inst.any():
+                ds = diag_scale(x, N, prob.map_order, *SQ)
+                for kk, (jo, _, _) in enumerate(contact_offsets(N, True, prob.map_order)):
+                    for a in range(3):
+                        col = jo + 3 + 4 * a + a
+                        scale[:, col] = np.where(sq_inst, np.maximum(scale[:, col], ds[:, kk, a]), scale[:, col])
+            ok, st = compare(got[k], ref[k], exact_mask=~jm, scale=scale)
+        elif k == "g":
+            ok, st = compare(got[k], ref[k], exact_mask=~gm)
+        else:
+            ok, st = compare(got[k], ref[k])
+        report[k] = st
+        assert ok, f"{env} N={N} B={B} output {k}: {st}"
+    return report
+
+
+@pytest.mark.parametrize("env", ["ground", "none", "superquadric", "mixed"])
+@pytest.mark.parametrize("N", [1, 4, 8, 12, 16])
+def test_parity_configs(env, N):
+    from centroidalplanner_amd.workload import generate, make_problem
+
+    prob = make_problem(N, env)
+    B = 777  # ragged: 12 full tiles + a partial one
+    x, mass, tag = generate(N, env, B, 1000 + N)
+    got, ref = _run(prob, x, mass, tag)
+    _check(prob, env, x, got, ref, tag)
+
+
+@pytest.mark.parametrize("B", [1, 63, 64, 65, 129])
+def test_parity_ragged_batches(B):
+    from centroidalplanner_amd.workload import generate, make_problem
+
+    prob = make_problem(4, "ground")
+    x, mass, tag = generate(4, "ground", B, B)
+    got, ref = _run(prob, x, mass, tag)
+    _check(prob, "ground", x, got, ref)
+
+
+def test_parity_default_mass_and_subsets():
+    """mass=None uses the template mass; any output subset may be requested."""
+    from centroidalplanner_amd.workload import generate, make_problem
+
+    prob = make_problem(4, "ground", mass=73.5)
+    x, _, _ = generate(4, "ground", 100, 5)
+    for outs in (("g",), ("jac",), ("f",), ("grad",), ("g", "f")):
+        got, ref = _run(prob, x, None, None, outputs=outs)
+        for k in outs:
+            assert np.array_equal(got[k], ref[k], equal_nan=True), k
+
+
+def test_parity_degenerate_points():
+    """NaN positions: x = 0 (IPOPT start), F = 0, p_k = C_k on the superquadric."""
+    from centroidalplanner_amd.workload import make_problem
+
+    for env in ("ground", "none", "superquadric"):
+        prob = make_problem(4, env)
+        n = prob.n
+        x = np.zeros((5, n))
+        x[1] = 0.3
+        x[2, 3:6] = 0.0                         # F = 0 for contact1
+        x[2, 6:9] = [0.0, 0.0, 1.0]             # p = C
+        x[2, 9:12] = [0.0, 0.0, 1.0]
+        x[3] = np.linspace(-1, 1, n)
+        x[4, 6:9] = [0.0, 0.05, 1.0]            # p_x = C_x
+        got, ref = _run(prob, x, np.full(5, 100.0))
+        for k in got:
+            assert np.array_equal(np.isnan(got[k]), np.isnan(ref[k])), (env, k)
+        if env != "superquadric":
+            for k in got:
+                assert np.array_equal(got[k], ref[k], equal_nan=True), (env, k)
+        assert np.isnan(ref["jac"]).any()
+
+
+def test_parity_superquadric_stress_box():
+    """Full box, including points within 1e-3 of the centre planes (ill-conditioned diagonals)."""
+    from centroidalplanner_amd.workload import generate, make_problem
+
+    prob = make_problem(8, "superquadric")
+    x, mass, tag = generate(8, "superquadric", 2000, 99, stress=True)
+    got, ref = _run(prob, x, mass, tag)
+    _check(prob, "superquadric", x, got, ref)
+
+
+def test_parity_contact_names_order():
+    """Arbitrary names: variables follow the vector order, constraints the std::map order."""
+    from centroidalplanner_amd import CplProblem, Ground
+    from centroidalplanner_amd.workload import generate
+
+    env = Ground()
+    env.SetGroundZ(0.05)
+    env.SetMu(0.7)
+    names = ["r_foot", "l_foot", "Hand", "arm_10", "arm_2", "zeta"]
+    prob = CplProblem(names, 80.0, env)
+    prob.SetManipulationWrench([1, 2, 3, 4, 5, 6])
+    prob.SetForceThreshold("l_foot", 20.0)
+    prob.SetContactPosWeight("arm_2", 3.0)
+    prob.SetForceRef("zeta", [1.0, -2.0, 30.0])
+    prob.SetCoMRef([0.1, 0.0, 0.9])
+    prob.SetCoMWeight(2.0)
+    x, mass, _ = generate(len(names), "ground", 300, 11)
+    got, ref = _run(prob, x, mass)
+    _check(prob, "ground", x, got, ref)
+
+
+def test_residual_norms_match_host():
+    from centroidalplanner_amd.workload import generate, make_problem
+
+    prob = make_problem(4, "ground")
+    x, mass, _ = generate(4, "ground", 5000, 3)
+    dev = torch.device("cuda:0")
+    out = prob.eval_batch(torch.tensor(x, device=dev), torch.tensor(mass, device=dev), outputs=("g",))
+    rn = prob.residual_norms(out["g"]).cpu().numpy()
+    g = pyoracle.eval_batch(prob.desc(), x, mass, outputs=("g",))["g"]
+    _, _, gl, gu = prob.get_bounds_info()
+    viol = np.maximum(np.maximum(gl - g, g - gu), 0.0)
+    assert rn[0] == viol.max()
+    assert abs(rn[1] - (viol ** 2).sum()) <= 1e-9 * (viol ** 2).sum()
