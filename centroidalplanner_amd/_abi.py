@@ -116,7 +116,23 @@ class OutOfRange(CplError, IndexError):
     """Reference: std::out_of_range."""
 
 
+def _hip_runtimes_mapped():
+    try:
+        with open("/proc/self/maps") as fh:
+            return sorted({ln.split()[-1] for ln in fh if "libamdhip64" in ln})
+    except OSError:  # pragma: no cover
+        return []
+
+
 def _load():
+    # One HIP runtime per process.  PyTorch-ROCm ships its own libamdhip64 (DT_NEEDED
+    # "libamdhip64.so", SONAME libamdhip64.so.7); this library needs "libamdhip64.so.7".  If torch
+    # is importable, let it load its runtime first: our DT_NEEDED then binds to that already-loaded
+    # SONAME instead of mapping /opt/rocm's copy as a second, device-less runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # C++/ctypes hosts without torch use /opt/rocm's runtime
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"{LIB_PATH} is missing: build the HIP extension first "
@@ -131,6 +147,9 @@ def _load():
 
 
 lib = _load()
+
+if len(_hip_runtimes_mapped()) > 1:  # pragma: no cover - would make every launch fail
+    raise ImportError(f"two HIP runtimes mapped in this process: {_hip_runtimes_mapped()}")
 
 
 def check(status: int) -> None:

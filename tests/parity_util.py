@@ -88,3 +88,57 @@ def compare(got, want, exact_mask=None, scale=None, rtol=RTOL):
     stats["max_scaled_err"] = float(rel.max()) if rel.size else 0.0
     ok = stats["nan_mismatch"] == 0 and stats["exact_violations"] == 0 and stats["max_scaled_err"] <= rtol
     return ok, stats
+
+
+def g_scale(x, N, map_order, got_ref, C, R, P, sq_inst):
+    """Scale of the Superquadric g entries: env value = sum pow - 1 -> sum|pow| + 1; normal value
+    n - n_env -> |n| + |n_env|."""
+    scale = np.abs(got_ref).copy()
+    with np.errstate(all="ignore"):
+        for jo, go, i in contact_offsets(N, True, map_order):
+            p = x[:, 6 + 9 * i: 9 + 9 * i]
+            nv = x[:, 9 + 9 * i: 12 + 9 * i]
+            d = p - C
+            s_env = (np.abs(d / R) ** P).sum(1) + 1.0
+            j = P / R ** P * np.abs(d) ** (P - 1)
+            en = j / np.linalg.norm(j, axis=1, keepdims=True)
+            scale[:, go] = np.where(sq_inst, np.maximum(scale[:, go], s_env), scale[:, go])
+            for a in range(3):
+                s_n = np.abs(nv[:, a]) + np.abs(en[:, a])
+                scale[:, go + 1 + a] = np.where(sq_inst, np.maximum(scale[:, go + 1 + a], s_n), scale[:, go + 1 + a])
+    return scale
+
+
+def check_outputs(prob, env, x, got, ref, tag=None):
+    """Apply the policy above to every output; returns {output: stats}; raises AssertionError."""
+    from centroidalplanner_amd import ENV_SUPERQUADRIC
+
+    N = len(prob.contact_names)
+    n, m, nnz = prob.get_nlp_info()
+    B = x.shape[0]
+    if env == "superquadric":
+        sq_inst = np.ones(B, dtype=bool)
+    elif env == "mixed":
+        sq_inst = tag == ENV_SUPERQUADRIC
+    else:
+        sq_inst = np.zeros(B, dtype=bool)
+    jm, gm = sq_entry_mask(N, prob.map_order, nnz, m, sq_inst)
+    report = {}
+    for k in got:
+        if k == "jac":
+            scale = np.abs(ref[k]).copy()
+            if sq_inst.any():
+                ds = diag_scale(x, N, prob.map_order, *SQ)
+                for kk, (jo, _, _) in enumerate(contact_offsets(N, True, prob.map_order)):
+                    for a in range(3):
+                        col = jo + 3 + 4 * a + a
+                        scale[:, col] = np.where(sq_inst, np.maximum(scale[:, col], ds[:, kk, a]), scale[:, col])
+            ok, st = compare(got[k], ref[k], exact_mask=~jm, scale=scale)
+        elif k == "g":
+            scale = g_scale(x, N, prob.map_order, ref[k], *SQ, sq_inst) if sq_inst.any() else None
+            ok, st = compare(got[k], ref[k], exact_mask=~gm, scale=scale)
+        else:
+            ok, st = compare(got[k], ref[k])
+        report[k] = st
+        assert ok, f"{env} N={N} B={B} output {k}: {st}"
+    return report

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 import pyoracle
-from parity_util import SQ, compare, contact_offsets, diag_scale, sq_entry_mask
+from parity_util import check_outputs
 
 torch = pytest.importorskip("torch")
 
@@ -31,36 +31,7 @@ def _run(prob, x, mass=None, tag=None, outputs=OUTPUTS):
 
 
 def _check(prob, env, x, got, ref, tag=None):
-    from centroidalplanner_amd import ENV_SUPERQUADRIC
-
-    N = len(prob.contact_names)
-    n, m, nnz = prob.get_nlp_info()
-    B = x.shape[0]
-    if env == "superquadric":
-        sq_inst = np.ones(B, dtype=bool)
-    elif env == "mixed":
-        sq_inst = tag == ENV_SUPERQUADRIC
-    else:
-        sq_inst = np.zeros(B, dtype=bool)
-    jm, gm = sq_entry_mask(N, prob.map_order, nnz, m, sq_inst)
-    report = {}
-    for k in got:
-        if k == "jac":
-            scale = np.abs(ref[k]).copy()
-            if sq_inst.any():
-                ds = diag_scale(x, N, prob.map_order, *SQ)
-                for kk, (jo, _, _) in enumerate(contact_offsets(N, True, prob.map_order)):
-                    for a in range(3):
-                        col = jo + 3 + 4 * a + a
-                        scale[:, col] = np.where(sq_inst, np.maximum(scale[:, col], ds[:, kk, a]), scale[:, col])
-            ok, st = compare(got[k], ref[k], exact_mask=~jm, scale=scale)
-        elif k == "g":
-            ok, st = compare(got[k], ref[k], exact_mask=~gm)
-        else:
-            ok, st = compare(got[k], ref[k])
-        report[k] = st
-        assert ok, f"{env} N={N} B={B} output {k}: {st}"
-    return report
+    return check_outputs(prob, env, x, got, ref, tag)
 
 
 @pytest.mark.parametrize("env", ["ground", "none", "superquadric", "mixed"])
