@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "NLP eval_g+eval_jac_g throughput (rows/sec) at batch*contacts; HBM GB/s vs peak"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
-KERNEL_NAME = "cpl_eval_kernel"
+KERNEL_NAME = "cpl_eval"  # matches cpl_eval_tile_kernel (default) and cpl_eval_kernel (row-staged)
 
 
 def algorithmic_bytes(N, env, outputs=("g", "jac"), with_mass=True):

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -55,6 +56,15 @@ struct KParams {
   double W_com, com_ref[3];
   double W_p[CPL_MAX_CONTACTS], W_F[CPL_MAX_CONTACTS];
   double p_ref[CPL_MAX_CONTACTS][3], F_ref[CPL_MAX_CONTACTS][3];
+  // tile layout of the tile-stationary kernel (doubles offsets into dynamic LDS)
+  int32_t T, logT;       // instances per tile (power of two)
+  int32_t S;             // work-item segments per instance
+  int32_t cost_seg;      // segment index of the cost item, -1 if f/grad not requested
+  int32_t offG, offJ, offD, offL, offI;
+  int32_t LR;            // doubles per instance in the SQ scratch (N*SQ_L + 1)
+  int32_t want_g, want_j, want_f, want_grad;
+  int32_t ablate;        // measurement-only ablation (cpl_set_tuning), 0 in production
+  int32_t sq_ladder;     // every P_a is an integer in [2, 64]: double-double power ladders
 };
 static_assert(sizeof(KParams) < 4096, "kernel parameters must fit the kernarg segment");
 
@@ -210,6 +220,63 @@ struct SQContact {
   double nj[3][3];   // GetNormalJacobian
 };
 
+// Range in which the double-double chains below stay exact-enough (error terms never underflow).
+constexpr double DD_TINY = 0x1p-960;
+constexpr double DD_HUGE = 0x1p+960;
+
+__device__ __forceinline__ dd dd_mul_d(dd a, double b) {
+  double p = a.hi * b;
+  double e = __builtin_fma(a.hi, b, -p);
+  e = __builtin_fma(a.lo, b, e);
+  return fast_two_sum(p, e);
+}
+
+// pow(S, 3/2) = S*sqrt(S) in double-double, rounded once (C pow semantics outside the safe range).
+// sqrt(S) only has to be close: s from v_rsq_f64 plus one Newton step (~2^-50), then the exact
+// residual S - s^2 (one fma) gives the double-double correction (error ~2^-100).
+__device__ __forceinline__ double pow_three_halves(double S) {
+  if (S > DD_TINY && S < DD_HUGE) {
+    const double r = __builtin_amdgcn_rsq(S);
+    double s = S * r;
+    double h = 0.5 * r;
+    const double e = __builtin_fma(-h, s, 0.5);
+    s = __builtin_fma(s, e, s);
+    h = __builtin_fma(h, e, h);
+    const double rs = __builtin_fma(-s, s, S);
+    const dd sq = fast_two_sum(s, rs * h);
+    return dd_mul_d(sq, S).hi;
+  }
+  return pow(S, 1.5);
+}
+
+// The five powers of d = p_a - C_a the normal Jacobian needs, for integer P in [2, 64]:
+// B = d^(P-2) by binary powering, then exact-product chains A = B d = d^(P-1), Q = A d = d^P,
+// d^(2P-3) = B A, d^(2P-2) = A^2, d^(2P) = Q^2, all in double-double and rounded once.
+struct AxisPowers {
+  double pm1, pP, p2Pm3, p2Pm2, p2P;
+};
+__device__ __forceinline__ void axis_powers(const KParams& K, int a, double d, AxisPowers& o) {
+  if (K.sq_ladder) {
+    const dd B = dd_ipow(d, (unsigned)K.P[a] - 2u);
+    const dd A = dd_mul_d(B, d);
+    const dd Q = dd_mul_d(A, d);
+    const double q2 = dd_sqr(Q).hi;
+    if (q2 == q2 && fabs(q2) >= DD_TINY && fabs(q2) <= DD_HUGE) {  // every chain member in range
+      o.pm1 = A.hi;
+      o.pP = Q.hi;
+      o.p2Pm3 = dd_mul(B, A).hi;
+      o.p2Pm2 = dd_sqr(A).hi;
+      o.p2P = q2;
+      return;
+    }
+  }
+  o.pm1 = cpow(d, K.Pm1[a]);
+  o.pP = cpow(d, K.P[a]);
+  o.p2Pm3 = cpow(d, K.P2m3[a]);
+  o.p2Pm2 = cpow(d, K.P2m2[a]);
+  o.p2P = cpow(d, K.P2[a]);
+}
+
 __device__ __forceinline__ void superquadric_contact(const KParams& K, double p0, double p1, double p2,
                                                      bool want_nj, SQContact& o) {
   const double p[3] = {p0, p1, p2};
@@ -220,17 +287,32 @@ __device__ __forceinline__ void superquadric_contact(const KParams& K, double p0
   // src/Superquadric.cpp:40-49: value += pow((p-C)/R, P) over the axes, then -= 1
   double v = 0.0;
 #pragma unroll
-  for (int a = 0; a < 3; ++a) v += cpow((p[a] - K.C[a]) / K.R[a], K.P[a]);
+  for (int a = 0; a < 3; ++a) {
+    const double u = (p[a] - K.C[a]) / K.R[a];
+    double w;
+    if (K.sq_ladder && fabs(u) >= DD_TINY && fabs(u) <= 0x1p+40) {
+      w = dd_ipow(u, (unsigned)K.P[a]).hi;
+      if (!(fabs(w) >= DD_TINY && fabs(w) <= DD_HUGE)) w = cpow(u, K.P[a]);
+    } else {
+      w = cpow(u, K.P[a]);
+    }
+    v += w;
+  }
   v -= 1.0;
   o.val = v;
 
-  // src/Superquadric.cpp:51-57 and 60-69
-  double pm1[3];
+  AxisPowers ap[3];
+  if (want_nj) {
 #pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    pm1[a] = cpow(p[a] - K.C[a], K.Pm1[a]);
-    o.ej[a] = K.EJ[a] * pm1[a];
+    for (int a = 0; a < 3; ++a) axis_powers(K, a, d[a], ap[a]);
+  } else {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) ap[a].pm1 = cpow(d[a], K.Pm1[a]);
   }
+
+  // src/Superquadric.cpp:51-57 and 60-69
+#pragma unroll
+  for (int a = 0; a < 3; ++a) o.ej[a] = K.EJ[a] * ap[a].pm1;
   const double nrm = sqrt((o.ej[0] * o.ej[0] + o.ej[1] * o.ej[1]) + o.ej[2] * o.ej[2]);
 #pragma unroll
   for (int a = 0; a < 3; ++a) o.en[a] = -o.ej[a] / nrm;
@@ -238,17 +320,13 @@ __device__ __forceinline__ void superquadric_contact(const KParams& K, double p0
   if (!want_nj) return;
 
   // src/Superquadric.cpp:72-209
-  double inv[3], pP[3], p2P[3], p2Pm2[3], p2Pm3[3], T[3], Dg[3];
+  double inv[3], T[3], Dg[3];
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     const double t = K.C[a] - p[a];
     inv[a] = 1.0 / (t * t);
-    pP[a] = cpow(d[a], K.P[a]);
-    p2P[a] = cpow(d[a], K.P2[a]);
-    p2Pm2[a] = cpow(d[a], K.P2m2[a]);
-    p2Pm3[a] = cpow(d[a], K.P2m3[a]);
-    T[a] = ((K.Rm2[a] * inv[a]) * K.Psq[a]) * p2P[a];
-    Dg[a] = (K.Kb[a] * p2P[a]) * inv[a];
+    T[a] = ((K.Rm2[a] * inv[a]) * K.Psq[a]) * ap[a].p2P;
+    Dg[a] = (K.Kb[a] * ap[a].p2P) * inv[a];
   }
   // diagonal entries (a, a); b < c are the other two axes
 #pragma unroll
@@ -258,19 +336,20 @@ __device__ __forceinline__ void superquadric_contact(const KParams& K, double p0
     double lead = K.Ka[a];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      lead = lead * (k == a ? pP[a] : K.Rm2[k]);
+      lead = lead * (k == a ? ap[a].pP : K.Rm2[k]);
       lead = lead * inv[k];
     }
     lead = lead * K.Pm1[a];
     lead = lead * 1.0;
     const double S = (T[b] + T[c]) + Dg[a];
-    const double E = (((((((K.C[b] * K.C[b]) * K.Psq[c]) * p2P[c]) * K.Rp2[b] +
-                         (((K.C[c] * K.C[c]) * K.Psq[b]) * p2P[b]) * K.Rp2[c]) +
-                        (((p[b] * p[b]) * K.Psq[c]) * p2P[c]) * K.Rp2[b]) +
-                       (((p[c] * p[c]) * K.Psq[b]) * p2P[b]) * K.Rp2[c]) -
-                      ((((K.C[b] * p[b]) * K.Psq[c]) * p2P[c]) * K.Rp2[b]) * 2.0) -
-                     ((((K.C[c] * p[c]) * K.Psq[b]) * p2P[b]) * K.Rp2[c]) * 2.0;
-    o.nj[a][a] = lead / cpow(S, 3.0 / 2.0) * E;
+    const double p2Pb = ap[b].p2P, p2Pc = ap[c].p2P;
+    const double E = (((((((K.C[b] * K.C[b]) * K.Psq[c]) * p2Pc) * K.Rp2[b] +
+                         (((K.C[c] * K.C[c]) * K.Psq[b]) * p2Pb) * K.Rp2[c]) +
+                        (((p[b] * p[b]) * K.Psq[c]) * p2Pc) * K.Rp2[b]) +
+                       (((p[c] * p[c]) * K.Psq[b]) * p2Pb) * K.Rp2[c]) -
+                      ((((K.C[b] * p[b]) * K.Psq[c]) * p2Pc) * K.Rp2[b]) * 2.0) -
+                     ((((K.C[c] * p[c]) * K.Psq[b]) * p2Pb) * K.Rp2[c]) * 2.0;
+    o.nj[a][a] = lead / pow_three_halves(S) * E;
   }
   // off-diagonal entries (a, b), o = remaining axis
 #pragma unroll
@@ -281,20 +360,20 @@ __device__ __forceinline__ void superquadric_contact(const KParams& K, double p0
       const int oo = 3 - a - b;
       double lead = K.Ka[a];
       if (a < b) {  // src/Superquadric.cpp:109, 119, 163
-        lead = lead * pm1[a];
+        lead = lead * ap[a].pm1;
         lead = lead * K.Psq[b];
-        lead = lead * p2Pm3[b];
+        lead = lead * ap[b].p2Pm3;
         lead = lead * K.P2m2[b];
       } else {      // src/Superquadric.cpp:129, 173, 183
         lead = lead * K.Psq[b];
-        lead = lead * p2Pm3[b];
+        lead = lead * ap[b].p2Pm3;
         lead = lead * K.P2m2[b];
-        lead = lead * pm1[a];
+        lead = lead * ap[a].pm1;
       }
       lead = lead * K.Rm2[b];
       lead = lead * 1.0;
-      const double S = (K.Kb[oo] * p2Pm2[oo] + K.Kb[a] * p2Pm2[a]) + (K.Psq[b] * p2Pm2[b]) * K.Rm2[b];
-      o.nj[a][b] = lead / cpow(S, 3.0 / 2.0) * (-1.0 / 2.0);
+      const double S = (K.Kb[oo] * ap[oo].p2Pm2 + K.Kb[a] * ap[a].p2Pm2) + (K.Psq[b] * ap[b].p2Pm2) * K.Rm2[b];
+      o.nj[a][b] = lead / pow_three_halves(S) * (-1.0 / 2.0);
     }
   }
 }
@@ -517,6 +596,483 @@ __global__ __launch_bounds__(TILE) void cpl_eval_kernel(const KParams K, int64_t
   }
 }
 
+
+// ------------------------------------------------------------------------------------------
+// v2 (default): tile-stationary evaluation.
+//   * a workgroup owns a tile of T consecutive instances; x, g, jac (and grad) of the whole tile
+//     live in LDS ([T][n], [T][m], [T][nnz], [T][n]: the AoS image of the HBM records);
+//   * the per-instance work is cut into segments (contact blocks in std::map order, the statics
+//     values + force rows, the three torque rows, the cost) and every (segment, instance) work
+//     item is one thread's job: 256 threads compute T*(N+4) items in lock-step;
+//   * the finished tile is copied out linearly with 16-byte stores: tile boundaries fall on
+//     128-byte lines (T*record is a multiple of 16 doubles), so every HBM line of g / jac is
+//     written exactly once and whole.
+// ------------------------------------------------------------------------------------------
+constexpr int SEG_CONTACT0 = 0;  // segments [0, N): contacts in map order
+// then N: statics values + rows 0-2, N+1..N+3: torque rows 3..5, N+4: cost (optional)
+
+template <int WG>
+__device__ __forceinline__ void copy_in(double* __restrict__ dst, const double* __restrict__ src, int count,
+                                        int tid, bool vec) {
+  if (vec) {
+    const int pairs = count >> 1;
+    const double2* s2 = reinterpret_cast<const double2*>(src);
+    double2* d2 = reinterpret_cast<double2*>(dst);
+    for (int e = tid; e < pairs; e += WG) d2[e] = s2[e];
+    if ((count & 1) && tid == 0) dst[count - 1] = src[count - 1];
+  } else {
+    for (int e = tid; e < count; e += WG) dst[e] = src[e];
+  }
+}
+
+template <int WG, bool NT>
+__device__ __forceinline__ void copy_out(double* __restrict__ dst, const double* __restrict__ src, int count,
+                                         int tid) {
+  if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+    const int pairs = count >> 1;
+    const double2* s2 = reinterpret_cast<const double2*>(src);
+    double2* d2 = reinterpret_cast<double2*>(dst);
+    for (int e = tid; e < pairs; e += WG) {
+      if (NT) {
+        const double2 v = s2[e];
+        __builtin_nontemporal_store(v.x, &d2[e].x);
+        __builtin_nontemporal_store(v.y, &d2[e].y);
+      } else {
+        d2[e] = s2[e];
+      }
+    }
+    if ((count & 1) && tid == 0) dst[count - 1] = src[count - 1];
+  } else {
+    for (int e = tid; e < count; e += WG) dst[e] = src[e];
+  }
+}
+
+// one contact block (map position k, vector index i): g rows env(1) normal(3) cone(2),
+// jac rows env p(3) | normal r: p(3) n_r(1) | cone 0: F(3) n(3) | cone 1: F(3) n(3)
+template <int ENVK>
+__device__ __forceinline__ void contact_item(const KParams& K, const double* __restrict__ xr, int kind, int k,
+                                             double* __restrict__ Gr, double* __restrict__ Jr) {
+  const int i = K.map_order[k];
+  const double* q = xr + 3 + 9 * i;
+  const double F0 = q[0], F1 = q[1], F2 = q[2];
+  const double p0 = q[3], p1 = q[4], p2 = q[5];
+  const double n0 = q[6], n1 = q[7], n2 = q[8];
+  const bool wg = K.want_g, wj = K.want_j;
+  double* gk = Gr + 6 + (K.has_env ? 6 : 2) * k;
+  double* jk = Jr + 6 + 15 * K.N + (K.has_env ? 27 : 12) * k;
+  if (ENVK != CPL_ENV_NONE) {
+    double gv[4], ej[3], nj[3][3];
+    if (ENVK == CPL_ENV_GROUND || (ENVK == CPL_ENV_MIXED && kind == CPL_ENV_GROUND)) {
+      // src/Ground.cpp:23-50
+      gv[0] = p2 - K.ground_z;
+      gv[1] = n0 - 0.0; gv[2] = n1 - 0.0; gv[3] = n2 - 1.0;
+      ej[0] = 0.0; ej[1] = 0.0; ej[2] = 1.0;
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) nj[r][c] = 0.0;
+    } else {
+      SQContact s;
+      superquadric_contact(K, p0, p1, p2, wj, s);
+      gv[0] = s.val;
+      gv[1] = n0 - s.en[0]; gv[2] = n1 - s.en[1]; gv[3] = n2 - s.en[2];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        ej[r] = s.ej[r];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) nj[r][c] = wj ? s.nj[r][c] : 0.0;
+      }
+    }
+    if (wg) { gk[0] = gv[0]; gk[1] = gv[1]; gk[2] = gv[2]; gk[3] = gv[3]; }
+    if (wj) {
+      jk[0] = ej[0]; jk[1] = ej[1]; jk[2] = ej[2];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        jk[3 + 4 * r] = nj[r][0]; jk[4 + 4 * r] = nj[r][1]; jk[5 + 4 * r] = nj[r][2]; jk[6 + 4 * r] = 1.0;
+      }
+    }
+    gk += 4;
+    jk += 15;
+  }
+  // FrictionCone, src/Constraints/FrictionCone.cpp:30-103
+  const double mu = K.mu;
+  const double t1 = dot3(F0, F1, F2, n0, n1, n2);
+  if (wg) {
+    const double nF = dot3(n0, n1, n2, F0, F1, F2);
+    const double u0 = F0 - nF * n0, u1 = F1 - nF * n1, u2 = F2 - nF * n2;
+    gk[0] = -t1 + K.F_thr[i];
+    gk[1] = sqrt((u0 * u0 + u1 * u1) + u2 * u2) - mu * t1;
+  }
+  if (wj) {
+    const double t2 = F0 - n0 * t1;
+    const double t3 = F1 - n1 * t1;
+    const double t4 = F2 - n2 * t1;
+    const double t5 = F0 * n0;
+    const double t6 = F1 * n1;
+    const double t7 = F2 * n2;
+    const double s = sqrt(t2 * t2 + t3 * t3 + t4 * t4);
+    jk[0] = -n0; jk[1] = -n1; jk[2] = -n2;
+    jk[3] = -F0; jk[4] = -F1; jk[5] = -F2;
+    jk[6] = (t2 * (n0 * n0 - 1.0) * 2.0 + n0 * n1 * t3 * 2.0 + n0 * n2 * t4 * 2.0) * 1.0 / s * (-1.0 / 2.0) - mu * n0;
+    jk[7] = (t3 * (n1 * n1 - 1.0) * 2.0 + n0 * n1 * t2 * 2.0 + n1 * n2 * t4 * 2.0) * 1.0 / s * (-1.0 / 2.0) - mu * n1;
+    jk[8] = (t4 * (n2 * n2 - 1.0) * 2.0 + n0 * n2 * t2 * 2.0 + n1 * n2 * t3 * 2.0) * 1.0 / s * (-1.0 / 2.0) - mu * n2;
+    jk[9] = (t2 * (t6 + t7 + t5 * 2.0) * 2.0 + F0 * n1 * t3 * 2.0 + F0 * n2 * t4 * 2.0) * 1.0 / s * (-1.0 / 2.0) - mu * F0;
+    jk[10] = (t3 * (t5 + t7 + t6 * 2.0) * 2.0 + F1 * n0 * t2 * 2.0 + F1 * n2 * t4 * 2.0) * 1.0 / s * (-1.0 / 2.0) - mu * F1;
+    jk[11] = (t4 * (t5 + t6 + t7 * 2.0) * 2.0 + F2 * n0 * t2 * 2.0 + F2 * n1 * t3 * 2.0) * 1.0 / s * (-1.0 / 2.0) - mu * F2;
+  }
+}
+
+// CentroidalStatics::GetValues (src/Constraints/CentroidalStatics.cpp:37-61) and Jacobian rows 0-2
+// (the I3 of every F_i, :93-95)
+__device__ __forceinline__ void statics_values_item(const KParams& K, const double* __restrict__ xr, double m_i,
+                                                    double* __restrict__ Gr, double* __restrict__ Jr) {
+  const int N = K.N;
+  if (K.want_g) {
+    const double c0 = xr[0], c1 = xr[1], c2 = xr[2];
+    double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0, v4 = 0.0, v5 = 0.0;
+    for (int k = 0; k < N; ++k) {
+      const double* q = xr + 3 + 9 * K.map_order[k];
+      const double F0 = q[0], F1 = q[1], F2 = q[2];
+      const double d0 = q[3] - c0, d1 = q[4] - c1, d2 = q[5] - c2;
+      v0 += F0; v1 += F1; v2 += F2;
+      v3 += d1 * F2 - d2 * F1;
+      v4 += d2 * F0 - d0 * F2;
+      v5 += d0 * F1 - d1 * F0;
+    }
+    v0 -= K.wrench[0]; v1 -= K.wrench[1]; v2 -= K.wrench[2];
+    v3 -= K.wrench[3]; v4 -= K.wrench[4]; v5 -= K.wrench[5];
+    v0 += m_i * K.gravity[0]; v1 += m_i * K.gravity[1]; v2 += m_i * K.gravity[2];
+    Gr[0] = v0; Gr[1] = v1; Gr[2] = v2; Gr[3] = v3; Gr[4] = v4; Gr[5] = v5;
+  }
+  if (K.want_j)
+    for (int e = 0; e < 3 * N; ++e) Jr[e] = 1.0;
+}
+
+// Torque row 3+q of CentroidalStatics::FillJacobianBlock (src/Constraints/CentroidalStatics.cpp:75-137):
+// [CoM pair | per contact in column order: F pair, p pair].  For row q the F pair is
+// (sF1*(p[e1]-c[e1]), sF2*(p[e2]-c[e2])) and the p pair / CoM accumulation uses (-sF1*F[e1], -sF2*F[e2]);
+// negation is exact, so every entry keeps the reference's bits.
+__device__ __forceinline__ void statics_row_item(const KParams& K, const double* __restrict__ xr, int q,
+                                                 double* __restrict__ Jr) {
+  const int N = K.N;
+  // (e1, e2) and sign of the F-block entries: row3 (2,-)(1,+), row4 (2,+)(0,-), row5 (1,-)(0,+)
+  const int e1 = q == 2 ? 1 : 2;
+  const int e2 = q == 0 ? 1 : 0;
+  const double s1 = q == 1 ? 1.0 : -1.0;
+  const double s2 = q == 1 ? -1.0 : 1.0;
+  const double ce1 = xr[e1], ce2 = xr[e2];
+  double a1 = 0.0, a2 = 0.0;
+  for (int k = 0; k < N; ++k) {  // CoM block: -= the p-block entries in map order (:119-136)
+    const double* F = xr + 3 + 9 * K.map_order[k];
+    a1 -= -s1 * F[e1];
+    a2 -= -s2 * F[e2];
+  }
+  double* row = Jr + 3 * N + q * (2 + 4 * N);
+  row[0] = a1;
+  row[1] = a2;
+  for (int i = 0; i < N; ++i) {
+    const double* F = xr + 3 + 9 * i;
+    const double* p = F + 3;
+    row[2 + 4 * i] = s1 * (p[e1] - ce1);
+    row[3 + 4 * i] = s2 * (p[e2] - ce2);
+    row[4 + 4 * i] = -s1 * F[e1];
+    row[5 + 4 * i] = -s2 * F[e2];
+  }
+}
+
+// MinimizeCentroidalVariables::GetCost / FillJacobianBlock, src/MinimizeCentroidalVariables.cpp:124-192
+__device__ __forceinline__ void cost_item(const KParams& K, const double* __restrict__ xr, double* __restrict__ f,
+                                          double* __restrict__ Dr) {
+  const int N = K.N;
+  const double c0 = xr[0], c1 = xr[1], c2 = xr[2];
+  if (K.want_f) {
+    double value = 0;
+    for (int k = 0; k < N; ++k) {
+      const int i = K.map_order[k];
+      const double* q = xr + 3 + 9 * i;
+      const double e0 = q[3] - K.p_ref[i][0], e1 = q[4] - K.p_ref[i][1], e2 = q[5] - K.p_ref[i][2];
+      const double h0 = q[0] - K.F_ref[i][0], h1 = q[1] - K.F_ref[i][1], h2 = q[2] - K.F_ref[i][2];
+      value += 0.5 * K.W_p[i] * ((e0 * e0 + e1 * e1) + e2 * e2) + 0.5 * K.W_F[i] * ((h0 * h0 + h1 * h1) + h2 * h2);
+    }
+    const double r0 = c0 - K.com_ref[0], r1 = c1 - K.com_ref[1], r2 = c2 - K.com_ref[2];
+    value += 0.5 * K.W_com * ((r0 * r0 + r1 * r1) + r2 * r2);
+    *f = value;
+  }
+  if (K.want_grad) {
+    Dr[0] = K.W_com * (c0 - K.com_ref[0]);
+    Dr[1] = K.W_com * (c1 - K.com_ref[1]);
+    Dr[2] = K.W_com * (c2 - K.com_ref[2]);
+    for (int i = 0; i < N; ++i) {
+      const double* q = xr + 3 + 9 * i;
+      double* d = Dr + 3 + 9 * i;
+      d[0] = K.W_F[i] * (q[0] - K.F_ref[i][0]);
+      d[1] = K.W_F[i] * (q[1] - K.F_ref[i][1]);
+      d[2] = K.W_F[i] * (q[2] - K.F_ref[i][2]);
+      d[3] = K.W_p[i] * (q[3] - K.p_ref[i][0]);
+      d[4] = K.W_p[i] * (q[4] - K.p_ref[i][1]);
+      d[5] = K.W_p[i] * (q[5] - K.p_ref[i][2]);
+      d[6] = 0.0; d[7] = 0.0; d[8] = 0.0;
+    }
+  }
+}
+
+
+// ---- Superquadric contacts in two phases (tile kernel) -----------------------------------
+// Phase 1, one item per (instance, contact, axis): the powers of d = p_a - C_a and
+// ((p_a - C_a)/R_a)^P_a, and 1/(C_a - p_a)^2, into an LDS scratch row of SQ_L doubles per contact.
+// Phase 2, one item per (instance, contact, normal-Jacobian row): the three entries of that row
+// from the scratch; row 0 also emits the environment value / Jacobian / normal, row 1 the cone.
+constexpr int SQ_L = 21;  // per contact: 3 axes x {pm1, pP, p2Pm3, p2Pm2, p2P, inv, wenv}
+enum { L_PM1 = 0, L_PP, L_P2PM3, L_P2PM2, L_P2P, L_INV, L_WENV, L_AXIS };
+
+__device__ __forceinline__ void sq_axis_item(const KParams& K, const double* __restrict__ xr, int k, int a,
+                                             double* __restrict__ Lc) {
+  const int i = K.map_order[k];
+  const double pa = xr[6 + 9 * i + a];
+  const double d = -K.C[a] + pa;
+  double* o = Lc + a * L_AXIS;
+  // src/Superquadric.cpp:45  pow((p-C)/R, P)
+  const double u = (pa - K.C[a]) / K.R[a];
+  double w;
+  if (K.sq_ladder && fabs(u) >= DD_TINY && fabs(u) <= 0x1p+40) {
+    w = dd_ipow(u, (unsigned)K.P[a]).hi;
+    if (!(fabs(w) >= DD_TINY && fabs(w) <= DD_HUGE)) w = cpow(u, K.P[a]);
+  } else {
+    w = cpow(u, K.P[a]);
+  }
+  o[L_WENV] = w;
+  if (K.want_j) {
+    AxisPowers ap;
+    axis_powers(K, a, d, ap);
+    o[L_PM1] = ap.pm1;
+    o[L_PP] = ap.pP;
+    o[L_P2PM3] = ap.p2Pm3;
+    o[L_P2PM2] = ap.p2Pm2;
+    o[L_P2P] = ap.p2P;
+    const double t = K.C[a] - pa;
+    o[L_INV] = 1.0 / (t * t);
+  } else {
+    o[L_PM1] = cpow(d, K.Pm1[a]);  // src/Superquadric.cpp:54-56 (normal value only)
+  }
+}
+
+// FrictionCone rows of one contact (src/Constraints/FrictionCone.cpp:30-103)
+__device__ __forceinline__ void cone_rows(const KParams& K, int i, const double* __restrict__ q, double* gk,
+                                          double* jk) {
+  const double F0 = q[0], F1 = q[1], F2 = q[2];
+  const double n0 = q[6], n1 = q[7], n2 = q[8];
+  const double mu = K.mu;
+  const double t1 = dot3(F0, F1, F2, n0, n1, n2);
+  if (K.want_g) {
+    const double nF = dot3(n0, n1, n2, F0, F1, F2);
+    const double u0 = F0 - nF * n0, u1 = F1 - nF * n1, u2 = F2 - nF * n2;
+    gk[0] = -t1 + K.F_thr[i];
+    gk[1] = sqrt((u0 * u0 + u1 * u1) + u2 * u2) - mu * t1;
+  }
+  if (K.want_j) {
+    const double t2 = F0 - n0 * t1;
+    const double t3 = F1 - n1 * t1;
+    const double t4 = F2 - n2 * t1;
+    const double t5 = F0 * n0;
+    const double t6 = F1 * n1;
+    const double t7 = F2 * n2;
+    const double s = sqrt(t2 * t2 + t3 * t3 + t4 * t4);
+    jk[0] = -n0; jk[1] = -n1; jk[2] = -n2;
+    jk[3] = -F0; jk[4] = -F1; jk[5] = -F2;
+    jk[6] = (t2 * (n0 * n0 - 1.0) * 2.0 + n0 * n1 * t3 * 2.0 + n0 * n2 * t4 * 2.0) * 1.0 / s * (-1.0 / 2.0) - mu * n0;
+    jk[7] = (t3 * (n1 * n1 - 1.0) * 2.0 + n0 * n1 * t2 * 2.0 + n1 * n2 * t4 * 2.0) * 1.0 / s * (-1.0 / 2.0) - mu * n1;
+    jk[8] = (t4 * (n2 * n2 - 1.0) * 2.0 + n0 * n2 * t2 * 2.0 + n1 * n2 * t3 * 2.0) * 1.0 / s * (-1.0 / 2.0) - mu * n2;
+    jk[9] = (t2 * (t6 + t7 + t5 * 2.0) * 2.0 + F0 * n1 * t3 * 2.0 + F0 * n2 * t4 * 2.0) * 1.0 / s * (-1.0 / 2.0) - mu * F0;
+    jk[10] = (t3 * (t5 + t7 + t6 * 2.0) * 2.0 + F1 * n0 * t2 * 2.0 + F1 * n2 * t4 * 2.0) * 1.0 / s * (-1.0 / 2.0) - mu * F1;
+    jk[11] = (t4 * (t5 + t6 + t7 * 2.0) * 2.0 + F2 * n0 * t2 * 2.0 + F2 * n1 * t3 * 2.0) * 1.0 / s * (-1.0 / 2.0) - mu * F2;
+  }
+}
+
+__device__ __forceinline__ void sq_row_item(const KParams& K, const double* __restrict__ xr, int k, int a,
+                                            const double* __restrict__ Lc, double* __restrict__ Gr,
+                                            double* __restrict__ Jr) {
+  const int i = K.map_order[k];
+  const double* q = xr + 3 + 9 * i;
+  double* gk = Gr + 6 + 6 * k;
+  double* jk = Jr + 6 + 15 * K.N + 27 * k;
+  if (a == 0) {
+    // EnvironmentConstraint / EnvironmentNormal values and the env Jacobian row
+    // (src/Superquadric.cpp:40-69; src/Constraints/EnvironmentConstraint.cpp:16-61; EnvironmentNormal.cpp:16-33)
+    double v = 0.0;
+    v += Lc[0 * L_AXIS + L_WENV];
+    v += Lc[1 * L_AXIS + L_WENV];
+    v += Lc[2 * L_AXIS + L_WENV];
+    v -= 1.0;
+    const double ej0 = K.EJ[0] * Lc[0 * L_AXIS + L_PM1];
+    const double ej1 = K.EJ[1] * Lc[1 * L_AXIS + L_PM1];
+    const double ej2 = K.EJ[2] * Lc[2 * L_AXIS + L_PM1];
+    const double nrm = sqrt((ej0 * ej0 + ej1 * ej1) + ej2 * ej2);
+    if (K.want_g) {
+      gk[0] = v;
+      gk[1] = q[6] - -ej0 / nrm;
+      gk[2] = q[7] - -ej1 / nrm;
+      gk[3] = q[8] - -ej2 / nrm;
+    }
+    if (K.want_j) { jk[0] = ej0; jk[1] = ej1; jk[2] = ej2; }
+  } else if (a == 1) {
+    cone_rows(K, i, q, gk + 4, jk + 15);
+  }
+  if (!K.want_j) return;
+  // EnvironmentNormal p block row a = GetNormalJacobian row a (src/Superquadric.cpp:72-209), n_a = 1
+  const int b = a == 0 ? 1 : 0;
+  const int c = a == 2 ? 1 : 2;
+  const double* La = Lc + a * L_AXIS;
+  const double* Lb = Lc + b * L_AXIS;
+  const double* Lcc = Lc + c * L_AXIS;
+  const double p_b = q[3 + b], p_c = q[3 + c];
+  double out[3];
+  {  // diagonal (a, a)
+    double lead = K.Ka[a];
+#pragma unroll
+    for (int kk = 0; kk < 3; ++kk) {
+      lead = lead * (kk == a ? La[L_PP] : K.Rm2[kk]);
+      lead = lead * Lc[kk * L_AXIS + L_INV];
+    }
+    lead = lead * K.Pm1[a];
+    lead = lead * 1.0;
+    const double Tb = ((K.Rm2[b] * Lb[L_INV]) * K.Psq[b]) * Lb[L_P2P];
+    const double Tc = ((K.Rm2[c] * Lcc[L_INV]) * K.Psq[c]) * Lcc[L_P2P];
+    const double Dg = (K.Kb[a] * La[L_P2P]) * La[L_INV];
+    const double S = (Tb + Tc) + Dg;
+    const double p2Pb = Lb[L_P2P], p2Pc = Lcc[L_P2P];
+    const double E = (((((((K.C[b] * K.C[b]) * K.Psq[c]) * p2Pc) * K.Rp2[b] +
+                         (((K.C[c] * K.C[c]) * K.Psq[b]) * p2Pb) * K.Rp2[c]) +
+                        (((p_b * p_b) * K.Psq[c]) * p2Pc) * K.Rp2[b]) +
+                       (((p_c * p_c) * K.Psq[b]) * p2Pb) * K.Rp2[c]) -
+                      ((((K.C[b] * p_b) * K.Psq[c]) * p2Pc) * K.Rp2[b]) * 2.0) -
+                     ((((K.C[c] * p_c) * K.Psq[b]) * p2Pb) * K.Rp2[c]) * 2.0;
+    out[a] = lead / pow_three_halves(S) * E;
+  }
+#pragma unroll
+  for (int bb = 0; bb < 3; ++bb) {  // off-diagonals (a, bb)
+    if (bb == a) continue;
+    const int oo = 3 - a - bb;
+    const double* Lbb = Lc + bb * L_AXIS;
+    double lead = K.Ka[a];
+    if (a < bb) {  // src/Superquadric.cpp:109, 119, 163
+      lead = lead * La[L_PM1];
+      lead = lead * K.Psq[bb];
+      lead = lead * Lbb[L_P2PM3];
+      lead = lead * K.P2m2[bb];
+    } else {       // src/Superquadric.cpp:129, 173, 183
+      lead = lead * K.Psq[bb];
+      lead = lead * Lbb[L_P2PM3];
+      lead = lead * K.P2m2[bb];
+      lead = lead * La[L_PM1];
+    }
+    lead = lead * K.Rm2[bb];
+    lead = lead * 1.0;
+    const double S = (K.Kb[oo] * Lc[oo * L_AXIS + L_P2PM2] + K.Kb[a] * La[L_P2PM2]) +
+                     (K.Psq[bb] * Lbb[L_P2PM2]) * K.Rm2[bb];
+    out[bb] = lead / pow_three_halves(S) * (-1.0 / 2.0);
+  }
+  double* row = jk + 3 + 4 * a;
+  row[0] = out[0]; row[1] = out[1]; row[2] = out[2]; row[3] = 1.0;
+}
+
+template <int ENVK, int WG, bool NT>
+__global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int64_t batch,
+                                                            const double* __restrict__ x,
+                                                            const double* __restrict__ mass,
+                                                            const uint8_t* __restrict__ env_tag,
+                                                            double* __restrict__ g_out,
+                                                            double* __restrict__ jac_out,
+                                                            double* __restrict__ f_out,
+                                                            double* __restrict__ grad_out) {
+  extern __shared__ __align__(16) double smem[];
+  const int tid = threadIdx.x;
+  const int T = K.T;
+  const int n = K.n, m = K.m, nnz = K.nnz, N = K.N;
+  const int64_t b0 = (int64_t)blockIdx.x * T;
+  const int valid = (int)((batch - b0) < T ? (batch - b0) : T);
+  double* X = smem;
+  double* Gt = smem + K.offG;
+  double* Jt = smem + K.offJ;
+  double* Dt = smem + K.offD;
+  double* L = smem + K.offL;                                    // [T][LR] (SQ / mixed)
+  int* lists = reinterpret_cast<int*>(smem + K.offI);          // sq_list[64], gr_list[64], n_sq
+  constexpr bool HAS_SQ = ENVK == CPL_ENV_SUPERQUADRIC || ENVK == CPL_ENV_MIXED;
+
+  copy_in<WG>(X, x + b0 * n, valid * n, tid, K.x_aligned16 != 0);
+  int n_sq = ENVK == CPL_ENV_SUPERQUADRIC ? valid : 0;
+  if (ENVK == CPL_ENV_MIXED) {
+    // compact the tile's instances by environment kind so that every wave runs one code path
+    if (tid < 64) {
+      const bool is_sq = tid < valid && env_tag[b0 + tid] == CPL_ENV_SUPERQUADRIC;
+      const unsigned long long mask = __ballot(is_sq);
+      if (tid < valid) {
+        const int before = __popcll(mask & ((1ull << tid) - 1ull));
+        if (is_sq) lists[before] = tid;
+        else lists[64 + tid - before] = tid;
+      }
+      if (tid == 0) lists[128] = __popcll(mask);
+    }
+  }
+  __syncthreads();
+  if (ENVK == CPL_ENV_MIXED) n_sq = lists[128];
+  const int n_gr = valid - n_sq;
+  const bool compute = K.ablate != 1;
+
+  // ---- phase 1 (Superquadric): per-axis power ladders into the LDS scratch
+  if (HAS_SQ && compute && n_sq > 0 && (K.want_g || K.want_j)) {
+    const int items1 = 3 * N * n_sq;
+    for (int it = tid; it < items1; it += WG) {
+      const int j = it % n_sq, ka = it / n_sq;
+      const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
+      const int k = ka / 3, a = ka - 3 * k;
+      sq_axis_item(K, X + r * n, k, a, L + r * K.LR + k * SQ_L);
+    }
+    __syncthreads();
+  }
+
+  // ---- phase 2: SQ rows | Ground / no-env contacts | statics | cost
+  if (compute) {
+    const int r_sq = (HAS_SQ && (K.want_g || K.want_j)) ? 3 * N * n_sq : 0;
+    const int r_gr = (ENVK != CPL_ENV_SUPERQUADRIC && (K.want_g || K.want_j)) ? N * n_gr : 0;
+    const int r_st = (K.want_g || K.want_j) ? 4 * valid : 0;
+    const int r_co = K.cost_seg >= 0 ? valid : 0;
+    const int items2 = r_sq + r_gr + r_st + r_co;
+    for (int it = tid; it < items2; it += WG) {
+      int e = it;
+      if (e < r_sq) {
+        const int j = e % n_sq, ka = e / n_sq;
+        const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
+        const int k = ka / 3, a = ka - 3 * k;
+        sq_row_item(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m, Jt + r * nnz);
+        continue;
+      }
+      e -= r_sq;
+      if (e < r_gr) {
+        const int j = e % n_gr, k = e / n_gr;
+        const int r = ENVK == CPL_ENV_MIXED ? lists[64 + j] : j;
+        contact_item<ENVK == CPL_ENV_NONE ? CPL_ENV_NONE : CPL_ENV_GROUND>(K, X + r * n, CPL_ENV_GROUND, k,
+                                                                          Gt + r * m, Jt + r * nnz);
+        continue;
+      }
+      e -= r_gr;
+      if (e < r_st) {
+        const int r = e % valid, sg = e / valid;
+        const double* xr = X + r * n;
+        if (sg == 0) statics_values_item(K, xr, mass ? mass[b0 + r] : K.mass_default, Gt + r * m, Jt + r * nnz);
+        else if (K.want_j) statics_row_item(K, xr, sg - 1, Jt + r * nnz);
+        continue;
+      }
+      e -= r_st;
+      cost_item(K, X + e * n, f_out ? f_out + b0 + e : nullptr, Dt + e * n);
+    }
+  }
+  __syncthreads();
+  if (K.ablate == 2) return;
+  if (K.want_g) copy_out<WG, NT>(g_out + b0 * m, Gt, valid * m, tid);
+  if (K.want_j) copy_out<WG, NT>(jac_out + b0 * nnz, Jt, valid * nnz, tid);
+  if (K.want_grad) copy_out<WG, NT>(grad_out + b0 * n, Dt, valid * n, tid);
+}
+
 // ------------------------------------------------------------------------------------------
 // Residual norms of g against its bounds (per shard), deterministic two-stage reduction
 // ------------------------------------------------------------------------------------------
@@ -617,6 +1173,11 @@ static void fill_params(const cpl_problem_desc* d, KParams& K, const double* d_x
     K.P2m2[a] = P * 2.0 - 2.0;
     K.P2m3[a] = P * 2.0 - 3.0;
   }
+  K.sq_ladder = 1;
+  for (int a = 0; a < 3; ++a) {
+    const double P = d->sq_P[a];
+    if (!(P >= 2.0 && P <= 64.0 && P == std::floor(P))) K.sq_ladder = 0;
+  }
   for (int i = 0; i < CPL_MAX_CONTACTS; ++i) {
     K.F_thr[i] = d->F_thr[i];
     K.W_p[i] = d->W_p[i];
@@ -629,6 +1190,40 @@ static void fill_params(const cpl_problem_desc* d, KParams& K, const double* d_x
 
 static size_t eval_lds_bytes(int n) { return sizeof(double) * (size_t)(TILE * n + 2 * TILE * SROW); }
 
+// Tuning knobs (cpl_set_tuning): kernel variant and the LDS budget of one tile workgroup.
+// Default 64 KiB -> two workgroups (8 waves) per CU.
+static int g_variant = 0;          // 0 = tile-stationary (default), 1 = row-staged lane-per-instance
+static size_t g_tile_budget = 32 * 1024;
+static int g_wg = 256;             // threads per tile workgroup (128 or 256)
+static int g_nt = 1;               // non-temporal output stores
+static int g_ablate = 0;           // measurement-only: 1 = skip the compute phase, 2 = skip the stores
+
+static size_t tile_budget() { return g_tile_budget; }
+static bool use_rowstage() { return g_variant == 1; }
+
+static int32_t plan_tile(KParams& K, bool g, bool j, bool f, bool grad) {
+  K.want_g = g; K.want_j = j; K.want_f = f; K.want_grad = grad;
+  const bool sq = K.env_kind == CPL_ENV_SUPERQUADRIC || K.env_kind == CPL_ENV_MIXED;
+  K.LR = K.N * SQ_L + 1;  // odd instance stride of the SQ scratch: conflict-free LDS banks
+  const size_t per = sizeof(double) * (size_t)(K.n + (g ? K.m : 0) + (j ? K.nnz : 0) + (grad ? K.n : 0) +
+                                               (sq ? K.LR : 0));
+  const size_t fixed = sizeof(double) * 72;  // index lists
+  int T = 64, logT = 6;
+  while (T > 8 && (size_t)T * per + fixed > tile_budget()) { T >>= 1; --logT; }
+  // (T >= 8 is even, so every tile of every record array starts on a 16-byte boundary)
+  if ((size_t)T * per + fixed > 160 * 1024) return fail(CPL_ERR_UNSUPPORTED, "problem too large for one LDS tile");
+  K.T = T; K.logT = logT;
+  K.cost_seg = (f || grad) ? K.N + 4 : -1;
+  K.S = K.N + 4 + ((f || grad) ? 1 : 0);
+  K.offG = T * K.n;
+  K.offJ = K.offG + (g ? T * K.m : 0);
+  K.offD = K.offJ + (j ? T * K.nnz : 0);
+  K.offL = K.offD + (grad ? T * K.n : 0);
+  K.offI = K.offL + (sq ? T * K.LR : 0);
+  K.offI = (K.offI + 1) & ~1;
+  return CPL_OK;
+}
+
 static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
                            const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
                            hipStream_t stream) {
@@ -639,15 +1234,34 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
   if (!d_x) return fail(CPL_ERR_INVALID_ARGUMENT, "x is required");
   if (d->env_kind == CPL_ENV_MIXED && !d_env_tag)
     return fail(CPL_ERR_INVALID_ARGUMENT, "mixed environment batch needs a per-instance env tag array");
-  if ((batch + TILE - 1) / TILE > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "batch too large");
+  if ((batch + 7) / 8 > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "batch too large");
   if (!d_g && !d_jac && !d_f && !d_grad) return CPL_OK;
   KParams K;
   fill_params(d, K, d_x);
-  const size_t lds = eval_lds_bytes(K.n);
-  if (lds > 160 * 1024) return fail(CPL_ERR_UNSUPPORTED, "problem too large for one LDS tile");
-  const unsigned grid = (unsigned)((batch + TILE - 1) / TILE);
-  hipLaunchKernelGGL(cpl_eval_kernel, dim3(grid), dim3(TILE), lds, stream, K, batch, d_x, d_mass, d_env_tag,
-                     d_g, d_jac, d_f, d_grad);
+  if (use_rowstage()) {
+    const size_t lds = eval_lds_bytes(K.n);
+    if (lds > 160 * 1024) return fail(CPL_ERR_UNSUPPORTED, "problem too large for one LDS tile");
+    const unsigned grid = (unsigned)((batch + TILE - 1) / TILE);
+    hipLaunchKernelGGL(cpl_eval_kernel, dim3(grid), dim3(TILE), lds, stream, K, batch, d_x, d_mass, d_env_tag,
+                       d_g, d_jac, d_f, d_grad);
+  } else {
+    st = plan_tile(K, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr);
+    if (st) return st;
+    K.ablate = g_ablate;
+    const size_t lds = sizeof(double) * (size_t)(K.offI + 72);
+    const unsigned grid = (unsigned)((batch + K.T - 1) / K.T);
+    using KernT = void (*)(const KParams, int64_t, const double*, const double*, const uint8_t*, double*, double*,
+                           double*, double*);
+#define CPL_TILE_KERNELS(E) \
+  {cpl_eval_tile_kernel<E, 128, false>, cpl_eval_tile_kernel<E, 128, true>, cpl_eval_tile_kernel<E, 256, false>, \
+   cpl_eval_tile_kernel<E, 256, true>}
+    static const KernT table[4][4] = {CPL_TILE_KERNELS(CPL_ENV_NONE), CPL_TILE_KERNELS(CPL_ENV_GROUND),
+                                      CPL_TILE_KERNELS(CPL_ENV_SUPERQUADRIC), CPL_TILE_KERNELS(CPL_ENV_MIXED)};
+#undef CPL_TILE_KERNELS
+    const KernT kern = table[K.env_kind][(g_wg == 256 ? 2 : 0) + (g_nt ? 1 : 0)];
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(g_wg), lds, stream, K, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f,
+                       d_grad);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "cpl_eval_kernel launch");
   return CPL_OK;
@@ -667,6 +1281,20 @@ int32_t cpl_eval_batch(const cpl_problem_desc* d, int64_t batch, const double* d
                        const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
                        void* stream) {
   return launch_eval(d, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f, d_grad, (hipStream_t)stream);
+}
+
+int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_threads, int32_t nt_stores,
+                       int32_t ablate) {
+  if (ablate < 0 || ablate > 2) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
+  g_ablate = ablate;
+  if (kernel_variant < 0 || kernel_variant > 1) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown kernel variant");
+  if (tile_lds_kb < 8 || tile_lds_kb > 160) return fail(CPL_ERR_INVALID_ARGUMENT, "tile LDS budget out of [8, 160] KiB");
+  if (wg_threads != 128 && wg_threads != 256) return fail(CPL_ERR_INVALID_ARGUMENT, "workgroup size must be 128 or 256");
+  g_variant = kernel_variant;
+  g_tile_budget = (size_t)tile_lds_kb * 1024;
+  g_wg = wg_threads;
+  g_nt = nt_stores ? 1 : 0;
+  return CPL_OK;
 }
 
 int32_t cpl_residual_norms(const cpl_problem_desc* d, int64_t batch, const double* d_g, double* d_out, void* stream) {
@@ -711,12 +1339,12 @@ int32_t cpl_time_eval_batch(const cpl_problem_desc* d, int64_t batch, const doub
   hipError_t e = hipEventCreate(&e0);
   if (e != hipSuccess) return hip_fail(e, "hipEventCreate");
   e = hipEventCreate(&e1);
-  if (e != hipSuccess) { hipEventDestroy(e0); return hip_fail(e, "hipEventCreate"); }
+  if (e != hipSuccess) { (void)hipEventDestroy(e0); return hip_fail(e, "hipEventCreate"); }
   int32_t st = CPL_OK;
-  hipEventRecord(e0, s);
+  (void)hipEventRecord(e0, s);
   for (int32_t r = 0; r < reps && st == CPL_OK; ++r)
     st = launch_eval(d, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f, d_grad, s);
-  hipEventRecord(e1, s);
+  (void)hipEventRecord(e1, s);
   e = hipEventSynchronize(e1);
   if (st == CPL_OK && e != hipSuccess) st = hip_fail(e, "hipEventSynchronize");
   float ms = 0.0f;
@@ -724,8 +1352,8 @@ int32_t cpl_time_eval_batch(const cpl_problem_desc* d, int64_t batch, const doub
     e = hipEventElapsedTime(&ms, e0, e1);
     if (e != hipSuccess) st = hip_fail(e, "hipEventElapsedTime");
   }
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
   if (st == CPL_OK) *ms_per_launch = (double)ms / reps;
   return st;
 }

@@ -171,6 +171,15 @@ int32_t cpl_time_eval_batch(const cpl_problem_desc* d, int64_t batch, const doub
                             double* d_jac, double* d_f, double* d_grad, void* stream,
                             int32_t reps, double* ms_per_launch);
 
+/* Tuning knobs (process-wide, for A/B measurements): kernel_variant 0 = tile-stationary
+ * (default), 1 = row-staged lane-per-instance; tile_lds_kb = LDS budget of one tile workgroup
+ * (8..160 KiB, default 32); wg_threads = 128 or 256 (default 256); nt_stores = non-temporal
+ * output stores (default 1); ablate = measurement-only ablation of the tile kernel (0 = off,
+ * 1 = skip the compute phase, 2 = skip the output stores: results are then garbage).
+ * Not thread-safe against concurrent launches. */
+int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_threads, int32_t nt_stores,
+                       int32_t ablate);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,60 @@
+"""A/B of eval-kernel variants in ONE process, interleaved rounds (guide §5.4 rule 24).
+
+python scripts/ab_kernels.py [--config ground4] [--rounds 5] [--reps 20]
+Prints one JSON line per (variant, lds budget) with median / min ms and achieved GB/s.
+"""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from bench import algorithmic_bytes  # noqa: E402
+from centroidalplanner_amd import _abi  # noqa: E402
+from centroidalplanner_amd.workload import CONFIGS, config_inputs  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="ground4")
+ap.add_argument("--batch", type=int, default=0)
+ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--reps", type=int, default=20)
+ap.add_argument("--variants", default="0:32:256:0,0:16:128:0,0:24:128:0,0:32:128:0,0:32:256:1,0:16:128:1,0:48:256:0")
+ap.add_argument("--outputs", default="g,jac")
+args = ap.parse_args()
+
+cfg = CONFIGS[args.config]
+B = args.batch or cfg.batch
+prob, x, mass, tag = config_inputs(cfg, B)
+dev = torch.device("cuda:0")
+xt, mt = torch.tensor(x, device=dev), torch.tensor(mass, device=dev)
+tt = None if tag is None else torch.tensor(tag, device=dev)
+outs = tuple(args.outputs.split(","))
+out = prob.eval_batch(xt, mt, tt, outputs=outs)
+stream = torch.cuda.current_stream()
+variants = [tuple(int(v) for v in s.split(":")) for s in args.variants.split(",")]
+times = {v: [] for v in variants}
+
+
+def p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+for _ in range(args.rounds):
+    for v in variants:
+        _abi.check(_abi.lib.cpl_set_tuning(v[0], v[1], v[2], v[3], v[4] if len(v) > 4 else 0))
+        ms = ctypes.c_double()
+        _abi.check(_abi.lib.cpl_time_eval_batch(ctypes.byref(prob.desc()), B, p(xt), p(mt), p(tt), p(out.get("g")),
+                                                p(out.get("jac")), p(out.get("f")), p(out.get("grad")),
+                                                ctypes.c_void_p(stream.cuda_stream), args.reps, ctypes.byref(ms)))
+        times[v].append(ms.value)
+bpi, m = algorithmic_bytes(cfg.n_contacts, cfg.env, outs)
+for v, ts in times.items():
+    med = statistics.median(ts)
+    print(json.dumps({"config": args.config, "batch": B, "variant": v[0], "lds_kb": v[1], "wg": v[2], "nt": v[3], "ablate": v[4] if len(v) > 4 else 0, "median_ms": med,
+                      "min_ms": min(ts), "GBps": bpi * B / (med * 1e-3) / 1e9,
+                      "rows_per_s": B * m / (med * 1e-3)}), flush=True)
