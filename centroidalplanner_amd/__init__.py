@@ -7,9 +7,14 @@ Importing it loads ``libcpl_mi355x.so`` and fails loudly if it has not been buil
 """
 from ._abi import (ENV_GROUND, ENV_MIXED, ENV_NONE, ENV_SUPERQUADRIC, INF, MAX_CONTACTS, CplError, InvalidArgument,
                    OutOfRange, ProblemDesc)
+from .planner import CentroidalPlanner, CoMPlanner, ContactValues, Solution
 from .problem import CplProblem, EnvironmentClass, Ground, MixedEnvironment, Superquadric
 
 __all__ = [
+    "CentroidalPlanner",
+    "CoMPlanner",
+    "Solution",
+    "ContactValues",
     "CplProblem",
     "EnvironmentClass",
     "Ground",

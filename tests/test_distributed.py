@@ -1,0 +1,95 @@
+"""Multi-process (world_size 2, gloo on CPU) test of the sharded path: each rank evaluates its
+contiguous shard of one seeded batch (here through the oracle: the CPU stands in for the rank's GPU),
+computes its shard's residual norms, and the all-gather + combine must reproduce the norms of the
+whole batch; the shards must tile the batch exactly."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from centroidalplanner_amd.distributed import combine_norms, shard
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _norms(g, gl, gu):
+    viol = np.maximum(np.maximum(gl - g, g - gu), 0.0)
+    viol = np.where(np.isnan(g), np.inf, viol)
+    return np.array([viol.max(initial=0.0), (viol ** 2).sum()])
+
+
+def _worker(rank, world, port, batch, q):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    import pyoracle
+    import torch.distributed as dist
+
+    from centroidalplanner_amd.distributed import all_gather_norms
+    from centroidalplanner_amd.workload import generate, make_problem
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    prob = make_problem(4, "ground")
+    x, mass, _ = generate(4, "ground", batch, 2024)
+    start, count = shard(batch, rank, world)
+    g = pyoracle.eval_batch(prob.desc(), x[start:start + count], mass[start:start + count], outputs=("g",),
+                            nthreads=1)["g"]
+    _, _, gl, gu = prob.get_bounds_info()
+    local = torch.tensor(_norms(g, gl, gu), dtype=torch.float64)
+    out, work = all_gather_norms(local, async_op=True)
+    work.wait()
+    q.put((rank, start, count, out.numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("batch", [1001, 64])
+def test_sharded_norms_gloo_world2(batch):
+    import pyoracle
+    from centroidalplanner_amd.workload import generate, make_problem
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, batch, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    assert sum(r[2] for r in res) == batch and res[0][1] == 0 and res[1][1] == res[0][2]
+    assert np.array_equal(res[0][3], res[1][3])  # every rank sees the same gathered vector
+    gmax, gsum = combine_norms(res[0][3])
+    prob = make_problem(4, "ground")
+    x, mass, _ = generate(4, "ground", batch, 2024)
+    g = pyoracle.eval_batch(prob.desc(), x, mass, outputs=("g",), nthreads=1)["g"]
+    _, _, gl, gu = prob.get_bounds_info()
+    full = _norms(g, gl, gu)
+    assert gmax == full[0]
+    assert gsum == pytest.approx(full[1], rel=1e-12)
+
+
+def test_shard_tiles_batch():
+    for batch in (0, 1, 7, 65536, 1048577):
+        for world in (1, 2, 3, 8):
+            got = [shard(batch, r, world) for r in range(world)]
+            assert got[0][0] == 0
+            assert all(got[r][0] + got[r][1] == got[r + 1][0] for r in range(world - 1))
+            assert got[-1][0] + got[-1][1] == batch
+            assert max(c for _, c in got) - min(c for _, c in got) <= 1
