@@ -28,7 +28,8 @@ ERR_UNSUPPORTED = 5
 INF = 1.0e20
 
 LIB_NAME = "libcpl_mi355x.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# CPL_LIB: measurement-only override (A/B of two builds of the same ABI)
+LIB_PATH = os.environ.get("CPL_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 _V3 = c_double * 3
 _V3N = _V3 * MAX_CONTACTS

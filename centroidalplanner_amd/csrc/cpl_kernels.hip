@@ -62,11 +62,37 @@ struct KParams {
   int32_t cost_seg;      // segment index of the cost item, -1 if f/grad not requested
   int32_t offG, offJ, offD, offL, offI;
   int32_t LR;            // doubles per instance in the SQ scratch (N*SQ_L + 1)
+  int32_t offX1, offMB, offTB;  // pipelined kernel: second x buffer, masses, env tags
   int32_t want_g, want_j, want_f, want_grad;
   int32_t ablate;        // measurement-only ablation (cpl_set_tuning), 0 in production
   int32_t sq_ladder;     // every P_a is an integer in [2, 64]: double-double power ladders
 };
 static_assert(sizeof(KParams) < 4096, "kernel parameters must fit the kernarg segment");
+
+// Per-block LDS copy of the parameter tables the work items index with a lane-varying contact or
+// axis index.  A kernarg read with a divergent index is a vector memory load, and its vmcnt wait
+// would also drain the wave's in-flight output stores; an LDS read waits on lgkmcnt only.
+struct CTab {
+  int32_t map_order[CPL_MAX_CONTACTS];
+  double F_thr[CPL_MAX_CONTACTS];
+  double C[3], R[3], P[3], Pm1[3], P2[3], P2m2[3], P2m3[3], EJ[3], Ka[3], Kb[3], Rm2[3], Rp2[3], Psq[3];
+};
+__shared__ CTab s_ct;
+
+// cooperative fill; the caller's next block barrier publishes it
+__device__ __forceinline__ void load_ctab(const KParams& K) {
+  const int t = threadIdx.x;
+  if (t < CPL_MAX_CONTACTS) {
+    s_ct.map_order[t] = K.map_order[t];
+    s_ct.F_thr[t] = K.F_thr[t];
+  } else if (t < CPL_MAX_CONTACTS + 3) {
+    const int a = t - CPL_MAX_CONTACTS;
+    s_ct.C[a] = K.C[a]; s_ct.R[a] = K.R[a]; s_ct.P[a] = K.P[a];
+    s_ct.Pm1[a] = K.Pm1[a]; s_ct.P2[a] = K.P2[a]; s_ct.P2m2[a] = K.P2m2[a]; s_ct.P2m3[a] = K.P2m3[a];
+    s_ct.EJ[a] = K.EJ[a]; s_ct.Ka[a] = K.Ka[a]; s_ct.Kb[a] = K.Kb[a];
+    s_ct.Rm2[a] = K.Rm2[a]; s_ct.Rp2[a] = K.Rp2[a]; s_ct.Psq[a] = K.Psq[a];
+  }
+}
 
 // ------------------------------------------------------------------------------------------
 // double-double helpers for exact-exponent pow
@@ -257,7 +283,7 @@ struct AxisPowers {
 };
 __device__ __forceinline__ void axis_powers(const KParams& K, int a, double d, AxisPowers& o) {
   if (K.sq_ladder) {
-    const dd B = dd_ipow(d, (unsigned)K.P[a] - 2u);
+    const dd B = dd_ipow(d, (unsigned)s_ct.P[a] - 2u);
     const dd A = dd_mul_d(B, d);
     const dd Q = dd_mul_d(A, d);
     const double q2 = dd_sqr(Q).hi;
@@ -270,11 +296,11 @@ __device__ __forceinline__ void axis_powers(const KParams& K, int a, double d, A
       return;
     }
   }
-  o.pm1 = cpow(d, K.Pm1[a]);
-  o.pP = cpow(d, K.P[a]);
-  o.p2Pm3 = cpow(d, K.P2m3[a]);
-  o.p2Pm2 = cpow(d, K.P2m2[a]);
-  o.p2P = cpow(d, K.P2[a]);
+  o.pm1 = cpow(d, s_ct.Pm1[a]);
+  o.pP = cpow(d, s_ct.P[a]);
+  o.p2Pm3 = cpow(d, s_ct.P2m3[a]);
+  o.p2Pm2 = cpow(d, s_ct.P2m2[a]);
+  o.p2P = cpow(d, s_ct.P2[a]);
 }
 
 __device__ __forceinline__ void superquadric_contact(const KParams& K, double p0, double p1, double p2,
@@ -390,6 +416,8 @@ __global__ __launch_bounds__(TILE) void cpl_eval_kernel(const KParams K, int64_t
                                                          double* __restrict__ f_out,
                                                          double* __restrict__ grad_out) {
   extern __shared__ __align__(16) double smem[];
+  load_ctab(K);
+  __syncthreads();
   const int lane = threadIdx.x;
   const int n = K.n;
   const int N = K.N;
@@ -652,7 +680,7 @@ __device__ __forceinline__ void copy_out(double* __restrict__ dst, const double*
 template <int ENVK>
 __device__ __forceinline__ void contact_item(const KParams& K, const double* __restrict__ xr, int kind, int k,
                                              double* __restrict__ Gr, double* __restrict__ Jr) {
-  const int i = K.map_order[k];
+  const int i = s_ct.map_order[k];
   const double* q = xr + 3 + 9 * i;
   const double F0 = q[0], F1 = q[1], F2 = q[2];
   const double p0 = q[3], p1 = q[4], p2 = q[5];
@@ -700,7 +728,7 @@ __device__ __forceinline__ void contact_item(const KParams& K, const double* __r
   if (wg) {
     const double nF = dot3(n0, n1, n2, F0, F1, F2);
     const double u0 = F0 - nF * n0, u1 = F1 - nF * n1, u2 = F2 - nF * n2;
-    gk[0] = -t1 + K.F_thr[i];
+    gk[0] = -t1 + s_ct.F_thr[i];
     gk[1] = sqrt((u0 * u0 + u1 * u1) + u2 * u2) - mu * t1;
   }
   if (wj) {
@@ -731,7 +759,7 @@ __device__ __forceinline__ void statics_values_item(const KParams& K, const doub
     const double c0 = xr[0], c1 = xr[1], c2 = xr[2];
     double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0, v4 = 0.0, v5 = 0.0;
     for (int k = 0; k < N; ++k) {
-      const double* q = xr + 3 + 9 * K.map_order[k];
+      const double* q = xr + 3 + 9 * s_ct.map_order[k];
       const double F0 = q[0], F1 = q[1], F2 = q[2];
       const double d0 = q[3] - c0, d1 = q[4] - c1, d2 = q[5] - c2;
       v0 += F0; v1 += F1; v2 += F2;
@@ -763,7 +791,7 @@ __device__ __forceinline__ void statics_row_item(const KParams& K, const double*
   const double ce1 = xr[e1], ce2 = xr[e2];
   double a1 = 0.0, a2 = 0.0;
   for (int k = 0; k < N; ++k) {  // CoM block: -= the p-block entries in map order (:119-136)
-    const double* F = xr + 3 + 9 * K.map_order[k];
+    const double* F = xr + 3 + 9 * s_ct.map_order[k];
     a1 -= -s1 * F[e1];
     a2 -= -s2 * F[e2];
   }
@@ -788,7 +816,7 @@ __device__ __forceinline__ void cost_item(const KParams& K, const double* __rest
   if (K.want_f) {
     double value = 0;
     for (int k = 0; k < N; ++k) {
-      const int i = K.map_order[k];
+      const int i = s_ct.map_order[k];
       const double* q = xr + 3 + 9 * i;
       const double e0 = q[3] - K.p_ref[i][0], e1 = q[4] - K.p_ref[i][1], e2 = q[5] - K.p_ref[i][2];
       const double h0 = q[0] - K.F_ref[i][0], h1 = q[1] - K.F_ref[i][1], h2 = q[2] - K.F_ref[i][2];
@@ -827,18 +855,18 @@ enum { L_PM1 = 0, L_PP, L_P2PM3, L_P2PM2, L_P2P, L_INV, L_WENV, L_AXIS };
 
 __device__ __forceinline__ void sq_axis_item(const KParams& K, const double* __restrict__ xr, int k, int a,
                                              double* __restrict__ Lc) {
-  const int i = K.map_order[k];
+  const int i = s_ct.map_order[k];
   const double pa = xr[6 + 9 * i + a];
-  const double d = -K.C[a] + pa;
+  const double d = -s_ct.C[a] + pa;
   double* o = Lc + a * L_AXIS;
   // src/Superquadric.cpp:45  pow((p-C)/R, P)
-  const double u = (pa - K.C[a]) / K.R[a];
+  const double u = (pa - s_ct.C[a]) / s_ct.R[a];
   double w;
   if (K.sq_ladder && fabs(u) >= DD_TINY && fabs(u) <= 0x1p+40) {
-    w = dd_ipow(u, (unsigned)K.P[a]).hi;
-    if (!(fabs(w) >= DD_TINY && fabs(w) <= DD_HUGE)) w = cpow(u, K.P[a]);
+    w = dd_ipow(u, (unsigned)s_ct.P[a]).hi;
+    if (!(fabs(w) >= DD_TINY && fabs(w) <= DD_HUGE)) w = cpow(u, s_ct.P[a]);
   } else {
-    w = cpow(u, K.P[a]);
+    w = cpow(u, s_ct.P[a]);
   }
   o[L_WENV] = w;
   if (K.want_j) {
@@ -849,10 +877,10 @@ __device__ __forceinline__ void sq_axis_item(const KParams& K, const double* __r
     o[L_P2PM3] = ap.p2Pm3;
     o[L_P2PM2] = ap.p2Pm2;
     o[L_P2P] = ap.p2P;
-    const double t = K.C[a] - pa;
+    const double t = s_ct.C[a] - pa;
     o[L_INV] = 1.0 / (t * t);
   } else {
-    o[L_PM1] = cpow(d, K.Pm1[a]);  // src/Superquadric.cpp:54-56 (normal value only)
+    o[L_PM1] = cpow(d, s_ct.Pm1[a]);  // src/Superquadric.cpp:54-56 (normal value only)
   }
 }
 
@@ -866,7 +894,7 @@ __device__ __forceinline__ void cone_rows(const KParams& K, int i, const double*
   if (K.want_g) {
     const double nF = dot3(n0, n1, n2, F0, F1, F2);
     const double u0 = F0 - nF * n0, u1 = F1 - nF * n1, u2 = F2 - nF * n2;
-    gk[0] = -t1 + K.F_thr[i];
+    gk[0] = -t1 + s_ct.F_thr[i];
     gk[1] = sqrt((u0 * u0 + u1 * u1) + u2 * u2) - mu * t1;
   }
   if (K.want_j) {
@@ -891,7 +919,7 @@ __device__ __forceinline__ void cone_rows(const KParams& K, int i, const double*
 __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __restrict__ xr, int k, int a,
                                             const double* __restrict__ Lc, double* __restrict__ Gr,
                                             double* __restrict__ Jr) {
-  const int i = K.map_order[k];
+  const int i = s_ct.map_order[k];
   const double* q = xr + 3 + 9 * i;
   double* gk = Gr + 6 + 6 * k;
   double* jk = Jr + 6 + 15 * K.N + 27 * k;
@@ -927,25 +955,25 @@ __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __re
   const double p_b = q[3 + b], p_c = q[3 + c];
   double out[3];
   {  // diagonal (a, a)
-    double lead = K.Ka[a];
+    double lead = s_ct.Ka[a];
 #pragma unroll
     for (int kk = 0; kk < 3; ++kk) {
       lead = lead * (kk == a ? La[L_PP] : K.Rm2[kk]);
       lead = lead * Lc[kk * L_AXIS + L_INV];
     }
-    lead = lead * K.Pm1[a];
+    lead = lead * s_ct.Pm1[a];
     lead = lead * 1.0;
-    const double Tb = ((K.Rm2[b] * Lb[L_INV]) * K.Psq[b]) * Lb[L_P2P];
-    const double Tc = ((K.Rm2[c] * Lcc[L_INV]) * K.Psq[c]) * Lcc[L_P2P];
-    const double Dg = (K.Kb[a] * La[L_P2P]) * La[L_INV];
+    const double Tb = ((s_ct.Rm2[b] * Lb[L_INV]) * s_ct.Psq[b]) * Lb[L_P2P];
+    const double Tc = ((s_ct.Rm2[c] * Lcc[L_INV]) * s_ct.Psq[c]) * Lcc[L_P2P];
+    const double Dg = (s_ct.Kb[a] * La[L_P2P]) * La[L_INV];
     const double S = (Tb + Tc) + Dg;
     const double p2Pb = Lb[L_P2P], p2Pc = Lcc[L_P2P];
-    const double E = (((((((K.C[b] * K.C[b]) * K.Psq[c]) * p2Pc) * K.Rp2[b] +
-                         (((K.C[c] * K.C[c]) * K.Psq[b]) * p2Pb) * K.Rp2[c]) +
-                        (((p_b * p_b) * K.Psq[c]) * p2Pc) * K.Rp2[b]) +
-                       (((p_c * p_c) * K.Psq[b]) * p2Pb) * K.Rp2[c]) -
-                      ((((K.C[b] * p_b) * K.Psq[c]) * p2Pc) * K.Rp2[b]) * 2.0) -
-                     ((((K.C[c] * p_c) * K.Psq[b]) * p2Pb) * K.Rp2[c]) * 2.0;
+    const double E = (((((((s_ct.C[b] * s_ct.C[b]) * s_ct.Psq[c]) * p2Pc) * s_ct.Rp2[b] +
+                         (((s_ct.C[c] * s_ct.C[c]) * s_ct.Psq[b]) * p2Pb) * s_ct.Rp2[c]) +
+                        (((p_b * p_b) * s_ct.Psq[c]) * p2Pc) * s_ct.Rp2[b]) +
+                       (((p_c * p_c) * s_ct.Psq[b]) * p2Pb) * s_ct.Rp2[c]) -
+                      ((((s_ct.C[b] * p_b) * s_ct.Psq[c]) * p2Pc) * s_ct.Rp2[b]) * 2.0) -
+                     ((((s_ct.C[c] * p_c) * s_ct.Psq[b]) * p2Pb) * s_ct.Rp2[c]) * 2.0;
     out[a] = lead / pow_three_halves(S) * E;
   }
 #pragma unroll
@@ -953,7 +981,7 @@ __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __re
     if (bb == a) continue;
     const int oo = 3 - a - bb;
     const double* Lbb = Lc + bb * L_AXIS;
-    double lead = K.Ka[a];
+    double lead = s_ct.Ka[a];
     if (a < bb) {  // src/Superquadric.cpp:109, 119, 163
       lead = lead * La[L_PM1];
       lead = lead * K.Psq[bb];
@@ -967,7 +995,7 @@ __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __re
     }
     lead = lead * K.Rm2[bb];
     lead = lead * 1.0;
-    const double S = (K.Kb[oo] * Lc[oo * L_AXIS + L_P2PM2] + K.Kb[a] * La[L_P2PM2]) +
+    const double S = (s_ct.Kb[oo] * Lc[oo * L_AXIS + L_P2PM2] + s_ct.Kb[a] * La[L_P2PM2]) +
                      (K.Psq[bb] * Lbb[L_P2PM2]) * K.Rm2[bb];
     out[bb] = lead / pow_three_halves(S) * (-1.0 / 2.0);
   }
@@ -985,6 +1013,8 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
                                                             double* __restrict__ f_out,
                                                             double* __restrict__ grad_out) {
   extern __shared__ __align__(16) double smem[];
+  load_ctab(K);
+  __syncthreads();
   const int tid = threadIdx.x;
   const int T = K.T;
   const int n = K.n, m = K.m, nnz = K.nnz, N = K.N;
@@ -1071,6 +1101,219 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
   if (K.want_g) copy_out<WG, NT>(g_out + b0 * m, Gt, valid * m, tid);
   if (K.want_j) copy_out<WG, NT>(jac_out + b0 * nnz, Jt, valid * nnz, tid);
   if (K.want_grad) copy_out<WG, NT>(grad_out + b0 * n, Dt, valid * n, tid);
+}
+
+
+// ------------------------------------------------------------------------------------------
+// v3: persistent, warp-specialised pipeline over tiles.
+//   * a workgroup = NCW compute waves + 1 loader wave, resident for the whole launch, walking tiles
+//     blockIdx.x, blockIdx.x + gridDim.x, ...;
+//   * the loader wave DMAs the NEXT tile's x into the other half of a double-buffered LDS image
+//     (global_load_lds_dwordx4, 1 KiB per wave-instruction) and stages its masses / env tags, while
+//     the compute waves evaluate the current tile; the loader issues no stores, so its vmcnt drain
+//     waits for its own loads only;
+//   * the compute waves issue no global loads and synchronise with LDS-only barriers
+//     (s_waitcnt lgkmcnt(0) + s_barrier), so their output stores keep draining across tiles;
+//   * work items and the full-line copy-out are those of the tile kernel above.
+// ------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// loader wave: DMA `count` doubles (16-B aligned source) into LDS; the odd last double is returned
+// through *tail for a plain store after the drain
+__device__ __forceinline__ void dma_tile(double* dst, const double* src, int count, int lane) {
+  const int pieces = (count + 127) >> 7;
+  for (int p = 0; p < pieces; ++p) {
+    const int e = p * 128 + lane * 2;
+    if (e + 1 < count) __builtin_amdgcn_global_load_lds((glb_void_t*)(src + e), (lds_void_t*)(dst + p * 128), 16, 0, 0);
+  }
+}
+
+template <int CT, bool NT>
+__device__ __forceinline__ void copy_out_ct(double* __restrict__ dst, const double* __restrict__ src, int count,
+                                            int tid) {
+  if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+    const int pairs = count >> 1;
+    const double2* s2 = reinterpret_cast<const double2*>(src);
+    double2* d2 = reinterpret_cast<double2*>(dst);
+    for (int e = tid; e < pairs; e += CT) {
+      const double2 v = s2[e];
+      if (NT) {
+        __builtin_nontemporal_store(v.x, &d2[e].x);
+        __builtin_nontemporal_store(v.y, &d2[e].y);
+      } else {
+        d2[e] = v;
+      }
+    }
+    if ((count & 1) && tid == 0) dst[count - 1] = src[count - 1];
+  } else {
+    for (int e = tid; e < count; e += CT) dst[e] = src[e];
+  }
+}
+
+template <int ENVK, int NCW, bool NT>
+__global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KParams K, int64_t batch,
+                                                                        const double* __restrict__ x,
+                                                                        const double* __restrict__ mass,
+                                                                        const uint8_t* __restrict__ env_tag,
+                                                                        double* __restrict__ g_out,
+                                                                        double* __restrict__ jac_out,
+                                                                        double* __restrict__ f_out,
+                                                                        double* __restrict__ grad_out) {
+  constexpr int CT = 64 * NCW;  // compute threads
+  constexpr bool HAS_SQ = ENVK == CPL_ENV_SUPERQUADRIC || ENVK == CPL_ENV_MIXED;
+  extern __shared__ __align__(16) double smem[];
+  load_ctab(K);
+  __syncthreads();
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const bool loader = (tid >> 6) == NCW;
+  const int T = K.T;
+  const int n = K.n, m = K.m, nnz = K.nnz, N = K.N;
+  const int64_t ntiles = (batch + T - 1) / T;
+  // buffer selection by offset from smem (an array of pointers would lose the LDS address space
+  // and turn every access into a flat access that also counts in vmcnt)
+  auto XB = [&](int bi) { return smem + (bi ? K.offX1 : 0); };
+  auto MB = [&](int bi) { return smem + K.offMB + (bi ? T : 0); };
+  auto TB = [&](int bi) { return reinterpret_cast<int*>(smem + K.offTB) + (bi ? T : 0); };
+  double* Gt = smem + K.offG;
+  double* Jt = smem + K.offJ;
+  double* Dt = smem + K.offD;
+  double* L = smem + K.offL;
+  int* lists = reinterpret_cast<int*>(smem + K.offI);
+
+  int64_t t = blockIdx.x;
+  if (t >= ntiles) return;
+
+  // loader: stage tile `tt` into buffer `bi`; loads only (the drain comes later)
+  double st_mass = 0.0, st_tail = 0.0;
+  int st_tag = 0;
+  auto stage = [&](int64_t tt, int bi) {
+    const int64_t b0s = tt * T;
+    const int vs = (int)((batch - b0s) < T ? (batch - b0s) : T);
+    const int count = vs * n;
+    dma_tile(XB(bi), x + b0s * n, count, lane);
+    if ((count & 1) && lane == 0) st_tail = x[b0s * n + count - 1];
+    if (lane < vs) {
+      st_mass = mass ? mass[b0s + lane] : K.mass_default;
+      if (ENVK == CPL_ENV_MIXED) st_tag = env_tag[b0s + lane];
+    }
+  };
+  auto finish_stage = [&](int64_t tt, int bi) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int64_t b0s = tt * T;
+    const int vs = (int)((batch - b0s) < T ? (batch - b0s) : T);
+    const int count = vs * n;
+    if ((count & 1) && lane == 0) XB(bi)[count - 1] = st_tail;
+    if (lane < vs) {
+      MB(bi)[lane] = st_mass;
+      if (ENVK == CPL_ENV_MIXED) TB(bi)[lane] = st_tag;
+    }
+  };
+
+  // The two roles run separate loops with the same barrier sequence per tile, so the compiler's
+  // wait-count analysis never sees a pending LDS-DMA on the compute path (no vmcnt drains there).
+  if (loader) {
+    stage(t, 0);
+    finish_stage(t, 0);
+    lds_barrier();
+    int cur = 0;
+    for (; t < ntiles; t += gridDim.x) {
+      const int64_t tn = t + gridDim.x;
+      if (tn < ntiles) stage(tn, cur ^ 1);
+      if (ENVK == CPL_ENV_MIXED) lds_barrier();
+      if (HAS_SQ) lds_barrier();
+      lds_barrier();
+      if (tn < ntiles) finish_stage(tn, cur ^ 1);
+      lds_barrier();
+      cur ^= 1;
+    }
+    return;
+  }
+
+  lds_barrier();
+  int cur = 0;
+  for (; t < ntiles; t += gridDim.x) {
+    const int64_t b0 = t * T;
+    const int valid = (int)((batch - b0) < T ? (batch - b0) : T);
+    const double* X = XB(cur);
+    if (ENVK == CPL_ENV_MIXED) {
+      if (tid < 64) {
+        const bool is_sq = tid < valid && TB(cur)[tid] == CPL_ENV_SUPERQUADRIC;
+        const unsigned long long msk = __ballot(is_sq);
+        if (tid < valid) {
+          const int before = __popcll(msk & ((1ull << tid) - 1ull));
+          if (is_sq) lists[before] = tid;
+          else lists[64 + tid - before] = tid;
+        }
+        if (tid == 0) lists[128] = __popcll(msk);
+      }
+      lds_barrier();
+    }
+    const int n_sq = ENVK == CPL_ENV_SUPERQUADRIC ? valid : (ENVK == CPL_ENV_MIXED ? lists[128] : 0);
+    const int n_gr = valid - n_sq;
+    const bool wgj = K.want_g || K.want_j;
+
+    // ---- phase 1 (Superquadric power ladders)
+    if (HAS_SQ) {
+      if (n_sq > 0 && wgj && K.ablate != 1) {
+        const int items1 = 3 * N * n_sq;
+        for (int it = tid; it < items1; it += CT) {
+          const int j = it % n_sq, ka = it / n_sq;
+          const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
+          const int k = ka / 3, a = ka - 3 * k;
+          sq_axis_item(K, X + r * n, k, a, L + r * K.LR + k * SQ_L);
+        }
+      }
+      lds_barrier();
+    }
+    // ---- phase 2
+    if (K.ablate != 1) {
+      const int r_sq = (HAS_SQ && wgj) ? 3 * N * n_sq : 0;
+      const int r_gr = (ENVK != CPL_ENV_SUPERQUADRIC && wgj) ? N * n_gr : 0;
+      const int r_st = wgj ? 4 * valid : 0;
+      const int r_co = K.cost_seg >= 0 ? valid : 0;
+      const int items2 = r_sq + r_gr + r_st + r_co;
+      for (int it = tid; it < items2; it += CT) {
+        int e = it;
+        if (HAS_SQ && e < r_sq) {
+          const int j = e % n_sq, ka = e / n_sq;
+          const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
+          const int k = ka / 3, a = ka - 3 * k;
+          sq_row_item(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m, Jt + r * nnz);
+          continue;
+        }
+        e -= r_sq;
+        if (e < r_gr) {
+          const int j = e % n_gr, k = e / n_gr;
+          const int r = ENVK == CPL_ENV_MIXED ? lists[64 + j] : j;
+          contact_item<ENVK == CPL_ENV_NONE ? CPL_ENV_NONE : CPL_ENV_GROUND>(K, X + r * n, CPL_ENV_GROUND, k,
+                                                                            Gt + r * m, Jt + r * nnz);
+          continue;
+        }
+        e -= r_gr;
+        if (e < r_st) {
+          const int r = e % valid, sg = e / valid;
+          const double* xr = X + r * n;
+          if (sg == 0) statics_values_item(K, xr, MB(cur)[r], Gt + r * m, Jt + r * nnz);
+          else if (K.want_j) statics_row_item(K, xr, sg - 1, Jt + r * nnz);
+          continue;
+        }
+        e -= r_st;
+        cost_item(K, X + e * n, f_out ? f_out + b0 + e : nullptr, Dt + e * n);
+      }
+    }
+    lds_barrier();  // the tile image is complete
+    if (K.ablate != 2) {
+      if (K.want_g) copy_out_ct<CT, NT>(g_out + b0 * m, Gt, valid * m, tid);
+      if (K.want_j) copy_out_ct<CT, NT>(jac_out + b0 * nnz, Jt, valid * nnz, tid);
+      if (K.want_grad) copy_out_ct<CT, NT>(grad_out + b0 * n, Dt, valid * n, tid);
+    }
+    lds_barrier();  // next x landed, tile image free
+    cur ^= 1;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1207,7 +1450,7 @@ static int32_t plan_tile(KParams& K, bool g, bool j, bool f, bool grad) {
   K.LR = K.N * SQ_L + 1;  // odd instance stride of the SQ scratch: conflict-free LDS banks
   const size_t per = sizeof(double) * (size_t)(K.n + (g ? K.m : 0) + (j ? K.nnz : 0) + (grad ? K.n : 0) +
                                                (sq ? K.LR : 0));
-  const size_t fixed = sizeof(double) * 72;  // index lists
+  const size_t fixed = sizeof(double) * 72 + sizeof(CTab);  // index lists + parameter table
   int T = 64, logT = 6;
   while (T > 8 && (size_t)T * per + fixed > tile_budget()) { T >>= 1; --logT; }
   // (T >= 8 is even, so every tile of every record array starts on a 16-byte boundary)
@@ -1224,6 +1467,38 @@ static int32_t plan_tile(KParams& K, bool g, bool j, bool f, bool grad) {
   return CPL_OK;
 }
 
+// Pipelined kernel layout: x double buffer, masses and tags (double buffered), outputs, SQ scratch
+static int32_t plan_pipe(KParams& K, bool g, bool j, bool f, bool grad) {
+  K.want_g = g; K.want_j = j; K.want_f = f; K.want_grad = grad;
+  const bool sq = K.env_kind == CPL_ENV_SUPERQUADRIC || K.env_kind == CPL_ENV_MIXED;
+  K.LR = K.N * SQ_L + 1;
+  const size_t per = sizeof(double) * (size_t)(2 * K.n + 3 + (g ? K.m : 0) + (j ? K.nnz : 0) + (grad ? K.n : 0) +
+                                               (sq ? K.LR : 0));
+  const size_t fixed = sizeof(double) * (72 + 8) + sizeof(CTab);
+  int T = 64, logT = 6;
+  while (T > 8 && (size_t)T * per + fixed > tile_budget()) { T >>= 1; --logT; }
+  if ((size_t)T * per + fixed > 160 * 1024) return fail(CPL_ERR_UNSUPPORTED, "problem too large for one LDS tile");
+  K.T = T; K.logT = logT;
+  K.cost_seg = (f || grad) ? K.N + 4 : -1;
+  K.S = K.N + 4 + ((f || grad) ? 1 : 0);
+  auto up2 = [](int v) { return (v + 1) & ~1; };
+  K.offX1 = up2(T * K.n);
+  K.offMB = K.offX1 + up2(T * K.n);
+  K.offTB = K.offMB + 2 * T;
+  K.offG = K.offTB + T;  // 2*T ints
+  K.offJ = K.offG + (g ? T * K.m : 0);
+  K.offD = K.offJ + (j ? T * K.nnz : 0);
+  K.offL = K.offD + (grad ? T * K.n : 0);
+  K.offI = up2(K.offL + (sq ? T * K.LR : 0));
+  return CPL_OK;
+}
+
+struct PipeLaunch {
+  const void* fn;
+  size_t lds;
+  int blocks_per_cu;
+};
+
 static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
                            const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
                            hipStream_t stream) {
@@ -1238,7 +1513,30 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
   if (!d_g && !d_jac && !d_f && !d_grad) return CPL_OK;
   KParams K;
   fill_params(d, K, d_x);
-  if (use_rowstage()) {
+  if (g_variant == 2 && K.x_aligned16) {
+    st = plan_pipe(K, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr);
+    if (st) return st;
+    K.ablate = g_ablate;
+    const size_t lds = sizeof(double) * (size_t)(K.offI + 72);
+    using KernT = void (*)(const KParams, int64_t, const double*, const double*, const uint8_t*, double*, double*,
+                           double*, double*);
+    static const KernT table[4][2] = {
+        {cpl_eval_pipe_kernel<CPL_ENV_NONE, 3, false>, cpl_eval_pipe_kernel<CPL_ENV_NONE, 3, true>},
+        {cpl_eval_pipe_kernel<CPL_ENV_GROUND, 3, false>, cpl_eval_pipe_kernel<CPL_ENV_GROUND, 3, true>},
+        {cpl_eval_pipe_kernel<CPL_ENV_SUPERQUADRIC, 3, false>, cpl_eval_pipe_kernel<CPL_ENV_SUPERQUADRIC, 3, true>},
+        {cpl_eval_pipe_kernel<CPL_ENV_MIXED, 3, false>, cpl_eval_pipe_kernel<CPL_ENV_MIXED, 3, true>}};
+    const KernT kern = table[K.env_kind][g_nt ? 1 : 0];
+    int dev = 0, cus = 256, per_cu = 1;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), 256, lds) !=
+            hipSuccess || per_cu < 1)
+      per_cu = 1;
+    const int64_t ntiles = (batch + K.T - 1) / K.T;
+    const int64_t want = (int64_t)cus * per_cu;
+    const unsigned grid = (unsigned)(ntiles < want ? ntiles : want);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, stream, K, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f,
+                       d_grad);
+  } else if (use_rowstage()) {
     const size_t lds = eval_lds_bytes(K.n);
     if (lds > 160 * 1024) return fail(CPL_ERR_UNSUPPORTED, "problem too large for one LDS tile");
     const unsigned grid = (unsigned)((batch + TILE - 1) / TILE);
@@ -1287,7 +1585,7 @@ int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_t
                        int32_t ablate) {
   if (ablate < 0 || ablate > 2) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
   g_ablate = ablate;
-  if (kernel_variant < 0 || kernel_variant > 1) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown kernel variant");
+  if (kernel_variant < 0 || kernel_variant > 2) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown kernel variant");
   if (tile_lds_kb < 8 || tile_lds_kb > 160) return fail(CPL_ERR_INVALID_ARGUMENT, "tile LDS budget out of [8, 160] KiB");
   if (wg_threads != 128 && wg_threads != 256) return fail(CPL_ERR_INVALID_ARGUMENT, "workgroup size must be 128 or 256");
   g_variant = kernel_variant;

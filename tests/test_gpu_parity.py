@@ -137,7 +137,8 @@ def test_residual_norms_match_host():
     assert abs(rn[1] - (viol ** 2).sum()) <= 1e-9 * (viol ** 2).sum()
 
 
-@pytest.mark.parametrize("variant,lds_kb,wg,nt", [(1, 64, 256, 0), (0, 16, 128, 1), (0, 160, 256, 0), (0, 8, 128, 0)])
+@pytest.mark.parametrize("variant,lds_kb,wg,nt", [(1, 64, 256, 0), (0, 16, 128, 1), (0, 160, 256, 0), (0, 8, 128, 0),
+                                                  (2, 32, 256, 1), (2, 64, 256, 0), (2, 8, 256, 1)])
 @pytest.mark.parametrize("env,N", [("ground", 4), ("superquadric", 8), ("mixed", 16), ("none", 3)])
 def test_parity_kernel_variants(variant, lds_kb, wg, nt, env, N):
     """Every kernel variant / tile size gives the same results (tile sizes 8..64, odd records)."""
@@ -147,6 +148,23 @@ def test_parity_kernel_variants(variant, lds_kb, wg, nt, env, N):
     prob = make_problem(N, env)
     x, mass, tag = generate(N, env, 333, 77 + N)
     _abi.check(_abi.lib.cpl_set_tuning(variant, lds_kb, wg, nt, 0))
+    try:
+        got, ref = _run(prob, x, mass, tag)
+    finally:
+        _abi.check(_abi.lib.cpl_set_tuning(0, 32, 256, 1, 0))
+    _check(prob, env, x, got, ref, tag)
+
+
+@pytest.mark.parametrize("env,N,B", [("ground", 4, 100003), ("superquadric", 8, 40001), ("mixed", 16, 20011)])
+def test_parity_pipelined_many_tiles(env, N, B):
+    """The persistent pipelined kernel (variant 2) walks many tiles per workgroup through its double
+    buffer; a batch far above the resident grid exercises every buffer hand-off and the odd tail."""
+    from centroidalplanner_amd import _abi
+    from centroidalplanner_amd.workload import generate, make_problem
+
+    prob = make_problem(N, env)
+    x, mass, tag = generate(N, env, B, 991 + N)
+    _abi.check(_abi.lib.cpl_set_tuning(2, 32, 256, 1, 0))
     try:
         got, ref = _run(prob, x, mass, tag)
     finally:
