@@ -12,7 +12,7 @@ Default workload = BASELINE.json configs[1]: 4-contact Ground env, batch 65,536 
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 Rank 0 prints one JSON line.  Fields beyond the driver contract:
-  roofline      dominant kernel (cpl_eval_kernel): algorithmic bytes per launch / mean launch
+  roofline      dominant kernel (cpl_eval_*): algorithmic bytes per launch / mean launch
                 duration from HIP events on the launch stream; traffic = HBM bytes per launch from
                 rocprofv3 PMC passes (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE)
   cpu_baseline  the oracle (CPU restatement, "port") on the host cores, bounded sample
@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "NLP eval_g+eval_jac_g throughput (rows/sec) at batch*contacts; HBM GB/s vs peak"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
-KERNEL_NAME = "cpl_eval"  # matches cpl_eval_tile_kernel (default) and cpl_eval_kernel (row-staged)
+KERNEL_NAME = "cpl_eval"  # matches cpl_eval_pipe_kernel (none/Ground), cpl_eval_tile_kernel, cpl_eval_kernel
 
 
 def algorithmic_bytes(N, env, outputs=("g", "jac"), with_mass=True):
@@ -127,29 +127,26 @@ def collect_pmc(args, timeout=240):
 # CPU baseline: the oracle (CPU restatement of the reference path) on the host cores
 # ------------------------------------------------------------------------------------------
 def cpu_baseline(cfg, seconds):
+    """The oracle on the host cores: a fixed sample of the workload evaluated `reps` times so that
+    the timed CPU work lasts about `seconds` (10-30 s), threads = the box's CPU share."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     from centroidalplanner_amd.workload import config_inputs
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
-    B = 2048
-    while True:  # calibrate on a sample long enough to amortise thread start-up
-        prob, x, mass, tag = config_inputs(cfg, B)
-        t = pyoracle.time_eval_batch(prob.desc(), x, mass, tag, outputs=("g", "jac"), nthreads=threads, reps=1)
-        if t > 0.25 or B >= 1 << 20:
-            break
-        B *= 4
-    per_inst = t / x.shape[0]
-    B = int(min(max(seconds / max(per_inst, 1e-9), 2048), 4_000_000))
+    B = min(cfg.batch, 262144)
     prob, x, mass, tag = config_inputs(cfg, B)
-    t = pyoracle.time_eval_batch(prob.desc(), x, mass, tag, outputs=("g", "jac"), nthreads=threads, reps=1)
-    _, m = algorithmic_bytes(cfg.n_contacts, cfg.env)
+    t1 = pyoracle.time_eval_batch(prob.desc(), x, mass, tag, outputs=("g", "jac"), nthreads=threads, reps=1)
+    reps = max(1, int(round(seconds / max(t1, 1e-6))))
+    t = pyoracle.time_eval_batch(prob.desc(), x, mass, tag, outputs=("g", "jac"), nthreads=threads, reps=reps)
+    _, m = algorithmic_bytes(cfg.n_contacts, cfg.env)  # t: seconds per pass
     return {
         "value": B * m / t,
         "unit": "rows/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{B} instances of '{cfg.name}' (g+jac, IFOPT-order assembly) in {t:.2f} s on {threads} threads",
+        "sample": f"{B} instances of '{cfg.name}' x {reps} passes (g+jac, IFOPT-order assembly) in {t * reps:.1f} s "
+                  f"on {threads} threads",
         "instances_per_s": B / t,
     }
 
@@ -202,7 +199,7 @@ def main():
     mt = torch.tensor(mass, device=dev)
     tt = None if tag is None else torch.tensor(tag, device=dev)
     del x, mass, tag
-    out = prob.eval_batch(xt, mt, tt, outputs=("g", "jac"))
+    out = prob.eval_batch(xt, mt, tt, outputs=("g", "jac", "norms"))
     stream = torch.cuda.current_stream(dev)
     K, W = args.steps, args.warmup
     norms = [torch.zeros(2, dtype=torch.float64, device=dev) for _ in range(max(K, 1))]
@@ -211,10 +208,10 @@ def main():
     import ctypes
 
     def step(i):
-        prob.eval_batch(xt, mt, tt, outputs=("g", "jac"), out=out, stream=stream)
+        # one fused launch: values + CSR Jacobian values + the shard's residual norms
         nb = norms[i % len(norms)]
-        _abi.check(_abi.lib.cpl_residual_norms(ctypes.byref(prob.desc()), batch, out["g"].data_ptr(), nb.data_ptr(),
-                                               stream.cuda_stream))
+        out["norms"] = nb
+        prob.eval_batch(xt, mt, tt, outputs=("g", "jac", "norms"), out=out, stream=stream)
         if world > 1:
             from centroidalplanner_amd.distributed import all_gather_norms
 
@@ -255,7 +252,8 @@ def main():
         return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
     _abi.check(_abi.lib.cpl_time_eval_batch(ctypes.byref(prob.desc()), batch, p(xt), p(mt), p(tt), p(out["g"]), p(out["jac"]),
-                                            None, None, ctypes.c_void_p(stream.cuda_stream), reps, ctypes.byref(ms)))
+                                            None, None, p(norms[0]), ctypes.c_void_p(stream.cuda_stream), reps,
+                                            ctypes.byref(ms)))
     kernel_ms = ms.value
 
     bytes_inst, m = algorithmic_bytes(cfg.n_contacts, cfg.env)
@@ -274,9 +272,10 @@ def main():
         x1, m1, _ = generate(tcfg.n_contacts, tcfg.env, tb, 0xC910 + tcfg.config_id)
         x1t, m1t = torch.tensor(x1, device=dev), torch.tensor(m1, device=dev)
         del x1, m1
-        o1 = tp.eval_batch(x1t, m1t, outputs=("g", "jac"))
+        o1 = tp.eval_batch(x1t, m1t, outputs=("g", "jac", "norms"))
         _abi.check(_abi.lib.cpl_time_eval_batch(ctypes.byref(tp.desc()), tb, p(x1t), p(m1t), None, p(o1["g"]), p(o1["jac"]), None,
-                                                None, ctypes.c_void_p(stream.cuda_stream), 20, ctypes.byref(ms)))
+                                                None, p(o1["norms"]), ctypes.c_void_p(stream.cuda_stream), 20,
+                                                ctypes.byref(ms)))
         tbytes, tm = algorithmic_bytes(4, "ground")
         target = {
             "workload": tcfg.name,

@@ -93,10 +93,14 @@ SIGNATURES = {
     ),
     "cpl_set_tuning": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int32]),
     "cpl_residual_norms": (c_int32, [_DESC_P, c_int64, c_void_p, c_void_p, c_void_p]),
+    "cpl_eval_batch_norms": (
+        c_int32,
+        [_DESC_P, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
     "cpl_time_eval_batch": (
         c_int32,
         [_DESC_P, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-         c_int32, _DP],
+         c_void_p, c_int32, _DP],
     ),
 }
 

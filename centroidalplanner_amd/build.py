@@ -59,6 +59,32 @@ def build_extension(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+HOST_DIR = os.path.join(HERE, "host")
+HOST_LIB = os.path.join(HERE, "libcpl_host.so")
+HOST_SOURCES = ["cpl_problem.cpp", "cpl_planner.cpp", "cpl_broker.cpp"]
+HOST_HEADERS = ["Environment.hpp", "CplProblem.hpp", "CentroidalPlanner.hpp", "BatchBroker.hpp"]
+
+
+def build_host(force: bool = False, verbose: bool = False) -> str:
+    """The C++ host facade (cpl::CentroidalPlanner / CoMPlanner / CplProblem / CplTNLP / BatchBroker)
+    above the C-ABI: host code only, linked against libcpl_mi355x.so (rpath $ORIGIN)."""
+    deps = ([os.path.join(HOST_DIR, s) for s in HOST_SOURCES] +
+            [os.path.join(ROOT, "include", "cpl", h) for h in HOST_HEADERS] + [LIB])
+    if not force and not _stale(HOST_LIB, deps):
+        return HOST_LIB
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    cmd = ([_hipcc(), "-x", "c++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-D__HIP_PLATFORM_AMD__",
+            "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(rocm, "include")] +
+           [os.path.join(HOST_DIR, s) for s in HOST_SOURCES] +
+           ["-o", HOST_LIB + ".tmp", "-L" + HERE, "-lcpl_mi355x", "-L" + os.path.join(rocm, "lib"), "-lamdhip64",
+            "-Wl,-rpath,$ORIGIN"])
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True, cwd=HOST_DIR)
+    os.replace(HOST_LIB + ".tmp", HOST_LIB)
+    return HOST_LIB
+
+
 def build_oracle(verbose: bool = False) -> str:
     """Build the CPU restatement (test infrastructure) with its own Makefile."""
     odir = os.path.join(ROOT, "oracle")
@@ -71,3 +97,4 @@ def build_oracle(verbose: bool = False) -> str:
 
 if __name__ == "__main__":
     print(build_extension(force="--force" in sys.argv, verbose=True))
+    print(build_host(force="--force" in sys.argv, verbose=True))

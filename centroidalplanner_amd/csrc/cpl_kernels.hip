@@ -19,6 +19,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 
@@ -64,6 +65,8 @@ struct KParams {
   int32_t LR;            // doubles per instance in the SQ scratch (N*SQ_L + 1)
   int32_t offX1, offMB, offTB;  // pipelined kernel: second x buffer, masses, env tags
   int32_t want_g, want_j, want_f, want_grad;
+  int32_t want_norms;    // fused residual norms of g (cpl_eval_batch_norms)
+  int32_t contact_rows;  // constraint rows per contact: 6 (environment) or 2
   int32_t ablate;        // measurement-only ablation (cpl_set_tuning), 0 in production
   int32_t sq_ladder;     // every P_a is an integer in [2, 64]: double-double power ladders
 };
@@ -72,10 +75,11 @@ static_assert(sizeof(KParams) < 4096, "kernel parameters must fit the kernarg se
 // Per-block LDS copy of the parameter tables the work items index with a lane-varying contact or
 // axis index.  A kernarg read with a divergent index is a vector memory load, and its vmcnt wait
 // would also drain the wave's in-flight output stores; an LDS read waits on lgkmcnt only.
+constexpr int CPL_MAX_ROWS = 6 + 6 * CPL_MAX_CONTACTS;
 struct CTab {
   int32_t map_order[CPL_MAX_CONTACTS];
   double F_thr[CPL_MAX_CONTACTS];
-  double C[3], R[3], P[3], Pm1[3], P2[3], P2m2[3], P2m3[3], EJ[3], Ka[3], Kb[3], Rm2[3], Rp2[3], Psq[3];
+  uint8_t cone[CPL_MAX_ROWS];  // row r of g is a FrictionCone row (bounds (-inf, 0]) — residual norms
 };
 __shared__ CTab s_ct;
 
@@ -85,12 +89,94 @@ __device__ __forceinline__ void load_ctab(const KParams& K) {
   if (t < CPL_MAX_CONTACTS) {
     s_ct.map_order[t] = K.map_order[t];
     s_ct.F_thr[t] = K.F_thr[t];
-  } else if (t < CPL_MAX_CONTACTS + 3) {
-    const int a = t - CPL_MAX_CONTACTS;
-    s_ct.C[a] = K.C[a]; s_ct.R[a] = K.R[a]; s_ct.P[a] = K.P[a];
-    s_ct.Pm1[a] = K.Pm1[a]; s_ct.P2[a] = K.P2[a]; s_ct.P2m2[a] = K.P2m2[a]; s_ct.P2m3[a] = K.P2m3[a];
-    s_ct.EJ[a] = K.EJ[a]; s_ct.Ka[a] = K.Ka[a]; s_ct.Kb[a] = K.Kb[a];
-    s_ct.Rm2[a] = K.Rm2[a]; s_ct.Rp2[a] = K.Rp2[a]; s_ct.Psq[a] = K.Psq[a];
+  }
+  for (int r = t; r < K.m; r += blockDim.x)
+    s_ct.cone[r] = r >= 6 && ((r - 6) % K.contact_rows) >= K.contact_rows - 2;
+}
+
+// ---- residual norms of g against its bounds: max violation and sum of squared violations.
+// Equality rows (statics, environment, normal) have bounds [0, 0]; cone rows (-1e20, 0]
+// (src/Constraints/*.cpp GetBounds).  NaN counts as an infinite violation.
+__device__ __forceinline__ double row_violation(double g, bool cone) {
+  if (g != g) return INFINITY;
+  if (cone) return g > 0.0 ? g : 0.0;  // [-1e20, 0]: lower bound never active at finite g
+  return fabs(g);
+}
+
+struct NormAcc {
+  double vmax = 0.0, vsum = 0.0;
+  int r = 0, rstep = 0;  // row of this thread's next element, row advance per stride
+  __device__ void init(int tid, int nthreads, int m) {
+    r = tid % m;
+    rstep = nthreads % m;
+  }
+  // the g records of one tile (count = rows * instances, contiguous) from LDS
+  __device__ __forceinline__ void add_tile(const double* __restrict__ Gt, int count, int tid, int nthreads, int m) {
+    int rr = r;
+    for (int e = tid; e < count; e += nthreads) {
+      const double v = row_violation(Gt[e], s_ct.cone[rr]);
+      vmax = v > vmax ? v : vmax;
+      vsum += v * v;
+      rr += rstep;
+      if (rr >= m) rr -= m;
+    }
+  }
+};
+
+// Block reduction of every thread's NormAcc, one partial per block into ws, and a grid-wide
+// finish by the last block to arrive (fixed summation order -> deterministic for a fixed grid).
+// ws layout: [0] arrival counter (uint32, reset by the last block), partials from ws + 8.
+__device__ void finish_norms(const NormAcc& a, double* __restrict__ ws, double* __restrict__ out) {
+  __shared__ double red_max[16], red_sum[16];
+  __shared__ int is_last;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = (blockDim.x + 63) >> 6;
+  double vmax = a.vmax, vsum = a.vsum;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double om = __shfl_xor(vmax, o);
+    const double os = __shfl_xor(vsum, o);
+    vmax = om > vmax ? om : vmax;
+    vsum += os;
+  }
+  if (lane == 0) { red_max[wave] = vmax; red_sum[wave] = vsum; }
+  __syncthreads();
+  double* part = ws + 8;
+  unsigned* counter = reinterpret_cast<unsigned*>(ws);
+  if (tid == 0) {
+    double bm = 0.0, bs = 0.0;
+    for (int w = 0; w < nw; ++w) { bm = red_max[w] > bm ? red_max[w] : bm; bs += red_sum[w]; }
+    part[2 * blockIdx.x] = bm;
+    part[2 * blockIdx.x + 1] = bs;
+    __threadfence();
+    is_last = atomicAdd(counter, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!is_last) return;
+  __threadfence();
+  vmax = 0.0;
+  vsum = 0.0;
+  for (unsigned b = tid; b < gridDim.x; b += blockDim.x) {
+    const double pm = __builtin_nontemporal_load(&part[2 * b]);
+    const double ps = __builtin_nontemporal_load(&part[2 * b + 1]);
+    vmax = pm > vmax ? pm : vmax;
+    vsum += ps;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double om = __shfl_xor(vmax, o);
+    const double os = __shfl_xor(vsum, o);
+    vmax = om > vmax ? om : vmax;
+    vsum += os;
+  }
+  __syncthreads();
+  if (lane == 0) { red_max[wave] = vmax; red_sum[wave] = vsum; }
+  __syncthreads();
+  if (tid == 0) {
+    double bm = 0.0, bs = 0.0;
+    for (int w = 0; w < nw; ++w) { bm = red_max[w] > bm ? red_max[w] : bm; bs += red_sum[w]; }
+    out[0] = bm;
+    out[1] = bs;
+    *counter = 0u;  // ready for the next launch on this stream
   }
 }
 
@@ -283,7 +369,7 @@ struct AxisPowers {
 };
 __device__ __forceinline__ void axis_powers(const KParams& K, int a, double d, AxisPowers& o) {
   if (K.sq_ladder) {
-    const dd B = dd_ipow(d, (unsigned)s_ct.P[a] - 2u);
+    const dd B = dd_ipow(d, (unsigned)K.P[a] - 2u);
     const dd A = dd_mul_d(B, d);
     const dd Q = dd_mul_d(A, d);
     const double q2 = dd_sqr(Q).hi;
@@ -296,11 +382,11 @@ __device__ __forceinline__ void axis_powers(const KParams& K, int a, double d, A
       return;
     }
   }
-  o.pm1 = cpow(d, s_ct.Pm1[a]);
-  o.pP = cpow(d, s_ct.P[a]);
-  o.p2Pm3 = cpow(d, s_ct.P2m3[a]);
-  o.p2Pm2 = cpow(d, s_ct.P2m2[a]);
-  o.p2P = cpow(d, s_ct.P2[a]);
+  o.pm1 = cpow(d, K.Pm1[a]);
+  o.pP = cpow(d, K.P[a]);
+  o.p2Pm3 = cpow(d, K.P2m3[a]);
+  o.p2Pm2 = cpow(d, K.P2m2[a]);
+  o.p2P = cpow(d, K.P2[a]);
 }
 
 __device__ __forceinline__ void superquadric_contact(const KParams& K, double p0, double p1, double p2,
@@ -857,16 +943,16 @@ __device__ __forceinline__ void sq_axis_item(const KParams& K, const double* __r
                                              double* __restrict__ Lc) {
   const int i = s_ct.map_order[k];
   const double pa = xr[6 + 9 * i + a];
-  const double d = -s_ct.C[a] + pa;
+  const double d = -K.C[a] + pa;
   double* o = Lc + a * L_AXIS;
   // src/Superquadric.cpp:45  pow((p-C)/R, P)
-  const double u = (pa - s_ct.C[a]) / s_ct.R[a];
+  const double u = (pa - K.C[a]) / K.R[a];
   double w;
   if (K.sq_ladder && fabs(u) >= DD_TINY && fabs(u) <= 0x1p+40) {
-    w = dd_ipow(u, (unsigned)s_ct.P[a]).hi;
-    if (!(fabs(w) >= DD_TINY && fabs(w) <= DD_HUGE)) w = cpow(u, s_ct.P[a]);
+    w = dd_ipow(u, (unsigned)K.P[a]).hi;
+    if (!(fabs(w) >= DD_TINY && fabs(w) <= DD_HUGE)) w = cpow(u, K.P[a]);
   } else {
-    w = cpow(u, s_ct.P[a]);
+    w = cpow(u, K.P[a]);
   }
   o[L_WENV] = w;
   if (K.want_j) {
@@ -877,10 +963,10 @@ __device__ __forceinline__ void sq_axis_item(const KParams& K, const double* __r
     o[L_P2PM3] = ap.p2Pm3;
     o[L_P2PM2] = ap.p2Pm2;
     o[L_P2P] = ap.p2P;
-    const double t = s_ct.C[a] - pa;
+    const double t = K.C[a] - pa;
     o[L_INV] = 1.0 / (t * t);
   } else {
-    o[L_PM1] = cpow(d, s_ct.Pm1[a]);  // src/Superquadric.cpp:54-56 (normal value only)
+    o[L_PM1] = cpow(d, K.Pm1[a]);  // src/Superquadric.cpp:54-56 (normal value only)
   }
 }
 
@@ -955,25 +1041,25 @@ __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __re
   const double p_b = q[3 + b], p_c = q[3 + c];
   double out[3];
   {  // diagonal (a, a)
-    double lead = s_ct.Ka[a];
+    double lead = K.Ka[a];
 #pragma unroll
     for (int kk = 0; kk < 3; ++kk) {
       lead = lead * (kk == a ? La[L_PP] : K.Rm2[kk]);
       lead = lead * Lc[kk * L_AXIS + L_INV];
     }
-    lead = lead * s_ct.Pm1[a];
+    lead = lead * K.Pm1[a];
     lead = lead * 1.0;
-    const double Tb = ((s_ct.Rm2[b] * Lb[L_INV]) * s_ct.Psq[b]) * Lb[L_P2P];
-    const double Tc = ((s_ct.Rm2[c] * Lcc[L_INV]) * s_ct.Psq[c]) * Lcc[L_P2P];
-    const double Dg = (s_ct.Kb[a] * La[L_P2P]) * La[L_INV];
+    const double Tb = ((K.Rm2[b] * Lb[L_INV]) * K.Psq[b]) * Lb[L_P2P];
+    const double Tc = ((K.Rm2[c] * Lcc[L_INV]) * K.Psq[c]) * Lcc[L_P2P];
+    const double Dg = (K.Kb[a] * La[L_P2P]) * La[L_INV];
     const double S = (Tb + Tc) + Dg;
     const double p2Pb = Lb[L_P2P], p2Pc = Lcc[L_P2P];
-    const double E = (((((((s_ct.C[b] * s_ct.C[b]) * s_ct.Psq[c]) * p2Pc) * s_ct.Rp2[b] +
-                         (((s_ct.C[c] * s_ct.C[c]) * s_ct.Psq[b]) * p2Pb) * s_ct.Rp2[c]) +
-                        (((p_b * p_b) * s_ct.Psq[c]) * p2Pc) * s_ct.Rp2[b]) +
-                       (((p_c * p_c) * s_ct.Psq[b]) * p2Pb) * s_ct.Rp2[c]) -
-                      ((((s_ct.C[b] * p_b) * s_ct.Psq[c]) * p2Pc) * s_ct.Rp2[b]) * 2.0) -
-                     ((((s_ct.C[c] * p_c) * s_ct.Psq[b]) * p2Pb) * s_ct.Rp2[c]) * 2.0;
+    const double E = (((((((K.C[b] * K.C[b]) * K.Psq[c]) * p2Pc) * K.Rp2[b] +
+                         (((K.C[c] * K.C[c]) * K.Psq[b]) * p2Pb) * K.Rp2[c]) +
+                        (((p_b * p_b) * K.Psq[c]) * p2Pc) * K.Rp2[b]) +
+                       (((p_c * p_c) * K.Psq[b]) * p2Pb) * K.Rp2[c]) -
+                      ((((K.C[b] * p_b) * K.Psq[c]) * p2Pc) * K.Rp2[b]) * 2.0) -
+                     ((((K.C[c] * p_c) * K.Psq[b]) * p2Pb) * K.Rp2[c]) * 2.0;
     out[a] = lead / pow_three_halves(S) * E;
   }
 #pragma unroll
@@ -981,7 +1067,7 @@ __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __re
     if (bb == a) continue;
     const int oo = 3 - a - bb;
     const double* Lbb = Lc + bb * L_AXIS;
-    double lead = s_ct.Ka[a];
+    double lead = K.Ka[a];
     if (a < bb) {  // src/Superquadric.cpp:109, 119, 163
       lead = lead * La[L_PM1];
       lead = lead * K.Psq[bb];
@@ -995,7 +1081,7 @@ __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __re
     }
     lead = lead * K.Rm2[bb];
     lead = lead * 1.0;
-    const double S = (s_ct.Kb[oo] * Lc[oo * L_AXIS + L_P2PM2] + s_ct.Kb[a] * La[L_P2PM2]) +
+    const double S = (K.Kb[oo] * Lc[oo * L_AXIS + L_P2PM2] + K.Kb[a] * La[L_P2PM2]) +
                      (K.Psq[bb] * Lbb[L_P2PM2]) * K.Rm2[bb];
     out[bb] = lead / pow_three_halves(S) * (-1.0 / 2.0);
   }
@@ -1011,7 +1097,9 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
                                                             double* __restrict__ g_out,
                                                             double* __restrict__ jac_out,
                                                             double* __restrict__ f_out,
-                                                            double* __restrict__ grad_out) {
+                                                            double* __restrict__ grad_out,
+                                                            double* __restrict__ norms_out,
+                                                            double* __restrict__ norms_ws) {
   extern __shared__ __align__(16) double smem[];
   load_ctab(K);
   __syncthreads();
@@ -1097,10 +1185,17 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
     }
   }
   __syncthreads();
-  if (K.ablate == 2) return;
-  if (K.want_g) copy_out<WG, NT>(g_out + b0 * m, Gt, valid * m, tid);
-  if (K.want_j) copy_out<WG, NT>(jac_out + b0 * nnz, Jt, valid * nnz, tid);
-  if (K.want_grad) copy_out<WG, NT>(grad_out + b0 * n, Dt, valid * n, tid);
+  if (K.ablate != 2) {
+    if (K.want_g) copy_out<WG, NT>(g_out + b0 * m, Gt, valid * m, tid);
+    if (K.want_j) copy_out<WG, NT>(jac_out + b0 * nnz, Jt, valid * nnz, tid);
+    if (K.want_grad) copy_out<WG, NT>(grad_out + b0 * n, Dt, valid * n, tid);
+  }
+  if (K.want_norms) {
+    NormAcc acc;
+    acc.init(tid, WG, m);
+    acc.add_tile(Gt, valid * m, tid, WG, m);
+    finish_norms(acc, norms_ws, norms_out);
+  }
 }
 
 
@@ -1161,7 +1256,9 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
                                                                         double* __restrict__ g_out,
                                                                         double* __restrict__ jac_out,
                                                                         double* __restrict__ f_out,
-                                                                        double* __restrict__ grad_out) {
+                                                                        double* __restrict__ grad_out,
+                                                                        double* __restrict__ norms_out,
+                                                                        double* __restrict__ norms_ws) {
   constexpr int CT = 64 * NCW;  // compute threads
   constexpr bool HAS_SQ = ENVK == CPL_ENV_SUPERQUADRIC || ENVK == CPL_ENV_MIXED;
   extern __shared__ __align__(16) double smem[];
@@ -1185,7 +1282,9 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
   int* lists = reinterpret_cast<int*>(smem + K.offI);
 
   int64_t t = blockIdx.x;
-  if (t >= ntiles) return;
+  if (t >= ntiles) return;  // (never: the host sizes the grid to at most ntiles)
+  NormAcc acc;
+  acc.init(tid, CT, m);
 
   // loader: stage tile `tt` into buffer `bi`; loads only (the drain comes later)
   double st_mass = 0.0, st_tail = 0.0;
@@ -1230,9 +1329,7 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
       lds_barrier();
       cur ^= 1;
     }
-    return;
-  }
-
+  } else {
   lds_barrier();
   int cur = 0;
   for (; t < ntiles; t += gridDim.x) {
@@ -1311,9 +1408,12 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
       if (K.want_j) copy_out_ct<CT, NT>(jac_out + b0 * nnz, Jt, valid * nnz, tid);
       if (K.want_grad) copy_out_ct<CT, NT>(grad_out + b0 * n, Dt, valid * n, tid);
     }
+    if (K.want_norms) acc.add_tile(Gt, valid * m, tid, CT, m);
     lds_barrier();  // next x landed, tile image free
     cur ^= 1;
   }
+  }  // compute role
+  if (K.want_norms) finish_norms(acc, norms_ws, norms_out);  // the loader contributes zeros
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1321,12 +1421,6 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
 // ------------------------------------------------------------------------------------------
 constexpr int RN_BLOCK = 256;
 constexpr int RN_GRID = 1024;
-
-__device__ __forceinline__ double row_violation(double g, bool cone) {
-  if (g != g) return INFINITY;
-  if (cone) return g > 0.0 ? g : 0.0;  // [-1e20, 0]: lower bound never active at finite g
-  return fabs(g);
-}
 
 __global__ __launch_bounds__(RN_BLOCK) void cpl_residual_partial(int64_t total, int m, int contact_rows,
                                                                  const double* __restrict__ g,
@@ -1395,6 +1489,8 @@ static void fill_params(const cpl_problem_desc* d, KParams& K, const double* d_x
   K.N = D.N; K.n = D.n; K.m = D.m; K.nnz = D.nnz;
   K.env_kind = d->env_kind;
   K.has_env = has_env(d->env_kind) ? 1 : 0;
+  K.contact_rows = D.contact_rows;
+  K.want_norms = 0;
   K.x_aligned16 = (reinterpret_cast<uintptr_t>(d_x) & 15) == 0 ? 1 : 0;
   for (int k = 0; k < d->n_contacts; ++k) K.map_order[k] = (int8_t)d->map_order[k];
   K.mass_default = d->mass;
@@ -1433,16 +1529,25 @@ static void fill_params(const cpl_problem_desc* d, KParams& K, const double* d_x
 
 static size_t eval_lds_bytes(int n) { return sizeof(double) * (size_t)(TILE * n + 2 * TILE * SROW); }
 
-// Tuning knobs (cpl_set_tuning): kernel variant and the LDS budget of one tile workgroup.
-// Default 64 KiB -> two workgroups (8 waves) per CU.
-static int g_variant = 0;          // 0 = tile-stationary (default), 1 = row-staged lane-per-instance
-static size_t g_tile_budget = 32 * 1024;
+// Tuning knobs (cpl_set_tuning): kernel variant and the LDS budget of one workgroup.
+// Variant 0 (auto, the default) takes the pipelined kernel for the HBM-bound environments (none,
+// Ground) and the tile-stationary kernel for the VALU-bound ones (Superquadric, mixed), where the
+// pipelined kernel's three compute waves per workgroup leave the FP64 pipes under-filled.
+enum { VAR_AUTO = 0, VAR_ROWSTAGE = 1, VAR_PIPE = 2, VAR_TILE = 3 };
+static int g_variant = VAR_AUTO;
+static size_t g_lds_budget = 0;    // 0 = per-kernel default (tile 32 KiB, pipelined 48 KiB)
 static int g_wg = 256;             // threads per tile workgroup (128 or 256)
 static int g_nt = 1;               // non-temporal output stores
 static int g_ablate = 0;           // measurement-only: 1 = skip the compute phase, 2 = skip the stores
 
-static size_t tile_budget() { return g_tile_budget; }
-static bool use_rowstage() { return g_variant == 1; }
+static size_t tile_budget() { return g_lds_budget ? g_lds_budget : 32 * 1024; }
+static size_t pipe_budget() { return g_lds_budget ? g_lds_budget : 48 * 1024; }
+static bool use_rowstage() { return g_variant == VAR_ROWSTAGE; }
+static bool use_pipe(const KParams& K) {
+  if (!K.x_aligned16) return false;  // the LDS-DMA loader copies 16-byte granules
+  if (g_variant == VAR_PIPE) return true;
+  return g_variant == VAR_AUTO && (K.env_kind == CPL_ENV_NONE || K.env_kind == CPL_ENV_GROUND);
+}
 
 static int32_t plan_tile(KParams& K, bool g, bool j, bool f, bool grad) {
   K.want_g = g; K.want_j = j; K.want_f = f; K.want_grad = grad;
@@ -1476,7 +1581,7 @@ static int32_t plan_pipe(KParams& K, bool g, bool j, bool f, bool grad) {
                                                (sq ? K.LR : 0));
   const size_t fixed = sizeof(double) * (72 + 8) + sizeof(CTab);
   int T = 64, logT = 6;
-  while (T > 8 && (size_t)T * per + fixed > tile_budget()) { T >>= 1; --logT; }
+  while (T > 8 && (size_t)T * per + fixed > pipe_budget()) { T >>= 1; --logT; }
   if ((size_t)T * per + fixed > 160 * 1024) return fail(CPL_ERR_UNSUPPORTED, "problem too large for one LDS tile");
   K.T = T; K.logT = logT;
   K.cost_seg = (f || grad) ? K.N + 4 : -1;
@@ -1499,13 +1604,51 @@ struct PipeLaunch {
   int blocks_per_cu;
 };
 
+// Workspace of the fused residual norms: arrival counter + one partial pair per workgroup, per
+// (device, stream) so that launches on different streams never share a counter.  Grown on demand
+// (hipFree synchronises the device, so a smaller buffer is never freed under a running kernel).
+struct NormWs {
+  double* ptr = nullptr;
+  size_t cap = 0;  // partial pairs
+};
+static std::mutex g_norm_ws_mutex;
+static std::map<std::pair<int, hipStream_t>, NormWs> g_norm_ws;
+
+static int32_t norm_workspace(hipStream_t stream, size_t blocks, double** out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+  std::lock_guard<std::mutex> lk(g_norm_ws_mutex);
+  NormWs& w = g_norm_ws[{dev, stream}];
+  if (w.cap < blocks) {
+    if (w.ptr) (void)hipFree(w.ptr);
+    w.ptr = nullptr;
+    w.cap = 0;
+    const size_t cap = blocks < 4096 ? 4096 : blocks;
+    e = hipMalloc(&w.ptr, sizeof(double) * (8 + 2 * cap));
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc norms workspace");
+    e = hipMemset(w.ptr, 0, sizeof(double) * 8);  // arrival counter
+    if (e != hipSuccess) return hip_fail(e, "hipMemset norms workspace");
+    w.cap = cap;
+  }
+  *out = w.ptr;
+  return CPL_OK;
+}
+
 static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
                            const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
-                           hipStream_t stream) {
+                           double* d_norms, hipStream_t stream) {
   int32_t st = validate_desc(d);
   if (st) return st;
   if (batch < 0) return fail(CPL_ERR_INVALID_ARGUMENT, "negative batch");
-  if (batch == 0) return CPL_OK;
+  if (d_norms && !d_g) return fail(CPL_ERR_INVALID_ARGUMENT, "residual norms need the g output");
+  if (batch == 0) {
+    if (d_norms) {
+      hipError_t e = hipMemsetAsync(d_norms, 0, 2 * sizeof(double), stream);
+      if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync norms");
+    }
+    return CPL_OK;
+  }
   if (!d_x) return fail(CPL_ERR_INVALID_ARGUMENT, "x is required");
   if (d->env_kind == CPL_ENV_MIXED && !d_env_tag)
     return fail(CPL_ERR_INVALID_ARGUMENT, "mixed environment batch needs a per-instance env tag array");
@@ -1513,13 +1656,15 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
   if (!d_g && !d_jac && !d_f && !d_grad) return CPL_OK;
   KParams K;
   fill_params(d, K, d_x);
-  if (g_variant == 2 && K.x_aligned16) {
+  K.want_norms = d_norms != nullptr;
+  double* ws = nullptr;
+  if (use_pipe(K)) {
     st = plan_pipe(K, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr);
     if (st) return st;
     K.ablate = g_ablate;
     const size_t lds = sizeof(double) * (size_t)(K.offI + 72);
     using KernT = void (*)(const KParams, int64_t, const double*, const double*, const uint8_t*, double*, double*,
-                           double*, double*);
+                           double*, double*, double*, double*);
     static const KernT table[4][2] = {
         {cpl_eval_pipe_kernel<CPL_ENV_NONE, 3, false>, cpl_eval_pipe_kernel<CPL_ENV_NONE, 3, true>},
         {cpl_eval_pipe_kernel<CPL_ENV_GROUND, 3, false>, cpl_eval_pipe_kernel<CPL_ENV_GROUND, 3, true>},
@@ -1534,22 +1679,28 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
     const int64_t ntiles = (batch + K.T - 1) / K.T;
     const int64_t want = (int64_t)cus * per_cu;
     const unsigned grid = (unsigned)(ntiles < want ? ntiles : want);
+    if (K.want_norms && (st = norm_workspace(stream, grid, &ws))) return st;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, stream, K, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f,
-                       d_grad);
+                       d_grad, d_norms, ws);
   } else if (use_rowstage()) {
     const size_t lds = eval_lds_bytes(K.n);
     if (lds > 160 * 1024) return fail(CPL_ERR_UNSUPPORTED, "problem too large for one LDS tile");
     const unsigned grid = (unsigned)((batch + TILE - 1) / TILE);
     hipLaunchKernelGGL(cpl_eval_kernel, dim3(grid), dim3(TILE), lds, stream, K, batch, d_x, d_mass, d_env_tag,
                        d_g, d_jac, d_f, d_grad);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "cpl_eval_kernel launch");
+    // the row-staged kernel has no fused epilogue: a separate pass over g
+    return d_norms ? cpl_residual_norms(d, batch, d_g, d_norms, stream) : CPL_OK;
   } else {
     st = plan_tile(K, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr);
     if (st) return st;
     K.ablate = g_ablate;
     const size_t lds = sizeof(double) * (size_t)(K.offI + 72);
     const unsigned grid = (unsigned)((batch + K.T - 1) / K.T);
+    if (K.want_norms && (st = norm_workspace(stream, grid, &ws))) return st;
     using KernT = void (*)(const KParams, int64_t, const double*, const double*, const uint8_t*, double*, double*,
-                           double*, double*);
+                           double*, double*, double*, double*);
 #define CPL_TILE_KERNELS(E) \
   {cpl_eval_tile_kernel<E, 128, false>, cpl_eval_tile_kernel<E, 128, true>, cpl_eval_tile_kernel<E, 256, false>, \
    cpl_eval_tile_kernel<E, 256, true>}
@@ -1558,7 +1709,7 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
 #undef CPL_TILE_KERNELS
     const KernT kern = table[K.env_kind][(g_wg == 256 ? 2 : 0) + (g_nt ? 1 : 0)];
     hipLaunchKernelGGL(kern, dim3(grid), dim3(g_wg), lds, stream, K, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f,
-                       d_grad);
+                       d_grad, d_norms, ws);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "cpl_eval_kernel launch");
@@ -1578,18 +1729,26 @@ extern "C" {
 int32_t cpl_eval_batch(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
                        const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
                        void* stream) {
-  return launch_eval(d, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f, d_grad, (hipStream_t)stream);
+  return launch_eval(d, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f, d_grad, nullptr, (hipStream_t)stream);
+}
+
+int32_t cpl_eval_batch_norms(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
+                             const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
+                             double* d_norms, void* stream) {
+  if (!d_norms) return fail(CPL_ERR_INVALID_ARGUMENT, "d_norms is required");
+  return launch_eval(d, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f, d_grad, d_norms, (hipStream_t)stream);
 }
 
 int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_threads, int32_t nt_stores,
                        int32_t ablate) {
   if (ablate < 0 || ablate > 2) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
   g_ablate = ablate;
-  if (kernel_variant < 0 || kernel_variant > 2) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown kernel variant");
-  if (tile_lds_kb < 8 || tile_lds_kb > 160) return fail(CPL_ERR_INVALID_ARGUMENT, "tile LDS budget out of [8, 160] KiB");
+  if (kernel_variant < VAR_AUTO || kernel_variant > VAR_TILE) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown kernel variant");
+  if (tile_lds_kb != 0 && (tile_lds_kb < 8 || tile_lds_kb > 160))
+    return fail(CPL_ERR_INVALID_ARGUMENT, "LDS budget out of [8, 160] KiB");
   if (wg_threads != 128 && wg_threads != 256) return fail(CPL_ERR_INVALID_ARGUMENT, "workgroup size must be 128 or 256");
   g_variant = kernel_variant;
-  g_tile_budget = (size_t)tile_lds_kb * 1024;
+  g_lds_budget = (size_t)tile_lds_kb * 1024;
   g_wg = wg_threads;
   g_nt = nt_stores ? 1 : 0;
   return CPL_OK;
@@ -1630,7 +1789,7 @@ int32_t cpl_residual_norms(const cpl_problem_desc* d, int64_t batch, const doubl
 
 int32_t cpl_time_eval_batch(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
                             const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
-                            void* stream, int32_t reps, double* ms_per_launch) {
+                            double* d_norms, void* stream, int32_t reps, double* ms_per_launch) {
   if (!ms_per_launch || reps < 1) return fail(CPL_ERR_INVALID_ARGUMENT, "bad timing arguments");
   hipStream_t s = (hipStream_t)stream;
   hipEvent_t e0, e1;
@@ -1641,7 +1800,7 @@ int32_t cpl_time_eval_batch(const cpl_problem_desc* d, int64_t batch, const doub
   int32_t st = CPL_OK;
   (void)hipEventRecord(e0, s);
   for (int32_t r = 0; r < reps && st == CPL_OK; ++r)
-    st = launch_eval(d, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f, d_grad, s);
+    st = launch_eval(d, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f, d_grad, d_norms, s);
   (void)hipEventRecord(e1, s);
   e = hipEventSynchronize(e1);
   if (st == CPL_OK && e != hipSuccess) st = hip_fail(e, "hipEventSynchronize");

@@ -352,13 +352,20 @@ class CplProblem:
         """Evaluate B instances on the GPU in one launch.
 
         x: torch.float64 CUDA tensor [B, n] (contiguous).  mass: [B] or None.  env_tag: uint8 [B]
-        (mixed environment only).  outputs: subset of {"g", "jac", "f", "grad"}.  out: optional
+        (mixed environment only).  outputs: subset of {"g", "jac", "f", "grad", "norms"}; "norms"
+        (with "g") fuses the per-batch residual norms [max violation, sum of squared violations]
+        into the same launch (cpl_eval_batch_norms).  out: optional
         dict of preallocated output tensors.  Returns the dict of output tensors; asynchronous on
         ``stream`` (default: torch's current stream).
         """
         import torch
 
         n, m, nnz = self._dims()
+        outputs = tuple(outputs)
+        want_norms = "norms" in outputs
+        if want_norms and "g" not in outputs:
+            raise InvalidArgument(_abi.ERR_INVALID_ARGUMENT, "'norms' needs the 'g' output")
+        outputs = tuple(k for k in outputs if k != "norms")
         if x.dtype != torch.float64 or not x.is_cuda or x.dim() != 2 or x.shape[1] != n or not x.is_contiguous():
             raise InvalidArgument(_abi.ERR_INVALID_ARGUMENT, f"x must be a contiguous float64 CUDA tensor [B, {n}]")
         B = x.shape[0]
@@ -382,6 +389,17 @@ class CplProblem:
         def p(t):
             return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
+        if want_norms:  # fused residual norms of g: one launch, no second pass over g
+            t = out.get("norms") if out else None
+            if t is None:
+                t = torch.empty(2, dtype=torch.float64, device=x.device)
+            elif tuple(t.shape) != (2,) or t.dtype != torch.float64:
+                raise InvalidArgument(_abi.ERR_INVALID_ARGUMENT, "output 'norms' must be float64 (2,)")
+            res["norms"] = t
+            check(lib.cpl_eval_batch_norms(ctypes.byref(self.desc()), B, p(x), p(mass), p(env_tag), p(res.get("g")),
+                                           p(res.get("jac")), p(res.get("f")), p(res.get("grad")), p(t),
+                                           ctypes.c_void_p(s.cuda_stream)))
+            return res
         check(lib.cpl_eval_batch(ctypes.byref(self.desc()), B, p(x), p(mass), p(env_tag), p(res.get("g")),
                                  p(res.get("jac")), p(res.get("f")), p(res.get("grad")),
                                  ctypes.c_void_p(s.cuda_stream)))

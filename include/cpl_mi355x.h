@@ -163,20 +163,34 @@ int32_t cpl_eval_batch(const cpl_problem_desc* d, int64_t batch, const double* d
 int32_t cpl_residual_norms(const cpl_problem_desc* d, int64_t batch, const double* d_g,
                            double* d_out, void* stream);
 
-/* Kernel timing helper for the bench: launches cpl_eval_batch `reps` times on `stream`
- * bracketed by HIP events recorded on that same stream and returns the mean milliseconds per
- * launch in *ms_per_launch (synchronises the stream). */
+/*
+ * cpl_eval_batch and cpl_residual_norms of the g it produces in ONE launch: the norms are
+ * reduced from the tile images in LDS (no second pass over g in HBM) and finished by the last
+ * workgroup to arrive (deterministic for a given device).  d_g is required; d_norms: device,
+ * 2 doubles, same meaning as cpl_residual_norms.  Launches on one stream are ordered; launches
+ * on different streams use separate workspaces.
+ */
+int32_t cpl_eval_batch_norms(const cpl_problem_desc* d, int64_t batch, const double* d_x,
+                             const double* d_mass, const uint8_t* d_env_tag, double* d_g,
+                             double* d_jac, double* d_f, double* d_grad, double* d_norms,
+                             void* stream);
+
+/* Kernel timing helper for the bench: launches cpl_eval_batch (cpl_eval_batch_norms when
+ * d_norms != NULL) `reps` times on `stream` bracketed by HIP events recorded on that same stream
+ * and returns the mean milliseconds per launch in *ms_per_launch (synchronises the stream). */
 int32_t cpl_time_eval_batch(const cpl_problem_desc* d, int64_t batch, const double* d_x,
                             const double* d_mass, const uint8_t* d_env_tag, double* d_g,
-                            double* d_jac, double* d_f, double* d_grad, void* stream,
-                            int32_t reps, double* ms_per_launch);
+                            double* d_jac, double* d_f, double* d_grad, double* d_norms,
+                            void* stream, int32_t reps, double* ms_per_launch);
 
-/* Tuning knobs (process-wide, for A/B measurements): kernel_variant 0 = tile-stationary
- * (default), 1 = row-staged lane-per-instance; tile_lds_kb = LDS budget of one tile workgroup
- * (8..160 KiB, default 32); wg_threads = 128 or 256 (default 256); nt_stores = non-temporal
- * output stores (default 1); ablate = measurement-only ablation of the tile kernel (0 = off,
- * 1 = skip the compute phase, 2 = skip the output stores: results are then garbage).
- * Not thread-safe against concurrent launches. */
+/* Tuning knobs (process-wide, for A/B measurements): kernel_variant 0 = auto (default: the
+ * pipelined kernel for none/Ground, the tile-stationary kernel for Superquadric/mixed),
+ * 1 = row-staged lane-per-instance, 2 = pipelined (persistent, warp-specialized), 3 =
+ * tile-stationary; tile_lds_kb = LDS budget of one workgroup (8..160 KiB; 0 = per-kernel
+ * default: 32 tile, 48 pipelined); wg_threads = 128 or 256 for the tile kernel (default 256);
+ * nt_stores = non-temporal output stores (default 1); ablate = measurement-only ablation
+ * (0 = off, 1 = skip the compute phase, 2 = skip the output stores: results are then garbage).
+ * Every variant computes bit-identical results.  Not thread-safe against concurrent launches. */
 int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_threads, int32_t nt_stores,
                        int32_t ablate);
 

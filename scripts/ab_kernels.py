@@ -23,8 +23,9 @@ ap.add_argument("--config", default="ground4")
 ap.add_argument("--batch", type=int, default=0)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=20)
-ap.add_argument("--variants", default="0:32:256:0,0:16:128:0,0:24:128:0,0:32:128:0,0:32:256:1,0:16:128:1,0:48:256:0")
+ap.add_argument("--variants", default="0:0:256:1,3:32:256:1,2:48:256:1")
 ap.add_argument("--outputs", default="g,jac")
+ap.add_argument("--norms", action="store_true", help="fused residual norms (cpl_eval_batch_norms)")
 args = ap.parse_args()
 
 cfg = CONFIGS[args.config]
@@ -36,6 +37,7 @@ tt = None if tag is None else torch.tensor(tag, device=dev)
 outs = tuple(args.outputs.split(","))
 out = prob.eval_batch(xt, mt, tt, outputs=outs)
 stream = torch.cuda.current_stream()
+norms = torch.zeros(2, dtype=torch.float64, device=xt.device) if args.norms else None
 variants = [tuple(int(v) for v in s.split(":")) for s in args.variants.split(",")]
 times = {v: [] for v in variants}
 
@@ -49,7 +51,7 @@ for _ in range(args.rounds):
         _abi.check(_abi.lib.cpl_set_tuning(v[0], v[1], v[2], v[3], v[4] if len(v) > 4 else 0))
         ms = ctypes.c_double()
         _abi.check(_abi.lib.cpl_time_eval_batch(ctypes.byref(prob.desc()), B, p(xt), p(mt), p(tt), p(out.get("g")),
-                                                p(out.get("jac")), p(out.get("f")), p(out.get("grad")),
+                                                p(out.get("jac")), p(out.get("f")), p(out.get("grad")), p(norms),
                                                 ctypes.c_void_p(stream.cuda_stream), args.reps, ctypes.byref(ms)))
         times[v].append(ms.value)
 bpi, m = algorithmic_bytes(cfg.n_contacts, cfg.env, outs)

@@ -9,14 +9,15 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 
 def _ensure_built():
-    lib = os.path.join(ROOT, "centroidalplanner_amd", "libcpl_mi355x.so")
-    if not os.path.exists(lib):
-        import importlib.util
+    import importlib.util
 
-        spec = importlib.util.spec_from_file_location("_cpl_build", os.path.join(ROOT, "centroidalplanner_amd", "build.py"))
-        mod = importlib.util.module_from_spec(spec)
-        spec.loader.exec_module(mod)
+    spec = importlib.util.spec_from_file_location("_cpl_build", os.path.join(ROOT, "centroidalplanner_amd", "build.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    if not os.path.exists(mod.LIB):
         mod.build_extension()
+    if not os.path.exists(mod.HOST_LIB):
+        mod.build_host()
 
 
 _ensure_built()

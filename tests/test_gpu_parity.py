@@ -137,8 +137,8 @@ def test_residual_norms_match_host():
     assert abs(rn[1] - (viol ** 2).sum()) <= 1e-9 * (viol ** 2).sum()
 
 
-@pytest.mark.parametrize("variant,lds_kb,wg,nt", [(1, 64, 256, 0), (0, 16, 128, 1), (0, 160, 256, 0), (0, 8, 128, 0),
-                                                  (2, 32, 256, 1), (2, 64, 256, 0), (2, 8, 256, 1)])
+@pytest.mark.parametrize("variant,lds_kb,wg,nt", [(1, 64, 256, 0), (3, 16, 128, 1), (3, 160, 256, 0), (3, 8, 128, 0),
+                                                  (2, 32, 256, 1), (2, 64, 256, 0), (2, 8, 256, 1), (0, 0, 256, 1)])
 @pytest.mark.parametrize("env,N", [("ground", 4), ("superquadric", 8), ("mixed", 16), ("none", 3)])
 def test_parity_kernel_variants(variant, lds_kb, wg, nt, env, N):
     """Every kernel variant / tile size gives the same results (tile sizes 8..64, odd records)."""
@@ -151,7 +151,7 @@ def test_parity_kernel_variants(variant, lds_kb, wg, nt, env, N):
     try:
         got, ref = _run(prob, x, mass, tag)
     finally:
-        _abi.check(_abi.lib.cpl_set_tuning(0, 32, 256, 1, 0))
+        _abi.check(_abi.lib.cpl_set_tuning(0, 0, 256, 1, 0))
     _check(prob, env, x, got, ref, tag)
 
 
@@ -168,5 +168,53 @@ def test_parity_pipelined_many_tiles(env, N, B):
     try:
         got, ref = _run(prob, x, mass, tag)
     finally:
-        _abi.check(_abi.lib.cpl_set_tuning(0, 32, 256, 1, 0))
+        _abi.check(_abi.lib.cpl_set_tuning(0, 0, 256, 1, 0))
     _check(prob, env, x, got, ref, tag)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("env,N,B", [("ground", 4, 70001), ("none", 4, 5000), ("superquadric", 8, 3001),
+                                     ("mixed", 16, 2003), ("ground", 4, 1)])
+def test_fused_residual_norms(variant, env, N, B):
+    """cpl_eval_batch_norms: the norms reduced inside the eval launch equal the host reduction of
+    the oracle's g; g / jac are unchanged; repeated launches give bit-identical norms."""
+    from centroidalplanner_amd import _abi
+    from centroidalplanner_amd.workload import generate, make_problem
+
+    prob = make_problem(N, env)
+    x, mass, tag = generate(N, env, B, 4242 + N)
+    dev = torch.device("cuda:0")
+    xt, mt = torch.tensor(x, device=dev), torch.tensor(mass, device=dev)
+    tt = None if tag is None else torch.tensor(tag, device=dev)
+    _abi.check(_abi.lib.cpl_set_tuning(variant, 0, 256, 1, 0))
+    try:
+        out = prob.eval_batch(xt, mt, tt, outputs=("g", "jac", "norms"))
+        n1 = out["norms"].clone()
+        out2 = prob.eval_batch(xt, mt, tt, outputs=("g", "jac", "norms"))
+        torch.cuda.synchronize()
+    finally:
+        _abi.check(_abi.lib.cpl_set_tuning(0, 0, 256, 1, 0))
+    assert torch.equal(n1, out2["norms"])
+    ref = pyoracle.eval_batch(prob.desc(), x, mass, tag, outputs=("g", "jac"))
+    got = {"g": out["g"].cpu().numpy(), "jac": out["jac"].cpu().numpy()}
+    _check(prob, env, x, got, ref, tag)
+    _, _, gl, gu = prob.get_bounds_info()
+    viol = np.maximum(np.maximum(gl - got["g"], got["g"] - gu), 0.0)
+    rn = n1.cpu().numpy()
+    assert rn[0] == viol.max()
+    assert abs(rn[1] - (viol ** 2).sum()) <= 1e-12 * (viol ** 2).sum()
+    sep = prob.residual_norms(out["g"]).cpu().numpy()
+    assert sep[0] == rn[0]
+
+
+def test_fused_residual_norms_empty_batch():
+    from centroidalplanner_amd import _abi
+    from centroidalplanner_amd.workload import make_problem
+
+    prob = make_problem(4, "ground")
+    dev = torch.device("cuda:0")
+    xt = torch.empty(0, prob.n, dtype=torch.float64, device=dev)
+    out = prob.eval_batch(xt, outputs=("g", "norms"), out={"norms": torch.full((2,), 7.0, dtype=torch.float64, device=dev)})
+    assert out["norms"].cpu().tolist() == [0.0, 0.0]
+    with pytest.raises(_abi.InvalidArgument):
+        prob.eval_batch(torch.zeros(3, prob.n, dtype=torch.float64, device=dev), outputs=("jac", "norms"))
