@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Benchmark of the hot path: batched IFOPT eval_g + eval_jac_g of CentroidalPlanner instances.
 
-One step = one pass of the hot path over one batch resident in HBM: the eval kernel (values +
-CSR Jacobian values of every instance) plus the per-shard residual norms; with N > 1 ranks the
-norms are all-gathered over RCCL (asynchronously, on the collective stream).  Instances shard
+One step = one pass of the hot path over one batch resident in HBM: the fused eval kernel (values
++ CSR Jacobian values of every instance + per-workgroup residual partials) and the one-workgroup
+finish of the per-shard residual norms, replayed as one HIP graph; with N > 1 ranks the norms are
+all-gathered over RCCL (asynchronously, on the collective stream).  Instances shard
 across ranks with no data-path exchange: per-rank batch is fixed -> weak scaling.
 
 Default workload = BASELINE.json configs[1]: 4-contact Ground env, batch 65,536 per GPU.
@@ -65,6 +66,7 @@ def parse():
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-target", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="launch each step from Python instead of a HIP graph")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--pmc-child", default="", help=argparse.SUPPRESS)
     return ap.parse_args()
@@ -200,25 +202,51 @@ def main():
     tt = None if tag is None else torch.tensor(tag, device=dev)
     del x, mass, tag
     out = prob.eval_batch(xt, mt, tt, outputs=("g", "jac", "norms"))
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)  # launch stream: graph capture and replay
     K, W = args.steps, args.warmup
-    norms = [torch.zeros(2, dtype=torch.float64, device=dev) for _ in range(max(K, 1))]
+    norms = [torch.zeros(2, dtype=torch.float64, device=dev) for _ in range(2)]  # double-buffered
     gathered = []
 
     import ctypes
 
-    def step(i):
-        # one fused launch: values + CSR Jacobian values + the shard's residual norms
-        nb = norms[i % len(norms)]
+    def launch(nb):
+        # one step's device work: the fused eval (values + CSR Jacobian values + per-workgroup
+        # residual partials) and the one-workgroup finish of the shard's norms
         out["norms"] = nb
-        prob.eval_batch(xt, mt, tt, outputs=("g", "jac", "norms"), out=out, stream=stream)
-        if world > 1:
-            from centroidalplanner_amd.distributed import all_gather_norms
+        prob.eval_batch(xt, mt, tt, outputs=("g", "jac", "norms"), out=out, stream=torch.cuda.current_stream(dev))
 
-            out_norms, work = all_gather_norms(nb, async_op=True)  # RCCL over xGMI, overlaps the next step
-            if i == K - 1:
-                gathered.append(out_norms)
-            return work
+    with torch.cuda.stream(stream):  # warm the launch path (per-stream workspaces) before capture
+        for nb in norms:
+            launch(nb)
+    torch.cuda.synchronize()
+    graphs = []
+    if not args.no_graph:  # the step's launches as one HIP graph per norms buffer
+        for nb in norms:
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr, stream=stream):
+                launch(nb)
+            graphs.append(gr)
+        torch.cuda.synchronize()
+    pending = [None, None]
+
+    def step(i):
+        j = i % 2
+        if pending[j] is not None:  # the all-gather still reading norms[j] (two steps ago)
+            pending[j].wait()
+            pending[j] = None
+        with torch.cuda.stream(stream):
+            if graphs:
+                graphs[j].replay()
+            else:
+                launch(norms[j])
+            if world > 1:
+                from centroidalplanner_amd.distributed import all_gather_norms
+
+                out_norms, work = all_gather_norms(norms[j], async_op=True)  # RCCL over xGMI, overlaps the next step
+                pending[j] = work
+                if i == K - 1:
+                    gathered.append(out_norms)
+                return work
         return None
 
     for i in range(W):
@@ -306,6 +334,7 @@ def main():
                 "batch_per_gpu": batch,
                 "outputs": "g + jac (IFOPT CSR values), per-shard residual norms",
                 "parallelism": f"instance-sharded x{world}" + (" + RCCL all-gather of residual norms" if world > 1 else ""),
+                "launch": "hip-graph" if graphs else "eager",
             },
             "instances_per_s": batch * world * K / dt,
             "roofline": {

@@ -123,12 +123,10 @@ struct NormAcc {
   }
 };
 
-// Block reduction of every thread's NormAcc, one partial per block into ws, and a grid-wide
-// finish by the last block to arrive (fixed summation order -> deterministic for a fixed grid).
-// ws layout: [0] arrival counter (uint32, reset by the last block), partials from ws + 8.
-__device__ void finish_norms(const NormAcc& a, double* __restrict__ ws, double* __restrict__ out) {
+// Block reduction of every thread's NormAcc into one partial pair per workgroup.
+// Result valid in thread 0.
+__device__ __forceinline__ void block_norms(const NormAcc& a, double& bm, double& bs) {
   __shared__ double red_max[16], red_sum[16];
-  __shared__ int is_last;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = (blockDim.x + 63) >> 6;
   double vmax = a.vmax, vsum = a.vsum;
 #pragma unroll
@@ -138,45 +136,31 @@ __device__ void finish_norms(const NormAcc& a, double* __restrict__ ws, double* 
     vmax = om > vmax ? om : vmax;
     vsum += os;
   }
+  __syncthreads();  // red_* may still be read by a previous call
   if (lane == 0) { red_max[wave] = vmax; red_sum[wave] = vsum; }
   __syncthreads();
-  double* part = ws + 8;
-  unsigned* counter = reinterpret_cast<unsigned*>(ws);
-  if (tid == 0) {
-    double bm = 0.0, bs = 0.0;
+  bm = 0.0;
+  bs = 0.0;
+  if (tid == 0)
     for (int w = 0; w < nw; ++w) { bm = red_max[w] > bm ? red_max[w] : bm; bs += red_sum[w]; }
+}
+
+// Workspace of the fused norms: NORM_HDR doubles of header (reserved), then one partial pair per
+// workgroup; the host finishes with cpl_residual_final right after the eval launch.  (A
+// single-launch grid finish — last-arrival atomics at agent scope — measured 4-5 us slower at
+// 65 536 x 4: its store-ack / atomic / reload round trips sit on the kernel's tail.)
+constexpr int NORM_HDR = 128;
+
+// LDS-only workgroup barrier: no vmcnt drain of in-flight global stores
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// partial pair per workgroup with plain stores (the kernel boundary is the coherence point)
+__device__ void partial_norms(const NormAcc& a, double* __restrict__ part) {
+  double bm, bs;
+  block_norms(a, bm, bs);
+  if (threadIdx.x == 0) {
     part[2 * blockIdx.x] = bm;
     part[2 * blockIdx.x + 1] = bs;
-    __threadfence();
-    is_last = atomicAdd(counter, 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!is_last) return;
-  __threadfence();
-  vmax = 0.0;
-  vsum = 0.0;
-  for (unsigned b = tid; b < gridDim.x; b += blockDim.x) {
-    const double pm = __builtin_nontemporal_load(&part[2 * b]);
-    const double ps = __builtin_nontemporal_load(&part[2 * b + 1]);
-    vmax = pm > vmax ? pm : vmax;
-    vsum += ps;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const double om = __shfl_xor(vmax, o);
-    const double os = __shfl_xor(vsum, o);
-    vmax = om > vmax ? om : vmax;
-    vsum += os;
-  }
-  __syncthreads();
-  if (lane == 0) { red_max[wave] = vmax; red_sum[wave] = vsum; }
-  __syncthreads();
-  if (tid == 0) {
-    double bm = 0.0, bs = 0.0;
-    for (int w = 0; w < nw; ++w) { bm = red_max[w] > bm ? red_max[w] : bm; bs += red_sum[w]; }
-    out[0] = bm;
-    out[1] = bs;
-    *counter = 0u;  // ready for the next launch on this stream
   }
 }
 
@@ -722,8 +706,8 @@ __global__ __launch_bounds__(TILE) void cpl_eval_kernel(const KParams K, int64_t
 //     128-byte lines (T*record is a multiple of 16 doubles), so every HBM line of g / jac is
 //     written exactly once and whole.
 // ------------------------------------------------------------------------------------------
-constexpr int SEG_CONTACT0 = 0;  // segments [0, N): contacts in map order
-// then N: statics values + rows 0-2, N+1..N+3: torque rows 3..5, N+4: cost (optional)
+// Segments: [0, N) contacts in map order, then N: statics values + rows 0-2, N+1..N+3: torque
+// rows 3..5, N+4: cost (optional).
 
 template <int WG>
 __device__ __forceinline__ void copy_in(double* __restrict__ dst, const double* __restrict__ src, int count,
@@ -1098,7 +1082,6 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
                                                             double* __restrict__ jac_out,
                                                             double* __restrict__ f_out,
                                                             double* __restrict__ grad_out,
-                                                            double* __restrict__ norms_out,
                                                             double* __restrict__ norms_ws) {
   extern __shared__ __align__(16) double smem[];
   load_ctab(K);
@@ -1194,7 +1177,7 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
     NormAcc acc;
     acc.init(tid, WG, m);
     acc.add_tile(Gt, valid * m, tid, WG, m);
-    finish_norms(acc, norms_ws, norms_out);
+    partial_norms(acc, norms_ws + NORM_HDR);
   }
 }
 
@@ -1214,7 +1197,6 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // loader wave: DMA `count` doubles (16-B aligned source) into LDS; the odd last double is returned
 // through *tail for a plain store after the drain
@@ -1257,7 +1239,6 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
                                                                         double* __restrict__ jac_out,
                                                                         double* __restrict__ f_out,
                                                                         double* __restrict__ grad_out,
-                                                                        double* __restrict__ norms_out,
                                                                         double* __restrict__ norms_ws) {
   constexpr int CT = 64 * NCW;  // compute threads
   constexpr bool HAS_SQ = ENVK == CPL_ENV_SUPERQUADRIC || ENVK == CPL_ENV_MIXED;
@@ -1413,7 +1394,7 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
     cur ^= 1;
   }
   }  // compute role
-  if (K.want_norms) finish_norms(acc, norms_ws, norms_out);  // the loader contributes zeros
+  if (K.want_norms) partial_norms(acc, norms_ws + NORM_HDR);  // the loader contributes zeros
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1604,8 +1585,8 @@ struct PipeLaunch {
   int blocks_per_cu;
 };
 
-// Workspace of the fused residual norms: arrival counter + one partial pair per workgroup, per
-// (device, stream) so that launches on different streams never share a counter.  Grown on demand
+// Workspace of the fused residual norms: one partial pair per workgroup, per (device, stream) so
+// that launches on different streams never share it.  Grown on demand
 // (hipFree synchronises the device, so a smaller buffer is never freed under a running kernel).
 struct NormWs {
   double* ptr = nullptr;
@@ -1625,10 +1606,8 @@ static int32_t norm_workspace(hipStream_t stream, size_t blocks, double** out) {
     w.ptr = nullptr;
     w.cap = 0;
     const size_t cap = blocks < 4096 ? 4096 : blocks;
-    e = hipMalloc(&w.ptr, sizeof(double) * (8 + 2 * cap));
+    e = hipMalloc(&w.ptr, sizeof(double) * (NORM_HDR + 4 * cap));
     if (e != hipSuccess) return hip_fail(e, "hipMalloc norms workspace");
-    e = hipMemset(w.ptr, 0, sizeof(double) * 8);  // arrival counter
-    if (e != hipSuccess) return hip_fail(e, "hipMemset norms workspace");
     w.cap = cap;
   }
   *out = w.ptr;
@@ -1641,14 +1620,14 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
   int32_t st = validate_desc(d);
   if (st) return st;
   if (batch < 0) return fail(CPL_ERR_INVALID_ARGUMENT, "negative batch");
-  if (d_norms && !d_g) return fail(CPL_ERR_INVALID_ARGUMENT, "residual norms need the g output");
-  if (batch == 0) {
+  if (batch == 0) {  // (an empty g may arrive as a null pointer)
     if (d_norms) {
       hipError_t e = hipMemsetAsync(d_norms, 0, 2 * sizeof(double), stream);
       if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync norms");
     }
     return CPL_OK;
   }
+  if (d_norms && !d_g) return fail(CPL_ERR_INVALID_ARGUMENT, "residual norms need the g output");
   if (!d_x) return fail(CPL_ERR_INVALID_ARGUMENT, "x is required");
   if (d->env_kind == CPL_ENV_MIXED && !d_env_tag)
     return fail(CPL_ERR_INVALID_ARGUMENT, "mixed environment batch needs a per-instance env tag array");
@@ -1664,7 +1643,7 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
     K.ablate = g_ablate;
     const size_t lds = sizeof(double) * (size_t)(K.offI + 72);
     using KernT = void (*)(const KParams, int64_t, const double*, const double*, const uint8_t*, double*, double*,
-                           double*, double*, double*, double*);
+                           double*, double*, double*);
     static const KernT table[4][2] = {
         {cpl_eval_pipe_kernel<CPL_ENV_NONE, 3, false>, cpl_eval_pipe_kernel<CPL_ENV_NONE, 3, true>},
         {cpl_eval_pipe_kernel<CPL_ENV_GROUND, 3, false>, cpl_eval_pipe_kernel<CPL_ENV_GROUND, 3, true>},
@@ -1678,10 +1657,15 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
       per_cu = 1;
     const int64_t ntiles = (batch + K.T - 1) / K.T;
     const int64_t want = (int64_t)cus * per_cu;
-    const unsigned grid = (unsigned)(ntiles < want ? ntiles : want);
+    unsigned grid = (unsigned)(ntiles < want ? ntiles : want);
     if (K.want_norms && (st = norm_workspace(stream, grid, &ws))) return st;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, stream, K, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f,
-                       d_grad, d_norms, ws);
+                       d_grad, ws);
+    if (K.want_norms) {  // per-workgroup partials -> final pair
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return hip_fail(e, "cpl_eval_pipe_kernel launch");
+      hipLaunchKernelGGL(cpl_residual_final, dim3(1), dim3(RN_BLOCK), 0, stream, (int)grid, ws + NORM_HDR, d_norms);
+    }
   } else if (use_rowstage()) {
     const size_t lds = eval_lds_bytes(K.n);
     if (lds > 160 * 1024) return fail(CPL_ERR_UNSUPPORTED, "problem too large for one LDS tile");
@@ -1700,7 +1684,7 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
     const unsigned grid = (unsigned)((batch + K.T - 1) / K.T);
     if (K.want_norms && (st = norm_workspace(stream, grid, &ws))) return st;
     using KernT = void (*)(const KParams, int64_t, const double*, const double*, const uint8_t*, double*, double*,
-                           double*, double*, double*, double*);
+                           double*, double*, double*);
 #define CPL_TILE_KERNELS(E) \
   {cpl_eval_tile_kernel<E, 128, false>, cpl_eval_tile_kernel<E, 128, true>, cpl_eval_tile_kernel<E, 256, false>, \
    cpl_eval_tile_kernel<E, 256, true>}
@@ -1709,7 +1693,12 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
 #undef CPL_TILE_KERNELS
     const KernT kern = table[K.env_kind][(g_wg == 256 ? 2 : 0) + (g_nt ? 1 : 0)];
     hipLaunchKernelGGL(kern, dim3(grid), dim3(g_wg), lds, stream, K, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f,
-                       d_grad, d_norms, ws);
+                       d_grad, ws);
+    if (K.want_norms) {  // per-tile partials -> final pair
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return hip_fail(e, "cpl_eval_tile_kernel launch");
+      hipLaunchKernelGGL(cpl_residual_final, dim3(1), dim3(RN_BLOCK), 0, stream, (int)grid, ws + NORM_HDR, d_norms);
+    }
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "cpl_eval_kernel launch");

@@ -164,11 +164,11 @@ int32_t cpl_residual_norms(const cpl_problem_desc* d, int64_t batch, const doubl
                            double* d_out, void* stream);
 
 /*
- * cpl_eval_batch and cpl_residual_norms of the g it produces in ONE launch: the norms are
- * reduced from the tile images in LDS (no second pass over g in HBM) and finished by the last
- * workgroup to arrive (deterministic for a given device).  d_g is required; d_norms: device,
- * 2 doubles, same meaning as cpl_residual_norms.  Launches on one stream are ordered; launches
- * on different streams use separate workspaces.
+ * cpl_eval_batch and cpl_residual_norms of the g it produces, fused: each workgroup reduces the
+ * violations of its tiles from the tile images in LDS (no second pass over g in HBM) and a
+ * one-workgroup reduction launched right after on the same stream finishes the pair
+ * (deterministic for a given device).  d_g is required; d_norms: device, 2 doubles, same
+ * meaning as cpl_residual_norms.  Launches on different streams use separate workspaces.
  */
 int32_t cpl_eval_batch_norms(const cpl_problem_desc* d, int64_t batch, const double* d_x,
                              const double* d_mass, const uint8_t* d_env_tag, double* d_g,
