@@ -279,6 +279,7 @@ def main():
     def p(t):
         return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
+    # the step's launches (eval with fused norms + finish); events bracket each eval kernel alone
     _abi.check(_abi.lib.cpl_time_eval_batch(ctypes.byref(prob.desc()), batch, p(xt), p(mt), p(tt), p(out["g"]), p(out["jac"]),
                                             None, None, p(norms[0]), ctypes.c_void_p(stream.cuda_stream), reps,
                                             ctypes.byref(ms)))

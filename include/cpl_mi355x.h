@@ -175,9 +175,11 @@ int32_t cpl_eval_batch_norms(const cpl_problem_desc* d, int64_t batch, const dou
                              double* d_jac, double* d_f, double* d_grad, double* d_norms,
                              void* stream);
 
-/* Kernel timing helper for the bench: launches cpl_eval_batch (cpl_eval_batch_norms when
- * d_norms != NULL) `reps` times on `stream` bracketed by HIP events recorded on that same stream
- * and returns the mean milliseconds per launch in *ms_per_launch (synchronises the stream). */
+/* Kernel timing helper for the bench: launches the eval kernel of cpl_eval_batch (of
+ * cpl_eval_batch_norms, i.e. with the fused per-workgroup norms, when d_norms != NULL) `reps` times
+ * back to back on `stream` between two HIP events recorded on that same stream and returns the mean
+ * milliseconds per eval kernel in *ms_per_launch.  The one-workgroup norms finish is not part of the
+ * timed launches; one more complete launch afterwards leaves d_norms valid.  Synchronises the stream. */
 int32_t cpl_time_eval_batch(const cpl_problem_desc* d, int64_t batch, const double* d_x,
                             const double* d_mass, const uint8_t* d_env_tag, double* d_g,
                             double* d_jac, double* d_f, double* d_grad, double* d_norms,
