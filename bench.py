@@ -61,7 +61,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="ground4")
+    ap.add_argument("--config", default="ground4", help="ground4 | sq8 | mixed16 | ground4_1m | none4 | solve5")
     ap.add_argument("--batch", type=int, default=0, help="override per-GPU batch")
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
@@ -154,10 +154,93 @@ def cpu_baseline(cfg, seconds):
 
 
 # ------------------------------------------------------------------------------------------
+def solve_bench(args):
+    """BASELINE.json configs[4]: the full solve loop, 8,192 concurrent 4-contact Ground instances on
+    one GPU (centroidalplanner_amd/batch_ipm.py).  One step = one complete batched solve from the
+    starting points to termination of every instance; every callback of every iteration is one
+    cpl_eval_batch launch.  cpu_baseline = the same solver over the oracle's callbacks on the host
+    (CPU torch), a bounded sample of the instances."""
+    import torch
+
+    from centroidalplanner_amd.batch_ipm import KernelEvaluator, batch_ipm_solve
+    from centroidalplanner_amd.workload import SOLVE_CONFIG, solve_inputs, solve_problem
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    B = args.batch or SOLVE_CONFIG.batch
+    prob = solve_problem().GetCplProblem()
+    X0, mass = solve_inputs(prob, B, seed=0xC910 + 5 + 7919 * rank)
+    X0t, mt = torch.tensor(X0, device=dev), torch.tensor(mass, device=dev)
+    steps = max(1, min(args.steps, 5))
+    warm = 1 if args.warmup > 0 else 0
+    for _ in range(warm):
+        batch_ipm_solve(prob, X0t, mt, max_iter=300)
+    torch.cuda.synchronize()
+    print(f"[solve5] warmup done", file=sys.stderr, flush=True)
+    if world > 1:
+        dist.barrier()
+    ev = KernelEvaluator(prob)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r = batch_ipm_solve(prob, X0t, mt, evaluator=ev, max_iter=300)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tdt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tdt, op=dist.ReduceOp.MAX)
+        dt = float(tdt.item())
+    ok = int((r.status <= 1).sum().item())
+    its = r.iterations.double()
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            from test_batch_solve import OracleBatchEvaluator
+
+            Bc = 64
+            tc = time.perf_counter()
+            rc = batch_ipm_solve(prob, torch.tensor(X0[:Bc]), torch.tensor(mass[:Bc]),
+                                 evaluator=OracleBatchEvaluator(prob), max_iter=300)
+            tc = time.perf_counter() - tc
+            cpu = {"value": Bc / tc, "unit": "solves/s", "cores": 4, "kind": "port",
+                   "sample": f"{Bc} instances, the same batched solver over the oracle's callbacks on CPU torch "
+                             f"({rc.iterations_run} iterations, {tc:.1f} s)"}
+        except Exception as e:  # noqa: BLE001
+            cpu = {"error": str(e)}
+    if rank == 0:
+        print(json.dumps({
+            "metric": "concurrent CentroidalPlanner solves per second (full interior-point solve loop, GPU callbacks)",
+            "value": B * world * steps / dt, "unit": "solves/s", "n_gpus": world, "steps": steps, "warmup": warm,
+            "ms_per_step": dt / steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f64", "data": "synthetic (TestBasic ground scenario, per-instance mass U[80,150])",
+            "config": {"workload": SOLVE_CONFIG.name, "contacts": 4, "environment": "ground", "batch_per_gpu": B,
+                       "parallelism": f"instance-sharded x{world}", "hessian": "exact (batched central differences)"},
+            "solved": ok, "iterations_max": int(its.max().item()), "iterations_mean": float(its.mean().item()),
+            "lockstep_iterations": r.iterations_run, "eval_launches_per_solve": ev.launches // steps,
+            "instances_evaluated_per_solve": ev.instances // steps,
+            "cpu_baseline": cpu,
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     if args.pmc_child:
         pmc_child(args)
+        return
+    if args.config == "solve5":
+        solve_bench(args)
         return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

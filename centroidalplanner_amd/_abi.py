@@ -102,6 +102,12 @@ SIGNATURES = {
         [_DESC_P, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_void_p, c_int32, _DP],
     ),
+    "cpl_kkt_workspace_doubles": (c_int64, [c_int32, c_int32]),
+    "cpl_kkt_solve": (
+        c_int32,
+        [c_int32, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
 }
 
 

@@ -1,0 +1,413 @@
+// cpl_kkt.hip — batched primal-dual Newton step of the solve loop (centroidalplanner_amd/batch_ipm.py)
+// on gfx950: one workgroup per solver instance, every matrix of the step resident in LDS.
+//
+// Per instance (IPOPT's KKT system, Waechter & Biegler 2006, eq. 13 with the bound terms folded in):
+//     [ M    A^T ] [dw]   [r1]        M  = W + Sigma   (nw x nw, symmetric)
+//     [ A     0  ] [dy] = [r2]        A  = [J_free | -P] (m x nw)
+// solved by the null-space method on a Householder QR of A^T = Q [R; 0], Q = [Y Z]:
+//     R^T p_y = r2,   (Z^T (M + dW I) Z) p_z = Z^T (r1 - (M + dW I) Y p_y),   dw = Y p_y + Z p_z,
+//     R dy = Y^T (r1 - (M + dW I) dw),
+// with IPOPT's inertia correction inside the kernel: the KKT matrix has inertia (nw+, m-, 0) iff A
+// has full row rank and the reduced Hessian Z^T M Z is positive definite, so the Cholesky of the
+// reduced Hessian is the inertia test and dW follows IPOPT's schedule (first trial 1e-4, or
+// dW_last / 3; growth x100 without history, x8 with) until it succeeds; a rank-deficient A (|R_jj|
+// tiny) gets dC = 1e-8 mu^(1/4) |R|max on R's diagonal (IPOPT's jacobian_regularization_value).
+// One step of iterative refinement against the unregularised system follows when dC = 0.
+// The factors are kept in a per-instance workspace so second-order corrections re-solve with
+// another r2 without refactorising (mode 1).
+//
+// No library calls: the per-instance data-dependent retry loops run on the device, so the host
+// never synchronises on them.  Sizes: nw <= KKT_MAX_NW (=128), m <= nw.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <string>
+
+#include "cpl_status.hpp"
+
+namespace cpl {
+
+constexpr int KKT_THREADS = 256;
+constexpr int KKT_MAX_NW = 128;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Right-looking Cholesky of the n x n matrix H (row-major, stride n) in LDS, lower factor in place.
+// Returns true on success (every pivot positive and finite).  All threads call it.
+__device__ bool lds_cholesky(double* H, int n, int* flag) {
+  const int tid = threadIdx.x;
+  if (tid == 0) *flag = 0;
+  __syncthreads();
+  for (int k = 0; k < n; ++k) {
+    if (tid == 0) {
+      const double d = H[k * n + k];
+      if (!(d > 0.0) || !(d < INFINITY)) *flag = 1;
+      H[k * n + k] = sqrt(d > 0.0 ? d : 1.0);
+    }
+    __syncthreads();
+    if (*flag) return false;
+    const double lkk = H[k * n + k];
+    for (int i = k + 1 + tid; i < n; i += blockDim.x) H[i * n + k] /= lkk;
+    __syncthreads();
+    // trailing update of the lower triangle: (i, j), k < j <= i < n
+    const int t = n - k - 1;
+    const int pairs = t * (t + 1) / 2;
+    for (int p = tid; p < pairs; p += blockDim.x) {
+      // p -> (ii, jj) with 0 <= jj <= ii < t
+      int ii = (int)((sqrt(8.0 * p + 1.0) - 1.0) * 0.5);
+      while ((ii + 1) * (ii + 2) / 2 <= p) ++ii;
+      while (ii * (ii + 1) / 2 > p) --ii;
+      const int jj = p - ii * (ii + 1) / 2;
+      const int i = k + 1 + ii, j = k + 1 + jj;
+      H[i * n + j] -= H[i * n + k] * H[j * n + k];
+    }
+    __syncthreads();
+  }
+  return true;
+}
+
+struct KktShared {
+  int flag;
+  int rank_def;
+  double delta_w, delta_c;
+};
+
+// Solve with the factors in LDS: Q [nw][nw] (row-major: Q[r*nw + c]), QR array (row j = column j of
+// A^T after the reflections; R[i][j] = QR[j*nw + i] for i < j, R[j][j] = Rd[j]), L [nz][nz] the
+// Cholesky of the reduced Hessian, M [nw][nw] (plus delta_w on the diagonal, applied here).
+// Vectors in LDS: q1 [nw], q2 [m] -> dw [nw], dy [m].  tmp: >= 2*nw doubles.
+__device__ void kkt_solve_lds(int nw, int m, const double* Q, const double* QR, const double* Rd, const double* L,
+                              const double* M, double dW, const double* q1, const double* q2, double* dw,
+                              double* dy, double* tmp) {
+  const int tid = threadIdx.x;
+  const int nz = nw - m;
+  double* py = tmp;          // [m]
+  double* t = tmp + nw;      // [nw]
+  // R^T p_y = q2 (forward substitution; R^T is lower with (R^T)[i][k] = R[k][i] = QR[i*nw + k])
+  if (tid == 0) {
+    for (int i = 0; i < m; ++i) {
+      double s = q2[i];
+      for (int k = 0; k < i; ++k) s -= QR[i * nw + k] * py[k];
+      py[i] = s / Rd[i];
+    }
+  }
+  __syncthreads();
+  // dw <- Y p_y
+  for (int r = tid; r < nw; r += blockDim.x) {
+    double s = 0.0;
+    for (int k = 0; k < m; ++k) s += Q[r * nw + k] * py[k];
+    dw[r] = s;
+  }
+  __syncthreads();
+  // t = q1 - (M + dW I) Y p_y
+  for (int r = tid; r < nw; r += blockDim.x) {
+    double s = q1[r] - dW * dw[r];
+    for (int k = 0; k < nw; ++k) s -= M[r * nw + k] * dw[k];
+    t[r] = s;
+  }
+  __syncthreads();
+  if (nz > 0) {
+    // rz = Z^T t into tmp[m .. m+nz) (py still needed) -> p_z by the two triangular solves
+    double* rz = tmp + m;
+    for (int c = tid; c < nz; c += blockDim.x) {
+      double s = 0.0;
+      for (int r = 0; r < nw; ++r) s += Q[r * nw + m + c] * t[r];
+      rz[c] = s;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      for (int i = 0; i < nz; ++i) {
+        double s = rz[i];
+        for (int k = 0; k < i; ++k) s -= L[i * nz + k] * rz[k];
+        rz[i] = s / L[i * nz + i];
+      }
+      for (int i = nz - 1; i >= 0; --i) {
+        double s = rz[i];
+        for (int k = i + 1; k < nz; ++k) s -= L[k * nz + i] * rz[k];
+        rz[i] = s / L[i * nz + i];
+      }
+    }
+    __syncthreads();
+    // dw += Z p_z
+    for (int r = tid; r < nw; r += blockDim.x) {
+      double s = 0.0;
+      for (int c = 0; c < nz; ++c) s += Q[r * nw + m + c] * rz[c];
+      dw[r] += s;
+    }
+    __syncthreads();
+  }
+  // u = q1 - (M + dW I) dw  -> s = Y^T u -> R dy = s
+  for (int r = tid; r < nw; r += blockDim.x) {
+    double s = q1[r] - dW * dw[r];
+    for (int k = 0; k < nw; ++k) s -= M[r * nw + k] * dw[k];
+    t[r] = s;
+  }
+  __syncthreads();
+  for (int k = tid; k < m; k += blockDim.x) {
+    double s = 0.0;
+    for (int r = 0; r < nw; ++r) s += Q[r * nw + k] * t[r];
+    py[k] = s;  // (py no longer needed)
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int i = m - 1; i >= 0; --i) {
+      double s = py[i];
+      for (int k = i + 1; k < m; ++k) s -= QR[k * nw + i] * dy[k];
+      dy[i] = s / Rd[i];
+    }
+  }
+  __syncthreads();
+}
+
+// Workspace layout per instance (doubles): Q [nw*nw] | QR [m*nw] | Rd [m] | L [nz*nz] | scalars [4]
+__host__ __device__ inline int64_t kkt_ws_per(int nw, int m) {
+  const int nz = nw - m;
+  return (int64_t)nw * nw + (int64_t)m * nw + m + (int64_t)nz * nz + 4;
+}
+
+// LDS layout (doubles): Q | QR | Rd | L | M | q1 | q2 | dw | dy | e1 | e2 | tmp(2 nw)
+__host__ __device__ inline int kkt_lds_doubles(int nw, int m) {
+  const int nz = nw - m;
+  return nw * nw + m * nw + m + nz * nz + nw * nw + 5 * nw + 2 * m + 2 * nw;
+}
+
+__global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
+    int mode, int64_t batch, int nw, int m, const double* __restrict__ Mg, const double* __restrict__ Ag,
+    const double* __restrict__ r1g, const double* __restrict__ r2g, const double* __restrict__ mug,
+    const double* __restrict__ dw_last, const uint8_t* __restrict__ active, double* __restrict__ dwg,
+    double* __restrict__ dyg, double* __restrict__ dWg, double* __restrict__ dCg, int32_t* __restrict__ info,
+    double* __restrict__ ws) {
+  extern __shared__ __align__(16) double sm[];
+  __shared__ KktShared sh;
+  const int64_t b = blockIdx.x;
+  if (b >= batch) return;
+  const int tid = threadIdx.x;
+  const int nz = nw - m;
+  double* Q = sm;
+  double* QR = Q + nw * nw;
+  double* Rd = QR + m * nw;
+  double* L = Rd + m;
+  double* M = L + nz * nz;
+  double* q1 = M + nw * nw;
+  double* q2 = q1 + nw;
+  double* dw = q2 + m;
+  double* dy = dw + nw;
+  double* e1 = dy + m;
+  double* e2 = e1 + nw;
+  double* tmp = e2 + nw;  // 2 nw (+ slack)
+  const double* Mb = Mg + b * nw * nw;
+  const double* Ab = Ag + b * m * nw;
+  double* wsb = ws + b * kkt_ws_per(nw, m);
+
+  if (active && !active[b]) {
+    for (int i = tid; i < nw; i += blockDim.x) dwg[b * nw + i] = 0.0;
+    for (int i = tid; i < m; i += blockDim.x) dyg[b * m + i] = 0.0;
+    if (tid == 0 && mode == 0) { dWg[b] = 0.0; dCg[b] = 0.0; info[b] = 0; }
+    return;
+  }
+  for (int i = tid; i < nw * nw; i += blockDim.x) M[i] = Mb[i];
+  for (int i = tid; i < nw; i += blockDim.x) q1[i] = r1g[b * nw + i];
+  for (int i = tid; i < m; i += blockDim.x) q2[i] = r2g[b * m + i];
+
+  if (mode == 1) {  // re-solve with the kept factors
+    const int64_t per = kkt_ws_per(nw, m);
+    for (int64_t i = tid; i < per - 4; i += blockDim.x) sm[i] = wsb[i];
+    if (tid == 0) { sh.delta_w = wsb[per - 4]; sh.delta_c = wsb[per - 3]; }
+    __syncthreads();
+    kkt_solve_lds(nw, m, Q, QR, Rd, L, M, sh.delta_w, q1, q2, dw, dy, tmp);
+    for (int i = tid; i < nw; i += blockDim.x) dwg[b * nw + i] = dw[i];
+    for (int i = tid; i < m; i += blockDim.x) dyg[b * m + i] = dy[i];
+    return;
+  }
+
+  // ---- Householder QR of A^T: row j of QR = column j of A^T
+  for (int i = tid; i < m * nw; i += blockDim.x) QR[i] = Ab[i];
+  __syncthreads();
+  double* beta = tmp;  // [m]
+  const int lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
+  for (int j = 0; j < m; ++j) {
+    double* x = QR + j * nw;  // column j of A^T, rows j..nw-1 active
+    if (wave == 0) {
+      double sig = 0.0;
+      for (int i = j + 1 + lane; i < nw; i += 64) sig += x[i] * x[i];
+      sig = wave_sum(sig);
+      if (lane == 0) {
+        const double alpha = x[j];
+        if (sig == 0.0) {
+          beta[j] = 0.0;
+          Rd[j] = alpha;
+        } else {
+          const double nrm = sqrt(alpha * alpha + sig);
+          const double v0 = alpha <= 0.0 ? alpha - nrm : -sig / (alpha + nrm);
+          beta[j] = 2.0 * v0 * v0 / (sig + v0 * v0);
+          Rd[j] = nrm;
+          tmp[m + j] = v0;  // (scaled below)
+        }
+      }
+    }
+    __syncthreads();
+    if (beta[j] != 0.0) {
+      const double v0 = tmp[m + j];
+      for (int i = j + 1 + tid; i < nw; i += blockDim.x) x[i] /= v0;  // v (v_j = 1 implicit)
+      __syncthreads();
+      // apply H_j to the columns k > j: y <- y - beta v (v^T y), one wave per column
+      for (int k = j + 1 + wave; k < m; k += nwaves) {
+        double* y = QR + k * nw;
+        double s = 0.0;
+        for (int i = j + lane; i < nw; i += 64) s += (i == j ? 1.0 : x[i]) * y[i];
+        s = wave_sum(s) * beta[j];
+        for (int i = j + lane; i < nw; i += 64) y[i] -= s * (i == j ? 1.0 : x[i]);
+      }
+    }
+    __syncthreads();
+  }
+  // ---- Q = H_0 ... H_{m-1} I (backward accumulation), one thread per column
+  for (int i = tid; i < nw * nw; i += blockDim.x) Q[i] = (i / nw == i % nw) ? 1.0 : 0.0;
+  __syncthreads();
+  for (int j = m - 1; j >= 0; --j) {
+    const double bj = beta[j];
+    if (bj != 0.0) {
+      const double* v = QR + j * nw;
+      for (int c = tid; c < nw; c += blockDim.x) {
+        double s = Q[j * nw + c];
+        for (int r = j + 1; r < nw; ++r) s += v[r] * Q[r * nw + c];
+        s *= bj;
+        Q[j * nw + c] -= s;
+        for (int r = j + 1; r < nw; ++r) Q[r * nw + c] -= s * v[r];
+      }
+    }
+    __syncthreads();
+  }
+  // ---- rank deficiency: delta_c on R's diagonal
+  if (tid == 0) {
+    double rmax = 0.0;
+    for (int j = 0; j < m; ++j) rmax = fabs(Rd[j]) > rmax ? fabs(Rd[j]) : rmax;
+    const double dc = 1e-8 * pow(mug[b], 0.25) * (rmax > 0.0 ? rmax : 1.0);
+    int def = 0;
+    for (int j = 0; j < m; ++j)
+      if (!(fabs(Rd[j]) >= 1e-10 * rmax) || rmax == 0.0) {
+        Rd[j] = Rd[j] < 0.0 ? Rd[j] - dc : Rd[j] + dc;
+        def = 1;
+      }
+    sh.rank_def = def;
+    sh.delta_c = def ? dc : 0.0;
+  }
+  __syncthreads();
+  // ---- reduced Hessian Hr = Z^T M Z (into tmp area: MZ [nw][nz] staged in e1.. is too small ->
+  // compute entry-wise: Hr[a][c] = sum_r Z[r][a] (sum_k M[r][k] Z[k][c]))
+  // MZ is staged in the dw/dy/e1/e2/tmp region, which is free at this point (>= 4 nw + m doubles).
+  double* Hr0 = L;  // keep the unshifted reduced Hessian in the workspace slot of L first
+  if (nz > 0) {
+    double* MZ = ws + b * kkt_ws_per(nw, m);  // global scratch (the workspace; overwritten at the end)
+    for (int e = tid; e < nw * nz; e += blockDim.x) {
+      const int r = e / nz, c = e % nz;
+      double s = 0.0;
+      for (int k = 0; k < nw; ++k) s += M[r * nw + k] * Q[k * nw + m + c];
+      MZ[e] = s;
+    }
+    __syncthreads();
+    for (int e = tid; e < nz * nz; e += blockDim.x) {
+      const int a = e / nz, c = e % nz;
+      double s = 0.0;
+      for (int r = 0; r < nw; ++r) s += Q[r * nw + m + a] * MZ[r * nz + c];
+      Hr0[e] = s;
+    }
+    __syncthreads();
+    // symmetrise, keep a copy in dw.. region (nz*nz may exceed it: use the global scratch again)
+    double* Hsave = MZ;
+    for (int e = tid; e < nz * nz; e += blockDim.x) {
+      const int a = e / nz, c = e % nz;
+      Hsave[e] = 0.5 * (Hr0[a * nz + c] + Hr0[c * nz + a]);
+    }
+    __syncthreads();
+    // ---- inertia correction: Cholesky of Hr + delta_w I, IPOPT's delta_w schedule
+    const double last = dw_last ? dw_last[b] : 0.0;
+    double dW = 0.0;
+    int32_t inf = 0;
+    for (int attempt = 0; attempt < 64; ++attempt) {
+      for (int e = tid; e < nz * nz; e += blockDim.x) L[e] = Hsave[e] + ((e / nz == e % nz) ? dW : 0.0);
+      __syncthreads();
+      if (lds_cholesky(L, nz, &sh.flag)) break;
+      if (dW == 0.0) dW = last == 0.0 ? 1e-4 : fmax(1e-20, last / 3.0);
+      else dW *= last == 0.0 ? 100.0 : 8.0;
+      if (dW > 1e40) { inf = 1; break; }
+      __syncthreads();
+    }
+    if (tid == 0) sh.delta_w = dW;
+    if (tid == 0 && info) info[b] = inf;
+    __syncthreads();
+  } else {
+    if (tid == 0) { sh.delta_w = 0.0; if (info) info[b] = 0; }
+    __syncthreads();
+  }
+  const double dW = sh.delta_w;
+  // ---- solve, then one step of iterative refinement on the unregularised system
+  kkt_solve_lds(nw, m, Q, QR, Rd, L, M, dW, q1, q2, dw, dy, tmp);
+  if (!sh.rank_def) {
+    for (int r = tid; r < nw; r += blockDim.x) {
+      double s = q1[r] - dW * dw[r];
+      for (int k = 0; k < nw; ++k) s -= M[r * nw + k] * dw[k];
+      for (int k = 0; k < m; ++k) s -= Ab[k * nw + r] * dy[k];
+      e1[r] = s;
+    }
+    for (int k = tid; k < m; k += blockDim.x) {
+      double s = q2[k];
+      for (int r = 0; r < nw; ++r) s -= Ab[k * nw + r] * dw[r];
+      e2[k] = s;
+    }
+    __syncthreads();
+    // the correction reuses q1/q2 as outputs: (e1, e2) -> (q1, q2)
+    kkt_solve_lds(nw, m, Q, QR, Rd, L, M, dW, e1, e2, q1, q2, tmp);
+    for (int r = tid; r < nw; r += blockDim.x) dw[r] += q1[r];
+    for (int k = tid; k < m; k += blockDim.x) dy[k] += q2[k];
+    __syncthreads();
+  }
+  for (int i = tid; i < nw; i += blockDim.x) dwg[b * nw + i] = dw[i];
+  for (int i = tid; i < m; i += blockDim.x) dyg[b * m + i] = dy[i];
+  if (tid == 0) { dWg[b] = dW; dCg[b] = sh.delta_c; }
+  // keep the factors for mode 1 (the global scratch use above is finished: barrier first)
+  __syncthreads();
+  const int64_t per = kkt_ws_per(nw, m);
+  for (int64_t i = tid; i < per - 4; i += blockDim.x) wsb[i] = sm[i];
+  if (tid == 0) { wsb[per - 4] = dW; wsb[per - 3] = sh.delta_c; wsb[per - 2] = 0.0; wsb[per - 1] = 0.0; }
+}
+
+}  // namespace cpl
+
+using namespace cpl;
+
+extern "C" {
+
+int64_t cpl_kkt_workspace_doubles(int32_t nw, int32_t m) {
+  if (nw <= 0 || m < 0 || m > nw) return -1;
+  return kkt_ws_per(nw, m);
+}
+
+int32_t cpl_kkt_solve(int32_t mode, int64_t batch, int32_t nw, int32_t m, const double* d_M, const double* d_A,
+                      const double* d_r1, const double* d_r2, const double* d_mu, const double* d_delta_w_last,
+                      const uint8_t* d_active, double* d_dw, double* d_dy, double* d_delta_w, double* d_delta_c,
+                      int32_t* d_info, double* d_ws, void* stream) {
+  if (mode != 0 && mode != 1) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_solve: mode must be 0 or 1");
+  if (batch < 0 || nw <= 0 || m < 0 || m > nw || nw > KKT_MAX_NW)
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_solve: need 0 <= m <= nw <= 128");
+  if (batch == 0) return CPL_OK;
+  if (!d_M || (m > 0 && !d_A) || !d_r1 || (m > 0 && !d_r2) || !d_dw || (m > 0 && !d_dy) || !d_ws)
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_solve: missing buffer");
+  if (mode == 0 && (!d_mu || !d_delta_w || !d_delta_c || !d_info))
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_solve: factorisation needs mu, delta_w, delta_c, info");
+  if (batch > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_solve: batch too large");
+  const size_t lds = sizeof(double) * (size_t)(kkt_lds_doubles(nw, m) + 8);
+  if (lds > 160 * 1024) return fail(CPL_ERR_UNSUPPORTED, "cpl_kkt_solve: system too large for one LDS image");
+  hipLaunchKernelGGL(cpl_kkt_kernel, dim3((unsigned)batch), dim3(KKT_THREADS), lds, (hipStream_t)stream, (int)mode,
+                     batch, (int)nw, (int)m, d_M, d_A, d_r1, d_r2, d_mu, d_delta_w_last, d_active, d_dw, d_dy,
+                     d_delta_w, d_delta_c, d_info, d_ws);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_kkt_kernel launch: ") + hipGetErrorString(e));
+  return CPL_OK;
+}
+
+}  // extern "C"

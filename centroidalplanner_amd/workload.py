@@ -136,4 +136,53 @@ def config_inputs(cfg: Config, batch: Optional[int] = None, stress: bool = False
     return prob, x, mass, tag
 
 
-__all__ = ["Config", "CONFIGS", "make_problem", "generate", "config_inputs", "ENV_NONE", "ENV_MIXED"]
+# BASELINE.json configs[4]: the full solve loop, 4 contacts, 8,192 concurrent instances on one GPU
+SOLVE_CONFIG = Config("Full solve loop with GPU eval callbacks, 4-contact Ground, 8,192 concurrent instances",
+                      4, "ground", 8192, 5)
+
+
+def solve_problem(n_contacts: int = 4, force_weight: float = 1.0):
+    """The TestBasic ground scenario (tests/TestBasic.cpp:64-100: Ground z=0.1, mu=0.5, CoM weight 2,
+    contact positions boxed to [-0.3,0.3]^2 x [0,1], wrench (100,0,0,0,0,100)) as the shared
+    template of a batched solve.  force_weight: TestBasic sets 0 (forces then only constrained:
+    a degenerate problem); the batched workload keeps the reference default 1
+    (src/MinimizeCentroidalVariables.cpp:11-25)."""
+    from .planner import CentroidalPlanner
+
+    names = [f"contact{i + 1}" for i in range(n_contacts)]
+    env = Ground()
+    env.SetGroundZ(GROUND_Z)
+    env.SetMu(MU)
+    cpl = CentroidalPlanner(names, 100.0, env)
+    cpl.SetCoMWeight(2.0)
+    cpl.SetForceWeight(force_weight)
+    for c in names:
+        cpl.SetPosBounds(c, np.array([-0.3, -0.3, 0.0]), np.array([0.3, 0.3, 1.0]))
+    cpl.SetManipulationWrench(WRENCH)
+    return cpl
+
+
+def solve_inputs(prob, batch: int, seed: int = 0xC910 + 5):
+    """Per-instance robot masses U[80, 150] kg (feasible under the wrench: the friction needed for
+    the lateral force and the yaw torque stays inside mu * m g) and a non-degenerate start per
+    instance: CoM at its reference, F_i = (1, 1, m g / N), p_i on a circle of radius 0.2 at
+    z = 0.05, n_i = (0, 0, 1) — clipped into the variable bounds.  Host arrays (X0 [B, n], mass [B])."""
+    rng = np.random.default_rng(seed)
+    N = len(prob.contact_names)
+    mass = rng.uniform(80.0, 150.0, batch)
+    x0 = np.zeros(prob.n)
+    x0[0:3] = prob.GetCoMRef()
+    X0 = np.tile(x0, (batch, 1))
+    for i in range(N):
+        ang = 2.0 * np.pi * (i + 0.125) / N
+        X0[:, 3 + 9 * i] = 1.0
+        X0[:, 4 + 9 * i] = 1.0
+        X0[:, 5 + 9 * i] = mass * 9.81 / N
+        X0[:, 6 + 9 * i: 9 + 9 * i] = [0.2 * np.cos(ang), 0.2 * np.sin(ang), 0.05]
+        X0[:, 9 + 9 * i: 12 + 9 * i] = [0.0, 0.0, 1.0]
+    xl, xu, _, _ = prob.get_bounds_info()
+    return np.clip(X0, xl, xu), mass
+
+
+__all__ = ["Config", "CONFIGS", "SOLVE_CONFIG", "make_problem", "generate", "config_inputs", "solve_problem",
+           "solve_inputs", "ENV_NONE", "ENV_MIXED"]

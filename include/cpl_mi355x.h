@@ -196,6 +196,32 @@ int32_t cpl_time_eval_batch(const cpl_problem_desc* d, int64_t batch, const doub
 int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_threads, int32_t nt_stores,
                        int32_t ablate);
 
+/* ---- the solve loop's Newton step (device) ------------------------------------------- */
+/*
+ * Batched primal-dual Newton step of the interior-point solve loop (centroidalplanner_amd/
+ * batch_ipm.py; replaces, per instance, IPOPT's PDFullSpaceSolver / inertia-correcting
+ * factorisation behind src/CentroidalPlanner.cpp:29 [IPOPT-ext]):
+ *     [M  A^T] [dw]   [r1]
+ *     [A   0 ] [dy] = [r2]        M = W + Sigma (nw x nw), A (m x nw), instance-major row-major
+ * by the null-space method on a Householder QR of A^T, with IPOPT's inertia correction on the
+ * device (delta_w on M until the reduced Hessian Z^T M Z is positive definite: first trial 1e-4 or
+ * delta_w_last/3, growth x100 / x8; delta_c = 1e-8 mu^(1/4) |R|max on R's diagonal where A is
+ * rank-deficient) and one step of iterative refinement.  One workgroup per instance; all of the
+ * step's matrices in LDS.  nw <= 128, 0 <= m <= nw, and the LDS image must fit 160 KiB.
+ *   mode 0: factorise + solve; d_mu [batch] (barrier parameter), d_delta_w_last [batch] or NULL,
+ *           outputs d_delta_w, d_delta_c [batch], d_info [batch] (0 ok, 1 inertia not corrected)
+ *   mode 1: re-solve with the factors mode 0 left in d_ws (second-order corrections: same M, A,
+ *           r1 up to the caller, another r2)
+ *   d_active [batch] uint8 or NULL: inactive instances are skipped (dw = dy = 0)
+ *   d_ws: cpl_kkt_workspace_doubles(nw, m) doubles per instance (device)
+ * Asynchronous on `stream`.
+ */
+int64_t cpl_kkt_workspace_doubles(int32_t nw, int32_t m);
+int32_t cpl_kkt_solve(int32_t mode, int64_t batch, int32_t nw, int32_t m, const double* d_M, const double* d_A,
+                      const double* d_r1, const double* d_r2, const double* d_mu, const double* d_delta_w_last,
+                      const uint8_t* d_active, double* d_dw, double* d_dy, double* d_delta_w, double* d_delta_c,
+                      int32_t* d_info, double* d_ws, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,146 @@
+"""The batched solve loop (centroidalplanner_amd/batch_ipm.py, BASELINE.json configs[4]).
+
+CPU: the solver's host logic driven by the oracle's callbacks (test infrastructure), on a few
+instances of the TestBasic ground scenario (tests/TestBasic.cpp:64-135) with the reference's
+default force weight; every solution is certified independently:
+  * TestBasic's own assertions (force / torque balance with the manipulation wrench, contacts on
+    the ground, unit normals, friction cones, bounds);
+  * a first-order KKT certificate of the returned primal-dual pair through the oracle's callbacks
+    (stationarity, sign and complementarity of the cone multipliers);
+  * the objective is at least as good as an independent single-instance solve (SLSQP over the same
+    callbacks; the problem is nonconvex, so both are local optima).
+GPU: the same solve with the product callbacks (the HIP kernel through cpl_eval_batch) on a larger
+batch, checked with the same certificates and against the oracle-driven batched solve.
+"""
+import numpy as np
+import pytest
+
+import pyoracle
+from centroidalplanner_amd.batch_ipm import STATUS_ACCEPTABLE, batch_ipm_solve
+from centroidalplanner_amd.workload import MU, GROUND_Z, WRENCH, solve_inputs, solve_problem
+
+torch = pytest.importorskip("torch")
+
+
+class OracleBatchEvaluator:
+    """Batched callbacks through the CPU restatement, on CPU torch tensors."""
+
+    def __init__(self, problem):
+        self.problem = problem
+
+    def __call__(self, X, mass):
+        o = pyoracle.eval_batch(self.problem.desc(), X.cpu().numpy(), None if mass is None else mass.cpu().numpy(),
+                                None, outputs=("g", "jac", "f", "grad"), nthreads=4)
+        return {k: torch.as_tensor(v, device=X.device) for k, v in o.items()}
+
+
+def _certify(prob, x, y, mass, tol_kkt=1e-7):
+    """TestBasic.cpp:101-132 assertions + a KKT certificate through the oracle at x."""
+    n, m, _ = prob.get_nlp_info()
+    xl, xu, gl, gu = prob.get_bounds_info()
+    N = len(prob.contact_names)
+    c = x[0:3]
+    F_sum, T_sum = np.zeros(3), np.zeros(3)
+    for i in range(N):
+        F, p, nv = x[3 + 9 * i: 6 + 9 * i], x[6 + 9 * i: 9 + 9 * i], x[9 + 9 * i: 12 + 9 * i]
+        F_sum += F
+        T_sum += np.cross(p - c, F)
+        assert p[2] == pytest.approx(GROUND_Z, abs=1e-6)
+        assert np.linalg.norm(nv) == pytest.approx(1.0, abs=1e-6)
+        assert nv[2] == pytest.approx(1.0, abs=1e-6)
+        assert -F.dot(nv) <= 1e-9
+        assert np.linalg.norm(F - nv.dot(F) * nv) - MU * F.dot(nv) <= 1e-7
+    assert F_sum[0] == pytest.approx(WRENCH[0], abs=1e-6)
+    assert F_sum[1] == pytest.approx(WRENCH[1], abs=1e-6)
+    assert F_sum[2] == pytest.approx(mass * 9.81 + WRENCH[2], abs=1e-6)
+    np.testing.assert_allclose(T_sum, WRENCH[3:], atol=1e-5)
+    assert (x >= xl - 1e-9).all() and (x <= xu + 1e-9).all()
+    # first-order certificate of the returned primal-dual pair, through the oracle's callbacks:
+    # stationarity grad f + J^T y = 0 (bounds inactive), y >= 0 on the cone rows (g <= 0) and
+    # complementarity y_r g_r = 0 there
+    o = pyoracle.eval_batch(prob.desc(), x[None], np.array([mass]), None, outputs=("g", "jac", "f", "grad"))
+    iR, jC = prob.get_structure()
+    J = np.zeros((m, n))
+    J[iR, jC] = np.nan_to_num(o["jac"][0])
+    g = o["g"][0]
+    res = o["grad"][0] + J.T @ y
+    bound_act = (np.abs(x - xl) <= 1e-6) | (np.abs(x - xu) <= 1e-6)
+    res[bound_act] = 0.0
+    scale = max(1.0, np.abs(o["grad"][0]).max())
+    assert np.abs(res).max() <= tol_kkt * scale
+    ineq = gl != gu
+    ymax = max(1.0, np.abs(y).max())
+    assert (y[ineq] >= -1e-8 * ymax).all()
+    assert (np.abs(y[ineq] * g[ineq]) <= 1e-6 * ymax).all()
+    return float(o["f"][0])
+
+
+def _slsqp_objective(prob, x0, mass):
+    from centroidalplanner_amd.solver import solve
+
+    class E:
+        def eval_batch(self, X):
+            X = np.atleast_2d(X)
+            return pyoracle.eval_batch(prob.desc(), X, np.full(X.shape[0], mass), None,
+                                       outputs=("g", "jac", "f", "grad"), nthreads=1)
+
+    r = solve(prob, E(), x0=x0, tol=1e-12, max_iter=500)
+    o = E().eval_batch(r.x)
+    return float(o["f"][0])
+
+
+def test_batch_solve_oracle_cpu():
+    cpl = solve_problem()
+    prob = cpl.GetCplProblem()
+    X0, mass = solve_inputs(prob, 6, seed=11)
+    r = batch_ipm_solve(prob, torch.as_tensor(X0), torch.as_tensor(mass), evaluator=OracleBatchEvaluator(prob),
+                        max_iter=200)
+    assert bool((r.status <= STATUS_ACCEPTABLE).all()), r.status
+    assert r.iterations_run < 100
+    for b in range(X0.shape[0]):
+        x = r.x[b].numpy()
+        f = _certify(prob, x, r.y[b].numpy(), mass[b])
+        assert f == pytest.approx(float(r.objective[b]), rel=1e-12)
+        if b < 3:
+            # the problem is nonconvex (bilinear torque balance): both points are certified local
+            # optima; the batched interior-point solve must reach one at least as good
+            assert f <= _slsqp_objective(prob, X0[b], mass[b]) * (1.0 + 1e-7)
+
+
+def test_batch_solve_rejects_host_inputs_without_gpu_callbacks():
+    """The product evaluator is the HIP kernel: host tensors are refused, never evaluated on the CPU."""
+    from centroidalplanner_amd._abi import CplError
+
+    cpl = solve_problem()
+    prob = cpl.GetCplProblem()
+    X0, mass = solve_inputs(prob, 2)
+    with pytest.raises(CplError):
+        batch_ipm_solve(prob, torch.as_tensor(X0), torch.as_tensor(mass), max_iter=2)
+
+
+@pytest.mark.gpu
+def test_batch_solve_gpu_kernel_callbacks():
+    from centroidalplanner_amd.batch_ipm import KernelEvaluator
+
+    cpl = solve_problem()
+    prob = cpl.GetCplProblem()
+    B = 512
+    X0, mass = solve_inputs(prob, B, seed=5)
+    dev = torch.device("cuda:0")
+    ev = KernelEvaluator(prob)
+    r = batch_ipm_solve(prob, torch.as_tensor(X0, device=dev), torch.as_tensor(mass, device=dev), evaluator=ev,
+                        max_iter=200)
+    assert ev.launches == r.evaluations  # every callback of the batch went through the kernel
+    st = r.status.cpu().numpy()
+    assert (st <= STATUS_ACCEPTABLE).all()
+    X = r.x.cpu().numpy()
+    Y = r.y.cpu().numpy()
+    obj = r.objective.cpu().numpy()
+    # certify a sample; compare a smaller sample with the oracle-driven batched solve (same algorithm)
+    for b in range(0, B, 37):
+        f = _certify(prob, X[b], Y[b], mass[b])
+        assert f == pytest.approx(obj[b], rel=1e-12)
+    sub = np.arange(0, B, 64)
+    rc = batch_ipm_solve(prob, torch.as_tensor(X0[sub]), torch.as_tensor(mass[sub]),
+                         evaluator=OracleBatchEvaluator(prob), max_iter=200)
+    np.testing.assert_allclose(obj[sub], rc.objective.numpy(), rtol=1e-8)
