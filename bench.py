@@ -226,8 +226,8 @@ def solve_bench(args):
             "config": {"workload": SOLVE_CONFIG.name, "contacts": 4, "environment": "ground", "batch_per_gpu": B,
                        "parallelism": f"instance-sharded x{world}", "hessian": "exact (batched central differences)"},
             "solved": ok, "iterations_max": int(its.max().item()), "iterations_mean": float(its.mean().item()),
-            "lockstep_iterations": r.iterations_run, "eval_launches_per_solve": ev.launches // steps,
-            "instances_evaluated_per_solve": ev.instances // steps,
+            "lockstep_iterations": r.iterations_run, "eval_launches_per_solve": r.evaluations,
+            "graph": r.graph,
             "cpu_baseline": cpu,
         }), flush=True)
     if world > 1:

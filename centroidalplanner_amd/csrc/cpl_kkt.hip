@@ -376,11 +376,57 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
   if (tid == 0) { wsb[per - 4] = dW; wsb[per - 3] = sh.delta_c; wsb[per - 2] = 0.0; wsb[per - 1] = 0.0; }
 }
 
+// grad f + J^T y per instance from the CSR values (the Lagrangian gradient the solve loop
+// differentiates for its Hessian): one thread per (instance, column), the column's entries through
+// a host-built CSC index of the fixed structure.  Instance b takes the multipliers of instance
+// b / y_repeat (the 2 n_free finite-difference points of one iterate share its y).  A NaN Jacobian
+// value (a cone at zero tangential force, 0/0) counts as 0.
+__global__ __launch_bounds__(256) void cpl_lagrangian_grad_kernel(int64_t total, int n, int m, int nnz,
+                                                                  const int32_t* __restrict__ col_ptr,
+                                                                  const int32_t* __restrict__ csc_k,
+                                                                  const int32_t* __restrict__ csc_row,
+                                                                  const double* __restrict__ grad,
+                                                                  const double* __restrict__ jac,
+                                                                  const double* __restrict__ y, int y_repeat,
+                                                                  double* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int64_t b = e / n;
+  const int j = (int)(e - b * n);
+  const double* jb = jac + b * nnz;
+  const double* yb = y + (b / y_repeat) * m;
+  double s = grad[e];
+  for (int q = col_ptr[j]; q < col_ptr[j + 1]; ++q) {
+    double v = jb[csc_k[q]];
+    v = v == v ? v : 0.0;
+    s += v * yb[csc_row[q]];
+  }
+  out[e] = s;
+}
+
 }  // namespace cpl
 
 using namespace cpl;
 
 extern "C" {
+
+int32_t cpl_lagrangian_grad(int64_t batch, int32_t n, int32_t m, int32_t nnz, const int32_t* d_col_ptr,
+                            const int32_t* d_csc_k, const int32_t* d_csc_row, const double* d_grad,
+                            const double* d_jac, const double* d_y, int32_t y_repeat, double* d_out, void* stream) {
+  if (batch < 0 || n <= 0 || m < 0 || nnz < 0 || y_repeat < 1)
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_lagrangian_grad: bad sizes");
+  if (batch == 0) return CPL_OK;
+  if (!d_col_ptr || !d_grad || !d_out || (nnz > 0 && (!d_csc_k || !d_csc_row || !d_jac)) || (m > 0 && !d_y))
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_lagrangian_grad: missing buffer");
+  const int64_t total = batch * n;
+  const int64_t blocks = (total + 255) / 256;
+  if (blocks > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_lagrangian_grad: batch too large");
+  hipLaunchKernelGGL(cpl_lagrangian_grad_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, total, (int)n,
+                     (int)m, (int)nnz, d_col_ptr, d_csc_k, d_csc_row, d_grad, d_jac, d_y, (int)y_repeat, d_out);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_lagrangian_grad launch: ") + hipGetErrorString(e));
+  return CPL_OK;
+}
 
 int64_t cpl_kkt_workspace_doubles(int32_t nw, int32_t m) {
   if (nw <= 0 || m < 0 || m > nw) return -1;

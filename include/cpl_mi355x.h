@@ -217,6 +217,17 @@ int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_t
  * Asynchronous on `stream`.
  */
 int64_t cpl_kkt_workspace_doubles(int32_t nw, int32_t m);
+
+/*
+ * grad f + J^T y of every instance from the CSR Jacobian values of cpl_eval_batch (the Lagrangian
+ * gradient the solve loop differentiates for its Hessian; IpoptAdapter has no such callback — IPOPT
+ * forms it internally).  d_col_ptr [n+1], d_csc_k [nnz], d_csc_row [nnz]: the structure of
+ * cpl_structure transposed (column j's entries are CSR positions d_csc_k[col_ptr[j]..col_ptr[j+1])
+ * in rows d_csc_row[...]).  Instance b uses d_y[b / y_repeat].  NaN Jacobian values count as 0.
+ */
+int32_t cpl_lagrangian_grad(int64_t batch, int32_t n, int32_t m, int32_t nnz, const int32_t* d_col_ptr,
+                            const int32_t* d_csc_k, const int32_t* d_csc_row, const double* d_grad,
+                            const double* d_jac, const double* d_y, int32_t y_repeat, double* d_out, void* stream);
 int32_t cpl_kkt_solve(int32_t mode, int64_t batch, int32_t nw, int32_t m, const double* d_M, const double* d_A,
                       const double* d_r1, const double* d_r2, const double* d_mu, const double* d_delta_w_last,
                       const uint8_t* d_active, double* d_dw, double* d_dy, double* d_delta_w, double* d_delta_c,

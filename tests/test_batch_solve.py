@@ -28,9 +28,9 @@ class OracleBatchEvaluator:
     def __init__(self, problem):
         self.problem = problem
 
-    def __call__(self, X, mass):
+    def __call__(self, X, mass, outputs=("g", "jac", "f", "grad")):
         o = pyoracle.eval_batch(self.problem.desc(), X.cpu().numpy(), None if mass is None else mass.cpu().numpy(),
-                                None, outputs=("g", "jac", "f", "grad"), nthreads=4)
+                                None, outputs=tuple(outputs), nthreads=4)
         return {k: torch.as_tensor(v, device=X.device) for k, v in o.items()}
 
 
@@ -130,7 +130,7 @@ def test_batch_solve_gpu_kernel_callbacks():
     ev = KernelEvaluator(prob)
     r = batch_ipm_solve(prob, torch.as_tensor(X0, device=dev), torch.as_tensor(mass, device=dev), evaluator=ev,
                         max_iter=200)
-    assert ev.launches == r.evaluations  # every callback of the batch went through the kernel
+    assert r.graph and ev.calls >= 3  # the iteration was captured with the kernel callbacks in it
     st = r.status.cpu().numpy()
     assert (st <= STATUS_ACCEPTABLE).all()
     X = r.x.cpu().numpy()
