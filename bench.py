@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--no-target", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch each step from Python instead of a HIP graph")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--max-ls", type=int, default=4, help="solve5: line-search trials per iteration")
+    ap.add_argument("--max-soc", type=int, default=1, help="solve5: second-order corrections per iteration")
     ap.add_argument("--pmc-child", default="", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -180,8 +182,9 @@ def solve_bench(args):
     X0t, mt = torch.tensor(X0, device=dev), torch.tensor(mass, device=dev)
     steps = max(1, min(args.steps, 5))
     warm = 1 if args.warmup > 0 else 0
+    opts = dict(max_iter=300, max_ls=args.max_ls, max_soc=args.max_soc)
     for _ in range(warm):
-        batch_ipm_solve(prob, X0t, mt, max_iter=300)
+        batch_ipm_solve(prob, X0t, mt, **opts)
     torch.cuda.synchronize()
     print(f"[solve5] warmup done", file=sys.stderr, flush=True)
     if world > 1:
@@ -189,7 +192,7 @@ def solve_bench(args):
     ev = KernelEvaluator(prob)
     t0 = time.perf_counter()
     for _ in range(steps):
-        r = batch_ipm_solve(prob, X0t, mt, evaluator=ev, max_iter=300)
+        r = batch_ipm_solve(prob, X0t, mt, evaluator=ev, **opts)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -210,7 +213,7 @@ def solve_bench(args):
             Bc = 64
             tc = time.perf_counter()
             rc = batch_ipm_solve(prob, torch.tensor(X0[:Bc]), torch.tensor(mass[:Bc]),
-                                 evaluator=OracleBatchEvaluator(prob), max_iter=300)
+                                 evaluator=OracleBatchEvaluator(prob), **opts)
             tc = time.perf_counter() - tc
             cpu = {"value": Bc / tc, "unit": "solves/s", "cores": 4, "kind": "port",
                    "sample": f"{Bc} instances, the same batched solver over the oracle's callbacks on CPU torch "
@@ -224,7 +227,8 @@ def solve_bench(args):
             "ms_per_step": dt / steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f64", "data": "synthetic (TestBasic ground scenario, per-instance mass U[80,150])",
             "config": {"workload": SOLVE_CONFIG.name, "contacts": 4, "environment": "ground", "batch_per_gpu": B,
-                       "parallelism": f"instance-sharded x{world}", "hessian": "exact (batched central differences)"},
+                       "parallelism": f"instance-sharded x{world}", "hessian": "exact (batched central differences)",
+                       "max_ls": args.max_ls, "max_soc": args.max_soc},
             "solved": ok, "iterations_max": int(its.max().item()), "iterations_mean": float(its.mean().item()),
             "lockstep_iterations": r.iterations_run, "eval_launches_per_solve": r.evaluations,
             "graph": r.graph,

@@ -102,7 +102,7 @@ class BatchSolveResult:
 
 def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None, tol: float = 1e-8,
                     max_iter: int = 3000, mu_init: float = 0.1, acceptable_tol: float = 1e-6,
-                    acceptable_iter: int = 15, max_ls: int = 10, max_soc: int = 2, hessian: str = "exact",
+                    acceptable_iter: int = 15, max_ls: int = 4, max_soc: int = 1, hessian: str = "exact",
                     fd_step: float = 1e-6, graph: Optional[bool] = None, check_every: int = 4,
                     verbose: int = 0) -> BatchSolveResult:
     """Solve B instances of `problem`'s template from the starting points X0 [B, n] (torch float64,

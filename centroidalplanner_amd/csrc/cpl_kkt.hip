@@ -76,6 +76,60 @@ struct KktShared {
   double delta_w, delta_c;
 };
 
+// Dot product of two strided LDS vectors with four independent accumulators (latency, not order,
+// bounds these short loops; the solver is not a parity-critical path).
+__device__ __forceinline__ double lds_dot(const double* a, int sa, const double* b, int sb, int len) {
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  int k = 0;
+  for (; k + 3 < len; k += 4) {
+    s0 += a[k * sa] * b[k * sb];
+    s1 += a[(k + 1) * sa] * b[(k + 1) * sb];
+    s2 += a[(k + 2) * sa] * b[(k + 2) * sb];
+    s3 += a[(k + 3) * sa] * b[(k + 3) * sb];
+  }
+  for (; k < len; ++k) s0 += a[k * sa] * b[k * sb];
+  return (s0 + s1) + (s2 + s3);
+}
+
+// The same with one operand in global memory (L2-resident): eight loads in flight per thread.
+__device__ __forceinline__ double glb_dot(const double* a, int sa, const double* b, int sb, int len) {
+  double s[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  int k = 0;
+  for (; k + 7 < len; k += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s[u] += a[(k + u) * sa] * b[(k + u) * sb];
+  }
+  for (; k < len; ++k) s[0] += a[k * sa] * b[k * sb];
+  return ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+}
+
+// Triangular solve T x = b in place (x holds b on entry), n <= 128, by wave 0 alone: rows live in
+// lanes (lane, lane + 64); column-oriented substitution, the solved component broadcast by a
+// shuffle, one LDS read + FMA per lane and step.  T(i, k) = Tm[i * si + k * sk]; diagonal
+// D[i * sd].  lower: forward substitution; otherwise backward.  Callers barrier afterwards.
+__device__ void wave_trsv(int n, bool lower, const double* Tm, int si, int sk, const double* D, int sd, double* x) {
+  const int lane = threadIdx.x & 63;
+  const int r0 = lane, r1 = lane + 64;
+  double a0 = r0 < n ? x[r0] : 0.0;
+  double a1 = r1 < n ? x[r1] : 0.0;
+  for (int t = 0; t < n; ++t) {
+    const int i = lower ? t : n - 1 - t;
+    const double ai = i < 64 ? __shfl(a0, i) : __shfl(a1, i - 64);
+    const double xi = ai / D[i * sd];
+    if (r0 == i) a0 = xi;
+    if (r1 == i) a1 = xi;
+    if (lower) {
+      if (r0 > i && r0 < n) a0 -= Tm[r0 * si + i * sk] * xi;
+      if (r1 > i && r1 < n) a1 -= Tm[r1 * si + i * sk] * xi;
+    } else {
+      if (r0 < i) a0 -= Tm[r0 * si + i * sk] * xi;
+      if (r1 < i) a1 -= Tm[r1 * si + i * sk] * xi;
+    }
+  }
+  if (r0 < n) x[r0] = a0;
+  if (r1 < n) x[r1] = a1;
+}
+
 // Solve with the factors in LDS: Q [nw][nw] (row-major: Q[r*nw + c]), QR array (row j = column j of
 // A^T after the reflections; R[i][j] = QR[j*nw + i] for i < j, R[j][j] = Rd[j]), L [nz][nz] the
 // Cholesky of the reduced Hessian, M [nw][nw] (plus delta_w on the diagonal, applied here).
@@ -87,79 +141,38 @@ __device__ void kkt_solve_lds(int nw, int m, const double* Q, const double* QR, 
   const int nz = nw - m;
   double* py = tmp;          // [m]
   double* t = tmp + nw;      // [nw]
-  // R^T p_y = q2 (forward substitution; R^T is lower with (R^T)[i][k] = R[k][i] = QR[i*nw + k])
-  if (tid == 0) {
-    for (int i = 0; i < m; ++i) {
-      double s = q2[i];
-      for (int k = 0; k < i; ++k) s -= QR[i * nw + k] * py[k];
-      py[i] = s / Rd[i];
-    }
-  }
+  // R^T p_y = q2 (forward substitution; (R^T)[i][k] = R[k][i] = QR[i*nw + k])
+  for (int i = tid; i < m; i += blockDim.x) py[i] = q2[i];
+  __syncthreads();
+  if (tid < 64) wave_trsv(m, true, QR, nw, 1, Rd, 1, py);
   __syncthreads();
   // dw <- Y p_y
-  for (int r = tid; r < nw; r += blockDim.x) {
-    double s = 0.0;
-    for (int k = 0; k < m; ++k) s += Q[r * nw + k] * py[k];
-    dw[r] = s;
-  }
+  for (int r = tid; r < nw; r += blockDim.x) dw[r] = lds_dot(Q + r * nw, 1, py, 1, m);
   __syncthreads();
   // t = q1 - (M + dW I) Y p_y
-  for (int r = tid; r < nw; r += blockDim.x) {
-    double s = q1[r] - dW * dw[r];
-    for (int k = 0; k < nw; ++k) s -= M[r * nw + k] * dw[k];
-    t[r] = s;
-  }
+  for (int r = tid; r < nw; r += blockDim.x) t[r] = q1[r] - dW * dw[r] - lds_dot(M + r * nw, 1, dw, 1, nw);
   __syncthreads();
   if (nz > 0) {
     // rz = Z^T t into tmp[m .. m+nz) (py still needed) -> p_z by the two triangular solves
     double* rz = tmp + m;
-    for (int c = tid; c < nz; c += blockDim.x) {
-      double s = 0.0;
-      for (int r = 0; r < nw; ++r) s += Q[r * nw + m + c] * t[r];
-      rz[c] = s;
-    }
+    for (int c = tid; c < nz; c += blockDim.x) rz[c] = lds_dot(Q + m + c, nw, t, 1, nw);
     __syncthreads();
-    if (tid == 0) {
-      for (int i = 0; i < nz; ++i) {
-        double s = rz[i];
-        for (int k = 0; k < i; ++k) s -= L[i * nz + k] * rz[k];
-        rz[i] = s / L[i * nz + i];
-      }
-      for (int i = nz - 1; i >= 0; --i) {
-        double s = rz[i];
-        for (int k = i + 1; k < nz; ++k) s -= L[k * nz + i] * rz[k];
-        rz[i] = s / L[i * nz + i];
-      }
+    if (tid < 64) {
+      wave_trsv(nz, true, L, nz, 1, L, nz + 1, rz);    // L y = rz
+      wave_trsv(nz, false, L, 1, nz, L, nz + 1, rz);   // L^T z = y
     }
     __syncthreads();
     // dw += Z p_z
-    for (int r = tid; r < nw; r += blockDim.x) {
-      double s = 0.0;
-      for (int c = 0; c < nz; ++c) s += Q[r * nw + m + c] * rz[c];
-      dw[r] += s;
-    }
+    for (int r = tid; r < nw; r += blockDim.x) dw[r] += lds_dot(Q + r * nw + m, 1, rz, 1, nz);
     __syncthreads();
   }
   // u = q1 - (M + dW I) dw  -> s = Y^T u -> R dy = s
-  for (int r = tid; r < nw; r += blockDim.x) {
-    double s = q1[r] - dW * dw[r];
-    for (int k = 0; k < nw; ++k) s -= M[r * nw + k] * dw[k];
-    t[r] = s;
-  }
+  for (int r = tid; r < nw; r += blockDim.x) t[r] = q1[r] - dW * dw[r] - lds_dot(M + r * nw, 1, dw, 1, nw);
   __syncthreads();
-  for (int k = tid; k < m; k += blockDim.x) {
-    double s = 0.0;
-    for (int r = 0; r < nw; ++r) s += Q[r * nw + k] * t[r];
-    py[k] = s;  // (py no longer needed)
-  }
+  for (int k = tid; k < m; k += blockDim.x) dy[k] = lds_dot(Q + k, nw, t, 1, nw);
   __syncthreads();
-  if (tid == 0) {
-    for (int i = m - 1; i >= 0; --i) {
-      double s = py[i];
-      for (int k = i + 1; k < m; ++k) s -= QR[k * nw + i] * dy[k];
-      dy[i] = s / Rd[i];
-    }
-  }
+  // R dy = s (backward substitution; R[i][k] = QR[k*nw + i])
+  if (tid < 64) wave_trsv(m, false, QR, 1, nw, Rd, 1, dy);
   __syncthreads();
 }
 
@@ -252,7 +265,8 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
     __syncthreads();
     if (beta[j] != 0.0) {
       const double v0 = tmp[m + j];
-      for (int i = j + 1 + tid; i < nw; i += blockDim.x) x[i] /= v0;  // v (v_j = 1 implicit)
+      const double rv0 = 1.0 / v0;
+      for (int i = j + 1 + tid; i < nw; i += blockDim.x) x[i] *= rv0;  // v (v_j = 1 implicit)
       __syncthreads();
       // apply H_j to the columns k > j: y <- y - beta v (v^T y), one wave per column
       for (int k = j + 1 + wave; k < m; k += nwaves) {
@@ -273,9 +287,7 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
     if (bj != 0.0) {
       const double* v = QR + j * nw;
       for (int c = tid; c < nw; c += blockDim.x) {
-        double s = Q[j * nw + c];
-        for (int r = j + 1; r < nw; ++r) s += v[r] * Q[r * nw + c];
-        s *= bj;
+        const double s = (Q[j * nw + c] + lds_dot(v + j + 1, 1, Q + (j + 1) * nw + c, nw, nw - j - 1)) * bj;
         Q[j * nw + c] -= s;
         for (int r = j + 1; r < nw; ++r) Q[r * nw + c] -= s * v[r];
       }
@@ -305,16 +317,12 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
     double* MZ = ws + b * kkt_ws_per(nw, m);  // global scratch (the workspace; overwritten at the end)
     for (int e = tid; e < nw * nz; e += blockDim.x) {
       const int r = e / nz, c = e % nz;
-      double s = 0.0;
-      for (int k = 0; k < nw; ++k) s += M[r * nw + k] * Q[k * nw + m + c];
-      MZ[e] = s;
+      MZ[e] = lds_dot(M + r * nw, 1, Q + m + c, nw, nw);
     }
     __syncthreads();
     for (int e = tid; e < nz * nz; e += blockDim.x) {
       const int a = e / nz, c = e % nz;
-      double s = 0.0;
-      for (int r = 0; r < nw; ++r) s += Q[r * nw + m + a] * MZ[r * nz + c];
-      Hr0[e] = s;
+      Hr0[e] = glb_dot(Q + m + a, nw, MZ + c, nz, nw);
     }
     __syncthreads();
     // symmetrise, keep a copy in dw.. region (nz*nz may exceed it: use the global scratch again)
@@ -348,17 +356,9 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
   // ---- solve, then one step of iterative refinement on the unregularised system
   kkt_solve_lds(nw, m, Q, QR, Rd, L, M, dW, q1, q2, dw, dy, tmp);
   if (!sh.rank_def) {
-    for (int r = tid; r < nw; r += blockDim.x) {
-      double s = q1[r] - dW * dw[r];
-      for (int k = 0; k < nw; ++k) s -= M[r * nw + k] * dw[k];
-      for (int k = 0; k < m; ++k) s -= Ab[k * nw + r] * dy[k];
-      e1[r] = s;
-    }
-    for (int k = tid; k < m; k += blockDim.x) {
-      double s = q2[k];
-      for (int r = 0; r < nw; ++r) s -= Ab[k * nw + r] * dw[r];
-      e2[k] = s;
-    }
+    for (int r = tid; r < nw; r += blockDim.x)
+      e1[r] = q1[r] - dW * dw[r] - lds_dot(M + r * nw, 1, dw, 1, nw) - glb_dot(dy, 1, Ab + r, nw, m);
+    for (int k = tid; k < m; k += blockDim.x) e2[k] = q2[k] - glb_dot(dw, 1, Ab + k * nw, 1, nw);
     __syncthreads();
     // the correction reuses q1/q2 as outputs: (e1, e2) -> (q1, q2)
     kkt_solve_lds(nw, m, Q, QR, Rd, L, M, dW, e1, e2, q1, q2, tmp);
