@@ -53,17 +53,12 @@ __device__ bool lds_cholesky(double* H, int n, int* flag) {
     const double lkk = H[k * n + k];
     for (int i = k + 1 + tid; i < n; i += blockDim.x) H[i * n + k] /= lkk;
     __syncthreads();
-    // trailing update of the lower triangle: (i, j), k < j <= i < n
+    // trailing update of the lower triangle, (i, j) with k < j <= i < n: (row, column-chunk) items
     const int t = n - k - 1;
-    const int pairs = t * (t + 1) / 2;
-    for (int p = tid; p < pairs; p += blockDim.x) {
-      // p -> (ii, jj) with 0 <= jj <= ii < t
-      int ii = (int)((sqrt(8.0 * p + 1.0) - 1.0) * 0.5);
-      while ((ii + 1) * (ii + 2) / 2 <= p) ++ii;
-      while (ii * (ii + 1) / 2 > p) --ii;
-      const int jj = p - ii * (ii + 1) / 2;
-      const int i = k + 1 + ii, j = k + 1 + jj;
-      H[i * n + j] -= H[i * n + k] * H[j * n + k];
+    for (int p = tid; p < t * 4; p += blockDim.x) {
+      const int i = k + 1 + p / 4, c0 = p % 4;
+      const double lik = H[i * n + k];
+      for (int j = k + 1 + c0; j <= i; j += 4) H[i * n + j] -= lik * H[j * n + k];
     }
     __syncthreads();
   }
@@ -103,6 +98,14 @@ __device__ __forceinline__ double glb_dot(const double* a, int sa, const double*
   return ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
 }
 
+// Broadcast lane `src` (wave-uniform) of a double with two v_readlane_b32 (no LDS round trip).
+__device__ __forceinline__ double wave_bcast(double v, int src) {
+  const long long bits = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(bits & 0xffffffffLL), src);
+  const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), src);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 // Triangular solve T x = b in place (x holds b on entry), n <= 128, by wave 0 alone: rows live in
 // lanes (lane, lane + 64); column-oriented substitution, the solved component broadcast by a
 // shuffle, one LDS read + FMA per lane and step.  T(i, k) = Tm[i * si + k * sk]; diagonal
@@ -114,7 +117,7 @@ __device__ void wave_trsv(int n, bool lower, const double* Tm, int si, int sk, c
   double a1 = r1 < n ? x[r1] : 0.0;
   for (int t = 0; t < n; ++t) {
     const int i = lower ? t : n - 1 - t;
-    const double ai = i < 64 ? __shfl(a0, i) : __shfl(a1, i - 64);
+    const double ai = i < 64 ? wave_bcast(a0, i) : wave_bcast(a1, i - 64);
     const double xi = ai / D[i * sd];
     if (r0 == i) a0 = xi;
     if (r1 == i) a1 = xi;
@@ -211,7 +214,7 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
   double* dy = dw + nw;
   double* e1 = dy + m;
   double* e2 = e1 + nw;
-  double* tmp = e2 + nw;  // 2 nw (+ slack)
+  double* tmp = e2 + nw;  // 3 nw
   const double* Mb = Mg + b * nw * nw;
   const double* Ab = Ag + b * m * nw;
   double* wsb = ws + b * kkt_ws_per(nw, m);
@@ -241,40 +244,39 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
   for (int i = tid; i < m * nw; i += blockDim.x) QR[i] = Ab[i];
   __syncthreads();
   double* beta = tmp;  // [m]
-  const int lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
   for (int j = 0; j < m; ++j) {
     double* x = QR + j * nw;  // column j of A^T, rows j..nw-1 active
-    if (wave == 0) {
-      double sig = 0.0;
-      for (int i = j + 1 + lane; i < nw; i += 64) sig += x[i] * x[i];
-      sig = wave_sum(sig);
-      if (lane == 0) {
-        const double alpha = x[j];
-        if (sig == 0.0) {
-          beta[j] = 0.0;
-          Rd[j] = alpha;
-        } else {
-          const double nrm = sqrt(alpha * alpha + sig);
-          const double v0 = alpha <= 0.0 ? alpha - nrm : -sig / (alpha + nrm);
-          beta[j] = 2.0 * v0 * v0 / (sig + v0 * v0);
-          Rd[j] = nrm;
-          tmp[m + j] = v0;  // (scaled below)
-        }
+    if (tid == 0) {
+      const double sig = lds_dot(x + j + 1, 1, x + j + 1, 1, nw - j - 1);
+      const double alpha = x[j];
+      if (sig == 0.0) {
+        beta[j] = 0.0;
+        Rd[j] = alpha;
+      } else {
+        const double nrm = sqrt(alpha * alpha + sig);
+        const double v0 = alpha <= 0.0 ? alpha - nrm : -sig / (alpha + nrm);
+        beta[j] = 2.0 * v0 * v0 / (sig + v0 * v0);
+        Rd[j] = nrm;
+        tmp[m + j] = 1.0 / v0;
       }
     }
     __syncthreads();
-    if (beta[j] != 0.0) {
-      const double v0 = tmp[m + j];
-      const double rv0 = 1.0 / v0;
+    const double bj = beta[j];
+    if (bj != 0.0) {
+      const double rv0 = tmp[m + j];
       for (int i = j + 1 + tid; i < nw; i += blockDim.x) x[i] *= rv0;  // v (v_j = 1 implicit)
       __syncthreads();
-      // apply H_j to the columns k > j: y <- y - beta v (v^T y), one wave per column
-      for (int k = j + 1 + wave; k < m; k += nwaves) {
-        double* y = QR + k * nw;
-        double s = 0.0;
-        for (int i = j + lane; i < nw; i += 64) s += (i == j ? 1.0 : x[i]) * y[i];
-        s = wave_sum(s) * beta[j];
-        for (int i = j + lane; i < nw; i += 64) y[i] -= s * (i == j ? 1.0 : x[i]);
+      // H_j on the columns k > j: y <- y - beta v (v^T y); the dots one thread per column
+      double* sdot = tmp + 2 * m;  // [m] (tmp holds 3 nw >= 3 m doubles)
+      for (int k = j + 1 + tid; k < m; k += blockDim.x) {
+        const double* y = QR + k * nw;
+        sdot[k] = (y[j] + lds_dot(x + j + 1, 1, y + j + 1, 1, nw - j - 1)) * bj;
+      }
+      __syncthreads();
+      const int L = nw - j;
+      for (int e = tid; e < (m - j - 1) * L; e += blockDim.x) {
+        const int k = j + 1 + e / L, i = j + e % L;
+        QR[k * nw + i] -= sdot[k] * (i == j ? 1.0 : x[i]);
       }
     }
     __syncthreads();
