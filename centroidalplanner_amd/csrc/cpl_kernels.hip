@@ -1550,7 +1550,7 @@ static int g_wg = 256;             // threads per tile workgroup (128 or 256)
 static int g_nt = 1;               // non-temporal output stores
 static int g_ablate = 0;           // measurement-only: 1 = skip the compute phase, 2 = skip the stores
 
-static size_t tile_budget() { return g_lds_budget ? g_lds_budget : 32 * 1024; }
+static size_t tile_budget() { return g_lds_budget ? g_lds_budget : 48 * 1024; }
 static size_t pipe_budget() { return g_lds_budget ? g_lds_budget : 48 * 1024; }
 static bool use_rowstage() { return g_variant == VAR_ROWSTAGE; }
 static bool use_pipe(const KParams& K) {
@@ -1559,7 +1559,7 @@ static bool use_pipe(const KParams& K) {
   return g_variant == VAR_AUTO && (K.env_kind == CPL_ENV_NONE || K.env_kind == CPL_ENV_GROUND);
 }
 
-static int32_t plan_tile(KParams& K, bool g, bool j, bool f, bool grad) {
+static int32_t plan_tile(KParams& K, bool g, bool j, bool f, bool grad, int t_max = 64) {
   K.want_g = g; K.want_j = j; K.want_f = f; K.want_grad = grad;
   const bool sq = K.env_kind == CPL_ENV_SUPERQUADRIC || K.env_kind == CPL_ENV_MIXED;
   K.LR = K.N * SQ_L + 1;  // odd instance stride of the SQ scratch: conflict-free LDS banks
@@ -1567,8 +1567,11 @@ static int32_t plan_tile(KParams& K, bool g, bool j, bool f, bool grad) {
                                                (sq ? K.LR : 0));
   const size_t fixed = sizeof(double) * 72 + sizeof(CTab);  // index lists + parameter table
   int T = 64, logT = 6;
-  while (T > 8 && (size_t)T * per + fixed > tile_budget()) { T >>= 1; --logT; }
-  // (T >= 8 is even, so every tile of every record array starts on a 16-byte boundary)
+  while (T > t_max) { T >>= 1; --logT; }
+  while (T > 2 && (size_t)T * per + fixed > tile_budget()) { T >>= 1; --logT; }
+  // (T >= 2 is even, so every tile of every record array starts on a 16-byte boundary; below 8 the
+  // tile boundaries no longer fall on 128-byte lines — the price of more resident workgroups for
+  // the large VALU-bound records)
   if ((size_t)T * per + fixed > 160 * 1024) return fail(CPL_ERR_UNSUPPORTED, "problem too large for one LDS tile");
   K.T = T; K.logT = logT;
   K.cost_seg = (f || grad) ? K.N + 4 : -1;
@@ -1707,6 +1710,14 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
     return d_norms && finish ? cpl_residual_norms(d, batch, d_g, d_norms, stream) : CPL_OK;
   } else {
     st = plan_tile(K, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr);
+    int wg = g_wg;
+    if (!st && g_lds_budget == 0 && K.T < 8) {
+      // records too large for 8 per 48 KiB tile (e.g. 16 Superquadric / mixed contacts, ~10 KiB
+      // each): 2-instance tiles on 128-thread workgroups keep more tiles resident per CU, which the
+      // latency-bound power / division chains need (measured 1.7x over 8-instance tiles)
+      st = plan_tile(K, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr, 2);
+      wg = 128;
+    }
     if (st) return st;
     K.ablate = g_ablate;
     const size_t lds = sizeof(double) * (size_t)(K.offI + 72);
@@ -1720,8 +1731,8 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
     static const KernT table[4][4] = {CPL_TILE_KERNELS(CPL_ENV_NONE), CPL_TILE_KERNELS(CPL_ENV_GROUND),
                                       CPL_TILE_KERNELS(CPL_ENV_SUPERQUADRIC), CPL_TILE_KERNELS(CPL_ENV_MIXED)};
 #undef CPL_TILE_KERNELS
-    const KernT kern = table[K.env_kind][(g_wg == 256 ? 2 : 0) + (g_nt ? 1 : 0)];
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(g_wg), lds, stream, K, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f,
+    const KernT kern = table[K.env_kind][(wg == 256 ? 2 : 0) + (g_nt ? 1 : 0)];
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(wg), lds, stream, K, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f,
                        d_grad, ws);
     if (K.want_norms) {  // per-tile partials -> final pair
       hipError_t e = hipGetLastError();
