@@ -10,7 +10,9 @@ uses, batched over instances, with every per-instance quantity a row of a device
 
   * variables w = [x_free, s]: fixed variables (x_l == x_u, CoMPlanner's positions / normals) are
     parameters (fixed_variable_treatment = make_parameter); one slack per inequality row
-    (g_I(x) - s = 0, s within [g_l, g_u]); bound_push / bound_frac = 1e-2; bound multipliers start
+    (g_I(x) - s = 0, s within [g_l, g_u]); bounds relaxed by bound_relax_factor = 1e-8, the final
+    point projected back (honor_original_bounds);
+    bound_push / bound_frac = 1e-2; bound multipliers start
     at 1 (bound_mult_init_val), constraint multipliers at the least-squares estimate when it is
     <= 1e3 (constr_mult_init_max);
   * Hessian of the Lagrangian (hessian="exact", IPOPT's default): central differences of its
@@ -30,7 +32,8 @@ uses, batched over instances, with every per-instance quantity a row of a device
     line search (switching condition, Armijo on the barrier objective for f-type steps, filter
     augmentation after h-type steps) with second-order corrections on the first trial,
     kappa_Sigma = 1e10 safeguard on the bound multipliers; no restoration phase: an instance whose
-    line search finds no acceptable point takes the last trial and restarts its filter;
+    line search finds no acceptable point takes one feasibility (min-norm Gauss-Newton) step when
+    that cuts its violation, else the last trial, and restarts its filter;
   * termination on IPOPT's scaled optimality error (s_max = 100) <= tol, or <= acceptable_tol
     (1e-6) for 15 consecutive iterations.
 
@@ -100,6 +103,10 @@ class BatchSolveResult:
         return self.status <= STATUS_ACCEPTABLE
 
 
+_PIVOT_REL = 2.220446049250313e-16  # DBL_EPSILON: the KKT inertia test's zero-pivot level
+_DEBUG_EIG = False
+
+
 def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None, tol: float = 1e-8,
                     max_iter: int = 3000, mu_init: float = 0.1, acceptable_tol: float = 1e-6,
                     acceptable_iter: int = 15, max_ls: int = 4, max_soc: int = 1, hessian: str = "exact",
@@ -154,6 +161,11 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     ninf = torch.full((nI,), -float("inf"), dtype=dt, device=dev)
     wl = torch.cat([xl[free], torch.where(gl[I] > -BIG, gl[I], ninf)])
     wu = torch.cat([xu[free], torch.where(gu[I] < BIG, gu[I], -ninf)])
+    # IPOPT bound_relax_factor = 1e-8: every finite bound moves outwards by 1e-8 max(1, |bound|), so
+    # an inequality that is identically active (a lifting contact's cone rows at F = 0) keeps an
+    # interior for its slack
+    wl = wl - 1e-8 * torch.clamp(wl.abs(), min=1.0)
+    wu = wu + 1e-8 * torch.clamp(wu.abs(), min=1.0)
     hasL, hasU = torch.isfinite(wl), torch.isfinite(wu)
     wl0, wu0 = torch.where(hasL, wl, torch.zeros_like(wl)), torch.where(hasU, wu, torch.zeros_like(wu))
     nbounds = int(hasL.sum().item() + hasU.sum().item())
@@ -267,57 +279,72 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         return dw, dy, delta_w, solve_primal
 
     def kkt_host(M, A, r1, r2, mu, dwl, active):
-        """The same step from torch's dense factorisations (host tensors), null-space method in
-        projector form: G = A A^T (+ delta_c I if rank-deficient), P = I - A^T G^-1 A,
-        (P M P + gamma (I - P)) v = P (r1 - M A^T G^-1 r2) — positive definite iff the reduced
-        Hessian is (the inertia test) — dw = A^T G^-1 r2 + v, G dy = A (r1 - M dw); one refinement."""
-        G = A @ A.transpose(1, 2)
-        LG, infoG = torch.linalg.cholesky_ex(G)
-        delta_c = zeros_B.clone()
-        for _ in range(12):
-            bad = infoG != 0
-            if not bool(bad.any()):
-                break
-            gscale = G.diagonal(dim1=1, dim2=2).amax(1).clamp(min=1e-300)
-            delta_c = torch.where(bad, torch.where(delta_c == 0, 1e-8 * mu ** 0.25 * gscale, delta_c * 100.0), delta_c)
-            LGn, infoGn = torch.linalg.cholesky_ex(G + delta_c[:, None, None] * eye_m)
-            LG = torch.where(bad[:, None, None], LGn, LG)
-            infoG = torch.where(bad, infoGn, infoG)
-        GiA = torch.cholesky_solve(A, LG)
-        Pn = eye_w - A.transpose(1, 2) @ GiA
-        gamma = M.diagonal(dim1=1, dim2=2).abs().mean(1).clamp(min=1.0)
-        Kp = Pn @ M @ Pn + gamma[:, None, None] * (eye_w - Pn)
+        """The same step as cpl_kkt_solve from torch's dense factorisations (host tensors), step for
+        step: QR of A^T = [Y Z] [R; 0], delta_c on R's diagonal where |R_jj| < 1e-10 |R|max, the
+        reduced Hessian Z^T M Z with the inertia test = its Cholesky (pivots at or below
+        _PIVOT_REL |M|max count as zero eigenvalues), dw = Y R^-T q2 + Z p_z, R dy = Y^T (q1 - M dw),
+        one refinement step when A has full rank."""
+        Qf, Rf = torch.linalg.qr(A.transpose(1, 2), mode="complete")
+        Y, Z = Qf[:, :, :m], Qf[:, :, m:]
+        R = Rf[:, :m, :m].clone()
+        Rd = R.diagonal(dim1=1, dim2=2)
+        rmax = Rd.abs().amax(1) if m else zeros_B
+        dc = 1e-8 * mu ** 0.25 * torch.where(rmax > 0, rmax, torch.ones_like(rmax))
+        small = ~(Rd.abs() >= 1e-10 * rmax[:, None]) | (rmax[:, None] == 0)
+        rank_def = small.any(1) if m else torch.zeros(B, dtype=torch.bool)
+        delta_c = torch.where(rank_def, dc, zeros_B)
+        Rd.copy_(torch.where(small, Rd + torch.where(Rd < 0, -dc[:, None], dc[:, None]), Rd))
+        Hr = Z.transpose(1, 2) @ M @ Z
+        Hr = 0.5 * (Hr + Hr.transpose(1, 2))
+        nz = nw - m
+        eye_z = torch.eye(nz, dtype=dt)
+        piv_tol = _PIVOT_REL * M.diagonal(dim1=1, dim2=2).abs().amax(1)
+
+        def chol(dw_):
+            Lf, inf_ = torch.linalg.cholesky_ex(Hr + dw_[:, None, None] * eye_z)
+            if nz:
+                inf_ = torch.where((inf_ == 0) & ((Lf.diagonal(dim1=1, dim2=2) ** 2).amin(1) <= piv_tol),
+                                   torch.ones_like(inf_), inf_)
+            return Lf, inf_
+
         delta_w = zeros_B.clone()
-        L1, info1 = torch.linalg.cholesky_ex(Kp)
-        for _ in range(40):
+        L1, info1 = chol(delta_w)
+        if _DEBUG_EIG and nz:
+            print("  eig(Hr) min", torch.linalg.eigvalsh(Hr)[:, 0].tolist(), "tol", piv_tol.tolist())
+        for _ in range(64):
             bad = info1 != 0
             if not bool(bad.any()):
                 break
             first_dw = torch.where(dwl == 0, torch.full_like(delta_w, 1e-4), torch.clamp(dwl / 3.0, min=1e-20))
             grow = delta_w * torch.where(dwl == 0, 100.0, 8.0)
             delta_w = torch.where(bad, torch.where(delta_w == 0, first_dw, grow), delta_w)
-            L1n, info1n = torch.linalg.cholesky_ex(Kp + delta_w[:, None, None] * Pn)
+            L1n, info1n = chol(delta_w)
             L1 = torch.where(bad[:, None, None], L1n, L1)
             info1 = torch.where(bad, info1n, info1)
         Mw = M + delta_w[:, None, None] * eye_w
 
         def solve(q1, q2):
-            dwy = GiA.transpose(1, 2) @ q2.unsqueeze(2)
-            dw_ = dwy + torch.cholesky_solve(Pn @ (q1.unsqueeze(2) - Mw @ dwy), L1)
-            dy_ = torch.cholesky_solve(A @ (q1.unsqueeze(2) - Mw @ dw_), LG)
+            py = torch.linalg.solve_triangular(R.transpose(1, 2), q2.unsqueeze(2), upper=False)
+            dw_ = Y @ py
+            if nz:
+                pz = torch.cholesky_solve(Z.transpose(1, 2) @ (q1.unsqueeze(2) - Mw @ dw_), L1)
+                dw_ = dw_ + Z @ pz
+            dy_ = torch.linalg.solve_triangular(R, Y.transpose(1, 2) @ (q1.unsqueeze(2) - Mw @ dw_), upper=True)
             return dw_.squeeze(2), dy_.squeeze(2)
 
         def refined(q1, q2):
             d1, d2 = solve(q1, q2)
             e1 = q1 - (Mw @ d1.unsqueeze(2)).squeeze(2) - (A.transpose(1, 2) @ d2.unsqueeze(2)).squeeze(2)
-            e2 = q2 - (A @ d1.unsqueeze(2)).squeeze(2) + delta_c[:, None] * d2
+            e2 = q2 - (A @ d1.unsqueeze(2)).squeeze(2)
             c1, c2 = solve(e1, e2)
-            return d1 + c1, d2 + c2
+            keep = rank_def[:, None]
+            return torch.where(keep, d1, d1 + c1), torch.where(keep, d2, d2 + c2)
 
         dw, dy = refined(r1, r2)
         return dw, dy, delta_w, lambda r2v: refined(r1, r2v)[0]
 
     kkt = kkt_device if use_hip else kkt_host
+
 
     def errors(o, wv, yv, zl, zu):
         A_ = jac_w(o["J"])
@@ -484,10 +511,22 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                     th_old = ths
                     ct = cons(os_["g"], ws[:, nf:])
             alpha = torch.where(st["searching"], 0.5 * alpha, alpha)
-        # no acceptable trial (IPOPT would enter its restoration phase): take the last trial and
-        # restart that instance's filter
+        # no acceptable trial: a feasibility step stands in for IPOPT's restoration phase —
+        # min 1/2 dw^T (Sigma + sqrt(mu) D_R^2) dw s.t. A dw = -c (D_R = diag(1 / max(1, |w|)),
+        # IPOPT's restoration proximity weight), fraction to the boundary, taken when it cuts the
+        # violation by 10 %; the multipliers stay.  Otherwise the last trial.  Either way the
+        # instance's filter restarts.  (The KKT kernel skips the instances outside the mask.)
         failed = st["searching"]
-        take(failed, wt, o, 2.0 * alpha, torch.zeros_like(failed))
+        Mr = torch.diag_embed(Sig + mu.sqrt()[:, None] * torch.clamp(w.abs(), min=1.0) ** -2)
+        dwr = kkt(Mr, A, torch.zeros_like(w), -c, mu, zeros_B, failed)[0]
+        ar = torch.minimum(max_step(w, dwr, hasL, wl0, tau), max_step(-w, -dwr, hasU, -wu0, tau))
+        wr = w + ar[:, None] * dwr
+        orr = evaluate_fg(unpack(torch.where(failed[:, None], wr, st["w"])))
+        thr = cons(orr["g"], wr[:, nf:]).abs().sum(1)
+        rest = failed & torch.isfinite(thr) & torch.isfinite(orr["f"]) & (thr <= 0.9 * theta_k)
+        take(rest, wr, orr, zeros_B, torch.zeros_like(failed))
+        take(st["searching"], wt, o, 2.0 * alpha, torch.zeros_like(failed))
+        a_z = torch.where(rest, zeros_B, a_z)
         addm = st["aug"] & active
         fi = fslot == torch.remainder(fc, FMAX)[:, None]
         ft = torch.where(addm[:, None] & fi, ((1.0 - 1e-5) * theta_k)[:, None], ft)
@@ -551,7 +590,9 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
             b = int(verbose) - 2
             print(f"   [{b}] mu={float(mu[b]):.2e} err0={float(E['err0'][b]):.2e} a_max={float(a_max[b]):.2e} "
                   f"alpha={float(al[b]):.2e} dw={float(dw[b].abs().max()):.2e} dy={float(dy[b].abs().max()):.2e} "
-                  f"dW={float(delta_w[b]):.1e} f={float(cur['f'][b]):.6e}")
+                  f"dW={float(delta_w[b]):.1e} f={float(cur['f'][b]):.6e} d_inf={float(E['d_inf'][b]):.2e} "
+                  f"c_inf={float(E['base'][b]):.2e} argdw={int(dw[b].abs().argmax())} "
+                  f"argdual={int(((E['gw'] + (E['A'].transpose(1, 2) @ y.unsqueeze(2)).squeeze(2) - S['zL'] + S['zU'])[b]).abs().argmax())}")
 
     # ---- drive the iterations
     it_run = 0
@@ -581,8 +622,12 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
             print(f"it {it_run:4d} active {int(S['active'].sum())}")
     # final convergence test at the last iterate
     check(errors({"f": S["f"], "grad": S["grad"], "g": S["g"], "J": S["J"]}, S["w"], S["y"], S["zL"], S["zU"]))
-    g = S["g"]
+    # IPOPT honor_original_bounds: the final point is projected back into the unrelaxed bounds and
+    # its objective / constraint values reported there
+    Xf = torch.minimum(torch.maximum(unpack(S["w"]), xl), xu).contiguous()
+    fin = evaluate_fg(Xf)
+    g = fin["g"]
     viol = torch.clamp(torch.maximum(gl - g, g - gu), min=0.0).amax(1) if m else zeros_B
-    return BatchSolveResult(x=unpack(S["w"]), y=S["y"], status=S["status"], iterations=S["iters"],
-                            objective=S["f"], primal_inf=viol, dual_inf=S["d_inf"], evaluations=n_eval,
+    return BatchSolveResult(x=Xf, y=S["y"], status=S["status"], iterations=S["iters"],
+                            objective=fin["f"].clone(), primal_inf=viol, dual_inf=S["d_inf"], evaluations=n_eval,
                             iterations_run=it_run, graph=use_graph)

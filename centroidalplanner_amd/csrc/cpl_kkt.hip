@@ -9,7 +9,7 @@
 //     R dy = Y^T (r1 - (M + dW I) dw),
 // with IPOPT's inertia correction inside the kernel: the KKT matrix has inertia (nw+, m-, 0) iff A
 // has full row rank and the reduced Hessian Z^T M Z is positive definite, so the Cholesky of the
-// reduced Hessian is the inertia test and dW follows IPOPT's schedule (first trial 1e-4, or
+// reduced Hessian is the inertia test (pivots at the rounding level eps max|M_ii| count as zero) and dW follows IPOPT's schedule (first trial 1e-4, or
 // dW_last / 3; growth x100 without history, x8 with) until it succeeds; a rank-deficient A (|R_jj|
 // tiny) gets dC = 1e-8 mu^(1/4) |R|max on R's diagonal (IPOPT's jacobian_regularization_value).
 // One step of iterative refinement against the unregularised system follows when dC = 0.
@@ -37,15 +37,15 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 // Right-looking Cholesky of the n x n matrix H (row-major, stride n) in LDS, lower factor in place.
-// Returns true on success (every pivot positive and finite).  All threads call it.
-__device__ bool lds_cholesky(double* H, int n, int* flag) {
+// Returns true on success (every pivot above pivot_min and finite).  All threads call it.
+__device__ bool lds_cholesky(double* H, int n, int* flag, double pivot_min) {
   const int tid = threadIdx.x;
   if (tid == 0) *flag = 0;
   __syncthreads();
   for (int k = 0; k < n; ++k) {
     if (tid == 0) {
       const double d = H[k * n + k];
-      if (!(d > 0.0) || !(d < INFINITY)) *flag = 1;
+      if (!(d > pivot_min) || !(d < INFINITY)) *flag = 1;
       H[k * n + k] = sqrt(d > 0.0 ? d : 1.0);
     }
     __syncthreads();
@@ -338,10 +338,16 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
     const double last = dw_last ? dw_last[b] : 0.0;
     double dW = 0.0;
     int32_t inf = 0;
+    // a pivot at or below DBL_EPSILON max|M_ii| — the rounding level of Z^T M Z's entries, M
+    // carrying barrier terms up to ~1e12 — counts as a zero eigenvalue (wrong inertia, as IPOPT
+    // counts zero eigenvalues): numerically flat directions get delta_w, not an unbounded step
+    double mmax = 0.0;
+    for (int a = 0; a < nw; ++a) mmax = fmax(mmax, fabs(M[a * nw + a]));
+    const double pivot_min = 2.220446049250313e-16 * mmax;
     for (int attempt = 0; attempt < 64; ++attempt) {
       for (int e = tid; e < nz * nz; e += blockDim.x) L[e] = Hsave[e] + ((e / nz == e % nz) ? dW : 0.0);
       __syncthreads();
-      if (lds_cholesky(L, nz, &sh.flag)) break;
+      if (lds_cholesky(L, nz, &sh.flag, pivot_min)) break;
       if (dW == 0.0) dW = last == 0.0 ? 1e-4 : fmax(1e-20, last / 3.0);
       else dW *= last == 0.0 ? 100.0 : 8.0;
       if (dW > 1e40) { inf = 1; break; }

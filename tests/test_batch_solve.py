@@ -144,3 +144,106 @@ def test_batch_solve_gpu_kernel_callbacks():
     rc = batch_ipm_solve(prob, torch.as_tensor(X0[sub]), torch.as_tensor(mass[sub]),
                          evaluator=OracleBatchEvaluator(prob), max_iter=200)
     np.testing.assert_allclose(obj[sub], rc.objective.numpy(), rtol=1e-8)
+
+
+# ---- the other TestBasic scenarios, many instances at once (per-instance robot masses) -------------
+def _scenario(which):
+    """TestBasic.cpp:138-222 (Superquadric, force weight 0 as in the test) and :225-292 (CoMPlanner:
+    fixed contact positions / normals, contact4 lifting, thresholds 20)."""
+    from centroidalplanner_amd import CentroidalPlanner, CoMPlanner, Superquadric
+
+    names = ["contact1", "contact2", "contact3", "contact4"]
+    if which == "superquadric":
+        env = Superquadric()
+        env.SetMu(MU)
+        env.SetParameters([0.0, 0.0, 1.0], [0.3, 0.3, 10.0], [10.0, 10.0, 10.0])
+        cpl = CentroidalPlanner(names, 100.0, env)
+        cpl.SetForceWeight(0.0)
+        for c in names:
+            cpl.SetPosBounds(c, np.array([-0.5, -0.5, 0.5]), np.array([0.5, 0.5, 1.5]))
+        cpl.SetManipulationWrench(WRENCH)
+        prob = cpl.GetCplProblem()
+        x0 = np.zeros(prob.n)
+        x0[0:3] = [0.0, 0.0, 1.0]
+        for i, (px, py) in enumerate([(0.3, 0.0), (0.0, 0.3), (-0.3, 0.0), (0.0, -0.3)]):
+            nrm = -np.array([px, py, 0.0]) / 0.3
+            x0[3 + 9 * i: 6 + 9 * i] = nrm * 300.0 + np.array([0.0, 0.0, 250.0])
+            x0[6 + 9 * i: 9 + 9 * i] = [px, py, 1.0 + 0.01 * (i - 1.5)]
+            x0[9 + 9 * i: 12 + 9 * i] = nrm
+        wrench = WRENCH
+    else:
+        cpl = CoMPlanner(names, 100.0)
+        cpl.SetMu(MU)
+        for c, p in zip(names, ([1.0, 1.0, 0.0], [-1.0, 1.0, 0.0], [-1.0, -1.0, 0.0], [1.0, -1.0, 0.0])):
+            cpl.SetContactPosition(c, p)
+        cpl.SetLiftingContact("contact4")
+        for c in names:
+            cpl.SetForceThreshold(c, 20.0)
+        prob = cpl.GetCplProblem()
+        x0 = np.zeros(prob.n)
+        x0[0:3] = [0.0, 0.0, 1.0]
+        for i in range(4):
+            x0[3 + 9 * i: 6 + 9 * i] = [1.0, 1.0, 330.0]
+        wrench = np.zeros(6)
+    xl, xu, _, _ = prob.get_bounds_info()
+    return prob, np.clip(x0, xl, xu), wrench
+
+
+def _certify_scenario(which, prob, x, mass, wrench):
+    """TestBasic's own assertions for the scenario (TestBasic.cpp:187-220 / :271-290)."""
+    C, R, P = np.array([0.0, 0.0, 1.0]), np.array([0.3, 0.3, 10.0]), np.array([10.0, 10.0, 10.0])
+    xl, xu, _, _ = prob.get_bounds_info()
+    assert (x >= xl).all() and (x <= xu).all()
+    c = x[0:3]
+    F_sum, T_sum = np.zeros(3), np.zeros(3)
+    for i in range(4):
+        F, p, nv = x[3 + 9 * i: 6 + 9 * i], x[6 + 9 * i: 9 + 9 * i], x[9 + 9 * i: 12 + 9 * i]
+        F_sum += F
+        T_sum += np.cross(p - c, F)
+        assert -F.dot(nv) <= 1e-9
+        assert np.linalg.norm(F - nv.dot(F) * nv) - MU * F.dot(nv) <= 1e-7
+        if which == "superquadric":
+            assert sum(((p[k] - C[k]) / R[k]) ** P[k] for k in range(3)) == pytest.approx(1.0, abs=1e-4)
+            assert np.linalg.norm(nv) == pytest.approx(1.0, abs=1e-6)
+    assert F_sum[0] == pytest.approx(wrench[0], abs=1e-6)
+    assert F_sum[1] == pytest.approx(wrench[1], abs=1e-6)
+    assert F_sum[2] == pytest.approx(mass * 9.81 + wrench[2], abs=1e-6)
+    np.testing.assert_allclose(T_sum, wrench[3:], atol=1e-4)
+    if which == "com":  # the lifting contact carries no force
+        np.testing.assert_array_equal(x[3 + 27: 6 + 27], 0.0)
+
+
+@pytest.mark.parametrize("which", ["superquadric", "com"])
+def test_batch_solve_other_scenarios_oracle_cpu(which):
+    prob, x0, wrench = _scenario(which)
+    B = 4
+    mass = np.random.default_rng(3).uniform(80.0, 150.0, B)
+    r = batch_ipm_solve(prob, torch.as_tensor(np.tile(x0, (B, 1))), torch.as_tensor(mass),
+                        evaluator=OracleBatchEvaluator(prob), max_iter=300)
+    assert bool((r.status <= STATUS_ACCEPTABLE).all()), r.status
+    for b in range(B):
+        _certify_scenario(which, prob, r.x[b].numpy(), mass[b], wrench)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["superquadric", "com"])
+def test_batch_solve_other_scenarios_gpu(which):
+    prob, x0, wrench = _scenario(which)
+    B = 256
+    mass = np.random.default_rng(4).uniform(80.0, 150.0, B)
+    dev = torch.device("cuda:0")
+    r = batch_ipm_solve(prob, torch.as_tensor(np.tile(x0, (B, 1)), device=dev), torch.as_tensor(mass, device=dev),
+                        max_iter=1000)
+    assert r.graph
+    st = r.status.cpu().numpy()
+    ok = st <= STATUS_ACCEPTABLE
+    if which == "superquadric":
+        assert ok.all(), np.bincount(st)
+    else:
+        # CoMPlanner: the contact held at its force threshold ends at zero tangential force, where
+        # |F_t| - mu F_n is not differentiable (the reference's Jacobian is 0/0 there): Newton
+        # converges slowly around the kink (30-800 iterations on the CPU sample)
+        assert ok.mean() >= 0.97, np.bincount(st)
+    X = r.x.cpu().numpy()
+    for b in np.flatnonzero(ok)[::17]:
+        _certify_scenario(which, prob, X[b], mass[b], wrench)
