@@ -113,6 +113,14 @@ SIGNATURES = {
         [c_int32, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     ),
+    "cpl_ipm_trial_point": (
+        c_int32,
+        [c_int64, c_int32, c_int32, c_int32] + [c_void_p] * 11,
+    ),
+    "cpl_ipm_judge_take": (
+        c_int32,
+        [c_int64, c_int32, c_int32, c_int32, c_int32] + [c_void_p] * 28,
+    ),
 }
 
 

@@ -169,6 +169,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     hasL, hasU = torch.isfinite(wl), torch.isfinite(wu)
     wl0, wu0 = torch.where(hasL, wl, torch.zeros_like(wl)), torch.where(hasU, wu, torch.zeros_like(wu))
     nbounds = int(hasL.sum().item() + hasU.sum().item())
+    hasL_u8, hasU_u8 = hasL.to(torch.uint8).contiguous(), hasU.to(torch.uint8).contiguous()
     eye_m = torch.eye(m, dtype=dt, device=dev)
     eye_w = torch.eye(nw, dtype=dt, device=dev)
     eye_f = torch.eye(nf, dtype=dt, device=dev)
@@ -181,6 +182,9 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     np.add.at(col_ptr_np, jCol.astype(np.int64) + 1, 1)
     col_ptr_np = np.cumsum(col_ptr_np)
     csc = [torch.as_tensor(a.astype(np.int32), device=dev) for a in (col_ptr_np, order, iRow[order])]
+    row_slack_np = np.full(m, -1, dtype=np.int32)
+    row_slack_np[I_np] = np.arange(nI, dtype=np.int32)
+    row_slack = torch.as_tensor(row_slack_np, device=dev)
     if use_hip:
         kkt_ws = torch.empty(B * int(_abi.lib.cpl_kkt_workspace_doubles(nw, m)), dtype=dt, device=dev)
 
@@ -466,8 +470,9 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         phi_k = cur["f"] + barrier(w, mu)
         gd = (gphi * dw).sum(1)
         switch_ok = (theta_k <= theta_min) & (gd < 0)
-        st = {"searching": active.clone(), "f": cur["f"], "g": cur["g"], "w": w, "alpha": zeros_B,
-              "aug": torch.zeros(B, dtype=torch.bool, device=dev)}
+        # line-search state (fresh tensors: the device path updates them in place)
+        st = {"searching": active.clone(), "f": cur["f"].clone(), "g": cur["g"].clone(), "w": w.clone(),
+              "alpha": zeros_B.clone(), "aug": torch.zeros(B, dtype=torch.bool, device=dev)}
 
         def judge(wt, o, al):  # o: {"f", "g"} at the trial points
             th = cons(o["g"], wt[:, nf:]).abs().sum(1)
@@ -488,13 +493,47 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
             st["aug"] = torch.where(mask, aug_mask, st["aug"])
             st["searching"] = st["searching"] & ~mask
 
+        if use_hip:  # the fused kernels of csrc/cpl_ipm.hip (one launch per trial for each)
+            sw_ok = switch_ok.contiguous()
+            ftc, fpc = ft.contiguous(), fp.contiguous()
+
+            def trial(d, al, mask):
+                """w_t = w + al d; the evaluation point takes w_t where mask, else the state's w."""
+                wt_ = torch.empty_like(w)
+                Xt = torch.empty(B, n, dtype=dt, device=dev)
+                _abi.check(_abi.lib.cpl_ipm_trial_point(B, n, nf, nw, _ptr(free), _ptr(fixed), _ptr(Xbase), _ptr(w),
+                                                        _ptr(d.contiguous()), _ptr(al.contiguous()),
+                                                        _ptr(mask.contiguous()), _ptr(st["w"]), _ptr(wt_), _ptr(Xt),
+                                                        stream()))
+                return wt_, evaluate_fg(Xt)
+
+            def judge_take(wt_, o_, al, extra=None):
+                """IPOPT's acceptance test + take for searching (& extra) instances; (ok, theta)."""
+                th_ = torch.empty(B, dtype=dt, device=dev)
+                ok_ = torch.empty(B, dtype=torch.bool, device=dev)
+                _abi.check(_abi.lib.cpl_ipm_judge_take(
+                    B, nw, m, nf, FMAX, _ptr(row_slack), _ptr(gl), _ptr(hasL_u8), _ptr(hasU_u8), _ptr(wl0), _ptr(wu0),
+                    _ptr(wt_), _ptr(o_["f"].contiguous()), _ptr(o_["g"].contiguous()), _ptr(al.contiguous()),
+                    _ptr(mu.contiguous()), _ptr(theta_k.contiguous()), _ptr(phi_k.contiguous()), _ptr(gd.contiguous()),
+                    _ptr(sw_ok), _ptr(theta_max), _ptr(ftc), _ptr(fpc), None if extra is None else _ptr(extra.contiguous()),
+                    _ptr(st["searching"]), _ptr(st["f"]), _ptr(st["g"]), _ptr(st["w"]), _ptr(st["alpha"]),
+                    _ptr(st["aug"]), _ptr(th_), _ptr(ok_), stream()))
+                return ok_, th_
+        else:
+            def trial(d, al, mask):
+                wt_ = w + al[:, None] * d
+                return wt_, evaluate_fg(unpack(torch.where(mask[:, None], wt_, st["w"])))
+
+            def judge_take(wt_, o_, al, extra=None):
+                ok_, augm_, th_ = judge(wt_, o_, al)
+                take(st["searching"] & ok_ & (True if extra is None else extra), wt_, o_, al, augm_)
+                return ok_, th_
+
         alpha = a_max
         wt, o = w, cur
         for ls in range(max(1, max_ls)):
-            wt = w + alpha[:, None] * dw
-            o = evaluate_fg(unpack(torch.where(st["searching"][:, None], wt, st["w"])))
-            ok, augm, th = judge(wt, o, alpha)
-            take(st["searching"] & ok, wt, o, alpha, augm)
+            wt, o = trial(dw, alpha, st["searching"])
+            ok, th = judge_take(wt, o, alpha)
             if ls == 0 and max_soc > 0:
                 soc = st["searching"] & (th >= theta_k)
                 c_soc, a_soc, th_old = c, alpha, theta_k
@@ -503,10 +542,8 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                     c_soc = a_soc[:, None] * c_soc + ct
                     dws = solve_primal(-c_soc)
                     a_soc = torch.minimum(max_step(w, dws, hasL, wl0, tau), max_step(-w, -dws, hasU, -wu0, tau))
-                    ws = w + a_soc[:, None] * dws
-                    os_ = evaluate_fg(unpack(torch.where(soc[:, None], ws, st["w"])))
-                    oks, augs, ths = judge(ws, os_, alpha)
-                    take(soc & oks, ws, os_, alpha, augs)
+                    ws, os_ = trial(dws, a_soc, soc)
+                    oks, ths = judge_take(ws, os_, alpha, soc)
                     soc = soc & ~oks & (ths <= 0.99 * th_old)  # kappa_soc = 0.99
                     th_old = ths
                     ct = cons(os_["g"], ws[:, nf:])
@@ -516,12 +553,11 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         # IPOPT's restoration proximity weight), fraction to the boundary, taken when it cuts the
         # violation by 10 %; the multipliers stay.  Otherwise the last trial.  Either way the
         # instance's filter restarts.  (The KKT kernel skips the instances outside the mask.)
-        failed = st["searching"]
+        failed = st["searching"].clone()
         Mr = torch.diag_embed(Sig + mu.sqrt()[:, None] * torch.clamp(w.abs(), min=1.0) ** -2)
         dwr = kkt(Mr, A, torch.zeros_like(w), -c, mu, zeros_B, failed)[0]
         ar = torch.minimum(max_step(w, dwr, hasL, wl0, tau), max_step(-w, -dwr, hasU, -wu0, tau))
-        wr = w + ar[:, None] * dwr
-        orr = evaluate_fg(unpack(torch.where(failed[:, None], wr, st["w"])))
+        wr, orr = trial(dwr, ar, failed)
         thr = cons(orr["g"], wr[:, nf:]).abs().sum(1)
         rest = failed & torch.isfinite(thr) & torch.isfinite(orr["f"]) & (thr <= 0.9 * theta_k)
         take(rest, wr, orr, zeros_B, torch.zeros_like(failed))

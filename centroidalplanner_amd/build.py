@@ -17,7 +17,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libcpl_mi355x.so")
 
-SOURCES = ["cpl_host.cpp", "cpl_kernels.hip", "cpl_kkt.hip"]
+SOURCES = ["cpl_host.cpp", "cpl_kernels.hip", "cpl_kkt.hip", "cpl_ipm.hip"]
 HEADERS = ["cpl_layout.hpp", "cpl_status.hpp"]
 
 HIPCC_FLAGS = [

@@ -1,0 +1,162 @@
+// cpl_ipm.hip — fused per-instance vector work of the solve loop's filter line search
+// (centroidalplanner_amd/batch_ipm.py): the trial point and the acceptance test of IPOPT's filter
+// line search (Waechter & Biegler 2006, §2.3-2.4) for every instance in one launch each, instead of
+// ~50 elementwise tensor launches per trial.  One wave per instance: lanes run over the instance's
+// primal-slack vector (nw <= 128) and constraint rows, sums by xor shuffles.  Every quantity is
+// float64; the decisions are the ones batch_ipm.py's host (torch) path takes, with sums reduced in
+// a different order (last-bit differences only).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <string>
+
+#include "cpl_status.hpp"
+
+namespace cpl {
+
+constexpr int IPM_WAVES = 4;  // instances per 256-thread workgroup
+
+__device__ __forceinline__ double ipm_wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// wt = w + alpha d;  X[b, free[k]] = (mask ? wt : w_keep)[k],  X[b, fixed[j]] = Xbase[b, fixed[j]]
+__global__ __launch_bounds__(256) void cpl_ipm_trial_point_kernel(
+    int64_t batch, int n, int nf, int nw, const int64_t* __restrict__ free_idx, const int64_t* __restrict__ fixed_idx,
+    const double* __restrict__ Xbase, const double* __restrict__ w, const double* __restrict__ d,
+    const double* __restrict__ alpha, const uint8_t* __restrict__ mask, const double* __restrict__ w_keep,
+    double* __restrict__ wt, double* __restrict__ X) {
+  const int64_t b = (int64_t)blockIdx.x * IPM_WAVES + (threadIdx.x >> 6);
+  if (b >= batch) return;
+  const int lane = threadIdx.x & 63;
+  const double a = alpha[b];
+  const bool m = mask[b] != 0;
+  for (int k = lane; k < nw; k += 64) {
+    const double v = w[b * nw + k] + a * d[b * nw + k];
+    wt[b * nw + k] = v;
+    if (k < nf) X[b * n + free_idx[k]] = m ? v : w_keep[b * nw + k];
+  }
+  for (int j = lane; j < n - nf; j += 64) X[b * n + fixed_idx[j]] = Xbase[b * n + fixed_idx[j]];
+}
+
+// IPOPT's acceptance test of one trial point per instance, and the take() of batch_ipm.py:
+//   theta = sum |c(w_t)|, phi = f_t - mu (sum log(w_t - wl) + sum log(wu - w_t)),
+//   ok = finite & theta <= theta_max & filter-acceptable & (f-type ? Armijo : sufficient decrease)
+// for instances with searching & (extra_mask or 1); accepted ones copy (f, g, w_t, alpha, aug) into
+// the line-search state and stop searching.  th_out / ok_out: theta and ok of every instance.
+__global__ __launch_bounds__(256) void cpl_ipm_judge_take_kernel(
+    int64_t batch, int nw, int m, int nf, int nfilt, const int32_t* __restrict__ row_slack,
+    const double* __restrict__ gl, const uint8_t* __restrict__ hasL, const uint8_t* __restrict__ hasU,
+    const double* __restrict__ wl0, const double* __restrict__ wu0, const double* __restrict__ wt,
+    const double* __restrict__ f_t, const double* __restrict__ g_t, const double* __restrict__ alpha,
+    const double* __restrict__ mu, const double* __restrict__ theta_k, const double* __restrict__ phi_k,
+    const double* __restrict__ gd, const uint8_t* __restrict__ switch_ok, const double* __restrict__ theta_max,
+    const double* __restrict__ filt_t, const double* __restrict__ filt_p, const uint8_t* __restrict__ extra_mask,
+    uint8_t* __restrict__ searching, double* __restrict__ st_f, double* __restrict__ st_g, double* __restrict__ st_w,
+    double* __restrict__ st_alpha, uint8_t* __restrict__ st_aug, double* __restrict__ th_out,
+    uint8_t* __restrict__ ok_out) {
+  const int64_t b = (int64_t)blockIdx.x * IPM_WAVES + (threadIdx.x >> 6);
+  if (b >= batch) return;
+  const int lane = threadIdx.x & 63;
+  const double* wb = wt + b * nw;
+  const double* gb = g_t + b * m;
+  double th = 0.0;
+  for (int r = lane; r < m; r += 64) {
+    const int s = row_slack[r];
+    th += fabs(s < 0 ? gb[r] - gl[r] : gb[r] - wb[nf + s]);
+  }
+  double lg = 0.0;
+  for (int k = lane; k < nw; k += 64) {
+    if (hasL[k]) lg += log(wb[k] - wl0[k]);
+    if (hasU[k]) lg += log(wu0[k] - wb[k]);
+  }
+  th = ipm_wave_sum(th);
+  lg = ipm_wave_sum(lg);
+  const double ph = f_t[b] - mu[b] * lg;
+  bool rejected = false;
+  for (int k = lane; k < nfilt; k += 64) {
+    const double ft = filt_t[b * nfilt + k], fp = filt_p[b * nfilt + k];
+    rejected |= !((th <= (1.0 - 1e-5) * ft) || (ph <= fp - 1e-8 * ft));
+  }
+  const bool in_filter = __ballot(rejected) == 0;
+  const double al = alpha[b], tk = theta_k[b], pk = phi_k[b], g = gd[b];
+  const bool fin = isfinite(ph) && isfinite(th);
+  const bool ftype = switch_ok[b] && (al * pow(fmax(-g, 0.0), 2.3) > pow(tk, 1.1));
+  const bool armijo = ph <= pk + 1e-8 * al * g;
+  const bool suff = (th <= (1.0 - 1e-5) * tk) || (ph <= pk - 1e-8 * tk);
+  const bool ok = fin && th <= theta_max[b] && in_filter && (ftype ? armijo : suff);
+  const bool take = ok && searching[b] && (extra_mask == nullptr || extra_mask[b]);
+  if (take) {
+    for (int r = lane; r < m; r += 64) st_g[b * m + r] = gb[r];
+    for (int k = lane; k < nw; k += 64) st_w[b * nw + k] = wb[k];
+  }
+  if (lane == 0) {
+    th_out[b] = th;
+    ok_out[b] = ok ? 1 : 0;
+    if (take) {
+      st_f[b] = f_t[b];
+      st_alpha[b] = al;
+      st_aug[b] = (ftype && armijo) ? 0 : 1;
+      searching[b] = 0;
+    }
+  }
+}
+
+}  // namespace cpl
+
+using namespace cpl;
+
+extern "C" {
+
+int32_t cpl_ipm_trial_point(int64_t batch, int32_t n, int32_t nf, int32_t nw, const int64_t* d_free_idx,
+                            const int64_t* d_fixed_idx, const double* d_Xbase, const double* d_w, const double* d_dir,
+                            const double* d_alpha, const uint8_t* d_mask, const double* d_w_keep, double* d_wt,
+                            double* d_X, void* stream) {
+  if (batch < 0 || n <= 0 || nf < 0 || nf > n || nw < nf)
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_trial_point: bad sizes");
+  if (batch == 0) return CPL_OK;
+  if (!d_free_idx || (n > nf && !d_fixed_idx) || !d_Xbase || !d_w || !d_dir || !d_alpha || !d_mask || !d_w_keep ||
+      !d_wt || !d_X)
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_trial_point: missing buffer");
+  const int64_t blocks = (batch + IPM_WAVES - 1) / IPM_WAVES;
+  if (blocks > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_trial_point: batch too large");
+  hipLaunchKernelGGL(cpl_ipm_trial_point_kernel, dim3((unsigned)blocks), dim3(64 * IPM_WAVES), 0, (hipStream_t)stream,
+                     batch, (int)n, (int)nf, (int)nw, d_free_idx, d_fixed_idx, d_Xbase, d_w, d_dir, d_alpha, d_mask,
+                     d_w_keep, d_wt, d_X);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_ipm_trial_point launch: ") + hipGetErrorString(e));
+  return CPL_OK;
+}
+
+int32_t cpl_ipm_judge_take(int64_t batch, int32_t nw, int32_t m, int32_t nf, int32_t nfilt, const int32_t* d_row_slack,
+                           const double* d_gl, const uint8_t* d_hasL, const uint8_t* d_hasU, const double* d_wl0,
+                           const double* d_wu0, const double* d_wt, const double* d_f_t, const double* d_g_t,
+                           const double* d_alpha, const double* d_mu, const double* d_theta_k, const double* d_phi_k,
+                           const double* d_gd, const uint8_t* d_switch_ok, const double* d_theta_max,
+                           const double* d_filt_t, const double* d_filt_p, const uint8_t* d_extra_mask,
+                           uint8_t* d_searching, double* d_st_f, double* d_st_g, double* d_st_w, double* d_st_alpha,
+                           uint8_t* d_st_aug, double* d_th_out, uint8_t* d_ok_out, void* stream) {
+  if (batch < 0 || nw <= 0 || m < 0 || nf < 0 || nf > nw || nfilt < 0)
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_judge_take: bad sizes");
+  if (batch == 0) return CPL_OK;
+  if ((m > 0 && (!d_row_slack || !d_gl || !d_g_t || !d_st_g)) || !d_hasL || !d_hasU || !d_wl0 || !d_wu0 || !d_wt ||
+      !d_f_t || !d_alpha || !d_mu || !d_theta_k || !d_phi_k || !d_gd || !d_switch_ok || !d_theta_max ||
+      (nfilt > 0 && (!d_filt_t || !d_filt_p)) || !d_searching || !d_st_f || !d_st_w || !d_st_alpha || !d_st_aug ||
+      !d_th_out || !d_ok_out)
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_judge_take: missing buffer");
+  const int64_t blocks = (batch + IPM_WAVES - 1) / IPM_WAVES;
+  if (blocks > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_judge_take: batch too large");
+  hipLaunchKernelGGL(cpl_ipm_judge_take_kernel, dim3((unsigned)blocks), dim3(64 * IPM_WAVES), 0, (hipStream_t)stream,
+                     batch, (int)nw, (int)m, (int)nf, (int)nfilt, d_row_slack, d_gl, d_hasL, d_hasU, d_wl0, d_wu0, d_wt,
+                     d_f_t, d_g_t, d_alpha, d_mu, d_theta_k, d_phi_k, d_gd, d_switch_ok, d_theta_max, d_filt_t,
+                     d_filt_p, d_extra_mask, d_searching, d_st_f, d_st_g, d_st_w, d_st_alpha, d_st_aug, d_th_out,
+                     d_ok_out);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_ipm_judge_take launch: ") + hipGetErrorString(e));
+  return CPL_OK;
+}
+
+}  // extern "C"

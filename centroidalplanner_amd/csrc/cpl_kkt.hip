@@ -98,6 +98,35 @@ __device__ __forceinline__ double glb_dot(const double* a, int sa, const double*
   return ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
 }
 
+// Dot products of n strided vectors with one shared operand, G lanes per vector (G | 64): lane
+// `part` of a group sums k = part, part + G, ... and the group reduces with log2(G) xor shuffles;
+// fin(r, dot) runs on the group's first lane.  Every thread of the workgroup must call it (the
+// shuffles run on all lanes; groups never straddle a wave).  Row r of A starts at A + r * sr, its
+// k-th element at stride sk.
+template <int G, class F>
+__device__ __forceinline__ void group_dots(int n, int len, const double* A, int sr, int sk, const double* x, int sx,
+                                           F fin) {
+  const int part = threadIdx.x % G;
+  for (int base = 0; base < n * G; base += blockDim.x) {
+    const int r = (base + (int)threadIdx.x) / G;
+    const bool act = r < n;
+    double s0 = 0.0, s1 = 0.0;
+    if (act) {
+      const double* a = A + (int64_t)r * sr;
+      int k = part;
+      for (; k + G < len; k += 2 * G) {
+        s0 += a[k * sk] * x[k * sx];
+        s1 += a[(k + G) * sk] * x[(k + G) * sx];
+      }
+      if (k < len) s0 += a[k * sk] * x[k * sx];
+    }
+    double s = s0 + s1;
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) s += __shfl_xor(s, o);
+    if (act && part == 0) fin(r, s);
+  }
+}
+
 // Broadcast lane `src` (wave-uniform) of a double with two v_readlane_b32 (no LDS round trip).
 __device__ __forceinline__ double wave_bcast(double v, int src) {
   const long long bits = __double_as_longlong(v);
@@ -150,15 +179,15 @@ __device__ void kkt_solve_lds(int nw, int m, const double* Q, const double* QR, 
   if (tid < 64) wave_trsv(m, true, QR, nw, 1, Rd, 1, py);
   __syncthreads();
   // dw <- Y p_y
-  for (int r = tid; r < nw; r += blockDim.x) dw[r] = lds_dot(Q + r * nw, 1, py, 1, m);
+  group_dots<4>(nw, m, Q, nw, 1, py, 1, [&](int r, double d) { dw[r] = d; });
   __syncthreads();
   // t = q1 - (M + dW I) Y p_y
-  for (int r = tid; r < nw; r += blockDim.x) t[r] = q1[r] - dW * dw[r] - lds_dot(M + r * nw, 1, dw, 1, nw);
+  group_dots<4>(nw, nw, M, nw, 1, dw, 1, [&](int r, double d) { t[r] = q1[r] - dW * dw[r] - d; });
   __syncthreads();
   if (nz > 0) {
     // rz = Z^T t into tmp[m .. m+nz) (py still needed) -> p_z by the two triangular solves
     double* rz = tmp + m;
-    for (int c = tid; c < nz; c += blockDim.x) rz[c] = lds_dot(Q + m + c, nw, t, 1, nw);
+    group_dots<4>(nz, nw, Q + m, 1, nw, t, 1, [&](int c, double d) { rz[c] = d; });
     __syncthreads();
     if (tid < 64) {
       wave_trsv(nz, true, L, nz, 1, L, nz + 1, rz);    // L y = rz
@@ -166,13 +195,13 @@ __device__ void kkt_solve_lds(int nw, int m, const double* Q, const double* QR, 
     }
     __syncthreads();
     // dw += Z p_z
-    for (int r = tid; r < nw; r += blockDim.x) dw[r] += lds_dot(Q + r * nw + m, 1, rz, 1, nz);
+    group_dots<4>(nw, nz, Q + m, nw, 1, rz, 1, [&](int r, double d) { dw[r] += d; });
     __syncthreads();
   }
   // u = q1 - (M + dW I) dw  -> s = Y^T u -> R dy = s
-  for (int r = tid; r < nw; r += blockDim.x) t[r] = q1[r] - dW * dw[r] - lds_dot(M + r * nw, 1, dw, 1, nw);
+  group_dots<4>(nw, nw, M, nw, 1, dw, 1, [&](int r, double d) { t[r] = q1[r] - dW * dw[r] - d; });
   __syncthreads();
-  for (int k = tid; k < m; k += blockDim.x) dy[k] = lds_dot(Q + k, nw, t, 1, nw);
+  group_dots<4>(m, nw, Q, 1, nw, t, 1, [&](int k, double d) { dy[k] = d; });
   __syncthreads();
   // R dy = s (backward substitution; R[i][k] = QR[k*nw + i])
   if (tid < 64) wave_trsv(m, false, QR, 1, nw, Rd, 1, dy);
@@ -246,8 +275,14 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
   double* beta = tmp;  // [m]
   for (int j = 0; j < m; ++j) {
     double* x = QR + j * nw;  // column j of A^T, rows j..nw-1 active
+    if (tid < 64) {  // |x[j+1:]|^2 by wave 0 (two elements per lane + xor reduction)
+      const int i0 = j + 1 + tid, i1 = i0 + 64;
+      double sq = (i0 < nw ? x[i0] * x[i0] : 0.0) + (i1 < nw ? x[i1] * x[i1] : 0.0);
+      sq = wave_sum(sq);
+      if (tid == 0) tmp[2 * m] = sq;
+    }
     if (tid == 0) {
-      const double sig = lds_dot(x + j + 1, 1, x + j + 1, 1, nw - j - 1);
+      const double sig = tmp[2 * m];
       const double alpha = x[j];
       if (sig == 0.0) {
         beta[j] = 0.0;
@@ -268,10 +303,8 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
       __syncthreads();
       // H_j on the columns k > j: y <- y - beta v (v^T y); the dots one thread per column
       double* sdot = tmp + 2 * m;  // [m] (tmp holds 3 nw >= 3 m doubles)
-      for (int k = j + 1 + tid; k < m; k += blockDim.x) {
-        const double* y = QR + k * nw;
-        sdot[k] = (y[j] + lds_dot(x + j + 1, 1, y + j + 1, 1, nw - j - 1)) * bj;
-      }
+      group_dots<8>(m - j - 1, nw - j - 1, QR + (j + 1) * nw + j + 1, nw, 1, x + j + 1, 1,
+                    [&](int kk, double d) { sdot[j + 1 + kk] = (QR[(j + 1 + kk) * nw + j] + d) * bj; });
       __syncthreads();
       const int L = nw - j;
       for (int e = tid; e < (m - j - 1) * L; e += blockDim.x) {
@@ -287,11 +320,25 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
   for (int j = m - 1; j >= 0; --j) {
     const double bj = beta[j];
     if (bj != 0.0) {
+      // 4 lanes per column: partial dots over rows j+1+part (step 4), xor-reduced, then each lane
+      // updates its own rows of the column
       const double* v = QR + j * nw;
-      for (int c = tid; c < nw; c += blockDim.x) {
-        const double s = (Q[j * nw + c] + lds_dot(v + j + 1, 1, Q + (j + 1) * nw + c, nw, nw - j - 1)) * bj;
-        Q[j * nw + c] -= s;
-        for (int r = j + 1; r < nw; ++r) Q[r * nw + c] -= s * v[r];
+      const int part = tid & 3;
+      for (int base = 0; base < nw * 4; base += blockDim.x) {
+        const int c = (base + tid) >> 2;
+        const bool act = c < nw;
+        double s = 0.0;
+        if (act) {
+          if (part == 0) s = Q[j * nw + c];
+          for (int r = j + 1 + part; r < nw; r += 4) s += v[r] * Q[r * nw + c];
+        }
+        s += __shfl_xor(s, 1);
+        s += __shfl_xor(s, 2);
+        s *= bj;
+        if (act) {
+          if (part == 0) Q[j * nw + c] -= s;
+          for (int r = j + 1 + part; r < nw; r += 4) Q[r * nw + c] -= s * v[r];
+        }
       }
     }
     __syncthreads();
@@ -364,9 +411,10 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
   // ---- solve, then one step of iterative refinement on the unregularised system
   kkt_solve_lds(nw, m, Q, QR, Rd, L, M, dW, q1, q2, dw, dy, tmp);
   if (!sh.rank_def) {
-    for (int r = tid; r < nw; r += blockDim.x)
-      e1[r] = q1[r] - dW * dw[r] - lds_dot(M + r * nw, 1, dw, 1, nw) - glb_dot(dy, 1, Ab + r, nw, m);
-    for (int k = tid; k < m; k += blockDim.x) e2[k] = q2[k] - glb_dot(dw, 1, Ab + k * nw, 1, nw);
+    // e1[r] is written and then updated by the same lane (group assignment depends on r only)
+    group_dots<4>(nw, m, Ab, 1, nw, dy, 1, [&](int r, double d) { e1[r] = q1[r] - dW * dw[r] - d; });
+    group_dots<4>(nw, nw, M, nw, 1, dw, 1, [&](int r, double d) { e1[r] -= d; });
+    group_dots<4>(m, nw, Ab, nw, 1, dw, 1, [&](int k, double d) { e2[k] = q2[k] - d; });
     __syncthreads();
     // the correction reuses q1/q2 as outputs: (e1, e2) -> (q1, q2)
     kkt_solve_lds(nw, m, Q, QR, Rd, L, M, dW, e1, e2, q1, q2, tmp);

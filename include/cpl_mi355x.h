@@ -234,6 +234,33 @@ int32_t cpl_kkt_solve(int32_t mode, int64_t batch, int32_t nw, int32_t m, const 
                       const uint8_t* d_active, double* d_dw, double* d_dy, double* d_delta_w, double* d_delta_c,
                       int32_t* d_info, double* d_ws, void* stream);
 
+/*
+ * Solve-loop line search, fused per instance (csrc/cpl_ipm.hip; no reference counterpart — the
+ * work IPOPT's BacktrackingLineSearch / FilterLSAcceptor do for one instance per trial, batched):
+ *
+ * cpl_ipm_trial_point: w_t = w + alpha[b] d (written to d_wt [batch, nw]) and the evaluation point
+ *   X [batch, n]: X[b, free[k]] = mask[b] ? w_t[k] : w_keep[b, k] (k < nf), X[b, fixed[j]] =
+ *   Xbase[b, fixed[j]].  Index arrays are int64, masks one byte per instance.
+ * cpl_ipm_judge_take: IPOPT's acceptance test at the trial points (theta = sum |c|, barrier
+ *   objective phi, filter of `nfilt` (theta, phi) entries per instance, switching condition /
+ *   Armijo / sufficient decrease, theta_max); instances with searching & extra_mask (NULL: all)
+ *   that pass copy (f_t, g_t, w_t, alpha, augment flag) into the line-search state and clear
+ *   searching.  d_th_out / d_ok_out get theta and the test result of every instance.
+ *   row_slack[r] = slack index of inequality row r, -1 for an equality row.
+ */
+int32_t cpl_ipm_trial_point(int64_t batch, int32_t n, int32_t nf, int32_t nw, const int64_t* d_free_idx,
+                            const int64_t* d_fixed_idx, const double* d_Xbase, const double* d_w, const double* d_dir,
+                            const double* d_alpha, const uint8_t* d_mask, const double* d_w_keep, double* d_wt,
+                            double* d_X, void* stream);
+int32_t cpl_ipm_judge_take(int64_t batch, int32_t nw, int32_t m, int32_t nf, int32_t nfilt, const int32_t* d_row_slack,
+                           const double* d_gl, const uint8_t* d_hasL, const uint8_t* d_hasU, const double* d_wl0,
+                           const double* d_wu0, const double* d_wt, const double* d_f_t, const double* d_g_t,
+                           const double* d_alpha, const double* d_mu, const double* d_theta_k, const double* d_phi_k,
+                           const double* d_gd, const uint8_t* d_switch_ok, const double* d_theta_max,
+                           const double* d_filt_t, const double* d_filt_p, const uint8_t* d_extra_mask,
+                           uint8_t* d_searching, double* d_st_f, double* d_st_g, double* d_st_w, double* d_st_alpha,
+                           uint8_t* d_st_aug, double* d_th_out, uint8_t* d_ok_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
