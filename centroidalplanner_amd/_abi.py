@@ -121,6 +121,11 @@ SIGNATURES = {
         c_int32,
         [c_int64, c_int32, c_int32, c_int32, c_int32] + [c_void_p] * 28,
     ),
+    "cpl_ipm_optimality": (
+        c_int32,
+        [c_int64, c_int32, c_int32, c_int32, c_int32, c_double, c_double, c_int32] + [c_void_p] * 26,
+    ),
+    "cpl_ipm_max_step": (c_int32, [c_int64, c_int32] + [c_void_p] * 11),
 }
 
 

@@ -436,16 +436,43 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         """One lock-step iteration of every instance; no host synchronisation (graph-capturable)."""
         w, y, zL, zU, mu = S["w"], S["y"], S["zL"], S["zU"], S["mu"]
         cur = {"f": S["f"], "grad": S["grad"], "g": S["g"], "J": S["J"]}
-        E = errors(cur, w, y, zL, zU)
-        active = check(E).clone()
-        A, gradw, c = E["A"], E["gw"], E["c"]
-        # ---- monotone barrier update (two rounds per iteration), filter reset where mu changed
-        ft, fp, fc = S["filt_t"], S["filt_p"], S["fcount"]
-        for _ in range(2):
-            upd = active & (err_mu(E, mu) <= 10.0 * mu) & (mu > tol / 10.0)
-            mu = torch.where(upd, torch.clamp(torch.minimum(0.2 * mu, mu ** 1.5), min=tol / 10.0), mu)
-            ft, fp, fc = reset_filter(upd, ft, fp, fc)
+        if use_hip:  # optimality error, convergence test and barrier update: one fused launch
+            A = jac_w(cur["J"])
+            gradw = torch.cat([cur["grad"][:, free], zeros_I], 1)
+            c = cons(cur["g"], w[:, nf:])
+            E = {k: torch.empty(B, dtype=dt, device=dev) for k in ("d_inf", "err0", "base")}
+            mu_o = torch.empty(B, dtype=dt, device=dev)
+            ft, fp = torch.empty_like(S["filt_t"]), torch.empty_like(S["filt_p"])
+            fc = torch.empty_like(S["fcount"])
+            _abi.check(_abi.lib.cpl_ipm_optimality(
+                B, nw, m, FMAX, nbounds, tol, acceptable_tol, acceptable_iter, _ptr(A), _ptr(gradw), _ptr(c), _ptr(w),
+                _ptr(y), _ptr(zL), _ptr(zU), _ptr(hasL_u8), _ptr(hasU_u8), _ptr(wl0), _ptr(wu0), _ptr(mu),
+                _ptr(S["filt_t"]), _ptr(S["filt_p"]), _ptr(S["fcount"]), _ptr(S["active"]), _ptr(S["status"]),
+                _ptr(S["acc"]), _ptr(E["d_inf"]), _ptr(E["err0"]), _ptr(E["base"]), _ptr(mu_o), _ptr(ft), _ptr(fp),
+                _ptr(fc), stream()))
+            S["d_inf"].copy_(E["d_inf"])
+            active = S["active"].clone()
+            mu = mu_o
+        else:
+            E = errors(cur, w, y, zL, zU)
+            active = check(E).clone()
+            A, gradw, c = E["A"], E["gw"], E["c"]
+            # ---- monotone barrier update (two rounds per iteration), filter reset where mu changed
+            ft, fp, fc = S["filt_t"], S["filt_p"], S["fcount"]
+            for _ in range(2):
+                upd = active & (err_mu(E, mu) <= 10.0 * mu) & (mu > tol / 10.0)
+                mu = torch.where(upd, torch.clamp(torch.minimum(0.2 * mu, mu ** 1.5), min=tol / 10.0), mu)
+                ft, fp, fc = reset_filter(upd, ft, fp, fc)
         tau = torch.clamp(1.0 - mu, min=0.99)
+
+        def primal_step(d):  # fraction to the boundary along d from w
+            if use_hip:
+                out = torch.empty(B, dtype=dt, device=dev)
+                _abi.check(_abi.lib.cpl_ipm_max_step(B, nw, _ptr(w), _ptr(d.contiguous()), None, None, _ptr(hasL_u8),
+                                                     _ptr(hasU_u8), _ptr(wl0), _ptr(wu0), _ptr(tau), _ptr(out),
+                                                     stream()))
+                return out
+            return torch.minimum(max_step(w, d, hasL, wl0, tau), max_step(-w, -d, hasU, -wu0, tau))
 
         dl = torch.where(hasL, w - wl0, torch.ones_like(w))
         du = torch.where(hasU, wu0 - w, torch.ones_like(w))
@@ -460,8 +487,14 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         dwl = torch.where(active, delta_w, S["dwl"])
         dzL = torch.where(hasL, mu[:, None] / dl - zL - zL / dl * dw, torch.zeros_like(w))
         dzU = torch.where(hasU, mu[:, None] / du - zU + zU / du * dw, torch.zeros_like(w))
-        a_max = torch.minimum(max_step(w, dw, hasL, wl0, tau), max_step(-w, -dw, hasU, -wu0, tau))
-        a_z = torch.minimum(max_step(zL, dzL, hasL, 0.0, tau), max_step(zU, dzU, hasU, 0.0, tau))
+        a_max = primal_step(dw)
+        if use_hip:
+            a_z = torch.empty(B, dtype=dt, device=dev)
+            _abi.check(_abi.lib.cpl_ipm_max_step(B, nw, _ptr(zL), _ptr(dzL.contiguous()), _ptr(zU), _ptr(dzU.contiguous()),
+                                                 _ptr(hasL_u8), _ptr(hasU_u8), None, None, _ptr(tau), _ptr(a_z),
+                                                 stream()))
+        else:
+            a_z = torch.minimum(max_step(zL, dzL, hasL, 0.0, tau), max_step(zU, dzU, hasU, 0.0, tau))
 
         # ---- filter line search (IPOPT: gamma_theta 1e-5, gamma_phi 1e-8, delta 1, s_theta 1.1,
         # s_phi 2.3, eta_phi 1e-8, theta_min/max = 1e-4/1e4 max(1, theta_0)), second-order
@@ -541,7 +574,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                 for _ in range(max_soc):
                     c_soc = a_soc[:, None] * c_soc + ct
                     dws = solve_primal(-c_soc)
-                    a_soc = torch.minimum(max_step(w, dws, hasL, wl0, tau), max_step(-w, -dws, hasU, -wu0, tau))
+                    a_soc = primal_step(dws)
                     ws, os_ = trial(dws, a_soc, soc)
                     oks, ths = judge_take(ws, os_, alpha, soc)
                     soc = soc & ~oks & (ths <= 0.99 * th_old)  # kappa_soc = 0.99
@@ -556,7 +589,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         failed = st["searching"].clone()
         Mr = torch.diag_embed(Sig + mu.sqrt()[:, None] * torch.clamp(w.abs(), min=1.0) ** -2)
         dwr = kkt(Mr, A, torch.zeros_like(w), -c, mu, zeros_B, failed)[0]
-        ar = torch.minimum(max_step(w, dwr, hasL, wl0, tau), max_step(-w, -dwr, hasU, -wu0, tau))
+        ar = primal_step(dwr)
         wr, orr = trial(dwr, ar, failed)
         thr = cons(orr["g"], wr[:, nf:]).abs().sum(1)
         rest = failed & torch.isfinite(thr) & torch.isfinite(orr["f"]) & (thr <= 0.9 * theta_k)
@@ -627,8 +660,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
             print(f"   [{b}] mu={float(mu[b]):.2e} err0={float(E['err0'][b]):.2e} a_max={float(a_max[b]):.2e} "
                   f"alpha={float(al[b]):.2e} dw={float(dw[b].abs().max()):.2e} dy={float(dy[b].abs().max()):.2e} "
                   f"dW={float(delta_w[b]):.1e} f={float(cur['f'][b]):.6e} d_inf={float(E['d_inf'][b]):.2e} "
-                  f"c_inf={float(E['base'][b]):.2e} argdw={int(dw[b].abs().argmax())} "
-                  f"argdual={int(((E['gw'] + (E['A'].transpose(1, 2) @ y.unsqueeze(2)).squeeze(2) - S['zL'] + S['zU'])[b]).abs().argmax())}")
+                  f"c_inf={float(E['base'][b]):.2e} argdw={int(dw[b].abs().argmax())}")
 
     # ---- drive the iterations
     it_run = 0

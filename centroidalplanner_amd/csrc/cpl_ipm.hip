@@ -105,6 +105,148 @@ __global__ __launch_bounds__(256) void cpl_ipm_judge_take_kernel(
   }
 }
 
+// IPOPT's scaled optimality error at the current iterate (s_max = 100), the convergence test and
+// the monotone barrier update of one iteration (batch_ipm.py errors / check / err_mu):
+//   dual = grad_w + A^T y - zL + zU,  comp = (w - wl) zL, (wu - w) zU,
+//   err0 = max(|dual|max / s_d, |c|max, comp_max / s_c)  -> optimal (tol) / acceptable (tol_acc for
+//   acc_iter consecutive iterations) / still active;
+//   two rounds of mu <- max(min(0.2 mu, mu^1.5), tol/10) while err_mu <= 10 mu and mu > tol/10, each
+//   resetting the instance's filter.  Writes status/acc/active/d_inf in place; mu, filter -> *_out.
+__global__ __launch_bounds__(256) void cpl_ipm_optimality_kernel(
+    int64_t batch, int nw, int m, int nfilt, int nbounds, double tol, double acc_tol, int acc_iter,
+    const double* __restrict__ A, const double* __restrict__ gw, const double* __restrict__ c,
+    const double* __restrict__ w, const double* __restrict__ y, const double* __restrict__ zL,
+    const double* __restrict__ zU, const uint8_t* __restrict__ hasL, const uint8_t* __restrict__ hasU,
+    const double* __restrict__ wl0, const double* __restrict__ wu0, const double* __restrict__ mu_in,
+    const double* __restrict__ filt_t, const double* __restrict__ filt_p, const int64_t* __restrict__ fcount,
+    uint8_t* __restrict__ active, int64_t* __restrict__ status, int64_t* __restrict__ acc,
+    double* __restrict__ d_inf_out, double* __restrict__ err0_out, double* __restrict__ base_out,
+    double* __restrict__ mu_out, double* __restrict__ filt_t_out, double* __restrict__ filt_p_out,
+    int64_t* __restrict__ fcount_out) {
+  const int64_t b = (int64_t)blockIdx.x * IPM_WAVES + (threadIdx.x >> 6);
+  if (b >= batch) return;
+  const int lane = threadIdx.x & 63;
+  const double* Ab = A + b * (int64_t)m * nw;
+  const double* yb = y + b * m;
+  // lanes own w entries k = lane, lane + 64 (nw <= 128)
+  double cl[2] = {0.0, 0.0}, cu[2] = {0.0, 0.0};
+  double dmax = 0.0, zs = 0.0, clmax = 0.0, cumax = 0.0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k = lane + 64 * h;
+    if (k < nw) {
+      double dual = gw[b * nw + k];
+      for (int r = 0; r < m; ++r) dual += Ab[r * nw + k] * yb[r];
+      const double zl = zL[b * nw + k], zu = zU[b * nw + k], wk = w[b * nw + k];
+      dual = dual - zl + zu;
+      dmax = fmax(dmax, fabs(dual));
+      zs += fabs(zl) + fabs(zu);
+      cl[h] = hasL[k] ? (wk - wl0[k]) * zl : 0.0;
+      cu[h] = hasU[k] ? (wu0[k] - wk) * zu : 0.0;
+      clmax = fmax(clmax, cl[h]);
+      cumax = fmax(cumax, cu[h]);
+    }
+  }
+  double ys = 0.0, cmax = 0.0;
+  for (int r = lane; r < m; r += 64) {
+    ys += fabs(yb[r]);
+    cmax = fmax(cmax, fabs(c[b * m + r]));
+  }
+  // wave reductions (max by xor shuffles; all lanes end with the totals)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    dmax = fmax(dmax, __shfl_xor(dmax, o));
+    clmax = fmax(clmax, __shfl_xor(clmax, o));
+    cumax = fmax(cumax, __shfl_xor(cumax, o));
+    cmax = fmax(cmax, __shfl_xor(cmax, o));
+  }
+  zs = ipm_wave_sum(zs);
+  ys = ipm_wave_sum(ys);
+  const double s_max = 100.0;
+  const double sd = fmax((ys + zs) / (double)max(m + nbounds, 1), s_max) / s_max;
+  const double sc = fmax(zs / (double)max(nbounds, 1), s_max) / s_max;
+  const double base = fmax(dmax / sd, cmax);
+  const double err0 = fmax(base, fmax(clmax, cumax) / sc);
+  // convergence test
+  bool act = active[b] != 0;
+  const bool done_now = act && err0 <= tol;
+  const int64_t acc_new = (act && err0 <= acc_tol) ? acc[b] + 1 : 0;
+  const bool acc_now = act && !done_now && acc_new >= acc_iter;
+  act = act && !done_now && !acc_now;
+  // barrier update, two rounds
+  double mu = mu_in[b];
+  bool reset = false;
+  for (int round = 0; round < 2; ++round) {
+    double em = 0.0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = lane + 64 * h;
+      if (k < nw) {
+        em = fmax(em, fabs(cl[h] - (hasL[k] ? mu : 0.0)));
+        em = fmax(em, fabs(cu[h] - (hasU[k] ? mu : 0.0)));
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) em = fmax(em, __shfl_xor(em, o));
+    const double err_mu = fmax(base, em / sc);
+    if (act && err_mu <= 10.0 * mu && mu > tol / 10.0) {
+      mu = fmax(fmin(0.2 * mu, pow(mu, 1.5)), tol / 10.0);
+      reset = true;
+    }
+  }
+  for (int k = lane; k < nfilt; k += 64) {
+    filt_t_out[b * nfilt + k] = reset ? INFINITY : filt_t[b * nfilt + k];
+    filt_p_out[b * nfilt + k] = reset ? INFINITY : filt_p[b * nfilt + k];
+  }
+  if (lane == 0) {
+    acc[b] = acc_new;
+    if (done_now) status[b] = 0;
+    else if (acc_now) status[b] = 1;
+    active[b] = act ? 1 : 0;
+    d_inf_out[b] = dmax;
+    err0_out[b] = err0;
+    base_out[b] = base;
+    mu_out[b] = mu;
+    fcount_out[b] = reset ? 0 : fcount[b];
+  }
+}
+
+// Fraction-to-the-boundary step (batch_ipm.py max_step, both sides): the largest alpha <= 1 with
+//   primal (v2 == NULL): -tau (v - lo) / d over hasL & d < 0 and
+//                        -tau (up - v) / -d over hasU & d > 0;
+//   dual (v2 != NULL):   multipliers zL = v (hasL), zU = v2 (hasU) kept >= 0: -tau v / d over
+//                        hasL & d < 0 and -tau v2 / d2 over hasU & d2 < 0.
+__global__ __launch_bounds__(256) void cpl_ipm_max_step_kernel(int64_t batch, int nw, const double* __restrict__ v,
+                                                               const double* __restrict__ d,
+                                                               const double* __restrict__ v2,
+                                                               const double* __restrict__ d2,
+                                                               const uint8_t* __restrict__ hasL,
+                                                               const uint8_t* __restrict__ hasU,
+                                                               const double* __restrict__ lo,
+                                                               const double* __restrict__ up,
+                                                               const double* __restrict__ tau,
+                                                               double* __restrict__ out) {
+  const int64_t b = (int64_t)blockIdx.x * IPM_WAVES + (threadIdx.x >> 6);
+  if (b >= batch) return;
+  const int lane = threadIdx.x & 63;
+  const double t = tau[b];
+  double r = INFINITY;
+  for (int k = lane; k < nw; k += 64) {
+    const double vk = v[b * nw + k], dk = d[b * nw + k];
+    if (v2 == nullptr) {
+      if (hasL[k] && dk < 0.0) r = fmin(r, -t * (vk - lo[k]) / dk);
+      if (hasU[k] && dk > 0.0) r = fmin(r, -t * (up[k] - vk) / -dk);
+    } else {
+      if (hasL[k] && dk < 0.0) r = fmin(r, -t * vk / dk);
+      const double v2k = v2[b * nw + k], d2k = d2[b * nw + k];
+      if (hasU[k] && d2k < 0.0) r = fmin(r, -t * v2k / d2k);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) r = fmin(r, __shfl_xor(r, o));
+  if (lane == 0) out[b] = fmin(r, 1.0);
+}
+
 }  // namespace cpl
 
 using namespace cpl;
@@ -156,6 +298,48 @@ int32_t cpl_ipm_judge_take(int64_t batch, int32_t nw, int32_t m, int32_t nf, int
                      d_ok_out);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_ipm_judge_take launch: ") + hipGetErrorString(e));
+  return CPL_OK;
+}
+
+int32_t cpl_ipm_optimality(int64_t batch, int32_t nw, int32_t m, int32_t nfilt, int32_t nbounds, double tol,
+                           double acc_tol, int32_t acc_iter, const double* d_A, const double* d_gw, const double* d_c,
+                           const double* d_w, const double* d_y, const double* d_zL, const double* d_zU,
+                           const uint8_t* d_hasL, const uint8_t* d_hasU, const double* d_wl0, const double* d_wu0,
+                           const double* d_mu, const double* d_filt_t, const double* d_filt_p,
+                           const int64_t* d_fcount, uint8_t* d_active, int64_t* d_status, int64_t* d_acc,
+                           double* d_d_inf, double* d_err0, double* d_base, double* d_mu_out, double* d_filt_t_out,
+                           double* d_filt_p_out, int64_t* d_fcount_out, void* stream) {
+  if (batch < 0 || nw <= 0 || nw > 128 || m < 0 || nfilt < 0 || nbounds < 0)
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_optimality: need 0 < nw <= 128, m >= 0");
+  if (batch == 0) return CPL_OK;
+  if ((m > 0 && (!d_A || !d_c || !d_y)) || !d_gw || !d_w || !d_zL || !d_zU || !d_hasL || !d_hasU || !d_wl0 ||
+      !d_wu0 || !d_mu || (nfilt > 0 && (!d_filt_t || !d_filt_p || !d_filt_t_out || !d_filt_p_out)) || !d_fcount ||
+      !d_active || !d_status || !d_acc || !d_d_inf || !d_err0 || !d_base || !d_mu_out || !d_fcount_out)
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_optimality: missing buffer");
+  const int64_t blocks = (batch + IPM_WAVES - 1) / IPM_WAVES;
+  if (blocks > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_optimality: batch too large");
+  hipLaunchKernelGGL(cpl_ipm_optimality_kernel, dim3((unsigned)blocks), dim3(64 * IPM_WAVES), 0, (hipStream_t)stream,
+                     batch, (int)nw, (int)m, (int)nfilt, (int)nbounds, tol, acc_tol, (int)acc_iter, d_A, d_gw, d_c, d_w,
+                     d_y, d_zL, d_zU, d_hasL, d_hasU, d_wl0, d_wu0, d_mu, d_filt_t, d_filt_p, d_fcount, d_active,
+                     d_status, d_acc, d_d_inf, d_err0, d_base, d_mu_out, d_filt_t_out, d_filt_p_out, d_fcount_out);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_ipm_optimality launch: ") + hipGetErrorString(e));
+  return CPL_OK;
+}
+
+int32_t cpl_ipm_max_step(int64_t batch, int32_t nw, const double* d_v, const double* d_dir, const double* d_v2,
+                         const double* d_dir2, const uint8_t* d_hasL, const uint8_t* d_hasU, const double* d_lo,
+                         const double* d_up, const double* d_tau, double* d_out, void* stream) {
+  if (batch < 0 || nw <= 0) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_max_step: bad sizes");
+  if (batch == 0) return CPL_OK;
+  if (!d_v || !d_dir || !d_hasL || !d_hasU || (d_v2 ? !d_dir2 : (!d_lo || !d_up)) || !d_tau || !d_out)
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_max_step: missing buffer");
+  const int64_t blocks = (batch + IPM_WAVES - 1) / IPM_WAVES;
+  if (blocks > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_max_step: batch too large");
+  hipLaunchKernelGGL(cpl_ipm_max_step_kernel, dim3((unsigned)blocks), dim3(64 * IPM_WAVES), 0, (hipStream_t)stream,
+                     batch, (int)nw, d_v, d_dir, d_v2, d_dir2, d_hasL, d_hasU, d_lo, d_up, d_tau, d_out);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_ipm_max_step launch: ") + hipGetErrorString(e));
   return CPL_OK;
 }
 

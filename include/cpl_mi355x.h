@@ -260,6 +260,28 @@ int32_t cpl_ipm_judge_take(int64_t batch, int32_t nw, int32_t m, int32_t nf, int
                            const double* d_filt_t, const double* d_filt_p, const uint8_t* d_extra_mask,
                            uint8_t* d_searching, double* d_st_f, double* d_st_g, double* d_st_w, double* d_st_alpha,
                            uint8_t* d_st_aug, double* d_th_out, uint8_t* d_ok_out, void* stream);
+/*
+ * cpl_ipm_optimality: IPOPT's scaled optimality error (s_max = 100) at the current iterates, the
+ *   convergence test (tol; acc_tol for acc_iter consecutive iterations) and the monotone barrier
+ *   update (two rounds of mu <- max(min(0.2 mu, mu^1.5), tol/10) while err_mu <= 10 mu), each
+ *   update resetting the instance's filter.  d_active / d_status (0 optimal, 1 acceptable) /
+ *   d_acc are updated in place; d_d_inf, d_err0, d_base (max(|dual|/s_d, |c|)), the new mu and
+ *   filter go to the *_out buffers.  nw <= 128.
+ * cpl_ipm_max_step: the fraction-to-the-boundary step: primal (d_v2 = NULL) against the bounds
+ *   d_lo (where d_hasL) / d_up (where d_hasU), or dual (multipliers d_v on d_hasL, d_v2 on d_hasU,
+ *   kept positive); alpha <= 1 per instance, tau per instance.
+ */
+int32_t cpl_ipm_optimality(int64_t batch, int32_t nw, int32_t m, int32_t nfilt, int32_t nbounds, double tol,
+                           double acc_tol, int32_t acc_iter, const double* d_A, const double* d_gw, const double* d_c,
+                           const double* d_w, const double* d_y, const double* d_zL, const double* d_zU,
+                           const uint8_t* d_hasL, const uint8_t* d_hasU, const double* d_wl0, const double* d_wu0,
+                           const double* d_mu, const double* d_filt_t, const double* d_filt_p,
+                           const int64_t* d_fcount, uint8_t* d_active, int64_t* d_status, int64_t* d_acc,
+                           double* d_d_inf, double* d_err0, double* d_base, double* d_mu_out, double* d_filt_t_out,
+                           double* d_filt_p_out, int64_t* d_fcount_out, void* stream);
+int32_t cpl_ipm_max_step(int64_t batch, int32_t nw, const double* d_v, const double* d_dir, const double* d_v2,
+                         const double* d_dir2, const uint8_t* d_hasL, const uint8_t* d_hasU, const double* d_lo,
+                         const double* d_up, const double* d_tau, double* d_out, void* stream);
 
 #ifdef __cplusplus
 }
