@@ -474,35 +474,52 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                 return out
             return torch.minimum(max_step(w, d, hasL, wl0, tau), max_step(-w, -d, hasU, -wu0, tau))
 
-        dl = torch.where(hasL, w - wl0, torch.ones_like(w))
-        du = torch.where(hasU, wu0 - w, torch.ones_like(w))
-        Sig = torch.where(hasL, zL / dl, torch.zeros_like(w)) + torch.where(hasU, zU / du, torch.zeros_like(w))
-        gphi = gradw - torch.where(hasL, mu[:, None] / dl, torch.zeros_like(w)) + \
-            torch.where(hasU, mu[:, None] / du, torch.zeros_like(w))
-        r1 = -(gphi + (A.transpose(1, 2) @ y.unsqueeze(2)).squeeze(2))
-        r2 = -c
-        M = torch.diag_embed(Sig)
-        M[:, :nf, :nf] += S["Hq"] if use_bfgs else fd_hessian(unpack(w), y)
-        dw, dy, delta_w, solve_primal = kkt(M, A, r1, r2, mu, S["dwl"], active)
-        dwl = torch.where(active, delta_w, S["dwl"])
-        dzL = torch.where(hasL, mu[:, None] / dl - zL - zL / dl * dw, torch.zeros_like(w))
-        dzU = torch.where(hasU, mu[:, None] / du - zU + zU / du * dw, torch.zeros_like(w))
-        a_max = primal_step(dw)
-        if use_hip:
-            a_z = torch.empty(B, dtype=dt, device=dev)
-            _abi.check(_abi.lib.cpl_ipm_max_step(B, nw, _ptr(zL), _ptr(dzL.contiguous()), _ptr(zU), _ptr(dzU.contiguous()),
-                                                 _ptr(hasL_u8), _ptr(hasU_u8), None, None, _ptr(tau), _ptr(a_z),
-                                                 stream()))
+        Hblk = S["Hq"] if use_bfgs else fd_hessian(unpack(w), y)
+        if use_hip:  # Newton system: one fused launch (csrc/cpl_ipm.hip)
+            M = torch.empty(B, nw, nw, dtype=dt, device=dev)
+            r1, gphi, mr_diag = (torch.empty(B, nw, dtype=dt, device=dev) for _ in range(3))
+            r2 = torch.empty(B, m, dtype=dt, device=dev)
+            theta_k, phi_k = torch.empty(B, dtype=dt, device=dev), torch.empty(B, dtype=dt, device=dev)
+            _abi.check(_abi.lib.cpl_ipm_newton_setup(
+                B, nw, m, nf, _ptr(w), _ptr(zL), _ptr(zU), _ptr(gradw), _ptr(A), _ptr(y), _ptr(c),
+                _ptr(cur["f"]), _ptr(mu), _ptr(hasL_u8), _ptr(hasU_u8), _ptr(wl0), _ptr(wu0), _ptr(Hblk.contiguous()),
+                _ptr(M), _ptr(r1), _ptr(r2), _ptr(gphi), _ptr(mr_diag), _ptr(theta_k), _ptr(phi_k), stream()))
         else:
+            dl = torch.where(hasL, w - wl0, torch.ones_like(w))
+            du = torch.where(hasU, wu0 - w, torch.ones_like(w))
+            Sig = torch.where(hasL, zL / dl, torch.zeros_like(w)) + torch.where(hasU, zU / du, torch.zeros_like(w))
+            gphi = gradw - torch.where(hasL, mu[:, None] / dl, torch.zeros_like(w)) + \
+                torch.where(hasU, mu[:, None] / du, torch.zeros_like(w))
+            r1 = -(gphi + (A.transpose(1, 2) @ y.unsqueeze(2)).squeeze(2))
+            r2 = -c
+            M = torch.diag_embed(Sig)
+            M[:, :nf, :nf] += Hblk
+            mr_diag = Sig + mu.sqrt()[:, None] * torch.clamp(w.abs(), min=1.0) ** -2
+            theta_k = c.abs().sum(1)
+            phi_k = cur["f"] + barrier(w, mu)
+        dw, dy, delta_w, solve_primal = kkt(M, A, r1, r2, mu, S["dwl"], active)
+        if use_hip:  # multiplier steps, fraction-to-boundary steps, gd, switching flag: one launch
+            dzL, dzU = torch.empty_like(w), torch.empty_like(w)
+            a_max, a_z, gd = (torch.empty(B, dtype=dt, device=dev) for _ in range(3))
+            switch_ok = torch.empty(B, dtype=torch.bool, device=dev)
+            _abi.check(_abi.lib.cpl_ipm_post_step(
+                B, nw, _ptr(w), _ptr(dw.contiguous()), _ptr(zL), _ptr(zU), _ptr(gphi), _ptr(mu), _ptr(tau),
+                _ptr(hasL_u8), _ptr(hasU_u8), _ptr(wl0), _ptr(wu0), _ptr(theta_k), _ptr(theta_min), _ptr(active),
+                _ptr(delta_w.contiguous()), _ptr(S["dwl"]), _ptr(dzL), _ptr(dzU), _ptr(a_max), _ptr(a_z), _ptr(gd),
+                _ptr(switch_ok), stream()))
+            dwl = S["dwl"]
+        else:
+            dwl = torch.where(active, delta_w, S["dwl"])
+            dzL = torch.where(hasL, mu[:, None] / dl - zL - zL / dl * dw, torch.zeros_like(w))
+            dzU = torch.where(hasU, mu[:, None] / du - zU + zU / du * dw, torch.zeros_like(w))
+            a_max = primal_step(dw)
             a_z = torch.minimum(max_step(zL, dzL, hasL, 0.0, tau), max_step(zU, dzU, hasU, 0.0, tau))
+            gd = (gphi * dw).sum(1)
+            switch_ok = (theta_k <= theta_min) & (gd < 0)
 
         # ---- filter line search (IPOPT: gamma_theta 1e-5, gamma_phi 1e-8, delta 1, s_theta 1.1,
         # s_phi 2.3, eta_phi 1e-8, theta_min/max = 1e-4/1e4 max(1, theta_0)), second-order
         # corrections on the first trial; fixed trip counts, masked acceptance
-        theta_k = c.abs().sum(1)
-        phi_k = cur["f"] + barrier(w, mu)
-        gd = (gphi * dw).sum(1)
-        switch_ok = (theta_k <= theta_min) & (gd < 0)
         # line-search state (fresh tensors: the device path updates them in place)
         st = {"searching": active.clone(), "f": cur["f"].clone(), "g": cur["g"].clone(), "w": w.clone(),
               "alpha": zeros_B.clone(), "aug": torch.zeros(B, dtype=torch.bool, device=dev)}
@@ -540,8 +557,9 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                                                         stream()))
                 return wt_, evaluate_fg(Xt)
 
-            def judge_take(wt_, o_, al, extra=None):
-                """IPOPT's acceptance test + take for searching (& extra) instances; (ok, theta)."""
+            def judge_take(wt_, o_, al, extra=None, mode=0):
+                """IPOPT's acceptance test + take for searching (& extra) instances; (ok, theta).
+                mode 1: the feasibility step's test; mode 2: take unconditionally."""
                 th_ = torch.empty(B, dtype=dt, device=dev)
                 ok_ = torch.empty(B, dtype=torch.bool, device=dev)
                 _abi.check(_abi.lib.cpl_ipm_judge_take(
@@ -550,7 +568,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                     _ptr(mu.contiguous()), _ptr(theta_k.contiguous()), _ptr(phi_k.contiguous()), _ptr(gd.contiguous()),
                     _ptr(sw_ok), _ptr(theta_max), _ptr(ftc), _ptr(fpc), None if extra is None else _ptr(extra.contiguous()),
                     _ptr(st["searching"]), _ptr(st["f"]), _ptr(st["g"]), _ptr(st["w"]), _ptr(st["alpha"]),
-                    _ptr(st["aug"]), _ptr(th_), _ptr(ok_), stream()))
+                    _ptr(st["aug"]), _ptr(th_), _ptr(ok_), mode, stream()))
                 return ok_, th_
         else:
             def trial(d, al, mask):
@@ -587,14 +605,35 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         # violation by 10 %; the multipliers stay.  Otherwise the last trial.  Either way the
         # instance's filter restarts.  (The KKT kernel skips the instances outside the mask.)
         failed = st["searching"].clone()
-        Mr = torch.diag_embed(Sig + mu.sqrt()[:, None] * torch.clamp(w.abs(), min=1.0) ** -2)
-        dwr = kkt(Mr, A, torch.zeros_like(w), -c, mu, zeros_B, failed)[0]
+        dwr = kkt(torch.diag_embed(mr_diag), A, torch.zeros_like(w), -c, mu, zeros_B, failed)[0]
         ar = primal_step(dwr)
         wr, orr = trial(dwr, ar, failed)
-        thr = cons(orr["g"], wr[:, nf:]).abs().sum(1)
-        rest = failed & torch.isfinite(thr) & torch.isfinite(orr["f"]) & (thr <= 0.9 * theta_k)
-        take(rest, wr, orr, zeros_B, torch.zeros_like(failed))
-        take(st["searching"], wt, o, 2.0 * alpha, torch.zeros_like(failed))
+        if use_hip:
+            ok_r, _ = judge_take(wr, orr, zeros_B, failed, mode=1)
+            rest = failed & ok_r
+            judge_take(wt, o, 2.0 * alpha, None, mode=2)
+        else:
+            thr = cons(orr["g"], wr[:, nf:]).abs().sum(1)
+            rest = failed & torch.isfinite(thr) & torch.isfinite(orr["f"]) & (thr <= 0.9 * theta_k)
+            take(rest, wr, orr, zeros_B, torch.zeros_like(failed))
+            take(st["searching"], wt, o, 2.0 * alpha, torch.zeros_like(failed))
+        w_new = st["w"]
+        al = st["alpha"]
+        # the accepted points with their derivatives: one full evaluation (trials carried f and g only)
+        new = evaluate(unpack(w_new))
+        if use_hip and not use_bfgs:  # accept + state write-back: one launch, plus masked row copies
+            _abi.check(_abi.lib.cpl_ipm_accept(
+                B, nw, m, FMAX, _ptr(active), _ptr(st["aug"]), _ptr(failed), _ptr(rest), _ptr(al), _ptr(a_z),
+                _ptr(theta_k), _ptr(phi_k), _ptr(ft), _ptr(fp), _ptr(fc), _ptr(w_new), _ptr(dy.contiguous()),
+                _ptr(dzL), _ptr(dzU), _ptr(mu), _ptr(hasL_u8), _ptr(hasU_u8), _ptr(wl0), _ptr(wu0), _ptr(S["w"]),
+                _ptr(S["y"]), _ptr(S["zL"]), _ptr(S["zU"]), _ptr(S["mu"]), _ptr(S["iters"]), _ptr(S["filt_t"]),
+                _ptr(S["filt_p"]), _ptr(S["fcount"]), stream()))
+            for k in ("f", "grad", "g", "J"):
+                _abi.check(_abi.lib.cpl_ipm_masked_rows(B, S[k].numel() // B, _ptr(active), _ptr(new[k].contiguous()),
+                                                        _ptr(S[k]), stream()))
+            if verbose > 1:
+                verbose_line(E, mu, a_max, al, dw, dy, delta_w, cur)
+            return
         a_z = torch.where(rest, zeros_B, a_z)
         addm = st["aug"] & active
         fi = fslot == torch.remainder(fc, FMAX)[:, None]
@@ -602,10 +641,6 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         fp = torch.where(addm[:, None] & fi, (phi_k - 1e-8 * theta_k)[:, None], fp)
         fc = fc + addm.to(fc.dtype)
         ft, fp, fc = reset_filter(failed, ft, fp, fc)
-        w_new = st["w"]
-        al = st["alpha"]
-        # the accepted points with their derivatives: one full evaluation (trials carried f and g only)
-        new = evaluate(unpack(w_new))
 
         # ---- accept: primal, multipliers, bound multipliers (kappa_Sigma safeguard)
         act = active[:, None]
@@ -656,11 +691,14 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         for k in ("f", "grad", "g", "J"):
             S[k].copy_(torch.where(active.view(-1, *([1] * (S[k].dim() - 1))), new[k], S[k]))
         if verbose > 1:
-            b = int(verbose) - 2
-            print(f"   [{b}] mu={float(mu[b]):.2e} err0={float(E['err0'][b]):.2e} a_max={float(a_max[b]):.2e} "
-                  f"alpha={float(al[b]):.2e} dw={float(dw[b].abs().max()):.2e} dy={float(dy[b].abs().max()):.2e} "
-                  f"dW={float(delta_w[b]):.1e} f={float(cur['f'][b]):.6e} d_inf={float(E['d_inf'][b]):.2e} "
-                  f"c_inf={float(E['base'][b]):.2e} argdw={int(dw[b].abs().argmax())}")
+            verbose_line(E, mu, a_max, al, dw, dy, delta_w, cur)
+
+    def verbose_line(E, mu, a_max, al, dw, dy, delta_w, cur):
+        b = int(verbose) - 2
+        print(f"   [{b}] mu={float(mu[b]):.2e} err0={float(E['err0'][b]):.2e} a_max={float(a_max[b]):.2e} "
+              f"alpha={float(al[b]):.2e} dw={float(dw[b].abs().max()):.2e} dy={float(dy[b].abs().max()):.2e} "
+              f"dW={float(delta_w[b]):.1e} f={float(cur['f'][b]):.6e} d_inf={float(E['d_inf'][b]):.2e} "
+              f"c_inf={float(E['base'][b]):.2e} argdw={int(dw[b].abs().argmax())}")
 
     # ---- drive the iterations
     it_run = 0

@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_judge_take_kernel(
     const double* __restrict__ filt_t, const double* __restrict__ filt_p, const uint8_t* __restrict__ extra_mask,
     uint8_t* __restrict__ searching, double* __restrict__ st_f, double* __restrict__ st_g, double* __restrict__ st_w,
     double* __restrict__ st_alpha, uint8_t* __restrict__ st_aug, double* __restrict__ th_out,
-    uint8_t* __restrict__ ok_out) {
+    uint8_t* __restrict__ ok_out, int mode) {
   const int64_t b = (int64_t)blockIdx.x * IPM_WAVES + (threadIdx.x >> 6);
   if (b >= batch) return;
   const int lane = threadIdx.x & 63;
@@ -87,7 +87,11 @@ __global__ __launch_bounds__(256) void cpl_ipm_judge_take_kernel(
   const bool ftype = switch_ok[b] && (al * pow(fmax(-g, 0.0), 2.3) > pow(tk, 1.1));
   const bool armijo = ph <= pk + 1e-8 * al * g;
   const bool suff = (th <= (1.0 - 1e-5) * tk) || (ph <= pk - 1e-8 * tk);
-  const bool ok = fin && th <= theta_max[b] && in_filter && (ftype ? armijo : suff);
+  // mode 0: the filter test; 1: the feasibility (restoration stand-in) step, taken when it cuts
+  // theta by 10 %; 2: unconditional (the last trial of a failed search)
+  const bool ok = mode == 0 ? (fin && th <= theta_max[b] && in_filter && (ftype ? armijo : suff))
+                : mode == 1 ? (isfinite(th) && isfinite(f_t[b]) && th <= 0.9 * tk)
+                            : true;
   const bool take = ok && searching[b] && (extra_mask == nullptr || extra_mask[b]);
   if (take) {
     for (int r = lane; r < m; r += 64) st_g[b * m + r] = gb[r];
@@ -99,7 +103,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_judge_take_kernel(
     if (take) {
       st_f[b] = f_t[b];
       st_alpha[b] = al;
-      st_aug[b] = (ftype && armijo) ? 0 : 1;
+      st_aug[b] = (mode == 0 && !(ftype && armijo)) ? 1 : 0;
       searching[b] = 0;
     }
   }
@@ -247,6 +251,188 @@ __global__ __launch_bounds__(256) void cpl_ipm_max_step_kernel(int64_t batch, in
   if (lane == 0) out[b] = fmin(r, 1.0);
 }
 
+// The Newton system's right-hand side and matrix (batch_ipm.py step, "setup"):
+//   Sigma = zL/(w - wl) + zU/(wu - w), grad_phi = grad_w - mu/(w - wl) + mu/(wu - w),
+//   r1 = -(grad_phi + A^T y), r2 = -c, M = diag(Sigma) + [H 0; 0 0] (H: nf x nf, may be NULL),
+//   theta = sum |c|, phi = f - mu (sum log(w - wl) + sum log(wu - w)),
+//   Mr_diag = Sigma + sqrt(mu) / max(1, |w|)^2 (the feasibility step's diagonal).
+__global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
+    int64_t batch, int nw, int m, int nf, const double* __restrict__ w, const double* __restrict__ zL,
+    const double* __restrict__ zU, const double* __restrict__ gw, const double* __restrict__ A,
+    const double* __restrict__ y, const double* __restrict__ c, const double* __restrict__ f,
+    const double* __restrict__ mu, const uint8_t* __restrict__ hasL, const uint8_t* __restrict__ hasU,
+    const double* __restrict__ wl0, const double* __restrict__ wu0, const double* __restrict__ H,
+    double* __restrict__ M, double* __restrict__ r1, double* __restrict__ r2, double* __restrict__ gphi,
+    double* __restrict__ mr_diag, double* __restrict__ theta, double* __restrict__ phi) {
+  const int64_t b = (int64_t)blockIdx.x * IPM_WAVES + (threadIdx.x >> 6);
+  if (b >= batch) return;
+  const int lane = threadIdx.x & 63;
+  const double mub = mu[b];
+  const double* Ab = A + b * (int64_t)m * nw;
+  const double* yb = y + b * m;
+  double* Mb = M + b * (int64_t)nw * nw;
+  double lg = 0.0;
+  for (int k = lane; k < nw; k += 64) {
+    const double wk = w[b * nw + k];
+    double sig = 0.0, gp = gw[b * nw + k];
+    if (hasL[k]) {
+      const double dl = wk - wl0[k];
+      sig += zL[b * nw + k] / dl;
+      gp -= mub / dl;
+      lg += log(dl);
+    }
+    if (hasU[k]) {
+      const double du = wu0[k] - wk;
+      sig += zU[b * nw + k] / du;
+      gp += mub / du;
+      lg += log(du);
+    }
+    double aty = 0.0;
+    for (int r = 0; r < m; ++r) aty += Ab[r * nw + k] * yb[r];
+    gphi[b * nw + k] = gp;
+    r1[b * nw + k] = -(gp + aty);
+    const double aw = fmax(fabs(wk), 1.0);
+    mr_diag[b * nw + k] = sig + sqrt(mub) / (aw * aw);
+    // row k of M: Sigma_k on the diagonal plus row k of H for k < nf
+    for (int j = 0; j < nw; ++j) {
+      double v = (j == k) ? sig : 0.0;
+      if (H && k < nf && j < nf) v += H[b * (int64_t)nf * nf + k * nf + j];
+      Mb[k * nw + j] = v;
+    }
+  }
+  double th = 0.0;
+  for (int r = lane; r < m; r += 64) {
+    const double cr = c[b * m + r];
+    r2[b * m + r] = -cr;
+    th += fabs(cr);
+  }
+  th = ipm_wave_sum(th);
+  lg = ipm_wave_sum(lg);
+  if (lane == 0) {
+    theta[b] = th;
+    phi[b] = f[b] - mub * lg;
+  }
+}
+
+// After the Newton step (batch_ipm.py step): bound-multiplier steps dzL = mu/dl - zL - zL/dl dw,
+// dzU = mu/du - zU + zU/du dw, their fraction-to-the-boundary step a_z, the primal one a_max,
+// gd = grad_phi . dw, switch_ok = theta <= theta_min & gd < 0, and delta_w_last <- delta_w on the
+// active instances.
+__global__ __launch_bounds__(256) void cpl_ipm_post_step_kernel(
+    int64_t batch, int nw, const double* __restrict__ w, const double* __restrict__ dw, const double* __restrict__ zL,
+    const double* __restrict__ zU, const double* __restrict__ gphi, const double* __restrict__ mu,
+    const double* __restrict__ tau, const uint8_t* __restrict__ hasL, const uint8_t* __restrict__ hasU,
+    const double* __restrict__ wl0, const double* __restrict__ wu0, const double* __restrict__ theta,
+    const double* __restrict__ theta_min, const uint8_t* __restrict__ active, const double* __restrict__ delta_w,
+    double* __restrict__ dwl, double* __restrict__ dzL, double* __restrict__ dzU, double* __restrict__ a_max,
+    double* __restrict__ a_z, double* __restrict__ gd_out, uint8_t* __restrict__ switch_ok) {
+  const int64_t b = (int64_t)blockIdx.x * IPM_WAVES + (threadIdx.x >> 6);
+  if (b >= batch) return;
+  const int lane = threadIdx.x & 63;
+  const double mub = mu[b], t = tau[b];
+  double rp = INFINITY, rz = INFINITY, gd = 0.0;
+  for (int k = lane; k < nw; k += 64) {
+    const double wk = w[b * nw + k], dk = dw[b * nw + k];
+    gd += gphi[b * nw + k] * dk;
+    double dzl = 0.0, dzu = 0.0;
+    if (hasL[k]) {
+      const double dl = wk - wl0[k], zl = zL[b * nw + k];
+      dzl = mub / dl - zl - zl / dl * dk;
+      if (dk < 0.0) rp = fmin(rp, -t * dl / dk);
+      if (dzl < 0.0) rz = fmin(rz, -t * zl / dzl);
+    }
+    if (hasU[k]) {
+      const double du = wu0[k] - wk, zu = zU[b * nw + k];
+      dzu = mub / du - zu + zu / du * dk;
+      if (dk > 0.0) rp = fmin(rp, -t * du / -dk);
+      if (dzu < 0.0) rz = fmin(rz, -t * zu / dzu);
+    }
+    dzL[b * nw + k] = dzl;
+    dzU[b * nw + k] = dzu;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    rp = fmin(rp, __shfl_xor(rp, o));
+    rz = fmin(rz, __shfl_xor(rz, o));
+  }
+  gd = ipm_wave_sum(gd);
+  if (lane == 0) {
+    a_max[b] = fmin(rp, 1.0);
+    a_z[b] = fmin(rz, 1.0);
+    gd_out[b] = gd;
+    switch_ok[b] = (theta[b] <= theta_min[b] && gd < 0.0) ? 1 : 0;
+    if (active[b]) dwl[b] = delta_w[b];
+  }
+}
+
+// Acceptance (batch_ipm.py step, "accept" + state write-back, in place): filter augmentation after
+// h-type steps (ring slot fcount mod nfilt), filter reset of failed searches, y += alpha dy,
+// z += a_z dz with the kappa_Sigma = 1e10 safeguard at the new point, w <- w_new, mu, iters.
+// a_z is taken as 0 where rest (the feasibility step keeps the multipliers).
+__global__ __launch_bounds__(256) void cpl_ipm_accept_kernel(
+    int64_t batch, int nw, int m, int nfilt, const uint8_t* __restrict__ active, const uint8_t* __restrict__ aug,
+    const uint8_t* __restrict__ failed, const uint8_t* __restrict__ rest, const double* __restrict__ alpha,
+    const double* __restrict__ a_z, const double* __restrict__ theta, const double* __restrict__ phi,
+    const double* __restrict__ filt_t_in, const double* __restrict__ filt_p_in, const int64_t* __restrict__ fcount_in,
+    const double* __restrict__ w_new, const double* __restrict__ dy, const double* __restrict__ dzL,
+    const double* __restrict__ dzU, const double* __restrict__ mu, const uint8_t* __restrict__ hasL,
+    const uint8_t* __restrict__ hasU, const double* __restrict__ wl0, const double* __restrict__ wu0,
+    double* __restrict__ w, double* __restrict__ y, double* __restrict__ zL, double* __restrict__ zU,
+    double* __restrict__ mu_state, int64_t* __restrict__ iters, double* __restrict__ filt_t,
+    double* __restrict__ filt_p, int64_t* __restrict__ fcount) {
+  const int64_t b = (int64_t)blockIdx.x * IPM_WAVES + (threadIdx.x >> 6);
+  if (b >= batch) return;
+  const int lane = threadIdx.x & 63;
+  const bool act = active[b] != 0;
+  const bool addm = act && aug[b];
+  const bool fail = failed[b] != 0;
+  const int64_t fc = fcount_in[b];
+  const int slot = (int)(fc % nfilt);
+  const double tk = theta[b], pk = phi[b];
+  for (int k = lane; k < nfilt; k += 64) {
+    double ft = filt_t_in[b * nfilt + k], fp = filt_p_in[b * nfilt + k];
+    if (addm && k == slot) {
+      ft = (1.0 - 1e-5) * tk;
+      fp = pk - 1e-8 * tk;
+    }
+    if (fail) ft = fp = INFINITY;
+    filt_t[b * nfilt + k] = ft;
+    filt_p[b * nfilt + k] = fp;
+  }
+  const double al = alpha[b], az = rest[b] ? 0.0 : a_z[b], mub = mu[b];
+  for (int r = lane; r < m; r += 64)
+    if (act) y[b * m + r] += al * dy[b * m + r];
+  for (int k = lane; k < nw; k += 64) {
+    const double wn = w_new[b * nw + k];
+    if (act) {
+      if (hasL[k]) {
+        const double dl = wn - wl0[k];
+        zL[b * nw + k] = fmin(fmax(zL[b * nw + k] + az * dzL[b * nw + k], mub / (1e10 * dl)), 1e10 * mub / dl);
+      }
+      if (hasU[k]) {
+        const double du = wu0[k] - wn;
+        zU[b * nw + k] = fmin(fmax(zU[b * nw + k] + az * dzU[b * nw + k], mub / (1e10 * du)), 1e10 * mub / du);
+      }
+      w[b * nw + k] = wn;
+    }
+  }
+  if (lane == 0) {
+    fcount[b] = fail ? 0 : fc + (addm ? 1 : 0);
+    mu_state[b] = mub;
+    if (act) iters[b] += 1;
+  }
+}
+
+// dst[b] = src[b] for the rows with mask[b] (row length len doubles), 16-byte accesses when aligned.
+__global__ __launch_bounds__(256) void cpl_ipm_masked_rows_kernel(int64_t total, int64_t len,
+                                                                  const uint8_t* __restrict__ mask,
+                                                                  const double* __restrict__ src,
+                                                                  double* __restrict__ dst) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  if (mask[e / len]) dst[e] = src[e];
+}
+
 }  // namespace cpl
 
 using namespace cpl;
@@ -280,8 +466,8 @@ int32_t cpl_ipm_judge_take(int64_t batch, int32_t nw, int32_t m, int32_t nf, int
                            const double* d_gd, const uint8_t* d_switch_ok, const double* d_theta_max,
                            const double* d_filt_t, const double* d_filt_p, const uint8_t* d_extra_mask,
                            uint8_t* d_searching, double* d_st_f, double* d_st_g, double* d_st_w, double* d_st_alpha,
-                           uint8_t* d_st_aug, double* d_th_out, uint8_t* d_ok_out, void* stream) {
-  if (batch < 0 || nw <= 0 || m < 0 || nf < 0 || nf > nw || nfilt < 0)
+                           uint8_t* d_st_aug, double* d_th_out, uint8_t* d_ok_out, int32_t mode, void* stream) {
+  if (batch < 0 || nw <= 0 || m < 0 || nf < 0 || nf > nw || nfilt < 0 || mode < 0 || mode > 2)
     return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_judge_take: bad sizes");
   if (batch == 0) return CPL_OK;
   if ((m > 0 && (!d_row_slack || !d_gl || !d_g_t || !d_st_g)) || !d_hasL || !d_hasU || !d_wl0 || !d_wu0 || !d_wt ||
@@ -295,7 +481,7 @@ int32_t cpl_ipm_judge_take(int64_t batch, int32_t nw, int32_t m, int32_t nf, int
                      batch, (int)nw, (int)m, (int)nf, (int)nfilt, d_row_slack, d_gl, d_hasL, d_hasU, d_wl0, d_wu0, d_wt,
                      d_f_t, d_g_t, d_alpha, d_mu, d_theta_k, d_phi_k, d_gd, d_switch_ok, d_theta_max, d_filt_t,
                      d_filt_p, d_extra_mask, d_searching, d_st_f, d_st_g, d_st_w, d_st_alpha, d_st_aug, d_th_out,
-                     d_ok_out);
+                     d_ok_out, (int)mode);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_ipm_judge_take launch: ") + hipGetErrorString(e));
   return CPL_OK;
@@ -340,6 +526,86 @@ int32_t cpl_ipm_max_step(int64_t batch, int32_t nw, const double* d_v, const dou
                      batch, (int)nw, d_v, d_dir, d_v2, d_dir2, d_hasL, d_hasU, d_lo, d_up, d_tau, d_out);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_ipm_max_step launch: ") + hipGetErrorString(e));
+  return CPL_OK;
+}
+
+#define IPM_LAUNCH(kernel, name, ...)                                                                   \
+  do {                                                                                                 \
+    const int64_t blocks_ = (batch + IPM_WAVES - 1) / IPM_WAVES;                                       \
+    if (blocks_ > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, name ": batch too large");       \
+    hipLaunchKernelGGL(kernel, dim3((unsigned)blocks_), dim3(64 * IPM_WAVES), 0, (hipStream_t)stream,   \
+                       __VA_ARGS__);                                                                   \
+    hipError_t e_ = hipGetLastError();                                                                 \
+    if (e_ != hipSuccess) return fail(CPL_ERR_HIP, std::string(name " launch: ") + hipGetErrorString(e_)); \
+    return CPL_OK;                                                                                     \
+  } while (0)
+
+int32_t cpl_ipm_newton_setup(int64_t batch, int32_t nw, int32_t m, int32_t nf, const double* d_w, const double* d_zL,
+                             const double* d_zU, const double* d_gw, const double* d_A, const double* d_y,
+                             const double* d_c, const double* d_f, const double* d_mu, const uint8_t* d_hasL,
+                             const uint8_t* d_hasU, const double* d_wl0, const double* d_wu0, const double* d_H,
+                             double* d_M, double* d_r1, double* d_r2, double* d_gphi, double* d_mr_diag,
+                             double* d_theta, double* d_phi, void* stream) {
+  if (batch < 0 || nw <= 0 || m < 0 || nf < 0 || nf > nw) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_newton_setup: bad sizes");
+  if (batch == 0) return CPL_OK;
+  if (!d_w || !d_zL || !d_zU || !d_gw || (m > 0 && (!d_A || !d_y || !d_c || !d_r2)) || !d_f || !d_mu || !d_hasL ||
+      !d_hasU || !d_wl0 || !d_wu0 || !d_M || !d_r1 || !d_gphi || !d_mr_diag || !d_theta || !d_phi)
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_newton_setup: missing buffer");
+  IPM_LAUNCH(cpl_ipm_newton_setup_kernel, "cpl_ipm_newton_setup", batch, (int)nw, (int)m, (int)nf, d_w, d_zL, d_zU,
+             d_gw, d_A, d_y, d_c, d_f, d_mu, d_hasL, d_hasU, d_wl0, d_wu0, d_H, d_M, d_r1, d_r2, d_gphi, d_mr_diag,
+             d_theta, d_phi);
+}
+
+int32_t cpl_ipm_post_step(int64_t batch, int32_t nw, const double* d_w, const double* d_dw, const double* d_zL,
+                          const double* d_zU, const double* d_gphi, const double* d_mu, const double* d_tau,
+                          const uint8_t* d_hasL, const uint8_t* d_hasU, const double* d_wl0, const double* d_wu0,
+                          const double* d_theta, const double* d_theta_min, const uint8_t* d_active,
+                          const double* d_delta_w, double* d_dwl, double* d_dzL, double* d_dzU, double* d_a_max,
+                          double* d_a_z, double* d_gd, uint8_t* d_switch_ok, void* stream) {
+  if (batch < 0 || nw <= 0) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_post_step: bad sizes");
+  if (batch == 0) return CPL_OK;
+  if (!d_w || !d_dw || !d_zL || !d_zU || !d_gphi || !d_mu || !d_tau || !d_hasL || !d_hasU || !d_wl0 || !d_wu0 ||
+      !d_theta || !d_theta_min || !d_active || !d_delta_w || !d_dwl || !d_dzL || !d_dzU || !d_a_max || !d_a_z ||
+      !d_gd || !d_switch_ok)
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_post_step: missing buffer");
+  IPM_LAUNCH(cpl_ipm_post_step_kernel, "cpl_ipm_post_step", batch, (int)nw, d_w, d_dw, d_zL, d_zU, d_gphi, d_mu, d_tau,
+             d_hasL, d_hasU, d_wl0, d_wu0, d_theta, d_theta_min, d_active, d_delta_w, d_dwl, d_dzL, d_dzU, d_a_max,
+             d_a_z, d_gd, d_switch_ok);
+}
+
+int32_t cpl_ipm_accept(int64_t batch, int32_t nw, int32_t m, int32_t nfilt, const uint8_t* d_active,
+                       const uint8_t* d_aug, const uint8_t* d_failed, const uint8_t* d_rest, const double* d_alpha,
+                       const double* d_a_z, const double* d_theta, const double* d_phi, const double* d_filt_t_in,
+                       const double* d_filt_p_in, const int64_t* d_fcount_in, const double* d_w_new,
+                       const double* d_dy, const double* d_dzL, const double* d_dzU, const double* d_mu,
+                       const uint8_t* d_hasL, const uint8_t* d_hasU, const double* d_wl0, const double* d_wu0,
+                       double* d_w, double* d_y, double* d_zL, double* d_zU, double* d_mu_state, int64_t* d_iters,
+                       double* d_filt_t, double* d_filt_p, int64_t* d_fcount, void* stream) {
+  if (batch < 0 || nw <= 0 || m < 0 || nfilt <= 0) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_accept: bad sizes");
+  if (batch == 0) return CPL_OK;
+  if (!d_active || !d_aug || !d_failed || !d_rest || !d_alpha || !d_a_z || !d_theta || !d_phi || !d_filt_t_in ||
+      !d_filt_p_in || !d_fcount_in || !d_w_new || (m > 0 && (!d_dy || !d_y)) || !d_dzL || !d_dzU || !d_mu ||
+      !d_hasL || !d_hasU || !d_wl0 || !d_wu0 || !d_w || !d_zL || !d_zU || !d_mu_state || !d_iters || !d_filt_t ||
+      !d_filt_p || !d_fcount)
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_accept: missing buffer");
+  IPM_LAUNCH(cpl_ipm_accept_kernel, "cpl_ipm_accept", batch, (int)nw, (int)m, (int)nfilt, d_active, d_aug, d_failed,
+             d_rest, d_alpha, d_a_z, d_theta, d_phi, d_filt_t_in, d_filt_p_in, d_fcount_in, d_w_new, d_dy, d_dzL,
+             d_dzU, d_mu, d_hasL, d_hasU, d_wl0, d_wu0, d_w, d_y, d_zL, d_zU, d_mu_state, d_iters, d_filt_t, d_filt_p,
+             d_fcount);
+}
+
+int32_t cpl_ipm_masked_rows(int64_t batch, int64_t row_len, const uint8_t* d_mask, const double* d_src, double* d_dst,
+                            void* stream) {
+  if (batch < 0 || row_len < 0) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_masked_rows: bad sizes");
+  if (batch == 0 || row_len == 0) return CPL_OK;
+  if (!d_mask || !d_src || !d_dst) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_masked_rows: missing buffer");
+  const int64_t total = batch * row_len;
+  const int64_t blocks = (total + 255) / 256;
+  if (blocks > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_masked_rows: batch too large");
+  hipLaunchKernelGGL(cpl_ipm_masked_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, total,
+                     row_len, d_mask, d_src, d_dst);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_ipm_masked_rows launch: ") + hipGetErrorString(e));
   return CPL_OK;
 }
 

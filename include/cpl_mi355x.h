@@ -245,7 +245,8 @@ int32_t cpl_kkt_solve(int32_t mode, int64_t batch, int32_t nw, int32_t m, const 
  *   objective phi, filter of `nfilt` (theta, phi) entries per instance, switching condition /
  *   Armijo / sufficient decrease, theta_max); instances with searching & extra_mask (NULL: all)
  *   that pass copy (f_t, g_t, w_t, alpha, augment flag) into the line-search state and clear
- *   searching.  d_th_out / d_ok_out get theta and the test result of every instance.
+ *   searching.  d_th_out / d_ok_out get theta and the test result of every instance.  mode 0: the
+ *   filter test; 1: the feasibility step's test (theta cut by 10 %); 2: take unconditionally.
  *   row_slack[r] = slack index of inequality row r, -1 for an equality row.
  */
 int32_t cpl_ipm_trial_point(int64_t batch, int32_t n, int32_t nf, int32_t nw, const int64_t* d_free_idx,
@@ -259,7 +260,7 @@ int32_t cpl_ipm_judge_take(int64_t batch, int32_t nw, int32_t m, int32_t nf, int
                            const double* d_gd, const uint8_t* d_switch_ok, const double* d_theta_max,
                            const double* d_filt_t, const double* d_filt_p, const uint8_t* d_extra_mask,
                            uint8_t* d_searching, double* d_st_f, double* d_st_g, double* d_st_w, double* d_st_alpha,
-                           uint8_t* d_st_aug, double* d_th_out, uint8_t* d_ok_out, void* stream);
+                           uint8_t* d_st_aug, double* d_th_out, uint8_t* d_ok_out, int32_t mode, void* stream);
 /*
  * cpl_ipm_optimality: IPOPT's scaled optimality error (s_max = 100) at the current iterates, the
  *   convergence test (tol; acc_tol for acc_iter consecutive iterations) and the monotone barrier
@@ -282,6 +283,38 @@ int32_t cpl_ipm_optimality(int64_t batch, int32_t nw, int32_t m, int32_t nfilt, 
 int32_t cpl_ipm_max_step(int64_t batch, int32_t nw, const double* d_v, const double* d_dir, const double* d_v2,
                          const double* d_dir2, const uint8_t* d_hasL, const uint8_t* d_hasU, const double* d_lo,
                          const double* d_up, const double* d_tau, double* d_out, void* stream);
+/*
+ * cpl_ipm_newton_setup: Sigma, grad_phi, r1 = -(grad_phi + A^T y), r2 = -c, M = diag(Sigma) + the
+ *   nf x nf Hessian block d_H (NULL: none), theta = |c|_1, the barrier objective phi and the
+ *   feasibility step's diagonal Sigma + sqrt(mu) / max(1, |w|)^2, per instance.
+ * cpl_ipm_post_step: dzL, dzU from the primal step, the primal and dual fraction-to-the-boundary
+ *   steps, gd = grad_phi . dw, the switching-condition flag, delta_w_last on active instances.
+ * cpl_ipm_accept: filter augmentation / reset, y, z (kappa_Sigma safeguard), w, mu and iteration
+ *   counters written back in place.
+ * cpl_ipm_masked_rows: dst[b, :] = src[b, :] where mask[b].
+ */
+int32_t cpl_ipm_newton_setup(int64_t batch, int32_t nw, int32_t m, int32_t nf, const double* d_w, const double* d_zL,
+                             const double* d_zU, const double* d_gw, const double* d_A, const double* d_y,
+                             const double* d_c, const double* d_f, const double* d_mu, const uint8_t* d_hasL,
+                             const uint8_t* d_hasU, const double* d_wl0, const double* d_wu0, const double* d_H,
+                             double* d_M, double* d_r1, double* d_r2, double* d_gphi, double* d_mr_diag,
+                             double* d_theta, double* d_phi, void* stream);
+int32_t cpl_ipm_post_step(int64_t batch, int32_t nw, const double* d_w, const double* d_dw, const double* d_zL,
+                          const double* d_zU, const double* d_gphi, const double* d_mu, const double* d_tau,
+                          const uint8_t* d_hasL, const uint8_t* d_hasU, const double* d_wl0, const double* d_wu0,
+                          const double* d_theta, const double* d_theta_min, const uint8_t* d_active,
+                          const double* d_delta_w, double* d_dwl, double* d_dzL, double* d_dzU, double* d_a_max,
+                          double* d_a_z, double* d_gd, uint8_t* d_switch_ok, void* stream);
+int32_t cpl_ipm_accept(int64_t batch, int32_t nw, int32_t m, int32_t nfilt, const uint8_t* d_active,
+                       const uint8_t* d_aug, const uint8_t* d_failed, const uint8_t* d_rest, const double* d_alpha,
+                       const double* d_a_z, const double* d_theta, const double* d_phi, const double* d_filt_t_in,
+                       const double* d_filt_p_in, const int64_t* d_fcount_in, const double* d_w_new,
+                       const double* d_dy, const double* d_dzL, const double* d_dzU, const double* d_mu,
+                       const uint8_t* d_hasL, const uint8_t* d_hasU, const double* d_wl0, const double* d_wu0,
+                       double* d_w, double* d_y, double* d_zL, double* d_zU, double* d_mu_state, int64_t* d_iters,
+                       double* d_filt_t, double* d_filt_p, int64_t* d_fcount, void* stream);
+int32_t cpl_ipm_masked_rows(int64_t batch, int64_t row_len, const uint8_t* d_mask, const double* d_src, double* d_dst,
+                            void* stream);
 
 #ifdef __cplusplus
 }
