@@ -271,6 +271,8 @@ __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
   const double* Ab = A + b * (int64_t)m * nw;
   const double* yb = y + b * m;
   double* Mb = M + b * (int64_t)nw * nw;
+  __shared__ double sig_s[IPM_WAVES][128];
+  double* sg = sig_s[threadIdx.x >> 6];
   double lg = 0.0;
   for (int k = lane; k < nw; k += 64) {
     const double wk = w[b * nw + k];
@@ -293,12 +295,18 @@ __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
     r1[b * nw + k] = -(gp + aty);
     const double aw = fmax(fabs(wk), 1.0);
     mr_diag[b * nw + k] = sig + sqrt(mub) / (aw * aw);
-    // row k of M: Sigma_k on the diagonal plus row k of H for k < nf
-    for (int j = 0; j < nw; ++j) {
-      double v = (j == k) ? sig : 0.0;
-      if (H && k < nf && j < nf) v += H[b * (int64_t)nf * nf + k * nf + j];
-      Mb[k * nw + j] = v;
-    }
+    sg[k] = sig;
+  }
+  // M = diag(Sigma) + [H 0; 0 0], written row by row with the lanes along the row (coalesced);
+  // the wave's own LDS row of Sigma needs no workgroup barrier, only the wave's LDS ordering
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS stores have landed
+  __builtin_amdgcn_wave_barrier();
+  const double* Hb = H ? H + b * (int64_t)nf * nf : nullptr;
+  for (int e = lane; e < nw * nw; e += 64) {
+    const int k = e / nw, j = e - k * nw;
+    double v = (j == k) ? sg[k] : 0.0;
+    if (Hb && k < nf && j < nf) v += Hb[k * nf + j];
+    Mb[e] = v;
   }
   double th = 0.0;
   for (int r = lane; r < m; r += 64) {
