@@ -27,6 +27,19 @@
 
 namespace cpl {
 
+// Phase timestamps for scripts/kkt_probe.hip (compiled with -DCPL_KKT_PROFILE only).
+#ifdef CPL_KKT_PROFILE
+__device__ long long* g_kkt_prof;
+#define KKT_MARK(i)                                                            \
+  do {                                                                         \
+    if (threadIdx.x == 0) g_kkt_prof[(int64_t)blockIdx.x * 8 + (i)] = clock64(); \
+  } while (0)
+#else
+#define KKT_MARK(i) \
+  do {              \
+  } while (0)
+#endif
+
 constexpr int KKT_THREADS = 256;
 constexpr int KKT_MAX_NW = 128;
 
@@ -115,8 +128,9 @@ __device__ __forceinline__ void group_dots(int n, int len, const double* A, int 
       const double* a = A + (int64_t)r * sr;
       int k = part;
       for (; k + G < len; k += 2 * G) {
-        s0 += a[k * sk] * x[k * sx];
-        s1 += a[(k + G) * sk] * x[(k + G) * sx];
+        const double p0 = a[k * sk], p1 = a[(k + G) * sk];
+        s0 += p0 * x[k * sx];
+        s1 += p1 * x[(k + G) * sx];
       }
       if (k < len) s0 += a[k * sk] * x[k * sx];
     }
@@ -144,10 +158,13 @@ __device__ void wave_trsv(int n, bool lower, const double* Tm, int si, int sk, c
   const int r0 = lane, r1 = lane + 64;
   double a0 = r0 < n ? x[r0] : 0.0;
   double a1 = r1 < n ? x[r1] : 0.0;
+  // reciprocal diagonal of the lane's rows, computed in parallel ahead of the sequential sweep
+  const double v0 = r0 < n ? 1.0 / D[r0 * sd] : 0.0;
+  const double v1 = r1 < n ? 1.0 / D[r1 * sd] : 0.0;
   for (int t = 0; t < n; ++t) {
     const int i = lower ? t : n - 1 - t;
     const double ai = i < 64 ? wave_bcast(a0, i) : wave_bcast(a1, i - 64);
-    const double xi = ai / D[i * sd];
+    const double xi = ai * (i < 64 ? wave_bcast(v0, i) : wave_bcast(v1, i - 64));
     if (r0 == i) a0 = xi;
     if (r1 == i) a1 = xi;
     if (lower) {
@@ -214,10 +231,12 @@ __host__ __device__ inline int64_t kkt_ws_per(int nw, int m) {
   return (int64_t)nw * nw + (int64_t)m * nw + m + (int64_t)nz * nz + 4;
 }
 
-// LDS layout (doubles): Q | QR | Rd | L | M | q1 | q2 | dw | dy | e1 | e2 | tmp(2 nw)
+// LDS layout (doubles): Q | QR | Rd | L | q1 | q2 | dw | dy | e1 | e2 | tmp(3 nw).  M stays in global
+// memory (L2-resident while its workgroup runs; read by the matrix-vector products and M Z): the
+// image is 35 KiB at nw = 47, m = 30, four workgroups per CU instead of three.
 __host__ __device__ inline int kkt_lds_doubles(int nw, int m) {
   const int nz = nw - m;
-  return nw * nw + m * nw + m + nz * nz + nw * nw + 5 * nw + 2 * m + 2 * nw;
+  return nw * nw + m * nw + m + nz * nz + 5 * nw + 2 * m + 2 * nw;
 }
 
 __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
@@ -236,8 +255,7 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
   double* QR = Q + nw * nw;
   double* Rd = QR + m * nw;
   double* L = Rd + m;
-  double* M = L + nz * nz;
-  double* q1 = M + nw * nw;
+  double* q1 = L + nz * nz;
   double* q2 = q1 + nw;
   double* dw = q2 + m;
   double* dy = dw + nw;
@@ -245,6 +263,7 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
   double* e2 = e1 + nw;
   double* tmp = e2 + nw;  // 3 nw
   const double* Mb = Mg + b * nw * nw;
+  const double* M = Mb;  // global
   const double* Ab = Ag + b * m * nw;
   double* wsb = ws + b * kkt_ws_per(nw, m);
 
@@ -254,7 +273,6 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
     if (tid == 0 && mode == 0) { dWg[b] = 0.0; dCg[b] = 0.0; info[b] = 0; }
     return;
   }
-  for (int i = tid; i < nw * nw; i += blockDim.x) M[i] = Mb[i];
   for (int i = tid; i < nw; i += blockDim.x) q1[i] = r1g[b * nw + i];
   for (int i = tid; i < m; i += blockDim.x) q2[i] = r2g[b * m + i];
 
@@ -272,48 +290,71 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
   // ---- Householder QR of A^T: row j of QR = column j of A^T
   for (int i = tid; i < m * nw; i += blockDim.x) QR[i] = Ab[i];
   __syncthreads();
-  double* beta = tmp;  // [m]
-  for (int j = 0; j < m; ++j) {
-    double* x = QR + j * nw;  // column j of A^T, rows j..nw-1 active
-    if (tid < 64) {  // |x[j+1:]|^2 by wave 0 (two elements per lane + xor reduction)
-      const int i0 = j + 1 + tid, i1 = i0 + 64;
-      double sq = (i0 < nw ? x[i0] * x[i0] : 0.0) + (i1 < nw ? x[i1] * x[i1] : 0.0);
-      sq = wave_sum(sq);
-      if (tid == 0) tmp[2 * m] = sq;
+  KKT_MARK(0);
+  // Per column j: wave 0 forms the reflector (v in place, v_j = 1 implicit; beta_j; R_jj), all
+  // waves take the dots v^T y of the later columns (8 lanes per column), then the update: wave 0
+  // updates column j+1 and goes straight on to its reflector, the other waves update the rest —
+  // two workgroup barriers per column.
+  double* beta = tmp;          // [m]
+  double* sdot = tmp + 2 * m;  // [m] (tmp holds 3 nw >= 3 m doubles)
+  const int wid = tid >> 6, lane = tid & 63;
+  const int nwaves = blockDim.x >> 6;
+  auto house = [&](int j) {
+    double* x = QR + j * nw;
+    const int i0 = j + 1 + lane, i1 = i0 + 64;
+    const double x0 = i0 < nw ? x[i0] : 0.0, x1 = i1 < nw ? x[i1] : 0.0;
+    const double sig = wave_sum(x0 * x0 + x1 * x1);
+    const double alpha = x[j];
+    if (sig == 0.0) {
+      if (lane == 0) { beta[j] = 0.0; Rd[j] = alpha; }
+    } else {
+      const double nrm = sqrt(alpha * alpha + sig);
+      const double v0 = alpha <= 0.0 ? alpha - nrm : -sig / (alpha + nrm);
+      const double rv0 = 1.0 / v0;
+      if (i0 < nw) x[i0] = x0 * rv0;
+      if (i1 < nw) x[i1] = x1 * rv0;
+      if (lane == 0) { beta[j] = 2.0 * v0 * v0 / (sig + v0 * v0); Rd[j] = nrm; }
     }
-    if (tid == 0) {
-      const double sig = tmp[2 * m];
-      const double alpha = x[j];
-      if (sig == 0.0) {
-        beta[j] = 0.0;
-        Rd[j] = alpha;
-      } else {
-        const double nrm = sqrt(alpha * alpha + sig);
-        const double v0 = alpha <= 0.0 ? alpha - nrm : -sig / (alpha + nrm);
-        beta[j] = 2.0 * v0 * v0 / (sig + v0 * v0);
-        Rd[j] = nrm;
-        tmp[m + j] = 1.0 / v0;
-      }
-    }
-    __syncthreads();
+  };
+  if (m > 0 && wid == 0) house(0);
+  __syncthreads();
+  for (int j = 0; j + 1 < m; ++j) {
     const double bj = beta[j];
-    if (bj != 0.0) {
-      const double rv0 = tmp[m + j];
-      for (int i = j + 1 + tid; i < nw; i += blockDim.x) x[i] *= rv0;  // v (v_j = 1 implicit)
-      __syncthreads();
-      // H_j on the columns k > j: y <- y - beta v (v^T y); the dots one thread per column
-      double* sdot = tmp + 2 * m;  // [m] (tmp holds 3 nw >= 3 m doubles)
-      group_dots<8>(m - j - 1, nw - j - 1, QR + (j + 1) * nw + j + 1, nw, 1, x + j + 1, 1,
-                    [&](int kk, double d) { sdot[j + 1 + kk] = (QR[(j + 1 + kk) * nw + j] + d) * bj; });
-      __syncthreads();
-      const int L = nw - j;
-      for (int e = tid; e < (m - j - 1) * L; e += blockDim.x) {
-        const int k = j + 1 + e / L, i = j + e % L;
-        QR[k * nw + i] -= sdot[k] * (i == j ? 1.0 : x[i]);
+    const double* x = QR + j * nw;
+    group_dots<8>(m - j - 1, nw - j - 1, QR + (j + 1) * nw + j + 1, nw, 1, x + j + 1, 1,
+                  [&](int kk, double d) { sdot[j + 1 + kk] = (QR[(j + 1 + kk) * nw + j] + d) * bj; });
+    __syncthreads();
+    if (wid == 0) {
+      double* y = QR + (j + 1) * nw;
+      const double sk = sdot[j + 1];
+      for (int i = j + lane; i < nw; i += 64) y[i] -= sk * (i == j ? 1.0 : x[i]);
+      house(j + 1);
+    } else {
+      // rows i0 = j + lane, i1 = i0 + 64 of every later column; four columns per round, loads first
+      const int i0 = j + lane, i1 = i0 + 64;
+      const double xa = i0 < nw ? (i0 == j ? 1.0 : x[i0]) : 0.0;
+      const double xb = i1 < nw ? x[i1] : 0.0;
+      const int ks = nwaves - 1;
+      for (int k = j + 1 + wid; k < m; k += 4 * ks) {
+        double ya[4], yb[4], sk[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int kk = k + u * ks;
+          ya[u] = (kk < m && i0 < nw) ? QR[kk * nw + i0] : 0.0;
+          yb[u] = (kk < m && i1 < nw) ? QR[kk * nw + i1] : 0.0;
+          sk[u] = kk < m ? sdot[kk] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int kk = k + u * ks;
+          if (kk < m && i0 < nw) QR[kk * nw + i0] = ya[u] - sk[u] * xa;
+          if (kk < m && i1 < nw) QR[kk * nw + i1] = yb[u] - sk[u] * xb;
+        }
       }
     }
     __syncthreads();
   }
+  KKT_MARK(1);
   // ---- Q = H_0 ... H_{m-1} I (backward accumulation), one thread per column
   for (int i = tid; i < nw * nw; i += blockDim.x) Q[i] = (i / nw == i % nw) ? 1.0 : 0.0;
   __syncthreads();
@@ -327,22 +368,40 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
       for (int base = 0; base < nw * 4; base += blockDim.x) {
         const int c = (base + tid) >> 2;
         const bool act = c < nw;
-        double s = 0.0;
+        double s = 0.0, s1 = 0.0;
         if (act) {
           if (part == 0) s = Q[j * nw + c];
-          for (int r = j + 1 + part; r < nw; r += 4) s += v[r] * Q[r * nw + c];
+          int r = j + 1 + part;
+          for (; r + 4 < nw; r += 8) {
+            s += v[r] * Q[r * nw + c];
+            s1 += v[r + 4] * Q[(r + 4) * nw + c];
+          }
+          if (r < nw) s += v[r] * Q[r * nw + c];
         }
+        s += s1;
         s += __shfl_xor(s, 1);
         s += __shfl_xor(s, 2);
         s *= bj;
         if (act) {
           if (part == 0) Q[j * nw + c] -= s;
-          for (int r = j + 1 + part; r < nw; r += 4) Q[r * nw + c] -= s * v[r];
+          // load four rows, then store them (the rows are this lane's own: no aliasing between them)
+          int r = j + 1 + part;
+          for (; r + 12 < nw; r += 16) {
+            const double q0 = Q[r * nw + c], q1 = Q[(r + 4) * nw + c], q2 = Q[(r + 8) * nw + c],
+                         q3 = Q[(r + 12) * nw + c];
+            const double w0 = v[r], w1 = v[r + 4], w2 = v[r + 8], w3 = v[r + 12];
+            Q[r * nw + c] = q0 - s * w0;
+            Q[(r + 4) * nw + c] = q1 - s * w1;
+            Q[(r + 8) * nw + c] = q2 - s * w2;
+            Q[(r + 12) * nw + c] = q3 - s * w3;
+          }
+          for (; r < nw; r += 4) Q[r * nw + c] -= s * v[r];
         }
       }
     }
     __syncthreads();
   }
+  KKT_MARK(2);
   // ---- rank deficiency: delta_c on R's diagonal
   if (tid == 0) {
     double rmax = 0.0;
@@ -364,14 +423,67 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
   double* Hr0 = L;  // keep the unshifted reduced Hessian in the workspace slot of L first
   if (nz > 0) {
     double* MZ = ws + b * kkt_ws_per(nw, m);  // global scratch (the workspace; overwritten at the end)
-    for (int e = tid; e < nw * nz; e += blockDim.x) {
-      const int r = e / nz, c = e % nz;
-      MZ[e] = lds_dot(M + r * nw, 1, Q + m + c, nw, nw);
+    // MZ = M Z: a thread per (row r, 4 columns), M[r][k] from global once per k, Z[k][c..c+3] from
+    // LDS (reads past Z's last column land inside the LDS image and are discarded)
+    const int nb = (nz + 3) >> 2;
+    for (int t = tid; t < nw * nb; t += blockDim.x) {
+      const int r = t / nb, cb = (t - r * nb) * 4;
+      const double* mr = M + r * nw;
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+      for (int k0 = 0; k0 < nw; k0 += 8) {  // eight global loads in flight, then the FMAs
+        double mv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) mv[u] = k0 + u < nw ? mr[k0 + u] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (k0 + u < nw) {
+            const double* zk = Q + (k0 + u) * nw + m + cb;
+            a0 += mv[u] * zk[0];
+            a1 += mv[u] * zk[1];
+            a2 += mv[u] * zk[2];
+            a3 += mv[u] * zk[3];
+          }
+        }
+      }
+      double* o = MZ + r * nz + cb;
+      o[0] = a0;
+      if (cb + 1 < nz) o[1] = a1;
+      if (cb + 2 < nz) o[2] = a2;
+      if (cb + 3 < nz) o[3] = a3;
     }
     __syncthreads();
-    for (int e = tid; e < nz * nz; e += blockDim.x) {
-      const int a = e / nz, c = e % nz;
-      Hr0[e] = glb_dot(Q + m + a, nw, MZ + c, nz, nw);
+    // Hr = Z^T (M Z): a thread per (row a, 4 columns), Z[r][a] from LDS, MZ[r][c..c+3] from global
+    for (int t = tid; t < nz * nb; t += blockDim.x) {
+      const int ar = t / nb, cb = (t - ar * nb) * 4;
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+      const int w1 = cb + 1 < nz, w2 = cb + 2 < nz, w3 = cb + 3 < nz;
+      for (int r0 = 0; r0 < nw; r0 += 2) {  // eight global loads in flight, then the FMAs
+        double mz[2][4];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const double* p = MZ + (r0 + u) * nz + cb;
+          const bool ok = r0 + u < nw;
+          mz[u][0] = ok ? p[0] : 0.0;
+          mz[u][1] = ok && w1 ? p[1] : 0.0;
+          mz[u][2] = ok && w2 ? p[2] : 0.0;
+          mz[u][3] = ok && w3 ? p[3] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          if (r0 + u < nw) {
+            const double zv = Q[(r0 + u) * nw + m + ar];
+            a0 += zv * mz[u][0];
+            a1 += zv * mz[u][1];
+            a2 += zv * mz[u][2];
+            a3 += zv * mz[u][3];
+          }
+        }
+      }
+      double* o = Hr0 + ar * nz + cb;
+      o[0] = a0;
+      if (cb + 1 < nz) o[1] = a1;
+      if (cb + 2 < nz) o[2] = a2;
+      if (cb + 3 < nz) o[3] = a3;
     }
     __syncthreads();
     // symmetrise, keep a copy in dw.. region (nz*nz may exceed it: use the global scratch again)
@@ -381,6 +493,7 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
       Hsave[e] = 0.5 * (Hr0[a * nz + c] + Hr0[c * nz + a]);
     }
     __syncthreads();
+    KKT_MARK(3);
     // ---- inertia correction: Cholesky of Hr + delta_w I, IPOPT's delta_w schedule
     const double last = dw_last ? dw_last[b] : 0.0;
     double dW = 0.0;
@@ -408,20 +521,38 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
     __syncthreads();
   }
   const double dW = sh.delta_w;
+  KKT_MARK(4);
   // ---- solve, then one step of iterative refinement on the unregularised system
   kkt_solve_lds(nw, m, Q, QR, Rd, L, M, dW, q1, q2, dw, dy, tmp);
+  KKT_MARK(5);
   if (!sh.rank_def) {
     // e1[r] is written and then updated by the same lane (group assignment depends on r only)
     group_dots<4>(nw, m, Ab, 1, nw, dy, 1, [&](int r, double d) { e1[r] = q1[r] - dW * dw[r] - d; });
     group_dots<4>(nw, nw, M, nw, 1, dw, 1, [&](int r, double d) { e1[r] -= d; });
     group_dots<4>(m, nw, Ab, nw, 1, dw, 1, [&](int k, double d) { e2[k] = q2[k] - d; });
     __syncthreads();
-    // the correction reuses q1/q2 as outputs: (e1, e2) -> (q1, q2)
-    kkt_solve_lds(nw, m, Q, QR, Rd, L, M, dW, e1, e2, q1, q2, tmp);
-    for (int r = tid; r < nw; r += blockDim.x) dw[r] += q1[r];
-    for (int k = tid; k < m; k += blockDim.x) dy[k] += q2[k];
+    // refine only when the residual is above 1e-13 of the right-hand side (wave 0 decides)
+    if (tid < 64) {
+      double rmax = 0.0, qmax = 0.0;
+      for (int r = tid; r < nw; r += 64) { rmax = fmax(rmax, fabs(e1[r])); qmax = fmax(qmax, fabs(q1[r])); }
+      for (int k = tid; k < m; k += 64) { rmax = fmax(rmax, fabs(e2[k])); qmax = fmax(qmax, fabs(q2[k])); }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        rmax = fmax(rmax, __shfl_xor(rmax, o));
+        qmax = fmax(qmax, __shfl_xor(qmax, o));
+      }
+      if (tid == 0) sh.flag = !(rmax <= 1e-13 * qmax);
+    }
     __syncthreads();
+    if (sh.flag) {
+      // the correction reuses q1/q2 as outputs: (e1, e2) -> (q1, q2)
+      kkt_solve_lds(nw, m, Q, QR, Rd, L, M, dW, e1, e2, q1, q2, tmp);
+      for (int r = tid; r < nw; r += blockDim.x) dw[r] += q1[r];
+      for (int k = tid; k < m; k += blockDim.x) dy[k] += q2[k];
+      __syncthreads();
+    }
   }
+  KKT_MARK(6);
   for (int i = tid; i < nw; i += blockDim.x) dwg[b * nw + i] = dw[i];
   for (int i = tid; i < m; i += blockDim.x) dyg[b * m + i] = dy[i];
   if (tid == 0) { dWg[b] = dW; dCg[b] = sh.delta_c; }
@@ -430,6 +561,7 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
   const int64_t per = kkt_ws_per(nw, m);
   for (int64_t i = tid; i < per - 4; i += blockDim.x) wsb[i] = sm[i];
   if (tid == 0) { wsb[per - 4] = dW; wsb[per - 3] = sh.delta_c; wsb[per - 2] = 0.0; wsb[per - 1] = 0.0; }
+  KKT_MARK(7);
 }
 
 // grad f + J^T y per instance from the CSR values (the Lagrangian gradient the solve loop
