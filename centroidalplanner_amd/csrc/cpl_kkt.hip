@@ -180,10 +180,10 @@ __device__ void wave_trsv(int n, bool lower, const double* Tm, int si, int sk, c
 }
 
 // Solve with the factors in LDS: Q [nw][nw] (row-major: Q[r*nw + c]), QR array (row j = column j of
-// A^T after the reflections; R[i][j] = QR[j*nw + i] for i < j, R[j][j] = Rd[j]), L [nz][nz] the
+// A^T after the reflections; R[i][j] = QR[j*nw + i] for i < j, R[j][j] = QR[j*nw + j]), L [nz][nz] the
 // Cholesky of the reduced Hessian, M [nw][nw] (plus delta_w on the diagonal, applied here).
 // Vectors in LDS: q1 [nw], q2 [m] -> dw [nw], dy [m].  tmp: >= 2*nw doubles.
-__device__ void kkt_solve_lds(int nw, int m, const double* Q, const double* QR, const double* Rd, const double* L,
+__device__ void kkt_solve_lds(int nw, int m, const double* Q, const double* QR, const double* L,
                               const double* M, double dW, const double* q1, const double* q2, double* dw,
                               double* dy, double* tmp) {
   const int tid = threadIdx.x;
@@ -193,7 +193,7 @@ __device__ void kkt_solve_lds(int nw, int m, const double* Q, const double* QR, 
   // R^T p_y = q2 (forward substitution; (R^T)[i][k] = R[k][i] = QR[i*nw + k])
   for (int i = tid; i < m; i += blockDim.x) py[i] = q2[i];
   __syncthreads();
-  if (tid < 64) wave_trsv(m, true, QR, nw, 1, Rd, 1, py);
+  if (tid < 64) wave_trsv(m, true, QR, nw, 1, QR, nw + 1, py);
   __syncthreads();
   // dw <- Y p_y
   group_dots<4>(nw, m, Q, nw, 1, py, 1, [&](int r, double d) { dw[r] = d; });
@@ -221,22 +221,23 @@ __device__ void kkt_solve_lds(int nw, int m, const double* Q, const double* QR, 
   group_dots<4>(m, nw, Q, 1, nw, t, 1, [&](int k, double d) { dy[k] = d; });
   __syncthreads();
   // R dy = s (backward substitution; R[i][k] = QR[k*nw + i])
-  if (tid < 64) wave_trsv(m, false, QR, 1, nw, Rd, 1, dy);
+  if (tid < 64) wave_trsv(m, false, QR, 1, nw, QR, nw + 1, dy);
   __syncthreads();
 }
 
-// Workspace layout per instance (doubles): Q [nw*nw] | QR [m*nw] | Rd [m] | L [nz*nz] | scalars [4]
+// Workspace layout per instance (doubles): Q [nw*nw] | QR [m*nw] (R's diagonal on its diagonal) |
+// L [nz*nz] | scalars [4]
 __host__ __device__ inline int64_t kkt_ws_per(int nw, int m) {
   const int nz = nw - m;
-  return (int64_t)nw * nw + (int64_t)m * nw + m + (int64_t)nz * nz + 4;
+  return (int64_t)nw * nw + (int64_t)m * nw + (int64_t)nz * nz + 4;
 }
 
-// LDS layout (doubles): Q | QR | Rd | L | q1 | q2 | dw | dy | e1 | e2 | tmp(3 nw).  M stays in global
-// memory (L2-resident while its workgroup runs; read by the matrix-vector products and M Z): the
-// image is 35 KiB at nw = 47, m = 30, four workgroups per CU instead of three.
+// LDS layout (doubles): Q | QR | L | dw | dy | tmp(max(2 nw, 3 m)).  M, the right-hand sides and the
+// refinement's residual / correction stay in global memory (L2-resident while the workgroup runs):
+// the image is 32.6 KiB at nw = 47, m = 30 — five workgroups per CU.
 __host__ __device__ inline int kkt_lds_doubles(int nw, int m) {
   const int nz = nw - m;
-  return nw * nw + m * nw + m + nz * nz + 5 * nw + 2 * m + 2 * nw;
+  return nw * nw + m * nw + nz * nz + nw + m + (2 * nw > 3 * m ? 2 * nw : 3 * m);
 }
 
 __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
@@ -253,19 +254,22 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
   const int nz = nw - m;
   double* Q = sm;
   double* QR = Q + nw * nw;
-  double* Rd = QR + m * nw;
-  double* L = Rd + m;
-  double* q1 = L + nz * nz;
-  double* q2 = q1 + nw;
-  double* dw = q2 + m;
+  double* L = QR + m * nw;
+  const double* q1 = r1g + b * nw;  // right-hand sides: global
+  const double* q2 = r2g + b * m;
+  double* dw = L + nz * nz;
   double* dy = dw + nw;
-  double* e1 = dy + m;
-  double* e2 = e1 + nw;
-  double* tmp = e2 + nw;  // 3 nw
+  double* tmp = dy + m;  // max(2 nw, 3 m)
   const double* Mb = Mg + b * nw * nw;
   const double* M = Mb;  // global
   const double* Ab = Ag + b * m * nw;
   double* wsb = ws + b * kkt_ws_per(nw, m);
+  // refinement residual and correction: global scratch past M Z in the workspace (overwritten by
+  // the factors at the end)
+  double* e1 = wsb + nw * nz;
+  double* e2 = e1 + nw;
+  double* c1 = e2 + m;
+  double* c2 = c1 + nw;
 
   if (active && !active[b]) {
     for (int i = tid; i < nw; i += blockDim.x) dwg[b * nw + i] = 0.0;
@@ -273,15 +277,13 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
     if (tid == 0 && mode == 0) { dWg[b] = 0.0; dCg[b] = 0.0; info[b] = 0; }
     return;
   }
-  for (int i = tid; i < nw; i += blockDim.x) q1[i] = r1g[b * nw + i];
-  for (int i = tid; i < m; i += blockDim.x) q2[i] = r2g[b * m + i];
 
   if (mode == 1) {  // re-solve with the kept factors
     const int64_t per = kkt_ws_per(nw, m);
     for (int64_t i = tid; i < per - 4; i += blockDim.x) sm[i] = wsb[i];
     if (tid == 0) { sh.delta_w = wsb[per - 4]; sh.delta_c = wsb[per - 3]; }
     __syncthreads();
-    kkt_solve_lds(nw, m, Q, QR, Rd, L, M, sh.delta_w, q1, q2, dw, dy, tmp);
+    kkt_solve_lds(nw, m, Q, QR, L, M, sh.delta_w, q1, q2, dw, dy, tmp);
     for (int i = tid; i < nw; i += blockDim.x) dwg[b * nw + i] = dw[i];
     for (int i = tid; i < m; i += blockDim.x) dyg[b * m + i] = dy[i];
     return;
@@ -306,14 +308,14 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
     const double sig = wave_sum(x0 * x0 + x1 * x1);
     const double alpha = x[j];
     if (sig == 0.0) {
-      if (lane == 0) { beta[j] = 0.0; Rd[j] = alpha; }
+      if (lane == 0) beta[j] = 0.0;  // R_jj = alpha stays on the diagonal
     } else {
       const double nrm = sqrt(alpha * alpha + sig);
       const double v0 = alpha <= 0.0 ? alpha - nrm : -sig / (alpha + nrm);
       const double rv0 = 1.0 / v0;
       if (i0 < nw) x[i0] = x0 * rv0;
       if (i1 < nw) x[i1] = x1 * rv0;
-      if (lane == 0) { beta[j] = 2.0 * v0 * v0 / (sig + v0 * v0); Rd[j] = nrm; }
+      if (lane == 0) { beta[j] = 2.0 * v0 * v0 / (sig + v0 * v0); x[j] = nrm; }  // R_jj on the diagonal
     }
   };
   if (m > 0 && wid == 0) house(0);
@@ -405,12 +407,13 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
   // ---- rank deficiency: delta_c on R's diagonal
   if (tid == 0) {
     double rmax = 0.0;
-    for (int j = 0; j < m; ++j) rmax = fabs(Rd[j]) > rmax ? fabs(Rd[j]) : rmax;
+    for (int j = 0; j < m; ++j) rmax = fabs(QR[j * nw + j]) > rmax ? fabs(QR[j * nw + j]) : rmax;
     const double dc = 1e-8 * pow(mug[b], 0.25) * (rmax > 0.0 ? rmax : 1.0);
     int def = 0;
     for (int j = 0; j < m; ++j)
-      if (!(fabs(Rd[j]) >= 1e-10 * rmax) || rmax == 0.0) {
-        Rd[j] = Rd[j] < 0.0 ? Rd[j] - dc : Rd[j] + dc;
+      if (!(fabs(QR[j * nw + j]) >= 1e-10 * rmax) || rmax == 0.0) {
+        double& rjj = QR[j * nw + j];
+        rjj = rjj < 0.0 ? rjj - dc : rjj + dc;
         def = 1;
       }
     sh.rank_def = def;
@@ -523,7 +526,7 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
   const double dW = sh.delta_w;
   KKT_MARK(4);
   // ---- solve, then one step of iterative refinement on the unregularised system
-  kkt_solve_lds(nw, m, Q, QR, Rd, L, M, dW, q1, q2, dw, dy, tmp);
+  kkt_solve_lds(nw, m, Q, QR, L, M, dW, q1, q2, dw, dy, tmp);
   KKT_MARK(5);
   if (!sh.rank_def) {
     // e1[r] is written and then updated by the same lane (group assignment depends on r only)
@@ -545,10 +548,10 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
     }
     __syncthreads();
     if (sh.flag) {
-      // the correction reuses q1/q2 as outputs: (e1, e2) -> (q1, q2)
-      kkt_solve_lds(nw, m, Q, QR, Rd, L, M, dW, e1, e2, q1, q2, tmp);
-      for (int r = tid; r < nw; r += blockDim.x) dw[r] += q1[r];
-      for (int k = tid; k < m; k += blockDim.x) dy[k] += q2[k];
+      // the correction (e1, e2) -> (c1, c2), global scratch
+      kkt_solve_lds(nw, m, Q, QR, L, M, dW, e1, e2, c1, c2, tmp);
+      for (int r = tid; r < nw; r += blockDim.x) dw[r] += c1[r];
+      for (int k = tid; k < m; k += blockDim.x) dy[k] += c2[k];
       __syncthreads();
     }
   }

@@ -12,7 +12,7 @@ from centroidalplanner_amd import _abi
 def test_workspace_size_and_argument_checks():
     nw, m = 47, 30
     nz = nw - m
-    assert _abi.lib.cpl_kkt_workspace_doubles(nw, m) == nw * nw + m * nw + m + nz * nz + 4
+    assert _abi.lib.cpl_kkt_workspace_doubles(nw, m) == nw * nw + m * nw + nz * nz + 4
     assert _abi.lib.cpl_kkt_workspace_doubles(10, 11) == -1
     # m > nw and nw > 128 are rejected before any device work
     st = _abi.lib.cpl_kkt_solve(0, 1, 10, 11, *([None] * 13), None)
