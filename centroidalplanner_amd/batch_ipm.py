@@ -84,6 +84,26 @@ class KernelEvaluator:
         self.calls += 1
         return self.problem.eval_batch(X, mass, self.env_tag, outputs=outputs)
 
+    def lagrangian_grad(self, X, mass, y, y_repeat, csc):
+        """grad f + J^T y of every instance in one fused launch (cpl_eval_lagrangian_grad: the
+        Jacobian stays in LDS); None where the fused path does not exist (Superquadric / mixed
+        batches: the caller takes eval + cpl_lagrangian_grad, the same result)."""
+        import torch
+
+        if getattr(self, "_no_fused", False):
+            return None
+        out = torch.empty(X.shape[0], X.shape[1], dtype=torch.float64, device=X.device)
+        st = _abi.lib.cpl_eval_lagrangian_grad(
+            ctypes.byref(self.problem.desc()), X.shape[0], _ptr(X), None if mass is None else _ptr(mass),
+            None if self.env_tag is None else _ptr(self.env_tag), _ptr(csc[0]), _ptr(csc[1]), _ptr(csc[2]), _ptr(y),
+            y_repeat, _ptr(out), ctypes.c_void_p(torch.cuda.current_stream(X.device).cuda_stream))
+        if st == _abi.ERR_UNSUPPORTED:
+            self._no_fused = True
+            return None
+        _abi.check(st)
+        self.calls += 1
+        return out
+
 
 @dataclass
 class BatchSolveResult:
@@ -244,14 +264,19 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         Xp[:, fd_cols, free] += h
         Xp[:, nf + fd_cols, free] -= h
         n_eval += 1
-        o = ev(Xp.view(B * 2 * nf, n), Mass_fd, outputs=("jac", "grad"))
-        if use_hip:  # grad f + J^T y on the device (cpl_lagrangian_grad), y shared by the 2 nf points
+        fused = ev.lagrangian_grad if use_hip and hasattr(ev, "lagrangian_grad") else None
+        gL = fused(Xp.view(B * 2 * nf, n), Mass_fd, yv.contiguous(), 2 * nf, csc) if fused else None
+        if gL is not None:  # one launch: eval + grad f + J^T y from the LDS tile image
+            pass
+        elif use_hip:  # grad f + J^T y on the device (cpl_lagrangian_grad), y shared by the 2 nf points
+            o = ev(Xp.view(B * 2 * nf, n), Mass_fd, outputs=("jac", "grad"))
             gL = torch.empty(B * 2 * nf, n, dtype=dt, device=dev)
             yc = yv.contiguous()
             _abi.check(_abi.lib.cpl_lagrangian_grad(B * 2 * nf, n, m, nnz, _ptr(csc[0]), _ptr(csc[1]), _ptr(csc[2]),
                                                     _ptr(o["grad"]), _ptr(o["jac"]), _ptr(yc), 2 * nf, _ptr(gL),
                                                     stream()))
         else:
+            o = ev(Xp.view(B * 2 * nf, n), Mass_fd, outputs=("jac", "grad"))
             gL = o["grad"].clone()
             gL.index_add_(1, jCol_t, torch.nan_to_num(o["jac"], nan=0.0) * yv.repeat_interleave(2 * nf, 0)[:, iRow_t])
         gL = gL.view(B, 2 * nf, n)[:, :, free]

@@ -70,6 +70,13 @@ struct KParams {
   int32_t contact_rows;  // constraint rows per contact: 6 (environment) or 2
   int32_t ablate;        // measurement-only ablation (cpl_set_tuning), 0 in production
   int32_t sq_ladder;     // every P_a is an integer in [2, 64]: double-double power ladders
+  // fused Lagrangian gradient (cpl_eval_lagrangian_grad): grad f + J^T y of every instance from the
+  // LDS tile image, through a CSC index of the fixed structure; instance b takes y[b / y_repeat]
+  int32_t want_lgrad, y_repeat;
+  const int32_t* col_ptr;
+  const int32_t* csc_k;
+  const int32_t* csc_row;
+  const double* ly;
 };
 static_assert(sizeof(KParams) < 4096, "kernel parameters must fit the kernarg segment");
 
@@ -1387,7 +1394,22 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
       }
     }
     lds_barrier();  // the tile image is complete
-    if (K.ablate != 2) {
+    if (K.want_lgrad) {
+      // grad f + J^T y per (instance, column), the operation order of cpl_lagrangian_grad (bitwise
+      // the same result) without the Jacobian's round trip through HBM; a 0/0 entry counts as 0
+      for (int e = tid; e < valid * n; e += CT) {
+        const int r = e / n, j = e - r * n;
+        const double* jr = Jt + r * nnz;
+        const double* yb = K.ly + ((b0 + r) / K.y_repeat) * m;
+        double s = Dt[r * n + j];
+        for (int q = K.col_ptr[j]; q < K.col_ptr[j + 1]; ++q) {
+          double v = jr[K.csc_k[q]];
+          v = v == v ? v : 0.0;
+          s += v * yb[K.csc_row[q]];
+        }
+        grad_out[(b0 + r) * n + j] = s;
+      }
+    } else if (K.ablate != 2) {
       if (K.want_g) copy_out_ct<CT, NT>(g_out + b0 * m, Gt, valid * m, tid);
       if (K.want_j) copy_out_ct<CT, NT>(jac_out + b0 * nnz, Jt, valid * nnz, tid);
       if (K.want_grad) copy_out_ct<CT, NT>(grad_out + b0 * n, Dt, valid * n, tid);
@@ -1646,9 +1668,18 @@ static int32_t norm_workspace(hipStream_t stream, size_t blocks, double** out) {
   return CPL_OK;
 }
 
+struct LGradArgs {
+  const int32_t* col_ptr;
+  const int32_t* csc_k;
+  const int32_t* csc_row;
+  const double* y;
+  int32_t y_repeat;
+};
+
 static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
                            const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
-                           double* d_norms, hipStream_t stream, bool finish = true) {
+                           double* d_norms, hipStream_t stream, bool finish = true,
+                           const LGradArgs* lg = nullptr) {
   int32_t st = validate_desc(d);
   if (st) return st;
   if (batch < 0) return fail(CPL_ERR_INVALID_ARGUMENT, "negative batch");
@@ -1668,10 +1699,26 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
   KParams K;
   fill_params(d, K, d_x);
   K.want_norms = d_norms != nullptr;
+  K.want_lgrad = 0;
+  K.y_repeat = 1;
+  K.col_ptr = K.csc_k = K.csc_row = nullptr;
+  K.ly = nullptr;
   double* ws = nullptr;
+  if (lg && !use_pipe(K))
+    return fail(CPL_ERR_UNSUPPORTED, "fused Lagrangian gradient: pipelined (Ground / no environment) path only");
   if (use_pipe(K)) {
-    st = plan_pipe(K, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr);
+    // the fused Lagrangian gradient computes jac and grad into the tile image and stores only d_grad
+    st = lg ? plan_pipe(K, false, true, false, true)
+            : plan_pipe(K, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr);
     if (st) return st;
+    if (lg) {
+      K.want_lgrad = 1;
+      K.y_repeat = lg->y_repeat;
+      K.col_ptr = lg->col_ptr;
+      K.csc_k = lg->csc_k;
+      K.csc_row = lg->csc_row;
+      K.ly = lg->y;
+    }
     K.ablate = g_ablate;
     const size_t lds = sizeof(double) * (size_t)(K.offI + 72);
     using KernT = void (*)(const KParams, int64_t, const double*, const double*, const uint8_t*, double*, double*,
@@ -1759,6 +1806,19 @@ int32_t cpl_eval_batch(const cpl_problem_desc* d, int64_t batch, const double* d
                        const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
                        void* stream) {
   return launch_eval(d, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f, d_grad, nullptr, (hipStream_t)stream);
+}
+
+int32_t cpl_eval_lagrangian_grad(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
+                                 const uint8_t* d_env_tag, const int32_t* d_col_ptr, const int32_t* d_csc_k,
+                                 const int32_t* d_csc_row, const double* d_y, int32_t y_repeat, double* d_out,
+                                 void* stream) {
+  if (y_repeat < 1) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_eval_lagrangian_grad: y_repeat must be >= 1");
+  if (batch > 0 && (!d_col_ptr || !d_csc_k || !d_csc_row || !d_y || !d_out))
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_eval_lagrangian_grad: missing buffer");
+  const LGradArgs lg{d_col_ptr, d_csc_k, d_csc_row, d_y, y_repeat};
+  // jac and grad f are computed into the tile image; only grad f + J^T y is stored (to d_out)
+  return launch_eval(d, batch, d_x, d_mass, d_env_tag, nullptr, nullptr, nullptr, d_out, nullptr, (hipStream_t)stream,
+                     true, &lg);
 }
 
 int32_t cpl_eval_batch_norms(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,

@@ -247,3 +247,41 @@ def test_batch_solve_other_scenarios_gpu(which):
     X = r.x.cpu().numpy()
     for b in np.flatnonzero(ok)[::17]:
         _certify_scenario(which, prob, X[b], mass[b], wrench)
+
+
+@pytest.mark.gpu
+def test_fused_lagrangian_grad_is_bitwise_the_two_launch_result():
+    """cpl_eval_lagrangian_grad (grad f + J^T y from the eval kernel's LDS tile) against
+    cpl_eval_batch (jac, grad) + cpl_lagrangian_grad: the same operations in the same order."""
+    import ctypes
+
+    from centroidalplanner_amd import _abi
+    from centroidalplanner_amd.batch_ipm import KernelEvaluator
+
+    cpl = solve_problem()
+    prob = cpl.GetCplProblem()
+    n, m, nnz = prob.get_nlp_info()
+    X0, mass = solve_inputs(prob, 333, seed=5)
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(6)
+    X = torch.as_tensor(X0 + rng.normal(scale=0.05, size=X0.shape), device=dev).contiguous()
+    X[::7, 3:5] = 0.0  # zero tangential force on a contact: the 0/0 cone Jacobian entries (NaN -> 0)
+    M = torch.as_tensor(mass, device=dev)
+    rep = 3
+    y = torch.as_tensor(rng.normal(size=((X.shape[0] + rep - 1) // rep, m)), device=dev).contiguous()
+    iRow, jCol = prob.get_structure()
+    order = np.lexsort((iRow, jCol))
+    col_ptr = np.zeros(n + 1, dtype=np.int64)
+    np.add.at(col_ptr, jCol.astype(np.int64) + 1, 1)
+    col_ptr = np.cumsum(col_ptr)
+    csc = [torch.as_tensor(a.astype(np.int32), device=dev) for a in (col_ptr, order, iRow[order])]
+    fused = KernelEvaluator(prob).lagrangian_grad(X, M, y, rep, csc)
+    assert fused is not None
+    o = prob.eval_batch(X, M, outputs=("jac", "grad"))
+    ref = torch.empty_like(fused)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    _abi.check(_abi.lib.cpl_lagrangian_grad(X.shape[0], n, m, nnz, p(csc[0]), p(csc[1]), p(csc[2]), p(o["grad"]),
+                                            p(o["jac"]), p(y), rep, p(ref), None))
+    torch.cuda.synchronize()
+    assert torch.isfinite(ref).all()
+    assert torch.equal(fused, ref)
