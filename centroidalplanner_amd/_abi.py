@@ -135,6 +135,7 @@ SIGNATURES = {
     "cpl_ipm_post_step": (c_int32, [c_int64, c_int32] + [c_void_p] * 23),
     "cpl_ipm_accept": (c_int32, [c_int64, c_int32, c_int32, c_int32] + [c_void_p] * 30),
     "cpl_ipm_masked_rows": (c_int32, [c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "cpl_ipm_dense_a": (c_int32, [c_int64, c_int32, c_int32, c_int32, c_int32] + [c_void_p] * 5),
 }
 
 

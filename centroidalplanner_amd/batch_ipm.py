@@ -205,6 +205,11 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     row_slack_np = np.full(m, -1, dtype=np.int32)
     row_slack_np[I_np] = np.arange(nI, dtype=np.int32)
     row_slack = torch.as_tensor(row_slack_np, device=dev)
+    # device path: the Jacobian state stays in CSR form; A = [J_free | -P] is gathered per iteration
+    csr_J = use_hip and not use_bfgs
+    dense_pos = np.full(m * n, -1, dtype=np.int64)
+    dense_pos[iRow.astype(np.int64) * n + jCol.astype(np.int64)] = np.arange(nnz)
+    amap = torch.as_tensor(dense_pos.reshape(m, n)[:, np.where(~fixed_np)[0]].astype(np.int32).copy(), device=dev)
     if use_hip:
         kkt_ws = torch.empty(B * int(_abi.lib.cpl_kkt_workspace_doubles(nw, m)), dtype=dt, device=dev)
 
@@ -235,6 +240,8 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         nonlocal n_eval
         n_eval += 1
         o = ev(Xe, Mass)
+        if csr_J:  # the device path keeps the CSR values; jac_w builds A from them in one launch
+            return {"f": o["f"], "grad": o["grad"], "g": o["g"], "J": o["jac"].contiguous()}
         J = torch.zeros(B, m * n, dtype=dt, device=dev)
         J[:, flat_idx] = torch.nan_to_num(o["jac"], nan=0.0)  # a cone at F_t = 0 has a 0/0 Jacobian
         return {"f": o["f"], "grad": o["grad"], "g": o["g"], "J": J.view(B, m, n)}
@@ -250,6 +257,11 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         return c
 
     def jac_w(J):
+        if csr_J:
+            A_ = torch.empty(B, m, nw, dtype=dt, device=dev)
+            _abi.check(_abi.lib.cpl_ipm_dense_a(B, m, nw, nf, nnz, _ptr(amap), _ptr(row_slack), _ptr(J), _ptr(A_),
+                                                stream()))
+            return A_
         return torch.cat([J[:, :, free], (-P).expand(B, m, nI)], dim=2)
 
     def barrier(wv, muv):

@@ -441,6 +441,33 @@ __global__ __launch_bounds__(256) void cpl_ipm_masked_rows_kernel(int64_t total,
   if (mask[e / len]) dst[e] = src[e];
 }
 
+// A = dc/dw = [J_free | -P] of every instance, dense [m, nw], straight from the CSR Jacobian values:
+// amap[r * nf + k] = CSR position of (row r, free column k) or -1 (structural zero), NaN -> 0
+// (a cone at zero tangential force); the slack block is -1 at (r, nf + row_slack[r]).
+__global__ __launch_bounds__(256) void cpl_ipm_dense_a_kernel(int64_t total, int m, int nw, int nf, int nnz,
+                                                              const int32_t* __restrict__ amap,
+                                                              const int32_t* __restrict__ row_slack,
+                                                              const double* __restrict__ jac,
+                                                              double* __restrict__ A) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int per = m * nw;
+  const int64_t b = e / per;
+  const int rc = (int)(e - b * per);
+  const int r = rc / nw, k = rc - r * nw;
+  double v = 0.0;
+  if (k < nf) {
+    const int q = amap[r * nf + k];
+    if (q >= 0) {
+      v = jac[b * nnz + q];
+      v = v == v ? v : 0.0;
+    }
+  } else if (row_slack[r] == k - nf) {
+    v = -1.0;
+  }
+  A[e] = v;
+}
+
 }  // namespace cpl
 
 using namespace cpl;
@@ -614,6 +641,23 @@ int32_t cpl_ipm_masked_rows(int64_t batch, int64_t row_len, const uint8_t* d_mas
                      row_len, d_mask, d_src, d_dst);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_ipm_masked_rows launch: ") + hipGetErrorString(e));
+  return CPL_OK;
+}
+
+int32_t cpl_ipm_dense_a(int64_t batch, int32_t m, int32_t nw, int32_t nf, int32_t nnz, const int32_t* d_amap,
+                        const int32_t* d_row_slack, const double* d_jac, double* d_A, void* stream) {
+  if (batch < 0 || m < 0 || nw <= 0 || nf < 0 || nf > nw || nnz < 0)
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_dense_a: bad sizes");
+  if (batch == 0 || m == 0) return CPL_OK;
+  if (!d_amap || !d_row_slack || (nnz > 0 && !d_jac) || !d_A)
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_dense_a: missing buffer");
+  const int64_t total = batch * (int64_t)m * nw;
+  const int64_t blocks = (total + 255) / 256;
+  if (blocks > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_dense_a: batch too large");
+  hipLaunchKernelGGL(cpl_ipm_dense_a_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, total, (int)m,
+                     (int)nw, (int)nf, (int)nnz, d_amap, d_row_slack, d_jac, d_A);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_ipm_dense_a launch: ") + hipGetErrorString(e));
   return CPL_OK;
 }
 

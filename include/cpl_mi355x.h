@@ -325,6 +325,10 @@ int32_t cpl_ipm_accept(int64_t batch, int32_t nw, int32_t m, int32_t nfilt, cons
                        double* d_filt_t, double* d_filt_p, int64_t* d_fcount, void* stream);
 int32_t cpl_ipm_masked_rows(int64_t batch, int64_t row_len, const uint8_t* d_mask, const double* d_src, double* d_dst,
                             void* stream);
+/* cpl_ipm_dense_a: A = [J_free | -P] dense [batch, m, nw] from the CSR Jacobian values (amap: CSR
+ * position of (row, free column) or -1; row_slack: slack of each inequality row or -1; NaN -> 0). */
+int32_t cpl_ipm_dense_a(int64_t batch, int32_t m, int32_t nw, int32_t nf, int32_t nnz, const int32_t* d_amap,
+                        const int32_t* d_row_slack, const double* d_jac, double* d_A, void* stream);
 
 #ifdef __cplusplus
 }
