@@ -309,11 +309,14 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                                           _ptr(dy), _ptr(delta_w), _ptr(delta_c), _ptr(info), _ptr(kkt_ws),
                                           stream()))
 
-        def solve_primal(r2v):  # second-order correction: the kept factors, another r2
+        def solve_primal(r2v, mask=None):
+            """Second-order correction: the kept factors, another r2; only the instances in mask
+            (default: the factorised ones) are solved, the others get 0 and cost nothing."""
             out_dw = torch.empty(B, nw, dtype=dt, device=dev)
             out_dy = torch.empty(B, m, dtype=dt, device=dev)
+            msk = act_u8 if mask is None else mask.to(torch.uint8)
             _abi.check(_abi.lib.cpl_kkt_solve(1, B, nw, m, _ptr(Mc), _ptr(Ac), _ptr(r1c), _ptr(r2v.contiguous()),
-                                              None, None, _ptr(act_u8), _ptr(out_dw), _ptr(out_dy), None, None, None,
+                                              None, None, _ptr(msk), _ptr(out_dw), _ptr(out_dy), None, None, None,
                                               _ptr(kkt_ws), stream()))
             return out_dw
 
@@ -382,7 +385,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
             return torch.where(keep, d1, d1 + c1), torch.where(keep, d2, d2 + c2)
 
         dw, dy = refined(r1, r2)
-        return dw, dy, delta_w, lambda r2v: refined(r1, r2v)[0]
+        return dw, dy, delta_w, lambda r2v, mask=None: refined(r1, r2v)[0]
 
     kkt = kkt_device if use_hip else kkt_host
 
@@ -628,7 +631,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                 ct = cons(o["g"], wt[:, nf:])
                 for _ in range(max_soc):
                     c_soc = a_soc[:, None] * c_soc + ct
-                    dws = solve_primal(-c_soc)
+                    dws = solve_primal(-c_soc, soc)  # only the instances that try a correction
                     a_soc = primal_step(dws)
                     ws, os_ = trial(dws, a_soc, soc)
                     oks, ths = judge_take(ws, os_, alpha, soc)
