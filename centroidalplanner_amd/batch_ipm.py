@@ -295,6 +295,30 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         H = (gL[:, :nf] - gL[:, nf:]) / (2.0 * h[:, :, None])
         return 0.5 * (H + H.transpose(1, 2))
 
+    freepos_np = np.full(n, -1, dtype=np.int32)
+    freepos_np[np.where(~fixed_np)[0]] = np.arange(nf, dtype=np.int32)
+    freepos = torch.as_tensor(freepos_np, device=dev)
+
+    def fd_grads_dev(Xc, yv):
+        """Device path of fd_hessian: the 2 nf points of every instance (cpl_ipm_fd_points) and their
+        Lagrangian gradients (one fused eval launch); the differencing happens in the Newton setup."""
+        nonlocal n_eval
+        Xp = torch.empty(B * 2 * nf, n, dtype=dt, device=dev)
+        h = torch.empty(B, nf, dtype=dt, device=dev)
+        _abi.check(_abi.lib.cpl_ipm_fd_points(B, n, nf, fd_step, _ptr(freepos), _ptr(Xc.contiguous()), _ptr(Xp),
+                                              _ptr(h), stream()))
+        n_eval += 1
+        yc = yv.contiguous()
+        fused = ev.lagrangian_grad if hasattr(ev, "lagrangian_grad") else None
+        gL = fused(Xp, Mass_fd, yc, 2 * nf, csc) if fused else None
+        if gL is None:
+            o = ev(Xp, Mass_fd, outputs=("jac", "grad"))
+            gL = torch.empty(B * 2 * nf, n, dtype=dt, device=dev)
+            _abi.check(_abi.lib.cpl_lagrangian_grad(B * 2 * nf, n, m, nnz, _ptr(csc[0]), _ptr(csc[1]), _ptr(csc[2]),
+                                                    _ptr(o["grad"]), _ptr(o["jac"]), _ptr(yc), 2 * nf, _ptr(gL),
+                                                    stream()))
+        return gL, h
+
     def kkt_device(M, A, r1, r2, mu, dwl, active):
         """cpl_kkt_solve: factorise + solve on the device; returns (dw, dy, delta_w, solve_primal)."""
         Mc, Ac, r1c = M.contiguous(), A.contiguous(), r1.contiguous()
@@ -514,7 +538,14 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                 return out
             return torch.minimum(max_step(w, d, hasL, wl0, tau), max_step(-w, -d, hasU, -wu0, tau))
 
-        Hblk = S["Hq"] if use_bfgs else fd_hessian(unpack(w), y)
+        gLfd = hfd = None
+        if use_bfgs:
+            Hblk = S["Hq"]
+        elif use_hip:  # central differences formed inside the Newton setup kernel
+            Hblk = None
+            gLfd, hfd = fd_grads_dev(unpack(w), y)
+        else:
+            Hblk = fd_hessian(unpack(w), y)
         if use_hip:  # Newton system: one fused launch (csrc/cpl_ipm.hip)
             M = torch.empty(B, nw, nw, dtype=dt, device=dev)
             r1, gphi, mr_diag = (torch.empty(B, nw, dtype=dt, device=dev) for _ in range(3))
@@ -522,7 +553,9 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
             theta_k, phi_k = torch.empty(B, dtype=dt, device=dev), torch.empty(B, dtype=dt, device=dev)
             _abi.check(_abi.lib.cpl_ipm_newton_setup(
                 B, nw, m, nf, _ptr(w), _ptr(zL), _ptr(zU), _ptr(gradw), _ptr(A), _ptr(y), _ptr(c),
-                _ptr(cur["f"]), _ptr(mu), _ptr(hasL_u8), _ptr(hasU_u8), _ptr(wl0), _ptr(wu0), _ptr(Hblk.contiguous()),
+                _ptr(cur["f"]), _ptr(mu), _ptr(hasL_u8), _ptr(hasU_u8), _ptr(wl0), _ptr(wu0),
+                None if Hblk is None else _ptr(Hblk.contiguous()), None if gLfd is None else _ptr(gLfd),
+                None if hfd is None else _ptr(hfd), _ptr(free), n,
                 _ptr(M), _ptr(r1), _ptr(r2), _ptr(gphi), _ptr(mr_diag), _ptr(theta_k), _ptr(phi_k), stream()))
         else:
             dl = torch.where(hasL, w - wl0, torch.ones_like(w))

@@ -262,6 +262,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
     const double* __restrict__ y, const double* __restrict__ c, const double* __restrict__ f,
     const double* __restrict__ mu, const uint8_t* __restrict__ hasL, const uint8_t* __restrict__ hasU,
     const double* __restrict__ wl0, const double* __restrict__ wu0, const double* __restrict__ H,
+    const double* __restrict__ gL, const double* __restrict__ hfd, const int64_t* __restrict__ free_idx, int n,
     double* __restrict__ M, double* __restrict__ r1, double* __restrict__ r2, double* __restrict__ gphi,
     double* __restrict__ mr_diag, double* __restrict__ theta, double* __restrict__ phi) {
   const int64_t b = (int64_t)blockIdx.x * IPM_WAVES + (threadIdx.x >> 6);
@@ -302,10 +303,21 @@ __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS stores have landed
   __builtin_amdgcn_wave_barrier();
   const double* Hb = H ? H + b * (int64_t)nf * nf : nullptr;
+  // or the central-difference Hessian straight from the Lagrangian gradients of the 2 nf points
+  // (the operations of batch_ipm.py fd_hessian: (gL+ - gL-) / (2 h), then 0.5 (H + H^T))
+  const double* gb = gL ? gL + b * (int64_t)2 * nf * n : nullptr;
   for (int e = lane; e < nw * nw; e += 64) {
     const int k = e / nw, j = e - k * nw;
     double v = (j == k) ? sg[k] : 0.0;
-    if (Hb && k < nf && j < nf) v += Hb[k * nf + j];
+    if (k < nf && j < nf) {
+      if (Hb) {
+        v += Hb[k * nf + j];
+      } else if (gb) {
+        const double hk = (gb[k * n + free_idx[j]] - gb[(nf + k) * n + free_idx[j]]) / (2.0 * hfd[b * nf + k]);
+        const double hj = (gb[j * n + free_idx[k]] - gb[(nf + j) * n + free_idx[k]]) / (2.0 * hfd[b * nf + j]);
+        v += 0.5 * (hk + hj);
+      }
+    }
     Mb[e] = v;
   }
   double th = 0.0;
@@ -468,6 +480,30 @@ __global__ __launch_bounds__(256) void cpl_ipm_dense_a_kernel(int64_t total, int
   A[e] = v;
 }
 
+// Central-difference points of the solve loop's Hessian (batch_ipm.py fd_hessian): for instance b
+// and free variable k, h = fd_step max(|x_free k|, 1); point p < nf is x + h e_{free p}, point
+// nf + p is x - h e_{free p}.  Xp [batch, 2 nf, n], h_out [batch, nf].  freepos[col] = k or -1.
+__global__ __launch_bounds__(256) void cpl_ipm_fd_points_kernel(int64_t total, int n, int nf, double fd_step,
+                                                                const int32_t* __restrict__ freepos,
+                                                                const double* __restrict__ X,
+                                                                double* __restrict__ Xp, double* __restrict__ h_out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int per = 2 * nf * n;
+  const int64_t b = e / per;
+  const int pc = (int)(e - b * per);
+  const int p = pc / n, col = pc - p * n;
+  const double xv = X[b * n + col];
+  const int k = freepos[col];
+  double v = xv;
+  if (k >= 0 && (p == k || p == nf + k)) {
+    const double h = fd_step * fmax(fabs(xv), 1.0);
+    v = p == k ? xv + h : xv - h;
+    if (p == k) h_out[b * nf + k] = h;
+  }
+  Xp[e] = v;
+}
+
 }  // namespace cpl
 
 using namespace cpl;
@@ -579,16 +615,18 @@ int32_t cpl_ipm_newton_setup(int64_t batch, int32_t nw, int32_t m, int32_t nf, c
                              const double* d_zU, const double* d_gw, const double* d_A, const double* d_y,
                              const double* d_c, const double* d_f, const double* d_mu, const uint8_t* d_hasL,
                              const uint8_t* d_hasU, const double* d_wl0, const double* d_wu0, const double* d_H,
+                             const double* d_gL, const double* d_hfd, const int64_t* d_free_idx, int32_t n,
                              double* d_M, double* d_r1, double* d_r2, double* d_gphi, double* d_mr_diag,
                              double* d_theta, double* d_phi, void* stream) {
   if (batch < 0 || nw <= 0 || m < 0 || nf < 0 || nf > nw) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_newton_setup: bad sizes");
   if (batch == 0) return CPL_OK;
   if (!d_w || !d_zL || !d_zU || !d_gw || (m > 0 && (!d_A || !d_y || !d_c || !d_r2)) || !d_f || !d_mu || !d_hasL ||
-      !d_hasU || !d_wl0 || !d_wu0 || !d_M || !d_r1 || !d_gphi || !d_mr_diag || !d_theta || !d_phi)
+      !d_hasU || !d_wl0 || !d_wu0 || !d_M || !d_r1 || !d_gphi || !d_mr_diag || !d_theta || !d_phi ||
+      (d_gL && (!d_hfd || !d_free_idx || n < nf)))
     return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_newton_setup: missing buffer");
   IPM_LAUNCH(cpl_ipm_newton_setup_kernel, "cpl_ipm_newton_setup", batch, (int)nw, (int)m, (int)nf, d_w, d_zL, d_zU,
-             d_gw, d_A, d_y, d_c, d_f, d_mu, d_hasL, d_hasU, d_wl0, d_wu0, d_H, d_M, d_r1, d_r2, d_gphi, d_mr_diag,
-             d_theta, d_phi);
+             d_gw, d_A, d_y, d_c, d_f, d_mu, d_hasL, d_hasU, d_wl0, d_wu0, d_H, d_gL, d_hfd, d_free_idx, (int)n, d_M,
+             d_r1, d_r2, d_gphi, d_mr_diag, d_theta, d_phi);
 }
 
 int32_t cpl_ipm_post_step(int64_t batch, int32_t nw, const double* d_w, const double* d_dw, const double* d_zL,
@@ -658,6 +696,21 @@ int32_t cpl_ipm_dense_a(int64_t batch, int32_t m, int32_t nw, int32_t nf, int32_
                      (int)nw, (int)nf, (int)nnz, d_amap, d_row_slack, d_jac, d_A);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_ipm_dense_a launch: ") + hipGetErrorString(e));
+  return CPL_OK;
+}
+
+int32_t cpl_ipm_fd_points(int64_t batch, int32_t n, int32_t nf, double fd_step, const int32_t* d_freepos,
+                          const double* d_X, double* d_Xp, double* d_h, void* stream) {
+  if (batch < 0 || n <= 0 || nf < 0 || nf > n) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_fd_points: bad sizes");
+  if (batch == 0 || nf == 0) return CPL_OK;
+  if (!d_freepos || !d_X || !d_Xp || !d_h) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_fd_points: missing buffer");
+  const int64_t total = batch * 2 * (int64_t)nf * n;
+  const int64_t blocks = (total + 255) / 256;
+  if (blocks > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_fd_points: batch too large");
+  hipLaunchKernelGGL(cpl_ipm_fd_points_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, total,
+                     (int)n, (int)nf, fd_step, d_freepos, d_X, d_Xp, d_h);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_ipm_fd_points launch: ") + hipGetErrorString(e));
   return CPL_OK;
 }
 
