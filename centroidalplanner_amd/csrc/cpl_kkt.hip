@@ -293,12 +293,16 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
   for (int i = tid; i < m * nw; i += blockDim.x) QR[i] = Ab[i];
   __syncthreads();
   KKT_MARK(0);
-  // Per column j: wave 0 forms the reflector (v in place, v_j = 1 implicit; beta_j; R_jj), all
-  // waves take the dots v^T y of the later columns (8 lanes per column), then the update: wave 0
-  // updates column j+1 and goes straight on to its reflector, the other waves update the rest —
-  // two workgroup barriers per column.
-  double* beta = tmp;          // [m]
-  double* sdot = tmp + 2 * m;  // [m] (tmp holds 3 nw >= 3 m doubles)
+  // Householder QR two columns at a time.  Wave 0 forms the reflector pair (j, j+1) — v in place
+  // (v_j = 1 implicit), beta, R_jj on the diagonal, H_j applied to column j+1 in between — and
+  // c_j = v_{j+1}^T v_j; then all waves take both dots of every later column in one pass
+  //   s0 = beta_j (y_j + v_j^T y),  s1 = beta_{j+1} (y_{j+1} + v_{j+1}^T y - s0 c_j)
+  // (8 lanes per column) and the update y -= s0 v_j + s1 v_{j+1}: wave 0 updates columns j+2, j+3
+  // and goes straight on to the next pair — two workgroup barriers per pair of columns.
+  double* beta = tmp;        // [m]
+  double* s0v = tmp + m;     // [m]
+  double* s1v = tmp + 2 * m; // [m] (tmp holds max(2 nw, 3 m) doubles)
+  double* cpair = dw;        // [m / 2 + 1]: c_j of the pair starting at j (dw is free until the solve)
   const int wid = tid >> 6, lane = tid & 63;
   const int nwaves = blockDim.x >> 6;
   auto house = [&](int j) {
@@ -318,90 +322,141 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
       if (lane == 0) { beta[j] = 2.0 * v0 * v0 / (sig + v0 * v0); x[j] = nrm; }  // R_jj on the diagonal
     }
   };
-  if (m > 0 && wid == 0) house(0);
+  auto house2 = [&](int j) {  // wave 0: reflectors j and j+1, c_j
+    house(j);
+    if (j + 1 >= m) return;
+    const double* v = QR + j * nw;
+    double* y = QR + (j + 1) * nw;
+    const int i0 = j + 1 + lane, i1 = i0 + 64;
+    const double p = wave_sum((i0 < nw ? v[i0] * y[i0] : 0.0) + (i1 < nw ? v[i1] * y[i1] : 0.0));
+    const double sj = beta[j] * (y[j] + p);
+    if (lane == 0) y[j] -= sj;
+    if (i0 < nw) y[i0] -= sj * v[i0];
+    if (i1 < nw) y[i1] -= sj * v[i1];
+    house(j + 1);
+    const double* v2 = QR + (j + 1) * nw;
+    const int k0 = j + 2 + lane, k1 = k0 + 64;
+    const double q = wave_sum((k0 < nw ? v[k0] * v2[k0] : 0.0) + (k1 < nw ? v[k1] * v2[k1] : 0.0));
+    if (lane == 0) cpair[j >> 1] = v[j + 1] + q;
+  };
+  if (m > 0 && wid == 0) house2(0);
   __syncthreads();
-  for (int j = 0; j + 1 < m; ++j) {
-    const double bj = beta[j];
-    const double* x = QR + j * nw;
-    group_dots<8>(m - j - 1, nw - j - 1, QR + (j + 1) * nw + j + 1, nw, 1, x + j + 1, 1,
-                  [&](int kk, double d) { sdot[j + 1 + kk] = (QR[(j + 1 + kk) * nw + j] + d) * bj; });
+  for (int j = 0; j + 2 < m; j += 2) {
+    const double b0 = beta[j], b1 = beta[j + 1], cj = cpair[j >> 1];
+    const double* v0 = QR + j * nw;
+    const double* v1 = QR + (j + 1) * nw;
+    {  // both dots of columns k >= j+2, 8 lanes per column
+      const int part = tid & 7;
+      const int ncol = m - j - 2;
+      for (int base = 0; base < ncol * 8; base += blockDim.x) {
+        const int kk = (base + tid) >> 3;
+        const bool act = kk < ncol;
+        double a0 = 0.0, a1 = 0.0;
+        const double* y = QR + (j + 2 + kk) * nw;
+        if (act)
+          for (int i = j + 2 + part; i < nw; i += 8) {
+            const double yi = y[i];
+            a0 += v0[i] * yi;
+            a1 += v1[i] * yi;
+          }
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+          a0 += __shfl_xor(a0, o);
+          a1 += __shfl_xor(a1, o);
+        }
+        if (act && part == 0) {
+          const double yj = y[j], yj1 = y[j + 1];
+          const double s0 = b0 * (yj + v0[j + 1] * yj1 + a0);
+          s0v[j + 2 + kk] = s0;
+          s1v[j + 2 + kk] = b1 * (yj1 + a1 - s0 * cj);
+        }
+      }
+    }
     __syncthreads();
+    // update rows i >= j of every later column: y_i -= s0 v0'_i + s1 v1'_i
+    auto upd = [&](int k) {
+      double* y = QR + k * nw;
+      const double s0 = s0v[k], s1 = s1v[k];
+      for (int i = j + lane; i < nw; i += 64) {
+        const double w0 = i == j ? 1.0 : v0[i];
+        const double w1 = i == j ? 0.0 : (i == j + 1 ? 1.0 : v1[i]);
+        y[i] -= s0 * w0 + s1 * w1;
+      }
+    };
     if (wid == 0) {
-      double* y = QR + (j + 1) * nw;
-      const double sk = sdot[j + 1];
-      for (int i = j + lane; i < nw; i += 64) y[i] -= sk * (i == j ? 1.0 : x[i]);
-      house(j + 1);
+      upd(j + 2);
+      if (j + 3 < m) upd(j + 3);
+      house2(j + 2);
     } else {
-      // rows i0 = j + lane, i1 = i0 + 64 of every later column; four columns per round, loads first
-      const int i0 = j + lane, i1 = i0 + 64;
-      const double xa = i0 < nw ? (i0 == j ? 1.0 : x[i0]) : 0.0;
-      const double xb = i1 < nw ? x[i1] : 0.0;
-      const int ks = nwaves - 1;
-      for (int k = j + 1 + wid; k < m; k += 4 * ks) {
-        double ya[4], yb[4], sk[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int kk = k + u * ks;
-          ya[u] = (kk < m && i0 < nw) ? QR[kk * nw + i0] : 0.0;
-          yb[u] = (kk < m && i1 < nw) ? QR[kk * nw + i1] : 0.0;
-          sk[u] = kk < m ? sdot[kk] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int kk = k + u * ks;
-          if (kk < m && i0 < nw) QR[kk * nw + i0] = ya[u] - sk[u] * xa;
-          if (kk < m && i1 < nw) QR[kk * nw + i1] = yb[u] - sk[u] * xb;
-        }
+      for (int k = j + 2 + 2 * wid; k < m; k += 2 * (nwaves - 1)) {
+        upd(k);
+        if (k + 1 < m) upd(k + 1);
       }
     }
     __syncthreads();
   }
   KKT_MARK(1);
-  // ---- Q = H_0 ... H_{m-1} I (backward accumulation), one thread per column
+  // ---- Q = H_0 ... H_{m-1} I, backward, a pair of reflectors per pass (the QR's pairs): per
+  // column q of Q, s1 = beta_{j+1} (q_{j+1} + v_{j+1}^T q), s0 = beta_j (q_j + v_j^T q - s1 c_j),
+  // q -= s1 v_{j+1} + s0 v_j; 4 lanes per column; a lone last reflector (m odd) goes first.
   for (int i = tid; i < nw * nw; i += blockDim.x) Q[i] = (i / nw == i % nw) ? 1.0 : 0.0;
   __syncthreads();
-  for (int j = m - 1; j >= 0; --j) {
-    const double bj = beta[j];
-    if (bj != 0.0) {
-      // 4 lanes per column: partial dots over rows j+1+part (step 4), xor-reduced, then each lane
-      // updates its own rows of the column
+  {
+    const int part = tid & 3;
+    int jtop = (m & 1) ? m - 1 : m;  // pairs (j, j+1) with j even below jtop
+    if (m & 1) {
+      const int j = m - 1;
+      const double bj = beta[j];
       const double* v = QR + j * nw;
-      const int part = tid & 3;
       for (int base = 0; base < nw * 4; base += blockDim.x) {
         const int c = (base + tid) >> 2;
         const bool act = c < nw;
-        double s = 0.0, s1 = 0.0;
+        double sv = 0.0;
         if (act) {
-          if (part == 0) s = Q[j * nw + c];
-          int r = j + 1 + part;
-          for (; r + 4 < nw; r += 8) {
-            s += v[r] * Q[r * nw + c];
-            s1 += v[r + 4] * Q[(r + 4) * nw + c];
-          }
-          if (r < nw) s += v[r] * Q[r * nw + c];
+          if (part == 0) sv = Q[j * nw + c];
+          for (int r = j + 1 + part; r < nw; r += 4) sv += v[r] * Q[r * nw + c];
         }
-        s += s1;
-        s += __shfl_xor(s, 1);
-        s += __shfl_xor(s, 2);
-        s *= bj;
+        sv += __shfl_xor(sv, 1);
+        sv += __shfl_xor(sv, 2);
+        sv *= bj;
         if (act) {
-          if (part == 0) Q[j * nw + c] -= s;
-          // load four rows, then store them (the rows are this lane's own: no aliasing between them)
-          int r = j + 1 + part;
-          for (; r + 12 < nw; r += 16) {
-            const double q0 = Q[r * nw + c], q1 = Q[(r + 4) * nw + c], q2 = Q[(r + 8) * nw + c],
-                         q3 = Q[(r + 12) * nw + c];
-            const double w0 = v[r], w1 = v[r + 4], w2 = v[r + 8], w3 = v[r + 12];
-            Q[r * nw + c] = q0 - s * w0;
-            Q[(r + 4) * nw + c] = q1 - s * w1;
-            Q[(r + 8) * nw + c] = q2 - s * w2;
-            Q[(r + 12) * nw + c] = q3 - s * w3;
-          }
-          for (; r < nw; r += 4) Q[r * nw + c] -= s * v[r];
+          if (part == 0) Q[j * nw + c] -= sv;
+          for (int r = j + 1 + part; r < nw; r += 4) Q[r * nw + c] -= sv * v[r];
         }
       }
+      __syncthreads();
     }
-    __syncthreads();
+    for (int j = jtop - 2; j >= 0; j -= 2) {
+      const double b0 = beta[j], b1 = beta[j + 1], cj = cpair[j >> 1];
+      const double* v0 = QR + j * nw;
+      const double* v1 = QR + (j + 1) * nw;
+      for (int base = 0; base < nw * 4; base += blockDim.x) {
+        const int c = (base + tid) >> 2;
+        const bool act = c < nw;
+        double a0 = 0.0, a1 = 0.0;
+        if (act)
+          for (int r = j + 2 + part; r < nw; r += 4) {
+            const double qr = Q[r * nw + c];
+            a0 += v0[r] * qr;
+            a1 += v1[r] * qr;
+          }
+        a0 += __shfl_xor(a0, 1);
+        a0 += __shfl_xor(a0, 2);
+        a1 += __shfl_xor(a1, 1);
+        a1 += __shfl_xor(a1, 2);
+        if (act) {
+          const double qj = Q[j * nw + c], qj1 = Q[(j + 1) * nw + c];
+          const double s1 = b1 * (qj1 + a1);
+          const double s0 = b0 * (qj + v0[j + 1] * qj1 + a0 - s1 * cj);
+          if (part == 0) {
+            Q[j * nw + c] = qj - s0;
+            Q[(j + 1) * nw + c] = qj1 - s1 - s0 * v0[j + 1];
+          }
+          for (int r = j + 2 + part; r < nw; r += 4) Q[r * nw + c] -= s1 * v1[r] + s0 * v0[r];
+        }
+      }
+      __syncthreads();
+    }
   }
   KKT_MARK(2);
   // ---- rank deficiency: delta_c on R's diagonal
