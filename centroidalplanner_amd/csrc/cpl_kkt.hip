@@ -49,31 +49,32 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-// Right-looking Cholesky of the n x n matrix H (row-major, stride n) in LDS, lower factor in place.
-// Returns true on success (every pivot above pivot_min and finite).  All threads call it.
-__device__ bool lds_cholesky(double* H, int n, int* flag, double pivot_min) {
-  const int tid = threadIdx.x;
-  if (tid == 0) *flag = 0;
-  __syncthreads();
+// Right-looking Cholesky of the n x n matrix H (row-major, stride n) in LDS, lower factor in place,
+// by one wave (wave-uniform control flow, no workgroup barriers): lanes own rows; LDS accesses of
+// one wave complete in order, so a lane reads the column entries other lanes scaled in the
+// previous instruction.  Returns true (wave-uniform) when every pivot is above pivot_min and finite.
+__device__ bool wave_cholesky(double* H, int n, double pivot_min) {
+  const int lane = threadIdx.x & 63;
+  __builtin_amdgcn_wave_barrier();
   for (int k = 0; k < n; ++k) {
-    if (tid == 0) {
-      const double d = H[k * n + k];
-      if (!(d > pivot_min) || !(d < INFINITY)) *flag = 1;
-      H[k * n + k] = sqrt(d > 0.0 ? d : 1.0);
+    const double d = H[k * n + k];
+    if (!(d > pivot_min) || !(d < INFINITY)) return false;
+    const double lkk = sqrt(d);
+    const double inv = 1.0 / lkk;
+    for (int i = k + 1 + lane; i < n; i += 64) H[i * n + k] *= inv;
+    if (lane == 0) H[k * n + k] = lkk;
+    __builtin_amdgcn_wave_barrier();
+    // trailing update of the lower triangle, the (i, j) entries of the trailing square spread over
+    // the lanes (independent read-modify-writes, about four per lane at n = 17)
+    const int sq = n - k - 1;
+    for (int e = lane; e < sq * sq; e += 64) {
+      const int ii = e / sq, jj = e - ii * sq;
+      if (jj <= ii) {
+        const int i = k + 1 + ii, j = k + 1 + jj;
+        H[i * n + j] -= H[i * n + k] * H[j * n + k];
+      }
     }
-    __syncthreads();
-    if (*flag) return false;
-    const double lkk = H[k * n + k];
-    for (int i = k + 1 + tid; i < n; i += blockDim.x) H[i * n + k] /= lkk;
-    __syncthreads();
-    // trailing update of the lower triangle, (i, j) with k < j <= i < n: (row, column-chunk) items
-    const int t = n - k - 1;
-    for (int p = tid; p < t * 4; p += blockDim.x) {
-      const int i = k + 1 + p / 4, c0 = p % 4;
-      const double lik = H[i * n + k];
-      for (int j = k + 1 + c0; j <= i; j += 4) H[i * n + j] -= lik * H[j * n + k];
-    }
-    __syncthreads();
+    __builtin_amdgcn_wave_barrier();
   }
   return true;
 }
@@ -552,27 +553,32 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
     }
     __syncthreads();
     KKT_MARK(3);
-    // ---- inertia correction: Cholesky of Hr + delta_w I, IPOPT's delta_w schedule
-    const double last = dw_last ? dw_last[b] : 0.0;
-    double dW = 0.0;
-    int32_t inf = 0;
-    // a pivot at or below DBL_EPSILON max|M_ii| — the rounding level of Z^T M Z's entries, M
-    // carrying barrier terms up to ~1e12 — counts as a zero eigenvalue (wrong inertia, as IPOPT
-    // counts zero eigenvalues): numerically flat directions get delta_w, not an unbounded step
-    double mmax = 0.0;
-    for (int a = 0; a < nw; ++a) mmax = fmax(mmax, fabs(M[a * nw + a]));
-    const double pivot_min = 2.220446049250313e-16 * mmax;
-    for (int attempt = 0; attempt < 64; ++attempt) {
-      for (int e = tid; e < nz * nz; e += blockDim.x) L[e] = Hsave[e] + ((e / nz == e % nz) ? dW : 0.0);
-      __syncthreads();
-      if (lds_cholesky(L, nz, &sh.flag, pivot_min)) break;
-      if (dW == 0.0) dW = last == 0.0 ? 1e-4 : fmax(1e-20, last / 3.0);
-      else dW *= last == 0.0 ? 100.0 : 8.0;
-      if (dW > 1e40) { inf = 1; break; }
-      __syncthreads();
+    // ---- inertia correction: Cholesky of Hr + delta_w I, IPOPT's delta_w schedule — wave 0 alone
+    // (no workgroup barriers inside the retry loop; the other waves wait at the next barrier)
+    if (tid < 64) {
+      const double last = dw_last ? dw_last[b] : 0.0;
+      double dW = 0.0;
+      int32_t inf = 0;
+      // a pivot at or below DBL_EPSILON max|M_ii| — the rounding level of Z^T M Z's entries, M
+      // carrying barrier terms up to ~1e12 — counts as a zero eigenvalue (wrong inertia, as IPOPT
+      // counts zero eigenvalues): numerically flat directions get delta_w, not an unbounded step
+      double mmax = 0.0;
+      for (int a = tid; a < nw; a += 64) mmax = fmax(mmax, fabs(M[a * nw + a]));
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mmax = fmax(mmax, __shfl_xor(mmax, o));
+      const double pivot_min = 2.220446049250313e-16 * mmax;
+      for (int attempt = 0; attempt < 64; ++attempt) {
+        for (int e = tid; e < nz * nz; e += 64) L[e] = Hsave[e] + ((e / nz == e % nz) ? dW : 0.0);
+        if (wave_cholesky(L, nz, pivot_min)) break;
+        if (dW == 0.0) dW = last == 0.0 ? 1e-4 : fmax(1e-20, last / 3.0);
+        else dW *= last == 0.0 ? 100.0 : 8.0;
+        if (dW > 1e40) { inf = 1; break; }
+      }
+      if (tid == 0) {
+        sh.delta_w = dW;
+        if (info) info[b] = inf;
+      }
     }
-    if (tid == 0) sh.delta_w = dW;
-    if (tid == 0 && info) info[b] = inf;
     __syncthreads();
   } else {
     if (tid == 0) { sh.delta_w = 0.0; if (info) info[b] = 0; }
