@@ -131,8 +131,9 @@ SIGNATURES = {
         [c_int64, c_int32, c_int32, c_int32, c_int32, c_double, c_double, c_int32] + [c_void_p] * 26,
     ),
     "cpl_ipm_max_step": (c_int32, [c_int64, c_int32] + [c_void_p] * 11),
-    "cpl_ipm_newton_setup": (c_int32, [c_int64, c_int32, c_int32, c_int32] + [c_void_p] * 17 + [c_int32]
+    "cpl_ipm_newton_setup": (c_int32, [c_int64, c_int32, c_int32, c_int32] + [c_void_p] * 14 + [c_int32]
                              + [c_void_p] * 8),
+    "cpl_ipm_fd_hessian_raw": (c_int32, [c_int64, c_int32, c_int32] + [c_void_p] * 5),
     "cpl_ipm_fd_points": (c_int32, [c_int64, c_int32, c_int32, c_double] + [c_void_p] * 5),
     "cpl_ipm_post_step": (c_int32, [c_int64, c_int32] + [c_void_p] * 23),
     "cpl_ipm_accept": (c_int32, [c_int64, c_int32, c_int32, c_int32] + [c_void_p] * 30),

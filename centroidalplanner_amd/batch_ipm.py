@@ -541,9 +541,11 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         gLfd = hfd = None
         if use_bfgs:
             Hblk = S["Hq"]
-        elif use_hip:  # central differences formed inside the Newton setup kernel
-            Hblk = None
+        elif use_hip:  # raw central differences here, symmetrised inside the Newton setup kernel
             gLfd, hfd = fd_grads_dev(unpack(w), y)
+            Hblk = torch.empty(B, nf, nf, dtype=dt, device=dev)
+            _abi.check(_abi.lib.cpl_ipm_fd_hessian_raw(B, n, nf, _ptr(free), _ptr(gLfd), _ptr(hfd), _ptr(Hblk),
+                                                       stream()))
         else:
             Hblk = fd_hessian(unpack(w), y)
         if use_hip:  # Newton system: one fused launch (csrc/cpl_ipm.hip)
@@ -554,8 +556,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
             _abi.check(_abi.lib.cpl_ipm_newton_setup(
                 B, nw, m, nf, _ptr(w), _ptr(zL), _ptr(zU), _ptr(gradw), _ptr(A), _ptr(y), _ptr(c),
                 _ptr(cur["f"]), _ptr(mu), _ptr(hasL_u8), _ptr(hasU_u8), _ptr(wl0), _ptr(wu0),
-                None if Hblk is None else _ptr(Hblk.contiguous()), None if gLfd is None else _ptr(gLfd),
-                None if hfd is None else _ptr(hfd), _ptr(free), n,
+                None if Hblk is None else _ptr(Hblk.contiguous()), 0 if use_bfgs else 1,
                 _ptr(M), _ptr(r1), _ptr(r2), _ptr(gphi), _ptr(mr_diag), _ptr(theta_k), _ptr(phi_k), stream()))
         else:
             dl = torch.where(hasL, w - wl0, torch.ones_like(w))

@@ -261,8 +261,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
     const double* __restrict__ zU, const double* __restrict__ gw, const double* __restrict__ A,
     const double* __restrict__ y, const double* __restrict__ c, const double* __restrict__ f,
     const double* __restrict__ mu, const uint8_t* __restrict__ hasL, const uint8_t* __restrict__ hasU,
-    const double* __restrict__ wl0, const double* __restrict__ wu0, const double* __restrict__ H,
-    const double* __restrict__ gL, const double* __restrict__ hfd, const int64_t* __restrict__ free_idx, int n,
+    const double* __restrict__ wl0, const double* __restrict__ wu0, const double* __restrict__ H, int h_sym,
     double* __restrict__ M, double* __restrict__ r1, double* __restrict__ r2, double* __restrict__ gphi,
     double* __restrict__ mr_diag, double* __restrict__ theta, double* __restrict__ phi) {
   const int64_t b = (int64_t)blockIdx.x * IPM_WAVES + (threadIdx.x >> 6);
@@ -303,21 +302,12 @@ __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS stores have landed
   __builtin_amdgcn_wave_barrier();
   const double* Hb = H ? H + b * (int64_t)nf * nf : nullptr;
-  // or the central-difference Hessian straight from the Lagrangian gradients of the 2 nf points
-  // (the operations of batch_ipm.py fd_hessian: (gL+ - gL-) / (2 h), then 0.5 (H + H^T))
-  const double* gb = gL ? gL + b * (int64_t)2 * nf * n : nullptr;
+  // h_sym: H is the raw central-difference matrix (cpl_ipm_fd_hessian_raw), symmetrised here as
+  // batch_ipm.py's fd_hessian does: 0.5 (H + H^T)
   for (int e = lane; e < nw * nw; e += 64) {
     const int k = e / nw, j = e - k * nw;
     double v = (j == k) ? sg[k] : 0.0;
-    if (k < nf && j < nf) {
-      if (Hb) {
-        v += Hb[k * nf + j];
-      } else if (gb) {
-        const double hk = (gb[k * n + free_idx[j]] - gb[(nf + k) * n + free_idx[j]]) / (2.0 * hfd[b * nf + k]);
-        const double hj = (gb[j * n + free_idx[k]] - gb[(nf + j) * n + free_idx[k]]) / (2.0 * hfd[b * nf + j]);
-        v += 0.5 * (hk + hj);
-      }
-    }
+    if (Hb && k < nf && j < nf) v += h_sym ? 0.5 * (Hb[k * nf + j] + Hb[j * nf + k]) : Hb[k * nf + j];
     Mb[e] = v;
   }
   double th = 0.0;
@@ -504,6 +494,25 @@ __global__ __launch_bounds__(256) void cpl_ipm_fd_points_kernel(int64_t total, i
   Xp[e] = v;
 }
 
+// Raw central-difference Hessian of the Lagrangian over the free variables (batch_ipm.py
+// fd_hessian): H[b, k, j] = (gL[b, k, free j] - gL[b, nf + k, free j]) / (2 h[b, k]); thread per
+// entry, rows of gL read contiguously.  Symmetrised by the Newton setup.
+__global__ __launch_bounds__(256) void cpl_ipm_fd_hessian_raw_kernel(int64_t total, int n, int nf,
+                                                                     const int64_t* __restrict__ free_idx,
+                                                                     const double* __restrict__ gL,
+                                                                     const double* __restrict__ h,
+                                                                     double* __restrict__ H) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int per = nf * nf;
+  const int64_t b = e / per;
+  const int kj = (int)(e - b * per);
+  const int k = kj / nf, j = kj - k * nf;
+  const double* gb = gL + b * (int64_t)2 * nf * n;
+  const int64_t c = free_idx[j];
+  H[e] = (gb[(int64_t)k * n + c] - gb[(int64_t)(nf + k) * n + c]) / (2.0 * h[b * nf + k]);
+}
+
 }  // namespace cpl
 
 using namespace cpl;
@@ -615,18 +624,16 @@ int32_t cpl_ipm_newton_setup(int64_t batch, int32_t nw, int32_t m, int32_t nf, c
                              const double* d_zU, const double* d_gw, const double* d_A, const double* d_y,
                              const double* d_c, const double* d_f, const double* d_mu, const uint8_t* d_hasL,
                              const uint8_t* d_hasU, const double* d_wl0, const double* d_wu0, const double* d_H,
-                             const double* d_gL, const double* d_hfd, const int64_t* d_free_idx, int32_t n,
-                             double* d_M, double* d_r1, double* d_r2, double* d_gphi, double* d_mr_diag,
+                             int32_t h_sym, double* d_M, double* d_r1, double* d_r2, double* d_gphi, double* d_mr_diag,
                              double* d_theta, double* d_phi, void* stream) {
   if (batch < 0 || nw <= 0 || m < 0 || nf < 0 || nf > nw) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_newton_setup: bad sizes");
   if (batch == 0) return CPL_OK;
   if (!d_w || !d_zL || !d_zU || !d_gw || (m > 0 && (!d_A || !d_y || !d_c || !d_r2)) || !d_f || !d_mu || !d_hasL ||
-      !d_hasU || !d_wl0 || !d_wu0 || !d_M || !d_r1 || !d_gphi || !d_mr_diag || !d_theta || !d_phi ||
-      (d_gL && (!d_hfd || !d_free_idx || n < nf)))
+      !d_hasU || !d_wl0 || !d_wu0 || !d_M || !d_r1 || !d_gphi || !d_mr_diag || !d_theta || !d_phi)
     return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_newton_setup: missing buffer");
   IPM_LAUNCH(cpl_ipm_newton_setup_kernel, "cpl_ipm_newton_setup", batch, (int)nw, (int)m, (int)nf, d_w, d_zL, d_zU,
-             d_gw, d_A, d_y, d_c, d_f, d_mu, d_hasL, d_hasU, d_wl0, d_wu0, d_H, d_gL, d_hfd, d_free_idx, (int)n, d_M,
-             d_r1, d_r2, d_gphi, d_mr_diag, d_theta, d_phi);
+             d_gw, d_A, d_y, d_c, d_f, d_mu, d_hasL, d_hasU, d_wl0, d_wu0, d_H, (int)h_sym, d_M, d_r1, d_r2, d_gphi,
+             d_mr_diag, d_theta, d_phi);
 }
 
 int32_t cpl_ipm_post_step(int64_t batch, int32_t nw, const double* d_w, const double* d_dw, const double* d_zL,
@@ -711,6 +718,21 @@ int32_t cpl_ipm_fd_points(int64_t batch, int32_t n, int32_t nf, double fd_step, 
                      (int)n, (int)nf, fd_step, d_freepos, d_X, d_Xp, d_h);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_ipm_fd_points launch: ") + hipGetErrorString(e));
+  return CPL_OK;
+}
+
+int32_t cpl_ipm_fd_hessian_raw(int64_t batch, int32_t n, int32_t nf, const int64_t* d_free_idx, const double* d_gL,
+                               const double* d_h, double* d_H, void* stream) {
+  if (batch < 0 || n <= 0 || nf < 0 || nf > n) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_fd_hessian_raw: bad sizes");
+  if (batch == 0 || nf == 0) return CPL_OK;
+  if (!d_free_idx || !d_gL || !d_h || !d_H) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_fd_hessian_raw: missing buffer");
+  const int64_t total = batch * (int64_t)nf * nf;
+  const int64_t blocks = (total + 255) / 256;
+  if (blocks > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_fd_hessian_raw: batch too large");
+  hipLaunchKernelGGL(cpl_ipm_fd_hessian_raw_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, total,
+                     (int)n, (int)nf, d_free_idx, d_gL, d_h, d_H);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_ipm_fd_hessian_raw launch: ") + hipGetErrorString(e));
   return CPL_OK;
 }
 

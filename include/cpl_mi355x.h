@@ -295,12 +295,13 @@ int32_t cpl_ipm_max_step(int64_t batch, int32_t nw, const double* d_v, const dou
                          const double* d_up, const double* d_tau, double* d_out, void* stream);
 /*
  * cpl_ipm_newton_setup: Sigma, grad_phi, r1 = -(grad_phi + A^T y), r2 = -c, M = diag(Sigma) + the
- *   nf x nf Hessian block — d_H, or (d_H = NULL, d_gL != NULL) the central differences of the
- *   Lagrangian gradients d_gL [batch, 2 nf, n] with steps d_hfd [batch, nf], symmetrised —
- *   theta = |c|_1, the barrier objective phi and the feasibility step's diagonal
+ *   nf x nf Hessian block d_H (NULL: none; h_sym: d_H is the raw central-difference matrix and
+ *   0.5 (H + H^T) is added) — theta = |c|_1, the barrier objective phi and the feasibility step's diagonal
  *   Sigma + sqrt(mu) / max(1, |w|)^2, per instance.
  * cpl_ipm_fd_points: the 2 nf central-difference points x +- h e_k of every instance
  *   (h = fd_step max(|x_k|, 1); freepos[col] = free index of a column or -1) and the steps.
+ * cpl_ipm_fd_hessian_raw: (gL[k, free j] - gL[nf + k, free j]) / (2 h_k) from the Lagrangian
+ *   gradients at those points, [batch, nf, nf].
  * cpl_ipm_post_step: dzL, dzU from the primal step, the primal and dual fraction-to-the-boundary
  *   steps, gd = grad_phi . dw, the switching-condition flag, delta_w_last on active instances.
  * cpl_ipm_accept: filter augmentation / reset, y, z (kappa_Sigma safeguard), w, mu and iteration
@@ -311,9 +312,10 @@ int32_t cpl_ipm_newton_setup(int64_t batch, int32_t nw, int32_t m, int32_t nf, c
                              const double* d_zU, const double* d_gw, const double* d_A, const double* d_y,
                              const double* d_c, const double* d_f, const double* d_mu, const uint8_t* d_hasL,
                              const uint8_t* d_hasU, const double* d_wl0, const double* d_wu0, const double* d_H,
-                             const double* d_gL, const double* d_hfd, const int64_t* d_free_idx, int32_t n,
-                             double* d_M, double* d_r1, double* d_r2, double* d_gphi, double* d_mr_diag,
+                             int32_t h_sym, double* d_M, double* d_r1, double* d_r2, double* d_gphi, double* d_mr_diag,
                              double* d_theta, double* d_phi, void* stream);
+int32_t cpl_ipm_fd_hessian_raw(int64_t batch, int32_t n, int32_t nf, const int64_t* d_free_idx, const double* d_gL,
+                               const double* d_h, double* d_H, void* stream);
 int32_t cpl_ipm_fd_points(int64_t batch, int32_t n, int32_t nf, double fd_step, const int32_t* d_freepos,
                           const double* d_X, double* d_Xp, double* d_h, void* stream);
 int32_t cpl_ipm_post_step(int64_t batch, int32_t nw, const double* d_w, const double* d_dw, const double* d_zL,
