@@ -1,0 +1,226 @@
+"""The solve loop's fused per-instance kernels (csrc/cpl_ipm.hip) against numpy restatements of the
+tensor code they replace (centroidalplanner_amd/batch_ipm.py, host path), on random instances with
+the edge cases the loop meets: infinite bounds, inactive instances, NaN Jacobian entries (a cone at
+zero tangential force), empty filters.  Decisions must agree exactly; sums agree to rounding
+(the kernels reduce in a different order), tolerance 1e-12 relative (1e-14 absolute where a
+residual cancels by construction)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from centroidalplanner_amd import _abi
+
+RTOL = 1e-12
+
+
+def _dev():
+    import torch
+
+    return torch.device("cuda:0")
+
+
+def _t(a, dtype=None):
+    import torch
+
+    a = np.ascontiguousarray(a)
+    return torch.as_tensor(a, device=_dev()) if dtype is None else torch.as_tensor(a, dtype=dtype, device=_dev())
+
+
+_KEEP = []
+
+
+def _p(t):
+    """Device pointer of t; t is kept alive until the test ends (a temporary's memory would be reused
+    by the next allocation before the kernel runs)."""
+    _KEEP.append(t)
+    return ctypes.c_void_p(t.data_ptr())
+
+
+@pytest.fixture(autouse=True)
+def _release():
+    yield
+    _KEEP.clear()
+
+
+def _bounds(rng, nw):
+    wl = rng.normal(size=nw) - 2.0
+    wu = wl + rng.uniform(1.0, 5.0, size=nw)
+    hasL = rng.uniform(size=nw) < 0.8
+    hasU = rng.uniform(size=nw) < 0.6
+    return np.where(hasL, wl, 0.0), np.where(hasU, wu, 0.0), hasL, hasU
+
+
+def _interior(rng, B, wl0, wu0, hasL, hasU):
+    lo = np.where(hasL, wl0, wu0 - 10.0)
+    hi = np.where(hasU, wu0, wl0 + 10.0)
+    lo = np.where(~hasL & ~hasU, -3.0, lo)
+    hi = np.where(~hasL & ~hasU, 3.0, hi)
+    return lo + (hi - lo) * rng.uniform(0.05, 0.95, size=(B, lo.size))
+
+
+@pytest.mark.gpu
+def test_max_step_primal_and_dual():
+    rng = np.random.default_rng(1)
+    B, nw = 37, 23
+    wl0, wu0, hasL, hasU = _bounds(rng, nw)
+    w = _interior(rng, B, wl0, wu0, hasL, hasU)
+    d = rng.normal(scale=3.0, size=(B, nw))
+    tau = rng.uniform(0.99, 0.999, size=B)
+
+    def ref_side(v, dv, mask, lo):
+        r = np.where(mask & (dv < 0), -tau[:, None] * (v - lo) / np.where(dv < 0, dv, -1.0), np.inf)
+        return np.minimum(r.min(1), 1.0)
+
+    ref = np.minimum(ref_side(w, d, hasL, wl0), ref_side(-w, -d, hasU, -wu0))
+    out = _t(np.zeros(B))
+    hl, hu = _t(hasL.astype(np.uint8)), _t(hasU.astype(np.uint8))
+    _abi.check(_abi.lib.cpl_ipm_max_step(B, nw, _p(_t(w)), _p(_t(d)), None, None, _p(hl), _p(hu), _p(_t(wl0)),
+                                         _p(_t(wu0)), _p(_t(tau)), _p(out), None))
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=RTOL)
+    # dual: multipliers zL (hasL), zU (hasU) kept positive
+    zL, zU = rng.uniform(0.1, 2.0, size=(B, nw)), rng.uniform(0.1, 2.0, size=(B, nw))
+    dzL, dzU = rng.normal(size=(B, nw)), rng.normal(size=(B, nw))
+    ref = np.minimum(ref_side(zL, dzL, hasL, 0.0), ref_side(zU, dzU, hasU, 0.0))
+    _abi.check(_abi.lib.cpl_ipm_max_step(B, nw, _p(_t(zL)), _p(_t(dzL)), _p(_t(zU)), _p(_t(dzU)), _p(hl), _p(hu),
+                                         None, None, _p(_t(tau)), _p(out), None))
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=RTOL)
+
+
+@pytest.mark.gpu
+def test_dense_a_from_csr_values():
+    rng = np.random.default_rng(2)
+    B, m, n = 29, 11, 17
+    dense_mask = rng.uniform(size=(m, n)) < 0.3
+    iRow, jCol = np.nonzero(dense_mask)
+    nnz = iRow.size
+    fixed = np.zeros(n, dtype=bool)
+    fixed[[3, 9]] = True
+    free = np.where(~fixed)[0]
+    nf = free.size
+    I = np.array([2, 5, 6, 10])  # inequality rows
+    nI = I.size
+    nw = nf + nI
+    jac = rng.normal(size=(B, nnz))
+    jac[::4, 0] = np.nan
+    pos = np.full(m * n, -1, dtype=np.int64)
+    pos[iRow * n + jCol] = np.arange(nnz)
+    amap = pos.reshape(m, n)[:, free].astype(np.int32)
+    row_slack = np.full(m, -1, dtype=np.int32)
+    row_slack[I] = np.arange(nI)
+    ref = np.zeros((B, m, nw))
+    J = np.zeros((B, m, n))
+    J[:, iRow, jCol] = np.nan_to_num(jac, nan=0.0)
+    ref[:, :, :nf] = J[:, :, free]
+    ref[:, I, nf + np.arange(nI)] = -1.0
+    A = _t(np.full((B, m, nw), 7.0))
+    _abi.check(_abi.lib.cpl_ipm_dense_a(B, m, nw, nf, nnz, _p(_t(amap)), _p(_t(row_slack)), _p(_t(jac)), _p(A), None))
+    np.testing.assert_array_equal(A.cpu().numpy(), ref)
+
+
+@pytest.mark.gpu
+def test_fd_points_and_raw_hessian():
+    rng = np.random.default_rng(3)
+    B, n = 13, 9
+    fixed = np.zeros(n, dtype=bool)
+    fixed[4] = True
+    free = np.where(~fixed)[0]
+    nf = free.size
+    X = rng.normal(scale=2.0, size=(B, n))
+    freepos = np.full(n, -1, dtype=np.int32)
+    freepos[free] = np.arange(nf)
+    Xp, h = _t(np.zeros((B * 2 * nf, n))), _t(np.zeros((B, nf)))
+    _abi.check(_abi.lib.cpl_ipm_fd_points(B, n, nf, 1e-6, _p(_t(freepos)), _p(_t(X)), _p(Xp), _p(h), None))
+    h_ref = 1e-6 * np.maximum(np.abs(X[:, free]), 1.0)
+    P = np.repeat(X[:, None, :], 2 * nf, axis=1)
+    P[:, np.arange(nf), free] += h_ref
+    P[:, nf + np.arange(nf), free] -= h_ref
+    np.testing.assert_array_equal(h.cpu().numpy(), h_ref)
+    np.testing.assert_array_equal(Xp.cpu().numpy(), P.reshape(B * 2 * nf, n))
+    gL = rng.normal(size=(B * 2 * nf, n))
+    H = _t(np.zeros((B, nf, nf)))
+    _abi.check(_abi.lib.cpl_ipm_fd_hessian_raw(B, n, nf, _p(_t(free.astype(np.int64))), _p(_t(gL)), _p(h), _p(H),
+                                               None))
+    g3 = gL.reshape(B, 2 * nf, n)[:, :, free]
+    ref = (g3[:, :nf] - g3[:, nf:]) / (2.0 * h_ref[:, :, None])
+    np.testing.assert_array_equal(H.cpu().numpy(), ref)
+
+
+@pytest.mark.gpu
+def test_optimality_error_convergence_and_barrier_update():
+    import torch
+
+    rng = np.random.default_rng(4)
+    B, nw, m, FM = 41, 19, 8, 6
+    wl0, wu0, hasL, hasU = _bounds(rng, nw)
+    w = _interior(rng, B, wl0, wu0, hasL, hasU)
+    A = rng.normal(size=(B, m, nw))
+    y = rng.normal(size=(B, m))
+    zL = np.where(hasL, rng.uniform(1e-3, 2.0, size=(B, nw)), 0.0)
+    zU = np.where(hasU, rng.uniform(1e-3, 2.0, size=(B, nw)), 0.0)
+    gw = -(np.einsum("bmk,bm->bk", A, y) - zL + zU) + rng.normal(scale=10.0 ** rng.uniform(-12, 0, size=(B, 1)),
+                                                                 size=(B, nw))
+    c = rng.normal(scale=10.0 ** rng.uniform(-12, -2, size=(B, 1)), size=(B, m))
+    mu = 10.0 ** rng.uniform(-9, -1, size=B)
+    active = rng.uniform(size=B) < 0.85
+    acc = rng.integers(0, 20, size=B)
+    # instances at an optimum (every 5th) and near one (acceptable, one iteration short of 15)
+    for b0, scale in ((0, 1e-11), (1, 1e-7)):
+        sel = np.arange(b0, B, 5)
+        zL[sel] *= scale
+        zU[sel] *= scale
+        c[sel] = rng.normal(scale=scale, size=(sel.size, m))
+        gw[sel] = -(np.einsum("bmk,bm->bk", A[sel], y[sel]) - zL[sel] + zU[sel])
+        acc[sel] = 14
+        active[sel] = True
+    status = np.full(B, 2, dtype=np.int64)
+    ft, fp = rng.normal(size=(B, FM)), rng.normal(size=(B, FM))
+    fc = rng.integers(0, 9, size=B)
+    tol, acc_tol, acc_iter = 1e-8, 1e-6, 15
+    nb = int(hasL.sum() + hasU.sum())
+    # numpy restatement of batch_ipm.py errors / check / barrier update (host path)
+    dual = gw + np.einsum("bmk,bm->bk", A, y) - zL + zU
+    cl = np.where(hasL, (w - wl0) * zL, 0.0)
+    cu = np.where(hasU, (wu0 - w) * zU, 0.0)
+    zsum = np.abs(zL).sum(1) + np.abs(zU).sum(1)
+    sd = np.maximum((np.abs(y).sum(1) + zsum) / max(m + nb, 1), 100.0) / 100.0
+    sc = np.maximum(zsum / max(nb, 1), 100.0) / 100.0
+    d_inf = np.abs(dual).max(1)
+    base = np.maximum(d_inf / sd, np.abs(c).max(1))
+    err0 = np.maximum(base, np.maximum(cl.max(1), cu.max(1)) / sc)
+    done = active & (err0 <= tol)
+    acc_new = np.where(active & (err0 <= acc_tol), acc + 1, 0)
+    acc_now = active & ~done & (acc_new >= acc_iter)
+    st_ref = np.where(done, 0, np.where(acc_now, 1, status))
+    act = active & ~done & ~acc_now
+    mu_r, reset = mu.copy(), np.zeros(B, dtype=bool)
+    for _ in range(2):
+        em = np.maximum(np.abs(cl - np.where(hasL, mu_r[:, None], 0.0)).max(1),
+                        np.abs(cu - np.where(hasU, mu_r[:, None], 0.0)).max(1))
+        upd = act & (np.maximum(base, em / sc) <= 10.0 * mu_r) & (mu_r > tol / 10.0)
+        mu_r = np.where(upd, np.maximum(np.minimum(0.2 * mu_r, mu_r ** 1.5), tol / 10.0), mu_r)
+        reset |= upd
+    T = {k: _t(v) for k, v in dict(A=A, gw=gw, c=c, w=w, y=y, zL=zL, zU=zU, wl0=wl0, wu0=wu0, mu=mu, ft=ft,
+                                    fp=fp).items()}
+    fcd, actd = _t(fc.astype(np.int64)), _t(active.astype(np.uint8))
+    std, accd = _t(status), _t(acc.astype(np.int64))
+    outs = {k: torch.empty(B, dtype=torch.float64, device=_dev()) for k in ("d_inf", "err0", "base", "mu")}
+    fto, fpo, fco = torch.empty_like(T["ft"]), torch.empty_like(T["fp"]), torch.empty_like(fcd)
+    _abi.check(_abi.lib.cpl_ipm_optimality(
+        B, nw, m, FM, nb, tol, acc_tol, acc_iter, _p(T["A"]), _p(T["gw"]), _p(T["c"]), _p(T["w"]), _p(T["y"]),
+        _p(T["zL"]), _p(T["zU"]), _p(_t(hasL.astype(np.uint8))), _p(_t(hasU.astype(np.uint8))), _p(T["wl0"]),
+        _p(T["wu0"]), _p(T["mu"]), _p(T["ft"]), _p(T["fp"]), _p(fcd), _p(actd), _p(std), _p(accd), _p(outs["d_inf"]),
+        _p(outs["err0"]), _p(outs["base"]), _p(outs["mu"]), _p(fto), _p(fpo), _p(fco), None))
+    torch.cuda.synchronize()
+    # the dual residual cancels by construction: its rounding is relative to the terms (~1), not to it
+    np.testing.assert_allclose(outs["err0"].cpu().numpy(), err0, rtol=RTOL, atol=1e-14)
+    np.testing.assert_allclose(outs["d_inf"].cpu().numpy(), d_inf, rtol=RTOL, atol=1e-14)
+    # decisions: exact (instances within 1e-9 of a threshold excluded from this random sample)
+    assert not np.any(np.abs(err0 / tol - 1.0) < 1e-9) and not np.any(np.abs(err0 / acc_tol - 1.0) < 1e-9)
+    np.testing.assert_array_equal(actd.cpu().numpy().astype(bool), act)
+    np.testing.assert_array_equal(std.cpu().numpy(), st_ref)
+    np.testing.assert_array_equal(accd.cpu().numpy(), acc_new)
+    np.testing.assert_allclose(outs["mu"].cpu().numpy(), mu_r, rtol=RTOL)
+    np.testing.assert_array_equal(np.isinf(fto.cpu().numpy()).all(1), reset)
+    np.testing.assert_array_equal(fco.cpu().numpy(), np.where(reset, 0, fc))
+    assert done.any() and acc_now.any() and reset.any() and act.any()  # every branch exercised
