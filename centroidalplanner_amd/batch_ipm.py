@@ -42,7 +42,8 @@ batched call of the evaluator for all instances.  The product evaluator (KernelE
 gfx950 eval kernel through cpl_eval_batch on device-resident tensors.  Instances that converged
 stay in the batch (frozen), so every launch keeps its shape; one iteration has no host
 synchronisation at all (fixed trip counts, masked updates), and on the device it is captured once
-as a HIP graph and replayed — the host only checks every `check_every` iterations whether any
+as a HIP graph and replayed — on the device path the host reads an "any active" flag one iteration
+behind (no stall); on host tensors it checks every `check_every` iterations whether any
 instance is still active.
 """
 from __future__ import annotations
@@ -792,14 +793,38 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         per_step_evals = n_eval - e0
         n_eval = e0
         replay = gr.replay
-    while it_run < max_iter:
-        if it_run % max(1, check_every) == 0 and not bool(S["active"].any()):
-            break
-        replay()
-        n_eval += per_step_evals
-        it_run += 1
-        if verbose:
-            print(f"it {it_run:4d} active {int(S['active'].sum())}")
+    if use_hip:
+        # termination test without stalling the device: after every iteration "any active" goes to
+        # a pinned host slot behind an event; the host reads the previous iteration's slot (normally
+        # landed already) while the current iteration runs — at most one iteration past the end
+        # (a no-op: every update is masked by the active flags)
+        flag = torch.zeros(2, dtype=torch.bool).pin_memory()
+        evs = [torch.cuda.Event(), torch.cuda.Event()]
+        if not bool(S["active"].any()):
+            max_iter = it_run
+        start = it_run
+        while it_run < max_iter:
+            replay()
+            n_eval += per_step_evals
+            it_run += 1
+            k = it_run & 1
+            flag[k].copy_(S["active"].any(), non_blocking=True)
+            evs[k].record()
+            if verbose:
+                print(f"it {it_run:4d} active {int(S['active'].sum())}")
+            if it_run - start >= 2:  # the previous iteration of this loop recorded its flag
+                evs[k ^ 1].synchronize()
+                if not bool(flag[k ^ 1]):
+                    break
+    else:
+        while it_run < max_iter:
+            if it_run % max(1, check_every) == 0 and not bool(S["active"].any()):
+                break
+            replay()
+            n_eval += per_step_evals
+            it_run += 1
+            if verbose:
+                print(f"it {it_run:4d} active {int(S['active'].sum())}")
     # final convergence test at the last iterate
     check(errors({"f": S["f"], "grad": S["grad"], "g": S["g"], "J": S["J"]}, S["w"], S["y"], S["zL"], S["zU"]))
     # IPOPT honor_original_bounds: the final point is projected back into the unrelaxed bounds and
