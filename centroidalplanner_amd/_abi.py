@@ -106,7 +106,7 @@ SIGNATURES = {
     "cpl_eval_lagrangian_grad": (
         c_int32,
         [_DESC_P, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
-         c_void_p],
+         c_void_p, c_void_p],
     ),
     "cpl_lagrangian_grad": (
         c_int32,

@@ -85,7 +85,7 @@ class KernelEvaluator:
         self.calls += 1
         return self.problem.eval_batch(X, mass, self.env_tag, outputs=outputs)
 
-    def lagrangian_grad(self, X, mass, y, y_repeat, csc):
+    def lagrangian_grad(self, X, mass, y, y_repeat, csc, active=None):
         """grad f + J^T y of every instance in one fused launch (cpl_eval_lagrangian_grad: the
         Jacobian stays in LDS); None where the fused path does not exist (Superquadric / mixed
         batches: the caller takes eval + cpl_lagrangian_grad, the same result)."""
@@ -97,7 +97,8 @@ class KernelEvaluator:
         st = _abi.lib.cpl_eval_lagrangian_grad(
             ctypes.byref(self.problem.desc()), X.shape[0], _ptr(X), None if mass is None else _ptr(mass),
             None if self.env_tag is None else _ptr(self.env_tag), _ptr(csc[0]), _ptr(csc[1]), _ptr(csc[2]), _ptr(y),
-            y_repeat, _ptr(out), ctypes.c_void_p(torch.cuda.current_stream(X.device).cuda_stream))
+            y_repeat, None if active is None else _ptr(active), _ptr(out),
+            ctypes.c_void_p(torch.cuda.current_stream(X.device).cuda_stream))
         if st == _abi.ERR_UNSUPPORTED:
             self._no_fused = True
             return None
@@ -311,7 +312,9 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         n_eval += 1
         yc = yv.contiguous()
         fused = ev.lagrangian_grad if hasattr(ev, "lagrangian_grad") else None
-        gL = fused(Xp, Mass_fd, yc, 2 * nf, csc) if fused else None
+        # converged instances are skipped: their rows of gL stay unwritten and only ever feed their
+        # own (masked) Newton step
+        gL = fused(Xp, Mass_fd, yc, 2 * nf, csc, S["active"]) if fused else None
         if gL is None:
             o = ev(Xp, Mass_fd, outputs=("jac", "grad"))
             gL = torch.empty(B * 2 * nf, n, dtype=dt, device=dev)

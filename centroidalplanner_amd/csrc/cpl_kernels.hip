@@ -77,6 +77,7 @@ struct KParams {
   const int32_t* csc_k;
   const int32_t* csc_row;
   const double* ly;
+  const uint8_t* lg_active;  // optional: instance b / y_repeat inactive -> its rows are skipped
 };
 static_assert(sizeof(KParams) < 4096, "kernel parameters must fit the kernarg segment");
 
@@ -1377,6 +1378,7 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
         if (e < r_gr) {
           const int j = e % n_gr, k = e / n_gr;
           const int r = ENVK == CPL_ENV_MIXED ? lists[64 + j] : j;
+          if (!HAS_SQ && K.lg_active && !K.lg_active[(b0 + r) / K.y_repeat]) continue;
           contact_item<ENVK == CPL_ENV_NONE ? CPL_ENV_NONE : CPL_ENV_GROUND>(K, X + r * n, CPL_ENV_GROUND, k,
                                                                             Gt + r * m, Jt + r * nnz);
           continue;
@@ -1384,12 +1386,14 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
         e -= r_gr;
         if (e < r_st) {
           const int r = e % valid, sg = e / valid;
+          if (!HAS_SQ && K.lg_active && !K.lg_active[(b0 + r) / K.y_repeat]) continue;
           const double* xr = X + r * n;
           if (sg == 0) statics_values_item(K, xr, MB(cur)[r], Gt + r * m, Jt + r * nnz);
           else if (K.want_j) statics_row_item(K, xr, sg - 1, Jt + r * nnz);
           continue;
         }
         e -= r_st;
+        if (!HAS_SQ && K.lg_active && !K.lg_active[(b0 + e) / K.y_repeat]) continue;
         cost_item(K, X + e * n, f_out ? f_out + b0 + e : nullptr, Dt + e * n);
       }
     }
@@ -1399,6 +1403,7 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
       // the same result) without the Jacobian's round trip through HBM; a 0/0 entry counts as 0
       for (int e = tid; e < valid * n; e += CT) {
         const int r = e / n, j = e - r * n;
+        if (K.lg_active && !K.lg_active[(b0 + r) / K.y_repeat]) continue;  // an inactive instance
         const double* jr = Jt + r * nnz;
         const double* yb = K.ly + ((b0 + r) / K.y_repeat) * m;
         double s = Dt[r * n + j];
@@ -1674,6 +1679,7 @@ struct LGradArgs {
   const int32_t* csc_row;
   const double* y;
   int32_t y_repeat;
+  const uint8_t* active;
 };
 
 static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
@@ -1703,6 +1709,7 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
   K.y_repeat = 1;
   K.col_ptr = K.csc_k = K.csc_row = nullptr;
   K.ly = nullptr;
+  K.lg_active = nullptr;
   double* ws = nullptr;
   if (lg && !use_pipe(K))
     return fail(CPL_ERR_UNSUPPORTED, "fused Lagrangian gradient: pipelined (Ground / no environment) path only");
@@ -1718,6 +1725,7 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
       K.csc_k = lg->csc_k;
       K.csc_row = lg->csc_row;
       K.ly = lg->y;
+      K.lg_active = lg->active;
     }
     K.ablate = g_ablate;
     const size_t lds = sizeof(double) * (size_t)(K.offI + 72);
@@ -1810,12 +1818,12 @@ int32_t cpl_eval_batch(const cpl_problem_desc* d, int64_t batch, const double* d
 
 int32_t cpl_eval_lagrangian_grad(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
                                  const uint8_t* d_env_tag, const int32_t* d_col_ptr, const int32_t* d_csc_k,
-                                 const int32_t* d_csc_row, const double* d_y, int32_t y_repeat, double* d_out,
-                                 void* stream) {
+                                 const int32_t* d_csc_row, const double* d_y, int32_t y_repeat,
+                                 const uint8_t* d_active, double* d_out, void* stream) {
   if (y_repeat < 1) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_eval_lagrangian_grad: y_repeat must be >= 1");
   if (batch > 0 && (!d_col_ptr || !d_csc_k || !d_csc_row || !d_y || !d_out))
     return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_eval_lagrangian_grad: missing buffer");
-  const LGradArgs lg{d_col_ptr, d_csc_k, d_csc_row, d_y, y_repeat};
+  const LGradArgs lg{d_col_ptr, d_csc_k, d_csc_row, d_y, y_repeat, d_active};
   // jac and grad f are computed into the tile image; only grad f + J^T y is stored (to d_out)
   return launch_eval(d, batch, d_x, d_mass, d_env_tag, nullptr, nullptr, nullptr, d_out, nullptr, (hipStream_t)stream,
                      true, &lg);

@@ -232,13 +232,15 @@ int32_t cpl_lagrangian_grad(int64_t batch, int32_t n, int32_t m, int32_t nnz, co
 /*
  * cpl_eval_lagrangian_grad: grad f + J^T y of every instance straight from the eval kernel's LDS
  * tile image (the Jacobian never goes to HBM); bitwise the result of cpl_eval_batch (jac, grad)
- * followed by cpl_lagrangian_grad.  Pipelined path only (Ground / no environment): returns
- * CPL_ERR_UNSUPPORTED for Superquadric / mixed batches, whose callers take the two-launch path.
+ * followed by cpl_lagrangian_grad.  d_active (optional, one byte per y row): instances whose
+ * y row is inactive are skipped (their output rows are left unwritten).  Pipelined path only
+ * (Ground / no environment): returns CPL_ERR_UNSUPPORTED for Superquadric / mixed batches, whose
+ * callers take the two-launch path.
  */
 int32_t cpl_eval_lagrangian_grad(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
                                  const uint8_t* d_env_tag, const int32_t* d_col_ptr, const int32_t* d_csc_k,
-                                 const int32_t* d_csc_row, const double* d_y, int32_t y_repeat, double* d_out,
-                                 void* stream);
+                                 const int32_t* d_csc_row, const double* d_y, int32_t y_repeat,
+                                 const uint8_t* d_active, double* d_out, void* stream);
 int32_t cpl_kkt_solve(int32_t mode, int64_t batch, int32_t nw, int32_t m, const double* d_M, const double* d_A,
                       const double* d_r1, const double* d_r2, const double* d_mu, const double* d_delta_w_last,
                       const uint8_t* d_active, double* d_dw, double* d_dy, double* d_delta_w, double* d_delta_c,

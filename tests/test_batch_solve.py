@@ -285,3 +285,9 @@ def test_fused_lagrangian_grad_is_bitwise_the_two_launch_result():
     torch.cuda.synchronize()
     assert torch.isfinite(ref).all()
     assert torch.equal(fused, ref)
+    # converged instances skipped: the active ones bitwise the same, the others untouched
+    active = torch.as_tensor(rng.uniform(size=y.shape[0]) < 0.5, device=dev)
+    masked = KernelEvaluator(prob).lagrangian_grad(X, M, y, rep, csc, active)
+    torch.cuda.synchronize()
+    rows = active.repeat_interleave(rep)[: X.shape[0]]
+    assert torch.equal(masked[rows], ref[rows])
