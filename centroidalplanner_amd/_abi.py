@@ -132,13 +132,13 @@ SIGNATURES = {
     ),
     "cpl_ipm_max_step": (c_int32, [c_int64, c_int32] + [c_void_p] * 11),
     "cpl_ipm_newton_setup": (c_int32, [c_int64, c_int32, c_int32, c_int32] + [c_void_p] * 14 + [c_int32]
-                             + [c_void_p] * 8),
-    "cpl_ipm_fd_hessian_raw": (c_int32, [c_int64, c_int32, c_int32] + [c_void_p] * 5),
-    "cpl_ipm_fd_points": (c_int32, [c_int64, c_int32, c_int32, c_double] + [c_void_p] * 5),
+                             + [c_void_p] * 9),
+    "cpl_ipm_fd_hessian_raw": (c_int32, [c_int64, c_int32, c_int32] + [c_void_p] * 6),
+    "cpl_ipm_fd_points": (c_int32, [c_int64, c_int32, c_int32, c_double] + [c_void_p] * 6),
     "cpl_ipm_post_step": (c_int32, [c_int64, c_int32] + [c_void_p] * 23),
     "cpl_ipm_accept": (c_int32, [c_int64, c_int32, c_int32, c_int32] + [c_void_p] * 30),
     "cpl_ipm_masked_rows": (c_int32, [c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "cpl_ipm_dense_a": (c_int32, [c_int64, c_int32, c_int32, c_int32, c_int32] + [c_void_p] * 5),
+    "cpl_ipm_dense_a": (c_int32, [c_int64, c_int32, c_int32, c_int32, c_int32] + [c_void_p] * 6),
 }
 
 

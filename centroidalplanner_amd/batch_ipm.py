@@ -258,11 +258,11 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         c[:, I] = g[:, I] - s
         return c
 
-    def jac_w(J):
-        if csr_J:
+    def jac_w(J, mask=None):
+        if csr_J:  # mask: rows of inactive instances are left unwritten (never read for them)
             A_ = torch.empty(B, m, nw, dtype=dt, device=dev)
             _abi.check(_abi.lib.cpl_ipm_dense_a(B, m, nw, nf, nnz, _ptr(amap), _ptr(row_slack), _ptr(J), _ptr(A_),
-                                                stream()))
+                                                None if mask is None else _ptr(mask), stream()))
             return A_
         return torch.cat([J[:, :, free], (-P).expand(B, m, nI)], dim=2)
 
@@ -308,7 +308,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         Xp = torch.empty(B * 2 * nf, n, dtype=dt, device=dev)
         h = torch.empty(B, nf, dtype=dt, device=dev)
         _abi.check(_abi.lib.cpl_ipm_fd_points(B, n, nf, fd_step, _ptr(freepos), _ptr(Xc.contiguous()), _ptr(Xp),
-                                              _ptr(h), stream()))
+                                              _ptr(h), _ptr(S["active"]), stream()))
         n_eval += 1
         yc = yv.contiguous()
         fused = ev.lagrangian_grad if hasattr(ev, "lagrangian_grad") else None
@@ -505,7 +505,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         w, y, zL, zU, mu = S["w"], S["y"], S["zL"], S["zU"], S["mu"]
         cur = {"f": S["f"], "grad": S["grad"], "g": S["g"], "J": S["J"]}
         if use_hip:  # optimality error, convergence test and barrier update: one fused launch
-            A = jac_w(cur["J"])
+            A = jac_w(cur["J"], S["active"])
             gradw = torch.cat([cur["grad"][:, free], zeros_I], 1)
             c = cons(cur["g"], w[:, nf:])
             E = {k: torch.empty(B, dtype=dt, device=dev) for k in ("d_inf", "err0", "base")}
@@ -549,7 +549,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
             gLfd, hfd = fd_grads_dev(unpack(w), y)
             Hblk = torch.empty(B, nf, nf, dtype=dt, device=dev)
             _abi.check(_abi.lib.cpl_ipm_fd_hessian_raw(B, n, nf, _ptr(free), _ptr(gLfd), _ptr(hfd), _ptr(Hblk),
-                                                       stream()))
+                                                       _ptr(S["active"]), stream()))
         else:
             Hblk = fd_hessian(unpack(w), y)
         if use_hip:  # Newton system: one fused launch (csrc/cpl_ipm.hip)
@@ -561,7 +561,8 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                 B, nw, m, nf, _ptr(w), _ptr(zL), _ptr(zU), _ptr(gradw), _ptr(A), _ptr(y), _ptr(c),
                 _ptr(cur["f"]), _ptr(mu), _ptr(hasL_u8), _ptr(hasU_u8), _ptr(wl0), _ptr(wu0),
                 None if Hblk is None else _ptr(Hblk.contiguous()), 0 if use_bfgs else 1,
-                _ptr(M), _ptr(r1), _ptr(r2), _ptr(gphi), _ptr(mr_diag), _ptr(theta_k), _ptr(phi_k), stream()))
+                _ptr(M), _ptr(r1), _ptr(r2), _ptr(gphi), _ptr(mr_diag), _ptr(theta_k), _ptr(phi_k),
+                _ptr(S["active"]) if not use_bfgs else None, stream()))
         else:
             dl = torch.where(hasL, w - wl0, torch.ones_like(w))
             du = torch.where(hasU, wu0 - w, torch.ones_like(w))

@@ -263,9 +263,10 @@ __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
     const double* __restrict__ mu, const uint8_t* __restrict__ hasL, const uint8_t* __restrict__ hasU,
     const double* __restrict__ wl0, const double* __restrict__ wu0, const double* __restrict__ H, int h_sym,
     double* __restrict__ M, double* __restrict__ r1, double* __restrict__ r2, double* __restrict__ gphi,
-    double* __restrict__ mr_diag, double* __restrict__ theta, double* __restrict__ phi) {
+    double* __restrict__ mr_diag, double* __restrict__ theta, double* __restrict__ phi,
+    const uint8_t* __restrict__ active) {
   const int64_t b = (int64_t)blockIdx.x * IPM_WAVES + (threadIdx.x >> 6);
-  if (b >= batch) return;
+  if (b >= batch || (active && !active[b])) return;  // converged: its Newton system is never read
   const int lane = threadIdx.x & 63;
   const double mub = mu[b];
   const double* Ab = A + b * (int64_t)m * nw;
@@ -450,11 +451,13 @@ __global__ __launch_bounds__(256) void cpl_ipm_dense_a_kernel(int64_t total, int
                                                               const int32_t* __restrict__ amap,
                                                               const int32_t* __restrict__ row_slack,
                                                               const double* __restrict__ jac,
-                                                              double* __restrict__ A) {
+                                                              double* __restrict__ A,
+                                                              const uint8_t* __restrict__ active) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total) return;
   const int per = m * nw;
   const int64_t b = e / per;
+  if (active && !active[b]) return;
   const int rc = (int)(e - b * per);
   const int r = rc / nw, k = rc - r * nw;
   double v = 0.0;
@@ -476,11 +479,13 @@ __global__ __launch_bounds__(256) void cpl_ipm_dense_a_kernel(int64_t total, int
 __global__ __launch_bounds__(256) void cpl_ipm_fd_points_kernel(int64_t total, int n, int nf, double fd_step,
                                                                 const int32_t* __restrict__ freepos,
                                                                 const double* __restrict__ X,
-                                                                double* __restrict__ Xp, double* __restrict__ h_out) {
+                                                                double* __restrict__ Xp, double* __restrict__ h_out,
+                                                                const uint8_t* __restrict__ active) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total) return;
   const int per = 2 * nf * n;
   const int64_t b = e / per;
+  if (active && !active[b]) return;
   const int pc = (int)(e - b * per);
   const int p = pc / n, col = pc - p * n;
   const double xv = X[b * n + col];
@@ -501,11 +506,13 @@ __global__ __launch_bounds__(256) void cpl_ipm_fd_hessian_raw_kernel(int64_t tot
                                                                      const int64_t* __restrict__ free_idx,
                                                                      const double* __restrict__ gL,
                                                                      const double* __restrict__ h,
-                                                                     double* __restrict__ H) {
+                                                                     double* __restrict__ H,
+                                                                     const uint8_t* __restrict__ active) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total) return;
   const int per = nf * nf;
   const int64_t b = e / per;
+  if (active && !active[b]) return;
   const int kj = (int)(e - b * per);
   const int k = kj / nf, j = kj - k * nf;
   const double* gb = gL + b * (int64_t)2 * nf * n;
@@ -625,7 +632,7 @@ int32_t cpl_ipm_newton_setup(int64_t batch, int32_t nw, int32_t m, int32_t nf, c
                              const double* d_c, const double* d_f, const double* d_mu, const uint8_t* d_hasL,
                              const uint8_t* d_hasU, const double* d_wl0, const double* d_wu0, const double* d_H,
                              int32_t h_sym, double* d_M, double* d_r1, double* d_r2, double* d_gphi, double* d_mr_diag,
-                             double* d_theta, double* d_phi, void* stream) {
+                             double* d_theta, double* d_phi, const uint8_t* d_active, void* stream) {
   if (batch < 0 || nw <= 0 || m < 0 || nf < 0 || nf > nw) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_newton_setup: bad sizes");
   if (batch == 0) return CPL_OK;
   if (!d_w || !d_zL || !d_zU || !d_gw || (m > 0 && (!d_A || !d_y || !d_c || !d_r2)) || !d_f || !d_mu || !d_hasL ||
@@ -633,7 +640,7 @@ int32_t cpl_ipm_newton_setup(int64_t batch, int32_t nw, int32_t m, int32_t nf, c
     return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_newton_setup: missing buffer");
   IPM_LAUNCH(cpl_ipm_newton_setup_kernel, "cpl_ipm_newton_setup", batch, (int)nw, (int)m, (int)nf, d_w, d_zL, d_zU,
              d_gw, d_A, d_y, d_c, d_f, d_mu, d_hasL, d_hasU, d_wl0, d_wu0, d_H, (int)h_sym, d_M, d_r1, d_r2, d_gphi,
-             d_mr_diag, d_theta, d_phi);
+             d_mr_diag, d_theta, d_phi, d_active);
 }
 
 int32_t cpl_ipm_post_step(int64_t batch, int32_t nw, const double* d_w, const double* d_dw, const double* d_zL,
@@ -690,7 +697,8 @@ int32_t cpl_ipm_masked_rows(int64_t batch, int64_t row_len, const uint8_t* d_mas
 }
 
 int32_t cpl_ipm_dense_a(int64_t batch, int32_t m, int32_t nw, int32_t nf, int32_t nnz, const int32_t* d_amap,
-                        const int32_t* d_row_slack, const double* d_jac, double* d_A, void* stream) {
+                        const int32_t* d_row_slack, const double* d_jac, double* d_A, const uint8_t* d_active,
+                        void* stream) {
   if (batch < 0 || m < 0 || nw <= 0 || nf < 0 || nf > nw || nnz < 0)
     return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_dense_a: bad sizes");
   if (batch == 0 || m == 0) return CPL_OK;
@@ -700,14 +708,14 @@ int32_t cpl_ipm_dense_a(int64_t batch, int32_t m, int32_t nw, int32_t nf, int32_
   const int64_t blocks = (total + 255) / 256;
   if (blocks > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_dense_a: batch too large");
   hipLaunchKernelGGL(cpl_ipm_dense_a_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, total, (int)m,
-                     (int)nw, (int)nf, (int)nnz, d_amap, d_row_slack, d_jac, d_A);
+                     (int)nw, (int)nf, (int)nnz, d_amap, d_row_slack, d_jac, d_A, d_active);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_ipm_dense_a launch: ") + hipGetErrorString(e));
   return CPL_OK;
 }
 
 int32_t cpl_ipm_fd_points(int64_t batch, int32_t n, int32_t nf, double fd_step, const int32_t* d_freepos,
-                          const double* d_X, double* d_Xp, double* d_h, void* stream) {
+                          const double* d_X, double* d_Xp, double* d_h, const uint8_t* d_active, void* stream) {
   if (batch < 0 || n <= 0 || nf < 0 || nf > n) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_fd_points: bad sizes");
   if (batch == 0 || nf == 0) return CPL_OK;
   if (!d_freepos || !d_X || !d_Xp || !d_h) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_fd_points: missing buffer");
@@ -715,14 +723,14 @@ int32_t cpl_ipm_fd_points(int64_t batch, int32_t n, int32_t nf, double fd_step, 
   const int64_t blocks = (total + 255) / 256;
   if (blocks > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_fd_points: batch too large");
   hipLaunchKernelGGL(cpl_ipm_fd_points_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, total,
-                     (int)n, (int)nf, fd_step, d_freepos, d_X, d_Xp, d_h);
+                     (int)n, (int)nf, fd_step, d_freepos, d_X, d_Xp, d_h, d_active);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_ipm_fd_points launch: ") + hipGetErrorString(e));
   return CPL_OK;
 }
 
 int32_t cpl_ipm_fd_hessian_raw(int64_t batch, int32_t n, int32_t nf, const int64_t* d_free_idx, const double* d_gL,
-                               const double* d_h, double* d_H, void* stream) {
+                               const double* d_h, double* d_H, const uint8_t* d_active, void* stream) {
   if (batch < 0 || n <= 0 || nf < 0 || nf > n) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_fd_hessian_raw: bad sizes");
   if (batch == 0 || nf == 0) return CPL_OK;
   if (!d_free_idx || !d_gL || !d_h || !d_H) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_fd_hessian_raw: missing buffer");
@@ -730,7 +738,7 @@ int32_t cpl_ipm_fd_hessian_raw(int64_t batch, int32_t n, int32_t nf, const int64
   const int64_t blocks = (total + 255) / 256;
   if (blocks > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_fd_hessian_raw: batch too large");
   hipLaunchKernelGGL(cpl_ipm_fd_hessian_raw_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, total,
-                     (int)n, (int)nf, d_free_idx, d_gL, d_h, d_H);
+                     (int)n, (int)nf, d_free_idx, d_gL, d_h, d_H, d_active);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_ipm_fd_hessian_raw launch: ") + hipGetErrorString(e));
   return CPL_OK;

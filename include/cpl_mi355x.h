@@ -309,17 +309,19 @@ int32_t cpl_ipm_max_step(int64_t batch, int32_t nw, const double* d_v, const dou
  * cpl_ipm_accept: filter augmentation / reset, y, z (kappa_Sigma safeguard), w, mu and iteration
  *   counters written back in place.
  * cpl_ipm_masked_rows: dst[b, :] = src[b, :] where mask[b].
+ * d_active (optional, where present): instances with active[b] == 0 are skipped — their outputs
+ * are left unwritten (converged instances of the solve loop, whose Newton data is never read).
  */
 int32_t cpl_ipm_newton_setup(int64_t batch, int32_t nw, int32_t m, int32_t nf, const double* d_w, const double* d_zL,
                              const double* d_zU, const double* d_gw, const double* d_A, const double* d_y,
                              const double* d_c, const double* d_f, const double* d_mu, const uint8_t* d_hasL,
                              const uint8_t* d_hasU, const double* d_wl0, const double* d_wu0, const double* d_H,
                              int32_t h_sym, double* d_M, double* d_r1, double* d_r2, double* d_gphi, double* d_mr_diag,
-                             double* d_theta, double* d_phi, void* stream);
+                             double* d_theta, double* d_phi, const uint8_t* d_active, void* stream);
 int32_t cpl_ipm_fd_hessian_raw(int64_t batch, int32_t n, int32_t nf, const int64_t* d_free_idx, const double* d_gL,
-                               const double* d_h, double* d_H, void* stream);
+                               const double* d_h, double* d_H, const uint8_t* d_active, void* stream);
 int32_t cpl_ipm_fd_points(int64_t batch, int32_t n, int32_t nf, double fd_step, const int32_t* d_freepos,
-                          const double* d_X, double* d_Xp, double* d_h, void* stream);
+                          const double* d_X, double* d_Xp, double* d_h, const uint8_t* d_active, void* stream);
 int32_t cpl_ipm_post_step(int64_t batch, int32_t nw, const double* d_w, const double* d_dw, const double* d_zL,
                           const double* d_zU, const double* d_gphi, const double* d_mu, const double* d_tau,
                           const uint8_t* d_hasL, const uint8_t* d_hasU, const double* d_wl0, const double* d_wu0,
@@ -339,7 +341,8 @@ int32_t cpl_ipm_masked_rows(int64_t batch, int64_t row_len, const uint8_t* d_mas
 /* cpl_ipm_dense_a: A = [J_free | -P] dense [batch, m, nw] from the CSR Jacobian values (amap: CSR
  * position of (row, free column) or -1; row_slack: slack of each inequality row or -1; NaN -> 0). */
 int32_t cpl_ipm_dense_a(int64_t batch, int32_t m, int32_t nw, int32_t nf, int32_t nnz, const int32_t* d_amap,
-                        const int32_t* d_row_slack, const double* d_jac, double* d_A, void* stream);
+                        const int32_t* d_row_slack, const double* d_jac, double* d_A, const uint8_t* d_active,
+                        void* stream);
 
 #ifdef __cplusplus
 }

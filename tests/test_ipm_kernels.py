@@ -114,7 +114,8 @@ def test_dense_a_from_csr_values():
     ref[:, :, :nf] = J[:, :, free]
     ref[:, I, nf + np.arange(nI)] = -1.0
     A = _t(np.full((B, m, nw), 7.0))
-    _abi.check(_abi.lib.cpl_ipm_dense_a(B, m, nw, nf, nnz, _p(_t(amap)), _p(_t(row_slack)), _p(_t(jac)), _p(A), None))
+    _abi.check(_abi.lib.cpl_ipm_dense_a(B, m, nw, nf, nnz, _p(_t(amap)), _p(_t(row_slack)), _p(_t(jac)), _p(A), None,
+                                        None))
     np.testing.assert_array_equal(A.cpu().numpy(), ref)
 
 
@@ -130,7 +131,7 @@ def test_fd_points_and_raw_hessian():
     freepos = np.full(n, -1, dtype=np.int32)
     freepos[free] = np.arange(nf)
     Xp, h = _t(np.zeros((B * 2 * nf, n))), _t(np.zeros((B, nf)))
-    _abi.check(_abi.lib.cpl_ipm_fd_points(B, n, nf, 1e-6, _p(_t(freepos)), _p(_t(X)), _p(Xp), _p(h), None))
+    _abi.check(_abi.lib.cpl_ipm_fd_points(B, n, nf, 1e-6, _p(_t(freepos)), _p(_t(X)), _p(Xp), _p(h), None, None))
     h_ref = 1e-6 * np.maximum(np.abs(X[:, free]), 1.0)
     P = np.repeat(X[:, None, :], 2 * nf, axis=1)
     P[:, np.arange(nf), free] += h_ref
@@ -140,7 +141,7 @@ def test_fd_points_and_raw_hessian():
     gL = rng.normal(size=(B * 2 * nf, n))
     H = _t(np.zeros((B, nf, nf)))
     _abi.check(_abi.lib.cpl_ipm_fd_hessian_raw(B, n, nf, _p(_t(free.astype(np.int64))), _p(_t(gL)), _p(h), _p(H),
-                                               None))
+                                               None, None))
     g3 = gL.reshape(B, 2 * nf, n)[:, :, free]
     ref = (g3[:, :nf] - g3[:, nf:]) / (2.0 * h_ref[:, :, None])
     np.testing.assert_array_equal(H.cpu().numpy(), ref)
