@@ -78,6 +78,7 @@ struct KParams {
   const int32_t* csc_row;
   const double* ly;
   const uint8_t* lg_active;  // optional: instance b / y_repeat inactive -> its rows are skipped
+  int32_t offC;              // doubles offset of the LDS copy of the CSC index (fused gradient)
 };
 static_assert(sizeof(KParams) < 4096, "kernel parameters must fit the kernarg segment");
 
@@ -1255,6 +1256,17 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
   constexpr bool HAS_SQ = ENVK == CPL_ENV_SUPERQUADRIC || ENVK == CPL_ENV_MIXED;
   extern __shared__ __align__(16) double smem[];
   load_ctab(K);
+  // fused Lagrangian gradient: the CSC index of the structure in LDS (read per column, per entry)
+  int* s_colp = reinterpret_cast<int*>(smem + K.offC);
+  int* s_csck = s_colp + K.n + 1;
+  int* s_cscr = s_csck + K.nnz;
+  if (K.want_lgrad) {
+    for (int i = threadIdx.x; i <= K.n; i += blockDim.x) s_colp[i] = K.col_ptr[i];
+    for (int i = threadIdx.x; i < K.nnz; i += blockDim.x) {
+      s_csck[i] = K.csc_k[i];
+      s_cscr[i] = K.csc_row[i];
+    }
+  }
   __syncthreads();
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1407,10 +1419,10 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
         const double* jr = Jt + r * nnz;
         const double* yb = K.ly + ((b0 + r) / K.y_repeat) * m;
         double s = Dt[r * n + j];
-        for (int q = K.col_ptr[j]; q < K.col_ptr[j + 1]; ++q) {
-          double v = jr[K.csc_k[q]];
+        for (int q = s_colp[j]; q < s_colp[j + 1]; ++q) {
+          double v = jr[s_csck[q]];
           v = v == v ? v : 0.0;
-          s += v * yb[K.csc_row[q]];
+          s += v * yb[s_cscr[q]];
         }
         grad_out[(b0 + r) * n + j] = s;
       }
@@ -1613,13 +1625,13 @@ static int32_t plan_tile(KParams& K, bool g, bool j, bool f, bool grad, int t_ma
 }
 
 // Pipelined kernel layout: x double buffer, masses and tags (double buffered), outputs, SQ scratch
-static int32_t plan_pipe(KParams& K, bool g, bool j, bool f, bool grad) {
+static int32_t plan_pipe(KParams& K, bool g, bool j, bool f, bool grad, size_t extra_fixed = 0) {
   K.want_g = g; K.want_j = j; K.want_f = f; K.want_grad = grad;
   const bool sq = K.env_kind == CPL_ENV_SUPERQUADRIC || K.env_kind == CPL_ENV_MIXED;
   K.LR = K.N * SQ_L + 1;
   const size_t per = sizeof(double) * (size_t)(2 * K.n + 3 + (g ? K.m : 0) + (j ? K.nnz : 0) + (grad ? K.n : 0) +
                                                (sq ? K.LR : 0));
-  const size_t fixed = sizeof(double) * (72 + 8) + sizeof(CTab);
+  const size_t fixed = sizeof(double) * (72 + 8) + sizeof(CTab) + extra_fixed;
   int T = 64, logT = 6;
   while (T > 8 && (size_t)T * per + fixed > pipe_budget()) { T >>= 1; --logT; }
   if ((size_t)T * per + fixed > 160 * 1024) return fail(CPL_ERR_UNSUPPORTED, "problem too large for one LDS tile");
@@ -1715,9 +1727,12 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
     return fail(CPL_ERR_UNSUPPORTED, "fused Lagrangian gradient: pipelined (Ground / no environment) path only");
   if (use_pipe(K)) {
     // the fused Lagrangian gradient computes jac and grad into the tile image and stores only d_grad
-    st = lg ? plan_pipe(K, false, true, false, true)
+    // (the fused gradient also keeps the CSC index, (n + 1) + 2 nnz ints, in LDS)
+    const int csc_doubles = lg ? (K.n + 1 + 2 * K.nnz + 1) / 2 : 0;
+    st = lg ? plan_pipe(K, false, true, false, true, sizeof(double) * (size_t)csc_doubles)
             : plan_pipe(K, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr);
     if (st) return st;
+    K.offC = K.offI + 72;
     if (lg) {
       K.want_lgrad = 1;
       K.y_repeat = lg->y_repeat;
@@ -1728,7 +1743,7 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
       K.lg_active = lg->active;
     }
     K.ablate = g_ablate;
-    const size_t lds = sizeof(double) * (size_t)(K.offI + 72);
+    const size_t lds = sizeof(double) * (size_t)(K.offC + csc_doubles);
     using KernT = void (*)(const KParams, int64_t, const double*, const double*, const uint8_t*, double*, double*,
                            double*, double*, double*);
     static const KernT table[4][2] = {
