@@ -291,3 +291,21 @@ def test_fused_lagrangian_grad_is_bitwise_the_two_launch_result():
     torch.cuda.synchronize()
     rows = active.repeat_interleave(rep)[: X.shape[0]]
     assert torch.equal(masked[rows], ref[rows])
+
+
+@pytest.mark.gpu
+def test_batch_solve_gpu_eight_contacts():
+    """The loop at N = 8 (configs[2]'s contact count on Ground: nw = 91, m = 54 — a 119 KiB KKT LDS
+    image), every instance certified like the 4-contact case."""
+    cpl = solve_problem(n_contacts=8)
+    prob = cpl.GetCplProblem()
+    B = 128
+    X0, mass = solve_inputs(prob, B, seed=8)
+    dev = torch.device("cuda:0")
+    r = batch_ipm_solve(prob, torch.as_tensor(X0, device=dev), torch.as_tensor(mass, device=dev), max_iter=300)
+    assert r.graph
+    st = r.status.cpu().numpy()
+    assert (st <= STATUS_ACCEPTABLE).all(), np.bincount(st)
+    X, Y = r.x.cpu().numpy(), r.y.cpu().numpy()
+    for b in range(0, B, 16):
+        _certify(prob, X[b], Y[b], mass[b])

@@ -71,9 +71,10 @@ def _dense(M, A, r1, r2, dW=None):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nw,m", [(47, 30), (39, 14), (12, 12), (20, 0), (91, 54)])
+@pytest.mark.parametrize("nw,m", [(47, 30), (39, 14), (12, 12), (20, 0), (91, 54), (100, 70)])
 def test_kkt_matches_dense_solve(nw, m):
-    if nw * nw * 2 + m * nw + 8 * nw > 20000:
+    nz = nw - m
+    if 8 * (nw * nw + m * nw + nz * nz + nw + m + max(2 * nw, 3 * m) + 8) > 160 * 1024:
         pytest.skip("LDS image above 160 KiB: rejected by design")
     B = 300
     M, A, r1, r2 = _systems(B, nw, m, seed=nw + m)
