@@ -154,7 +154,7 @@ __device__ __forceinline__ double wave_bcast(double v, int src) {
 // lanes (lane, lane + 64); column-oriented substitution, the solved component broadcast by a
 // shuffle, one LDS read + FMA per lane and step.  T(i, k) = Tm[i * si + k * sk]; diagonal
 // D[i * sd].  lower: forward substitution; otherwise backward.  Callers barrier afterwards.
-__device__ void wave_trsv(int n, bool lower, const double* Tm, int si, int sk, const double* D, int sd, double* x) {
+__device__ __forceinline__ void wave_trsv(int n, bool lower, const double* Tm, int si, int sk, const double* D, int sd, double* x) {
   const int lane = threadIdx.x & 63;
   const int r0 = lane, r1 = lane + 64;
   double a0 = r0 < n ? x[r0] : 0.0;
@@ -184,7 +184,7 @@ __device__ void wave_trsv(int n, bool lower, const double* Tm, int si, int sk, c
 // A^T after the reflections; R[i][j] = QR[j*nw + i] for i < j, R[j][j] = QR[j*nw + j]), L [nz][nz] the
 // Cholesky of the reduced Hessian, M [nw][nw] (plus delta_w on the diagonal, applied here).
 // Vectors in LDS: q1 [nw], q2 [m] -> dw [nw], dy [m].  tmp: >= 2*nw doubles.
-__device__ void kkt_solve_lds(int nw, int m, const double* Q, const double* QR, const double* L,
+__device__ __forceinline__ void kkt_solve_lds(int nw, int m, const double* Q, const double* QR, const double* L,
                               const double* M, double dW, const double* q1, const double* q2, double* dw,
                               double* dy, double* tmp) {
   const int tid = threadIdx.x;
