@@ -126,7 +126,6 @@ class BatchSolveResult:
 
 
 _PIVOT_REL = 2.220446049250313e-16  # DBL_EPSILON: the KKT inertia test's zero-pivot level
-_DEBUG_EIG = False
 
 
 def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None, tol: float = 1e-8,
@@ -381,8 +380,6 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
 
         delta_w = zeros_B.clone()
         L1, info1 = chol(delta_w)
-        if _DEBUG_EIG and nz:
-            print("  eig(Hr) min", torch.linalg.eigvalsh(Hr)[:, 0].tolist(), "tol", piv_tol.tolist())
         for _ in range(64):
             bad = info1 != 0
             if not bool(bad.any()):
