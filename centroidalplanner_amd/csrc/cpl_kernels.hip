@@ -1098,6 +1098,8 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
   extern __shared__ __align__(16) double smem[];
   load_ctab(K);
   __syncthreads();
+  double mass_def = K.mass_default;  // a value (see cpl_eval_pipe_kernel)
+  asm volatile("" : "+v"(mass_def));
   const int tid = threadIdx.x;
   const int T = K.T;
   const int n = K.n, m = K.m, nnz = K.nnz, N = K.N;
@@ -1171,7 +1173,7 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
       if (e < r_st) {
         const int r = e % valid, sg = e / valid;
         const double* xr = X + r * n;
-        if (sg == 0) statics_values_item(K, xr, mass ? mass[b0 + r] : K.mass_default, Gt + r * m, Jt + r * nnz);
+        if (sg == 0) statics_values_item(K, xr, mass ? mass[b0 + r] : mass_def, Gt + r * m, Jt + r * nnz);
         else if (K.want_j) statics_row_item(K, xr, sg - 1, Jt + r * nnz);
         continue;
       }
@@ -1287,6 +1289,10 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
 
   int64_t t = blockIdx.x;
   if (t >= ntiles) return;  // (never: the host sizes the grid to at most ntiles)
+  // the default mass as a value: `mass ? mass[i] : K.mass_default` would otherwise select between a
+  // global and a kernarg address — a flat load, with a full vmcnt/lgkmcnt wait, in the loader loop
+  double mass_def = K.mass_default;
+  asm volatile("" : "+v"(mass_def));  // a value from here on, never re-read through its address
   NormAcc acc;
   acc.init(tid, CT, m);
 
@@ -1300,7 +1306,7 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
     dma_tile(XB(bi), x + b0s * n, count, lane);
     if ((count & 1) && lane == 0) st_tail = x[b0s * n + count - 1];
     if (lane < vs) {
-      st_mass = mass ? mass[b0s + lane] : K.mass_default;
+      st_mass = mass ? mass[b0s + lane] : mass_def;
       if (ENVK == CPL_ENV_MIXED) st_tag = env_tag[b0s + lane];
     }
   };
