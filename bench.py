@@ -227,7 +227,7 @@ def solve_bench(args):
             "ms_per_step": dt / steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f64", "data": "synthetic (TestBasic ground scenario, per-instance mass U[80,150])",
             "config": {"workload": SOLVE_CONFIG.name, "contacts": 4, "environment": "ground", "batch_per_gpu": B,
-                       "parallelism": f"instance-sharded x{world}", "hessian": "exact (batched central differences)",
+                       "parallelism": f"instance-sharded x{world}", "hessian": "exact (analytic Lagrangian Hessian kernel)",
                        "max_ls": args.max_ls, "max_soc": args.max_soc},
             "solved": ok, "iterations_max": int(its.max().item()), "iterations_mean": float(its.mean().item()),
             "lockstep_iterations": r.iterations_run, "eval_launches_per_solve": r.evaluations,

@@ -103,6 +103,8 @@ SIGNATURES = {
          c_void_p, c_int32, _DP],
     ),
     "cpl_kkt_workspace_doubles": (c_int64, [c_int32, c_int32]),
+    "cpl_lagrangian_hessian": (c_int32, [_DESC_P, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
+                                         c_void_p]),
     "cpl_eval_lagrangian_grad": (
         c_int32,
         [_DESC_P, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,

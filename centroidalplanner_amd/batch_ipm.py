@@ -138,11 +138,13 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
 
     evaluator(X [B, n], mass, outputs) -> {name: tensor} for outputs among "f" [B], "grad" [B, n],
     "g" [B, m], "jac" [B, nnz], on X's device; default KernelEvaluator(problem) (the HIP kernel).
-    hessian: "exact" (batched finite differences of the Lagrangian gradient) or "limited-memory"
+    hessian: "exact" (the analytic Lagrangian Hessian, cpl_lagrangian_hessian, for Ground /
+    no-environment problems on the device; batched central differences of the Lagrangian gradient
+    otherwise), "fd" (always the central differences) or "limited-memory"
     (damped BFGS).  graph: capture one iteration as a HIP graph (default: on for device tensors).
     max_ls / max_soc: line-search trials / second-order corrections per iteration (fixed counts)."""
-    if hessian not in ("exact", "limited-memory"):
-        raise ValueError("hessian must be 'exact' or 'limited-memory'")
+    if hessian not in ("exact", "fd", "limited-memory"):
+        raise ValueError("hessian must be 'exact', 'fd' or 'limited-memory'")
     use_bfgs = hessian == "limited-memory"
     import torch
 
@@ -296,6 +298,12 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         H = (gL[:, :nf] - gL[:, nf:]) / (2.0 * h[:, :, None])
         return 0.5 * (H + H.transpose(1, 2))
 
+    # the analytic Hessian kernel where the problem's environment allows it (a batch-0 call only
+    # validates: CPL_ERR_UNSUPPORTED for Superquadric / mixed)
+    analytic_H = (use_hip and hessian == "exact" and
+                  _abi.lib.cpl_lagrangian_hessian(ctypes.byref(problem.desc()), 0, None, None, None, None, max(nf, 1),
+                                                  None, None) == _abi.OK)
+    free_i32 = torch.as_tensor(np.where(~fixed_np)[0].astype(np.int32), device=dev)
     freepos_np = np.full(n, -1, dtype=np.int32)
     freepos_np[np.where(~fixed_np)[0]] = np.arange(nf, dtype=np.int32)
     freepos = torch.as_tensor(freepos_np, device=dev)
@@ -542,6 +550,11 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         gLfd = hfd = None
         if use_bfgs:
             Hblk = S["Hq"]
+        elif analytic_H:  # the exact Hessian of the Lagrangian, one thread per entry
+            Hblk = torch.empty(B, nf, nf, dtype=dt, device=dev)
+            _abi.check(_abi.lib.cpl_lagrangian_hessian(ctypes.byref(problem.desc()), B, _ptr(unpack(w)),
+                                                       _ptr(y.contiguous()), _ptr(S["active"]), _ptr(free_i32), nf,
+                                                       _ptr(Hblk), stream()))
         elif use_hip:  # raw central differences here, symmetrised inside the Newton setup kernel
             gLfd, hfd = fd_grads_dev(unpack(w), y)
             Hblk = torch.empty(B, nf, nf, dtype=dt, device=dev)
@@ -557,7 +570,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
             _abi.check(_abi.lib.cpl_ipm_newton_setup(
                 B, nw, m, nf, _ptr(w), _ptr(zL), _ptr(zU), _ptr(gradw), _ptr(A), _ptr(y), _ptr(c),
                 _ptr(cur["f"]), _ptr(mu), _ptr(hasL_u8), _ptr(hasU_u8), _ptr(wl0), _ptr(wu0),
-                None if Hblk is None else _ptr(Hblk.contiguous()), 0 if use_bfgs else 1,
+                None if Hblk is None else _ptr(Hblk.contiguous()), 0 if (use_bfgs or analytic_H) else 1,
                 _ptr(M), _ptr(r1), _ptr(r2), _ptr(gphi), _ptr(mr_diag), _ptr(theta_k), _ptr(phi_k),
                 _ptr(S["active"]) if not use_bfgs else None, stream()))
         else:

@@ -1445,6 +1445,106 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
   if (K.want_norms) partial_norms(acc, norms_ws + NORM_HDR);  // the loader contributes zeros
 }
 
+
+// ------------------------------------------------------------------------------------------
+// Exact Hessian of the Lagrangian f + y^T g over the free variables (Ground / no environment:
+// the environment and normal rows are linear there, so only the cost, the torque rows of
+// CentroidalStatics and the two FrictionCone rows carry curvature).  For an entry (u, v) of the
+// variables x = [c | per contact (names order) F, p, n]:
+//   cost:   W_com, W_F,i, W_p,i on the diagonal (src/MinimizeCentroidalVariables.cpp:124-148);
+//   torque: rows 3+k = sum_i ((p_i - c) x F_i)_k  ->  d2/dp_a dF_b = E_ab, d2/dc_a dF_b = -E_ab,
+//           E_ab = sum_k y_{3+k} eps_kab (src/Constraints/CentroidalStatics.cpp:37-61);
+//   cone 0: -F.n                ->  d2/dF_a dn_b = -delta_ab
+//   cone 1: |t| - mu s, s = F.n, t = F - s n (src/Constraints/FrictionCone.cpp:30-45):
+//           Hess |t| = J^T (I - uu^T) J / |t| + sum_j u_j Hess t_j  (u = t / |t|), with
+//           J_F = I - n n^T, J_n = -(n F^T + s I), d2 t_j/dF_a dn_b = -(delta_ab n_j + n_a delta_jb),
+//           d2 t_j/dn_a dn_b = -(F_a delta_jb + F_b delta_ja); at |t| = 0 the |t| terms count as 0
+//           (the reference's Jacobian is 0/0 there; the product path takes NaN as 0).
+// One thread per entry of the [nf, nf] output (free_idx: free variable -> column of x).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void cpl_lagrangian_hessian_kernel(const KParams K, int64_t total, int nf,
+                                                                     const double* __restrict__ x,
+                                                                     const double* __restrict__ y,
+                                                                     const uint8_t* __restrict__ active,
+                                                                     const int32_t* __restrict__ free_idx,
+                                                                     double* __restrict__ H) {
+  __shared__ int s_pos[CPL_MAX_CONTACTS];  // block position (map order) of contact i
+  if (threadIdx.x < K.N) s_pos[K.map_order[threadIdx.x]] = threadIdx.x;
+  __syncthreads();
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int per = nf * nf;
+  const int64_t b = e / per;
+  if (active && !active[b]) return;
+  const int kl = (int)(e - b * per);
+  const int uu = free_idx[kl / nf], vv = free_idx[kl - (kl / nf) * nf];
+  // decode: kind 0 CoM, 1 F, 2 p, 3 n; contact i; axis a
+  auto decode = [](int u, int& kind, int& i, int& a) {
+    if (u < 3) { kind = 0; i = -1; a = u; return; }
+    const int r = u - 3;
+    i = r / 9;
+    const int t = r - 9 * i;
+    kind = 1 + t / 3;
+    a = t - 3 * (t / 3);
+  };
+  int ku, iu, au, kv, iv, av;
+  decode(uu, ku, iu, au);
+  decode(vv, kv, iv, av);
+  const double* xb = x + b * (int64_t)K.n;
+  const double* yb = y + b * (int64_t)K.m;
+  double h = 0.0;
+  // cost (diagonal)
+  if (uu == vv) h += ku == 0 ? K.W_com : (ku == 1 ? K.W_F[iu] : (ku == 2 ? K.W_p[iu] : 0.0));
+  // torque rows: E_ab = sum_k y_{3+k} eps_kab
+  auto E = [&](int a, int c) {
+    if (a == c) return 0.0;
+    const int k = 3 - a - c;                        // the third index
+    const double sgn = ((a + 1) % 3 == c) ? 1.0 : -1.0;  // eps_{k a c} for (a, c) in cyclic order
+    return sgn * yb[3 + k];
+  };
+  if (ku == 2 && kv == 1 && iu == iv) h += E(au, av);          // d2/dp_a dF_b
+  else if (ku == 1 && kv == 2 && iu == iv) h += E(av, au);     // d2/dF_b dp_a
+  else if (ku == 0 && kv == 1) h -= E(au, av);                 // d2/dc_a dF_b
+  else if (ku == 1 && kv == 0) h -= E(av, au);
+  // friction cone of the contact (F and n entries of one contact)
+  if (iu == iv && iu >= 0 && (ku == 1 || ku == 3) && (kv == 1 || kv == 3)) {
+    const double* q = xb + 3 + 9 * iu;
+    const double F[3] = {q[0], q[1], q[2]};
+    const double nn[3] = {q[6], q[7], q[8]};
+    const int r0 = 6 + K.contact_rows * s_pos[iu] + (K.contact_rows - 2);
+    const double y0 = yb[r0], y1 = yb[r0 + 1];
+    const double sdot = (F[0] * nn[0] + F[1] * nn[1]) + F[2] * nn[2];
+    const double t[3] = {F[0] - sdot * nn[0], F[1] - sdot * nn[1], F[2] - sdot * nn[2]};
+    const double rr = sqrt((t[0] * t[0] + t[1] * t[1]) + t[2] * t[2]);
+    const bool fn = (ku == 1 && kv == 3) || (ku == 3 && kv == 1);
+    const int aF = ku == 1 ? au : av, an = ku == 3 ? au : av;  // (for the mixed block)
+    if (fn && aF == an) h -= y0 + K.mu * y1;  // -F.n and -mu s: d2/dF_a dn_a = -1
+    if (rr > 0.0 && rr < INFINITY && y1 != 0.0) {
+      const double u[3] = {t[0] / rr, t[1] / rr, t[2] / rr};
+      // columns of J for the two variables
+      auto col = [&](int kind, int a, double* c) {
+        for (int j = 0; j < 3; ++j)
+          c[j] = kind == 1 ? ((j == a ? 1.0 : 0.0) - nn[j] * nn[a]) : -(nn[j] * F[a] + (j == a ? sdot : 0.0));
+      };
+      double cu[3], cv[3];
+      col(ku, au, cu);
+      col(kv, av, cv);
+      const double jj = (cu[0] * cv[0] + cu[1] * cv[1]) + cu[2] * cv[2];
+      const double pu = (u[0] * cu[0] + u[1] * cu[1]) + u[2] * cu[2];
+      const double pv = (u[0] * cv[0] + u[1] * cv[1]) + u[2] * cv[2];
+      double second = 0.0;
+      if (fn) {
+        const double un = (u[0] * nn[0] + u[1] * nn[1]) + u[2] * nn[2];
+        second = -((aF == an ? un : 0.0) + nn[aF] * u[an]);
+      } else if (ku == 3 && kv == 3) {
+        second = -(F[au] * u[av] + F[av] * u[au]);
+      }
+      h += y1 * ((jj - pu * pv) / rr + second);
+    }
+  }
+  H[e] = h;
+}
+
 // ------------------------------------------------------------------------------------------
 // Residual norms of g against its bounds (per shard), deterministic two-stage reduction
 // ------------------------------------------------------------------------------------------
@@ -1848,6 +1948,28 @@ int32_t cpl_eval_lagrangian_grad(const cpl_problem_desc* d, int64_t batch, const
   // jac and grad f are computed into the tile image; only grad f + J^T y is stored (to d_out)
   return launch_eval(d, batch, d_x, d_mass, d_env_tag, nullptr, nullptr, nullptr, d_out, nullptr, (hipStream_t)stream,
                      true, &lg);
+}
+
+int32_t cpl_lagrangian_hessian(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_y,
+                               const uint8_t* d_active, const int32_t* d_free_idx, int32_t nf, double* d_H,
+                               void* stream) {
+  int32_t st = validate_desc(d);
+  if (st) return st;
+  if (d->env_kind != CPL_ENV_GROUND && d->env_kind != CPL_ENV_NONE)
+    return fail(CPL_ERR_UNSUPPORTED, "cpl_lagrangian_hessian: Ground / no-environment problems only");
+  KParams K;
+  fill_params(d, K, d_x);
+  if (batch < 0 || nf <= 0 || nf > K.n) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_lagrangian_hessian: bad sizes");
+  if (batch == 0) return CPL_OK;
+  if (!d_x || !d_y || !d_free_idx || !d_H) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_lagrangian_hessian: missing buffer");
+  const int64_t total = batch * (int64_t)nf * nf;
+  const int64_t blocks = (total + 255) / 256;
+  if (blocks > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_lagrangian_hessian: batch too large");
+  hipLaunchKernelGGL(cpl_lagrangian_hessian_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, K, total,
+                     (int)nf, d_x, d_y, d_active, d_free_idx, d_H);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_fail(e, "cpl_lagrangian_hessian launch");
+  return CPL_OK;
 }
 
 int32_t cpl_eval_batch_norms(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,

@@ -241,6 +241,16 @@ int32_t cpl_eval_lagrangian_grad(const cpl_problem_desc* d, int64_t batch, const
                                  const uint8_t* d_env_tag, const int32_t* d_col_ptr, const int32_t* d_csc_k,
                                  const int32_t* d_csc_row, const double* d_y, int32_t y_repeat,
                                  const uint8_t* d_active, double* d_out, void* stream);
+/*
+ * cpl_lagrangian_hessian: the exact Hessian of f + y^T g over the free variables, [batch, nf, nf]
+ * (d_free_idx: free variable -> column of x, int32), per instance (y: [batch, m]); instances with
+ * d_active[b] == 0 are skipped.  Ground / no-environment problems only (their environment and
+ * normal rows are linear): CPL_ERR_UNSUPPORTED otherwise.  Where a cone's tangential force is
+ * exactly zero the |F_t| terms count as 0 (the reference's Jacobian is 0/0 there).
+ */
+int32_t cpl_lagrangian_hessian(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_y,
+                               const uint8_t* d_active, const int32_t* d_free_idx, int32_t nf, double* d_H,
+                               void* stream);
 int32_t cpl_kkt_solve(int32_t mode, int64_t batch, int32_t nw, int32_t m, const double* d_M, const double* d_A,
                       const double* d_r1, const double* d_r2, const double* d_mu, const double* d_delta_w_last,
                       const uint8_t* d_active, double* d_dw, double* d_dy, double* d_delta_w, double* d_delta_c,

@@ -225,3 +225,76 @@ def test_optimality_error_convergence_and_barrier_update():
     np.testing.assert_array_equal(np.isinf(fto.cpu().numpy()).all(1), reset)
     np.testing.assert_array_equal(fco.cpu().numpy(), np.where(reset, 0, fc))
     assert done.any() and acc_now.any() and reset.any() and act.any()  # every branch exercised
+
+
+def _fd_hessian_ref(prob, X, mass, y, free, h=1e-6):
+    """Central differences of grad f + J^T y through the product eval kernel, symmetrised — the
+    solve loop's "fd" Hessian — on the device."""
+    import torch
+
+    from centroidalplanner_amd.batch_ipm import KernelEvaluator
+
+    n, m, nnz = prob.get_nlp_info()
+    iRow, jCol = prob.get_structure()
+    ev = KernelEvaluator(prob)
+    B, nf = X.shape[0], free.size
+    out = torch.zeros(B, nf, nf, dtype=torch.float64, device=X.device)
+    J = torch.zeros(B, m, n, dtype=torch.float64, device=X.device)
+    for k in range(nf):
+        hk = h * torch.clamp(X[:, free[k]].abs(), min=1.0)
+        g = []
+        for sgn in (1.0, -1.0):
+            Xs = X.clone()
+            Xs[:, free[k]] += sgn * hk
+            o = ev(Xs.contiguous(), mass, outputs=("jac", "grad"))
+            J.zero_()
+            J[:, iRow, jCol] = torch.nan_to_num(o["jac"], nan=0.0)
+            g.append(o["grad"] + torch.einsum("bmn,bm->bn", J, y))
+        out[:, k, :] = ((g[0] - g[1]) / (2.0 * hk[:, None]))[:, free]
+    return 0.5 * (out + out.transpose(1, 2))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["ground", "com"])
+def test_analytic_lagrangian_hessian_matches_central_differences(which):
+    import torch
+
+    from centroidalplanner_amd.workload import solve_inputs, solve_problem
+
+    rng = np.random.default_rng(7)
+    if which == "ground":
+        prob = solve_problem().GetCplProblem()
+        X0, mass = solve_inputs(prob, 24, seed=3)
+        X0 = X0 + rng.normal(scale=0.05, size=X0.shape)
+    else:  # CoMPlanner: fixed positions / normals / lifting contact -> a strict free subset
+        from test_batch_solve import _scenario
+
+        prob, x0, _ = _scenario("com")
+        X0 = np.tile(x0, (24, 1)) + rng.normal(scale=0.05, size=(24, x0.size))
+        xl, xu, _, _ = prob.get_bounds_info()
+        X0 = np.clip(X0, xl, xu)
+        mass = rng.uniform(80.0, 150.0, 24)
+    n, m, _ = prob.get_nlp_info()
+    xl, xu, _, _ = prob.get_bounds_info()
+    free = np.where(~(np.abs(xu - xl) <= 1e-14 * np.maximum(1.0, np.abs(xl))))[0]
+    X = _t(X0)
+    M = _t(mass)
+    y = _t(rng.normal(scale=50.0, size=(24, m)))
+    H = _t(np.zeros((24, free.size, free.size)))
+    _abi.check(_abi.lib.cpl_lagrangian_hessian(ctypes.byref(prob.desc()), 24, _p(X), _p(y), None,
+                                               _p(_t(free.astype(np.int32))), free.size, _p(H), None))
+    ref = _fd_hessian_ref(prob, X, M, y, free)
+    torch.cuda.synchronize()
+    Hn, Rn = H.cpu().numpy(), ref.cpu().numpy()
+    scale = np.abs(Rn).max(axis=(1, 2), keepdims=True) + 1.0
+    np.testing.assert_allclose(Hn, Rn, rtol=0, atol=1e-5 * scale.max())
+    np.testing.assert_array_equal(Hn, np.transpose(Hn, (0, 2, 1)))  # symmetric by construction
+
+
+@pytest.mark.gpu
+def test_analytic_hessian_rejects_superquadric():
+    from test_batch_solve import _scenario
+
+    prob, _, _ = _scenario("superquadric")
+    st = _abi.lib.cpl_lagrangian_hessian(ctypes.byref(prob.desc()), 0, None, None, None, None, 1, None, None)
+    assert st == _abi.ERR_UNSUPPORTED
