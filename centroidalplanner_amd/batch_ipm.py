@@ -304,6 +304,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                   _abi.lib.cpl_lagrangian_hessian(ctypes.byref(problem.desc()), 0, None, None, None, None, max(nf, 1),
                                                   None, None) == _abi.OK)
     free_i32 = torch.as_tensor(np.where(~fixed_np)[0].astype(np.int32), device=dev)
+    Mr_buf = torch.zeros(B, nw, nw, dtype=dt, device=dev) if use_hip else None  # feasibility-step matrix
     freepos_np = np.full(n, -1, dtype=np.int32)
     freepos_np[np.where(~fixed_np)[0]] = np.arange(nf, dtype=np.int32)
     freepos = torch.as_tensor(freepos_np, device=dev)
@@ -694,7 +695,12 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         # violation by 10 %; the multipliers stay.  Otherwise the last trial.  Either way the
         # instance's filter restarts.  (The KKT kernel skips the instances outside the mask.)
         failed = st["searching"].clone()
-        dwr = kkt(torch.diag_embed(mr_diag), A, torch.zeros_like(w), -c, mu, zeros_B, failed)[0]
+        if use_hip:  # persistent zero matrix: only its diagonal changes (no 8 192 x nw x nw fill)
+            Mr_buf.diagonal(dim1=1, dim2=2).copy_(mr_diag)
+            Mr = Mr_buf
+        else:
+            Mr = torch.diag_embed(mr_diag)
+        dwr = kkt(Mr, A, torch.zeros_like(w), -c, mu, zeros_B, failed)[0]
         ar = primal_step(dwr)
         wr, orr = trial(dwr, ar, failed)
         if use_hip:
