@@ -100,5 +100,27 @@ int main(int argc, char** argv) {
       }
     }
   }
+  // occupancy sweep: the same mode-0 launch with extra dynamic LDS (argv[4..]: pad bytes), to see
+  // how the kernel's time scales with resident workgroups per CU
+  for (int a = 4; a < argc; ++a) {
+    const size_t pad = (size_t)std::atol(argv[a]);
+    const size_t lds = sizeof(double) * (size_t)(kkt_lds_doubles(nw, m) + 8) + pad;
+    int per_cu = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(cpl_kkt_kernel),
+                                                    KKT_THREADS, lds));
+    float best = 1e30f;
+    for (int rep = 0; rep < 5; ++rep) {
+      CK(hipEventRecord(e0));
+      hipLaunchKernelGGL(cpl_kkt_kernel, dim3((unsigned)B), dim3(KKT_THREADS), lds, 0, 0, (int64_t)B, nw, m, dM, dA,
+                         dr1, dr2, dmu, dlast, nullptr, ddw, ddy, ddW, ddC, dinfo, dws);
+      CK(hipGetLastError());
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      best = ms < best ? ms : best;
+    }
+    std::printf("pad %zu B: LDS %zu B, %d workgroups/CU: mode 0 %.3f ms\n", pad, lds, per_cu, best);
+  }
   return 0;
 }

@@ -93,3 +93,43 @@ def test_shard_tiles_batch():
             assert all(got[r][0] + got[r][1] == got[r + 1][0] for r in range(world - 1))
             assert got[-1][0] + got[-1][1] == batch
             assert max(c for _, c in got) - min(c for _, c in got) <= 1
+
+
+def _bucket_worker(rank, world, port, q):
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch.distributed as dist
+
+    from centroidalplanner_amd.distributed import all_gather_norms
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    bucket = torch.tensor([[10.0 * rank + s, 100.0 * rank + s] for s in range(3)], dtype=torch.float64)
+    out, work = all_gather_norms(bucket, async_op=True)  # one collective for a bucket of 3 steps
+    work.wait()
+    q.put((rank, out.numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bucketed_norms_gloo_world2():
+    """bench.py's bucketed gather: one all-gather carries S steps' norms, rank-major; combine_bucket
+    recovers every step's global (max, sumsq)."""
+    from centroidalplanner_amd.distributed import combine_bucket
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert np.array_equal(res[0][1], res[1][1])
+    steps = combine_bucket(res[0][1], world, 3)
+    assert steps == [(10.0 + s, (0.0 + s) + (100.0 + s)) for s in range(3)]
