@@ -53,9 +53,10 @@ __device__ __forceinline__ double wave_sum(double v) {
 // by one wave (wave-uniform control flow, no workgroup barriers): lanes own rows; LDS accesses of
 // one wave complete in order, so a lane reads the column entries other lanes scaled in the
 // previous instruction.  Returns true (wave-uniform) when every pivot is above pivot_min and finite.
-__device__ bool wave_cholesky(double* H, int n, double pivot_min) {
+__device__ __forceinline__ bool wave_cholesky(double* H, int n, double pivot_min) {
   const int lane = threadIdx.x & 63;
   __builtin_amdgcn_wave_barrier();
+  #pragma unroll 1
   for (int k = 0; k < n; ++k) {
     const double d = H[k * n + k];
     if (!(d > pivot_min) || !(d < INFINITY)) return false;
@@ -121,7 +122,7 @@ template <int G, class F>
 __device__ __forceinline__ void group_dots(int n, int len, const double* A, int sr, int sk, const double* x, int sx,
                                            F fin) {
   const int part = threadIdx.x % G;
-  for (int base = 0; base < n * G; base += blockDim.x) {
+  for (int base = 0; base < n * G; base += KKT_THREADS) {
     const int r = (base + (int)threadIdx.x) / G;
     const bool act = r < n;
     double s0 = 0.0, s1 = 0.0;
@@ -162,6 +163,7 @@ __device__ __forceinline__ void wave_trsv(int n, bool lower, const double* Tm, i
   // reciprocal diagonal of the lane's rows, computed in parallel ahead of the sequential sweep
   const double v0 = r0 < n ? 1.0 / D[r0 * sd] : 0.0;
   const double v1 = r1 < n ? 1.0 / D[r1 * sd] : 0.0;
+  #pragma unroll 1
   for (int t = 0; t < n; ++t) {
     const int i = lower ? t : n - 1 - t;
     const double ai = i < 64 ? wave_bcast(a0, i) : wave_bcast(a1, i - 64);
@@ -192,7 +194,7 @@ __device__ __forceinline__ void kkt_solve_lds(int nw, int m, const double* Q, co
   double* py = tmp;          // [m]
   double* t = tmp + nw;      // [nw]
   // R^T p_y = q2 (forward substitution; (R^T)[i][k] = R[k][i] = QR[i*nw + k])
-  for (int i = tid; i < m; i += blockDim.x) py[i] = q2[i];
+  for (int i = tid; i < m; i += KKT_THREADS) py[i] = q2[i];
   __syncthreads();
   if (tid < 64) wave_trsv(m, true, QR, nw, 1, QR, nw + 1, py);
   __syncthreads();
@@ -241,14 +243,21 @@ __host__ __device__ inline int kkt_lds_doubles(int nw, int m) {
   return nw * nw + m * nw + nz * nz + nw + m + (2 * nw > 3 * m ? 2 * nw : 3 * m);
 }
 
-__global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
-    int mode, int64_t batch, int nw, int m, const double* __restrict__ Mg, const double* __restrict__ Ag,
+// NW, MM > 0: the kernel specialised for one system size (nw = NW, m = MM; the arguments are
+// ignored) — every stride, trip count and index division becomes a compile-time constant, which
+// the instruction-issue-bound kernel needs (SQ counters: ~75 % of wave cycles parked, the SIMDs'
+// issue near saturation from 4 workgroups per CU); NW = 0: any size.
+template <int NW, int MM>
+__global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 8))) void cpl_kkt_kernel(
+    int mode, int64_t batch, int nw_arg, int m_arg, const double* __restrict__ Mg, const double* __restrict__ Ag,
     const double* __restrict__ r1g, const double* __restrict__ r2g, const double* __restrict__ mug,
     const double* __restrict__ dw_last, const uint8_t* __restrict__ active, double* __restrict__ dwg,
     double* __restrict__ dyg, double* __restrict__ dWg, double* __restrict__ dCg, int32_t* __restrict__ info,
     double* __restrict__ ws) {
   extern __shared__ __align__(16) double sm[];
   __shared__ KktShared sh;
+  const int nw = NW > 0 ? NW : nw_arg;
+  const int m = NW > 0 ? MM : m_arg;
   const int64_t b = blockIdx.x;
   if (b >= batch) return;
   const int tid = threadIdx.x;
@@ -273,25 +282,25 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
   double* c2 = c1 + nw;
 
   if (active && !active[b]) {
-    for (int i = tid; i < nw; i += blockDim.x) dwg[b * nw + i] = 0.0;
-    for (int i = tid; i < m; i += blockDim.x) dyg[b * m + i] = 0.0;
+    for (int i = tid; i < nw; i += KKT_THREADS) dwg[b * nw + i] = 0.0;
+    for (int i = tid; i < m; i += KKT_THREADS) dyg[b * m + i] = 0.0;
     if (tid == 0 && mode == 0) { dWg[b] = 0.0; dCg[b] = 0.0; info[b] = 0; }
     return;
   }
 
   if (mode == 1) {  // re-solve with the kept factors
     const int64_t per = kkt_ws_per(nw, m);
-    for (int64_t i = tid; i < per - 4; i += blockDim.x) sm[i] = wsb[i];
+    for (int64_t i = tid; i < per - 4; i += KKT_THREADS) sm[i] = wsb[i];
     if (tid == 0) { sh.delta_w = wsb[per - 4]; sh.delta_c = wsb[per - 3]; }
     __syncthreads();
     kkt_solve_lds(nw, m, Q, QR, L, M, sh.delta_w, q1, q2, dw, dy, tmp);
-    for (int i = tid; i < nw; i += blockDim.x) dwg[b * nw + i] = dw[i];
-    for (int i = tid; i < m; i += blockDim.x) dyg[b * m + i] = dy[i];
+    for (int i = tid; i < nw; i += KKT_THREADS) dwg[b * nw + i] = dw[i];
+    for (int i = tid; i < m; i += KKT_THREADS) dyg[b * m + i] = dy[i];
     return;
   }
 
   // ---- Householder QR of A^T: row j of QR = column j of A^T
-  for (int i = tid; i < m * nw; i += blockDim.x) QR[i] = Ab[i];
+  for (int i = tid; i < m * nw; i += KKT_THREADS) QR[i] = Ab[i];
   __syncthreads();
   KKT_MARK(0);
   // Householder QR two columns at a time.  Wave 0 forms the reflector pair (j, j+1) — v in place
@@ -305,7 +314,7 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
   double* s1v = tmp + 2 * m; // [m] (tmp holds max(2 nw, 3 m) doubles)
   double* cpair = dw;        // [m / 2 + 1]: c_j of the pair starting at j (dw is free until the solve)
   const int wid = tid >> 6, lane = tid & 63;
-  const int nwaves = blockDim.x >> 6;
+  const int nwaves = KKT_THREADS >> 6;
   auto house = [&](int j) {
     double* x = QR + j * nw;
     const int i0 = j + 1 + lane, i1 = i0 + 64;
@@ -342,6 +351,7 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
   };
   if (m > 0 && wid == 0) house2(0);
   __syncthreads();
+  #pragma unroll 1
   for (int j = 0; j + 2 < m; j += 2) {
     const double b0 = beta[j], b1 = beta[j + 1], cj = cpair[j >> 1];
     const double* v0 = QR + j * nw;
@@ -349,7 +359,7 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
     {  // both dots of columns k >= j+2, 8 lanes per column
       const int part = tid & 7;
       const int ncol = m - j - 2;
-      for (int base = 0; base < ncol * 8; base += blockDim.x) {
+      for (int base = 0; base < ncol * 8; base += KKT_THREADS) {
         const int kk = (base + tid) >> 3;
         const bool act = kk < ncol;
         double a0 = 0.0, a1 = 0.0;
@@ -400,7 +410,7 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
   // ---- Q = H_0 ... H_{m-1} I, backward, a pair of reflectors per pass (the QR's pairs): per
   // column q of Q, s1 = beta_{j+1} (q_{j+1} + v_{j+1}^T q), s0 = beta_j (q_j + v_j^T q - s1 c_j),
   // q -= s1 v_{j+1} + s0 v_j; 4 lanes per column; a lone last reflector (m odd) goes first.
-  for (int i = tid; i < nw * nw; i += blockDim.x) Q[i] = (i / nw == i % nw) ? 1.0 : 0.0;
+  for (int i = tid; i < nw * nw; i += KKT_THREADS) Q[i] = (i / nw == i % nw) ? 1.0 : 0.0;
   __syncthreads();
   {
     const int part = tid & 3;
@@ -409,7 +419,7 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
       const int j = m - 1;
       const double bj = beta[j];
       const double* v = QR + j * nw;
-      for (int base = 0; base < nw * 4; base += blockDim.x) {
+      for (int base = 0; base < nw * 4; base += KKT_THREADS) {
         const int c = (base + tid) >> 2;
         const bool act = c < nw;
         double sv = 0.0;
@@ -427,11 +437,12 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
       }
       __syncthreads();
     }
+    #pragma unroll 1
     for (int j = jtop - 2; j >= 0; j -= 2) {
       const double b0 = beta[j], b1 = beta[j + 1], cj = cpair[j >> 1];
       const double* v0 = QR + j * nw;
       const double* v1 = QR + (j + 1) * nw;
-      for (int base = 0; base < nw * 4; base += blockDim.x) {
+      for (int base = 0; base < nw * 4; base += KKT_THREADS) {
         const int c = (base + tid) >> 2;
         const bool act = c < nw;
         double a0 = 0.0, a1 = 0.0;
@@ -485,10 +496,12 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
     // MZ = M Z: a thread per (row r, 4 columns), M[r][k] from global once per k, Z[k][c..c+3] from
     // LDS (reads past Z's last column land inside the LDS image and are discarded)
     const int nb = (nz + 3) >> 2;
-    for (int t = tid; t < nw * nb; t += blockDim.x) {
+    #pragma unroll 1
+    for (int t = tid; t < nw * nb; t += KKT_THREADS) {
       const int r = t / nb, cb = (t - r * nb) * 4;
       const double* mr = M + r * nw;
       double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+      #pragma unroll 1
       for (int k0 = 0; k0 < nw; k0 += 8) {  // eight global loads in flight, then the FMAs
         double mv[8];
 #pragma unroll
@@ -512,10 +525,12 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
     }
     __syncthreads();
     // Hr = Z^T (M Z): a thread per (row a, 4 columns), Z[r][a] from LDS, MZ[r][c..c+3] from global
-    for (int t = tid; t < nz * nb; t += blockDim.x) {
+    #pragma unroll 1
+    for (int t = tid; t < nz * nb; t += KKT_THREADS) {
       const int ar = t / nb, cb = (t - ar * nb) * 4;
       double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
       const int w1 = cb + 1 < nz, w2 = cb + 2 < nz, w3 = cb + 3 < nz;
+      #pragma unroll 1
       for (int r0 = 0; r0 < nw; r0 += 2) {  // eight global loads in flight, then the FMAs
         double mz[2][4];
 #pragma unroll
@@ -547,7 +562,7 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
     __syncthreads();
     // symmetrise, keep a copy in dw.. region (nz*nz may exceed it: use the global scratch again)
     double* Hsave = MZ;
-    for (int e = tid; e < nz * nz; e += blockDim.x) {
+    for (int e = tid; e < nz * nz; e += KKT_THREADS) {
       const int a = e / nz, c = e % nz;
       Hsave[e] = 0.5 * (Hr0[a * nz + c] + Hr0[c * nz + a]);
     }
@@ -567,6 +582,7 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) mmax = fmax(mmax, __shfl_xor(mmax, o));
       const double pivot_min = 2.220446049250313e-16 * mmax;
+      #pragma unroll 1
       for (int attempt = 0; attempt < 64; ++attempt) {
         for (int e = tid; e < nz * nz; e += 64) L[e] = Hsave[e] + ((e / nz == e % nz) ? dW : 0.0);
         if (wave_cholesky(L, nz, pivot_min)) break;
@@ -611,19 +627,19 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_kernel(
     if (sh.flag) {
       // the correction (e1, e2) -> (c1, c2), global scratch
       kkt_solve_lds(nw, m, Q, QR, L, M, dW, e1, e2, c1, c2, tmp);
-      for (int r = tid; r < nw; r += blockDim.x) dw[r] += c1[r];
-      for (int k = tid; k < m; k += blockDim.x) dy[k] += c2[k];
+      for (int r = tid; r < nw; r += KKT_THREADS) dw[r] += c1[r];
+      for (int k = tid; k < m; k += KKT_THREADS) dy[k] += c2[k];
       __syncthreads();
     }
   }
   KKT_MARK(6);
-  for (int i = tid; i < nw; i += blockDim.x) dwg[b * nw + i] = dw[i];
-  for (int i = tid; i < m; i += blockDim.x) dyg[b * m + i] = dy[i];
+  for (int i = tid; i < nw; i += KKT_THREADS) dwg[b * nw + i] = dw[i];
+  for (int i = tid; i < m; i += KKT_THREADS) dyg[b * m + i] = dy[i];
   if (tid == 0) { dWg[b] = dW; dCg[b] = sh.delta_c; }
   // keep the factors for mode 1 (the global scratch use above is finished: barrier first)
   __syncthreads();
   const int64_t per = kkt_ws_per(nw, m);
-  for (int64_t i = tid; i < per - 4; i += blockDim.x) wsb[i] = sm[i];
+  for (int64_t i = tid; i < per - 4; i += KKT_THREADS) wsb[i] = sm[i];
   if (tid == 0) { wsb[per - 4] = dW; wsb[per - 3] = sh.delta_c; wsb[per - 2] = 0.0; wsb[per - 1] = 0.0; }
   KKT_MARK(7);
 }
@@ -659,6 +675,17 @@ __global__ __launch_bounds__(256) void cpl_lagrangian_grad_kernel(int64_t total,
 }  // namespace cpl
 
 using namespace cpl;
+
+using KktKernel = void (*)(int, int64_t, int, int, const double*, const double*, const double*, const double*,
+                          const double*, const double*, const uint8_t*, double*, double*, double*, double*, int32_t*,
+                          double*);
+
+// The size-specialised instance for the solve loop's 4-contact systems (nw 47, m 30: Ground /
+// Superquadric with an environment), the generic one otherwise.
+static inline KktKernel kkt_kernel_for(int nw, int m) {
+  if (nw == 47 && m == 30) return cpl_kkt_kernel<47, 30>;
+  return cpl_kkt_kernel<0, 0>;
+}
 
 extern "C" {
 
@@ -700,7 +727,7 @@ int32_t cpl_kkt_solve(int32_t mode, int64_t batch, int32_t nw, int32_t m, const 
   if (batch > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_solve: batch too large");
   const size_t lds = sizeof(double) * (size_t)(kkt_lds_doubles(nw, m) + 8);
   if (lds > 160 * 1024) return fail(CPL_ERR_UNSUPPORTED, "cpl_kkt_solve: system too large for one LDS image");
-  hipLaunchKernelGGL(cpl_kkt_kernel, dim3((unsigned)batch), dim3(KKT_THREADS), lds, (hipStream_t)stream, (int)mode,
+  hipLaunchKernelGGL(kkt_kernel_for(nw, m), dim3((unsigned)batch), dim3(KKT_THREADS), lds, (hipStream_t)stream, (int)mode,
                      batch, (int)nw, (int)m, d_M, d_A, d_r1, d_r2, d_mu, d_delta_w_last, d_active, d_dw, d_dy,
                      d_delta_w, d_delta_c, d_info, d_ws);
   hipError_t e = hipGetLastError();

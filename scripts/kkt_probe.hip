@@ -106,12 +106,12 @@ int main(int argc, char** argv) {
     const size_t pad = (size_t)std::atol(argv[a]);
     const size_t lds = sizeof(double) * (size_t)(kkt_lds_doubles(nw, m) + 8) + pad;
     int per_cu = 0;
-    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(cpl_kkt_kernel),
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kkt_kernel_for(nw, m)),
                                                     KKT_THREADS, lds));
     float best = 1e30f;
     for (int rep = 0; rep < 5; ++rep) {
       CK(hipEventRecord(e0));
-      hipLaunchKernelGGL(cpl_kkt_kernel, dim3((unsigned)B), dim3(KKT_THREADS), lds, 0, 0, (int64_t)B, nw, m, dM, dA,
+      hipLaunchKernelGGL(kkt_kernel_for(nw, m), dim3((unsigned)B), dim3(KKT_THREADS), lds, 0, 0, (int64_t)B, nw, m, dM, dA,
                          dr1, dr2, dmu, dlast, nullptr, ddw, ddy, ddW, ddC, dinfo, dws);
       CK(hipGetLastError());
       CK(hipEventRecord(e1));
