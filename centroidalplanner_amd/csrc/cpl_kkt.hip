@@ -43,10 +43,50 @@ __device__ long long* g_kkt_prof;
 constexpr int KKT_THREADS = 256;
 constexpr int KKT_MAX_NW = 128;
 
+// Lane permutations by DPP (a VALU operand modifier, no LDS round trip — ds_bpermute, what
+// __shfl_xor lowers to, costs an LDS-crossbar trip per dword on the reductions' critical path).
+// An f64 moves as its two dwords.  Lanes of rows outside ROW_MASK receive 0.
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ double dpp_mov(double v) {
+  const long long bits = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(bits & 0xffffffffLL), CTRL, ROW_MASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(bits >> 32), CTRL, ROW_MASK, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+constexpr int DPP_QUAD_XOR1 = 0xB1;        // quad_perm [1,0,3,2]
+constexpr int DPP_QUAD_XOR2 = 0x4E;        // quad_perm [2,3,0,1]
+constexpr int DPP_ROW_MIRROR = 0x140;      // lane i of a row of 16 <- lane 15 - i
+constexpr int DPP_ROW_HALF_MIRROR = 0x141; // lane i of a half-row of 8 <- lane 7 - i
+constexpr int DPP_ROW_BCAST15 = 0x142;     // lane 15 of each row -> the next row
+constexpr int DPP_ROW_BCAST31 = 0x143;     // lane 31 -> rows 2 and 3
+
+// Sums over aligned groups of 4 / 8 lanes, the total in every lane of the group (every lane of
+// the wave must execute them).
+__device__ __forceinline__ double group4_sum(double v) {
+  v += dpp_mov<DPP_QUAD_XOR1>(v);
+  return v + dpp_mov<DPP_QUAD_XOR2>(v);
+}
+__device__ __forceinline__ double group8_sum(double v) {
+  v = group4_sum(v);
+  return v + dpp_mov<DPP_ROW_HALF_MIRROR>(v);
+}
+
+// Broadcast lane `src` (wave-uniform) of a double with two v_readlane_b32 (no LDS round trip).
+__device__ __forceinline__ double wave_bcast(double v, int src) {
+  const long long bits = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(bits & 0xffffffffLL), src);
+  const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), src);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Sum over the wave, in every lane: rows of 16 by DPP, rows combined into lane 63 by the two row
+// broadcasts, then read out of lane 63.
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  v = group8_sum(v);
+  v += dpp_mov<DPP_ROW_MIRROR>(v);
+  v += dpp_mov<DPP_ROW_BCAST15, 0xa>(v);
+  v += dpp_mov<DPP_ROW_BCAST31, 0xc>(v);
+  return wave_bcast(v, 63);
 }
 
 // Right-looking Cholesky of the n x n matrix H (row-major, stride n) in LDS, lower factor in place,
@@ -137,18 +177,16 @@ __device__ __forceinline__ void group_dots(int n, int len, const double* A, int 
       if (k < len) s0 += a[k * sk] * x[k * sx];
     }
     double s = s0 + s1;
+    if constexpr (G == 4) {
+      s = group4_sum(s);
+    } else if constexpr (G == 8) {
+      s = group8_sum(s);
+    } else {
 #pragma unroll
-    for (int o = 1; o < G; o <<= 1) s += __shfl_xor(s, o);
+      for (int o = 1; o < G; o <<= 1) s += __shfl_xor(s, o);
+    }
     if (act && part == 0) fin(r, s);
   }
-}
-
-// Broadcast lane `src` (wave-uniform) of a double with two v_readlane_b32 (no LDS round trip).
-__device__ __forceinline__ double wave_bcast(double v, int src) {
-  const long long bits = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)(bits & 0xffffffffLL), src);
-  const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), src);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
 // Triangular solve T x = b in place (x holds b on entry), n <= 128, by wave 0 alone: rows live in
@@ -370,11 +408,8 @@ __global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 
             a0 += v0[i] * yi;
             a1 += v1[i] * yi;
           }
-#pragma unroll
-        for (int o = 1; o < 8; o <<= 1) {
-          a0 += __shfl_xor(a0, o);
-          a1 += __shfl_xor(a1, o);
-        }
+        a0 = group8_sum(a0);
+        a1 = group8_sum(a1);
         if (act && part == 0) {
           const double yj = y[j], yj1 = y[j + 1];
           const double s0 = b0 * (yj + v0[j + 1] * yj1 + a0);
@@ -427,8 +462,7 @@ __global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 
           if (part == 0) sv = Q[j * nw + c];
           for (int r = j + 1 + part; r < nw; r += 4) sv += v[r] * Q[r * nw + c];
         }
-        sv += __shfl_xor(sv, 1);
-        sv += __shfl_xor(sv, 2);
+        sv = group4_sum(sv);
         sv *= bj;
         if (act) {
           if (part == 0) Q[j * nw + c] -= sv;
@@ -452,10 +486,8 @@ __global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 
             a0 += v0[r] * qr;
             a1 += v1[r] * qr;
           }
-        a0 += __shfl_xor(a0, 1);
-        a0 += __shfl_xor(a0, 2);
-        a1 += __shfl_xor(a1, 1);
-        a1 += __shfl_xor(a1, 2);
+        a0 = group4_sum(a0);
+        a1 = group4_sum(a1);
         if (act) {
           const double qj = Q[j * nw + c], qj1 = Q[(j + 1) * nw + c];
           const double s1 = b1 * (qj1 + a1);
