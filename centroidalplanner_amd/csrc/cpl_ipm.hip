@@ -12,16 +12,13 @@
 #include <string>
 
 #include "cpl_status.hpp"
+#include "cpl_wave.hpp"
 
 namespace cpl {
 
 constexpr int IPM_WAVES = 4;  // instances per 256-thread workgroup
 
-__device__ __forceinline__ double ipm_wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
+__device__ __forceinline__ double ipm_wave_sum(double v) { return wave_sum(v); }
 
 // wt = w + alpha d;  X[b, free[k]] = (mask ? wt : w_keep)[k],  X[b, fixed[j]] = Xbase[b, fixed[j]]
 __global__ __launch_bounds__(256) void cpl_ipm_trial_point_kernel(
@@ -156,14 +153,11 @@ __global__ __launch_bounds__(256) void cpl_ipm_optimality_kernel(
     ys += fabs(yb[r]);
     cmax = fmax(cmax, fabs(c[b * m + r]));
   }
-  // wave reductions (max by xor shuffles; all lanes end with the totals)
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    dmax = fmax(dmax, __shfl_xor(dmax, o));
-    clmax = fmax(clmax, __shfl_xor(clmax, o));
-    cumax = fmax(cumax, __shfl_xor(cumax, o));
-    cmax = fmax(cmax, __shfl_xor(cmax, o));
-  }
+  // wave reductions (DPP, cpl_wave.hpp; all lanes end with the totals)
+  dmax = wave_max(dmax);
+  clmax = wave_max(clmax);
+  cumax = wave_max(cumax);
+  cmax = wave_max(cmax);
   zs = ipm_wave_sum(zs);
   ys = ipm_wave_sum(ys);
   const double s_max = 100.0;
@@ -190,8 +184,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_optimality_kernel(
         em = fmax(em, fabs(cu[h] - (hasU[k] ? mu : 0.0)));
       }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) em = fmax(em, __shfl_xor(em, o));
+    em = wave_max(em);
     const double err_mu = fmax(base, em / sc);
     if (act && err_mu <= 10.0 * mu && mu > tol / 10.0) {
       mu = fmax(fmin(0.2 * mu, pow(mu, 1.5)), tol / 10.0);
@@ -246,8 +239,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_max_step_kernel(int64_t batch, in
       if (hasU[k] && d2k < 0.0) r = fmin(r, -t * v2k / d2k);
     }
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) r = fmin(r, __shfl_xor(r, o));
+  r = wave_min(r);
   if (lane == 0) out[b] = fmin(r, 1.0);
 }
 
@@ -361,11 +353,8 @@ __global__ __launch_bounds__(256) void cpl_ipm_post_step_kernel(
     dzL[b * nw + k] = dzl;
     dzU[b * nw + k] = dzu;
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    rp = fmin(rp, __shfl_xor(rp, o));
-    rz = fmin(rz, __shfl_xor(rz, o));
-  }
+  rp = wave_min(rp);
+  rz = wave_min(rz);
   gd = ipm_wave_sum(gd);
   if (lane == 0) {
     a_max[b] = fmin(rp, 1.0);

@@ -24,6 +24,7 @@
 #include <string>
 
 #include "cpl_status.hpp"
+#include "cpl_wave.hpp"
 
 namespace cpl {
 
@@ -42,52 +43,6 @@ __device__ long long* g_kkt_prof;
 
 constexpr int KKT_THREADS = 256;
 constexpr int KKT_MAX_NW = 128;
-
-// Lane permutations by DPP (a VALU operand modifier, no LDS round trip — ds_bpermute, what
-// __shfl_xor lowers to, costs an LDS-crossbar trip per dword on the reductions' critical path).
-// An f64 moves as its two dwords.  Lanes of rows outside ROW_MASK receive 0.
-template <int CTRL, int ROW_MASK = 0xf>
-__device__ __forceinline__ double dpp_mov(double v) {
-  const long long bits = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(bits & 0xffffffffLL), CTRL, ROW_MASK, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(bits >> 32), CTRL, ROW_MASK, 0xf, false);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-constexpr int DPP_QUAD_XOR1 = 0xB1;        // quad_perm [1,0,3,2]
-constexpr int DPP_QUAD_XOR2 = 0x4E;        // quad_perm [2,3,0,1]
-constexpr int DPP_ROW_MIRROR = 0x140;      // lane i of a row of 16 <- lane 15 - i
-constexpr int DPP_ROW_HALF_MIRROR = 0x141; // lane i of a half-row of 8 <- lane 7 - i
-constexpr int DPP_ROW_BCAST15 = 0x142;     // lane 15 of each row -> the next row
-constexpr int DPP_ROW_BCAST31 = 0x143;     // lane 31 -> rows 2 and 3
-
-// Sums over aligned groups of 4 / 8 lanes, the total in every lane of the group (every lane of
-// the wave must execute them).
-__device__ __forceinline__ double group4_sum(double v) {
-  v += dpp_mov<DPP_QUAD_XOR1>(v);
-  return v + dpp_mov<DPP_QUAD_XOR2>(v);
-}
-__device__ __forceinline__ double group8_sum(double v) {
-  v = group4_sum(v);
-  return v + dpp_mov<DPP_ROW_HALF_MIRROR>(v);
-}
-
-// Broadcast lane `src` (wave-uniform) of a double with two v_readlane_b32 (no LDS round trip).
-__device__ __forceinline__ double wave_bcast(double v, int src) {
-  const long long bits = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)(bits & 0xffffffffLL), src);
-  const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), src);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-// Sum over the wave, in every lane: rows of 16 by DPP, rows combined into lane 63 by the two row
-// broadcasts, then read out of lane 63.
-__device__ __forceinline__ double wave_sum(double v) {
-  v = group8_sum(v);
-  v += dpp_mov<DPP_ROW_MIRROR>(v);
-  v += dpp_mov<DPP_ROW_BCAST15, 0xa>(v);
-  v += dpp_mov<DPP_ROW_BCAST31, 0xc>(v);
-  return wave_bcast(v, 63);
-}
 
 // Right-looking Cholesky of the n x n matrix H (row-major, stride n) in LDS, lower factor in place,
 // by one wave (wave-uniform control flow, no workgroup barriers): lanes own rows; LDS accesses of
@@ -611,8 +566,7 @@ __global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 
       // counts zero eigenvalues): numerically flat directions get delta_w, not an unbounded step
       double mmax = 0.0;
       for (int a = tid; a < nw; a += 64) mmax = fmax(mmax, fabs(M[a * nw + a]));
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) mmax = fmax(mmax, __shfl_xor(mmax, o));
+      mmax = wave_max(mmax);
       const double pivot_min = 2.220446049250313e-16 * mmax;
       #pragma unroll 1
       for (int attempt = 0; attempt < 64; ++attempt) {
@@ -648,11 +602,8 @@ __global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 
       double rmax = 0.0, qmax = 0.0;
       for (int r = tid; r < nw; r += 64) { rmax = fmax(rmax, fabs(e1[r])); qmax = fmax(qmax, fabs(q1[r])); }
       for (int k = tid; k < m; k += 64) { rmax = fmax(rmax, fabs(e2[k])); qmax = fmax(qmax, fabs(q2[k])); }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        rmax = fmax(rmax, __shfl_xor(rmax, o));
-        qmax = fmax(qmax, __shfl_xor(qmax, o));
-      }
+      rmax = wave_max(rmax);
+      qmax = wave_max(qmax);
       if (tid == 0) sh.flag = !(rmax <= 1e-13 * qmax);
     }
     __syncthreads();
