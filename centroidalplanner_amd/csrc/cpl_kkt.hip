@@ -63,8 +63,11 @@ __device__ __forceinline__ bool wave_cholesky(double* H, int n, double pivot_min
     // trailing update of the lower triangle, the (i, j) entries of the trailing square spread over
     // the lanes (independent read-modify-writes, about four per lane at n = 17)
     const int sq = n - k - 1;
+    // e / sq through a float reciprocal (exact: e < 128^2 and (e + 0.5) / sq sits >= 0.5 / sq from
+    // an integer, far above the float error) instead of an integer division per element
+    const float rsq = 1.0f / (float)(sq > 0 ? sq : 1);
     for (int e = lane; e < sq * sq; e += 64) {
-      const int ii = e / sq, jj = e - ii * sq;
+      const int ii = (int)(((float)e + 0.5f) * rsq), jj = e - ii * sq;
       if (jj <= ii) {
         const int i = k + 1 + ii, j = k + 1 + jj;
         H[i * n + j] -= H[i * n + k] * H[j * n + k];
@@ -409,8 +412,8 @@ __global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 
       const int j = m - 1;
       const double bj = beta[j];
       const double* v = QR + j * nw;
-      for (int base = 0; base < nw * 4; base += KKT_THREADS) {
-        const int c = (base + tid) >> 2;
+      for (int base = 0; base < (nw - j) * 4; base += KKT_THREADS) {
+        const int c = j + ((base + tid) >> 2);  // columns c < j are still e_c: H_j leaves them
         const bool act = c < nw;
         double sv = 0.0;
         if (act) {
@@ -431,8 +434,10 @@ __global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 
       const double b0 = beta[j], b1 = beta[j + 1], cj = cpair[j >> 1];
       const double* v0 = QR + j * nw;
       const double* v1 = QR + (j + 1) * nw;
-      for (int base = 0; base < nw * 4; base += KKT_THREADS) {
-        const int c = (base + tid) >> 2;
+      for (int base = 0; base < (nw - j) * 4; base += KKT_THREADS) {
+        // columns c < j are still e_c (every reflector applied so far, and H_j, H_{j+1}, are zero
+        // above their own row): only columns j .. nw-1 change
+        const int c = j + ((base + tid) >> 2);
         const bool act = c < nw;
         double a0 = 0.0, a1 = 0.0;
         if (act)
