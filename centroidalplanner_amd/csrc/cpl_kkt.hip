@@ -239,6 +239,17 @@ __host__ __device__ inline int kkt_lds_doubles(int nw, int m) {
   return nw * nw + m * nw + nz * nz + nw + m + (2 * nw > 3 * m ? 2 * nw : 3 * m);
 }
 
+// The factorisation (mode 0) also stages M Z [nw][nz] in LDS, right after tmp, when the larger
+// image still fits: the reduced Hessian's Z^T (M Z) then reads it from LDS instead of 24 dependent
+// rounds of L2 loads (at nw = 47, m = 30: 38.2 KiB, four workgroups per CU — measured as fast as
+// five for this kernel).  Otherwise M Z goes to the global workspace.
+__host__ __device__ inline bool kkt_mz_in_lds(int nw, int m) {
+  return (int64_t)(kkt_lds_doubles(nw, m) + nw * (nw - m) + 8) * 8 <= 160 * 1024;
+}
+__host__ __device__ inline int kkt_launch_lds_doubles(int nw, int m, int mode) {
+  return kkt_lds_doubles(nw, m) + (mode == 0 && kkt_mz_in_lds(nw, m) ? nw * (nw - m) : 0) + 8;
+}
+
 // NW, MM > 0: the kernel specialised for one system size (nw = NW, m = MM; the arguments are
 // ignored) — every stride, trip count and index division becomes a compile-time constant, which
 // the instruction-issue-bound kernel needs (SQ counters: ~75 % of wave cycles parked, the SIMDs'
@@ -479,12 +490,12 @@ __global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 
     sh.delta_c = def ? dc : 0.0;
   }
   __syncthreads();
-  // ---- reduced Hessian Hr = Z^T M Z (into tmp area: MZ [nw][nz] staged in e1.. is too small ->
-  // compute entry-wise: Hr[a][c] = sum_r Z[r][a] (sum_k M[r][k] Z[k][c]))
-  // MZ is staged in the dw/dy/e1/e2/tmp region, which is free at this point (>= 4 nw + m doubles).
+  // ---- reduced Hessian Hr = Z^T (M Z), M Z staged in LDS or the global workspace
   double* Hr0 = L;  // keep the unshifted reduced Hessian in the workspace slot of L first
   if (nz > 0) {
-    double* MZ = ws + b * kkt_ws_per(nw, m);  // global scratch (the workspace; overwritten at the end)
+    // LDS after tmp when it fits (kkt_mz_in_lds), else global scratch (the workspace; overwritten
+    // at the end)
+    double* MZ = kkt_mz_in_lds(nw, m) ? tmp + (2 * nw > 3 * m ? 2 * nw : 3 * m) : ws + b * kkt_ws_per(nw, m);
     // MZ = M Z: a thread per (row r, 4 columns), M[r][k] from global once per k, Z[k][c..c+3] from
     // LDS (reads past Z's last column land inside the LDS image and are discarded)
     const int nb = (nz + 3) >> 2;
@@ -713,7 +724,7 @@ int32_t cpl_kkt_solve(int32_t mode, int64_t batch, int32_t nw, int32_t m, const 
   if (mode == 0 && (!d_mu || !d_delta_w || !d_delta_c || !d_info))
     return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_solve: factorisation needs mu, delta_w, delta_c, info");
   if (batch > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_solve: batch too large");
-  const size_t lds = sizeof(double) * (size_t)(kkt_lds_doubles(nw, m) + 8);
+  const size_t lds = sizeof(double) * (size_t)kkt_launch_lds_doubles(nw, m, mode);
   if (lds > 160 * 1024) return fail(CPL_ERR_UNSUPPORTED, "cpl_kkt_solve: system too large for one LDS image");
   hipLaunchKernelGGL(kkt_kernel_for(nw, m), dim3((unsigned)batch), dim3(KKT_THREADS), lds, (hipStream_t)stream, (int)mode,
                      batch, (int)nw, (int)m, d_M, d_A, d_r1, d_r2, d_mu, d_delta_w_last, d_active, d_dw, d_dy,

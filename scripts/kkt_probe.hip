@@ -104,7 +104,7 @@ int main(int argc, char** argv) {
   // how the kernel's time scales with resident workgroups per CU
   for (int a = 4; a < argc; ++a) {
     const size_t pad = (size_t)std::atol(argv[a]);
-    const size_t lds = sizeof(double) * (size_t)(kkt_lds_doubles(nw, m) + 8) + pad;
+    const size_t lds = sizeof(double) * (size_t)kkt_launch_lds_doubles(nw, m, 0) + pad;
     int per_cu = 0;
     CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kkt_kernel_for(nw, m)),
                                                     KKT_THREADS, lds));
