@@ -403,9 +403,36 @@ __global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 
       if (j + 3 < m) upd(j + 3);
       house2(j + 2);
     } else {
-      for (int k = j + 2 + 2 * wid; k < m; k += 2 * (nwaves - 1)) {
-        upd(k);
-        if (k + 1 < m) upd(k + 1);
+      // the other waves: column pairs j+2+2 wid, then every 2 (nwaves-1) columns — four columns
+      // per pass with their loads issued together (the reflector weights of the lane's rows held
+      // in registers), the same arithmetic as upd()
+      const int i0 = j + lane, i1 = i0 + 64;
+      const double w00 = i0 == j ? 1.0 : (i0 < nw ? v0[i0] : 0.0);
+      const double w01 = i0 == j ? 0.0 : (i0 == j + 1 ? 1.0 : (i0 < nw ? v1[i0] : 0.0));
+      const double w10 = i1 < nw ? v0[i1] : 0.0;
+      const double w11 = i1 < nw ? v1[i1] : 0.0;
+      const int step = 2 * (nwaves - 1);
+#pragma unroll 1
+      for (int kb = j + 2 + 2 * wid; kb < m; kb += 2 * step) {
+        const int ks[4] = {kb, kb + 1, kb + step, kb + step + 1};
+        double y0[4], y1[4], s0[4], s1[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const bool ok = ks[u] < m;
+          const double* y = QR + ks[u] * nw;
+          y0[u] = ok && i0 < nw ? y[i0] : 0.0;
+          y1[u] = ok && i1 < nw ? y[i1] : 0.0;
+          s0[u] = ok ? s0v[ks[u]] : 0.0;
+          s1[u] = ok ? s1v[ks[u]] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (ks[u] < m) {
+            double* y = QR + ks[u] * nw;
+            if (i0 < nw) y[i0] = y0[u] - (s0[u] * w00 + s1[u] * w01);
+            if (i1 < nw) y[i1] = y1[u] - (s0[u] * w10 + s1[u] * w11);
+          }
+        }
       }
     }
     __syncthreads();
