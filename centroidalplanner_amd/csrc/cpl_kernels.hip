@@ -1460,24 +1460,14 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
 //           J_F = I - n n^T, J_n = -(n F^T + s I), d2 t_j/dF_a dn_b = -(delta_ab n_j + n_a delta_jb),
 //           d2 t_j/dn_a dn_b = -(F_a delta_jb + F_b delta_ja); at |t| = 0 the |t| terms count as 0
 //           (the reference's Jacobian is 0/0 there; the product path takes NaN as 0).
-// One thread per entry of the [nf, nf] output (free_idx: free variable -> column of x).
+// One workgroup per instance: the same-contact (F, n) x (F, n) entries — the only ones with the
+// cone's square root and divisions — are computed once per contact (36 per contact) into LDS, then
+// the [nf, nf] output is written row-major with coalesced stores, every other entry computed in
+// place (the cheap cost / torque terms).  Each entry is the same expression as a thread per entry
+// (bitwise the same values); this layout keeps the cone's transcendental path off every wave.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void cpl_lagrangian_hessian_kernel(const KParams K, int64_t total, int nf,
-                                                                     const double* __restrict__ x,
-                                                                     const double* __restrict__ y,
-                                                                     const uint8_t* __restrict__ active,
-                                                                     const int32_t* __restrict__ free_idx,
-                                                                     double* __restrict__ H) {
-  __shared__ int s_pos[CPL_MAX_CONTACTS];  // block position (map order) of contact i
-  if (threadIdx.x < K.N) s_pos[K.map_order[threadIdx.x]] = threadIdx.x;
-  __syncthreads();
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= total) return;
-  const int per = nf * nf;
-  const int64_t b = e / per;
-  if (active && !active[b]) return;
-  const int kl = (int)(e - b * per);
-  const int uu = free_idx[kl / nf], vv = free_idx[kl - (kl / nf) * nf];
+__device__ __forceinline__ double hessian_entry(const KParams& K, const double* __restrict__ xb,
+                                                const double* __restrict__ yb, const int* s_pos, int uu, int vv) {
   // decode: kind 0 CoM, 1 F, 2 p, 3 n; contact i; axis a
   auto decode = [](int u, int& kind, int& i, int& a) {
     if (u < 3) { kind = 0; i = -1; a = u; return; }
@@ -1490,8 +1480,6 @@ __global__ __launch_bounds__(256) void cpl_lagrangian_hessian_kernel(const KPara
   int ku, iu, au, kv, iv, av;
   decode(uu, ku, iu, au);
   decode(vv, kv, iv, av);
-  const double* xb = x + b * (int64_t)K.n;
-  const double* yb = y + b * (int64_t)K.m;
   double h = 0.0;
   // cost (diagonal)
   if (uu == vv) h += ku == 0 ? K.W_com : (ku == 1 ? K.W_F[iu] : (ku == 2 ? K.W_p[iu] : 0.0));
@@ -1542,7 +1530,51 @@ __global__ __launch_bounds__(256) void cpl_lagrangian_hessian_kernel(const KPara
       h += y1 * ((jj - pu * pv) / rr + second);
     }
   }
-  H[e] = h;
+  return h;
+}
+
+__global__ __launch_bounds__(256) void cpl_lagrangian_hessian_kernel(const KParams K, int64_t batch, int nf,
+                                                                     const double* __restrict__ x,
+                                                                     const double* __restrict__ y,
+                                                                     const uint8_t* __restrict__ active,
+                                                                     const int32_t* __restrict__ free_idx,
+                                                                     double* __restrict__ H) {
+  __shared__ int s_pos[CPL_MAX_CONTACTS];          // block position (map order) of contact i
+  __shared__ double s_cone[CPL_MAX_CONTACTS * 36];  // (F, n) x (F, n) entries of contact i
+  __shared__ int s_col[3 + 9 * CPL_MAX_CONTACTS];   // free index -> column of x
+  const int64_t b = blockIdx.x;
+  if (b >= batch || (active && !active[b])) return;  // (uniform per workgroup)
+  const int tid = threadIdx.x;
+  if (tid < K.N) s_pos[K.map_order[tid]] = tid;
+  for (int k = tid; k < nf; k += blockDim.x) s_col[k] = free_idx[k];
+  __syncthreads();
+  const double* xb = x + b * (int64_t)K.n;
+  const double* yb = y + b * (int64_t)K.m;
+  // (F, n) x (F, n) blocks: local index 0-2 F_a (column 3 + 9i + a), 3-5 n_a (column 9 + 9i + a)
+  for (int t = tid; t < 36 * K.N; t += blockDim.x) {
+    const int i = t / 36, r = t - 36 * i, u6 = r / 6, v6 = r - 6 * (r / 6);
+    const int uu = 3 + 9 * i + (u6 < 3 ? u6 : 3 + u6), vv = 3 + 9 * i + (v6 < 3 ? v6 : 3 + v6);
+    s_cone[t] = hessian_entry(K, xb, yb, s_pos, uu, vv);
+  }
+  __syncthreads();
+  double* Hb = H + b * (int64_t)nf * nf;
+  // row-major walk of the output: (row, col) of entry tid + 256 s advanced incrementally
+  const int step_r = blockDim.x / nf, step_c = blockDim.x - step_r * nf;
+  int row = tid / nf, col = tid - row * nf;
+  for (int e = tid; e < nf * nf; e += blockDim.x) {
+    const int uu = s_col[row], vv = s_col[col];
+    const int ru = uu - 3, rv = vv - 3;
+    const int iu = ru / 9, iv = rv / 9, tu = ru - 9 * iu, tv = rv - 9 * iv;
+    double h;
+    if (uu >= 3 && vv >= 3 && iu == iv && (tu < 3 || tu >= 6) && (tv < 3 || tv >= 6))
+      h = s_cone[36 * iu + 6 * (tu < 3 ? tu : tu - 3) + (tv < 3 ? tv : tv - 3)];
+    else
+      h = hessian_entry(K, xb, yb, s_pos, uu, vv);
+    Hb[e] = h;
+    row += step_r;
+    col += step_c;
+    if (col >= nf) { col -= nf; ++row; }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1968,10 +2000,8 @@ int32_t cpl_lagrangian_hessian(const cpl_problem_desc* d, int64_t batch, const d
   if (batch < 0 || nf <= 0 || nf > K.n) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_lagrangian_hessian: bad sizes");
   if (batch == 0) return CPL_OK;
   if (!d_x || !d_y || !d_free_idx || !d_H) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_lagrangian_hessian: missing buffer");
-  const int64_t total = batch * (int64_t)nf * nf;
-  const int64_t blocks = (total + 255) / 256;
-  if (blocks > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_lagrangian_hessian: batch too large");
-  hipLaunchKernelGGL(cpl_lagrangian_hessian_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, K, total,
+  if (batch > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_lagrangian_hessian: batch too large");
+  hipLaunchKernelGGL(cpl_lagrangian_hessian_kernel, dim3((unsigned)batch), dim3(256), 0, (hipStream_t)stream, K, batch,
                      (int)nf, d_x, d_y, d_active, d_free_idx, d_H);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "cpl_lagrangian_hessian launch");
