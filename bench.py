@@ -8,17 +8,21 @@ replay launches a bucket's steps, and with N > 1 ranks one RCCL all-gather (asyn
 collective stream) carries the bucket's per-step norms.  Instances shard
 across ranks with no data-path exchange: per-rank batch is fixed -> weak scaling.
 
-Default workload = BASELINE.json configs[1]: 4-contact Ground env, batch 65,536 per GPU.
+Default workload = the north-star point BASELINE.json's metric is quoted on: 4-contact Ground env,
+batch 1,048,576 per GPU (1.95 GB of algorithmic traffic per step, far past the 256 MiB Infinity
+Cache).  BASELINE.json configs[1] (65,536 instances) is reported beside it as a side field.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config ground4|sq8|mixed16|ground4_1m|none4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config ground4_1m|ground4|sq8|mixed16|none4|solve5]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 Rank 0 prints one JSON line.  Fields beyond the driver contract:
   roofline      dominant kernel (cpl_eval_*): algorithmic bytes per launch / mean launch
                 duration from HIP events on the launch stream; traffic = HBM bytes per launch from
                 rocprofv3 PMC passes (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE)
-  cpu_baseline  the oracle (CPU restatement, "port") on the host cores, bounded sample
-  target_1m     the north-star point (1,048,576 x 4 contacts, Ground) on the same GPU
+  cpu_baseline  the oracle (CPU restatement, "port") on the host cores, bounded sample, plus a
+                single-core figure, the CPU model and the affinity count
+  check         checker leg (after timing): a strided sample of the TIMED g / jac against the oracle
+  configs1_65k  BASELINE.json configs[1] (65,536 x 4 Ground) kernel time on the same GPU
 """
 from __future__ import annotations
 
@@ -62,11 +66,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="ground4", help="ground4 | sq8 | mixed16 | ground4_1m | none4 | solve5")
+    ap.add_argument("--config", default="ground4_1m", help="ground4_1m | ground4 | sq8 | mixed16 | none4 | solve5")
     ap.add_argument("--batch", type=int, default=0, help="override per-GPU batch")
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-target", action="store_true")
+    ap.add_argument("--no-side", action="store_true", help="skip the configs[1] side measurement")
+    ap.add_argument("--no-check", action="store_true", help="skip the checker leg")
+    ap.add_argument("--check-sample", type=int, default=4096, help="instances in the checker leg's strided sample")
     ap.add_argument("--no-graph", action="store_true", help="launch each step from Python instead of a HIP graph")
     ap.add_argument("--bucket", type=int, default=10,
                     help="steps per HIP-graph replay and per residual-norm all-gather (1 = per step)")
@@ -133,20 +139,49 @@ def collect_pmc(args, timeout=240):
 # ------------------------------------------------------------------------------------------
 # CPU baseline: the oracle (CPU restatement of the reference path) on the host cores
 # ------------------------------------------------------------------------------------------
+def host_cpu_info():
+    """CPU model, the affinity count of this process and the threads the CPU legs use.  Threads =
+    the CPUs this process may run on (sched_getaffinity), capped by OMP_NUM_THREADS when the
+    environment sets it (the GPU box sets it to the box's CPU share, 16 per GPU: its affinity mask
+    shows the whole host)."""
+    affinity = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(affinity, omp) if omp > 0 else affinity
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "affinity": affinity, "omp_num_threads": omp or None, "threads": threads}
+
+
 def cpu_baseline(cfg, seconds):
     """The oracle on the host cores: a fixed sample of the workload evaluated `reps` times so that
-    the timed CPU work lasts about `seconds` (10-30 s), threads = the box's CPU share."""
+    the timed CPU work lasts about `seconds` (10-30 s) on every usable core (host_cpu_info), then a
+    smaller sample on one core for about a quarter of that."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     from centroidalplanner_amd.workload import config_inputs
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+    info = host_cpu_info()
+    threads = info["threads"]
     B = min(cfg.batch, 262144)
     prob, x, mass, tag = config_inputs(cfg, B)
     t1 = pyoracle.time_eval_batch(prob.desc(), x, mass, tag, outputs=("g", "jac"), nthreads=threads, reps=1)
     reps = max(1, int(round(seconds / max(t1, 1e-6))))
     t = pyoracle.time_eval_batch(prob.desc(), x, mass, tag, outputs=("g", "jac"), nthreads=threads, reps=reps)
     _, m = algorithmic_bytes(cfg.n_contacts, cfg.env)  # t: seconds per pass
+    # single core: the first B1 instances of the same sample
+    B1 = min(B, 16384)
+    s1 = pyoracle.time_eval_batch(prob.desc(), x[:B1], None if mass is None else mass[:B1],
+                                  None if tag is None else tag[:B1], outputs=("g", "jac"), nthreads=1, reps=1)
+    reps1 = max(1, int(round(0.25 * seconds / max(s1, 1e-6))))
+    s1 = pyoracle.time_eval_batch(prob.desc(), x[:B1], None if mass is None else mass[:B1],
+                                  None if tag is None else tag[:B1], outputs=("g", "jac"), nthreads=1, reps=reps1)
     return {
         "value": B * m / t,
         "unit": "rows/s",
@@ -155,7 +190,43 @@ def cpu_baseline(cfg, seconds):
         "sample": f"{B} instances of '{cfg.name}' x {reps} passes (g+jac, IFOPT-order assembly) in {t * reps:.1f} s "
                   f"on {threads} threads",
         "instances_per_s": B / t,
+        "single_core": {"value": B1 * m / s1, "unit": "rows/s", "instances_per_s": B1 / s1,
+                        "sample": f"{B1} instances x {reps1} passes in {s1 * reps1:.1f} s on 1 thread"},
+        **{k: info[k] for k in ("cpu_model", "affinity", "omp_num_threads")},
     }
+
+
+def checker_leg(prob, env, xt, mt, tt, out, batch, sample):
+    """Checker (outside every timed region): a strided sample of the instances whose g / jac the
+    timed steps wrote, recomputed by the oracle from the same device inputs and compared with the
+    parity policy of tests/parity_util.py (bit-identical for everything without a data-dependent
+    pow).  Test infrastructure: the oracle is the checker here, never the thing measured."""
+    import numpy as np
+    import torch
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import pyoracle
+    from parity_util import check_outputs
+
+    stride = max(1, batch // max(1, sample))
+    idx = torch.arange(0, batch, stride, device=xt.device)
+    idx = torch.unique(torch.cat([idx, torch.tensor([batch - 1], device=xt.device)]))  # include the tail
+    x = xt[idx].cpu().numpy()
+    mass = mt[idx].cpu().numpy() if mt is not None else None
+    tag = tt[idx].cpu().numpy() if tt is not None else None
+    got = {k: out[k][idx].cpu().numpy() for k in ("g", "jac")}
+    ref = pyoracle.eval_batch(prob.desc(), x, mass, tag, outputs=("g", "jac"))
+    res = {"instances": int(idx.numel()), "stride": stride, "policy": "tests/parity_util.py"}
+    try:
+        rep = check_outputs(prob, env, x, got, ref, tag)
+        res["ok"] = True
+        res["bitwise_frac"] = {k: v["bitwise_frac"] for k, v in rep.items()}
+    except AssertionError as e:
+        res["ok"] = False
+        res["error"] = str(e)[:400]
+    res["finite"] = bool(np.isfinite(got["g"]).all() and np.isfinite(got["jac"]).all())
+    return res
 
 
 # ------------------------------------------------------------------------------------------
@@ -335,10 +406,13 @@ def main():
 
     def run_bucket(i, count):
         j = i % 2
-        if pending[j] is not None:  # the all-gather still reading norms[j] (two buckets ago)
-            pending[j].wait()
-            pending[j] = None
         with torch.cuda.stream(stream):
+            if pending[j] is not None:
+                # the all-gather of two buckets ago may still be reading norms[j]: on RCCL, wait()
+                # orders the CURRENT stream (the launch stream here) after the collective, so the
+                # replay below cannot overwrite norms[j] under it
+                pending[j].wait()
+                pending[j] = None
             if graphs:
                 graphs[(j, count)].replay()
             else:
@@ -382,7 +456,11 @@ def main():
 
         last, cnt = gathered[-1]
         step_norms = combine_bucket(last, world, cnt)
-        gather_info = {"steps_in_last_bucket": cnt, "last_step_global_norms": list(step_norms[-1])}
+        # this rank's rows of the gathered bucket must be the norms it computed locally
+        local = norms[(len(buckets(K)) - 1) % 2][:cnt]
+        mine = last.view(world, cnt, 2)[rank]  # rank-major [world * cnt, 2]
+        gather_info = {"steps_in_last_bucket": cnt, "last_step_global_norms": list(step_norms[-1]),
+                       "local_rows_match": bool(torch.equal(mine.to(local.device), local))}
 
     # live kernel timing: HIP events on the launch stream around back-to-back eval launches only
     ms = ctypes.c_double()
@@ -403,27 +481,36 @@ def main():
     value = rows_total / dt
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
 
-    target = None
-    if rank == 0 and world == 1 and not args.no_target and args.config == "ground4":
+    check = None
+    if rank == 0 and not args.no_check:
+        try:
+            check = checker_leg(prob, cfg.env, xt, mt, tt, out, batch, args.check_sample)
+        except Exception as e:  # noqa: BLE001
+            check = {"ok": False, "error": f"checker leg failed: {e}"}
+
+    side = None
+    if rank == 0 and world == 1 and not args.no_side and args.config == "ground4_1m":
+        # BASELINE.json configs[1] (65,536 x 4 Ground) on the same GPU: kernel time only
         del out
         torch.cuda.empty_cache()
-        tcfg = CONFIGS["ground4_1m"]
-        tb = tcfg.batch
-        tp = make_problem(tcfg.n_contacts, tcfg.env)
-        x1, m1, _ = generate(tcfg.n_contacts, tcfg.env, tb, 0xC910 + tcfg.config_id)
+        scfg = CONFIGS["ground4"]
+        sb = scfg.batch
+        sp = make_problem(scfg.n_contacts, scfg.env)
+        x1, m1, _ = generate(scfg.n_contacts, scfg.env, sb, 0xC910 + scfg.config_id)
         x1t, m1t = torch.tensor(x1, device=dev), torch.tensor(m1, device=dev)
         del x1, m1
-        o1 = tp.eval_batch(x1t, m1t, outputs=("g", "jac", "norms"))
-        _abi.check(_abi.lib.cpl_time_eval_batch(ctypes.byref(tp.desc()), tb, p(x1t), p(m1t), None, p(o1["g"]), p(o1["jac"]), None,
-                                                None, p(o1["norms"]), ctypes.c_void_p(stream.cuda_stream), 20,
+        o1 = sp.eval_batch(x1t, m1t, outputs=("g", "jac", "norms"))
+        _abi.check(_abi.lib.cpl_time_eval_batch(ctypes.byref(sp.desc()), sb, p(x1t), p(m1t), None, p(o1["g"]), p(o1["jac"]),
+                                                None, None, p(o1["norms"]), ctypes.c_void_p(stream.cuda_stream), 50,
                                                 ctypes.byref(ms)))
-        tbytes, tm = algorithmic_bytes(4, "ground")
-        target = {
-            "workload": tcfg.name,
+        sbytes, sm = algorithmic_bytes(4, "ground")
+        side = {
+            "workload": scfg.name,
             "kernel_ms": ms.value,
-            "rows_per_s": tb * tm / (ms.value * 1e-3),
-            "hbm_gbps": tbytes * tb / (ms.value * 1e-3) / 1e9,
-            "frac_of_peak": tbytes * tb / (ms.value * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+            "rows_per_s": sb * sm / (ms.value * 1e-3),
+            "hbm_gbps": sbytes * sb / (ms.value * 1e-3) / 1e9,
+            "frac_of_peak": sbytes * sb / (ms.value * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+            "note": "128 MB working set: fits the 256 MiB Infinity Cache",
         }
 
     if rank == 0:
@@ -467,8 +554,9 @@ def main():
             },
             "cpu_baseline": cpu,
         }
-        if target:
-            res["target_1m"] = target
+        res["check"] = check
+        if side:
+            res["configs1_65k"] = side
         print(json.dumps(res), flush=True)
 
     if world > 1:

@@ -175,6 +175,9 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     I = torch.as_tensor(I_np, device=dev)
     nI = I_np.size
     nw = nf + nI
+    if use_hip and nw > 128:  # the device kernels stage one instance's primal-slack vector per wave
+        raise ValueError(f"batch_ipm_solve: {nw} primal-slack unknowns (free variables + inequality rows); "
+                         "the device solve loop supports at most 128 (about 11 contacts with an environment)")
     zeros_B = torch.zeros(B, dtype=dt, device=dev)
     # A = dc/dw = [J[:, free] | -P], P[r, j] = 1 where row r is inequality j
     P = torch.zeros(m, nI, dtype=dt, device=dev)

@@ -623,6 +623,8 @@ int32_t cpl_ipm_newton_setup(int64_t batch, int32_t nw, int32_t m, int32_t nf, c
                              int32_t h_sym, double* d_M, double* d_r1, double* d_r2, double* d_gphi, double* d_mr_diag,
                              double* d_theta, double* d_phi, const uint8_t* d_active, void* stream) {
   if (batch < 0 || nw <= 0 || m < 0 || nf < 0 || nf > nw) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_newton_setup: bad sizes");
+  // Sigma is staged per wave in sig_s[IPM_WAVES][128] (same limit as cpl_ipm_optimality / cpl_kkt_solve)
+  if (nw > 128) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_newton_setup: nw > 128 is not supported");
   if (batch == 0) return CPL_OK;
   if (!d_w || !d_zL || !d_zU || !d_gw || (m > 0 && (!d_A || !d_y || !d_c || !d_r2)) || !d_f || !d_mu || !d_hasL ||
       !d_hasU || !d_wl0 || !d_wu0 || !d_M || !d_r1 || !d_gphi || !d_mr_diag || !d_theta || !d_phi)

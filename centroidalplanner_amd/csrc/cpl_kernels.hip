@@ -22,6 +22,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "cpl_layout.hpp"
@@ -1801,11 +1802,16 @@ struct PipeLaunch {
 };
 
 // Workspace of the fused residual norms: one partial pair per workgroup, per (device, stream) so
-// that launches on different streams never share it.  Grown on demand
-// (hipFree synchronises the device, so a smaller buffer is never freed under a running kernel).
+// that launches on different streams never share it.  Grown on demand, and a buffer is NEVER freed
+// while the process runs: a HIP graph captured on the stream keeps the pointer it saw, so a later,
+// larger launch on the same stream must not release it under the graph (the retired buffers are
+// kept in `old`).  Growing needs hipMalloc, which a stream capture forbids: warm the launch up on
+// the stream (one eager launch of the largest batch) before capturing it — a capture that would
+// have to grow the workspace fails with CPL_ERR_RUNTIME instead.
 struct NormWs {
   double* ptr = nullptr;
   size_t cap = 0;  // partial pairs
+  std::vector<double*> old;
 };
 static std::mutex g_norm_ws_mutex;
 static std::map<std::pair<int, hipStream_t>, NormWs> g_norm_ws;
@@ -1817,16 +1823,42 @@ static int32_t norm_workspace(hipStream_t stream, size_t blocks, double** out) {
   std::lock_guard<std::mutex> lk(g_norm_ws_mutex);
   NormWs& w = g_norm_ws[{dev, stream}];
   if (w.cap < blocks) {
-    if (w.ptr) (void)hipFree(w.ptr);
-    w.ptr = nullptr;
-    w.cap = 0;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+      return fail(CPL_ERR_RUNTIME,
+                  "fused residual norms: the per-stream workspace must grow, which a stream capture forbids; "
+                  "launch the largest batch once on this stream before capturing");
     const size_t cap = blocks < 4096 ? 4096 : blocks;
-    e = hipMalloc(&w.ptr, sizeof(double) * (NORM_HDR + 4 * cap));
+    double* p = nullptr;
+    e = hipMalloc(&p, sizeof(double) * (NORM_HDR + 4 * cap));
     if (e != hipSuccess) return hip_fail(e, "hipMalloc norms workspace");
+    if (w.ptr) w.old.push_back(w.ptr);  // possibly captured by a graph: kept alive
+    w.ptr = p;
     w.cap = cap;
   }
   *out = w.ptr;
   return CPL_OK;
+}
+
+// Launch geometry of the persistent pipelined kernel, cached per (device, kernel, LDS bytes): the
+// CU count and the occupancy query cost host time on every launch otherwise (the single-instance
+// TNLP path makes one launch per callback).
+static std::mutex g_occ_mutex;
+static std::map<std::tuple<int, const void*, size_t>, int64_t> g_occ;
+
+static int64_t resident_blocks(const void* kern, size_t lds) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  const auto key = std::make_tuple(dev, kern, lds);
+  std::lock_guard<std::mutex> lk(g_occ_mutex);
+  auto it = g_occ.find(key);
+  if (it != g_occ.end()) return it->second;
+  int cus = 256, per_cu = 1;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+  const int64_t v = (int64_t)(cus > 0 ? cus : 256) * per_cu;
+  g_occ.emplace(key, v);
+  return v;
 }
 
 struct LGradArgs {
@@ -1896,13 +1928,8 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
         {cpl_eval_pipe_kernel<CPL_ENV_SUPERQUADRIC, 3, false>, cpl_eval_pipe_kernel<CPL_ENV_SUPERQUADRIC, 3, true>},
         {cpl_eval_pipe_kernel<CPL_ENV_MIXED, 3, false>, cpl_eval_pipe_kernel<CPL_ENV_MIXED, 3, true>}};
     const KernT kern = table[K.env_kind][g_nt ? 1 : 0];
-    int dev = 0, cus = 256, per_cu = 1;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), 256, lds) !=
-            hipSuccess || per_cu < 1)
-      per_cu = 1;
     const int64_t ntiles = (batch + K.T - 1) / K.T;
-    const int64_t want = (int64_t)cus * per_cu;
+    const int64_t want = resident_blocks(reinterpret_cast<const void*>(kern), lds);
     unsigned grid = (unsigned)(ntiles < want ? ntiles : want);
     if (K.want_norms && (st = norm_workspace(stream, grid, &ws))) return st;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, stream, K, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f,

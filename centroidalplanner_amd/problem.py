@@ -377,13 +377,17 @@ class CplProblem:
             t = out.get(k) if out else None
             if t is None:
                 t = torch.empty(shapes[k], dtype=torch.float64, device=x.device)
-            elif tuple(t.shape) != shapes[k] or t.dtype != torch.float64 or not t.is_contiguous():
-                raise InvalidArgument(_abi.ERR_INVALID_ARGUMENT, f"output '{k}' must be float64 {shapes[k]}")
+            elif (tuple(t.shape) != shapes[k] or t.dtype != torch.float64 or not t.is_contiguous()
+                  or t.device != x.device):
+                raise InvalidArgument(_abi.ERR_INVALID_ARGUMENT,
+                                      f"output '{k}' must be a contiguous float64 tensor {shapes[k]} on {x.device}")
             res[k] = t
-        if mass is not None and (mass.dtype != torch.float64 or tuple(mass.shape) != (B,) or not mass.is_cuda):
-            raise InvalidArgument(_abi.ERR_INVALID_ARGUMENT, "mass must be a float64 CUDA tensor [B]")
-        if env_tag is not None and (env_tag.dtype != torch.uint8 or tuple(env_tag.shape) != (B,)):
-            raise InvalidArgument(_abi.ERR_INVALID_ARGUMENT, "env_tag must be a uint8 CUDA tensor [B]")
+        if mass is not None and (mass.dtype != torch.float64 or tuple(mass.shape) != (B,) or mass.device != x.device
+                                 or not mass.is_contiguous()):
+            raise InvalidArgument(_abi.ERR_INVALID_ARGUMENT, f"mass must be a contiguous float64 tensor [B] on {x.device}")
+        if env_tag is not None and (env_tag.dtype != torch.uint8 or tuple(env_tag.shape) != (B,)
+                                    or env_tag.device != x.device or not env_tag.is_contiguous()):
+            raise InvalidArgument(_abi.ERR_INVALID_ARGUMENT, f"env_tag must be a contiguous uint8 tensor [B] on {x.device}")
         s = stream if stream is not None else torch.cuda.current_stream(x.device)
 
         def p(t):
@@ -393,8 +397,8 @@ class CplProblem:
             t = out.get("norms") if out else None
             if t is None:
                 t = torch.empty(2, dtype=torch.float64, device=x.device)
-            elif tuple(t.shape) != (2,) or t.dtype != torch.float64:
-                raise InvalidArgument(_abi.ERR_INVALID_ARGUMENT, "output 'norms' must be float64 (2,)")
+            elif tuple(t.shape) != (2,) or t.dtype != torch.float64 or t.device != x.device or not t.is_contiguous():
+                raise InvalidArgument(_abi.ERR_INVALID_ARGUMENT, f"output 'norms' must be a contiguous float64 (2,) tensor on {x.device}")
             res["norms"] = t
             check(lib.cpl_eval_batch_norms(ctypes.byref(self.desc()), B, p(x), p(mass), p(env_tag), p(res.get("g")),
                                            p(res.get("jac")), p(res.get("f")), p(res.get("grad")), p(t),
