@@ -8,10 +8,12 @@ wrong constraint value or Jacobian in the oracle would either stop the solve fro
 produce a solution that violates the independently computed invariants below (force / torque
 balance, friction cone, surface and bounds).
 
-Start point: the reference starts IPOPT from x = 0, where FrictionCone's Jacobian is 0/0
-(src/Constraints/FrictionCone.cpp:85-87); the driver (centroidalplanner_amd/ipm.py, a restatement
-of IPOPT's method) starts from a non-degenerate point instead and treats NaN Jacobian entries (a cone
-at zero tangential force) as 0 — a property of the driver, not of the callbacks.
+Start point: the reference starts IPOPT from x = 0 (Variable3D init, src/Variable3D.cpp:8-10),
+where FrictionCone's Jacobian is 0/0 (src/Constraints/FrictionCone.cpp:85-87).  testSimpleProblem
+is solved from exactly that point by the batched interior-point loop on one instance
+(batch_ipm.py, IPOPT's method; NaN Jacobian entries of a cone at zero tangential force count as 0).
+The 4-contact scenarios run the facade's default single-instance driver (SLSQP) from a
+non-degenerate start.
 """
 import numpy as np
 import pytest
@@ -32,7 +34,7 @@ class OracleEvaluator:
 
 
 def _gpu_evaluator(problem):
-    from centroidalplanner_amd.ipm import TorchEvaluator
+    from centroidalplanner_amd.solver import TorchEvaluator
 
     return TorchEvaluator(problem)
 
@@ -60,16 +62,16 @@ BACKENDS = [pytest.param("oracle"), pytest.param("gpu", marks=pytest.mark.gpu)]
 
 @pytest.mark.parametrize("backend", BACKENDS)
 def test_simple_problem(backend):
-    """TestBasic.cpp:28-61.
+    """TestBasic.cpp:28-61, solved: CentroidalPlanner(["contact1"], 100, Ground z = 0.1), default
+    settings, Solve() from the reference's start point x = 0, TestBasic's assertions.
 
     With one contact the equality Jacobian is rank-deficient for every x (the torque about the
-    force line, F . ((p - c) x F), is identically zero), which SLSQP cannot take.  The optimum is
-    known in closed form instead: F = -m g (force balance), p directly below c (torque), p_z = z_g,
-    n = (0,0,1), and the cost 1/2|c - (0,0,1)|^2 + 1/2|p|^2 + 1/2|F|^2 then gives c = (0,0,1),
-    p = (0,0,z_g).  The callbacks must certify it: every equality row zero, cones strictly
-    satisfied, and the KKT stationarity grad f + J_E^T lambda = 0 solvable (least squares) —
-    then TestBasic's own assertions are applied to that point.
-    """
+    force line, F . ((p - c) x F), is identically zero) — SLSQP cannot take that, the interior-point
+    loop (IPOPT's method, delta_c regularisation of the rank-deficient rows) can.  From x = 0 the
+    torque rows are identically zero (F = 0, p = c), their multipliers grow to ~1e9 in the first
+    steps, and the loop stops on IPOPT's scaled 'acceptable' test (s_d scales the dual error by the
+    multipliers' size) — TestBasic asserts the contact point, normal and vertical force, not the CoM
+    height, and so do we; the returned point is also checked feasible through the oracle."""
     robot_mass, g = 100.0, -9.81
     names = ["contact1"]
     ground_z = 0.1
@@ -77,35 +79,26 @@ def test_simple_problem(backend):
     env.SetGroundZ(ground_z)
     cpl = CentroidalPlanner(names, robot_mass, env)
     prob = cpl.GetCplProblem()
-    ev = OracleEvaluator(prob) if backend == "oracle" else _gpu_evaluator(prob)
-    x = np.zeros(prob.n)
-    x[0:3] = [0.0, 0.0, 1.0]
-    x[3:6] = [0.0, 0.0, -robot_mass * g]
-    x[6:9] = [0.0, 0.0, ground_z]
-    x[9:12] = [0.0, 0.0, 1.0]
-    o = ev.eval_batch(x[None])
-    n, m, nnz = prob.get_nlp_info()
-    iR, jC = prob.get_structure()
-    xl, xu, gl, gu = prob.get_bounds_info()
+    assert not prob.get_starting_point().any()  # x = 0, Variable3D's initial value
+    cpl.solver_method = "ipm"
+    if backend == "oracle":
+        cpl.evaluator = OracleEvaluator(prob)
+    sol = cpl.Solve()
+    Fz_tot = 0.0
+    for name, v in sol.contact_values_map.items():
+        Fz_tot += v.force_value[2]
+        assert v.position_value[2] == pytest.approx(ground_z, abs=1e-6)
+        assert np.linalg.norm(v.normal_value) == pytest.approx(1.0, abs=1e-6)
+        assert v.normal_value[2] == pytest.approx(1.0, abs=1e-6)
+    assert Fz_tot == pytest.approx(-robot_mass * g, abs=1e-6)
+    # feasibility through the oracle's callbacks at the returned point
+    x = prob.get_starting_point()  # Solve() leaves the solution in the problem's variables
+    o = OracleEvaluator(prob).eval_batch(x[None])
+    _, _, gl, gu = prob.get_bounds_info()
     gv = o["g"][0]
     eq = gl == gu
-    assert np.abs(gv[eq]).max() <= 1e-9
-    assert (gv[~eq] < 0).all()                          # both cone rows inactive
-    J = np.zeros((m, n))
-    J[iR, jC] = o["jac"][0]
-    JE = J[eq]
-    assert np.isfinite(JE).all()                        # the NaNs are confined to the (inactive) cone rows
-    lam, *_ = np.linalg.lstsq(JE.T, -o["grad"][0], rcond=None)
-    assert np.abs(o["grad"][0] + JE.T @ lam).max() <= 1e-8 * max(1.0, np.abs(o["grad"][0]).max())
-    prob.SetVariables(x)
-    sol = prob.GetSolution()
-    Fz_tot = 0.0
-    for name, v in sol["contact_values_map"].items():
-        Fz_tot += v["force"][2]
-        assert v["position"][2] == pytest.approx(ground_z, abs=1e-6)
-        assert np.linalg.norm(v["normal"]) == pytest.approx(1.0, abs=1e-6)
-        assert v["normal"][2] == pytest.approx(1.0, abs=1e-6)
-    assert Fz_tot == pytest.approx(-robot_mass * g, abs=1e-6)
+    assert np.abs(gv[eq]).max() <= 1e-6
+    assert (gv[~eq] <= 1e-9).all()
 
 
 @pytest.mark.parametrize("backend", BACKENDS)
