@@ -22,6 +22,8 @@ Rank 0 prints one JSON line.  Fields beyond the driver contract:
   cpu_baseline  the oracle (CPU restatement, "port") on the host cores, bounded sample, plus a
                 single-core figure, the CPU model and the affinity count
   check         checker leg (after timing): a strided sample of the TIMED g / jac against the oracle
+  jac_folded    the same batch with values-only Jacobian records (CPL_EVAL_JAC_FOLDED: structural
+                constants skipped), kernel time and bytes
   configs1_65k  BASELINE.json configs[1] (65,536 x 4 Ground) kernel time on the same GPU
 """
 from __future__ import annotations
@@ -488,6 +490,31 @@ def main():
         except Exception as e:  # noqa: BLE001
             check = {"ok": False, "error": f"checker leg failed: {e}"}
 
+    folded = None
+    if rank == 0 and world == 1 and not args.no_side:
+        # the values-only Jacobian layout (CPL_EVAL_JAC_FOLDED) of the same batch: the structural
+        # constants are not written (same g, the remaining Jacobian values bit-identical)
+        fo = prob.eval_batch(xt, mt, tt, outputs=("g", "jac", "norms"), jac_folded=True)
+        _abi.check(_abi.lib.cpl_time_eval_batch_ex(ctypes.byref(prob.desc()), batch, p(xt), p(mt), p(tt), p(fo["g"]),
+                                                   p(fo["jac"]), None, None, p(fo["norms"]), _abi.EVAL_JAC_FOLDED,
+                                                   ctypes.c_void_p(stream.cuda_stream), max(K, 20), ctypes.byref(ms)))
+        var_k, _, _ = prob.jac_fold_info()
+        same = None
+        if not args.no_check:
+            same = bool(torch.equal(out["jac"][:, torch.as_tensor(var_k.astype("int64"), device=dev)], fo["jac"])
+                        and torch.equal(out["g"], fo["g"]))
+        fbytes = 8 * (prob.n + 1 + prob.m + int(var_k.size))
+        folded = {
+            "kernel_ms": ms.value,
+            "bytes_per_instance": fbytes,
+            "rows_per_s": batch * m / (ms.value * 1e-3),
+            "hbm_gbps": fbytes * batch / (ms.value * 1e-3) / 1e9,
+            "frac_of_peak": fbytes * batch / (ms.value * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+            "speedup_vs_csr": kernel_ms / ms.value,
+            "values_equal_csr": same,
+        }
+        del fo
+
     side = None
     if rank == 0 and world == 1 and not args.no_side and args.config == "ground4_1m":
         # BASELINE.json configs[1] (65,536 x 4 Ground) on the same GPU: kernel time only
@@ -555,6 +582,8 @@ def main():
             "cpu_baseline": cpu,
         }
         res["check"] = check
+        if folded:
+            res["jac_folded"] = folded
         if side:
             res["configs1_65k"] = side
         print(json.dumps(res), flush=True)

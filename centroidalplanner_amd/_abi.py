@@ -27,6 +27,10 @@ ERR_UNSUPPORTED = 5
 
 INF = 1.0e20
 
+# cpl_eval_batch_ex output layout flags
+EVAL_JAC_FOLDED = 1
+EVAL_SOA = 2
+
 LIB_NAME = "libcpl_mi355x.so"
 # CPL_LIB: measurement-only override (A/B of two builds of the same ABI)
 LIB_PATH = os.environ.get("CPL_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
@@ -101,6 +105,17 @@ SIGNATURES = {
         c_int32,
         [_DESC_P, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_void_p, c_int32, _DP],
+    ),
+    "cpl_eval_batch_ex": (
+        c_int32,
+        [_DESC_P, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
+         c_void_p],
+    ),
+    "cpl_jac_fold_info": (c_int32, [_DESC_P, _IP, _IP, _IP, _IP, _DP]),
+    "cpl_time_eval_batch_ex": (
+        c_int32,
+        [_DESC_P, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_int32, c_void_p, c_int32, _DP],
     ),
     "cpl_kkt_workspace_doubles": (c_int64, [c_int32, c_int32]),
     "cpl_lagrangian_hessian": (c_int32, [_DESC_P, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,

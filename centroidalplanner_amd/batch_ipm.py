@@ -81,9 +81,10 @@ class KernelEvaluator:
         self.env_tag = env_tag
         self.calls = 0
 
-    def __call__(self, X, mass, outputs=("g", "jac", "f", "grad")):
+    def __call__(self, X, mass, outputs=("g", "jac", "f", "grad"), jac_folded=False):
+        """jac_folded: values-only Jacobian records (CPL_EVAL_JAC_FOLDED; CplProblem.jac_fold_info)."""
         self.calls += 1
-        return self.problem.eval_batch(X, mass, self.env_tag, outputs=outputs)
+        return self.problem.eval_batch(X, mass, self.env_tag, outputs=outputs, jac_folded=jac_folded)
 
     def lagrangian_grad(self, X, mass, y, y_repeat, csc, active=None):
         """grad f + J^T y of every instance in one fused launch (cpl_eval_lagrangian_grad: the
@@ -215,7 +216,20 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     csr_J = use_hip and not use_bfgs
     dense_pos = np.full(m * n, -1, dtype=np.int64)
     dense_pos[iRow.astype(np.int64) * n + jCol.astype(np.int64)] = np.arange(nnz)
-    amap = torch.as_tensor(dense_pos.reshape(m, n)[:, np.where(~fixed_np)[0]].astype(np.int32).copy(), device=dev)
+    # the product evaluator writes values-only Jacobian records (the structural constants skipped,
+    # CPL_EVAL_JAC_FOLDED): amap points into the folded record, -2 marks a skipped constant 1
+    folded = csr_J and isinstance(ev, KernelEvaluator)
+    if folded:
+        var_k, const_k, const_val = problem.jac_fold_info()
+        rec_pos = np.full(nnz, -1, dtype=np.int64)
+        rec_pos[var_k] = np.arange(var_k.size)
+        rec_pos[const_k[const_val == 1.0]] = -2
+        assert set(np.unique(const_val)) <= {0.0, 1.0}
+        dense_rec = np.where(dense_pos >= 0, rec_pos[np.maximum(dense_pos, 0)], -1)
+        nnz_rec = int(var_k.size)
+    else:
+        dense_rec, nnz_rec = dense_pos, nnz
+    amap = torch.as_tensor(dense_rec.reshape(m, n)[:, np.where(~fixed_np)[0]].astype(np.int32).copy(), device=dev)
     if use_hip:
         kkt_ws = torch.empty(B * int(_abi.lib.cpl_kkt_workspace_doubles(nw, m)), dtype=dt, device=dev)
 
@@ -245,8 +259,8 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     def evaluate(Xe):
         nonlocal n_eval
         n_eval += 1
-        o = ev(Xe, Mass)
-        if csr_J:  # the device path keeps the CSR values; jac_w builds A from them in one launch
+        o = ev(Xe, Mass, jac_folded=True) if folded else ev(Xe, Mass)
+        if csr_J:  # the device path keeps the Jacobian records; jac_w builds A from them in one launch
             return {"f": o["f"], "grad": o["grad"], "g": o["g"], "J": o["jac"].contiguous()}
         J = torch.zeros(B, m * n, dtype=dt, device=dev)
         J[:, flat_idx] = torch.nan_to_num(o["jac"], nan=0.0)  # a cone at F_t = 0 has a 0/0 Jacobian
@@ -265,7 +279,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     def jac_w(J, mask=None):
         if csr_J:  # mask: rows of inactive instances are left unwritten (never read for them)
             A_ = torch.empty(B, m, nw, dtype=dt, device=dev)
-            _abi.check(_abi.lib.cpl_ipm_dense_a(B, m, nw, nf, nnz, _ptr(amap), _ptr(row_slack), _ptr(J), _ptr(A_),
+            _abi.check(_abi.lib.cpl_ipm_dense_a(B, m, nw, nf, nnz_rec, _ptr(amap), _ptr(row_slack), _ptr(J), _ptr(A_),
                                                 None if mask is None else _ptr(mask), stream()))
             return A_
         return torch.cat([J[:, :, free], (-P).expand(B, m, nI)], dim=2)

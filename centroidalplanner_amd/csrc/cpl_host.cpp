@@ -234,6 +234,49 @@ int32_t cpl_structure(const cpl_problem_desc* d, int32_t* iRow, int32_t* jCol, i
   return CPL_OK;
 }
 
+int32_t cpl_jac_fold_info(const cpl_problem_desc* d, int32_t* nnz_folded, int32_t* var_k, int32_t* n_const,
+                          int32_t* const_k, double* const_val) {
+  int32_t st = validate_desc(d);
+  if (st) return st;
+  const int32_t N = d->n_contacts;
+  const bool env = has_env(d->env_kind);
+  const int32_t lvl = fold_level(d->env_kind);
+  // the walk of cpl_structure, each CSR position classified as variable or constant
+  int32_t k = 0, nv = 0, nc = 0;
+  auto var = [&](int32_t count) {
+    for (int32_t e = 0; e < count; ++e) {
+      if (var_k) var_k[nv] = k;
+      ++nv;
+      ++k;
+    }
+  };
+  auto cst = [&](double v) {
+    if (const_k) const_k[nc] = k;
+    if (const_val) const_val[nc] = v;
+    ++nc;
+    ++k;
+  };
+  for (int32_t e = 0; e < 3 * N; ++e) cst(1.0);  // force balance: I3 per contact
+  var(3 * (2 + 4 * N));                            // torque rows
+  for (int32_t kk = 0; kk < N; ++kk) {
+    if (env) {
+      if (lvl == FOLD_GROUND) {  // Ground gradient (0, 0, 1) and zero normal Jacobian
+        cst(0.0); cst(0.0); cst(1.0);
+        for (int32_t r = 0; r < 3; ++r) { cst(0.0); cst(0.0); cst(0.0); cst(1.0); }
+      } else {
+        var(3);
+        for (int32_t r = 0; r < 3; ++r) { var(3); cst(1.0); }
+      }
+    }
+    var(12);  // friction cone
+  }
+  if (nv != folded_nnz(N, d->env_kind) || k != dims_of(N, d->env_kind).nnz)
+    return fail(CPL_ERR_RUNTIME, "cpl_jac_fold_info: layout mismatch");
+  if (nnz_folded) *nnz_folded = nv;
+  if (n_const) *n_const = nc;
+  return CPL_OK;
+}
+
 int32_t cpl_bounds(const cpl_problem_desc* d, double* x_l, double* x_u, double* g_l, double* g_u) {
   int32_t st = validate_desc(d);
   if (st) return st;

@@ -455,6 +455,8 @@ __global__ __launch_bounds__(256) void cpl_ipm_dense_a_kernel(int64_t total, int
     if (q >= 0) {
       v = jac[b * nnz + q];
       v = v == v ? v : 0.0;
+    } else if (q == -2) {  // a structural constant 1 the folded Jacobian layout skips
+      v = 1.0;
     }
   } else if (row_slack[r] == k - nf) {
     v = -1.0;

@@ -80,6 +80,11 @@ struct KParams {
   const double* ly;
   const uint8_t* lg_active;  // optional: instance b / y_repeat inactive -> its rows are skipped
   int32_t offC;              // doubles offset of the LDS copy of the CSC index (fused gradient)
+  // Jacobian output layout (cpl_eval_batch_ex): fold = FOLD_NONE (IFOPT CSR values), FOLD_COMMON /
+  // FOLD_GROUND (values only: the structurally constant entries skipped, cpl_layout.hpp); jbase /
+  // cstride = offset of the first contact block and length of one, in the (folded) record
+  int32_t fold, jbase, cstride;
+  int32_t soa;               // outputs entry-major ([m][B], [nnz][B], [n][B]) instead of instance-major
 };
 static_assert(sizeof(KParams) < 4096, "kernel parameters must fit the kernarg segment");
 
@@ -736,6 +741,22 @@ __device__ __forceinline__ void copy_in(double* __restrict__ dst, const double* 
   }
 }
 
+// Entry-major ("SoA") copy-out of a tile image [valid][rec] to dst[q * batch + r] (dst = the
+// output's base + the tile's first instance): lanes run along the instances, so each entry's run of
+// the tile is one contiguous segment (512 B for a 64-instance tile).
+template <int NTH, bool NT>
+__device__ __forceinline__ void copy_out_soa(double* __restrict__ dst, int64_t batch, const double* __restrict__ src,
+                                             int rec, int valid, int tid) {
+  const int count = rec * valid;
+  for (int e = tid; e < count; e += NTH) {
+    const int q = e / valid, r = e - q * valid;
+    const double v = src[r * rec + q];
+    double* d = dst + (int64_t)q * batch + r;
+    if (NT) __builtin_nontemporal_store(v, d);
+    else *d = v;
+  }
+}
+
 template <int WG, bool NT>
 __device__ __forceinline__ void copy_out(double* __restrict__ dst, const double* __restrict__ src, int count,
                                          int tid) {
@@ -770,7 +791,7 @@ __device__ __forceinline__ void contact_item(const KParams& K, const double* __r
   const double n0 = q[6], n1 = q[7], n2 = q[8];
   const bool wg = K.want_g, wj = K.want_j;
   double* gk = Gr + 6 + (K.has_env ? 6 : 2) * k;
-  double* jk = Jr + 6 + 15 * K.N + (K.has_env ? 27 : 12) * k;
+  double* jk = Jr + K.jbase + K.cstride * k;
   if (ENVK != CPL_ENV_NONE) {
     double gv[4], ej[3], nj[3][3];
     if (ENVK == CPL_ENV_GROUND || (ENVK == CPL_ENV_MIXED && kind == CPL_ENV_GROUND)) {
@@ -795,15 +816,20 @@ __device__ __forceinline__ void contact_item(const KParams& K, const double* __r
       }
     }
     if (wg) { gk[0] = gv[0]; gk[1] = gv[1]; gk[2] = gv[2]; gk[3] = gv[3]; }
-    if (wj) {
+    if (wj && K.fold == FOLD_NONE) {
       jk[0] = ej[0]; jk[1] = ej[1]; jk[2] = ej[2];
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         jk[3 + 4 * r] = nj[r][0]; jk[4 + 4 * r] = nj[r][1]; jk[5 + 4 * r] = nj[r][2]; jk[6 + 4 * r] = 1.0;
       }
-    }
+      jk += 15;
+    } else if (wj && K.fold == FOLD_COMMON) {  // values only: the normal rows' n_r entry (1) skipped
+      jk[0] = ej[0]; jk[1] = ej[1]; jk[2] = ej[2];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) { jk[3 + 3 * r] = nj[r][0]; jk[4 + 3 * r] = nj[r][1]; jk[5 + 3 * r] = nj[r][2]; }
+      jk += 12;
+    }  // FOLD_GROUND: the Ground gradient (0,0,1), the zero normal Jacobian and the ones are all constant
     gk += 4;
-    jk += 15;
   }
   // FrictionCone, src/Constraints/FrictionCone.cpp:30-103
   const double mu = K.mu;
@@ -855,7 +881,7 @@ __device__ __forceinline__ void statics_values_item(const KParams& K, const doub
     v0 += m_i * K.gravity[0]; v1 += m_i * K.gravity[1]; v2 += m_i * K.gravity[2];
     Gr[0] = v0; Gr[1] = v1; Gr[2] = v2; Gr[3] = v3; Gr[4] = v4; Gr[5] = v5;
   }
-  if (K.want_j)
+  if (K.want_j && K.fold == FOLD_NONE)  // folded layouts skip the constant I3 blocks
     for (int e = 0; e < 3 * N; ++e) Jr[e] = 1.0;
 }
 
@@ -878,7 +904,7 @@ __device__ __forceinline__ void statics_row_item(const KParams& K, const double*
     a1 -= -s1 * F[e1];
     a2 -= -s2 * F[e2];
   }
-  double* row = Jr + 3 * N + q * (2 + 4 * N);
+  double* row = Jr + (K.fold == FOLD_NONE ? 3 * N : 0) + q * (2 + 4 * N);
   row[0] = a1;
   row[1] = a2;
   for (int i = 0; i < N; ++i) {
@@ -1005,7 +1031,8 @@ __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __re
   const int i = s_ct.map_order[k];
   const double* q = xr + 3 + 9 * i;
   double* gk = Gr + 6 + 6 * k;
-  double* jk = Jr + 6 + 15 * K.N + 27 * k;
+  double* jk = Jr + K.jbase + K.cstride * k;
+  const bool fold = K.fold != FOLD_NONE;  // Superquadric / mixed fold: FOLD_COMMON
   if (a == 0) {
     // EnvironmentConstraint / EnvironmentNormal values and the env Jacobian row
     // (src/Superquadric.cpp:40-69; src/Constraints/EnvironmentConstraint.cpp:16-61; EnvironmentNormal.cpp:16-33)
@@ -1026,7 +1053,7 @@ __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __re
     }
     if (K.want_j) { jk[0] = ej0; jk[1] = ej1; jk[2] = ej2; }
   } else if (a == 1) {
-    cone_rows(K, i, q, gk + 4, jk + 15);
+    cone_rows(K, i, q, gk + 4, jk + (fold ? 12 : 15));
   }
   if (!K.want_j) return;
   // EnvironmentNormal p block row a = GetNormalJacobian row a (src/Superquadric.cpp:72-209), n_a = 1
@@ -1082,8 +1109,9 @@ __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __re
                      (K.Psq[bb] * Lbb[L_P2PM2]) * K.Rm2[bb];
     out[bb] = lead / pow_three_halves(S) * (-1.0 / 2.0);
   }
-  double* row = jk + 3 + 4 * a;
-  row[0] = out[0]; row[1] = out[1]; row[2] = out[2]; row[3] = 1.0;
+  double* row = jk + 3 + (fold ? 3 : 4) * a;
+  row[0] = out[0]; row[1] = out[1]; row[2] = out[2];
+  if (!fold) row[3] = 1.0;
 }
 
 template <int ENVK, int WG, bool NT>
@@ -1183,7 +1211,11 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
     }
   }
   __syncthreads();
-  if (K.ablate != 2) {
+  if (K.ablate != 2 && K.soa) {
+    if (K.want_g) copy_out_soa<WG, NT>(g_out + b0, batch, Gt, m, valid, tid);
+    if (K.want_j) copy_out_soa<WG, NT>(jac_out + b0, batch, Jt, nnz, valid, tid);
+    if (K.want_grad) copy_out_soa<WG, NT>(grad_out + b0, batch, Dt, n, valid, tid);
+  } else if (K.ablate != 2) {
     if (K.want_g) copy_out<WG, NT>(g_out + b0 * m, Gt, valid * m, tid);
     if (K.want_j) copy_out<WG, NT>(jac_out + b0 * nnz, Jt, valid * nnz, tid);
     if (K.want_grad) copy_out<WG, NT>(grad_out + b0 * n, Dt, valid * n, tid);
@@ -1433,6 +1465,10 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
         }
         grad_out[(b0 + r) * n + j] = s;
       }
+    } else if (K.ablate != 2 && K.soa) {
+      if (K.want_g) copy_out_soa<CT, NT>(g_out + b0, batch, Gt, m, valid, tid);
+      if (K.want_j) copy_out_soa<CT, NT>(jac_out + b0, batch, Jt, nnz, valid, tid);
+      if (K.want_grad) copy_out_soa<CT, NT>(grad_out + b0, batch, Dt, n, valid, tid);
     } else if (K.ablate != 2) {
       if (K.want_g) copy_out_ct<CT, NT>(g_out + b0 * m, Gt, valid * m, tid);
       if (K.want_j) copy_out_ct<CT, NT>(jac_out + b0 * nnz, Jt, valid * nnz, tid);
@@ -1719,6 +1755,10 @@ static void fill_params(const cpl_problem_desc* d, KParams& K, const double* d_x
   }
   K.W_com = d->W_com;
   for (int j = 0; j < 3; ++j) K.com_ref[j] = d->com_ref[j];
+  K.fold = FOLD_NONE;
+  K.jbase = D.statics_nnz;
+  K.cstride = D.contact_nnz;
+  K.soa = 0;
 }
 
 static size_t eval_lds_bytes(int n) { return sizeof(double) * (size_t)(TILE * n + 2 * TILE * SROW); }
@@ -1873,9 +1913,10 @@ struct LGradArgs {
 static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
                            const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
                            double* d_norms, hipStream_t stream, bool finish = true,
-                           const LGradArgs* lg = nullptr) {
+                           const LGradArgs* lg = nullptr, int32_t flags = 0) {
   int32_t st = validate_desc(d);
   if (st) return st;
+  if (flags & ~(CPL_EVAL_JAC_FOLDED | CPL_EVAL_SOA)) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown eval flags");
   if (batch < 0) return fail(CPL_ERR_INVALID_ARGUMENT, "negative batch");
   if (batch == 0) {  // (an empty g may arrive as a null pointer)
     if (d_norms) {
@@ -1892,6 +1933,13 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
   if (!d_g && !d_jac && !d_f && !d_grad) return CPL_OK;
   KParams K;
   fill_params(d, K, d_x);
+  if (flags & CPL_EVAL_JAC_FOLDED) {  // values-only Jacobian records (cpl_layout.hpp)
+    K.fold = fold_level(d->env_kind);
+    K.nnz = folded_nnz(K.N, d->env_kind);
+    K.jbase = 6 + 12 * K.N;
+    K.cstride = folded_contact_nnz(d->env_kind);
+  }
+  K.soa = (flags & CPL_EVAL_SOA) ? 1 : 0;
   K.want_norms = d_norms != nullptr;
   K.want_lgrad = 0;
   K.y_repeat = 1;
@@ -1939,7 +1987,7 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
       if (e != hipSuccess) return hip_fail(e, "cpl_eval_pipe_kernel launch");
       if (finish) launch_residual_final((int)grid, ws + NORM_HDR, d_norms, stream);
     }
-  } else if (use_rowstage()) {
+  } else if (use_rowstage() && flags == 0) {  // (the row-staged kernel writes IFOPT records only)
     const size_t lds = eval_lds_bytes(K.n);
     if (lds > 160 * 1024) return fail(CPL_ERR_UNSUPPORTED, "problem too large for one LDS tile");
     const unsigned grid = (unsigned)((batch + TILE - 1) / TILE);
@@ -2035,6 +2083,13 @@ int32_t cpl_lagrangian_hessian(const cpl_problem_desc* d, int64_t batch, const d
   return CPL_OK;
 }
 
+int32_t cpl_eval_batch_ex(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
+                          const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
+                          double* d_norms, int32_t flags, void* stream) {
+  return launch_eval(d, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f, d_grad, d_norms, (hipStream_t)stream, true,
+                     nullptr, flags);
+}
+
 int32_t cpl_eval_batch_norms(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
                              const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
                              double* d_norms, void* stream) {
@@ -2093,6 +2148,13 @@ int32_t cpl_residual_norms(const cpl_problem_desc* d, int64_t batch, const doubl
 int32_t cpl_time_eval_batch(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
                             const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
                             double* d_norms, void* stream, int32_t reps, double* ms_per_launch) {
+  return cpl_time_eval_batch_ex(d, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f, d_grad, d_norms, 0, stream, reps,
+                                ms_per_launch);
+}
+
+int32_t cpl_time_eval_batch_ex(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
+                               const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
+                               double* d_norms, int32_t flags, void* stream, int32_t reps, double* ms_per_launch) {
   if (!ms_per_launch || reps < 1) return fail(CPL_ERR_INVALID_ARGUMENT, "bad timing arguments");
   hipStream_t s = (hipStream_t)stream;
   hipEvent_t e0, e1;
@@ -2105,7 +2167,8 @@ int32_t cpl_time_eval_batch(const cpl_problem_desc* d, int64_t batch, const doub
   // back-to-back eval kernels (with the fused per-workgroup norms when d_norms != NULL; the
   // one-workgroup finish, a separate kernel, is left out of the timed launches)
   for (int32_t r = 0; r < reps && st == CPL_OK; ++r)
-    st = launch_eval(d, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f, d_grad, d_norms, s, /*finish=*/false);
+    st = launch_eval(d, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f, d_grad, d_norms, s, /*finish=*/false, nullptr,
+                     flags);
   (void)hipEventRecord(e1, s);
   e = hipEventSynchronize(e1);
   if (st == CPL_OK && e != hipSuccess) st = hip_fail(e, "hipEventSynchronize");
@@ -2118,7 +2181,8 @@ int32_t cpl_time_eval_batch(const cpl_problem_desc* d, int64_t batch, const doub
   (void)hipEventDestroy(e1);
   if (st == CPL_OK) *ms_per_launch = (double)ms / reps;
   // leave d_norms valid for the caller
-  if (st == CPL_OK && d_norms) st = launch_eval(d, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f, d_grad, d_norms, s);
+  if (st == CPL_OK && d_norms)
+    st = launch_eval(d, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f, d_grad, d_norms, s, true, nullptr, flags);
   return st;
 }
 

@@ -37,6 +37,24 @@ inline Dims dims_of(int32_t N, int32_t env_kind) {
   return d;
 }
 
+// Values-only ("folded") Jacobian layout (cpl_eval_batch_ex, CPL_EVAL_JAC_FOLDED): the entries that
+// are constant for every x are skipped in the output record, row-major order otherwise kept.
+//   FOLD_COMMON (every environment kind but Ground): the I3 blocks of the force-balance rows
+//     (src/Constraints/CentroidalStatics.cpp:93-95) and the n_r entry (1) of each normal row
+//     (src/Constraints/EnvironmentNormal.cpp:63-70);
+//   FOLD_GROUND: also the Ground gradient (0, 0, 1) (src/Ground.cpp:30-35) and the zero normal
+//     Jacobian (src/Ground.cpp:46-50) — per contact only the 12 friction-cone entries remain.
+enum { FOLD_NONE = 0, FOLD_COMMON = 1, FOLD_GROUND = 2 };
+
+inline int32_t fold_level(int32_t env_kind) { return env_kind == CPL_ENV_GROUND ? FOLD_GROUND : FOLD_COMMON; }
+
+// per-contact entries of a folded record: cone 12, + env 3 + normal 9 (p blocks) with a surface
+inline int32_t folded_contact_nnz(int32_t env_kind) {
+  if (env_kind == CPL_ENV_GROUND || !has_env(env_kind)) return 12;
+  return 24;
+}
+inline int32_t folded_nnz(int32_t N, int32_t env_kind) { return 6 + 12 * N + folded_contact_nnz(env_kind) * N; }
+
 // Column of component c of a variable set.
 inline int32_t col_com(int32_t c) { return c; }
 inline int32_t col_F(int32_t i, int32_t c) { return 3 + 9 * i + c; }

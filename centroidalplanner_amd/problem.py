@@ -302,6 +302,18 @@ class CplProblem:
         check(lib.cpl_structure(ctypes.byref(self.desc()), None, None, iptr(rp)))
         return rp
 
+    def jac_fold_info(self):
+        """The values-only Jacobian layout (cpl_jac_fold_info): (var_k, const_k, const_val) — the CSR
+        positions of the folded values, and the positions / values of the skipped constants."""
+        nf, nc = ctypes.c_int32(), ctypes.c_int32()
+        check(lib.cpl_jac_fold_info(ctypes.byref(self.desc()), ctypes.byref(nf), None, ctypes.byref(nc), None, None))
+        var_k = np.zeros(nf.value, dtype=np.int32)
+        const_k = np.zeros(nc.value, dtype=np.int32)
+        const_val = np.zeros(nc.value)
+        check(lib.cpl_jac_fold_info(ctypes.byref(self.desc()), ctypes.byref(nf), iptr(var_k), ctypes.byref(nc),
+                                    iptr(const_k), dptr(const_val)))
+        return var_k, const_k, const_val
+
     def get_bounds_info(self):
         n, m, _ = self._dims()
         xl, xu, gl, gu = np.zeros(n), np.zeros(n), np.zeros(m), np.zeros(m)
@@ -348,7 +360,7 @@ class CplProblem:
 
     # ---- the batched hot path ---------------------------------------------------------------
     def eval_batch(self, x, mass=None, env_tag=None, outputs: Iterable[str] = ("g", "jac"), out=None,
-                   stream=None):
+                   stream=None, jac_folded: bool = False, soa: bool = False):
         """Evaluate B instances on the GPU in one launch.
 
         x: torch.float64 CUDA tensor [B, n] (contiguous).  mass: [B] or None.  env_tag: uint8 [B]
@@ -357,6 +369,8 @@ class CplProblem:
         into the same launch (cpl_eval_batch_norms).  out: optional
         dict of preallocated output tensors.  Returns the dict of output tensors; asynchronous on
         ``stream`` (default: torch's current stream).
+        jac_folded: values-only Jacobian records (structural constants skipped, see jac_fold_info);
+        soa: entry-major outputs g [m, B], jac [nnz, B], grad [n, B] (cpl_eval_batch_ex).
         """
         import torch
 
@@ -369,7 +383,14 @@ class CplProblem:
         if x.dtype != torch.float64 or not x.is_cuda or x.dim() != 2 or x.shape[1] != n or not x.is_contiguous():
             raise InvalidArgument(_abi.ERR_INVALID_ARGUMENT, f"x must be a contiguous float64 CUDA tensor [B, {n}]")
         B = x.shape[0]
+        flags = (_abi.EVAL_JAC_FOLDED if jac_folded else 0) | (_abi.EVAL_SOA if soa else 0)
+        if jac_folded:
+            nf = ctypes.c_int32()
+            check(lib.cpl_jac_fold_info(ctypes.byref(self.desc()), ctypes.byref(nf), None, None, None, None))
+            nnz = nf.value
         shapes = {"g": (B, m), "jac": (B, nnz), "f": (B,), "grad": (B, n)}
+        if soa:
+            shapes = {k: (v[1], v[0]) if len(v) == 2 else v for k, v in shapes.items()}
         res = {}
         for k in outputs:
             if k not in shapes:
@@ -400,9 +421,10 @@ class CplProblem:
             elif tuple(t.shape) != (2,) or t.dtype != torch.float64 or t.device != x.device or not t.is_contiguous():
                 raise InvalidArgument(_abi.ERR_INVALID_ARGUMENT, f"output 'norms' must be a contiguous float64 (2,) tensor on {x.device}")
             res["norms"] = t
-            check(lib.cpl_eval_batch_norms(ctypes.byref(self.desc()), B, p(x), p(mass), p(env_tag), p(res.get("g")),
-                                           p(res.get("jac")), p(res.get("f")), p(res.get("grad")), p(t),
-                                           ctypes.c_void_p(s.cuda_stream)))
+        if flags or want_norms:
+            check(lib.cpl_eval_batch_ex(ctypes.byref(self.desc()), B, p(x), p(mass), p(env_tag), p(res.get("g")),
+                                        p(res.get("jac")), p(res.get("f")), p(res.get("grad")), p(res.get("norms")),
+                                        flags, ctypes.c_void_p(s.cuda_stream)))
             return res
         check(lib.cpl_eval_batch(ctypes.byref(self.desc()), B, p(x), p(mass), p(env_tag), p(res.get("g")),
                                  p(res.get("jac")), p(res.get("f")), p(res.get("grad")),

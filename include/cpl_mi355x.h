@@ -175,6 +175,39 @@ int32_t cpl_eval_batch_norms(const cpl_problem_desc* d, int64_t batch, const dou
                              double* d_jac, double* d_f, double* d_grad, double* d_norms,
                              void* stream);
 
+/*
+ * Output layout flags of cpl_eval_batch_ex (bitwise OR; 0 = exactly cpl_eval_batch's layout):
+ *   CPL_EVAL_JAC_FOLDED  values-only Jacobian records: the structurally constant entries (the same
+ *     for every x) are skipped and the remaining ones keep IFOPT's RowMajor-CSR order.  Record
+ *     length nnz_folded and the positions / values of the skipped entries: cpl_jac_fold_info().
+ *     Ground (N contacts): 6 + 24N values (18 of every 42 per-contact entries are constants: the
+ *     force-balance I3, src/Constraints/CentroidalStatics.cpp:93-95; the gradient (0,0,1),
+ *     src/Ground.cpp:30-35; the zero normal Jacobian, src/Ground.cpp:46-50; the normal rows' n_r
+ *     ones, src/Constraints/EnvironmentNormal.cpp:63-70).  Superquadric / mixed: 6 + 36N (the I3
+ *     blocks and the ones).  No environment: 6 + 24N (the I3 blocks).
+ *   CPL_EVAL_SOA  entry-major outputs: g [m][batch], jac [nnz(_folded)][batch], grad [n][batch]
+ *     (f stays [batch]); the inputs stay instance-major.
+ * Replaces nothing in the reference (IFOPT hands IPOPT the full CSR values, src/CentroidalPlanner.cpp:29
+ * [IFOPT-ext]); for GPU-side consumers of the batch (the solve loop, a batched factorisation).
+ */
+#define CPL_EVAL_JAC_FOLDED 1
+#define CPL_EVAL_SOA 2
+
+int32_t cpl_eval_batch_ex(const cpl_problem_desc* d, int64_t batch, const double* d_x,
+                          const double* d_mass, const uint8_t* d_env_tag, double* d_g,
+                          double* d_jac, double* d_f, double* d_grad, double* d_norms,
+                          int32_t flags, void* stream);
+
+/*
+ * The folded Jacobian layout of `d` (host only): *nnz_folded values per record; var_k[j] = the
+ * CSR position (0..nnz-1, cpl_structure order) of folded value j; const_k[c] / const_val[c] = the
+ * CSR position and value of skipped constant c, *n_const of them (nnz = nnz_folded + n_const).
+ * Any pointer may be NULL.  Scattering the folded values to var_k and const_val to const_k gives
+ * cpl_eval_batch's CSR values bit for bit.
+ */
+int32_t cpl_jac_fold_info(const cpl_problem_desc* d, int32_t* nnz_folded, int32_t* var_k,
+                          int32_t* n_const, int32_t* const_k, double* const_val);
+
 /* Kernel timing helper for the bench: launches the eval kernel of cpl_eval_batch (of
  * cpl_eval_batch_norms, i.e. with the fused per-workgroup norms, when d_norms != NULL) `reps` times
  * back to back on `stream` between two HIP events recorded on that same stream and returns the mean
@@ -184,6 +217,11 @@ int32_t cpl_time_eval_batch(const cpl_problem_desc* d, int64_t batch, const doub
                             const double* d_mass, const uint8_t* d_env_tag, double* d_g,
                             double* d_jac, double* d_f, double* d_grad, double* d_norms,
                             void* stream, int32_t reps, double* ms_per_launch);
+/* the same for cpl_eval_batch_ex's layouts */
+int32_t cpl_time_eval_batch_ex(const cpl_problem_desc* d, int64_t batch, const double* d_x,
+                               const double* d_mass, const uint8_t* d_env_tag, double* d_g,
+                               double* d_jac, double* d_f, double* d_grad, double* d_norms,
+                               int32_t flags, void* stream, int32_t reps, double* ms_per_launch);
 
 /* Tuning knobs (process-wide, for A/B measurements): kernel_variant 0 = auto (default: the
  * pipelined kernel for none/Ground, the tile-stationary kernel for Superquadric/mixed),
@@ -348,8 +386,10 @@ int32_t cpl_ipm_accept(int64_t batch, int32_t nw, int32_t m, int32_t nfilt, cons
                        double* d_filt_t, double* d_filt_p, int64_t* d_fcount, void* stream);
 int32_t cpl_ipm_masked_rows(int64_t batch, int64_t row_len, const uint8_t* d_mask, const double* d_src, double* d_dst,
                             void* stream);
-/* cpl_ipm_dense_a: A = [J_free | -P] dense [batch, m, nw] from the CSR Jacobian values (amap: CSR
- * position of (row, free column) or -1; row_slack: slack of each inequality row or -1; NaN -> 0). */
+/* cpl_ipm_dense_a: A = [J_free | -P] dense [batch, m, nw] from the Jacobian records of nnz values
+ * (IFOPT CSR, or the folded layout of CPL_EVAL_JAC_FOLDED): amap[row, free column] = position in the
+ * record, -1 for a structural zero (or a skipped constant 0), -2 for a skipped constant 1;
+ * row_slack: slack of each inequality row or -1; NaN -> 0. */
 int32_t cpl_ipm_dense_a(int64_t batch, int32_t m, int32_t nw, int32_t nf, int32_t nnz, const int32_t* d_amap,
                         const int32_t* d_row_slack, const double* d_jac, double* d_A, const uint8_t* d_active,
                         void* stream);

@@ -26,6 +26,8 @@ ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--variants", default="0:0:256:1,3:32:256:1,2:48:256:1")
 ap.add_argument("--outputs", default="g,jac")
 ap.add_argument("--norms", action="store_true", help="fused residual norms (cpl_eval_batch_norms)")
+ap.add_argument("--folded", action="store_true", help="values-only Jacobian records (CPL_EVAL_JAC_FOLDED)")
+ap.add_argument("--soa", action="store_true", help="entry-major outputs (CPL_EVAL_SOA)")
 args = ap.parse_args()
 
 cfg = CONFIGS[args.config]
@@ -35,7 +37,8 @@ dev = torch.device("cuda:0")
 xt, mt = torch.tensor(x, device=dev), torch.tensor(mass, device=dev)
 tt = None if tag is None else torch.tensor(tag, device=dev)
 outs = tuple(args.outputs.split(","))
-out = prob.eval_batch(xt, mt, tt, outputs=outs)
+out = prob.eval_batch(xt, mt, tt, outputs=outs, jac_folded=args.folded, soa=args.soa)
+flags = (_abi.EVAL_JAC_FOLDED if args.folded else 0) | (_abi.EVAL_SOA if args.soa else 0)
 stream = torch.cuda.current_stream()
 norms = torch.zeros(2, dtype=torch.float64, device=xt.device) if args.norms else None
 variants = [tuple(int(v) for v in s.split(":")) for s in args.variants.split(",")]
@@ -50,13 +53,16 @@ for _ in range(args.rounds):
     for v in variants:
         _abi.check(_abi.lib.cpl_set_tuning(v[0], v[1], v[2], v[3], v[4] if len(v) > 4 else 0))
         ms = ctypes.c_double()
-        _abi.check(_abi.lib.cpl_time_eval_batch(ctypes.byref(prob.desc()), B, p(xt), p(mt), p(tt), p(out.get("g")),
-                                                p(out.get("jac")), p(out.get("f")), p(out.get("grad")), p(norms),
-                                                ctypes.c_void_p(stream.cuda_stream), args.reps, ctypes.byref(ms)))
+        _abi.check(_abi.lib.cpl_time_eval_batch_ex(ctypes.byref(prob.desc()), B, p(xt), p(mt), p(tt), p(out.get("g")),
+                                                   p(out.get("jac")), p(out.get("f")), p(out.get("grad")), p(norms),
+                                                   flags, ctypes.c_void_p(stream.cuda_stream), args.reps,
+                                                   ctypes.byref(ms)))
         times[v].append(ms.value)
 bpi, m = algorithmic_bytes(cfg.n_contacts, cfg.env, outs)
+if args.folded and "jac" in outs:
+    bpi -= 8 * (prob.nnz - out["jac"].shape[1 if not args.soa else 0])
 for v, ts in times.items():
     med = statistics.median(ts)
-    print(json.dumps({"config": args.config, "batch": B, "variant": v[0], "lds_kb": v[1], "wg": v[2], "nt": v[3], "ablate": v[4] if len(v) > 4 else 0, "median_ms": med,
+    print(json.dumps({"config": args.config, "batch": B, "folded": args.folded, "soa": args.soa, "variant": v[0], "lds_kb": v[1], "wg": v[2], "nt": v[3], "ablate": v[4] if len(v) > 4 else 0, "median_ms": med,
                       "min_ms": min(ts), "GBps": bpi * B / (med * 1e-3) / 1e9,
                       "rows_per_s": B * m / (med * 1e-3)}), flush=True)
