@@ -81,6 +81,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--max-ls", type=int, default=4, help="solve5: line-search trials per iteration")
     ap.add_argument("--max-soc", type=int, default=1, help="solve5: second-order corrections per iteration")
+    ap.add_argument("--hessian", default="exact", choices=["exact", "limited-memory"],
+                    help="solve5: exact Lagrangian Hessian (analytic kernel) or IFOPT's limited-memory default")
+    ap.add_argument("--cpu-sample", type=int, default=64, help="solve5: instances in the CPU baseline's sample")
     ap.add_argument("--pmc-child", default="", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -104,38 +107,82 @@ def pmc_child(args):
     torch.cuda.synchronize()
 
 
-def collect_pmc(args, timeout=240):
+def _pmc_pass(args, counters, timeout=240):
+    """One rocprofv3 --pmc pass over the pmc child; returns {counter: mean per eval dispatch}."""
+    import csv
+
     rocprof = "/opt/rocm/bin/rocprofv3"
-    if not os.path.exists(rocprof):
+    d = tempfile.mkdtemp(prefix="cpl_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    cmd = [rocprof, "--pmc", *counters, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
+           sys.executable, os.path.join(ROOT, "bench.py"), "--pmc-child", "1", "--config", args.config]
+    if args.batch:
+        cmd += ["--batch", str(args.batch)]
+    subprocess.run(cmd, check=True, timeout=timeout, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, cwd=ROOT)
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise RuntimeError(f"no counter csv for {counters}")
+    per = {}
+    with open(files[0]) as fh:
+        for row in csv.DictReader(fh):
+            if KERNEL_NAME in row.get("Kernel_Name", ""):
+                per.setdefault(row["Counter_Name"], {}).setdefault(row["Dispatch_Id"], 0.0)
+                per[row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
+    if not per:
+        raise RuntimeError(f"no {counters} rows for {KERNEL_NAME}")
+    return {k: sum(v.values()) / len(v) for k, v in per.items()}
+
+
+def collect_pmc(args, timeout=240):
+    """HBM traffic of the eval kernel: FETCH_SIZE and WRITE_SIZE in separate passes."""
+    if not os.path.exists("/opt/rocm/bin/rocprofv3"):
         return None, "rocprofv3 not found"
     vals = {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-        d = tempfile.mkdtemp(prefix="cpl_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
-        cmd = [rocprof, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
-               sys.executable, os.path.join(ROOT, "bench.py"), "--pmc-child", "1", "--config", args.config]
-        if args.batch:
-            cmd += ["--batch", str(args.batch)]
         try:
-            subprocess.run(cmd, check=True, timeout=timeout, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
-                           cwd=ROOT)
+            vals.update(_pmc_pass(args, [counter], timeout))  # KB per dispatch
         except Exception as e:  # noqa: BLE001
             return None, f"rocprofv3 {counter} pass failed: {e}"
-        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
-        if not files:
-            return None, f"no counter csv for {counter}"
-        import csv
-
-        per = []
-        with open(files[0]) as fh:
-            for row in csv.DictReader(fh):
-                if KERNEL_NAME in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
-                    per.append(float(row["Counter_Value"]))
-        if not per:
-            return None, f"no {counter} rows for {KERNEL_NAME}"
-        vals[counter] = sum(per) / len(per)  # KB per dispatch
     # gfx950: FETCH_SIZE reads 1/2 of a wide coalesced stream's bytes (MI355X_MICROARCH.md §HBM)
     traffic = (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
     return traffic, vals
+
+
+# FP64 VALU of MI355X: 78.6 TFLOP/s = 256 CUs x 4 SIMDs x 16 FMA lanes x 2 x 2.4 GHz, i.e. one wave64
+# FP64 instruction per SIMD per 4 cycles; f32 / integer VALU one per 2 cycles (MI355X_MICROARCH.md)
+FP64_PEAK_TFLOPS = 78.6
+CLK_HZ = 2.4e9
+SIMDS = 256 * 4
+VALU_PASSES = (("SQ_INSTS_VALU", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                "SQ_INSTS_VALU_TRANS_F64", "SQ_INSTS_SALU"),
+               ("SQ_INSTS_VALU_FLOPS_FP64", "SQ_INSTS_VALU_FLOPS_FP64_TRANS", "SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES",
+                "SQ_WAIT_ANY"))
+
+
+def collect_valu_counters(args, timeout=240):
+    c = {}
+    for counters in VALU_PASSES:
+        c.update(_pmc_pass(args, counters, timeout))
+    return c
+
+
+def valu_roofline(c, kernel_ms):
+    """The VALU roofline of a transcendental-heavy eval kernel (Superquadric / mixed) from PMC passes:
+    issue_frac = the kernel's VALU issue cycles at full rate (4 cycles per wave64 FP64 instruction,
+    2 otherwise, over 1024 SIMDs at 2.4 GHz) / its duration; fp64 TFLOP/s = 64 lanes x
+    SQ_INSTS_VALU_FLOPS_FP64(+_TRANS) / duration against the 78.6 TFLOP/s FP64 vector peak.
+    c: counters per eval dispatch (collect_valu_counters, run before this process touches the GPU)."""
+    t = kernel_ms * 1e-3
+    f64 = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                                       "SQ_INSTS_VALU_TRANS_F64"))
+    issue_s = (4.0 * f64 + 2.0 * (c["SQ_INSTS_VALU"] - f64)) / (SIMDS * CLK_HZ)
+    tflops = 64.0 * (c.get("SQ_INSTS_VALU_FLOPS_FP64", 0.0) + c.get("SQ_INSTS_VALU_FLOPS_FP64_TRANS", 0.0)) / t / 1e12
+    return {
+        "bound": "valu", "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+        "frac": tflops / FP64_PEAK_TFLOPS, "issue_frac": issue_s / t, "issue_bound_ms": issue_s * 1e3,
+        "wait_frac": c.get("SQ_WAIT_ANY", 0.0) / max(c.get("SQ_WAVE_CYCLES", 1.0), 1.0),
+        "valu_active_frac": c.get("SQ_ACTIVE_INST_VALU", 0.0) / max(c.get("SQ_WAVE_CYCLES", 1.0), 1.0),
+        "counters_per_dispatch": c,
+    }
 
 
 # ------------------------------------------------------------------------------------------
@@ -258,7 +305,8 @@ def solve_bench(args):
     X0t, mt = torch.tensor(X0, device=dev), torch.tensor(mass, device=dev)
     steps = max(1, min(args.steps, 5))
     warm = 1 if args.warmup > 0 else 0
-    opts = dict(max_iter=300, max_ls=args.max_ls, max_soc=args.max_soc)
+    opts = dict(max_iter=300 if args.hessian == "exact" else 1000, max_ls=args.max_ls, max_soc=args.max_soc,
+                hessian=args.hessian)
     for _ in range(warm):
         batch_ipm_solve(prob, X0t, mt, **opts)
     torch.cuda.synchronize()
@@ -286,14 +334,21 @@ def solve_bench(args):
             sys.path.insert(0, os.path.join(ROOT, "tests"))
             from test_batch_solve import OracleBatchEvaluator
 
-            Bc = 64
+            info = host_cpu_info()
+            threads = info["threads"]
+            torch.set_num_threads(threads)
+            Bc = min(args.cpu_sample, B)
             tc = time.perf_counter()
             rc = batch_ipm_solve(prob, torch.tensor(X0[:Bc]), torch.tensor(mass[:Bc]),
-                                 evaluator=OracleBatchEvaluator(prob), **opts)
+                                 evaluator=OracleBatchEvaluator(prob, nthreads=threads), **opts)
             tc = time.perf_counter() - tc
-            cpu = {"value": Bc / tc, "unit": "solves/s", "cores": 4, "kind": "port",
-                   "sample": f"{Bc} instances, the same batched solver over the oracle's callbacks on CPU torch "
-                             f"({rc.iterations_run} iterations, {tc:.1f} s)"}
+            okc = int((rc.status <= 1).sum().item())
+            cpu = {"value": Bc / tc, "unit": "solves/s", "cores": threads, "kind": "port",
+                   "sample": f"the first {Bc} of the {B} instances: the same batched solver (hessian={args.hessian}; "
+                             f"exact = the oracle's restatement of the analytic Hessian kernel) over the oracle's "
+                             f"callbacks on CPU torch, {threads} threads ({rc.iterations_run} iterations, {okc}/{Bc} "
+                             f"solved, {tc:.1f} s)",
+                   **{k: info[k] for k in ("cpu_model", "affinity", "omp_num_threads")}}
         except Exception as e:  # noqa: BLE001
             cpu = {"error": str(e)}
     if rank == 0:
@@ -303,7 +358,9 @@ def solve_bench(args):
             "ms_per_step": dt / steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f64", "data": "synthetic (TestBasic ground scenario, per-instance mass U[80,150])",
             "config": {"workload": SOLVE_CONFIG.name, "contacts": 4, "environment": "ground", "batch_per_gpu": B,
-                       "parallelism": f"instance-sharded x{world}", "hessian": "exact (analytic Lagrangian Hessian kernel)",
+                       "parallelism": f"instance-sharded x{world}",
+                       "hessian": ("exact (analytic Lagrangian Hessian kernel)" if args.hessian == "exact"
+                                   else "limited-memory (damped BFGS, IFOPT's IpoptSolver default)"),
                        "max_ls": args.max_ls, "max_soc": args.max_soc},
             "solved": ok, "iterations_max": int(its.max().item()), "iterations_mean": float(its.mean().item()),
             "lockstep_iterations": r.iterations_run, "eval_launches_per_solve": r.evaluations,
@@ -336,9 +393,14 @@ def main():
 
         batch = shard(cfg.batch, rank, world)[1]  # config 4 is quoted as 1,048,576 over the node
 
-    traffic, pmc_info = None, None
+    traffic, pmc_info, valu_counters = None, None, None
     if world == 1 and not args.no_pmc:
         traffic, pmc_info = collect_pmc(args)
+        if cfg.env in ("superquadric", "mixed"):  # VALU-bound kernels: the VALU roofline too
+            try:
+                valu_counters = collect_valu_counters(args)
+            except Exception as e:  # noqa: BLE001
+                valu_counters = f"VALU PMC passes failed: {e}"
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -483,6 +545,12 @@ def main():
     value = rows_total / dt
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
 
+    valu = None
+    if isinstance(valu_counters, dict):
+        valu = valu_roofline(valu_counters, kernel_ms)
+    elif valu_counters:
+        valu = {"error": valu_counters}
+
     check = None
     if rank == 0 and not args.no_check:
         try:
@@ -582,6 +650,8 @@ def main():
             "cpu_baseline": cpu,
         }
         res["check"] = check
+        if valu:
+            res["roofline_valu"] = valu
         if folded:
             res["jac_folded"] = folded
         if side:

@@ -579,7 +579,11 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
             _abi.check(_abi.lib.cpl_ipm_fd_hessian_raw(B, n, nf, _ptr(free), _ptr(gLfd), _ptr(hfd), _ptr(Hblk),
                                                        _ptr(S["active"]), stream()))
         else:
-            Hblk = fd_hessian(unpack(w), y)
+            # host path: the evaluator's own analytic Hessian when it has one (the oracle's restatement
+            # of cpl_lagrangian_hessian, so the CPU solve takes the device's exact-Hessian steps)
+            Hblk = ev.hessian(unpack(w), y, free) if (hessian == "exact" and hasattr(ev, "hessian")) else None
+            if Hblk is None:
+                Hblk = fd_hessian(unpack(w), y)
         if use_hip:  # Newton system: one fused launch (csrc/cpl_ipm.hip)
             M = torch.empty(B, nw, nw, dtype=dt, device=dev)
             r1, gphi, mr_diag = (torch.empty(B, nw, dtype=dt, device=dev) for _ in range(3))

@@ -112,3 +112,97 @@ def time_eval_batch(desc, x, mass=None, env_tag=None, outputs=("g", "jac"), nthr
 
 def max_threads():
     return lib.cplo_max_threads()
+
+
+def lagrangian_hessian(desc, X, Y, free_idx=None):
+    """Exact Hessian of f + y^T g over the variables `free_idx` (default: all), [B, nf, nf] — the
+    checker of cpl_lagrangian_hessian (csrc/cpl_kernels.hip hessian_entry) and the CPU solve loop's
+    Hessian: per entry the same operations in the same order, so the GPU kernel is bitwise equal.
+    Ground / no-environment problems (their environment and normal rows are linear).
+      cost:   W_com, W_F,i, W_p,i on the diagonal (src/MinimizeCentroidalVariables.cpp:124-148);
+      torque: d2/dp_a dF_b = E_ab, d2/dc_a dF_b = -E_ab, E_ab = sum_k y_{3+k} eps_kab
+              (src/Constraints/CentroidalStatics.cpp:37-61);
+      cones:  -F.n and |t| - mu F.n, t = F - (F.n) n (src/Constraints/FrictionCone.cpp:30-45); the |t|
+              terms count as 0 where |t| = 0 (the reference's Jacobian is 0/0 there).
+    X [B, n], Y [B, m] float64 host arrays."""
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    Y = np.ascontiguousarray(Y, dtype=np.float64)
+    N = int(desc.n_contacts)
+    n = 3 + 9 * N
+    B = X.shape[0]
+    crow = 6 if desc.env_kind in (1, 2, 3) else 2
+    pos = np.zeros(N, dtype=np.int64)
+    for k in range(N):
+        pos[desc.map_order[k]] = k
+    H = np.zeros((B, n, n))
+    # cost diagonal: h = 0.0 + W
+    for a in range(3):
+        H[:, a, a] = 0.0 + desc.W_com
+    for i in range(N):
+        for a in range(3):
+            H[:, 3 + 9 * i + a, 3 + 9 * i + a] = 0.0 + desc.W_F[i]
+            H[:, 6 + 9 * i + a, 6 + 9 * i + a] = 0.0 + desc.W_p[i]
+            H[:, 9 + 9 * i + a, 9 + 9 * i + a] = 0.0 + 0.0
+
+    def E(a, c):
+        if a == c:
+            return np.zeros(B)
+        k = 3 - a - c
+        sgn = 1.0 if (a + 1) % 3 == c else -1.0
+        return sgn * Y[:, 3 + k]
+
+    for i in range(N):
+        for a in range(3):
+            for b in range(3):
+                Fb, pa, ca = 3 + 9 * i + b, 6 + 9 * i + a, a
+                H[:, pa, Fb] = 0.0 + E(a, b)       # d2/dp_a dF_b
+                H[:, Fb, pa] = 0.0 + E(a, b)       # d2/dF_b dp_a (E(av, au) with v = p_a)
+                H[:, ca, Fb] = 0.0 - E(a, b)       # d2/dc_a dF_b
+                H[:, Fb, ca] = 0.0 - E(a, b)
+    mu = desc.mu
+    with np.errstate(all="ignore"):
+        for i in range(N):
+            q = X[:, 3 + 9 * i: 12 + 9 * i]
+            F = [q[:, 0], q[:, 1], q[:, 2]]
+            nn = [q[:, 6], q[:, 7], q[:, 8]]
+            r0 = 6 + crow * int(pos[i]) + (crow - 2)
+            y0, y1 = Y[:, r0], Y[:, r0 + 1]
+            sdot = (F[0] * nn[0] + F[1] * nn[1]) + F[2] * nn[2]
+            t = [F[j] - sdot * nn[j] for j in range(3)]
+            rr = np.sqrt((t[0] * t[0] + t[1] * t[1]) + t[2] * t[2])
+            ok = (rr > 0.0) & (rr < np.inf) & (y1 != 0.0)
+            u = [t[j] / rr for j in range(3)]
+
+            def col(kind, a):
+                if kind == 1:
+                    return [(1.0 if j == a else 0.0) - nn[j] * nn[a] for j in range(3)]
+                return [-(nn[j] * F[a] + (sdot if j == a else 0.0)) for j in range(3)]
+
+            for u6 in range(6):
+                for v6 in range(6):
+                    ku, au = (1, u6) if u6 < 3 else (3, u6 - 3)
+                    kv, av = (1, v6) if v6 < 3 else (3, v6 - 3)
+                    uu = 3 + 9 * i + (u6 if u6 < 3 else 3 + u6)
+                    vv = 3 + 9 * i + (v6 if v6 < 3 else 3 + v6)
+                    h = H[:, uu, vv].copy()
+                    fn = (ku == 1 and kv == 3) or (ku == 3 and kv == 1)
+                    aF = au if ku == 1 else av
+                    an = au if ku == 3 else av
+                    if fn and aF == an:
+                        h = h - (y0 + mu * y1)
+                    cu, cv = col(ku, au), col(kv, av)
+                    jj = (cu[0] * cv[0] + cu[1] * cv[1]) + cu[2] * cv[2]
+                    pu = (u[0] * cu[0] + u[1] * cu[1]) + u[2] * cu[2]
+                    pv = (u[0] * cv[0] + u[1] * cv[1]) + u[2] * cv[2]
+                    if fn:
+                        un = (u[0] * nn[0] + u[1] * nn[1]) + u[2] * nn[2]
+                        second = -((un if aF == an else 0.0) + nn[aF] * u[an])
+                    elif ku == 3 and kv == 3:
+                        second = -(F[au] * u[av] + F[av] * u[au])
+                    else:
+                        second = 0.0
+                    H[:, uu, vv] = np.where(ok, h + y1 * ((jj - pu * pv) / rr + second), h)
+    if free_idx is not None:
+        fi = np.asarray(free_idx, dtype=np.int64)
+        H = H[:, fi][:, :, fi]
+    return H

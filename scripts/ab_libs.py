@@ -1,0 +1,60 @@
+"""A/B of two builds of the HIP library in ONE process (interleaved rounds, same inputs/outputs).
+
+python scripts/ab_libs.py --config sq8 --libs centroidalplanner_amd/libcpl_mi355x.so,build/libcpl_old.so
+Both libraries export the same C-ABI; each is loaded under its own handle (RTLD_LOCAL) and timed with
+its own cpl_time_eval_batch (HIP events on the launch stream).
+"""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from bench import algorithmic_bytes  # noqa: E402
+from centroidalplanner_amd import _abi  # noqa: E402
+from centroidalplanner_amd.workload import CONFIGS, config_inputs  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="sq8")
+ap.add_argument("--batch", type=int, default=0)
+ap.add_argument("--rounds", type=int, default=7)
+ap.add_argument("--reps", type=int, default=20)
+ap.add_argument("--libs", default="centroidalplanner_amd/libcpl_mi355x.so,build/libcpl_old.so")
+args = ap.parse_args()
+
+libs = {}
+for tag in args.libs.split(","):
+    path = tag
+    lib = ctypes.CDLL(os.path.abspath(path), mode=ctypes.RTLD_LOCAL)
+    fn = lib.cpl_time_eval_batch
+    res, sig = _abi.SIGNATURES["cpl_time_eval_batch"]
+    fn.restype, fn.argtypes = res, sig
+    libs[tag] = lib
+
+cfg = CONFIGS[args.config]
+B = args.batch or cfg.batch
+prob, x, mass, tag = config_inputs(cfg, B)
+dev = torch.device("cuda:0")
+xt, mt = torch.tensor(x, device=dev), torch.tensor(mass, device=dev)
+tt = None if tag is None else torch.tensor(tag, device=dev)
+out = prob.eval_batch(xt, mt, tt, outputs=("g", "jac", "norms"))
+stream = torch.cuda.current_stream()
+p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+times = {k: [] for k in libs}
+for _ in range(args.rounds):
+    for k, lib in libs.items():
+        ms = ctypes.c_double()
+        _abi.check(lib.cpl_time_eval_batch(ctypes.byref(prob.desc()), B, p(xt), p(mt), p(tt), p(out["g"]), p(out["jac"]),
+                                           None, None, p(out["norms"]), ctypes.c_void_p(stream.cuda_stream), args.reps,
+                                           ctypes.byref(ms)))
+        times[k].append(ms.value)
+bpi, m = algorithmic_bytes(cfg.n_contacts, cfg.env)
+for k, ts in times.items():
+    med = statistics.median(ts)
+    print(json.dumps({"config": args.config, "batch": B, "lib": k, "median_ms": med, "min_ms": min(ts),
+                      "GBps": bpi * B / (med * 1e-3) / 1e9}), flush=True)

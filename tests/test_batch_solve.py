@@ -23,15 +23,24 @@ torch = pytest.importorskip("torch")
 
 
 class OracleBatchEvaluator:
-    """Batched callbacks through the CPU restatement, on CPU torch tensors."""
+    """Batched callbacks through the CPU restatement, on CPU torch tensors; `hessian` is the oracle's
+    restatement of the analytic Lagrangian Hessian (Ground / no environment; None otherwise, and the
+    solve loop differences the Lagrangian gradient instead)."""
 
-    def __init__(self, problem):
+    def __init__(self, problem, nthreads=4):
         self.problem = problem
+        self.nthreads = nthreads
 
     def __call__(self, X, mass, outputs=("g", "jac", "f", "grad")):
         o = pyoracle.eval_batch(self.problem.desc(), X.cpu().numpy(), None if mass is None else mass.cpu().numpy(),
-                                None, outputs=tuple(outputs), nthreads=4)
+                                None, outputs=tuple(outputs), nthreads=self.nthreads)
         return {k: torch.as_tensor(v, device=X.device) for k, v in o.items()}
+
+    def hessian(self, X, y, free):
+        if self.problem.desc().env_kind not in (0, 1):
+            return None
+        H = pyoracle.lagrangian_hessian(self.problem.desc(), X.cpu().numpy(), y.cpu().numpy(), free.cpu().numpy())
+        return torch.as_tensor(H, device=X.device)
 
 
 def _certify(prob, x, y, mass, tol_kkt=1e-7):
@@ -309,3 +318,41 @@ def test_batch_solve_gpu_eight_contacts():
     X, Y = r.x.cpu().numpy(), r.y.cpu().numpy()
     for b in range(0, B, 16):
         _certify(prob, X[b], Y[b], mass[b])
+
+
+def test_batch_solve_limited_memory_oracle_cpu():
+    """IFOPT's default Hessian mode (the reference's IpoptSolver keeps it: src/CentroidalPlanner.cpp:22-29):
+    the damped BFGS model, on the host path over the oracle's callbacks."""
+    cpl = solve_problem()
+    prob = cpl.GetCplProblem()
+    X0, mass = solve_inputs(prob, 4, seed=11)
+    r = batch_ipm_solve(prob, torch.as_tensor(X0), torch.as_tensor(mass), evaluator=OracleBatchEvaluator(prob),
+                        max_iter=1000, hessian="limited-memory")
+    assert bool((r.status <= STATUS_ACCEPTABLE).all()), r.status
+    for b in range(X0.shape[0]):
+        _certify(prob, r.x[b].numpy(), r.y[b].numpy(), mass[b], tol_kkt=1e-5)
+
+
+@pytest.mark.gpu
+def test_batch_solve_gpu_limited_memory():
+    """The limited-memory (BFGS) mode on the device with the kernel callbacks, graph-captured."""
+    from centroidalplanner_amd.batch_ipm import KernelEvaluator
+
+    cpl = solve_problem()
+    prob = cpl.GetCplProblem()
+    B = 256
+    X0, mass = solve_inputs(prob, B, seed=9)
+    dev = torch.device("cuda:0")
+    ev = KernelEvaluator(prob)
+    r = batch_ipm_solve(prob, torch.as_tensor(X0, device=dev), torch.as_tensor(mass, device=dev), evaluator=ev,
+                        max_iter=1000, hessian="limited-memory")
+    assert r.graph
+    st = r.status.cpu().numpy()
+    assert (st <= STATUS_ACCEPTABLE).all(), np.bincount(st)
+    X, Y = r.x.cpu().numpy(), r.y.cpu().numpy()
+    for b in range(0, B, 23):
+        _certify(prob, X[b], Y[b], mass[b], tol_kkt=1e-5)
+    sub = np.arange(0, B, 64)
+    rc = batch_ipm_solve(prob, torch.as_tensor(X0[sub]), torch.as_tensor(mass[sub]), evaluator=OracleBatchEvaluator(prob),
+                         max_iter=1000, hessian="limited-memory")
+    np.testing.assert_allclose(r.objective.cpu().numpy()[sub], rc.objective.numpy(), rtol=1e-6)
