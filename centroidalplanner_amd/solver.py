@@ -1,15 +1,14 @@
-"""Solve() plumbing of the facade: a host NLP driver over the GPU callbacks.
+"""Solve() plumbing of the facade: the batched interior-point solve loop on a batch of one.
 
-The reference drives each solve with ifopt::IpoptSolver (src/CentroidalPlanner.cpp:22-34).  IPOPT
-is not in this image.  Two drivers consume the same TNLP hooks (get_bounds_info, eval_f,
-eval_grad_f, eval_g, eval_jac_g; the Jacobian scattered from the CSR values with the (iRow, jCol)
-structure):
-  * method="slsqp" (default): SciPy's SLSQP, one instance;
-  * method="ipm": the batched interior-point solve loop (batch_ipm.py, IPOPT's method) on a batch
-    of one — the driver of the 8,192-instance solves, here from the problem's current variables
-    (x = 0 initially, as the reference's IPOPT start point).  It takes rank-deficient equality
-    Jacobians (TestBasic's single-contact problem), which SLSQP cannot.
-Evaluators expose ``eval_batch(X[B, n]) -> {f, grad, g, jac}`` (host arrays); None = the GPU kernel.
+The reference drives each solve with ifopt::IpoptSolver (src/CentroidalPlanner.cpp:22-34): IPOPT
+with IFOPT's defaults — exact constraint Jacobian, limited-memory Hessian, max_iter 3000, tol 1e-8
+— from the problem's current variables (x = 0 initially, src/Variable3D.cpp:8-10).  IPOPT is not in
+this image; the same method runs here as the batched solve loop (batch_ipm.py, the driver of the
+8,192-instance solves) with B = 1: on the GPU (HIP kernels, the iteration captured as a HIP graph)
+when no evaluator is given, else on the host over the evaluator's callbacks (tests inject the
+oracle).  Like IFOPT's solver, a run that ends without convergence does not throw: the last iterate
+is kept (src/CentroidalPlanner.cpp:29-33), `success` says how it ended.
+Evaluators expose ``eval_batch(X[B, n]) -> {f, grad, g, jac}`` (host arrays).
 """
 from __future__ import annotations
 
@@ -18,7 +17,14 @@ from typing import Optional
 
 import numpy as np
 
-from ._abi import INF
+
+@dataclass
+class SolveResult:
+    x: np.ndarray
+    success: bool
+    status: str
+    iterations: int
+    primal_inf: float
 
 
 class TorchEvaluator:
@@ -38,10 +44,13 @@ class TorchEvaluator:
 
 
 class _HostBatchEvaluator:
-    """An eval_batch(X) evaluator as batch_ipm's callback (CPU tensors in and out)."""
+    """An eval_batch(X) evaluator as batch_ipm's callback (CPU tensors in and out); forwards an
+    analytic `hessian(X, y, free)` when the evaluator has one."""
 
     def __init__(self, ev):
         self.ev = ev
+        if hasattr(ev, "hessian"):
+            self.hessian = self._hessian
 
     def __call__(self, X, mass, outputs=("g", "jac", "f", "grad")):
         import torch
@@ -49,91 +58,31 @@ class _HostBatchEvaluator:
         o = self.ev.eval_batch(X.cpu().numpy())
         return {k: torch.as_tensor(np.asarray(o[k]), device=X.device) for k in outputs}
 
+    def _hessian(self, X, y, free):
+        import torch
 
-def _ipm_solve(problem, evaluator, x0, tol, max_iter) -> SolveResult:
-    """The batched solve loop on one instance: the GPU loop (HIP kernels, graph-captured) when no
-    evaluator is given, else the same algorithm's host path over the evaluator's callbacks."""
+        H = self.ev.hessian(X.cpu().numpy(), y.cpu().numpy(), free.cpu().numpy())
+        return None if H is None else torch.as_tensor(np.asarray(H), device=X.device)
+
+
+def solve(problem, evaluator=None, x0: Optional[np.ndarray] = None, tol: float = 1e-8, max_iter: int = 3000,
+          hessian: str = "limited-memory") -> SolveResult:
+    """One instance through the batched solve loop.  hessian: "limited-memory" (IFOPT's default, as
+    the reference runs) or "exact" (the analytic Lagrangian Hessian)."""
     import torch
 
-    from .batch_ipm import STATUS_ACCEPTABLE, batch_ipm_solve
+    from .batch_ipm import STATUS_ACCEPTABLE, STATUS_NAMES, batch_ipm_solve
 
-    xl, xu, gl, gu = problem.get_bounds_info()
+    xl, xu, _, _ = problem.get_bounds_info()
     x0 = np.clip(problem.get_starting_point() if x0 is None else np.asarray(x0, dtype=np.float64), xl, xu)
     if evaluator is None:
         X0 = torch.as_tensor(x0[None], device=torch.device("cuda", torch.cuda.current_device()))
-        r = batch_ipm_solve(problem, X0, None, tol=max(tol, 1e-8), max_iter=max_iter)
+        r = batch_ipm_solve(problem, X0, None, tol=tol, max_iter=max_iter, hessian=hessian)
     else:
         r = batch_ipm_solve(problem, torch.as_tensor(x0[None]), None, evaluator=_HostBatchEvaluator(evaluator),
-                            tol=max(tol, 1e-8), max_iter=max_iter)
+                            tol=tol, max_iter=max_iter, hessian=hessian)
     x = r.x[0].cpu().numpy()
     st = int(r.status[0])
     problem.SetVariables(x)  # the next Solve warm-starts here, like the reference's persistent variables
-    names = {0: "optimal", 1: "acceptable"}
-    return SolveResult(x, st <= STATUS_ACCEPTABLE, names.get(st, f"status {st}"), int(r.iterations[0]),
+    return SolveResult(x, st <= STATUS_ACCEPTABLE, STATUS_NAMES.get(st, f"status {st}"), int(r.iterations[0]),
                        float(r.primal_inf[0]))
-
-
-@dataclass
-class SolveResult:
-    x: np.ndarray
-    success: bool
-    status: str
-    iterations: int
-    primal_inf: float
-
-
-class _Cached:
-    """One evaluation per distinct x (SLSQP asks for f, grad, g, jac at the same point)."""
-
-    def __init__(self, ev, nan_jac_to_zero):
-        self.ev, self.key, self.out, self.nan0 = ev, None, None, nan_jac_to_zero
-
-    def __call__(self, x):
-        k = x.tobytes()
-        if k != self.key:
-            o = self.ev.eval_batch(np.asarray(x, dtype=np.float64)[None, :])
-            self.out = {q: v[0] for q, v in o.items()}
-            if self.nan0:
-                self.out["jac"] = np.nan_to_num(self.out["jac"], nan=0.0)
-            self.key = k
-        return self.out
-
-
-def solve(problem, evaluator=None, x0: Optional[np.ndarray] = None, tol: float = 1e-14, max_iter: int = 3000,
-          method: str = "slsqp") -> SolveResult:
-    if method == "ipm":
-        return _ipm_solve(problem, evaluator, x0, tol, max_iter)
-    if method != "slsqp":
-        raise ValueError("method must be 'slsqp' or 'ipm'")
-    ev = evaluator if evaluator is not None else TorchEvaluator(problem)
-    from scipy.optimize import minimize
-
-    n, m, nnz = problem.get_nlp_info()
-    iRow, jCol = problem.get_structure()
-    xl, xu, gl, gu = problem.get_bounds_info()
-    x0 = problem.get_starting_point() if x0 is None else np.asarray(x0, dtype=np.float64)
-    x0 = np.clip(x0, xl, xu)
-    at = _Cached(ev, nan_jac_to_zero=True)  # a cone at zero tangential force has a 0/0 Jacobian
-
-    def J(x):
-        A = np.zeros((m, n))
-        A[iRow, jCol] = at(x)["jac"]
-        return A
-
-    eq = np.where(gl == gu)[0]
-    up = np.where((gl != gu) & (gu < INF / 10))[0]
-    lo = np.where((gl != gu) & (gl > -INF / 10))[0]
-    cons = []
-    if eq.size:
-        cons.append({"type": "eq", "fun": lambda x: at(x)["g"][eq] - gu[eq], "jac": lambda x: J(x)[eq]})
-    if up.size:
-        cons.append({"type": "ineq", "fun": lambda x: gu[up] - at(x)["g"][up], "jac": lambda x: -J(x)[up]})
-    if lo.size:
-        cons.append({"type": "ineq", "fun": lambda x: at(x)["g"][lo] - gl[lo], "jac": lambda x: J(x)[lo]})
-    res = minimize(lambda x: float(at(x)["f"]), x0, jac=lambda x: at(x)["grad"], bounds=list(zip(xl, xu)),
-                   constraints=cons, method="SLSQP", options={"ftol": tol, "maxiter": max_iter})
-    x = np.clip(res.x, xl, xu)
-    g = at(x)["g"]
-    viol = np.maximum(np.maximum(gl - g, g - gu), 0.0)
-    problem.SetVariables(x)  # the next Solve warm-starts here, like the reference's persistent variables
-    return SolveResult(x, bool(res.success), str(res.message), int(res.nit), float(viol.max(initial=0.0)))

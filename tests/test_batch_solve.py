@@ -85,7 +85,7 @@ def _certify(prob, x, y, mass, tol_kkt=1e-7):
 
 
 def _slsqp_objective(prob, x0, mass):
-    from centroidalplanner_amd.solver import solve
+    from slsqp_ref import slsqp_solve
 
     class E:
         def eval_batch(self, X):
@@ -93,7 +93,7 @@ def _slsqp_objective(prob, x0, mass):
             return pyoracle.eval_batch(prob.desc(), X, np.full(X.shape[0], mass), None,
                                        outputs=("g", "jac", "f", "grad"), nthreads=1)
 
-    r = solve(prob, E(), x0=x0, tol=1e-12, max_iter=500)
+    r = slsqp_solve(prob, E(), x0=x0, tol=1e-12, max_iter=500)
     o = E().eval_batch(r.x)
     return float(o["f"][0])
 

@@ -10,10 +10,12 @@ balance, friction cone, surface and bounds).
 
 Start point: the reference starts IPOPT from x = 0 (Variable3D init, src/Variable3D.cpp:8-10),
 where FrictionCone's Jacobian is 0/0 (src/Constraints/FrictionCone.cpp:85-87).  testSimpleProblem
-is solved from exactly that point by the batched interior-point loop on one instance
-(batch_ipm.py, IPOPT's method; NaN Jacobian entries of a cone at zero tangential force count as 0).
-The 4-contact scenarios run the facade's default single-instance driver (SLSQP) from a
-non-degenerate start.
+is solved from exactly that point; every scenario runs the facade's Solve(): the batched
+interior-point loop on one instance (batch_ipm.py, IPOPT's method with IFOPT's defaults — the
+limited-memory Hessian, max_iter 3000; NaN Jacobian entries of a cone at zero tangential force count
+as 0).  The 4-contact scenarios start from a non-degenerate point (TestBasic's ground scenario with
+force weight 0 has a continuum of optimal force distributions; the loop reaches a feasible point
+satisfying every TestBasic assertion, within the 3000 iterations IPOPT is also limited to).
 """
 import numpy as np
 import pytest
@@ -66,8 +68,8 @@ def test_simple_problem(backend):
     settings, Solve() from the reference's start point x = 0, TestBasic's assertions.
 
     With one contact the equality Jacobian is rank-deficient for every x (the torque about the
-    force line, F . ((p - c) x F), is identically zero) — SLSQP cannot take that, the interior-point
-    loop (IPOPT's method, delta_c regularisation of the rank-deficient rows) can.  From x = 0 the
+    force line, F . ((p - c) x F), is identically zero) — the interior-point loop (IPOPT's method,
+    delta_c regularisation of the rank-deficient rows) takes it.  From x = 0 the
     torque rows are identically zero (F = 0, p = c), their multipliers grow to ~1e9 in the first
     steps, and the loop stops on IPOPT's scaled 'acceptable' test (s_d scales the dual error by the
     multipliers' size) — TestBasic asserts the contact point, normal and vertical force, not the CoM
@@ -80,7 +82,6 @@ def test_simple_problem(backend):
     cpl = CentroidalPlanner(names, robot_mass, env)
     prob = cpl.GetCplProblem()
     assert not prob.get_starting_point().any()  # x = 0, Variable3D's initial value
-    cpl.solver_method = "ipm"
     if backend == "oracle":
         cpl.evaluator = OracleEvaluator(prob)
     sol = cpl.Solve()
