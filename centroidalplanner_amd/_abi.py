@@ -74,6 +74,29 @@ class ProblemDesc(ctypes.Structure):
     ]
 
 
+class SolveOptions(ctypes.Structure):
+    """cpl_solve_options (include/cpl_mi355x.h)."""
+
+    _fields_ = [
+        ("max_iter", c_int32),
+        ("hessian", c_int32),
+        ("max_ls", c_int32),
+        ("max_soc", c_int32),
+        ("acceptable_iter", c_int32),
+        ("use_graph", c_int32),
+        ("reserved0", c_int32),
+        ("reserved1", c_int32),
+        ("tol", c_double),
+        ("acceptable_tol", c_double),
+        ("mu_init", c_double),
+        ("fd_step", c_double),
+    ]
+
+
+HESSIAN_EXACT = 0
+HESSIAN_LIMITED_MEMORY = 1
+HESSIAN_FD = 2
+
 # every symbol include/cpl_mi355x.h declares, with its ctypes signature
 _DESC_P = POINTER(ProblemDesc)
 _DP = POINTER(c_double)
@@ -156,6 +179,11 @@ SIGNATURES = {
     "cpl_ipm_accept": (c_int32, [c_int64, c_int32, c_int32, c_int32] + [c_void_p] * 30),
     "cpl_ipm_masked_rows": (c_int32, [c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
     "cpl_ipm_dense_a": (c_int32, [c_int64, c_int32, c_int32, c_int32, c_int32] + [c_void_p] * 6),
+    "cpl_solve_options_default": (None, [POINTER(SolveOptions)]),
+    "cpl_solver_create": (c_int32, [_DESC_P, c_int64, POINTER(SolveOptions), POINTER(c_void_p)]),
+    "cpl_solver_destroy": (c_int32, [c_void_p]),
+    "cpl_solver_solve": (c_int32, [c_void_p] + [c_void_p] * 10 + [POINTER(c_int32), POINTER(c_int64), c_void_p]),
+    "cpl_solver_dims": (c_int32, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
 }
 
 

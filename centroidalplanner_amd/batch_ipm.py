@@ -38,13 +38,18 @@ uses, batched over instances, with every per-instance quantity a row of a device
     (1e-6) for 15 consecutive iterations.
 
 Every evaluation — the iterate, each line-search trial point, the finite-difference points — is ONE
-batched call of the evaluator for all instances.  The product evaluator (KernelEvaluator) is the
-gfx950 eval kernel through cpl_eval_batch on device-resident tensors.  Instances that converged
-stay in the batch (frozen), so every launch keeps its shape; one iteration has no host
-synchronisation at all (fixed trip counts, masked updates), and on the device it is captured once
-as a HIP graph and replayed — on the device path the host reads an "any active" flag one iteration
-behind (no stall); on host tensors it checks every `check_every` iterations whether any
-instance is still active.
+batched call of the evaluator for all instances.  Instances that converged stay in the batch
+(frozen), so every launch keeps its shape; one iteration has no host synchronisation at all (fixed
+trip counts, masked updates).
+
+Two implementations of the same iteration:
+  * device tensors -> the native engine (csrc/cpl_solver.hip, C-ABI cpl_solver_*, NativeSolver
+    below): the product callbacks (cpl_eval_batch with values-only Jacobian records), the Newton
+    step in cpl_kkt_solve, the per-instance work in the cpl_ipm_* kernels and the glue in the
+    engine's own kernels; the iteration captured once as a HIP graph and replayed, the host reading
+    an "any active" flag one iteration behind.  No framework ops on the path;
+  * host tensors -> this module's torch restatement over any evaluator's callbacks (the tests drive
+    it with the oracle's): the checker of the device path — the same algorithm, step for step.
 """
 from __future__ import annotations
 
@@ -129,6 +134,73 @@ class BatchSolveResult:
 _PIVOT_REL = 2.220446049250313e-16  # DBL_EPSILON: the KKT inertia test's zero-pivot level
 
 
+class NativeSolver:
+    """The native batched solve engine (csrc/cpl_solver.hip, C-ABI cpl_solver_*): the device path of
+    batch_ipm_solve.  One handle per (problem template, batch, options): device buffers allocated
+    once, the iteration captured once as a HIP graph and replayed on every solve."""
+
+    def __init__(self, problem, batch, tol=1e-8, max_iter=3000, mu_init=0.1, acceptable_tol=1e-6,
+                 acceptable_iter=15, max_ls=4, max_soc=1, hessian="exact", fd_step=1e-6, graph=True):
+        o = _abi.SolveOptions()
+        _abi.lib.cpl_solve_options_default(ctypes.byref(o))
+        o.max_iter, o.max_ls, o.max_soc, o.acceptable_iter = int(max_iter), int(max_ls), int(max_soc), int(acceptable_iter)
+        o.tol, o.acceptable_tol, o.mu_init, o.fd_step = float(tol), float(acceptable_tol), float(mu_init), float(fd_step)
+        o.hessian = {"exact": _abi.HESSIAN_EXACT, "limited-memory": _abi.HESSIAN_LIMITED_MEMORY,
+                     "fd": _abi.HESSIAN_FD}[hessian]
+        o.use_graph = 1 if graph else 0
+        self.problem, self.batch = problem, int(batch)
+        self.desc = problem.desc()
+        self.handle = ctypes.c_void_p()
+        _abi.check(_abi.lib.cpl_solver_create(ctypes.byref(self.desc), self.batch, ctypes.byref(o),
+                                              ctypes.byref(self.handle)))
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and _abi is not None and getattr(_abi, "lib", None) is not None:
+            _abi.lib.cpl_solver_destroy(h)
+            self.handle = None
+
+    def solve(self, X0, mass=None, env_tag=None) -> "BatchSolveResult":
+        import torch
+
+        n, m, _ = self.problem.get_nlp_info()
+        B, dev = self.batch, X0.device
+        if X0.shape != (B, n) or X0.dtype != torch.float64 or not X0.is_cuda:
+            raise ValueError(f"X0 must be a float64 CUDA tensor [{B}, {n}]")
+        X0 = X0.contiguous()
+        mass = None if mass is None else mass.to(torch.float64).contiguous()
+        x = torch.empty(B, n, dtype=torch.float64, device=dev)
+        y = torch.empty(B, m, dtype=torch.float64, device=dev)
+        status = torch.empty(B, dtype=torch.int32, device=dev)
+        iters = torch.empty(B, dtype=torch.int32, device=dev)
+        obj, pinf, dinf = (torch.empty(B, dtype=torch.float64, device=dev) for _ in range(3))
+        it = ctypes.c_int32()
+        ev = ctypes.c_int64()
+        _abi.check(_abi.lib.cpl_solver_solve(
+            self.handle, _ptr(X0), None if mass is None else _ptr(mass), None if env_tag is None else _ptr(env_tag),
+            _ptr(x), _ptr(y), _ptr(status), _ptr(iters), _ptr(obj), _ptr(pinf), _ptr(dinf), ctypes.byref(it),
+            ctypes.byref(ev), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+        g = ctypes.c_int32()
+        _abi.check(_abi.lib.cpl_solver_dims(self.handle, None, None, ctypes.byref(g)))
+        return BatchSolveResult(x=x, y=y, status=status.to(torch.int64), iterations=iters.to(torch.int64),
+                                objective=obj, primal_inf=pinf, dual_inf=dinf, evaluations=int(ev.value),
+                                iterations_run=int(it.value), graph=bool(g.value))
+
+
+_NATIVE_CACHE = {}
+
+
+def _native(problem, B, **opts):
+    """A cached NativeSolver for this template / batch / options (the last few kept)."""
+    key = (bytes(problem.desc()), int(B), tuple(sorted(opts.items())))
+    s = _NATIVE_CACHE.get(key)
+    if s is None:
+        while len(_NATIVE_CACHE) >= 2:
+            _NATIVE_CACHE.pop(next(iter(_NATIVE_CACHE)))
+        s = _NATIVE_CACHE[key] = NativeSolver(problem, B, **opts)
+    return s
+
+
 def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None, tol: float = 1e-8,
                     max_iter: int = 3000, mu_init: float = 0.1, acceptable_tol: float = 1e-6,
                     acceptable_iter: int = 15, max_ls: int = 4, max_soc: int = 1, hessian: str = "exact",
@@ -149,11 +221,23 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     use_bfgs = hessian == "limited-memory"
     import torch
 
+    if X0.is_cuda:  # device tensors: the native engine (csrc/cpl_solver.hip) with the product callbacks
+        if evaluator is not None and not isinstance(evaluator, KernelEvaluator):
+            raise ValueError("device solves run the product callbacks (KernelEvaluator); custom evaluators take "
+                             "host tensors")
+        ns = _native(problem, X0.shape[0], tol=tol, max_iter=max_iter, mu_init=mu_init, acceptable_tol=acceptable_tol,
+                     acceptable_iter=acceptable_iter, max_ls=max_ls, max_soc=max_soc, hessian=hessian,
+                     fd_step=fd_step, graph=True if graph is None else bool(graph))
+        r = ns.solve(X0, mass, None if evaluator is None else evaluator.env_tag)
+        if evaluator is not None:
+            evaluator.calls += r.evaluations
+        return r
+
+    # host tensors: this module's restatement, step for step, of the engine's iteration — the checker
+    # of the device path over any evaluator's callbacks (tests drive it with the oracle's)
     ev = evaluator if evaluator is not None else KernelEvaluator(problem)
     dev, dt = X0.device, torch.float64
-    use_hip = X0.is_cuda  # device tensors: Newton step and J^T y on the device
-    use_graph = (use_hip if graph is None else bool(graph)) and verbose <= 1
-    if use_graph and not use_hip:
+    if graph:
         raise ValueError("graph capture needs device tensors")
     B = X0.shape[0]
     n, m, nnz = problem.get_nlp_info()
@@ -176,9 +260,6 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     I = torch.as_tensor(I_np, device=dev)
     nI = I_np.size
     nw = nf + nI
-    if use_hip and nw > 128:  # the device kernels stage one instance's primal-slack vector per wave
-        raise ValueError(f"batch_ipm_solve: {nw} primal-slack unknowns (free variables + inequality rows); "
-                         "the device solve loop supports at most 128 (about 11 contacts with an environment)")
     zeros_B = torch.zeros(B, dtype=dt, device=dev)
     # A = dc/dw = [J[:, free] | -P], P[r, j] = 1 where row r is inequality j
     P = torch.zeros(m, nI, dtype=dt, device=dev)
@@ -196,42 +277,12 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     hasL, hasU = torch.isfinite(wl), torch.isfinite(wu)
     wl0, wu0 = torch.where(hasL, wl, torch.zeros_like(wl)), torch.where(hasU, wu, torch.zeros_like(wu))
     nbounds = int(hasL.sum().item() + hasU.sum().item())
-    hasL_u8, hasU_u8 = hasL.to(torch.uint8).contiguous(), hasU.to(torch.uint8).contiguous()
     eye_m = torch.eye(m, dtype=dt, device=dev)
     eye_w = torch.eye(nw, dtype=dt, device=dev)
     eye_f = torch.eye(nf, dtype=dt, device=dev)
     fslot = torch.arange(FMAX, device=dev)[None, :]
     fd_cols = torch.arange(nf, device=dev)
 
-    # transposed (CSC) index of the fixed CSR structure, for the device Lagrangian gradient
-    order = np.lexsort((iRow, jCol))
-    col_ptr_np = np.zeros(n + 1, dtype=np.int64)
-    np.add.at(col_ptr_np, jCol.astype(np.int64) + 1, 1)
-    col_ptr_np = np.cumsum(col_ptr_np)
-    csc = [torch.as_tensor(a.astype(np.int32), device=dev) for a in (col_ptr_np, order, iRow[order])]
-    row_slack_np = np.full(m, -1, dtype=np.int32)
-    row_slack_np[I_np] = np.arange(nI, dtype=np.int32)
-    row_slack = torch.as_tensor(row_slack_np, device=dev)
-    # device path: the Jacobian state stays in CSR form; A = [J_free | -P] is gathered per iteration
-    csr_J = use_hip and not use_bfgs
-    dense_pos = np.full(m * n, -1, dtype=np.int64)
-    dense_pos[iRow.astype(np.int64) * n + jCol.astype(np.int64)] = np.arange(nnz)
-    # the product evaluator writes values-only Jacobian records (the structural constants skipped,
-    # CPL_EVAL_JAC_FOLDED): amap points into the folded record, -2 marks a skipped constant 1
-    folded = csr_J and isinstance(ev, KernelEvaluator)
-    if folded:
-        var_k, const_k, const_val = problem.jac_fold_info()
-        rec_pos = np.full(nnz, -1, dtype=np.int64)
-        rec_pos[var_k] = np.arange(var_k.size)
-        rec_pos[const_k[const_val == 1.0]] = -2
-        assert set(np.unique(const_val)) <= {0.0, 1.0}
-        dense_rec = np.where(dense_pos >= 0, rec_pos[np.maximum(dense_pos, 0)], -1)
-        nnz_rec = int(var_k.size)
-    else:
-        dense_rec, nnz_rec = dense_pos, nnz
-    amap = torch.as_tensor(dense_rec.reshape(m, n)[:, np.where(~fixed_np)[0]].astype(np.int32).copy(), device=dev)
-    if use_hip:
-        kkt_ws = torch.empty(B * int(_abi.lib.cpl_kkt_workspace_doubles(nw, m)), dtype=dt, device=dev)
 
     def push(v):  # IPOPT bound_push = bound_frac = 1e-2 (absolute and relative to the range)
         k = 1e-2
@@ -247,9 +298,6 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     Mass_fd = None if Mass is None else Mass.repeat_interleave(2 * nf).contiguous()
     n_eval = 0
 
-    def stream():
-        return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream) if use_hip else None
-
     def evaluate_fg(Xe):  # line-search trial points: constraint values and objective only
         nonlocal n_eval
         n_eval += 1
@@ -259,9 +307,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     def evaluate(Xe):
         nonlocal n_eval
         n_eval += 1
-        o = ev(Xe, Mass, jac_folded=True) if folded else ev(Xe, Mass)
-        if csr_J:  # the device path keeps the Jacobian records; jac_w builds A from them in one launch
-            return {"f": o["f"], "grad": o["grad"], "g": o["g"], "J": o["jac"].contiguous()}
+        o = ev(Xe, Mass)
         J = torch.zeros(B, m * n, dtype=dt, device=dev)
         J[:, flat_idx] = torch.nan_to_num(o["jac"], nan=0.0)  # a cone at F_t = 0 has a 0/0 Jacobian
         return {"f": o["f"], "grad": o["grad"], "g": o["g"], "J": J.view(B, m, n)}
@@ -277,11 +323,6 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         return c
 
     def jac_w(J, mask=None):
-        if csr_J:  # mask: rows of inactive instances are left unwritten (never read for them)
-            A_ = torch.empty(B, m, nw, dtype=dt, device=dev)
-            _abi.check(_abi.lib.cpl_ipm_dense_a(B, m, nw, nf, nnz_rec, _ptr(amap), _ptr(row_slack), _ptr(J), _ptr(A_),
-                                                None if mask is None else _ptr(mask), stream()))
-            return A_
         return torch.cat([J[:, :, free], (-P).expand(B, m, nI)], dim=2)
 
     def barrier(wv, muv):
@@ -296,84 +337,12 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         Xp[:, fd_cols, free] += h
         Xp[:, nf + fd_cols, free] -= h
         n_eval += 1
-        fused = ev.lagrangian_grad if use_hip and hasattr(ev, "lagrangian_grad") else None
-        gL = fused(Xp.view(B * 2 * nf, n), Mass_fd, yv.contiguous(), 2 * nf, csc) if fused else None
-        if gL is not None:  # one launch: eval + grad f + J^T y from the LDS tile image
-            pass
-        elif use_hip:  # grad f + J^T y on the device (cpl_lagrangian_grad), y shared by the 2 nf points
-            o = ev(Xp.view(B * 2 * nf, n), Mass_fd, outputs=("jac", "grad"))
-            gL = torch.empty(B * 2 * nf, n, dtype=dt, device=dev)
-            yc = yv.contiguous()
-            _abi.check(_abi.lib.cpl_lagrangian_grad(B * 2 * nf, n, m, nnz, _ptr(csc[0]), _ptr(csc[1]), _ptr(csc[2]),
-                                                    _ptr(o["grad"]), _ptr(o["jac"]), _ptr(yc), 2 * nf, _ptr(gL),
-                                                    stream()))
-        else:
-            o = ev(Xp.view(B * 2 * nf, n), Mass_fd, outputs=("jac", "grad"))
-            gL = o["grad"].clone()
-            gL.index_add_(1, jCol_t, torch.nan_to_num(o["jac"], nan=0.0) * yv.repeat_interleave(2 * nf, 0)[:, iRow_t])
+        o = ev(Xp.view(B * 2 * nf, n), Mass_fd, outputs=("jac", "grad"))
+        gL = o["grad"].clone()
+        gL.index_add_(1, jCol_t, torch.nan_to_num(o["jac"], nan=0.0) * yv.repeat_interleave(2 * nf, 0)[:, iRow_t])
         gL = gL.view(B, 2 * nf, n)[:, :, free]
         H = (gL[:, :nf] - gL[:, nf:]) / (2.0 * h[:, :, None])
         return 0.5 * (H + H.transpose(1, 2))
-
-    # the analytic Hessian kernel where the problem's environment allows it (a batch-0 call only
-    # validates: CPL_ERR_UNSUPPORTED for Superquadric / mixed)
-    analytic_H = (use_hip and hessian == "exact" and
-                  _abi.lib.cpl_lagrangian_hessian(ctypes.byref(problem.desc()), 0, None, None, None, None, max(nf, 1),
-                                                  None, None) == _abi.OK)
-    free_i32 = torch.as_tensor(np.where(~fixed_np)[0].astype(np.int32), device=dev)
-    Mr_buf = torch.zeros(B, nw, nw, dtype=dt, device=dev) if use_hip else None  # feasibility-step matrix
-    freepos_np = np.full(n, -1, dtype=np.int32)
-    freepos_np[np.where(~fixed_np)[0]] = np.arange(nf, dtype=np.int32)
-    freepos = torch.as_tensor(freepos_np, device=dev)
-
-    def fd_grads_dev(Xc, yv):
-        """Device path of fd_hessian: the 2 nf points of every instance (cpl_ipm_fd_points) and their
-        Lagrangian gradients (one fused eval launch); the differencing happens in the Newton setup."""
-        nonlocal n_eval
-        Xp = torch.empty(B * 2 * nf, n, dtype=dt, device=dev)
-        h = torch.empty(B, nf, dtype=dt, device=dev)
-        _abi.check(_abi.lib.cpl_ipm_fd_points(B, n, nf, fd_step, _ptr(freepos), _ptr(Xc.contiguous()), _ptr(Xp),
-                                              _ptr(h), _ptr(S["active"]), stream()))
-        n_eval += 1
-        yc = yv.contiguous()
-        fused = ev.lagrangian_grad if hasattr(ev, "lagrangian_grad") else None
-        # converged instances are skipped: their rows of gL stay unwritten and only ever feed their
-        # own (masked) Newton step
-        gL = fused(Xp, Mass_fd, yc, 2 * nf, csc, S["active"]) if fused else None
-        if gL is None:
-            o = ev(Xp, Mass_fd, outputs=("jac", "grad"))
-            gL = torch.empty(B * 2 * nf, n, dtype=dt, device=dev)
-            _abi.check(_abi.lib.cpl_lagrangian_grad(B * 2 * nf, n, m, nnz, _ptr(csc[0]), _ptr(csc[1]), _ptr(csc[2]),
-                                                    _ptr(o["grad"]), _ptr(o["jac"]), _ptr(yc), 2 * nf, _ptr(gL),
-                                                    stream()))
-        return gL, h
-
-    def kkt_device(M, A, r1, r2, mu, dwl, active):
-        """cpl_kkt_solve: factorise + solve on the device; returns (dw, dy, delta_w, solve_primal)."""
-        Mc, Ac, r1c = M.contiguous(), A.contiguous(), r1.contiguous()
-        act_u8 = active.to(torch.uint8)
-        dw = torch.empty(B, nw, dtype=dt, device=dev)
-        dy = torch.empty(B, m, dtype=dt, device=dev)
-        delta_w = torch.empty(B, dtype=dt, device=dev)
-        delta_c = torch.empty(B, dtype=dt, device=dev)
-        info = torch.empty(B, dtype=torch.int32, device=dev)
-        _abi.check(_abi.lib.cpl_kkt_solve(0, B, nw, m, _ptr(Mc), _ptr(Ac), _ptr(r1c), _ptr(r2.contiguous()),
-                                          _ptr(mu.contiguous()), _ptr(dwl.contiguous()), _ptr(act_u8), _ptr(dw),
-                                          _ptr(dy), _ptr(delta_w), _ptr(delta_c), _ptr(info), _ptr(kkt_ws),
-                                          stream()))
-
-        def solve_primal(r2v, mask=None):
-            """Second-order correction: the kept factors, another r2; only the instances in mask
-            (default: the factorised ones) are solved, the others get 0 and cost nothing."""
-            out_dw = torch.empty(B, nw, dtype=dt, device=dev)
-            out_dy = torch.empty(B, m, dtype=dt, device=dev)
-            msk = act_u8 if mask is None else mask.to(torch.uint8)
-            _abi.check(_abi.lib.cpl_kkt_solve(1, B, nw, m, _ptr(Mc), _ptr(Ac), _ptr(r1c), _ptr(r2v.contiguous()),
-                                              None, None, _ptr(msk), _ptr(out_dw), _ptr(out_dy), None, None, None,
-                                              _ptr(kkt_ws), stream()))
-            return out_dw
-
-        return dw, dy, delta_w, solve_primal
 
     def kkt_host(M, A, r1, r2, mu, dwl, active):
         """The same step as cpl_kkt_solve from torch's dense factorisations (host tensors), step for
@@ -438,7 +407,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         dw, dy = refined(r1, r2)
         return dw, dy, delta_w, lambda r2v, mask=None: refined(r1, r2v)[0]
 
-    kkt = kkt_device if use_hip else kkt_host
+    kkt = kkt_host
 
 
     def errors(o, wv, yv, zl, zu):
@@ -527,106 +496,48 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         """One lock-step iteration of every instance; no host synchronisation (graph-capturable)."""
         w, y, zL, zU, mu = S["w"], S["y"], S["zL"], S["zU"], S["mu"]
         cur = {"f": S["f"], "grad": S["grad"], "g": S["g"], "J": S["J"]}
-        if use_hip:  # optimality error, convergence test and barrier update: one fused launch
-            A = jac_w(cur["J"], S["active"])
-            gradw = torch.cat([cur["grad"][:, free], zeros_I], 1)
-            c = cons(cur["g"], w[:, nf:])
-            E = {k: torch.empty(B, dtype=dt, device=dev) for k in ("d_inf", "err0", "base")}
-            mu_o = torch.empty(B, dtype=dt, device=dev)
-            ft, fp = torch.empty_like(S["filt_t"]), torch.empty_like(S["filt_p"])
-            fc = torch.empty_like(S["fcount"])
-            _abi.check(_abi.lib.cpl_ipm_optimality(
-                B, nw, m, FMAX, nbounds, tol, acceptable_tol, acceptable_iter, _ptr(A), _ptr(gradw), _ptr(c), _ptr(w),
-                _ptr(y), _ptr(zL), _ptr(zU), _ptr(hasL_u8), _ptr(hasU_u8), _ptr(wl0), _ptr(wu0), _ptr(mu),
-                _ptr(S["filt_t"]), _ptr(S["filt_p"]), _ptr(S["fcount"]), _ptr(S["active"]), _ptr(S["status"]),
-                _ptr(S["acc"]), _ptr(E["d_inf"]), _ptr(E["err0"]), _ptr(E["base"]), _ptr(mu_o), _ptr(ft), _ptr(fp),
-                _ptr(fc), stream()))
-            S["d_inf"].copy_(E["d_inf"])
-            active = S["active"].clone()
-            mu = mu_o
-        else:
-            E = errors(cur, w, y, zL, zU)
-            active = check(E).clone()
-            A, gradw, c = E["A"], E["gw"], E["c"]
-            # ---- monotone barrier update (two rounds per iteration), filter reset where mu changed
-            ft, fp, fc = S["filt_t"], S["filt_p"], S["fcount"]
-            for _ in range(2):
-                upd = active & (err_mu(E, mu) <= 10.0 * mu) & (mu > tol / 10.0)
-                mu = torch.where(upd, torch.clamp(torch.minimum(0.2 * mu, mu ** 1.5), min=tol / 10.0), mu)
-                ft, fp, fc = reset_filter(upd, ft, fp, fc)
+        E = errors(cur, w, y, zL, zU)
+        active = check(E).clone()
+        A, gradw, c = E["A"], E["gw"], E["c"]
+        # ---- monotone barrier update (two rounds per iteration), filter reset where mu changed
+        ft, fp, fc = S["filt_t"], S["filt_p"], S["fcount"]
+        for _ in range(2):
+            upd = active & (err_mu(E, mu) <= 10.0 * mu) & (mu > tol / 10.0)
+            mu = torch.where(upd, torch.clamp(torch.minimum(0.2 * mu, mu ** 1.5), min=tol / 10.0), mu)
+            ft, fp, fc = reset_filter(upd, ft, fp, fc)
         tau = torch.clamp(1.0 - mu, min=0.99)
 
         def primal_step(d):  # fraction to the boundary along d from w
-            if use_hip:
-                out = torch.empty(B, dtype=dt, device=dev)
-                _abi.check(_abi.lib.cpl_ipm_max_step(B, nw, _ptr(w), _ptr(d.contiguous()), None, None, _ptr(hasL_u8),
-                                                     _ptr(hasU_u8), _ptr(wl0), _ptr(wu0), _ptr(tau), _ptr(out),
-                                                     stream()))
-                return out
             return torch.minimum(max_step(w, d, hasL, wl0, tau), max_step(-w, -d, hasU, -wu0, tau))
 
-        gLfd = hfd = None
         if use_bfgs:
             Hblk = S["Hq"]
-        elif analytic_H:  # the exact Hessian of the Lagrangian, one thread per entry
-            Hblk = torch.empty(B, nf, nf, dtype=dt, device=dev)
-            _abi.check(_abi.lib.cpl_lagrangian_hessian(ctypes.byref(problem.desc()), B, _ptr(unpack(w)),
-                                                       _ptr(y.contiguous()), _ptr(S["active"]), _ptr(free_i32), nf,
-                                                       _ptr(Hblk), stream()))
-        elif use_hip:  # raw central differences here, symmetrised inside the Newton setup kernel
-            gLfd, hfd = fd_grads_dev(unpack(w), y)
-            Hblk = torch.empty(B, nf, nf, dtype=dt, device=dev)
-            _abi.check(_abi.lib.cpl_ipm_fd_hessian_raw(B, n, nf, _ptr(free), _ptr(gLfd), _ptr(hfd), _ptr(Hblk),
-                                                       _ptr(S["active"]), stream()))
         else:
             # host path: the evaluator's own analytic Hessian when it has one (the oracle's restatement
             # of cpl_lagrangian_hessian, so the CPU solve takes the device's exact-Hessian steps)
             Hblk = ev.hessian(unpack(w), y, free) if (hessian == "exact" and hasattr(ev, "hessian")) else None
             if Hblk is None:
                 Hblk = fd_hessian(unpack(w), y)
-        if use_hip:  # Newton system: one fused launch (csrc/cpl_ipm.hip)
-            M = torch.empty(B, nw, nw, dtype=dt, device=dev)
-            r1, gphi, mr_diag = (torch.empty(B, nw, dtype=dt, device=dev) for _ in range(3))
-            r2 = torch.empty(B, m, dtype=dt, device=dev)
-            theta_k, phi_k = torch.empty(B, dtype=dt, device=dev), torch.empty(B, dtype=dt, device=dev)
-            _abi.check(_abi.lib.cpl_ipm_newton_setup(
-                B, nw, m, nf, _ptr(w), _ptr(zL), _ptr(zU), _ptr(gradw), _ptr(A), _ptr(y), _ptr(c),
-                _ptr(cur["f"]), _ptr(mu), _ptr(hasL_u8), _ptr(hasU_u8), _ptr(wl0), _ptr(wu0),
-                None if Hblk is None else _ptr(Hblk.contiguous()), 0 if (use_bfgs or analytic_H) else 1,
-                _ptr(M), _ptr(r1), _ptr(r2), _ptr(gphi), _ptr(mr_diag), _ptr(theta_k), _ptr(phi_k),
-                _ptr(S["active"]) if not use_bfgs else None, stream()))
-        else:
-            dl = torch.where(hasL, w - wl0, torch.ones_like(w))
-            du = torch.where(hasU, wu0 - w, torch.ones_like(w))
-            Sig = torch.where(hasL, zL / dl, torch.zeros_like(w)) + torch.where(hasU, zU / du, torch.zeros_like(w))
-            gphi = gradw - torch.where(hasL, mu[:, None] / dl, torch.zeros_like(w)) + \
-                torch.where(hasU, mu[:, None] / du, torch.zeros_like(w))
-            r1 = -(gphi + (A.transpose(1, 2) @ y.unsqueeze(2)).squeeze(2))
-            r2 = -c
-            M = torch.diag_embed(Sig)
-            M[:, :nf, :nf] += Hblk
-            mr_diag = Sig + mu.sqrt()[:, None] * torch.clamp(w.abs(), min=1.0) ** -2
-            theta_k = c.abs().sum(1)
-            phi_k = cur["f"] + barrier(w, mu)
+        dl = torch.where(hasL, w - wl0, torch.ones_like(w))
+        du = torch.where(hasU, wu0 - w, torch.ones_like(w))
+        Sig = torch.where(hasL, zL / dl, torch.zeros_like(w)) + torch.where(hasU, zU / du, torch.zeros_like(w))
+        gphi = gradw - torch.where(hasL, mu[:, None] / dl, torch.zeros_like(w)) + \
+            torch.where(hasU, mu[:, None] / du, torch.zeros_like(w))
+        r1 = -(gphi + (A.transpose(1, 2) @ y.unsqueeze(2)).squeeze(2))
+        r2 = -c
+        M = torch.diag_embed(Sig)
+        M[:, :nf, :nf] += Hblk
+        mr_diag = Sig + mu.sqrt()[:, None] * torch.clamp(w.abs(), min=1.0) ** -2
+        theta_k = c.abs().sum(1)
+        phi_k = cur["f"] + barrier(w, mu)
         dw, dy, delta_w, solve_primal = kkt(M, A, r1, r2, mu, S["dwl"], active)
-        if use_hip:  # multiplier steps, fraction-to-boundary steps, gd, switching flag: one launch
-            dzL, dzU = torch.empty_like(w), torch.empty_like(w)
-            a_max, a_z, gd = (torch.empty(B, dtype=dt, device=dev) for _ in range(3))
-            switch_ok = torch.empty(B, dtype=torch.bool, device=dev)
-            _abi.check(_abi.lib.cpl_ipm_post_step(
-                B, nw, _ptr(w), _ptr(dw.contiguous()), _ptr(zL), _ptr(zU), _ptr(gphi), _ptr(mu), _ptr(tau),
-                _ptr(hasL_u8), _ptr(hasU_u8), _ptr(wl0), _ptr(wu0), _ptr(theta_k), _ptr(theta_min), _ptr(active),
-                _ptr(delta_w.contiguous()), _ptr(S["dwl"]), _ptr(dzL), _ptr(dzU), _ptr(a_max), _ptr(a_z), _ptr(gd),
-                _ptr(switch_ok), stream()))
-            dwl = S["dwl"]
-        else:
-            dwl = torch.where(active, delta_w, S["dwl"])
-            dzL = torch.where(hasL, mu[:, None] / dl - zL - zL / dl * dw, torch.zeros_like(w))
-            dzU = torch.where(hasU, mu[:, None] / du - zU + zU / du * dw, torch.zeros_like(w))
-            a_max = primal_step(dw)
-            a_z = torch.minimum(max_step(zL, dzL, hasL, 0.0, tau), max_step(zU, dzU, hasU, 0.0, tau))
-            gd = (gphi * dw).sum(1)
-            switch_ok = (theta_k <= theta_min) & (gd < 0)
+        dwl = torch.where(active, delta_w, S["dwl"])
+        dzL = torch.where(hasL, mu[:, None] / dl - zL - zL / dl * dw, torch.zeros_like(w))
+        dzU = torch.where(hasU, mu[:, None] / du - zU + zU / du * dw, torch.zeros_like(w))
+        a_max = primal_step(dw)
+        a_z = torch.minimum(max_step(zL, dzL, hasL, 0.0, tau), max_step(zU, dzU, hasU, 0.0, tau))
+        gd = (gphi * dw).sum(1)
+        switch_ok = (theta_k <= theta_min) & (gd < 0)
 
         # ---- filter line search (IPOPT: gamma_theta 1e-5, gamma_phi 1e-8, delta 1, s_theta 1.1,
         # s_phi 2.3, eta_phi 1e-8, theta_min/max = 1e-4/1e4 max(1, theta_0)), second-order
@@ -654,42 +565,14 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
             st["aug"] = torch.where(mask, aug_mask, st["aug"])
             st["searching"] = st["searching"] & ~mask
 
-        if use_hip:  # the fused kernels of csrc/cpl_ipm.hip (one launch per trial for each)
-            sw_ok = switch_ok.contiguous()
-            ftc, fpc = ft.contiguous(), fp.contiguous()
+        def trial(d, al, mask):
+            wt_ = w + al[:, None] * d
+            return wt_, evaluate_fg(unpack(torch.where(mask[:, None], wt_, st["w"])))
 
-            def trial(d, al, mask):
-                """w_t = w + al d; the evaluation point takes w_t where mask, else the state's w."""
-                wt_ = torch.empty_like(w)
-                Xt = torch.empty(B, n, dtype=dt, device=dev)
-                _abi.check(_abi.lib.cpl_ipm_trial_point(B, n, nf, nw, _ptr(free), _ptr(fixed), _ptr(Xbase), _ptr(w),
-                                                        _ptr(d.contiguous()), _ptr(al.contiguous()),
-                                                        _ptr(mask.contiguous()), _ptr(st["w"]), _ptr(wt_), _ptr(Xt),
-                                                        stream()))
-                return wt_, evaluate_fg(Xt)
-
-            def judge_take(wt_, o_, al, extra=None, mode=0):
-                """IPOPT's acceptance test + take for searching (& extra) instances; (ok, theta).
-                mode 1: the feasibility step's test; mode 2: take unconditionally."""
-                th_ = torch.empty(B, dtype=dt, device=dev)
-                ok_ = torch.empty(B, dtype=torch.bool, device=dev)
-                _abi.check(_abi.lib.cpl_ipm_judge_take(
-                    B, nw, m, nf, FMAX, _ptr(row_slack), _ptr(gl), _ptr(hasL_u8), _ptr(hasU_u8), _ptr(wl0), _ptr(wu0),
-                    _ptr(wt_), _ptr(o_["f"].contiguous()), _ptr(o_["g"].contiguous()), _ptr(al.contiguous()),
-                    _ptr(mu.contiguous()), _ptr(theta_k.contiguous()), _ptr(phi_k.contiguous()), _ptr(gd.contiguous()),
-                    _ptr(sw_ok), _ptr(theta_max), _ptr(ftc), _ptr(fpc), None if extra is None else _ptr(extra.contiguous()),
-                    _ptr(st["searching"]), _ptr(st["f"]), _ptr(st["g"]), _ptr(st["w"]), _ptr(st["alpha"]),
-                    _ptr(st["aug"]), _ptr(th_), _ptr(ok_), mode, stream()))
-                return ok_, th_
-        else:
-            def trial(d, al, mask):
-                wt_ = w + al[:, None] * d
-                return wt_, evaluate_fg(unpack(torch.where(mask[:, None], wt_, st["w"])))
-
-            def judge_take(wt_, o_, al, extra=None):
-                ok_, augm_, th_ = judge(wt_, o_, al)
-                take(st["searching"] & ok_ & (True if extra is None else extra), wt_, o_, al, augm_)
-                return ok_, th_
+        def judge_take(wt_, o_, al, extra=None):
+            ok_, augm_, th_ = judge(wt_, o_, al)
+            take(st["searching"] & ok_ & (True if extra is None else extra), wt_, o_, al, augm_)
+            return ok_, th_
 
         alpha = a_max
         wt, o = w, cur
@@ -716,40 +599,18 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         # violation by 10 %; the multipliers stay.  Otherwise the last trial.  Either way the
         # instance's filter restarts.  (The KKT kernel skips the instances outside the mask.)
         failed = st["searching"].clone()
-        if use_hip:  # persistent zero matrix: only its diagonal changes (no 8 192 x nw x nw fill)
-            Mr_buf.diagonal(dim1=1, dim2=2).copy_(mr_diag)
-            Mr = Mr_buf
-        else:
-            Mr = torch.diag_embed(mr_diag)
+        Mr = torch.diag_embed(mr_diag)
         dwr = kkt(Mr, A, torch.zeros_like(w), -c, mu, zeros_B, failed)[0]
         ar = primal_step(dwr)
         wr, orr = trial(dwr, ar, failed)
-        if use_hip:
-            ok_r, _ = judge_take(wr, orr, zeros_B, failed, mode=1)
-            rest = failed & ok_r
-            judge_take(wt, o, 2.0 * alpha, None, mode=2)
-        else:
-            thr = cons(orr["g"], wr[:, nf:]).abs().sum(1)
-            rest = failed & torch.isfinite(thr) & torch.isfinite(orr["f"]) & (thr <= 0.9 * theta_k)
-            take(rest, wr, orr, zeros_B, torch.zeros_like(failed))
-            take(st["searching"], wt, o, 2.0 * alpha, torch.zeros_like(failed))
+        thr = cons(orr["g"], wr[:, nf:]).abs().sum(1)
+        rest = failed & torch.isfinite(thr) & torch.isfinite(orr["f"]) & (thr <= 0.9 * theta_k)
+        take(rest, wr, orr, zeros_B, torch.zeros_like(failed))
+        take(st["searching"], wt, o, 2.0 * alpha, torch.zeros_like(failed))
         w_new = st["w"]
         al = st["alpha"]
         # the accepted points with their derivatives: one full evaluation (trials carried f and g only)
         new = evaluate(unpack(w_new))
-        if use_hip and not use_bfgs:  # accept + state write-back: one launch, plus masked row copies
-            _abi.check(_abi.lib.cpl_ipm_accept(
-                B, nw, m, FMAX, _ptr(active), _ptr(st["aug"]), _ptr(failed), _ptr(rest), _ptr(al), _ptr(a_z),
-                _ptr(theta_k), _ptr(phi_k), _ptr(ft), _ptr(fp), _ptr(fc), _ptr(w_new), _ptr(dy.contiguous()),
-                _ptr(dzL), _ptr(dzU), _ptr(mu), _ptr(hasL_u8), _ptr(hasU_u8), _ptr(wl0), _ptr(wu0), _ptr(S["w"]),
-                _ptr(S["y"]), _ptr(S["zL"]), _ptr(S["zU"]), _ptr(S["mu"]), _ptr(S["iters"]), _ptr(S["filt_t"]),
-                _ptr(S["filt_p"]), _ptr(S["fcount"]), stream()))
-            for k in ("f", "grad", "g", "J"):
-                _abi.check(_abi.lib.cpl_ipm_masked_rows(B, S[k].numel() // B, _ptr(active), _ptr(new[k].contiguous()),
-                                                        _ptr(S[k]), stream()))
-            if verbose > 1:
-                verbose_line(E, mu, a_max, al, dw, dy, delta_w, cur)
-            return
         a_z = torch.where(rest, zeros_B, a_z)
         addm = st["aug"] & active
         fi = fslot == torch.remainder(fc, FMAX)[:, None]
@@ -818,54 +679,13 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
 
     # ---- drive the iterations
     it_run = 0
-    replay = step
-    per_step_evals = 0
-    if use_graph and max_iter > 0:
-        side = torch.cuda.Stream(device=dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):  # warm-up iteration (executed): per-stream state, allocator pools
-            step()
-        torch.cuda.current_stream(dev).wait_stream(side)
-        it_run = 1
-        e0 = n_eval
-        gr = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(gr):
-            step()
-        per_step_evals = n_eval - e0
-        n_eval = e0
-        replay = gr.replay
-    if use_hip:
-        # termination test without stalling the device: after every iteration "any active" goes to
-        # a pinned host slot behind an event; the host reads the previous iteration's slot (normally
-        # landed already) while the current iteration runs — at most one iteration past the end
-        # (a no-op: every update is masked by the active flags)
-        flag = torch.zeros(2, dtype=torch.bool).pin_memory()
-        evs = [torch.cuda.Event(), torch.cuda.Event()]
-        if not bool(S["active"].any()):
-            max_iter = it_run
-        start = it_run
-        while it_run < max_iter:
-            replay()
-            n_eval += per_step_evals
-            it_run += 1
-            k = it_run & 1
-            flag[k].copy_(S["active"].any(), non_blocking=True)
-            evs[k].record()
-            if verbose:
-                print(f"it {it_run:4d} active {int(S['active'].sum())}")
-            if it_run - start >= 2:  # the previous iteration of this loop recorded its flag
-                evs[k ^ 1].synchronize()
-                if not bool(flag[k ^ 1]):
-                    break
-    else:
-        while it_run < max_iter:
-            if it_run % max(1, check_every) == 0 and not bool(S["active"].any()):
-                break
-            replay()
-            n_eval += per_step_evals
-            it_run += 1
-            if verbose:
-                print(f"it {it_run:4d} active {int(S['active'].sum())}")
+    while it_run < max_iter:
+        if it_run % max(1, check_every) == 0 and not bool(S["active"].any()):
+            break
+        step()
+        it_run += 1
+        if verbose:
+            print(f"it {it_run:4d} active {int(S['active'].sum())}")
     # final convergence test at the last iterate
     check(errors({"f": S["f"], "grad": S["grad"], "g": S["g"], "J": S["J"]}, S["w"], S["y"], S["zL"], S["zU"]))
     # IPOPT honor_original_bounds: the final point is projected back into the unrelaxed bounds and
@@ -876,4 +696,4 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     viol = torch.clamp(torch.maximum(gl - g, g - gu), min=0.0).amax(1) if m else zeros_B
     return BatchSolveResult(x=Xf, y=S["y"], status=S["status"], iterations=S["iters"],
                             objective=fin["f"].clone(), primal_inf=viol, dual_inf=S["d_inf"], evaluations=n_eval,
-                            iterations_run=it_run, graph=use_graph)
+                            iterations_run=it_run, graph=False)

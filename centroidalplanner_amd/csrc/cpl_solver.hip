@@ -1,0 +1,981 @@
+// cpl_solver.hip — the native batched solve engine (C-ABI cpl_solver_*, include/cpl_mi355x.h).
+//
+// Many concurrent CentroidalPlanner solves in lock-step on one GPU: IPOPT's primal-dual
+// interior-point method (Waechter & Biegler 2006) as restated in centroidalplanner_amd/batch_ipm.py
+// — whose host path (CPU tensors, the oracle's callbacks) is the checker of this engine — with every
+// per-instance quantity a row of a device buffer:
+//   * callbacks: cpl_eval_batch(_ex) (values-only Jacobian records), the analytic Lagrangian Hessian
+//     (cpl_lagrangian_hessian) or central differences (cpl_ipm_fd_points + cpl_eval_lagrangian_grad
+//     + cpl_ipm_fd_hessian_raw), or a damped BFGS model (IFOPT's limited-memory default, the
+//     reference's configuration, src/CentroidalPlanner.cpp:22-29);
+//   * per-instance iteration work: cpl_ipm_optimality / newton_setup / post_step / trial_point /
+//     judge_take / accept / max_step / dense_a / masked_rows, the Newton step cpl_kkt_solve;
+//   * the glue between them (the line-search state, second-order corrections, the feasibility step
+//     standing in for the restoration phase, BFGS) in the small kernels below — no framework ops.
+// One iteration (fixed trip counts, masked updates, no host synchronisation) is captured once as a
+// HIP graph and replayed; the host reads an "any instance active" byte one iteration behind.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "cpl_layout.hpp"
+#include "cpl_status.hpp"
+
+namespace cpl {
+namespace {
+
+constexpr int FMAX = 64;          // filter entries kept per instance (a ring), as batch_ipm.FMAX
+constexpr double BIG = 1.0e19;    // |bound| >= 1e19 is infinite (IPOPT nlp_lower/upper_bound_inf)
+constexpr int WPB = 4;            // instances per 256-thread workgroup (one wave each)
+
+#define CK(expr)                      \
+  do {                                \
+    const int32_t st_ = (expr);       \
+    if (st_ != CPL_OK) return st_;    \
+  } while (0)
+
+inline unsigned blocks_for(int64_t batch) { return (unsigned)((batch + WPB - 1) / WPB); }
+inline unsigned blocks_elems(int64_t total) { return (unsigned)((total + 255) / 256); }
+
+__device__ __forceinline__ double wave_sum(double v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  return v;
+}
+
+// IPOPT bound_push = bound_frac = 1e-2 (absolute and relative to the range), batch_ipm.push
+__device__ __forceinline__ double push_into(double v, bool hl, bool hu, double lo, double up) {
+  const double k = 1e-2;
+  const double rng = (hl && hu) ? up - lo : INFINITY;
+  const double pl = fmin(k * fmax(fabs(lo), 1.0), k * rng);
+  const double pu = fmin(k * fmax(fabs(up), 1.0), k * rng);
+  if (hl) v = fmax(v, lo + pl);
+  if (hu) v = fmin(v, up - pu);
+  return v;
+}
+
+// constraint residual of row r: g - g_l (equality), g - s (inequality, slack s)
+__device__ __forceinline__ double cons_row(const double* g, const double* w, int nf, int r, const int32_t* row_slack,
+                                           const double* gl) {
+  const int s = row_slack[r];
+  return s >= 0 ? g[r] - w[nf + s] : g[r] - gl[r];
+}
+
+// Xbase = x0 with the fixed variables at their (equal) bounds
+__global__ void k_xbase(int64_t total, int n, const double* __restrict__ x0, const uint8_t* __restrict__ is_fixed,
+                        const double* __restrict__ xl, double* __restrict__ Xbase) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int j = (int)(e % n);
+  Xbase[e] = is_fixed[j] ? xl[j] : x0[e];
+}
+
+// the starting point's x: the free variables pushed into their bounds (batch_ipm: Xs)
+__global__ void k_start_x(int64_t total, int n, const int32_t* __restrict__ freepos, const double* __restrict__ Xbase,
+                          const uint8_t* __restrict__ hasL, const uint8_t* __restrict__ hasU,
+                          const double* __restrict__ wl0, const double* __restrict__ wu0, double* __restrict__ X) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int j = (int)(e % n);
+  const int k = freepos[j];
+  X[e] = k >= 0 ? push_into(Xbase[e], hasL[k], hasU[k], wl0[k], wu0[k]) : Xbase[e];
+}
+
+// the starting state of every instance (one wave each): w0 = push([x_free, g_I]), bound multipliers
+// 1, theta_0 and the filter's theta_max / theta_min, mu, flags; gw0 and the least-squares system's
+// right-hand side r1 = -(gw0 - zL0 + zU0) (the multiplier estimate is one KKT solve with M = I)
+__global__ __launch_bounds__(256) void k_init_state(
+    int64_t B, int n, int m, int nf, int nw, const int32_t* __restrict__ free_idx, const int32_t* __restrict__ ineq_row,
+    const int32_t* __restrict__ row_slack, const double* __restrict__ gl, const uint8_t* __restrict__ hasL,
+    const uint8_t* __restrict__ hasU, const double* __restrict__ wl0, const double* __restrict__ wu0, double mu_init,
+    const double* __restrict__ X, const double* __restrict__ g, const double* __restrict__ grad,
+    double* __restrict__ w, double* __restrict__ zL, double* __restrict__ zU, double* __restrict__ theta_max,
+    double* __restrict__ theta_min, double* __restrict__ mu, uint8_t* __restrict__ active,
+    int64_t* __restrict__ status, int64_t* __restrict__ iters, int64_t* __restrict__ acc, double* __restrict__ filt_t,
+    double* __restrict__ filt_p, int64_t* __restrict__ fcount, double* __restrict__ dwl, double* __restrict__ d_inf,
+    uint8_t* __restrict__ hq_init, double* __restrict__ r1, double* __restrict__ r2, double* __restrict__ M) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  double* wb = w + b * nw;
+  for (int k = lane; k < nw; k += 64) {
+    const double v = k < nf ? X[b * n + free_idx[k]] : g[b * m + ineq_row[k - nf]];
+    const bool hl = hasL[k], hu = hasU[k];
+    wb[k] = push_into(v, hl, hu, wl0[k], wu0[k]);
+    const double zl = hl ? 1.0 : 0.0, zu = hu ? 1.0 : 0.0;
+    zL[b * nw + k] = zl;
+    zU[b * nw + k] = zu;
+    const double gw = k < nf ? grad[b * n + free_idx[k]] : 0.0;
+    r1[b * nw + k] = -((gw - zl) + zu);
+    for (int j = 0; j < nw; ++j) M[(b * nw + k) * nw + j] = j == k ? 1.0 : 0.0;
+  }
+  double th = 0.0;
+  for (int r = lane; r < m; r += 64) {  // (the slack recomputed: this lane did not write it)
+    const int sl = row_slack[r];
+    const double gv = g[b * m + r];
+    const double c = sl >= 0 ? gv - push_into(gv, hasL[nf + sl], hasU[nf + sl], wl0[nf + sl], wu0[nf + sl]) : gv - gl[r];
+    th += fabs(c);
+    r2[b * m + r] = 0.0;
+  }
+  th = wave_sum(th);
+  for (int k = lane; k < FMAX; k += 64) {
+    filt_t[b * FMAX + k] = INFINITY;
+    filt_p[b * FMAX + k] = INFINITY;
+  }
+  if (lane == 0) {
+    theta_max[b] = 1e4 * fmax(th, 1.0);
+    theta_min[b] = 1e-4 * fmax(th, 1.0);
+    mu[b] = mu_init;
+    active[b] = 1;
+    status[b] = CPL_SOLVE_MAX_ITER;
+    iters[b] = 0;
+    acc[b] = 0;
+    fcount[b] = 0;
+    dwl[b] = 0.0;
+    d_inf[b] = 0.0;
+    hq_init[b] = 0;
+  }
+}
+
+// least-squares multipliers: kept when |y|max <= 1e3 (IPOPT constr_mult_init_max) and the solve succeeded
+__global__ __launch_bounds__(256) void k_y0(int64_t B, int m, const double* __restrict__ dy, const int32_t* __restrict__ info,
+                                            double* __restrict__ y) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  double mx = 0.0;
+  for (int r = lane; r < m; r += 64) mx = fmax(mx, fabs(dy[b * m + r]));
+  mx = wave_max(mx);
+  const bool keep = mx <= 1e3 && info[b] == 0;
+  for (int r = lane; r < m; r += 64) y[b * m + r] = keep ? dy[b * m + r] : 0.0;
+}
+
+// gradient over w (gw = [grad f over the free variables, 0]) and the constraint residual c
+__global__ __launch_bounds__(256) void k_prep(int64_t B, int n, int m, int nf, int nw, const int32_t* __restrict__ free_idx,
+                                              const int32_t* __restrict__ row_slack, const double* __restrict__ gl,
+                                              const double* __restrict__ grad, const double* __restrict__ g,
+                                              const double* __restrict__ w, double* __restrict__ gradw,
+                                              double* __restrict__ c) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  for (int k = lane; k < nw; k += 64) gradw[b * nw + k] = k < nf ? grad[b * n + free_idx[k]] : 0.0;
+  if (c)
+    for (int r = lane; r < m; r += 64) c[b * m + r] = cons_row(g + b * m, w + b * nw, nf, r, row_slack, gl);
+}
+
+// after the optimality kernel: tau = max(0.99, 1 - mu), the iteration's active snapshot, and the
+// evaluation point X = unpack(w) for the Hessian
+__global__ void k_unpack_tau(int64_t total, int n, int nw, const int32_t* __restrict__ freepos,
+                             const double* __restrict__ Xbase, const double* __restrict__ w,
+                             const double* __restrict__ mu, const uint8_t* __restrict__ active,
+                             double* __restrict__ X, double* __restrict__ tau, uint8_t* __restrict__ act) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int64_t b = e / n;
+  const int j = (int)(e - b * n);
+  const int k = freepos[j];
+  X[e] = k >= 0 ? w[b * nw + k] : Xbase[e];
+  if (j == 0) {
+    tau[b] = fmax(1.0 - mu[b], 0.99);
+    act[b] = active[b];
+  }
+}
+
+// X = unpack(w) (optionally clamped into [xl, xu]: IPOPT honor_original_bounds)
+__global__ void k_unpack(int64_t total, int n, int nw, const int32_t* __restrict__ freepos,
+                         const double* __restrict__ Xbase, const double* __restrict__ w, const double* __restrict__ xl,
+                         const double* __restrict__ xu, double* __restrict__ X) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int64_t b = e / n;
+  const int j = (int)(e - b * n);
+  const int k = freepos[j];
+  double v = k >= 0 ? w[b * nw + k] : Xbase[e];
+  if (xl) v = fmin(fmax(v, xl[j]), xu[j]);
+  X[e] = v;
+}
+
+// line-search state at the current iterate, the first trial step = the fraction-to-the-boundary one
+__global__ __launch_bounds__(256) void k_ls_init(int64_t B, int m, int nw, const uint8_t* __restrict__ act,
+                                                 const double* __restrict__ f, const double* __restrict__ g,
+                                                 const double* __restrict__ w, const double* __restrict__ a_max,
+                                                 uint8_t* __restrict__ searching, double* __restrict__ st_f,
+                                                 double* __restrict__ st_g, double* __restrict__ st_w,
+                                                 double* __restrict__ st_alpha, uint8_t* __restrict__ st_aug,
+                                                 double* __restrict__ alpha) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  for (int r = lane; r < m; r += 64) st_g[b * m + r] = g[b * m + r];
+  for (int k = lane; k < nw; k += 64) st_w[b * nw + k] = w[b * nw + k];
+  if (lane == 0) {
+    searching[b] = act[b];
+    st_f[b] = f[b];
+    st_alpha[b] = 0.0;
+    st_aug[b] = 0;
+    alpha[b] = a_max[b];
+  }
+}
+
+// second-order correction bookkeeping (batch_ipm step(): soc, c_soc, a_soc, th_old)
+__global__ __launch_bounds__(256) void k_soc_begin(int64_t B, int m, const uint8_t* __restrict__ searching,
+                                                   const double* __restrict__ th, const double* __restrict__ theta_k,
+                                                   const double* __restrict__ c, const double* __restrict__ alpha,
+                                                   uint8_t* __restrict__ soc, double* __restrict__ c_soc,
+                                                   double* __restrict__ a_soc, double* __restrict__ th_old) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  for (int r = lane; r < m; r += 64) c_soc[b * m + r] = c[b * m + r];
+  if (lane == 0) {
+    soc[b] = searching[b] && th[b] >= theta_k[b];
+    a_soc[b] = alpha[b];
+    th_old[b] = theta_k[b];
+  }
+}
+
+// c_soc = a_soc c_soc + c(trial point); the correction's right-hand side r2 = -c_soc
+__global__ __launch_bounds__(256) void k_soc_rhs(int64_t B, int m, int nf, int nw, const int32_t* __restrict__ row_slack,
+                                                 const double* __restrict__ gl, const double* __restrict__ g_t,
+                                                 const double* __restrict__ w_t, const double* __restrict__ a_soc,
+                                                 double* __restrict__ c_soc, double* __restrict__ r2) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  const double a = a_soc[b];
+  for (int r = lane; r < m; r += 64) {
+    const double ct = cons_row(g_t + b * m, w_t + b * nw, nf, r, row_slack, gl);
+    const double v = a * c_soc[b * m + r] + ct;
+    c_soc[b * m + r] = v;
+    r2[b * m + r] = -v;
+  }
+}
+
+__global__ void k_soc_after(int64_t B, uint8_t* __restrict__ soc, const uint8_t* __restrict__ ok,
+                            const double* __restrict__ th, double* __restrict__ th_old) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  soc[b] = soc[b] && !ok[b] && th[b] <= 0.99 * th_old[b];  // kappa_soc = 0.99
+  th_old[b] = th[b];
+}
+
+__global__ void k_halve(int64_t B, const uint8_t* __restrict__ searching, double* __restrict__ alpha) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  if (searching[b]) alpha[b] = 0.5 * alpha[b];
+}
+
+// the feasibility step's system: failed = still searching; Mr = diag(mr_diag) (its zero off-diagonal
+// part set once); r2 = -c
+__global__ __launch_bounds__(256) void k_feas_prep(int64_t B, int m, int nw, const uint8_t* __restrict__ searching,
+                                                   const double* __restrict__ mr_diag, const double* __restrict__ c,
+                                                   uint8_t* __restrict__ failed, double* __restrict__ Mr,
+                                                   double* __restrict__ negc) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  for (int k = lane; k < nw; k += 64) Mr[(b * nw + k) * nw + k] = mr_diag[b * nw + k];
+  for (int r = lane; r < m; r += 64) negc[b * m + r] = -c[b * m + r];
+  if (lane == 0) failed[b] = searching[b];
+}
+
+__global__ void k_rest(int64_t B, const uint8_t* __restrict__ failed, const uint8_t* __restrict__ ok_r,
+                       const double* __restrict__ alpha, uint8_t* __restrict__ rest, double* __restrict__ alpha2) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  rest[b] = failed[b] && ok_r[b];
+  alpha2[b] = 2.0 * alpha[b];
+}
+
+// damped BFGS update of the model over x_free (batch_ipm step(), use_bfgs), one workgroup per
+// active instance: s = dw_free, y_k = grad_w L(w_new, y_new) - grad_w L(w, y_new) (the Jacobian
+// parts from A = [J_free | -P] at both points), first update scaled like IPOPT's s'y / s's, Powell
+// damping (theta = 0.8 s'Hs / (s'Hs - s'y) when s'y < 0.2 s'Hs), symmetrised.
+__global__ __launch_bounds__(256) void k_bfgs(int64_t B, int m, int nf, int nw, const uint8_t* __restrict__ act,
+                                              const double* __restrict__ w_old, const double* __restrict__ w_new,
+                                              const double* __restrict__ y, const double* __restrict__ dy,
+                                              const double* __restrict__ alpha, const double* __restrict__ gw_old,
+                                              const double* __restrict__ A_old, const double* __restrict__ gw_new,
+                                              const double* __restrict__ A_new, double* __restrict__ Hq,
+                                              uint8_t* __restrict__ hq_init) {
+  const int64_t b = blockIdx.x;
+  if (b >= B || !act[b]) return;
+  __shared__ double s_k[128], y_k[128], Hs[128], rv[128], yn[256], red[8];
+  const int tid = threadIdx.x;
+  const double al = alpha[b];
+  for (int r = tid; r < m; r += blockDim.x) yn[r] = y[b * m + r] + al * dy[b * m + r];
+  __syncthreads();
+  for (int k = tid; k < nf; k += blockDim.x) {
+    double jn = 0.0, jo = 0.0;
+    for (int r = 0; r < m; ++r) {
+      jn += A_new[(b * m + r) * nw + k] * yn[r];
+      jo += A_old[(b * m + r) * nw + k] * yn[r];
+    }
+    s_k[k] = w_new[b * nw + k] - w_old[b * nw + k];
+    y_k[k] = (gw_new[b * nw + k] + jn) - (gw_old[b * nw + k] + jo);
+  }
+  __syncthreads();
+  auto block_dot = [&](const double* a, const double* c) {
+    double v = 0.0;
+    for (int k = tid; k < nf; k += blockDim.x) v += a[k] * c[k];
+    v = wave_sum(v);
+    __syncthreads();
+    if ((tid & 63) == 0) red[tid >> 6] = v;
+    __syncthreads();
+    double t = 0.0;
+    for (int q = 0; q < (int)(blockDim.x >> 6); ++q) t += red[q];
+    return t;
+  };
+  const double sy = block_dot(s_k, y_k);
+  const double ss = block_dot(s_k, s_k);
+  double* H = Hq + b * (int64_t)nf * nf;
+  if (!hq_init[b] && sy > 0.0 && ss > 0.0) {
+    const double sigma0 = sy / ss;
+    for (int e = tid; e < nf * nf; e += blockDim.x) H[e] = (e / nf == e % nf) ? sigma0 : 0.0;
+    __syncthreads();
+    if (tid == 0) hq_init[b] = 1;
+  }
+  __syncthreads();
+  for (int i = tid; i < nf; i += blockDim.x) {
+    double v = 0.0;
+    for (int j = 0; j < nf; ++j) v += H[i * nf + j] * s_k[j];
+    Hs[i] = v;
+  }
+  __syncthreads();
+  const double sHs = block_dot(s_k, Hs);
+  const double theta = sy >= 0.2 * sHs ? 1.0 : 0.8 * sHs / ((sHs - sy) != 0.0 ? (sHs - sy) : 1.0);
+  for (int k = tid; k < nf; k += blockDim.x) rv[k] = theta * y_k[k] + (1.0 - theta) * Hs[k];
+  __syncthreads();
+  const double sr = block_dot(s_k, rv);
+  if (!(ss > 1e-30 && sHs > 0.0 && sr > 0.0)) return;  // (uniform)
+  // Hn = H - Hs Hs^T / sHs + r r^T / sr, symmetrised: H <- (Hn + Hn^T) / 2, written in place by
+  // (i <= j) pairs so each pair reads both old entries before writing them
+  for (int e = tid; e < nf * nf; e += blockDim.x) {
+    const int i = e / nf, j = e - i * nf;
+    if (j < i) continue;
+    const double hij = H[i * nf + j] - Hs[i] * Hs[j] / sHs + rv[i] * rv[j] / sr;
+    const double hji = H[j * nf + i] - Hs[j] * Hs[i] / sHs + rv[j] * rv[i] / sr;
+    const double v = 0.5 * (hij + hji);
+    H[i * nf + j] = v;
+    H[j * nf + i] = v;
+  }
+}
+
+// "any instance still active" into one byte (read by the host one iteration behind)
+__global__ __launch_bounds__(256) void k_any(int64_t B, const uint8_t* __restrict__ active, uint8_t* __restrict__ out) {
+  __shared__ int s_any;
+  if (threadIdx.x == 0) s_any = 0;
+  __syncthreads();
+  int a = 0;
+  for (int64_t b = threadIdx.x; b < B; b += blockDim.x) a |= active[b] ? 1 : 0;
+  if (a) s_any = 1;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = (uint8_t)s_any;
+}
+
+// results: max violation of g against its bounds, int32 copies of status / iterations
+__global__ __launch_bounds__(256) void k_final(int64_t B, int m, const double* __restrict__ g, const double* __restrict__ gl,
+                                               const double* __restrict__ gu, const int64_t* __restrict__ status,
+                                               const int64_t* __restrict__ iters, double* __restrict__ pinf,
+                                               int32_t* __restrict__ st32, int32_t* __restrict__ it32) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  double v = 0.0;
+  for (int r = lane; r < m; r += 64) {
+    const double gv = g[b * m + r];
+    v = fmax(v, fmax(fmax(gl[r] - gv, gv - gu[r]), 0.0));
+    if (gv != gv) v = INFINITY;
+  }
+  v = wave_max(v);
+  if (lane == 0) {
+    if (pinf) pinf[b] = v;
+    if (st32) st32[b] = (int32_t)status[b];
+    if (it32) it32[b] = (int32_t)iters[b];
+  }
+}
+
+__global__ void k_eye(int64_t total, int nf, double* __restrict__ H) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int q = (int)(e % ((int64_t)nf * nf));
+  H[e] = (q / nf == q % nf) ? 1.0 : 0.0;
+}
+
+__global__ void k_repeat(int64_t B, int rep, const double* __restrict__ src, double* __restrict__ dst,
+                         const uint8_t* __restrict__ tsrc, uint8_t* __restrict__ tdst) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B * rep) return;
+  if (src) dst[e] = src[e / rep];
+  if (tsrc) tdst[e] = tsrc[e / rep];
+}
+
+// ------------------------------------------------------------------------------------------
+struct Arena {
+  char* base = nullptr;
+  size_t cap = 0, used = 0;
+  template <typename T>
+  T* take(size_t count) {
+    const size_t bytes = ((count ? count : 1) * sizeof(T) + 255) & ~size_t(255);
+    T* p = reinterpret_cast<T*>(base + used);
+    used += bytes;
+    return p;
+  }
+};
+
+}  // namespace
+}  // namespace cpl
+
+struct cpl_solver {
+  cpl_problem_desc desc;
+  cpl_solve_options opt;
+  int64_t B = 0;
+  int n = 0, m = 0, nnz = 0, nnz_rec = 0, nf = 0, nI = 0, nw = 0, nbounds = 0;
+  bool analytic_H = false, bfgs = false, fd = false, fd_fused = true;
+  hipStream_t stream = nullptr;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  uint8_t* h_flag = nullptr;  // pinned, 2 bytes
+  cpl::Arena arena;
+  const double* mass = nullptr;       // per solve
+  const uint8_t* tag = nullptr;
+  int64_t evals_per_step = 0;
+  // problem constants (device)
+  int32_t *free32, *ineq_row, *row_slack, *freepos, *amap, *col_ptr, *csc_k, *csc_row;
+  int64_t *free64, *fixed64;
+  uint8_t *is_fixed, *hasL, *hasU;
+  double *xl, *xu, *gl, *gu, *wl0, *wu0, *zeros_w, *zeros_B;
+  // state
+  double *Xbase, *w, *y, *zL, *zU, *mu, *filt_t, *filt_p, *dwl, *f, *grad, *g, *J, *d_inf, *Hq, *theta_max, *theta_min;
+  int64_t *status, *iters, *acc, *fcount;
+  uint8_t *active, *hq_init, *d_any;
+  // iteration temporaries
+  double *A, *A_new, *gradw, *gradw_new, *c, *err0, *base, *mu_o, *ft, *fp, *tau, *X, *H, *M, *Mr, *r1, *r2, *gphi,
+      *mr_diag, *theta_k, *phi_k, *dw, *dy, *delta_w, *delta_c, *dzL, *dzU, *a_max, *a_z, *gd, *ws;
+  int64_t* fc;
+  int32_t* info;
+  uint8_t *act, *switch_ok, *searching, *st_aug, *ok, *soc, *ok_s, *failed, *ok_r, *rest;
+  double *st_f, *st_g, *st_w, *st_alpha, *alpha, *alpha2, *th, *wt, *Xt, *f_t, *g_t;
+  double *c_soc, *a_soc, *th_old, *r2s, *dws, *dys, *ws_, *Xs, *f_s, *g_s, *th_s;
+  double *negc, *dwr, *dyr, *dwr_d, *dcr, *ar, *wr, *Xr, *f_r, *g_r, *th_r;
+  int32_t* infor;
+  double *Xn, *f_n, *grad_n, *g_n, *J_n, *Xp, *hfd, *gL, *mass_fd, *jac_fd, *grad_fd;
+  uint8_t* tag_fd;
+  double *fin_f, *fin_g;
+  int32_t *st32, *it32;
+};
+
+namespace cpl {
+namespace {
+
+int32_t hip_err(hipError_t e, const char* what) {
+  return fail(CPL_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+#define HK(expr, what)                                   \
+  do {                                                   \
+    hipError_t e_ = (expr);                              \
+    if (e_ != hipSuccess) return hip_err(e_, what);      \
+  } while (0)
+#define LAUNCHED(what) HK(hipGetLastError(), what)
+
+int32_t eval_fg(cpl_solver* S, const double* X, double* fo, double* go) {
+  return cpl_eval_batch(&S->desc, S->B, X, S->mass, S->tag, go, nullptr, fo, nullptr, S->stream);
+}
+int32_t eval_full(cpl_solver* S, const double* X, double* fo, double* grado, double* go, double* jo) {
+  return cpl_eval_batch_ex(&S->desc, S->B, X, S->mass, S->tag, go, jo, fo, grado, nullptr, CPL_EVAL_JAC_FOLDED,
+                           S->stream);
+}
+
+// one lock-step iteration of every instance (graph-capturable: no host synchronisation)
+int32_t step(cpl_solver* S) {
+  const int64_t B = S->B;
+  const int n = S->n, m = S->m, nf = S->nf, nw = S->nw;
+  hipStream_t st = S->stream;
+  const cpl_solve_options& o = S->opt;
+  // optimality error, convergence test, barrier update (filters reset where mu changed)
+  CK(cpl_ipm_dense_a(B, m, nw, nf, S->nnz_rec, S->amap, S->row_slack, S->J, S->A, S->active, st));
+  hipLaunchKernelGGL(k_prep, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->free32, S->row_slack, S->gl,
+                     S->grad, S->g, S->w, S->gradw, S->c);
+  LAUNCHED("k_prep");
+  CK(cpl_ipm_optimality(B, nw, m, FMAX, S->nbounds, o.tol, o.acceptable_tol, o.acceptable_iter, S->A, S->gradw, S->c,
+                        S->w, S->y, S->zL, S->zU, S->hasL, S->hasU, S->wl0, S->wu0, S->mu, S->filt_t, S->filt_p,
+                        S->fcount, S->active, S->status, S->acc, S->d_inf, S->err0, S->base, S->mu_o, S->ft, S->fp,
+                        S->fc, st));
+  hipLaunchKernelGGL(k_unpack_tau, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, nw, S->freepos, S->Xbase,
+                     S->w, S->mu_o, S->active, S->X, S->tau, S->act);
+  LAUNCHED("k_unpack_tau");
+  // Hessian of the Lagrangian over x_free
+  const double* Hblk = nullptr;
+  int h_sym = 0;
+  if (S->bfgs) {
+    Hblk = S->Hq;
+  } else if (S->analytic_H) {
+    CK(cpl_lagrangian_hessian(&S->desc, B, S->X, S->y, S->act, S->free32, nf, S->H, st));
+    Hblk = S->H;
+  } else {  // central differences of grad f + J^T y (the 2 nf points of every instance in one launch)
+    CK(cpl_ipm_fd_points(B, n, nf, o.fd_step, S->freepos, S->X, S->Xp, S->hfd, S->act, st));
+    int32_t rc = CPL_ERR_UNSUPPORTED;
+    if (S->fd_fused)
+      rc = cpl_eval_lagrangian_grad(&S->desc, B * 2 * nf, S->Xp, S->mass ? S->mass_fd : nullptr,
+                                    S->tag ? S->tag_fd : nullptr, S->col_ptr, S->csc_k, S->csc_row, S->y, 2 * nf,
+                                    S->act, S->gL, st);
+    if (rc == CPL_ERR_UNSUPPORTED) {  // Superquadric / mixed: eval + J^T y in two launches
+      S->fd_fused = false;
+      CK(cpl_eval_batch(&S->desc, B * 2 * nf, S->Xp, S->mass ? S->mass_fd : nullptr, S->tag ? S->tag_fd : nullptr,
+                        nullptr, S->jac_fd, nullptr, S->grad_fd, st));
+      CK(cpl_lagrangian_grad(B * 2 * nf, n, m, S->nnz, S->col_ptr, S->csc_k, S->csc_row, S->grad_fd, S->jac_fd, S->y,
+                             2 * nf, S->gL, st));
+    } else {
+      CK(rc);
+    }
+    CK(cpl_ipm_fd_hessian_raw(B, n, nf, S->free64, S->gL, S->hfd, S->H, S->act, st));
+    Hblk = S->H;
+    h_sym = 1;
+  }
+  // Newton system, step, multiplier steps, fraction-to-the-boundary steps
+  CK(cpl_ipm_newton_setup(B, nw, m, nf, S->w, S->zL, S->zU, S->gradw, S->A, S->y, S->c, S->f, S->mu_o, S->hasL,
+                          S->hasU, S->wl0, S->wu0, Hblk, h_sym, S->M, S->r1, S->r2, S->gphi, S->mr_diag, S->theta_k,
+                          S->phi_k, S->bfgs ? nullptr : S->act, st));
+  CK(cpl_kkt_solve(0, B, nw, m, S->M, S->A, S->r1, S->r2, S->mu_o, S->dwl, S->act, S->dw, S->dy, S->delta_w,
+                   S->delta_c, S->info, S->ws, st));
+  CK(cpl_ipm_post_step(B, nw, S->w, S->dw, S->zL, S->zU, S->gphi, S->mu_o, S->tau, S->hasL, S->hasU, S->wl0, S->wu0,
+                       S->theta_k, S->theta_min, S->act, S->delta_w, S->dwl, S->dzL, S->dzU, S->a_max, S->a_z, S->gd,
+                       S->switch_ok, st));
+  // filter line search with a second-order correction on the first trial
+  hipLaunchKernelGGL(k_ls_init, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nw, S->act, S->f, S->g, S->w, S->a_max,
+                     S->searching, S->st_f, S->st_g, S->st_w, S->st_alpha, S->st_aug, S->alpha);
+  LAUNCHED("k_ls_init");
+  auto judge = [&](const double* wt, const double* ft_, const double* gt_, const double* al, const uint8_t* extra,
+                   double* th, uint8_t* ok, int mode) {
+    return cpl_ipm_judge_take(B, nw, m, nf, FMAX, S->row_slack, S->gl, S->hasL, S->hasU, S->wl0, S->wu0, wt, ft_, gt_,
+                              al, S->mu_o, S->theta_k, S->phi_k, S->gd, S->switch_ok, S->theta_max, S->ft, S->fp,
+                              extra, S->searching, S->st_f, S->st_g, S->st_w, S->st_alpha, S->st_aug, th, ok, mode,
+                              st);
+  };
+  for (int ls = 0; ls < (o.max_ls > 0 ? o.max_ls : 1); ++ls) {
+    CK(cpl_ipm_trial_point(B, n, nf, nw, S->free64, S->fixed64, S->Xbase, S->w, S->dw, S->alpha, S->searching,
+                           S->st_w, S->wt, S->Xt, st));
+    CK(eval_fg(S, S->Xt, S->f_t, S->g_t));
+    CK(judge(S->wt, S->f_t, S->g_t, S->alpha, nullptr, S->th, S->ok, 0));
+    if (ls == 0 && o.max_soc > 0) {
+      hipLaunchKernelGGL(k_soc_begin, dim3(blocks_for(B)), dim3(256), 0, st, B, m, S->searching, S->th, S->theta_k,
+                         S->c, S->alpha, S->soc, S->c_soc, S->a_soc, S->th_old);
+      LAUNCHED("k_soc_begin");
+      const double *cg = S->g_t, *cw = S->wt;
+      for (int q = 0; q < o.max_soc; ++q) {
+        hipLaunchKernelGGL(k_soc_rhs, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nf, nw, S->row_slack, S->gl, cg, cw,
+                           S->a_soc, S->c_soc, S->r2s);
+        LAUNCHED("k_soc_rhs");
+        CK(cpl_kkt_solve(1, B, nw, m, S->M, S->A, S->r1, S->r2s, nullptr, nullptr, S->soc, S->dws, S->dys, nullptr,
+                         nullptr, nullptr, S->ws, st));
+        CK(cpl_ipm_max_step(B, nw, S->w, S->dws, nullptr, nullptr, S->hasL, S->hasU, S->wl0, S->wu0, S->tau, S->a_soc,
+                            st));
+        CK(cpl_ipm_trial_point(B, n, nf, nw, S->free64, S->fixed64, S->Xbase, S->w, S->dws, S->a_soc, S->soc, S->st_w,
+                               S->ws_, S->Xs, st));
+        CK(eval_fg(S, S->Xs, S->f_s, S->g_s));
+        CK(judge(S->ws_, S->f_s, S->g_s, S->alpha, S->soc, S->th_s, S->ok_s, 0));
+        hipLaunchKernelGGL(k_soc_after, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->soc, S->ok_s, S->th_s,
+                           S->th_old);
+        LAUNCHED("k_soc_after");
+        cg = S->g_s;
+        cw = S->ws_;
+      }
+    }
+    hipLaunchKernelGGL(k_halve, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->searching, S->alpha);
+    LAUNCHED("k_halve");
+  }
+  // no acceptable trial: the feasibility step (min 1/2 dw^T (Sigma + sqrt(mu) D_R^2) dw s.t. A dw = -c)
+  // stands in for IPOPT's restoration phase, taken when it cuts the violation by 10 %; else the last trial
+  hipLaunchKernelGGL(k_feas_prep, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nw, S->searching, S->mr_diag, S->c,
+                     S->failed, S->Mr, S->negc);
+  LAUNCHED("k_feas_prep");
+  CK(cpl_kkt_solve(0, B, nw, m, S->Mr, S->A, S->zeros_w, S->negc, S->mu_o, S->zeros_B, S->failed, S->dwr, S->dyr,
+                   S->dwr_d, S->dcr, S->infor, S->ws, st));
+  CK(cpl_ipm_max_step(B, nw, S->w, S->dwr, nullptr, nullptr, S->hasL, S->hasU, S->wl0, S->wu0, S->tau, S->ar, st));
+  CK(cpl_ipm_trial_point(B, n, nf, nw, S->free64, S->fixed64, S->Xbase, S->w, S->dwr, S->ar, S->failed, S->st_w, S->wr,
+                         S->Xr, st));
+  CK(eval_fg(S, S->Xr, S->f_r, S->g_r));
+  CK(judge(S->wr, S->f_r, S->g_r, S->zeros_B, S->failed, S->th_r, S->ok_r, 1));
+  hipLaunchKernelGGL(k_rest, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->failed, S->ok_r, S->alpha, S->rest,
+                     S->alpha2);
+  LAUNCHED("k_rest");
+  CK(judge(S->wt, S->f_t, S->g_t, S->alpha2, nullptr, S->th, S->ok, 2));
+  // the accepted points with their derivatives: one full evaluation
+  hipLaunchKernelGGL(k_unpack, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, nw, S->freepos, S->Xbase,
+                     S->st_w, nullptr, nullptr, S->Xn);
+  LAUNCHED("k_unpack");
+  CK(eval_full(S, S->Xn, S->f_n, S->grad_n, S->g_n, S->J_n));
+  if (S->bfgs) {
+    CK(cpl_ipm_dense_a(B, m, nw, nf, S->nnz_rec, S->amap, S->row_slack, S->J_n, S->A_new, S->act, st));
+    hipLaunchKernelGGL(k_prep, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->free32, S->row_slack, S->gl,
+                       S->grad_n, S->g_n, S->st_w, S->gradw_new, nullptr);
+    LAUNCHED("k_prep (new)");
+    hipLaunchKernelGGL(k_bfgs, dim3((unsigned)B), dim3(256), 0, st, B, m, nf, nw, S->act, S->w, S->st_w, S->y, S->dy,
+                       S->st_alpha, S->gradw, S->A, S->gradw_new, S->A_new, S->Hq, S->hq_init);
+    LAUNCHED("k_bfgs");
+  }
+  CK(cpl_ipm_accept(B, nw, m, FMAX, S->act, S->st_aug, S->failed, S->rest, S->st_alpha, S->a_z, S->theta_k, S->phi_k,
+                    S->ft, S->fp, S->fc, S->st_w, S->dy, S->dzL, S->dzU, S->mu_o, S->hasL, S->hasU, S->wl0, S->wu0,
+                    S->w, S->y, S->zL, S->zU, S->mu, S->iters, S->filt_t, S->filt_p, S->fcount, st));
+  CK(cpl_ipm_masked_rows(B, 1, S->act, S->f_n, S->f, st));
+  CK(cpl_ipm_masked_rows(B, n, S->act, S->grad_n, S->grad, st));
+  CK(cpl_ipm_masked_rows(B, m, S->act, S->g_n, S->g, st));
+  CK(cpl_ipm_masked_rows(B, S->nnz_rec, S->act, S->J_n, S->J, st));
+  hipLaunchKernelGGL(k_any, dim3(1), dim3(256), 0, st, B, S->active, S->d_any);
+  LAUNCHED("k_any");
+  return CPL_OK;
+}
+
+}  // namespace
+}  // namespace cpl
+
+using namespace cpl;
+
+extern "C" {
+
+void cpl_solve_options_default(cpl_solve_options* o) {
+  if (!o) return;
+  std::memset(o, 0, sizeof(*o));
+  o->max_iter = 3000;
+  o->hessian = CPL_HESSIAN_EXACT;
+  o->max_ls = 4;
+  o->max_soc = 1;
+  o->acceptable_iter = 15;
+  o->use_graph = 1;
+  o->tol = 1e-8;
+  o->acceptable_tol = 1e-6;
+  o->mu_init = 0.1;
+  o->fd_step = 1e-6;
+}
+
+int32_t cpl_solver_destroy(cpl_solver* S) {
+  if (!S) return CPL_OK;
+  if (S->gexec) (void)hipGraphExecDestroy(S->gexec);
+  if (S->graph) (void)hipGraphDestroy(S->graph);
+  for (auto& e : S->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (S->h_flag) (void)hipHostFree(S->h_flag);
+  if (S->arena.base) (void)hipFree(S->arena.base);
+  if (S->stream) (void)hipStreamDestroy(S->stream);
+  delete S;
+  return CPL_OK;
+}
+
+int32_t cpl_solver_dims(const cpl_solver* S, int32_t* nf, int32_t* n_ineq, int32_t* graph_captured) {
+  if (!S) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_solver_dims: null solver");
+  if (nf) *nf = S->nf;
+  if (n_ineq) *n_ineq = S->nI;
+  if (graph_captured) *graph_captured = S->gexec != nullptr;
+  return CPL_OK;
+}
+
+int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_solve_options* o, cpl_solver** out) {
+  if (!out) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_solver_create: null output");
+  *out = nullptr;
+  int32_t st = validate_desc(d);
+  if (st) return st;
+  if (batch < 1 || batch > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_solver_create: bad batch");
+  cpl_solve_options opt;
+  cpl_solve_options_default(&opt);
+  if (o) opt = *o;
+  if (opt.hessian < CPL_HESSIAN_EXACT || opt.hessian > CPL_HESSIAN_FD || opt.max_iter < 0 || opt.max_soc < 0 ||
+      opt.max_ls < 0 || !(opt.tol > 0.0))
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_solver_create: bad options");
+  int32_t n, m, nnz;
+  CK(cpl_dims(d, &n, &m, &nnz));
+  std::vector<int32_t> iRow(nnz), jCol(nnz);
+  CK(cpl_structure(d, iRow.data(), jCol.data(), nullptr));
+  std::vector<double> xl(n), xu(n), gl(m), gu(m);
+  CK(cpl_bounds(d, xl.data(), xu.data(), gl.data(), gu.data()));
+  // free / fixed variables (IPOPT fixed_variable_treatment = make_parameter), inequality rows
+  std::vector<int32_t> free_idx, fixed_idx, freepos(n, -1), ineq, row_slack(m, -1);
+  std::vector<uint8_t> is_fixed(n, 0);
+  for (int j = 0; j < n; ++j) {
+    if (std::fabs(xu[j] - xl[j]) <= 1e-14 * std::fmax(1.0, std::fabs(xl[j]))) {
+      is_fixed[j] = 1;
+      fixed_idx.push_back(j);
+    } else {
+      freepos[j] = (int32_t)free_idx.size();
+      free_idx.push_back(j);
+    }
+  }
+  for (int r = 0; r < m; ++r)
+    if (gl[r] != gu[r]) {
+      row_slack[r] = (int32_t)ineq.size();
+      ineq.push_back(r);
+    }
+  const int nf = (int)free_idx.size(), nI = (int)ineq.size(), nw = nf + nI;
+  if (nw > 128) return fail(CPL_ERR_UNSUPPORTED, "cpl_solver_create: more than 128 primal-slack unknowns");
+  if (m > nw) return fail(CPL_ERR_UNSUPPORTED, "cpl_solver_create: more constraints than primal-slack unknowns");
+  // w bounds: [x_free, s] against [x_l, g_l(I)] / [x_u, g_u(I)], relaxed by bound_relax_factor 1e-8
+  std::vector<double> wl0(nw), wu0(nw);
+  std::vector<uint8_t> hasL(nw), hasU(nw);
+  int nbounds = 0;
+  for (int k = 0; k < nw; ++k) {
+    double lo = k < nf ? xl[free_idx[k]] : gl[ineq[k - nf]];
+    double up = k < nf ? xu[free_idx[k]] : gu[ineq[k - nf]];
+    if (k >= nf) {
+      if (!(lo > -BIG)) lo = -INFINITY;
+      if (!(up < BIG)) up = INFINITY;
+    }
+    lo = lo - 1e-8 * std::fmax(std::fabs(lo), 1.0);
+    up = up + 1e-8 * std::fmax(std::fabs(up), 1.0);
+    hasL[k] = std::isfinite(lo);
+    hasU[k] = std::isfinite(up);
+    wl0[k] = hasL[k] ? lo : 0.0;
+    wu0[k] = hasU[k] ? up : 0.0;
+    nbounds += hasL[k] + hasU[k];
+  }
+  // Jacobian records: the values-only layout (CPL_EVAL_JAC_FOLDED); amap = record position of
+  // (row, free column), -1 structural zero / constant 0, -2 constant 1
+  int32_t nnz_rec = 0, n_const = 0;
+  CK(cpl_jac_fold_info(d, &nnz_rec, nullptr, &n_const, nullptr, nullptr));
+  std::vector<int32_t> var_k(nnz_rec), const_k(n_const);
+  std::vector<double> const_val(n_const);
+  CK(cpl_jac_fold_info(d, &nnz_rec, var_k.data(), &n_const, const_k.data(), const_val.data()));
+  std::vector<int32_t> rec(nnz, -1);
+  for (int q = 0; q < nnz_rec; ++q) rec[var_k[q]] = q;
+  for (int q = 0; q < n_const; ++q) rec[const_k[q]] = const_val[q] == 1.0 ? -2 : -1;
+  std::vector<int32_t> amap((size_t)m * (nf ? nf : 1), -1);
+  for (int k = 0; k < nnz; ++k)
+    if (freepos[jCol[k]] >= 0) amap[(size_t)iRow[k] * nf + freepos[jCol[k]]] = rec[k];
+  // CSC index of the full structure (central-difference Hessian: grad f + J^T y)
+  std::vector<int32_t> col_ptr(n + 1, 0), csc_k(nnz), csc_row(nnz);
+  for (int k = 0; k < nnz; ++k) ++col_ptr[jCol[k] + 1];
+  for (int j = 0; j < n; ++j) col_ptr[j + 1] += col_ptr[j];
+  {
+    std::vector<int32_t> fill(col_ptr.begin(), col_ptr.end() - 1);
+    for (int k = 0; k < nnz; ++k) {  // rows ascending within a column (CSR order)
+      const int q = fill[jCol[k]]++;
+      csc_k[q] = k;
+      csc_row[q] = iRow[k];
+    }
+  }
+
+  cpl_solver* S = new cpl_solver();
+  S->desc = *d;
+  S->opt = opt;
+  S->B = batch;
+  S->n = n; S->m = m; S->nnz = nnz; S->nnz_rec = nnz_rec; S->nf = nf; S->nI = nI; S->nw = nw; S->nbounds = nbounds;
+  S->bfgs = opt.hessian == CPL_HESSIAN_LIMITED_MEMORY;
+  S->analytic_H = opt.hessian == CPL_HESSIAN_EXACT && cpl_lagrangian_hessian(d, 0, nullptr, nullptr, nullptr, nullptr,
+                                                                             nf > 0 ? nf : 1, nullptr, nullptr) == CPL_OK;
+  S->fd = !S->bfgs && !S->analytic_H;
+  auto bad = [&](hipError_t e, const char* what) {
+    cpl_solver_destroy(S);
+    return hip_err(e, what);
+  };
+  hipError_t e = hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) return bad(e, "hipStreamCreate");
+  for (auto& ev : S->ev)
+    if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
+  if ((e = hipHostMalloc(&S->h_flag, 2)) != hipSuccess) return bad(e, "hipHostMalloc");
+  // every device buffer carved from one allocation: a measuring pass, then the real one
+  const size_t Bz = (size_t)batch, kws = (size_t)cpl_kkt_workspace_doubles(nw, m);
+  const size_t nfd = S->fd ? Bz * 2 * nf : 0;
+  auto carve = [&](Arena& a) {
+  // constants
+  S->free32 = a.take<int32_t>(nf); S->ineq_row = a.take<int32_t>(nI); S->row_slack = a.take<int32_t>(m);
+  S->freepos = a.take<int32_t>(n); S->amap = a.take<int32_t>((size_t)m * (nf ? nf : 1));
+  S->col_ptr = a.take<int32_t>(n + 1); S->csc_k = a.take<int32_t>(nnz); S->csc_row = a.take<int32_t>(nnz);
+  S->free64 = a.take<int64_t>(nf); S->fixed64 = a.take<int64_t>(fixed_idx.size());
+  S->is_fixed = a.take<uint8_t>(n); S->hasL = a.take<uint8_t>(nw); S->hasU = a.take<uint8_t>(nw);
+  S->xl = a.take<double>(n); S->xu = a.take<double>(n); S->gl = a.take<double>(m); S->gu = a.take<double>(m);
+  S->wl0 = a.take<double>(nw); S->wu0 = a.take<double>(nw);
+  // state
+  S->Xbase = a.take<double>(Bz * n); S->w = a.take<double>(Bz * nw); S->y = a.take<double>(Bz * m);
+  S->zL = a.take<double>(Bz * nw); S->zU = a.take<double>(Bz * nw); S->mu = a.take<double>(Bz);
+  S->filt_t = a.take<double>(Bz * FMAX); S->filt_p = a.take<double>(Bz * FMAX); S->dwl = a.take<double>(Bz);
+  S->f = a.take<double>(Bz); S->grad = a.take<double>(Bz * n); S->g = a.take<double>(Bz * m);
+  S->J = a.take<double>(Bz * nnz_rec); S->d_inf = a.take<double>(Bz); S->Hq = a.take<double>(Bz * nf * nf);
+  S->theta_max = a.take<double>(Bz); S->theta_min = a.take<double>(Bz);
+  S->status = a.take<int64_t>(Bz); S->iters = a.take<int64_t>(Bz); S->acc = a.take<int64_t>(Bz);
+  S->fcount = a.take<int64_t>(Bz); S->fc = a.take<int64_t>(Bz);
+  S->active = a.take<uint8_t>(Bz); S->hq_init = a.take<uint8_t>(Bz); S->d_any = a.take<uint8_t>(2);
+  // temporaries
+  S->A = a.take<double>(Bz * m * nw); S->A_new = a.take<double>(Bz * m * nw);
+  S->gradw = a.take<double>(Bz * nw); S->gradw_new = a.take<double>(Bz * nw); S->c = a.take<double>(Bz * m);
+  S->err0 = a.take<double>(Bz); S->base = a.take<double>(Bz); S->mu_o = a.take<double>(Bz);
+  S->ft = a.take<double>(Bz * FMAX); S->fp = a.take<double>(Bz * FMAX); S->tau = a.take<double>(Bz);
+  S->X = a.take<double>(Bz * n); S->H = a.take<double>(Bz * nf * nf); S->M = a.take<double>(Bz * nw * nw);
+  S->Mr = a.take<double>(Bz * nw * nw); S->r1 = a.take<double>(Bz * nw); S->r2 = a.take<double>(Bz * m);
+  S->gphi = a.take<double>(Bz * nw); S->mr_diag = a.take<double>(Bz * nw); S->theta_k = a.take<double>(Bz);
+  S->phi_k = a.take<double>(Bz); S->dw = a.take<double>(Bz * nw); S->dy = a.take<double>(Bz * m);
+  S->delta_w = a.take<double>(Bz); S->delta_c = a.take<double>(Bz); S->dzL = a.take<double>(Bz * nw);
+  S->dzU = a.take<double>(Bz * nw); S->a_max = a.take<double>(Bz); S->a_z = a.take<double>(Bz);
+  S->gd = a.take<double>(Bz); S->ws = a.take<double>(Bz * kws); S->info = a.take<int32_t>(Bz);
+  S->act = a.take<uint8_t>(Bz); S->switch_ok = a.take<uint8_t>(Bz); S->searching = a.take<uint8_t>(Bz);
+  S->st_aug = a.take<uint8_t>(Bz); S->ok = a.take<uint8_t>(Bz); S->soc = a.take<uint8_t>(Bz);
+  S->ok_s = a.take<uint8_t>(Bz); S->failed = a.take<uint8_t>(Bz); S->ok_r = a.take<uint8_t>(Bz);
+  S->rest = a.take<uint8_t>(Bz);
+  S->st_f = a.take<double>(Bz); S->st_g = a.take<double>(Bz * m); S->st_w = a.take<double>(Bz * nw);
+  S->st_alpha = a.take<double>(Bz); S->alpha = a.take<double>(Bz); S->alpha2 = a.take<double>(Bz);
+  S->th = a.take<double>(Bz); S->wt = a.take<double>(Bz * nw); S->Xt = a.take<double>(Bz * n);
+  S->f_t = a.take<double>(Bz); S->g_t = a.take<double>(Bz * m);
+  S->c_soc = a.take<double>(Bz * m); S->a_soc = a.take<double>(Bz); S->th_old = a.take<double>(Bz);
+  S->r2s = a.take<double>(Bz * m); S->dws = a.take<double>(Bz * nw); S->dys = a.take<double>(Bz * m);
+  S->ws_ = a.take<double>(Bz * nw); S->Xs = a.take<double>(Bz * n); S->f_s = a.take<double>(Bz);
+  S->g_s = a.take<double>(Bz * m); S->th_s = a.take<double>(Bz);
+  S->negc = a.take<double>(Bz * m); S->dwr = a.take<double>(Bz * nw); S->dyr = a.take<double>(Bz * m);
+  S->dwr_d = a.take<double>(Bz); S->dcr = a.take<double>(Bz); S->ar = a.take<double>(Bz);
+  S->wr = a.take<double>(Bz * nw); S->Xr = a.take<double>(Bz * n); S->f_r = a.take<double>(Bz);
+  S->g_r = a.take<double>(Bz * m); S->th_r = a.take<double>(Bz); S->infor = a.take<int32_t>(Bz);
+  S->Xn = a.take<double>(Bz * n); S->f_n = a.take<double>(Bz); S->grad_n = a.take<double>(Bz * n);
+  S->g_n = a.take<double>(Bz * m); S->J_n = a.take<double>(Bz * nnz_rec);
+  S->zeros_w = a.take<double>(Bz * nw); S->zeros_B = a.take<double>(Bz);
+  S->fin_f = a.take<double>(Bz); S->fin_g = a.take<double>(Bz * m);
+  S->st32 = a.take<int32_t>(Bz); S->it32 = a.take<int32_t>(Bz);
+  S->Xp = a.take<double>(nfd * n); S->gL = a.take<double>(nfd * n); S->hfd = a.take<double>(Bz * nf);
+  S->mass_fd = a.take<double>(nfd); S->jac_fd = a.take<double>(nfd * nnz); S->grad_fd = a.take<double>(nfd * n);
+  S->tag_fd = a.take<uint8_t>(nfd);
+  };
+  Arena probe;
+  carve(probe);
+  if ((e = hipMalloc(&S->arena.base, probe.used)) != hipSuccess) return bad(e, "hipMalloc solver arena");
+  S->arena.cap = probe.used;
+  carve(S->arena);
+  // constants up, zero buffers
+  std::vector<int64_t> f64(free_idx.begin(), free_idx.end()), x64(fixed_idx.begin(), fixed_idx.end());
+  struct Up { void* dst; const void* src; size_t bytes; };
+  const Up ups[] = {
+      {S->free32, free_idx.data(), 4 * free_idx.size()}, {S->ineq_row, ineq.data(), 4 * ineq.size()},
+      {S->row_slack, row_slack.data(), 4 * (size_t)m}, {S->freepos, freepos.data(), 4 * (size_t)n},
+      {S->amap, amap.data(), 4 * amap.size()}, {S->col_ptr, col_ptr.data(), 4 * col_ptr.size()},
+      {S->csc_k, csc_k.data(), 4 * (size_t)nnz}, {S->csc_row, csc_row.data(), 4 * (size_t)nnz},
+      {S->free64, f64.data(), 8 * f64.size()}, {S->fixed64, x64.data(), 8 * x64.size()},
+      {S->is_fixed, is_fixed.data(), (size_t)n}, {S->hasL, hasL.data(), (size_t)nw}, {S->hasU, hasU.data(), (size_t)nw},
+      {S->xl, xl.data(), 8 * (size_t)n}, {S->xu, xu.data(), 8 * (size_t)n}, {S->gl, gl.data(), 8 * (size_t)m},
+      {S->gu, gu.data(), 8 * (size_t)m}, {S->wl0, wl0.data(), 8 * (size_t)nw}, {S->wu0, wu0.data(), 8 * (size_t)nw}};
+  for (const Up& u : ups)
+    if (u.bytes && (e = hipMemcpy(u.dst, u.src, u.bytes, hipMemcpyHostToDevice)) != hipSuccess) return bad(e, "hipMemcpy");
+  if ((e = hipMemset(S->zeros_w, 0, 8 * Bz * nw)) != hipSuccess || (e = hipMemset(S->zeros_B, 0, 8 * Bz)) != hipSuccess ||
+      (e = hipMemset(S->Mr, 0, 8 * Bz * nw * nw)) != hipSuccess)
+    return bad(e, "hipMemset");
+  *out = S;
+  return CPL_OK;
+}
+
+int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass, const uint8_t* d_env_tag, double* d_x,
+                         double* d_y, int32_t* d_status, int32_t* d_iters, double* d_obj, double* d_primal_inf,
+                         double* d_dual_inf, int32_t* iterations_run, int64_t* evaluations, void* stream) {
+  if (!S || !d_x0) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_solver_solve: missing solver or x0");
+  if (S->desc.env_kind == CPL_ENV_MIXED && !d_env_tag)
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_solver_solve: mixed batches need the env tags");
+  const int64_t B = S->B;
+  const int n = S->n, m = S->m, nf = S->nf, nw = S->nw;
+  hipStream_t st = S->stream;
+  hipError_t e;
+  // order after the caller's stream (its inputs), then run on the solver's own stream
+  HK(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize (caller stream)");
+  // a graph captured for other inputs holds their pointers: re-capture when they change
+  if (S->gexec && (S->mass != d_mass || S->tag != d_env_tag)) {
+    (void)hipGraphExecDestroy(S->gexec);
+    (void)hipGraphDestroy(S->graph);
+    S->gexec = nullptr;
+    S->graph = nullptr;
+  }
+  S->mass = d_mass;
+  S->tag = d_env_tag;
+  int64_t evals = 0;
+  if (S->fd && (d_mass || d_env_tag)) {
+    hipLaunchKernelGGL(k_repeat, dim3(blocks_elems(B * 2 * nf)), dim3(256), 0, st, B, 2 * nf, d_mass, S->mass_fd,
+                       d_env_tag, S->tag_fd);
+    LAUNCHED("k_repeat");
+  }
+  // starting point: x pushed into its bounds, slacks = g_I(x) pushed into theirs, least-squares y
+  hipLaunchKernelGGL(k_xbase, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, d_x0, S->is_fixed, S->xl, S->Xbase);
+  LAUNCHED("k_xbase");
+  hipLaunchKernelGGL(k_start_x, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, S->freepos, S->Xbase, S->hasL,
+                     S->hasU, S->wl0, S->wu0, S->X);
+  LAUNCHED("k_start_x");
+  CK(eval_full(S, S->X, S->f, S->grad, S->g, S->J));
+  ++evals;
+  hipLaunchKernelGGL(k_init_state, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->free32, S->ineq_row,
+                     S->row_slack, S->gl, S->hasL, S->hasU, S->wl0, S->wu0, S->opt.mu_init, S->X, S->g, S->grad, S->w,
+                     S->zL, S->zU, S->theta_max, S->theta_min, S->mu, S->active, S->status, S->iters, S->acc,
+                     S->filt_t, S->filt_p, S->fcount, S->dwl, S->d_inf, S->hq_init, S->r1, S->r2, S->M);
+  LAUNCHED("k_init_state");
+  CK(cpl_ipm_dense_a(B, m, nw, nf, S->nnz_rec, S->amap, S->row_slack, S->J, S->A, nullptr, st));
+  CK(cpl_kkt_solve(0, B, nw, m, S->M, S->A, S->r1, S->r2, S->mu, S->zeros_B, nullptr, S->dw, S->dy, S->delta_w,
+                   S->delta_c, S->info, S->ws, st));
+  hipLaunchKernelGGL(k_y0, dim3(blocks_for(B)), dim3(256), 0, st, B, m, S->dy, S->info, S->y);
+  LAUNCHED("k_y0");
+  if (S->bfgs) {  // model initialised to I, rescaled by the first update (IPOPT's scalar1 s'y / s's)
+    hipLaunchKernelGGL(k_eye, dim3(blocks_elems(B * nf * nf)), dim3(256), 0, st, B * nf * nf, nf, S->Hq);
+    LAUNCHED("k_eye");
+  }
+  const int64_t per_step = (S->fd ? 1 : 0) + (S->opt.max_ls > 0 ? S->opt.max_ls : 1) + S->opt.max_soc + 2;
+  int it = 0;
+  const int max_iter = S->opt.max_iter;
+  if (max_iter > 0) {
+    // first iteration executed (warms per-stream state, the eval kernels' launch geometry)
+    CK(step(S));
+    ++it;
+    evals += per_step;
+    if (S->opt.use_graph && !S->gexec) {
+      HK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
+      const int32_t rc = step(S);
+      hipGraph_t gr = nullptr;
+      e = hipStreamEndCapture(st, &gr);
+      if (rc != CPL_OK) {
+        if (gr) (void)hipGraphDestroy(gr);
+        return rc;
+      }
+      HK(e, "hipStreamEndCapture");
+      S->graph = gr;
+      HK(hipGraphInstantiate(&S->gexec, gr, nullptr, nullptr, 0), "hipGraphInstantiate");
+    }
+    HK(hipMemcpyAsync(S->h_flag, S->d_any, 1, hipMemcpyDeviceToHost, st), "hipMemcpyAsync flag");
+    HK(hipStreamSynchronize(st), "hipStreamSynchronize");
+    int last = S->h_flag[0] ? max_iter : it;
+    const int start = it;
+    while (it < last) {
+      if (S->gexec) HK(hipGraphLaunch(S->gexec, st), "hipGraphLaunch");
+      else CK(step(S));
+      ++it;
+      evals += per_step;
+      const int k = it & 1;
+      HK(hipMemcpyAsync(S->h_flag + k, S->d_any, 1, hipMemcpyDeviceToHost, st), "hipMemcpyAsync flag");
+      HK(hipEventRecord(S->ev[k], st), "hipEventRecord");
+      if (it - start >= 2) {  // the previous iteration's flag (normally landed already)
+        HK(hipEventSynchronize(S->ev[k ^ 1]), "hipEventSynchronize");
+        if (!S->h_flag[k ^ 1]) break;
+      }
+    }
+  }
+  // final convergence test at the last iterate (the barrier update outputs go to scratch)
+  CK(cpl_ipm_dense_a(B, m, nw, nf, S->nnz_rec, S->amap, S->row_slack, S->J, S->A, S->active, st));
+  hipLaunchKernelGGL(k_prep, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->free32, S->row_slack, S->gl,
+                     S->grad, S->g, S->w, S->gradw, S->c);
+  LAUNCHED("k_prep");
+  CK(cpl_ipm_optimality(B, nw, m, FMAX, S->nbounds, S->opt.tol, S->opt.acceptable_tol, S->opt.acceptable_iter, S->A,
+                        S->gradw, S->c, S->w, S->y, S->zL, S->zU, S->hasL, S->hasU, S->wl0, S->wu0, S->mu, S->filt_t,
+                        S->filt_p, S->fcount, S->active, S->status, S->acc, S->d_inf, S->err0, S->base, S->mu_o, S->ft,
+                        S->fp, S->fc, st));
+  // IPOPT honor_original_bounds: the final point projected into the original bounds, re-evaluated
+  double* Xf = d_x ? d_x : S->Xn;
+  hipLaunchKernelGGL(k_unpack, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, nw, S->freepos, S->Xbase, S->w,
+                     S->xl, S->xu, Xf);
+  LAUNCHED("k_unpack (final)");
+  CK(eval_fg(S, Xf, d_obj ? d_obj : S->fin_f, S->fin_g));
+  ++evals;
+  hipLaunchKernelGGL(k_final, dim3(blocks_for(B)), dim3(256), 0, st, B, m, S->fin_g, S->gl, S->gu, S->status, S->iters,
+                     d_primal_inf, d_status, d_iters);
+  LAUNCHED("k_final");
+  if (d_y) HK(hipMemcpyAsync(d_y, S->y, 8 * (size_t)B * m, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync y");
+  if (d_dual_inf) HK(hipMemcpyAsync(d_dual_inf, S->d_inf, 8 * (size_t)B, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
+  HK(hipStreamSynchronize(st), "hipStreamSynchronize");
+  if (iterations_run) *iterations_run = it;
+  if (evaluations) *evaluations = evals;
+  return CPL_OK;
+}
+
+}  // extern "C"

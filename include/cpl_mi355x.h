@@ -394,6 +394,60 @@ int32_t cpl_ipm_dense_a(int64_t batch, int32_t m, int32_t nw, int32_t nf, int32_
                         const int32_t* d_row_slack, const double* d_jac, double* d_A, const uint8_t* d_active,
                         void* stream);
 
+/* ---- the native batched solve engine (device) ------------------------------------------ */
+/*
+ * cpl_solver: many concurrent CentroidalPlanner solves in lock-step on one GPU — IPOPT's
+ * primal-dual interior-point method (filter line search, second-order corrections, monotone barrier
+ * update, inertia-correcting Newton steps) with every callback of every instance
+ * one cpl_eval_batch launch, the Newton step in cpl_kkt_solve and the per-instance iteration work
+ * in the cpl_ipm_* kernels; one iteration is captured once as a HIP graph and replayed with no host
+ * synchronisation but a one-iteration-behind "any instance active" flag.  Replaces, per instance,
+ * ifopt::IpoptSolver::Solve behind CentroidalPlanner::Solve (src/CentroidalPlanner.cpp:22-34).
+ * Converged instances stay in the batch (frozen) until every instance has stopped.
+ */
+#define CPL_HESSIAN_EXACT 0          /* analytic Lagrangian Hessian (Ground / no environment), else FD */
+#define CPL_HESSIAN_LIMITED_MEMORY 1 /* damped BFGS: IFOPT's IpoptSolver default */
+#define CPL_HESSIAN_FD 2             /* central differences of grad f + J^T y */
+
+#define CPL_SOLVE_OPTIMAL 0
+#define CPL_SOLVE_ACCEPTABLE 1
+#define CPL_SOLVE_MAX_ITER 2
+
+typedef struct cpl_solve_options {
+  int32_t max_iter;        /* 3000 (IPOPT's default) */
+  int32_t hessian;         /* CPL_HESSIAN_*, default CPL_HESSIAN_EXACT */
+  int32_t max_ls;          /* line-search trials per iteration, 4 */
+  int32_t max_soc;         /* second-order corrections on the first trial, 1 */
+  int32_t acceptable_iter; /* 15 */
+  int32_t use_graph;       /* capture the iteration as a HIP graph, 1 */
+  int32_t reserved0, reserved1;
+  double tol;              /* 1e-8 */
+  double acceptable_tol;   /* 1e-6 */
+  double mu_init;          /* 0.1 */
+  double fd_step;          /* 1e-6 (CPL_HESSIAN_FD / Superquadric exact) */
+} cpl_solve_options;
+
+typedef struct cpl_solver cpl_solver;
+
+void cpl_solve_options_default(cpl_solve_options* o);
+/* A solver for `batch` instances of the template `d` (copied): plans the problem (free / fixed
+ * variables, slacks, the Jacobian maps) and allocates every device buffer on the current device.
+ * nw = free variables + inequality rows must be <= 128. */
+int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_solve_options* o, cpl_solver** out);
+int32_t cpl_solver_destroy(cpl_solver* s);
+/* Solve every instance from d_x0 [batch, n] (device; masses d_mass [batch] or NULL, tags
+ * d_env_tag for mixed batches) on `stream`; returns when every instance has stopped.  Outputs
+ * (device, any may be NULL): d_x [batch, n] (projected onto the original bounds, IPOPT
+ * honor_original_bounds), d_y [batch, m] constraint multipliers, d_status (CPL_SOLVE_*), d_iters
+ * (iterations per instance), d_obj (f at d_x), d_primal_inf (max violation at d_x), d_dual_inf.
+ * *iterations_run (host, may be NULL): lock-step iterations of the batch; *evaluations: eval launches. */
+int32_t cpl_solver_solve(cpl_solver* s, const double* d_x0, const double* d_mass, const uint8_t* d_env_tag,
+                         double* d_x, double* d_y, int32_t* d_status, int32_t* d_iters, double* d_obj,
+                         double* d_primal_inf, double* d_dual_inf, int32_t* iterations_run, int64_t* evaluations,
+                         void* stream);
+/* dims of the solver's primal-slack system: nf free variables, nI inequality rows (nw = nf + nI) */
+int32_t cpl_solver_dims(const cpl_solver* s, int32_t* nf, int32_t* n_ineq, int32_t* graph_captured);
+
 #ifdef __cplusplus
 }
 #endif
