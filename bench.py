@@ -245,6 +245,63 @@ def cpu_baseline(cfg, seconds):
     }
 
 
+def single_instance_latency(prob, cfg, dev, reps=2000):
+    """The single-instance TNLP path (one IPOPT callback pair per launch):
+    microseconds per eval_g + eval_jac_g of ONE instance, host x in, host g / jac out — H2D copy of x
+    from pinned memory, one cpl_eval_batch launch, D2H of g and jac, stream synchronise — against
+    the oracle's single-instance time on one core (the CPU restatement, IFOPT-order assembly).  Tells
+    integrators where batching starts to pay."""
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    from centroidalplanner_amd import _abi
+    from centroidalplanner_amd.workload import generate
+
+    n, m, nnz = prob.get_nlp_info()
+    x, mass, tag = generate(cfg.n_contacts, cfg.env, 1, 12345)
+    hx = torch.tensor(x, dtype=torch.float64).pin_memory()
+    hg = torch.empty(1, m, dtype=torch.float64).pin_memory()
+    hj = torch.empty(1, nnz, dtype=torch.float64).pin_memory()
+    dx = torch.empty(1, n, dtype=torch.float64, device=dev)
+    dg = torch.empty(1, m, dtype=torch.float64, device=dev)
+    dj = torch.empty(1, nnz, dtype=torch.float64, device=dev)
+    dt = None if tag is None else torch.tensor(tag, device=dev)
+    s = torch.cuda.Stream(dev)
+    sp = ctypes.c_void_p(s.cuda_stream)
+    desc = prob.desc()
+    p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+
+    def once():
+        with torch.cuda.stream(s):
+            dx.copy_(hx, non_blocking=True)
+            _abi.check(_abi.lib.cpl_eval_batch(ctypes.byref(desc), 1, p(dx), None, p(dt), p(dg), p(dj), None, None, sp))
+            hg.copy_(dg, non_blocking=True)
+            hj.copy_(dj, non_blocking=True)
+        s.synchronize()
+
+    for _ in range(50):
+        once()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        once()
+    gpu_us = (time.perf_counter() - t0) / reps * 1e6
+    res = {"gpu_us_per_callback_pair": gpu_us, "path": "pinned H2D x + cpl_eval_batch(B=1) + D2H g, jac + sync"}
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle
+
+        xs = np.repeat(x, 4096, axis=0)
+        t = pyoracle.time_eval_batch(desc, xs, None, None if tag is None else np.repeat(tag, 4096), outputs=("g", "jac"),
+                                     nthreads=1, reps=3)
+        res["cpu_us_per_instance_one_core"] = t / xs.shape[0] * 1e6
+        res["break_even_batch"] = gpu_us / res["cpu_us_per_instance_one_core"]
+    except Exception as e:  # noqa: BLE001
+        res["cpu_error"] = str(e)
+    return res
+
+
 def checker_leg(prob, env, xt, mt, tt, out, batch, sample):
     """Checker (outside every timed region): a strided sample of the instances whose g / jac the
     timed steps wrote, recomputed by the oracle from the same device inputs and compared with the
@@ -583,6 +640,10 @@ def main():
         }
         del fo
 
+    single = None
+    if rank == 0 and world == 1 and not args.no_side:
+        single = single_instance_latency(prob, cfg, dev)
+
     side = None
     if rank == 0 and world == 1 and not args.no_side and args.config == "ground4_1m":
         # BASELINE.json configs[1] (65,536 x 4 Ground) on the same GPU: kernel time only
@@ -656,6 +717,8 @@ def main():
             res["jac_folded"] = folded
         if side:
             res["configs1_65k"] = side
+        if single:
+            res["single_instance"] = single
         print(json.dumps(res), flush=True)
 
     if world > 1:

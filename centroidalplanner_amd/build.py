@@ -61,7 +61,7 @@ def build_extension(force: bool = False, verbose: bool = False) -> str:
 
 HOST_DIR = os.path.join(HERE, "host")
 HOST_LIB = os.path.join(HERE, "libcpl_host.so")
-HOST_SOURCES = ["cpl_problem.cpp", "cpl_planner.cpp", "cpl_broker.cpp"]
+HOST_SOURCES = ["cpl_problem.cpp", "cpl_planner.cpp", "cpl_broker.cpp", "cpl_native.cpp"]
 HOST_HEADERS = ["Environment.hpp", "CplProblem.hpp", "CentroidalPlanner.hpp", "BatchBroker.hpp"]
 
 

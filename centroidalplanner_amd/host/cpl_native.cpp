@@ -1,0 +1,91 @@
+// Host side of the native solve engine: solver::BatchSolver (many instances, host arrays) and
+// solver::NativeSolver (CentroidalPlanner's default NlpSolver: a batch of one) over the C-ABI
+// cpl_solver_* (csrc/cpl_solver.hip).  Reference: the IPOPT solve behind
+// src/CentroidalPlanner.cpp:22-34 (ifopt::IpoptSolver::Solve), with IFOPT's defaults.
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "cpl/CentroidalPlanner.hpp"
+
+namespace cpl {
+namespace solver {
+
+static void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+static void engine_check(int32_t st) {
+  if (st != CPL_OK) throw std::runtime_error(std::string("cpl_solver: ") + cpl_last_error());
+}
+
+BatchSolver::BatchSolver(CplProblem::Ptr problem, int64_t batch, const SolveOptions& opt)
+    : _problem(std::move(problem)), _batch(batch) {
+  const size_t B = (size_t)batch, n = (size_t)_problem->n(), m = (size_t)_problem->m();
+  engine_check(cpl_solver_create(&_problem->Desc(), batch, &opt, &_solver));
+  try {
+    hipStream_t s = nullptr;
+    hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+    _stream = s;
+    hip_check(hipMalloc(&_dx0, 8 * B * n), "hipMalloc");
+    hip_check(hipMalloc(&_dmass, 8 * B), "hipMalloc");
+    hip_check(hipMalloc(&_dx, 8 * B * n), "hipMalloc");
+    hip_check(hipMalloc(&_dy, 8 * B * m), "hipMalloc");
+    hip_check(hipMalloc(&_dobj, 8 * B), "hipMalloc");
+    hip_check(hipMalloc(&_dpinf, 8 * B), "hipMalloc");
+    hip_check(hipMalloc(&_dstatus, 4 * B), "hipMalloc");
+    hip_check(hipMalloc(&_diters, 4 * B), "hipMalloc");
+  } catch (...) {
+    this->~BatchSolver();
+    throw;
+  }
+}
+
+BatchSolver::~BatchSolver() {
+  for (void* p : {(void*)_dx0, (void*)_dmass, (void*)_dx, (void*)_dy, (void*)_dobj, (void*)_dpinf, (void*)_dstatus,
+                  (void*)_diters})
+    if (p) (void)hipFree(p);
+  _dx0 = _dmass = _dx = _dy = _dobj = _dpinf = nullptr;
+  _dstatus = _diters = nullptr;
+  if (_stream) (void)hipStreamDestroy((hipStream_t)_stream);
+  _stream = nullptr;
+  if (_solver) cpl_solver_destroy(_solver);
+  _solver = nullptr;
+}
+
+bool BatchSolver::graph_captured() const {
+  int32_t g = 0;
+  return _solver && cpl_solver_dims(_solver, nullptr, nullptr, &g) == CPL_OK && g;
+}
+
+void BatchSolver::Solve(const double* x0, const double* mass, double* x, double* y, int32_t* status,
+                        int32_t* iterations, double* objective, double* primal_inf) {
+  const size_t B = (size_t)_batch, n = (size_t)_problem->n(), m = (size_t)_problem->m();
+  hipStream_t s = (hipStream_t)_stream;
+  hip_check(hipMemcpyAsync(_dx0, x0, 8 * B * n, hipMemcpyHostToDevice, s), "hipMemcpyAsync x0");
+  if (mass) hip_check(hipMemcpyAsync(_dmass, mass, 8 * B, hipMemcpyHostToDevice, s), "hipMemcpyAsync mass");
+  engine_check(cpl_solver_solve(_solver, _dx0, mass ? _dmass : nullptr, nullptr, _dx, _dy, _dstatus, _diters, _dobj,
+                                _dpinf, nullptr, &_iterations_run, nullptr, s));
+  if (x) hip_check(hipMemcpyAsync(x, _dx, 8 * B * n, hipMemcpyDeviceToHost, s), "hipMemcpyAsync x");
+  if (y) hip_check(hipMemcpyAsync(y, _dy, 8 * B * m, hipMemcpyDeviceToHost, s), "hipMemcpyAsync y");
+  if (status) hip_check(hipMemcpyAsync(status, _dstatus, 4 * B, hipMemcpyDeviceToHost, s), "hipMemcpyAsync status");
+  if (iterations) hip_check(hipMemcpyAsync(iterations, _diters, 4 * B, hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
+  if (objective) hip_check(hipMemcpyAsync(objective, _dobj, 8 * B, hipMemcpyDeviceToHost, s), "hipMemcpyAsync obj");
+  if (primal_inf) hip_check(hipMemcpyAsync(primal_inf, _dpinf, 8 * B, hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
+  hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+}
+
+bool NativeSolver::Solve(CplTNLP& nlp) {
+  const CplProblem::Ptr& prob = nlp.problem();
+  const int32_t n = prob->n();
+  std::vector<double> x0(n), x(n);
+  nlp.get_starting_point(n, true, x0.data());
+  BatchSolver bs(prob, 1, _opt);
+  bs.Solve(x0.data(), nullptr, x.data(), nullptr, &_status, &_iterations, nullptr, &_primal_inf);
+  nlp.finalize_solution(n, x.data());
+  return _status == CPL_SOLVE_OPTIMAL || _status == CPL_SOLVE_ACCEPTABLE;
+}
+
+}  // namespace solver
+}  // namespace cpl

@@ -16,8 +16,10 @@ CentroidalPlanner::CentroidalPlanner(std::vector<std::string> contact_names, dou
 }
 
 // src/CentroidalPlanner.cpp:22-34: solve, then read the solution out of the persistent variables
+// (the default solver, like the reference's ifopt::IpoptSolver member, is created with the planner's
+// first Solve: the native engine with IFOPT's defaults)
 solver::Solution CentroidalPlanner::Solve() {
-  if (!_cpl_solver) throw std::runtime_error("CentroidalPlanner::Solve: no NLP solver attached (SetSolver)");
+  if (!_cpl_solver) _cpl_solver = std::make_shared<solver::NativeSolver>();
   solver::CplTNLP nlp(_cpl_problem);
   _last_ok = _cpl_solver->Solve(nlp);
   solver::Solution sol;

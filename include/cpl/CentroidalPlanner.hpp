@@ -5,8 +5,10 @@
 // src/CoMPlanner.cpp).  The reference's solver member is an ifopt::IpoptSolver
 // (CentroidalPlanner.h:232); IPOPT is not part of this build, so the solver is the NlpSolver
 // interface below: any NLP solver that drives a CplTNLP (an Ipopt::TNLP forwarding adapter, see
-// INTEGRATION.md §1, or a built-in driver).  Solve() without an attached solver throws
-// std::runtime_error.
+// INTEGRATION.md §1), by default the native engine (NativeSolver: IPOPT's interior-point method on
+// the GPU, csrc/cpl_solver.hip, with IFOPT's IpoptSolver defaults — limited-memory Hessian,
+// max_iter 3000, tol 1e-8).  Like IFOPT's solver, a solve that ends unconverged does not throw
+// (LastSolveSucceeded() tells); a HIP failure throws std::runtime_error.
 #pragma once
 
 #include <map>
@@ -25,6 +27,58 @@ class NlpSolver {
   virtual ~NlpSolver() = default;
   // runs the solve; must call nlp.finalize_solution with the final iterate.  true on success.
   virtual bool Solve(CplTNLP& nlp) = 0;
+};
+
+// The native engine's options (cpl_solve_options), IFOPT's IpoptSolver defaults: limited-memory
+// Hessian (src/CentroidalPlanner.cpp:22-29 keeps IFOPT's setting), max_iter 3000, tol 1e-8.
+struct SolveOptions : cpl_solve_options {
+  SolveOptions() {
+    cpl_solve_options_default(this);
+    hessian = CPL_HESSIAN_LIMITED_MEMORY;
+  }
+};
+
+// Many instances of one problem template solved at once on the GPU by the native engine
+// (cpl_solver_*): host arrays in and out, device buffers and the captured iteration kept between
+// solves.  x0 / x: [batch * n] (vector order of CplProblem), mass: [batch] or nullptr (the
+// template's), outputs may be nullptr.  Throws std::runtime_error on a HIP / engine failure.
+class BatchSolver {
+ public:
+  BatchSolver(CplProblem::Ptr problem, int64_t batch, const SolveOptions& opt = SolveOptions());
+  ~BatchSolver();
+  BatchSolver(const BatchSolver&) = delete;
+  BatchSolver& operator=(const BatchSolver&) = delete;
+
+  void Solve(const double* x0, const double* mass, double* x, double* y = nullptr, int32_t* status = nullptr,
+             int32_t* iterations = nullptr, double* objective = nullptr, double* primal_inf = nullptr);
+  int64_t batch() const { return _batch; }
+  int32_t iterations_run() const { return _iterations_run; }
+  bool graph_captured() const;
+
+ private:
+  CplProblem::Ptr _problem;
+  int64_t _batch;
+  cpl_solver* _solver = nullptr;
+  void* _stream = nullptr;
+  double *_dx0 = nullptr, *_dmass = nullptr, *_dx = nullptr, *_dy = nullptr, *_dobj = nullptr, *_dpinf = nullptr;
+  int32_t *_dstatus = nullptr, *_diters = nullptr;
+  int32_t _iterations_run = 0;
+};
+
+// CentroidalPlanner's default solver: the native engine on a batch of one, from the problem's
+// current variables (x = 0 initially, src/Variable3D.cpp:8-10), finalize_solution with the result.
+class NativeSolver : public NlpSolver {
+ public:
+  explicit NativeSolver(const SolveOptions& opt = SolveOptions()) : _opt(opt) {}
+  bool Solve(CplTNLP& nlp) override;
+  int32_t status() const { return _status; }        // CPL_SOLVE_*
+  int32_t iterations() const { return _iterations; }
+  double primal_inf() const { return _primal_inf; }
+
+ private:
+  SolveOptions _opt;
+  int32_t _status = -1, _iterations = 0;
+  double _primal_inf = 0.0;
 };
 }  // namespace solver
 

@@ -131,6 +131,7 @@ class CplTNLP {
   void finalize_solution(int32_t n, const double* x);  // saves x into the problem's variables
 
   int64_t launches() const { return _launches; }
+  const CplProblem::Ptr& problem() const { return _problem; }
 
  private:
   bool Evaluate(const double* x, bool new_x);

@@ -86,7 +86,12 @@ static void test_planner_api() {
   ground->SetMu(0.3);
   CHECK(cpl.GetMu() == 0.3 && other.GetMu() == 0.3);
   CHECK(throws<std::invalid_argument>([&] { ground->SetMu(0.0); }, "Invalid friction coefficient"));
-  CHECK(throws<std::runtime_error>([&] { cpl.Solve(); }, "no NLP solver"));
+}
+
+// without a GPU the default solver (the native engine) cannot run: a HIP failure is a runtime_error
+static void test_solve_without_gpu() {
+  CentroidalPlanner cpl(NAMES, 100.0, std::make_shared<env::Ground>());
+  CHECK(throws<std::runtime_error>([&] { cpl.Solve(); }));
 }
 
 static void test_environment() {
@@ -284,6 +289,195 @@ static void test_solve_plumbing() {
   CHECK(sol.com_sol[2] == 1.0 && sol.contact_values_map.size() == 4);
 }
 
+// ---- TestBasic (tests/TestBasic.cpp) through the C++ facade with its default solver: the native
+// engine (IPOPT's method, IFOPT's defaults), TestBasic's own assertions and tolerances.
+struct StartFrom : solver::NlpSolver {  // sets the problem's variables, then the default solver
+  std::vector<double> x0;
+  solver::NativeSolver inner;
+  bool Solve(solver::CplTNLP& nlp) override {
+    nlp.problem()->SetVariables(x0);
+    return inner.Solve(nlp);
+  }
+};
+
+static Vector3d cross3(const Vector3d& a, const Vector3d& b) {
+  return {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+}
+static double dot3(const Vector3d& a, const Vector3d& b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static double norm3(const Vector3d& a) { return std::sqrt(dot3(a, a)); }
+#define NEAR(a, b, tol) CHECK(std::fabs((a) - (b)) <= (tol))
+
+static void check_balance(const solver::Solution& sol, double mass, const std::vector<double>& w, double mu,
+                          double ttol) {
+  Vector3d F{0, 0, 0}, T{0, 0, 0};
+  for (const auto& e : sol.contact_values_map) {
+    const auto& v = e.second;
+    Vector3d r{v.position_value[0] - sol.com_sol[0], v.position_value[1] - sol.com_sol[1],
+               v.position_value[2] - sol.com_sol[2]};
+    const Vector3d t = cross3(r, v.force_value);
+    for (int k = 0; k < 3; ++k) { F[k] += v.force_value[k]; T[k] += t[k]; }
+    const double fn = dot3(v.force_value, v.normal_value);
+    Vector3d ft;
+    for (int k = 0; k < 3; ++k) ft[k] = v.force_value[k] - fn * v.normal_value[k];
+    CHECK(-fn <= 1e-9);                           // TestBasic.cpp:117-124 (cone signs)
+    CHECK(norm3(ft) - mu * fn <= 1e-9);
+  }
+  NEAR(F[0], w[0], 1e-6);
+  NEAR(F[1], w[1], 1e-6);
+  NEAR(F[2], mass * 9.81 + w[2], 1e-6);
+  NEAR(T[0], w[3], ttol);
+  NEAR(T[1], w[4], ttol);
+  NEAR(T[2], w[5], ttol);
+}
+
+static void test_testbasic_native() {
+  const double mass = 100.0, g = -9.81;
+  {  // testSimpleProblem (TestBasic.cpp:28-61): default settings, from x = 0
+    auto ground = std::make_shared<env::Ground>();
+    ground->SetGroundZ(0.1);
+    CentroidalPlanner cpl({"contact1"}, mass, ground);
+    solver::Solution sol = cpl.Solve();
+    double Fz = 0.0;
+    for (const auto& e : sol.contact_values_map) {
+      Fz += e.second.force_value[2];
+      NEAR(e.second.position_value[2], 0.1, 1e-6);
+      NEAR(norm3(e.second.normal_value), 1.0, 1e-6);
+      NEAR(e.second.normal_value[2], 1.0, 1e-6);
+    }
+    NEAR(Fz, -mass * g, 1e-6);
+  }
+  const std::vector<double> wrench = {100, 0, 0, 0, 0, 100};
+  {  // testGroundEnv (TestBasic.cpp:64-135)
+    auto ground = std::make_shared<env::Ground>();
+    ground->SetGroundZ(0.1);
+    ground->SetMu(0.5);
+    CentroidalPlanner cpl(NAMES, mass, ground);
+    cpl.SetCoMWeight(2.0);
+    cpl.SetForceWeight(0.0);
+    for (const auto& c : NAMES) cpl.SetPosBounds(c, {-0.3, -0.3, 0.0}, {0.3, 0.3, 1.0});
+    cpl.SetManipulationWrench(wrench);
+    auto st = std::make_shared<StartFrom>();
+    st->x0.assign(39, 0.0);
+    st->x0[2] = 1.0;
+    for (int i = 0; i < 4; ++i) {
+      const double ang = 2.0 * M_PI * (i + 0.125) / 4;
+      double* q = &st->x0[3 + 9 * i];
+      q[0] = 1.0; q[1] = 1.0; q[2] = mass * 9.81 / 4;
+      q[3] = 0.2 * std::cos(ang); q[4] = 0.2 * std::sin(ang); q[5] = 0.05;
+      q[6] = 0.0; q[7] = 0.0; q[8] = 1.0;
+    }
+    cpl.SetSolver(st);
+    solver::Solution sol = cpl.Solve();
+    for (const auto& e : sol.contact_values_map) {
+      NEAR(e.second.position_value[2], 0.1, 1e-6);
+      NEAR(norm3(e.second.normal_value), 1.0, 1e-6);
+      NEAR(e.second.normal_value[2], 1.0, 1e-6);
+    }
+    check_balance(sol, mass, wrench, 0.5, 1e-5);
+  }
+  {  // testSuperquadricEnv (TestBasic.cpp:138-222)
+    auto sq = std::make_shared<env::Superquadric>();
+    sq->SetMu(0.5);
+    sq->SetParameters({0, 0, 1}, {0.3, 0.3, 10}, {10, 10, 10});
+    CentroidalPlanner cpl(NAMES, mass, sq);
+    cpl.SetForceWeight(0.0);
+    for (const auto& c : NAMES) cpl.SetPosBounds(c, {-0.5, -0.5, 0.5}, {0.5, 0.5, 1.5});
+    cpl.SetManipulationWrench(wrench);
+    auto st = std::make_shared<StartFrom>();
+    st->x0.assign(39, 0.0);
+    st->x0[2] = 1.0;
+    const double sides[4][2] = {{0.3, 0.0}, {0.0, 0.3}, {-0.3, 0.0}, {0.0, -0.3}};
+    for (int i = 0; i < 4; ++i) {
+      const Vector3d nr{-sides[i][0] / 0.3, -sides[i][1] / 0.3, 0.0};
+      double* q = &st->x0[3 + 9 * i];
+      q[0] = nr[0] * 300.0; q[1] = nr[1] * 300.0; q[2] = 250.0;
+      q[3] = sides[i][0]; q[4] = sides[i][1]; q[5] = 1.0 + 0.01 * (i - 1.5);
+      q[6] = nr[0]; q[7] = nr[1]; q[8] = nr[2];
+    }
+    cpl.SetSolver(st);
+    solver::Solution sol = cpl.Solve();
+    for (const auto& e : sol.contact_values_map) {
+      const Vector3d& p = e.second.position_value;
+      const double C[3] = {0, 0, 1}, R[3] = {0.3, 0.3, 10};
+      double v = 0.0;
+      for (int k = 0; k < 3; ++k) v += std::pow((p[k] - C[k]) / R[k], 10.0);
+      NEAR(v, 1.0, 1e-4);
+      NEAR(norm3(e.second.normal_value), 1.0, 1e-6);
+      CHECK(p[0] >= -0.5 && p[0] <= 0.5 && p[1] >= -0.5 && p[1] <= 0.5 && p[2] >= 0.5 && p[2] <= 1.5);
+    }
+    check_balance(sol, mass, wrench, 0.5, 1e-4);
+  }
+  {  // testCoMPlanner (TestBasic.cpp:225-292)
+    CoMPlanner cpl(NAMES, mass);
+    cpl.SetMu(0.5);
+    cpl.SetContactPosition("contact1", {1.0, 1.0, 0.0});
+    cpl.SetContactPosition("contact2", {-1.0, 1.0, 0.0});
+    cpl.SetContactPosition("contact3", {-1.0, -1.0, 0.0});
+    cpl.SetContactPosition("contact4", {1.0, -1.0, 0.0});
+    cpl.SetLiftingContact("contact4");
+    for (const auto& c : NAMES) cpl.SetForceThreshold(c, 20.0);
+    auto st = std::make_shared<StartFrom>();
+    st->x0.assign(39, 0.0);
+    st->x0[2] = 1.0;
+    const double pos[4][2] = {{1, 1}, {-1, 1}, {-1, -1}, {1, -1}};
+    for (int i = 0; i < 4; ++i) {
+      double* q = &st->x0[3 + 9 * i];
+      q[0] = 1.0; q[1] = 1.0; q[2] = 330.0;
+      q[3] = pos[i][0]; q[4] = pos[i][1]; q[5] = 0.0;  // the fixed positions / normals
+      q[6] = 0.0; q[7] = 0.0; q[8] = 1.0;
+    }
+    st->x0[3 + 27] = st->x0[4 + 27] = st->x0[5 + 27] = 0.0;  // the lifting contact's force bounds are 0
+    cpl.SetSolver(st);
+    solver::Solution sol = cpl.Solve();
+    check_balance(sol, mass, std::vector<double>(6, 0.0), 0.5, 1e-4);
+  }
+}
+
+// the batched engine from C++: many instances, host arrays (configs[4]'s problem)
+static void test_batch_solver() {
+  auto ground = std::make_shared<env::Ground>();
+  ground->SetGroundZ(0.1);
+  ground->SetMu(0.5);
+  auto prob = std::make_shared<solver::CplProblem>(NAMES, 100.0, ground);
+  prob->SetCoMWeight(2.0);
+  for (const auto& c : NAMES) prob->SetPosBounds(c, {-0.3, -0.3, 0.0}, {0.3, 0.3, 1.0});
+  prob->SetManipulationWrench({100, 0, 0, 0, 0, 100});
+  const int64_t B = 64;
+  const int n = prob->n();
+  std::vector<double> x0(B * n, 0.0), mass(B), x(B * n), obj(B), pinf(B);
+  std::vector<int32_t> status(B), its(B);
+  for (int64_t b = 0; b < B; ++b) {
+    mass[b] = 80.0 + 70.0 * (double)b / (double)(B - 1);
+    double* xb = &x0[b * n];
+    xb[2] = 1.0;
+    for (int i = 0; i < 4; ++i) {
+      const double ang = 2.0 * M_PI * (i + 0.125) / 4;
+      double* q = xb + 3 + 9 * i;
+      q[0] = 1.0; q[1] = 1.0; q[2] = mass[b] * 9.81 / 4;
+      q[3] = 0.2 * std::cos(ang); q[4] = 0.2 * std::sin(ang); q[5] = 0.05;
+      q[8] = 1.0;
+    }
+  }
+  solver::SolveOptions opt;
+  opt.hessian = CPL_HESSIAN_EXACT;
+  solver::BatchSolver bs(prob, B, opt);
+  for (int rep = 0; rep < 2; ++rep) {  // the second solve replays the captured iteration
+    bs.Solve(x0.data(), mass.data(), x.data(), nullptr, status.data(), its.data(), obj.data(), pinf.data());
+    CHECK(bs.graph_captured());
+    double worst = 0.0;
+    for (int64_t b = 0; b < B; ++b) {
+      CHECK(status[b] == CPL_SOLVE_OPTIMAL || status[b] == CPL_SOLVE_ACCEPTABLE);
+      worst = std::fmax(worst, pinf[b]);
+      // force balance against this instance's mass (TestBasic.cpp:126-128 tolerance)
+      double Fz = 0.0;
+      for (int i = 0; i < 4; ++i) Fz += x[b * n + 5 + 9 * i];
+      NEAR(Fz, mass[b] * 9.81, 1e-6);
+    }
+    std::printf("batch solver: %d lock-step iterations, worst primal infeasibility %.3g\n", bs.iterations_run(), worst);
+    CHECK(worst <= 1e-4);  // IPOPT constr_viol_tol
+  }
+}
+
 int main(int argc, char** argv) {
   bool gpu = false;
   const char* oracle = nullptr;
@@ -296,6 +490,7 @@ int main(int argc, char** argv) {
     test_environment();
     test_problem_layout();
     test_com_planner();
+    if (!gpu) test_solve_without_gpu();
     if (gpu) {
       if (!oracle) throw std::runtime_error("--gpu needs --oracle <libcpl_oracle.so>");
       load_oracle(oracle);
@@ -309,6 +504,8 @@ int main(int argc, char** argv) {
       test_broker(ground, 3001, 0.0);
       test_broker(sq, 1001, 1e-9);
       test_solve_plumbing();
+      test_testbasic_native();
+      test_batch_solver();
     }
   } catch (const std::exception& e) {
     std::fprintf(stderr, "FAIL: uncaught exception: %s\n", e.what());
