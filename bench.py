@@ -421,6 +421,7 @@ def solve_bench(args):
                        "max_ls": args.max_ls, "max_soc": args.max_soc},
             "solved": ok, "iterations_max": int(its.max().item()), "iterations_mean": float(its.mean().item()),
             "lockstep_iterations": r.iterations_run, "eval_launches_per_solve": r.evaluations,
+            "compactions": r.compactions,
             "graph": r.graph,
             "cpu_baseline": cpu,
         }), flush=True)

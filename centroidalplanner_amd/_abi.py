@@ -84,7 +84,7 @@ class SolveOptions(ctypes.Structure):
         ("max_soc", c_int32),
         ("acceptable_iter", c_int32),
         ("use_graph", c_int32),
-        ("reserved0", c_int32),
+        ("compact", c_int32),
         ("reserved1", c_int32),
         ("tol", c_double),
         ("acceptable_tol", c_double),
@@ -184,6 +184,7 @@ SIGNATURES = {
     "cpl_solver_destroy": (c_int32, [c_void_p]),
     "cpl_solver_solve": (c_int32, [c_void_p] + [c_void_p] * 10 + [POINTER(c_int32), POINTER(c_int64), c_void_p]),
     "cpl_solver_dims": (c_int32, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
+    "cpl_solver_stats": (c_int32, [c_void_p, POINTER(c_int32), POINTER(c_int64)]),
 }
 
 

@@ -125,6 +125,7 @@ class BatchSolveResult:
     evaluations: int     # batched evaluator launches (graph replays included)
     iterations_run: int  # lock-step iterations of the batch
     graph: bool          # the iteration ran as a captured HIP graph
+    compactions: int = 0  # active-set compactions of the native engine (the batch shrank this often)
 
     @property
     def success(self):
@@ -140,7 +141,7 @@ class NativeSolver:
     once, the iteration captured once as a HIP graph and replayed on every solve."""
 
     def __init__(self, problem, batch, tol=1e-8, max_iter=3000, mu_init=0.1, acceptable_tol=1e-6,
-                 acceptable_iter=15, max_ls=4, max_soc=1, hessian="exact", fd_step=1e-6, graph=True):
+                 acceptable_iter=15, max_ls=4, max_soc=1, hessian="exact", fd_step=1e-6, graph=True, compact=True):
         o = _abi.SolveOptions()
         _abi.lib.cpl_solve_options_default(ctypes.byref(o))
         o.max_iter, o.max_ls, o.max_soc, o.acceptable_iter = int(max_iter), int(max_ls), int(max_soc), int(acceptable_iter)
@@ -148,6 +149,7 @@ class NativeSolver:
         o.hessian = {"exact": _abi.HESSIAN_EXACT, "limited-memory": _abi.HESSIAN_LIMITED_MEMORY,
                      "fd": _abi.HESSIAN_FD}[hessian]
         o.use_graph = 1 if graph else 0
+        o.compact = 1 if compact else 0
         self.problem, self.batch = problem, int(batch)
         self.desc = problem.desc()
         self.handle = ctypes.c_void_p()
@@ -182,9 +184,12 @@ class NativeSolver:
             ctypes.byref(ev), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
         g = ctypes.c_int32()
         _abi.check(_abi.lib.cpl_solver_dims(self.handle, None, None, ctypes.byref(g)))
+        nc, rows = ctypes.c_int32(), ctypes.c_int64()
+        _abi.check(_abi.lib.cpl_solver_stats(self.handle, ctypes.byref(nc), ctypes.byref(rows)))
+        self.compactions, self.final_rows = int(nc.value), int(rows.value)
         return BatchSolveResult(x=x, y=y, status=status.to(torch.int64), iterations=iters.to(torch.int64),
                                 objective=obj, primal_inf=pinf, dual_inf=dinf, evaluations=int(ev.value),
-                                iterations_run=int(it.value), graph=bool(g.value))
+                                iterations_run=int(it.value), graph=bool(g.value), compactions=int(nc.value))
 
 
 _NATIVE_CACHE = {}
@@ -205,7 +210,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                     max_iter: int = 3000, mu_init: float = 0.1, acceptable_tol: float = 1e-6,
                     acceptable_iter: int = 15, max_ls: int = 4, max_soc: int = 1, hessian: str = "exact",
                     fd_step: float = 1e-6, graph: Optional[bool] = None, check_every: int = 4,
-                    verbose: int = 0) -> BatchSolveResult:
+                    verbose: int = 0, compact: bool = True) -> BatchSolveResult:
     """Solve B instances of `problem`'s template from the starting points X0 [B, n] (torch float64,
     device tensor), per-instance robot masses `mass` [B] (None: the template's).
 
@@ -227,7 +232,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                              "host tensors")
         ns = _native(problem, X0.shape[0], tol=tol, max_iter=max_iter, mu_init=mu_init, acceptable_tol=acceptable_tol,
                      acceptable_iter=acceptable_iter, max_ls=max_ls, max_soc=max_soc, hessian=hessian,
-                     fd_step=fd_step, graph=True if graph is None else bool(graph))
+                     fd_step=fd_step, graph=True if graph is None else bool(graph), compact=compact)
         r = ns.solve(X0, mass, None if evaluator is None else evaluator.env_tag)
         if evaluator is not None:
             evaluator.calls += r.evaluations

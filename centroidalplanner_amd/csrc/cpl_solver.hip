@@ -18,7 +18,10 @@
 
 #include <cmath>
 #include <cstring>
+#include <algorithm>
+#include <map>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "cpl_layout.hpp"
@@ -368,16 +371,105 @@ __global__ __launch_bounds__(256) void k_bfgs(int64_t B, int m, int nf, int nw, 
   }
 }
 
-// "any instance still active" into one byte (read by the host one iteration behind)
-__global__ __launch_bounds__(256) void k_any(int64_t B, const uint8_t* __restrict__ active, uint8_t* __restrict__ out) {
-  __shared__ int s_any;
-  if (threadIdx.x == 0) s_any = 0;
+// the number of instances still active into one int (read by the host one iteration behind):
+// zeroed by k_count_zero at the iteration's start, one atomic per workgroup
+__global__ void k_count_zero(int32_t* __restrict__ count) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) count[0] = 0;
+}
+__global__ __launch_bounds__(256) void k_count(int64_t B, const uint8_t* __restrict__ active, int32_t* __restrict__ count) {
+  __shared__ int s_cnt;
+  if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
-  int a = 0;
-  for (int64_t b = threadIdx.x; b < B; b += blockDim.x) a |= active[b] ? 1 : 0;
-  if (a) s_any = 1;
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int a = (b < B && active[b]) ? 1 : 0;
+  const unsigned long long bal = __ballot(a);
+  if ((threadIdx.x & 63) == 0 && bal) atomicAdd(&s_cnt, __popcll(bal));
   __syncthreads();
-  if (threadIdx.x == 0) out[0] = (uint8_t)s_any;
+  if (threadIdx.x == 0 && s_cnt) atomicAdd(count, s_cnt);
+}
+
+// ---- active-set compaction (the lock-step batch shrinks to its active instances) ----------
+// pos[j] = the row of the j-th active instance (j < count), one workgroup scanning the flags
+__global__ __launch_bounds__(1024) void k_positions(int64_t B, const uint8_t* __restrict__ active,
+                                                    int32_t* __restrict__ pos) {
+  __shared__ int s_base;
+  __shared__ int s_wave[16];
+  if (threadIdx.x == 0) s_base = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int64_t c0 = 0; c0 < B; c0 += blockDim.x) {
+    const int64_t b = c0 + threadIdx.x;
+    const int a = (b < B && active[b]) ? 1 : 0;
+    const unsigned long long bal = __ballot(a);
+    if (lane == 0) s_wave[wave] = __popcll(bal);
+    __syncthreads();
+    int off = s_base;
+    for (int w = 0; w < wave; ++w) off += s_wave[w];
+    if (a) pos[off + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)b;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int t = 0;
+      for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += s_wave[w];
+      s_base += t;
+    }
+    __syncthreads();
+  }
+}
+
+// dst[j] = src[pos[j]] for rows of `len` 8-byte words (j < k); rows j in [k, rows) untouched
+__global__ void k_gather_rows(int64_t k, int64_t len, const int32_t* __restrict__ pos, const uint64_t* __restrict__ src,
+                              uint64_t* __restrict__ dst) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= k * len) return;
+  const int64_t j = e / len;
+  dst[e] = src[(int64_t)pos[j] * len + (e - j * len)];
+}
+__global__ void k_gather_bytes(int64_t k, const int32_t* __restrict__ pos, const uint8_t* __restrict__ src,
+                               uint8_t* __restrict__ dst) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < k) dst[j] = src[pos[j]];
+}
+
+// the final state of every row that leaves the batch (finished, or at the end: all rows), written
+// to the instance's own position orig[r] of the full-batch result arrays
+__global__ __launch_bounds__(256) void k_scatter_final(int64_t rows, int n, int m, int nw, bool finished_only,
+                                                       const int32_t* __restrict__ orig, const uint8_t* __restrict__ active,
+                                                       const double* __restrict__ w, const double* __restrict__ y,
+                                                       const double* __restrict__ Xbase, const double* __restrict__ d_inf,
+                                                       const int64_t* __restrict__ status, const int64_t* __restrict__ iters,
+                                                       double* __restrict__ fw, double* __restrict__ fy,
+                                                       double* __restrict__ fX, double* __restrict__ fdinf,
+                                                       int64_t* __restrict__ fstatus, int64_t* __restrict__ fiters) {
+  const int64_t r = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const int32_t o = orig[r];
+  if (o < 0 || (finished_only && active[r])) return;
+  const int lane = threadIdx.x & 63;
+  for (int k = lane; k < nw; k += 64) fw[(int64_t)o * nw + k] = w[r * nw + k];
+  for (int k = lane; k < m; k += 64) fy[(int64_t)o * m + k] = y[r * m + k];
+  for (int k = lane; k < n; k += 64) fX[(int64_t)o * n + k] = Xbase[r * n + k];
+  if (lane == 0) {
+    fdinf[o] = d_inf[r];
+    fstatus[o] = status[r];
+    fiters[o] = iters[r];
+  }
+}
+
+__global__ void k_gather_i32(int64_t k, const int32_t* __restrict__ pos, const int32_t* __restrict__ src,
+                             int32_t* __restrict__ dst) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < k) dst[j] = src[pos[j]];
+}
+__global__ void k_pad(int64_t k, int64_t rows, uint8_t* __restrict__ active, int32_t* __restrict__ orig) {
+  const int64_t j = k + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= rows) return;
+  active[j] = 0;
+  orig[j] = -1;
+}
+
+__global__ void k_iota(int64_t B, int32_t* __restrict__ orig) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) orig[b] = (int32_t)b;
 }
 
 // results: max violation of g against its bounds, int32 copies of status / iterations
@@ -437,11 +529,13 @@ struct cpl_solver {
   cpl_problem_desc desc;
   cpl_solve_options opt;
   int64_t B = 0;
+  int64_t Bcur = 0;  // rows in play: B, shrunk by active-set compaction
   int n = 0, m = 0, nnz = 0, nnz_rec = 0, nf = 0, nI = 0, nw = 0, nbounds = 0;
   bool analytic_H = false, bfgs = false, fd = false, fd_fused = true;
   hipStream_t stream = nullptr;
-  hipGraph_t graph = nullptr;
+  hipGraph_t graph = nullptr;  // the graph of the current (Bcur, mass / tag presence)
   hipGraphExec_t gexec = nullptr;
+  std::map<int64_t, std::pair<hipGraph_t, hipGraphExec_t>> graphs;  // every captured size
   hipEvent_t ev[2] = {nullptr, nullptr};
   uint8_t* h_flag = nullptr;  // pinned, 2 bytes
   cpl::Arena arena;
@@ -471,6 +565,14 @@ struct cpl_solver {
   uint8_t* tag_fd;
   double *fin_f, *fin_g;
   int32_t *st32, *it32;
+  // compaction: original instance of each row, compacted masses / tags, full-batch results
+  int32_t *orig, *pos, *d_count, *h_count = nullptr;
+  double *mass_c, *fw, *fy, *fX, *fdinf;
+  uint8_t* tag_c;
+  int64_t *fstatus, *fiters;
+  uint64_t* scratch;
+  int64_t scratch_words = 0;
+  int32_t compactions = 0;
 };
 
 namespace cpl {
@@ -487,20 +589,22 @@ int32_t hip_err(hipError_t e, const char* what) {
 #define LAUNCHED(what) HK(hipGetLastError(), what)
 
 int32_t eval_fg(cpl_solver* S, const double* X, double* fo, double* go) {
-  return cpl_eval_batch(&S->desc, S->B, X, S->mass, S->tag, go, nullptr, fo, nullptr, S->stream);
+  return cpl_eval_batch(&S->desc, S->Bcur, X, S->mass, S->tag, go, nullptr, fo, nullptr, S->stream);
 }
 int32_t eval_full(cpl_solver* S, const double* X, double* fo, double* grado, double* go, double* jo) {
-  return cpl_eval_batch_ex(&S->desc, S->B, X, S->mass, S->tag, go, jo, fo, grado, nullptr, CPL_EVAL_JAC_FOLDED,
+  return cpl_eval_batch_ex(&S->desc, S->Bcur, X, S->mass, S->tag, go, jo, fo, grado, nullptr, CPL_EVAL_JAC_FOLDED,
                            S->stream);
 }
 
 // one lock-step iteration of every instance (graph-capturable: no host synchronisation)
 int32_t step(cpl_solver* S) {
-  const int64_t B = S->B;
+  const int64_t B = S->Bcur;
   const int n = S->n, m = S->m, nf = S->nf, nw = S->nw;
   hipStream_t st = S->stream;
   const cpl_solve_options& o = S->opt;
   // optimality error, convergence test, barrier update (filters reset where mu changed)
+  hipLaunchKernelGGL(k_count_zero, dim3(1), dim3(64), 0, st, S->d_count);
+  LAUNCHED("k_count_zero");
   CK(cpl_ipm_dense_a(B, m, nw, nf, S->nnz_rec, S->amap, S->row_slack, S->J, S->A, S->active, st));
   hipLaunchKernelGGL(k_prep, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->free32, S->row_slack, S->gl,
                      S->grad, S->g, S->w, S->gradw, S->c);
@@ -629,8 +733,91 @@ int32_t step(cpl_solver* S) {
   CK(cpl_ipm_masked_rows(B, n, S->act, S->grad_n, S->grad, st));
   CK(cpl_ipm_masked_rows(B, m, S->act, S->g_n, S->g, st));
   CK(cpl_ipm_masked_rows(B, S->nnz_rec, S->act, S->J_n, S->J, st));
-  hipLaunchKernelGGL(k_any, dim3(1), dim3(256), 0, st, B, S->active, S->d_any);
-  LAUNCHED("k_any");
+  hipLaunchKernelGGL(k_count, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->active, S->d_count);
+  LAUNCHED("k_count");
+  return CPL_OK;
+}
+
+// the graph of one iteration at the current batch size (captured once per size, then replayed)
+int32_t graph_for(cpl_solver* S) {
+  const int64_t key = S->Bcur * 4 + (S->mass ? 2 : 0) + (S->tag ? 1 : 0);
+  auto it = S->graphs.find(key);
+  if (it == S->graphs.end()) {
+    HK(hipStreamBeginCapture(S->stream, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
+    const int32_t rc = step(S);
+    hipGraph_t gr = nullptr;
+    const hipError_t e = hipStreamEndCapture(S->stream, &gr);
+    if (rc != CPL_OK) {
+      if (gr) (void)hipGraphDestroy(gr);
+      return rc;
+    }
+    HK(e, "hipStreamEndCapture");
+    hipGraphExec_t ex = nullptr;
+    const hipError_t e2 = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
+    if (e2 != hipSuccess) {
+      (void)hipGraphDestroy(gr);
+      return hip_err(e2, "hipGraphInstantiate");
+    }
+    it = S->graphs.emplace(key, std::make_pair(gr, ex)).first;
+  }
+  S->graph = it->second.first;
+  S->gexec = it->second.second;
+  return CPL_OK;
+}
+
+// Active-set compaction: the finished rows' results go to the full-batch arrays, the `count` active
+// rows move to the front (every per-instance state buffer gathered), the batch shrinks to Bn rows
+// (the rows past `count` padded inactive), so later iterations cost what their active instances do.
+int32_t compact(cpl_solver* S, int64_t count, int64_t Bn) {
+  hipStream_t st = S->stream;
+  const int64_t Bc = S->Bcur;
+  const int n = S->n, m = S->m, nw = S->nw;
+  hipLaunchKernelGGL(k_scatter_final, dim3(blocks_for(Bc)), dim3(256), 0, st, Bc, n, m, nw, true, S->orig, S->active,
+                     S->w, S->y, S->Xbase, S->d_inf, S->status, S->iters, S->fw, S->fy, S->fX, S->fdinf, S->fstatus,
+                     S->fiters);
+  LAUNCHED("k_scatter_final");
+  hipLaunchKernelGGL(k_positions, dim3(1), dim3(1024), 0, st, Bc, S->active, S->pos);
+  LAUNCHED("k_positions");
+  auto move = [&](void* buf, int64_t words) -> int32_t {
+    if (!buf || words <= 0) return CPL_OK;
+    hipLaunchKernelGGL(k_gather_rows, dim3(blocks_elems(count * words)), dim3(256), 0, st, count, words, S->pos,
+                       (const uint64_t*)buf, S->scratch);
+    LAUNCHED("k_gather_rows");
+    HK(hipMemcpyAsync(buf, S->scratch, 8 * (size_t)(count * words), hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
+    return CPL_OK;
+  };
+  const int nf = S->nf;
+  CK(move(S->w, nw)); CK(move(S->y, m)); CK(move(S->zL, nw)); CK(move(S->zU, nw)); CK(move(S->mu, 1));
+  CK(move(S->filt_t, FMAX)); CK(move(S->filt_p, FMAX)); CK(move(S->dwl, 1)); CK(move(S->f, 1));
+  CK(move(S->grad, n)); CK(move(S->g, m)); CK(move(S->J, S->nnz_rec)); CK(move(S->d_inf, 1));
+  CK(move(S->theta_max, 1)); CK(move(S->theta_min, 1)); CK(move(S->Xbase, n));
+  CK(move(S->status, 1)); CK(move(S->iters, 1)); CK(move(S->acc, 1)); CK(move(S->fcount, 1));
+  if (S->bfgs) CK(move(S->Hq, (int64_t)nf * nf));
+  if (S->mass) CK(move(S->mass_c, 1));
+  // 1-byte and 4-byte rows
+  auto move_bytes = [&](uint8_t* buf) -> int32_t {
+    hipLaunchKernelGGL(k_gather_bytes, dim3(blocks_elems(count)), dim3(256), 0, st, count, S->pos, buf,
+                       (uint8_t*)S->scratch);
+    LAUNCHED("k_gather_bytes");
+    HK(hipMemcpyAsync(buf, S->scratch, (size_t)count, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
+    return CPL_OK;
+  };
+  CK(move_bytes(S->active));
+  CK(move_bytes(S->hq_init));
+  if (S->tag) CK(move_bytes(S->tag_c));
+  hipLaunchKernelGGL(k_gather_i32, dim3(blocks_elems(count)), dim3(256), 0, st, count, S->pos, S->orig,
+                     (int32_t*)S->scratch);
+  LAUNCHED("k_gather_i32");
+  HK(hipMemcpyAsync(S->orig, S->scratch, 4 * (size_t)count, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
+  hipLaunchKernelGGL(k_pad, dim3(blocks_elems(Bn)), dim3(256), 0, st, count, Bn, S->active, S->orig);
+  LAUNCHED("k_pad");
+  S->Bcur = Bn;
+  if (S->fd && (S->mass || S->tag)) {
+    hipLaunchKernelGGL(k_repeat, dim3(blocks_elems(Bn * 2 * nf)), dim3(256), 0, st, Bn, 2 * nf, S->mass,
+                       S->mass_fd, S->tag, S->tag_fd);
+    LAUNCHED("k_repeat");
+  }
+  ++S->compactions;
   return CPL_OK;
 }
 
@@ -650,6 +837,7 @@ void cpl_solve_options_default(cpl_solve_options* o) {
   o->max_soc = 1;
   o->acceptable_iter = 15;
   o->use_graph = 1;
+  o->compact = 1;
   o->tol = 1e-8;
   o->acceptable_tol = 1e-6;
   o->mu_init = 0.1;
@@ -658,11 +846,15 @@ void cpl_solve_options_default(cpl_solve_options* o) {
 
 int32_t cpl_solver_destroy(cpl_solver* S) {
   if (!S) return CPL_OK;
-  if (S->gexec) (void)hipGraphExecDestroy(S->gexec);
-  if (S->graph) (void)hipGraphDestroy(S->graph);
+  for (auto& g : S->graphs) {
+    (void)hipGraphExecDestroy(g.second.second);
+    (void)hipGraphDestroy(g.second.first);
+  }
+  S->graphs.clear();
   for (auto& e : S->ev)
     if (e) (void)hipEventDestroy(e);
   if (S->h_flag) (void)hipHostFree(S->h_flag);
+  if (S->h_count) (void)hipHostFree(S->h_count);
   if (S->arena.base) (void)hipFree(S->arena.base);
   if (S->stream) (void)hipStreamDestroy(S->stream);
   delete S;
@@ -674,6 +866,13 @@ int32_t cpl_solver_dims(const cpl_solver* S, int32_t* nf, int32_t* n_ineq, int32
   if (nf) *nf = S->nf;
   if (n_ineq) *n_ineq = S->nI;
   if (graph_captured) *graph_captured = S->gexec != nullptr;
+  return CPL_OK;
+}
+
+int32_t cpl_solver_stats(const cpl_solver* S, int32_t* compactions, int64_t* final_rows) {
+  if (!S) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_solver_stats: null solver");
+  if (compactions) *compactions = S->compactions;
+  if (final_rows) *final_rows = S->Bcur;
   return CPL_OK;
 }
 
@@ -778,9 +977,15 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   for (auto& ev : S->ev)
     if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
   if ((e = hipHostMalloc(&S->h_flag, 2)) != hipSuccess) return bad(e, "hipHostMalloc");
+  if ((e = hipHostMalloc(&S->h_count, 2 * sizeof(int32_t))) != hipSuccess) return bad(e, "hipHostMalloc");
   // every device buffer carved from one allocation: a measuring pass, then the real one
   const size_t Bz = (size_t)batch, kws = (size_t)cpl_kkt_workspace_doubles(nw, m);
   const size_t nfd = S->fd ? Bz * 2 * nf : 0;
+  {  // the widest per-instance row the compaction moves
+    int64_t wmax = nnz_rec;
+    for (int64_t v : {(int64_t)n, (int64_t)nw, (int64_t)m, (int64_t)FMAX, S->bfgs ? (int64_t)nf * nf : 0}) wmax = std::max(wmax, v);
+    S->scratch_words = wmax;
+  }
   auto carve = [&](Arena& a) {
   // constants
   S->free32 = a.take<int32_t>(nf); S->ineq_row = a.take<int32_t>(nI); S->row_slack = a.take<int32_t>(m);
@@ -836,6 +1041,11 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   S->Xp = a.take<double>(nfd * n); S->gL = a.take<double>(nfd * n); S->hfd = a.take<double>(Bz * nf);
   S->mass_fd = a.take<double>(nfd); S->jac_fd = a.take<double>(nfd * nnz); S->grad_fd = a.take<double>(nfd * n);
   S->tag_fd = a.take<uint8_t>(nfd);
+  S->orig = a.take<int32_t>(Bz); S->pos = a.take<int32_t>(Bz); S->d_count = a.take<int32_t>(2);
+  S->mass_c = a.take<double>(Bz); S->tag_c = a.take<uint8_t>(Bz);
+  S->fw = a.take<double>(Bz * nw); S->fy = a.take<double>(Bz * m); S->fX = a.take<double>(Bz * n);
+  S->fdinf = a.take<double>(Bz); S->fstatus = a.take<int64_t>(Bz); S->fiters = a.take<int64_t>(Bz);
+  S->scratch = a.take<uint64_t>(Bz * (size_t)S->scratch_words);
   };
   Arena probe;
   carve(probe);
@@ -872,22 +1082,22 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
   const int64_t B = S->B;
   const int n = S->n, m = S->m, nf = S->nf, nw = S->nw;
   hipStream_t st = S->stream;
-  hipError_t e;
   // order after the caller's stream (its inputs), then run on the solver's own stream
   HK(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize (caller stream)");
-  // a graph captured for other inputs holds their pointers: re-capture when they change
-  if (S->gexec && (S->mass != d_mass || S->tag != d_env_tag)) {
-    (void)hipGraphExecDestroy(S->gexec);
-    (void)hipGraphDestroy(S->graph);
-    S->gexec = nullptr;
-    S->graph = nullptr;
-  }
-  S->mass = d_mass;
-  S->tag = d_env_tag;
+  S->Bcur = B;
+  S->compactions = 0;
+  // the iteration reads the solver's own copies of the masses / tags (compaction reorders them), so
+  // a captured graph never holds a caller's pointer
+  S->mass = d_mass ? S->mass_c : nullptr;
+  S->tag = d_env_tag ? S->tag_c : nullptr;
+  if (d_mass) HK(hipMemcpyAsync(S->mass_c, d_mass, 8 * (size_t)B, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync mass");
+  if (d_env_tag) HK(hipMemcpyAsync(S->tag_c, d_env_tag, (size_t)B, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync tag");
+  hipLaunchKernelGGL(k_iota, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->orig);
+  LAUNCHED("k_iota");
   int64_t evals = 0;
   if (S->fd && (d_mass || d_env_tag)) {
-    hipLaunchKernelGGL(k_repeat, dim3(blocks_elems(B * 2 * nf)), dim3(256), 0, st, B, 2 * nf, d_mass, S->mass_fd,
-                       d_env_tag, S->tag_fd);
+    hipLaunchKernelGGL(k_repeat, dim3(blocks_elems(B * 2 * nf)), dim3(256), 0, st, B, 2 * nf, S->mass, S->mass_fd,
+                       S->tag, S->tag_fd);
     LAUNCHED("k_repeat");
   }
   // starting point: x pushed into its bounds, slacks = g_I(x) pushed into theirs, least-squares y
@@ -912,66 +1122,76 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
     hipLaunchKernelGGL(k_eye, dim3(blocks_elems(B * nf * nf)), dim3(256), 0, st, B * nf * nf, nf, S->Hq);
     LAUNCHED("k_eye");
   }
-  const int64_t per_step = (S->fd ? 1 : 0) + (S->opt.max_ls > 0 ? S->opt.max_ls : 1) + S->opt.max_soc + 2;
+  const int64_t per_step_full = (S->fd ? 1 : 0) + (S->opt.max_ls > 0 ? S->opt.max_ls : 1) + S->opt.max_soc + 2;
   int it = 0;
   const int max_iter = S->opt.max_iter;
+  const bool compacting = S->opt.compact != 0 && S->opt.use_graph;
+  const int64_t min_rows = 256;
   if (max_iter > 0) {
     // first iteration executed (warms per-stream state, the eval kernels' launch geometry)
     CK(step(S));
     ++it;
-    evals += per_step;
-    if (S->opt.use_graph && !S->gexec) {
-      HK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
-      const int32_t rc = step(S);
-      hipGraph_t gr = nullptr;
-      e = hipStreamEndCapture(st, &gr);
-      if (rc != CPL_OK) {
-        if (gr) (void)hipGraphDestroy(gr);
-        return rc;
-      }
-      HK(e, "hipStreamEndCapture");
-      S->graph = gr;
-      HK(hipGraphInstantiate(&S->gexec, gr, nullptr, nullptr, 0), "hipGraphInstantiate");
-    }
-    HK(hipMemcpyAsync(S->h_flag, S->d_any, 1, hipMemcpyDeviceToHost, st), "hipMemcpyAsync flag");
+    evals += per_step_full;
+    if (S->opt.use_graph) CK(graph_for(S));
+    HK(hipMemcpyAsync(S->h_count, S->d_count, 4, hipMemcpyDeviceToHost, st), "hipMemcpyAsync count");
     HK(hipStreamSynchronize(st), "hipStreamSynchronize");
-    int last = S->h_flag[0] ? max_iter : it;
-    const int start = it;
+    int last = S->h_count[0] ? max_iter : it;
+    int start = it;
     while (it < last) {
-      if (S->gexec) HK(hipGraphLaunch(S->gexec, st), "hipGraphLaunch");
+      if (S->opt.use_graph) HK(hipGraphLaunch(S->gexec, st), "hipGraphLaunch");
       else CK(step(S));
       ++it;
-      evals += per_step;
+      evals += per_step_full;
       const int k = it & 1;
-      HK(hipMemcpyAsync(S->h_flag + k, S->d_any, 1, hipMemcpyDeviceToHost, st), "hipMemcpyAsync flag");
+      HK(hipMemcpyAsync(S->h_count + k, S->d_count, 4, hipMemcpyDeviceToHost, st), "hipMemcpyAsync count");
       HK(hipEventRecord(S->ev[k], st), "hipEventRecord");
-      if (it - start >= 2) {  // the previous iteration's flag (normally landed already)
+      if (it - start >= 2) {  // the previous iteration's count (normally landed already)
         HK(hipEventSynchronize(S->ev[k ^ 1]), "hipEventSynchronize");
-        if (!S->h_flag[k ^ 1]) break;
+        const int64_t cnt = S->h_count[k ^ 1];
+        if (cnt == 0) break;
+        if (compacting && S->Bcur > min_rows && 2 * cnt <= S->Bcur) {
+          // shrink to the smallest halving of the current size that holds the active instances
+          HK(hipStreamSynchronize(st), "hipStreamSynchronize");
+          const int64_t now = S->h_count[k];
+          if (now == 0) break;
+          int64_t Bn = S->Bcur;
+          while (Bn / 2 >= now && Bn / 2 >= min_rows) Bn = (Bn + 1) / 2;
+          if (Bn < S->Bcur) {
+            CK(compact(S, now, Bn));
+            CK(graph_for(S));
+            start = it;  // the flag pipeline restarts at the new size
+          }
+        }
       }
     }
   }
   // final convergence test at the last iterate (the barrier update outputs go to scratch)
-  CK(cpl_ipm_dense_a(B, m, nw, nf, S->nnz_rec, S->amap, S->row_slack, S->J, S->A, S->active, st));
-  hipLaunchKernelGGL(k_prep, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->free32, S->row_slack, S->gl,
+  const int64_t Bc = S->Bcur;
+  CK(cpl_ipm_dense_a(Bc, m, nw, nf, S->nnz_rec, S->amap, S->row_slack, S->J, S->A, S->active, st));
+  hipLaunchKernelGGL(k_prep, dim3(blocks_for(Bc)), dim3(256), 0, st, Bc, n, m, nf, nw, S->free32, S->row_slack, S->gl,
                      S->grad, S->g, S->w, S->gradw, S->c);
   LAUNCHED("k_prep");
-  CK(cpl_ipm_optimality(B, nw, m, FMAX, S->nbounds, S->opt.tol, S->opt.acceptable_tol, S->opt.acceptable_iter, S->A,
+  CK(cpl_ipm_optimality(Bc, nw, m, FMAX, S->nbounds, S->opt.tol, S->opt.acceptable_tol, S->opt.acceptable_iter, S->A,
                         S->gradw, S->c, S->w, S->y, S->zL, S->zU, S->hasL, S->hasU, S->wl0, S->wu0, S->mu, S->filt_t,
                         S->filt_p, S->fcount, S->active, S->status, S->acc, S->d_inf, S->err0, S->base, S->mu_o, S->ft,
                         S->fp, S->fc, st));
+  // every row still in the batch to its instance's place in the full-batch results
+  hipLaunchKernelGGL(k_scatter_final, dim3(blocks_for(Bc)), dim3(256), 0, st, Bc, n, m, nw, false, S->orig, S->active,
+                     S->w, S->y, S->Xbase, S->d_inf, S->status, S->iters, S->fw, S->fy, S->fX, S->fdinf, S->fstatus,
+                     S->fiters);
+  LAUNCHED("k_scatter_final");
   // IPOPT honor_original_bounds: the final point projected into the original bounds, re-evaluated
   double* Xf = d_x ? d_x : S->Xn;
-  hipLaunchKernelGGL(k_unpack, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, nw, S->freepos, S->Xbase, S->w,
+  hipLaunchKernelGGL(k_unpack, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, nw, S->freepos, S->fX, S->fw,
                      S->xl, S->xu, Xf);
   LAUNCHED("k_unpack (final)");
-  CK(eval_fg(S, Xf, d_obj ? d_obj : S->fin_f, S->fin_g));
+  CK(cpl_eval_batch(&S->desc, B, Xf, d_mass, d_env_tag, S->fin_g, nullptr, d_obj ? d_obj : S->fin_f, nullptr, st));
   ++evals;
-  hipLaunchKernelGGL(k_final, dim3(blocks_for(B)), dim3(256), 0, st, B, m, S->fin_g, S->gl, S->gu, S->status, S->iters,
-                     d_primal_inf, d_status, d_iters);
+  hipLaunchKernelGGL(k_final, dim3(blocks_for(B)), dim3(256), 0, st, B, m, S->fin_g, S->gl, S->gu, S->fstatus,
+                     S->fiters, d_primal_inf, d_status, d_iters);
   LAUNCHED("k_final");
-  if (d_y) HK(hipMemcpyAsync(d_y, S->y, 8 * (size_t)B * m, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync y");
-  if (d_dual_inf) HK(hipMemcpyAsync(d_dual_inf, S->d_inf, 8 * (size_t)B, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
+  if (d_y) HK(hipMemcpyAsync(d_y, S->fy, 8 * (size_t)B * m, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync y");
+  if (d_dual_inf) HK(hipMemcpyAsync(d_dual_inf, S->fdinf, 8 * (size_t)B, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
   HK(hipStreamSynchronize(st), "hipStreamSynchronize");
   if (iterations_run) *iterations_run = it;
   if (evaluations) *evaluations = evals;

@@ -420,7 +420,11 @@ typedef struct cpl_solve_options {
   int32_t max_soc;         /* second-order corrections on the first trial, 1 */
   int32_t acceptable_iter; /* 15 */
   int32_t use_graph;       /* capture the iteration as a HIP graph, 1 */
-  int32_t reserved0, reserved1;
+  int32_t compact;         /* active-set compaction, 1: once at most half of the batch is still
+                              active, the active instances move to the front and the lock-step
+                              batch shrinks to them (halvings of the size, >= 256 rows; one graph per
+                              size); the results come back in the instances' own order */
+  int32_t reserved1;
   double tol;              /* 1e-8 */
   double acceptable_tol;   /* 1e-6 */
   double mu_init;          /* 0.1 */
@@ -447,6 +451,8 @@ int32_t cpl_solver_solve(cpl_solver* s, const double* d_x0, const double* d_mass
                          void* stream);
 /* dims of the solver's primal-slack system: nf free variables, nI inequality rows (nw = nf + nI) */
 int32_t cpl_solver_dims(const cpl_solver* s, int32_t* nf, int32_t* n_ineq, int32_t* graph_captured);
+/* the last solve's active-set compactions and its final lock-step batch size */
+int32_t cpl_solver_stats(const cpl_solver* s, int32_t* compactions, int64_t* final_rows);
 
 #ifdef __cplusplus
 }
