@@ -959,25 +959,32 @@ __device__ __forceinline__ void cost_item(const KParams& K, const double* __rest
 // ((p_a - C_a)/R_a)^P_a, and 1/(C_a - p_a)^2, into an LDS scratch row of SQ_L doubles per contact.
 // Phase 2, one item per (instance, contact, normal-Jacobian row): the three entries of that row
 // from the scratch; row 0 also emits the environment value / Jacobian / normal, row 1 the cone.
-constexpr int SQ_L = 21;  // per contact: 3 axes x {pm1, pP, p2Pm3, p2Pm2, p2P, inv, wenv}
-enum { L_PM1 = 0, L_PP, L_P2PM3, L_P2PM2, L_P2P, L_INV, L_WENV, L_AXIS };
+// The environment-value term of axis a, pow((p_a-C_a)/R_a, P_a), is parked in the contact's
+// normal-residual slot a of the staged g row (g[1+a] of the contact block): the phase-2 row-0 item
+// sums the three terms before it overwrites those slots with the normal residuals.  Keeping it out
+// of the scratch (18 instead of 21 doubles per contact) fits the 8-contact tile in 40 KiB of LDS,
+// i.e. four resident workgroups per CU instead of three.
+constexpr int SQ_L = 18;  // per contact: 3 axes x {pm1, pP, p2Pm3, p2Pm2, p2P, inv}
+enum { L_PM1 = 0, L_PP, L_P2PM3, L_P2PM2, L_P2P, L_INV, L_AXIS };
 
 __device__ __forceinline__ void sq_axis_item(const KParams& K, const double* __restrict__ xr, int k, int a,
-                                             double* __restrict__ Lc) {
+                                             double* __restrict__ Lc, double* __restrict__ Gr) {
   const int i = s_ct.map_order[k];
   const double pa = xr[6 + 9 * i + a];
   const double d = -K.C[a] + pa;
   double* o = Lc + a * L_AXIS;
-  // src/Superquadric.cpp:45  pow((p-C)/R, P)
-  const double u = (pa - K.C[a]) / K.R[a];
-  double w;
-  if (K.sq_ladder && fabs(u) >= DD_TINY && fabs(u) <= 0x1p+40) {
-    w = dd_ipow(u, (unsigned)K.P[a]).hi;
-    if (!(fabs(w) >= DD_TINY && fabs(w) <= DD_HUGE)) w = cpow(u, K.P[a]);
-  } else {
-    w = cpow(u, K.P[a]);
+  if (K.want_g) {
+    // src/Superquadric.cpp:45  pow((p-C)/R, P)
+    const double u = (pa - K.C[a]) / K.R[a];
+    double w;
+    if (K.sq_ladder && fabs(u) >= DD_TINY && fabs(u) <= 0x1p+40) {
+      w = dd_ipow(u, (unsigned)K.P[a]).hi;
+      if (!(fabs(w) >= DD_TINY && fabs(w) <= DD_HUGE)) w = cpow(u, K.P[a]);
+    } else {
+      w = cpow(u, K.P[a]);
+    }
+    Gr[6 + 6 * k + 1 + a] = w;
   }
-  o[L_WENV] = w;
   if (K.want_j) {
     AxisPowers ap;
     axis_powers(K, a, d, ap);
@@ -1037,10 +1044,12 @@ __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __re
     // EnvironmentConstraint / EnvironmentNormal values and the env Jacobian row
     // (src/Superquadric.cpp:40-69; src/Constraints/EnvironmentConstraint.cpp:16-61; EnvironmentNormal.cpp:16-33)
     double v = 0.0;
-    v += Lc[0 * L_AXIS + L_WENV];
-    v += Lc[1 * L_AXIS + L_WENV];
-    v += Lc[2 * L_AXIS + L_WENV];
-    v -= 1.0;
+    if (K.want_g) {  // the three terms parked by sq_axis_item
+      v += gk[1];
+      v += gk[2];
+      v += gk[3];
+      v -= 1.0;
+    }
     const double ej0 = K.EJ[0] * Lc[0 * L_AXIS + L_PM1];
     const double ej1 = K.EJ[1] * Lc[1 * L_AXIS + L_PM1];
     const double ej2 = K.EJ[2] * Lc[2 * L_AXIS + L_PM1];
@@ -1169,7 +1178,7 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
       const int j = it % n_sq, ka = it / n_sq;
       const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
       const int k = ka / 3, a = ka - 3 * k;
-      sq_axis_item(K, X + r * n, k, a, L + r * K.LR + k * SQ_L);
+      sq_axis_item(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m);
     }
     __syncthreads();
   }
@@ -1404,7 +1413,7 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
           const int j = it % n_sq, ka = it / n_sq;
           const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
           const int k = ka / 3, a = ka - 3 * k;
-          sq_axis_item(K, X + r * n, k, a, L + r * K.LR + k * SQ_L);
+          sq_axis_item(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m);
         }
       }
       lds_barrier();
