@@ -93,6 +93,21 @@ class SolveOptions(ctypes.Structure):
     ]
 
 
+class DerivativeReport(ctypes.Structure):
+    """cpl_derivative_report (include/cpl_mi355x.h)."""
+
+    _fields_ = [
+        ("n_checked", c_int64),
+        ("n_flagged", c_int64),
+        ("max_rel_error", c_double),
+        ("worst_instance", c_int64),
+        ("worst_row", c_int32),
+        ("worst_col", c_int32),
+        ("worst_exact", c_double),
+        ("worst_approx", c_double),
+    ]
+
+
 HESSIAN_EXACT = 0
 HESSIAN_LIMITED_MEMORY = 1
 HESSIAN_FD = 2
@@ -139,6 +154,15 @@ SIGNATURES = {
         c_int32,
         [_DESC_P, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_int32, c_void_p, c_int32, _DP],
+    ),
+    "cpl_eval_batch_host": (
+        c_int32,
+        [_DESC_P, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32],
+    ),
+    "cpl_derivative_test": (
+        c_int32,
+        [_DESC_P, c_int64, c_void_p, c_void_p, c_void_p, c_double, c_double, c_void_p, POINTER(DerivativeReport),
+         c_void_p],
     ),
     "cpl_kkt_workspace_doubles": (c_int64, [c_int32, c_int32]),
     "cpl_lagrangian_hessian": (c_int32, [_DESC_P, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,

@@ -17,7 +17,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libcpl_mi355x.so")
 
-SOURCES = ["cpl_host.cpp", "cpl_kernels.hip", "cpl_kkt.hip", "cpl_ipm.hip", "cpl_solver.hip"]
+SOURCES = ["cpl_host.cpp", "cpl_kernels.hip", "cpl_kkt.hip", "cpl_ipm.hip", "cpl_solver.hip", "cpl_check.hip"]
 HEADERS = ["cpl_layout.hpp", "cpl_status.hpp", "cpl_wave.hpp"]
 
 HIPCC_FLAGS = [

@@ -81,6 +81,19 @@ bool NativeSolver::Solve(CplTNLP& nlp) {
   const int32_t n = prob->n();
   std::vector<double> x0(n), x(n);
   nlp.get_starting_point(n, true, x0.data());
+  _dreport = cpl_derivative_report{};
+  if (_opt.derivative_test) {  // IPOPT checks the first derivatives before it iterates
+    double* dx = nullptr;
+    hip_check(hipMalloc(&dx, 8 * (size_t)n), "hipMalloc");
+    hipError_t e = hipMemcpy(dx, x0.data(), 8 * (size_t)n, hipMemcpyHostToDevice);
+    const int32_t st = e == hipSuccess ? cpl_derivative_test(&prob->Desc(), 1, dx, nullptr, nullptr,
+                                                             _opt.derivative_test_perturbation,
+                                                             _opt.derivative_test_tol, nullptr, &_dreport, nullptr)
+                                       : CPL_OK;
+    (void)hipFree(dx);
+    hip_check(e, "hipMemcpy x0");
+    engine_check(st);
+  }
   BatchSolver bs(prob, 1, _opt);
   bs.Solve(x0.data(), nullptr, x.data(), nullptr, &_status, &_iterations, nullptr, &_primal_inf);
   nlp.finalize_solution(n, x.data());

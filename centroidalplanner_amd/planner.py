@@ -66,11 +66,17 @@ class CentroidalPlanner:
         self.solver_tol = 1e-8
         self.solver_max_iter = 3000
         self.solver_hessian = "limited-memory"
+        # src/CentroidalPlanner.cpp:26 SetOption("derivative_test", "first-order"): IPOPT checks the
+        # first derivatives at the start point of every solve; the report lands here
+        self.solver_derivative_test = "first-order"
+        self.last_derivative_report = None
 
     # ---- Solve (src/CentroidalPlanner.cpp:22-34) ------------------------------------------
     def Solve(self) -> Solution:
         res = solve(self._cpl_problem, evaluator=self.evaluator, tol=self.solver_tol, max_iter=self.solver_max_iter,
-                    hessian=self.solver_hessian)
+                    hessian=self.solver_hessian,
+                    derivative_test=self.solver_derivative_test if self.evaluator is None else "none")
+        self.last_derivative_report = res.derivative_report
         sol = self._cpl_problem.GetSolution()
         out = Solution(com_sol=sol["com"], success=res.success, message=res.status)
         for name, cv in sol["contact_values_map"].items():

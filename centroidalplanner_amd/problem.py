@@ -326,12 +326,71 @@ class CplProblem:
     def SetVariables(self, x):
         self._x = np.asarray(x, dtype=np.float64).reshape(self.n).copy()
 
-    def _eval_one(self, x, want):
+    def eval_batch_host(self, x, mass=None, env_tag=None, outputs: Iterable[str] = ("g", "jac"),
+                        jac_folded: bool = False):
+        """cpl_eval_batch_host: numpy arrays in and out, evaluated by the GPU kernel (staged through
+        the library's device workspace; synchronous).  x: [B, n]; mass: [B] or None; env_tag: uint8
+        [B] (mixed only); outputs: subset of {"g", "jac", "f", "grad", "norms"}."""
+        n, m, nnz = self._dims()
+        x = np.ascontiguousarray(np.asarray(x, dtype=np.float64).reshape(-1, n))
+        B = x.shape[0]
+        outputs = tuple(outputs)
+        if "norms" in outputs and "g" not in outputs:
+            raise InvalidArgument(_abi.ERR_INVALID_ARGUMENT, "'norms' needs the 'g' output")
+        if jac_folded:
+            nf = ctypes.c_int32()
+            check(lib.cpl_jac_fold_info(ctypes.byref(self.desc()), ctypes.byref(nf), None, None, None, None))
+            nnz = nf.value
+        shapes = {"g": (B, m), "jac": (B, nnz), "f": (B,), "grad": (B, n), "norms": (2,)}
+        res = {}
+        for k in outputs:
+            if k not in shapes:
+                raise InvalidArgument(_abi.ERR_INVALID_ARGUMENT, f"unknown output '{k}'")
+            res[k] = np.empty(shapes[k])
+        if mass is not None:
+            mass = np.ascontiguousarray(np.asarray(mass, dtype=np.float64).reshape(B))
+        if env_tag is not None:
+            env_tag = np.ascontiguousarray(np.asarray(env_tag, dtype=np.uint8).reshape(B))
+
+        def p(a):
+            return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+        flags = _abi.EVAL_JAC_FOLDED if jac_folded else 0
+        check(lib.cpl_eval_batch_host(ctypes.byref(self.desc()), B, p(x), p(mass), p(env_tag), p(res.get("g")),
+                                      p(res.get("jac")), p(res.get("f")), p(res.get("grad")), p(res.get("norms")),
+                                      flags))
+        return res
+
+    def derivative_test(self, x, mass=None, env_tag=None, perturbation: float = 1e-8, tol: float = 1e-4,
+                        per_instance: bool = False, stream=None):
+        """IPOPT's first-order derivative checker over a batch (cpl_derivative_test; the reference runs
+        it on every solve, src/CentroidalPlanner.cpp:26).  x: float64 CUDA tensor [B, n].  Returns a
+        dict with n_checked, n_flagged, max_rel_error, worst_instance / row (-1 = objective gradient)
+        / col / exact / approx, and ``flagged`` (int32 tensor [B]) when per_instance."""
         import torch
 
-        xt = torch.as_tensor(np.asarray(x, dtype=np.float64).reshape(1, -1), device="cuda")
-        out = self.eval_batch(xt, outputs=want)
-        return {k: v[0].cpu().numpy() for k, v in out.items()}
+        n, _, _ = self._dims()
+        if x.dtype != torch.float64 or not x.is_cuda or x.dim() != 2 or x.shape[1] != n or not x.is_contiguous():
+            raise InvalidArgument(_abi.ERR_INVALID_ARGUMENT, f"x must be a contiguous float64 CUDA tensor [B, {n}]")
+        B = x.shape[0]
+        flagged = torch.zeros(B, dtype=torch.int32, device=x.device) if per_instance else None
+        rep = _abi.DerivativeReport()
+        s = stream if stream is not None else torch.cuda.current_stream(x.device)
+
+        def p(t):
+            return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+        check(lib.cpl_derivative_test(ctypes.byref(self.desc()), B, p(x), p(mass), p(env_tag), float(perturbation),
+                                      float(tol), p(flagged), ctypes.byref(rep), ctypes.c_void_p(s.cuda_stream)))
+        out = {k: getattr(rep, k) for k, _ in _abi.DerivativeReport._fields_}
+        if per_instance:
+            out["flagged"] = flagged
+        return out
+
+    def _eval_one(self, x, want):
+        # the single-instance IFOPT-style callback path: host arrays through cpl_eval_batch_host
+        out = self.eval_batch_host(np.asarray(x, dtype=np.float64).reshape(1, -1), outputs=want)
+        return {k: v[0] for k, v in out.items()}
 
     def eval_f(self, x) -> float:
         return float(self._eval_one(x, ("f",))["f"])

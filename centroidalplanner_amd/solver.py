@@ -25,6 +25,7 @@ class SolveResult:
     status: str
     iterations: int
     primal_inf: float
+    derivative_report: Optional[dict] = None  # derivative_test = "first-order" (cpl_derivative_test)
 
 
 class TorchEvaluator:
@@ -66,17 +67,24 @@ class _HostBatchEvaluator:
 
 
 def solve(problem, evaluator=None, x0: Optional[np.ndarray] = None, tol: float = 1e-8, max_iter: int = 3000,
-          hessian: str = "limited-memory") -> SolveResult:
+          hessian: str = "limited-memory", derivative_test: str = "none") -> SolveResult:
     """One instance through the batched solve loop.  hessian: "limited-memory" (IFOPT's default, as
-    the reference runs) or "exact" (the analytic Lagrangian Hessian)."""
+    the reference runs) or "exact" (the analytic Lagrangian Hessian).  derivative_test:
+    "first-order" runs IPOPT's first-order derivative checker at the start point first, as the
+    reference's solver option does (src/CentroidalPlanner.cpp:26); its report is returned."""
+    if derivative_test not in ("none", "first-order"):
+        raise ValueError(f"derivative_test must be 'none' or 'first-order', not {derivative_test!r}")
     import torch
 
     from .batch_ipm import STATUS_ACCEPTABLE, STATUS_NAMES, batch_ipm_solve
 
     xl, xu, _, _ = problem.get_bounds_info()
     x0 = np.clip(problem.get_starting_point() if x0 is None else np.asarray(x0, dtype=np.float64), xl, xu)
+    report = None
     if evaluator is None:
         X0 = torch.as_tensor(x0[None], device=torch.device("cuda", torch.cuda.current_device()))
+        if derivative_test == "first-order":
+            report = problem.derivative_test(X0)
         r = batch_ipm_solve(problem, X0, None, tol=tol, max_iter=max_iter, hessian=hessian)
     else:
         r = batch_ipm_solve(problem, torch.as_tensor(x0[None]), None, evaluator=_HostBatchEvaluator(evaluator),
@@ -85,4 +93,4 @@ def solve(problem, evaluator=None, x0: Optional[np.ndarray] = None, tol: float =
     st = int(r.status[0])
     problem.SetVariables(x)  # the next Solve warm-starts here, like the reference's persistent variables
     return SolveResult(x, st <= STATUS_ACCEPTABLE, STATUS_NAMES.get(st, f"status {st}"), int(r.iterations[0]),
-                       float(r.primal_inf[0]))
+                       float(r.primal_inf[0]), report)

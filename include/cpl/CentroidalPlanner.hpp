@@ -36,6 +36,12 @@ struct SolveOptions : cpl_solve_options {
     cpl_solve_options_default(this);
     hessian = CPL_HESSIAN_LIMITED_MEMORY;
   }
+  // src/CentroidalPlanner.cpp:26 SetOption("derivative_test", "first-order"): IPOPT's first-order
+  // derivative checker at the start point of every solve (cpl_derivative_test); NativeSolver keeps
+  // the report.  IPOPT's defaults for the perturbation and the tolerance.
+  bool derivative_test = true;
+  double derivative_test_perturbation = 1e-8;
+  double derivative_test_tol = 1e-4;
 };
 
 // Many instances of one problem template solved at once on the GPU by the native engine
@@ -74,11 +80,14 @@ class NativeSolver : public NlpSolver {
   int32_t status() const { return _status; }        // CPL_SOLVE_*
   int32_t iterations() const { return _iterations; }
   double primal_inf() const { return _primal_inf; }
+  // the derivative checker's report of the last Solve (n_checked == 0 when it did not run)
+  const cpl_derivative_report& derivative_report() const { return _dreport; }
 
  private:
   SolveOptions _opt;
   int32_t _status = -1, _iterations = 0;
   double _primal_inf = 0.0;
+  cpl_derivative_report _dreport{};
 };
 }  // namespace solver
 

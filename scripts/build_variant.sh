@@ -7,4 +7,4 @@ mkdir -p "$root/build/include"
 cp "$root/include/cpl_mi355x.h" "$root/build/include/"
 sed -i 's#../../include/cpl_mi355x.h#../include/cpl_mi355x.h#' "$src/cpl_layout.hpp"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fno-fast-math -std=c++17 -fPIC -shared -w \
-  "$src/cpl_host.cpp" "$src/cpl_kernels.hip" "$src/cpl_kkt.hip" "$src/cpl_ipm.hip" "$src/cpl_solver.hip" -o "$root/build/$name.so"
+  "$src/cpl_host.cpp" "$src/cpl_kernels.hip" "$src/cpl_kkt.hip" "$src/cpl_ipm.hip" "$src/cpl_solver.hip" "$src/cpl_check.hip" -o "$root/build/$name.so"

@@ -368,6 +368,11 @@ static void test_testbasic_native() {
     }
     cpl.SetSolver(st);
     solver::Solution sol = cpl.Solve();
+    {  // derivative_test = first-order ran at the start point (src/CentroidalPlanner.cpp:26)
+      const cpl_derivative_report& dr = st->inner.derivative_report();
+      CHECK(dr.n_checked == 39 * (30 + 1));
+      CHECK(dr.max_rel_error == dr.max_rel_error && dr.worst_row >= -1 && dr.worst_col >= 0);
+    }
     for (const auto& e : sol.contact_values_map) {
       NEAR(e.second.position_value[2], 0.1, 1e-6);
       NEAR(norm3(e.second.normal_value), 1.0, 1e-6);
