@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <string>
 
 #include "cpl_status.hpp"
@@ -698,6 +699,512 @@ __global__ __launch_bounds__(256) void cpl_lagrangian_grad_kernel(int64_t total,
   out[e] = s;
 }
 
+// ==========================================================================================
+// One wave per system, size-specialised (NW x MM known at compile time, NW <= 64): the same
+// null-space step with the same inertia correction as the workgroup kernel above, but every phase
+// runs on ONE wave — no workgroup barriers (the workgroup kernel parks ~75 % of its wave cycles on
+// them) — and each phase issues its memory operations in bulk before it computes, so that a step
+// pays one LDS / L2 round trip instead of one per pass:
+//   * nw-vectors live one element per lane; a lane keeps its row of every Householder vector in
+//     registers (vr[j] = v_j[lane]);
+//   * QR of A^T: reflector j by a wave sum, the trailing columns 8 lanes per column;
+//   * Z = H_0 ... H_{m-1} [0; I] (only Z, not the whole Q), 4 lanes per column;
+//   * Y p_y = Q [p_y; 0] and Y^T u = (Q^T u)[0, m) as reflector chains, two reflectors per wave
+//     sum (c_p = v_{2p}^T v_{2p+1} precomputed);
+//   * M Z a lane per row with M's column (symmetric M: coalesced) loaded 16 at a time; Z^T (M Z)
+//     a lane per upper-triangle entry through the L2-resident workspace.
+// LDS image QR | Z | L | beta | cp | 3 nw + m vector slots: 21.7 KiB at nw = 47, m = 30, i.e.
+// seven systems per CU.  Factor workspace (mode 1): QR | Z | L | beta | cp | dW, dC.
+// ==========================================================================================
+template <int NW, int MM>
+struct KktWave {
+  static constexpr int NZ = NW - MM;
+  static constexpr int NP = MM / 2;                 // reflector pairs (a lone last one when MM is odd)
+  static constexpr int NFAC = MM * NW + NW * NZ + NZ * NZ + MM + NP + 1;
+  static constexpr int LDS = ((NFAC + 3 * NW + MM) + 1) & ~1;
+  static_assert(NW <= 64 && MM <= NW, "one wave per system: nw <= 64");
+};
+
+__host__ __device__ inline int kktw_lds_doubles(int nw, int m) {
+  const int nz = nw - m;
+  return ((m * nw + nw * nz + nz * nz + m + m / 2 + 1 + 3 * nw + m) + 1) & ~1;
+}
+
+// two wave sums, their DPP chains interleaved (the result in every lane)
+__device__ __forceinline__ void wave_sum2(double a, double b, double& A, double& B) {
+  a += dpp_mov<DPP_QUAD_XOR1>(a);
+  b += dpp_mov<DPP_QUAD_XOR1>(b);
+  a += dpp_mov<DPP_QUAD_XOR2>(a);
+  b += dpp_mov<DPP_QUAD_XOR2>(b);
+  a += dpp_mov<DPP_ROW_HALF_MIRROR>(a);
+  b += dpp_mov<DPP_ROW_HALF_MIRROR>(b);
+  a += dpp_mov<DPP_ROW_MIRROR>(a);
+  b += dpp_mov<DPP_ROW_MIRROR>(b);
+  a += dpp_mov<DPP_ROW_BCAST15, 0xa>(a, 0.0);
+  b += dpp_mov<DPP_ROW_BCAST15, 0xa>(b, 0.0);
+  a += dpp_mov<DPP_ROW_BCAST31, 0xc>(a, 0.0);
+  b += dpp_mov<DPP_ROW_BCAST31, 0xc>(b, 0.0);
+  A = wave_bcast(a, 63);
+  B = wave_bcast(b, 63);
+}
+
+// The lane's entry of reflector j: v_j[lane] (1 at lane j, 0 above it)
+template <int NW>
+__device__ __forceinline__ double refl_entry(const double* QR, int j) {
+  const int lane = threadIdx.x & 63;
+  return (lane > j && lane < NW) ? QR[j * NW + lane] : (lane == j ? 1.0 : 0.0);
+}
+
+// x <- Q x = H_0 H_1 ... H_{MM-1} x   (bl: beta_j in lane j, cl: c_p in lane p).  Rolled over the
+// reflector pairs with the next pair's entries loaded one step ahead: two reflectors per wave-sum
+// latency, a handful of VGPRs.
+template <int NW, int MM>
+__device__ __forceinline__ double chain_Q(double x, const double* QR, double bl, double cl) {
+  if constexpr (MM & 1) {
+    constexpr int j = MM - 1;
+    const double v = refl_entry<NW>(QR, j);
+    x -= wave_bcast(bl, j) * wave_sum(v * x) * v;
+  }
+  if constexpr (MM >= 2) {
+    double v0 = refl_entry<NW>(QR, MM / 2 * 2 - 2), v1 = refl_entry<NW>(QR, MM / 2 * 2 - 1);
+    #pragma unroll 1
+    for (int p = MM / 2 - 1; p >= 0; --p) {  // H_{2p} H_{2p+1}: s1 first, s0 corrected by c_p
+      const int j = 2 * p;
+      const double n0 = p > 0 ? refl_entry<NW>(QR, j - 2) : 0.0, n1 = p > 0 ? refl_entry<NW>(QR, j - 1) : 0.0;
+      double A0, A1;
+      wave_sum2(v0 * x, v1 * x, A0, A1);
+      const double s1 = wave_bcast(bl, j + 1) * A1;
+      const double s0 = wave_bcast(bl, j) * (A0 - s1 * wave_bcast(cl, p));
+      x -= s1 * v1 + s0 * v0;
+      v0 = n0;
+      v1 = n1;
+    }
+  }
+  return x;
+}
+
+// x <- Q^T x = H_{MM-1} ... H_1 H_0 x
+template <int NW, int MM>
+__device__ __forceinline__ double chain_Qt(double x, const double* QR, double bl, double cl) {
+  if constexpr (MM >= 2) {
+    double v0 = refl_entry<NW>(QR, 0), v1 = refl_entry<NW>(QR, 1);
+    #pragma unroll 1
+    for (int p = 0; p < MM / 2; ++p) {  // H_{2p+1} H_{2p}: s0 first, s1 corrected by c_p
+      const int j = 2 * p;
+      const bool more = p + 1 < MM / 2;
+      const double n0 = more ? refl_entry<NW>(QR, j + 2) : 0.0, n1 = more ? refl_entry<NW>(QR, j + 3) : 0.0;
+      double A0, A1;
+      wave_sum2(v0 * x, v1 * x, A0, A1);
+      const double s0 = wave_bcast(bl, j) * A0;
+      const double s1 = wave_bcast(bl, j + 1) * (A1 - s0 * wave_bcast(cl, p));
+      x -= s0 * v0 + s1 * v1;
+      v0 = n0;
+      v1 = n1;
+    }
+  }
+  if constexpr (MM & 1) {
+    constexpr int j = MM - 1;
+    const double v = refl_entry<NW>(QR, j);
+    x -= wave_bcast(bl, j) * wave_sum(v * x) * v;
+  }
+  return x;
+}
+
+// sum_{k < K} a[k * stride] * v[k] (a in global memory, v in LDS): the loads issued 16 at a time
+// before their FMAs (one L2 round trip per 16 terms, 32 VGPRs in flight)
+template <int K>
+__device__ __forceinline__ double col_dot_u(const double* a, int stride, const double* v, int vstride = 1) {
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  #pragma unroll 1
+  for (int k0 = 0; k0 < K; k0 += 16) {
+    double av[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) av[u] = k0 + u < K ? a[(k0 + u) * stride] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (k0 + u < K) s[u & 3] += av[u] * v[(k0 + u) * vstride];
+  }
+  return (s[0] + s[1]) + (s[2] + s[3]);
+}
+
+// The null-space solve on one wave.  q1v (lanes < NW), q2v (lanes < MM): the right-hand sides in
+// registers; returns dw in *dwv (lanes < NW) and dy in *dyv (lanes < MM).  s1, s2: LDS scratch of NW
+// doubles.  M: the system's (symmetric) M in global memory, read by columns.
+template <int NW, int MM>
+__device__ __forceinline__ void wave_null_solve_t(const double* QR, const double* Z, const double* L,
+                                                  const double* beta, const double* cp, const double* M,
+                                                  double dW, double q1v, double q2v, double* s1, double* s2,
+                                                  double* dwv, double* dyv) {
+  constexpr int NZ = NW - MM;
+  const int lane = threadIdx.x & 63;
+  // beta and c_p for the two chains (lanes j / p)
+  const double bl = lane < MM ? beta[lane] : 0.0;
+  const double cl = lane < MM / 2 ? cp[lane] : 0.0;
+  const bool rw = lane < NW;
+  const int lc = rw ? lane : 0;
+  // R^T p_y = q2   ((R^T)[i][k] = QR[i * NW + k])
+  if (lane < MM) s1[lane] = q2v;
+  __builtin_amdgcn_wave_barrier();
+  wave_trsv(MM, true, QR, NW, 1, QR, NW + 1, s1);
+  __builtin_amdgcn_wave_barrier();
+  // x = Y p_y = Q [p_y; 0]
+  double x = chain_Q<NW, MM>(lane < MM ? s1[lane] : 0.0, QR, bl, cl);
+  if (rw) s2[lane] = x;
+  __builtin_amdgcn_wave_barrier();
+  if constexpr (NZ > 0) {
+    // t = q1 - (M + dW I) Y p_y  ->  rz = Z^T t  ->  L L^T p_z = rz
+    const double mx = col_dot_u<NW>(M + lc, NW, s2);
+    if (rw) s1[lane] = q1v - dW * x - mx;
+    __builtin_amdgcn_wave_barrier();
+    double rz = 0.0;
+    if (lane < NZ) {
+      double a[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 8
+      for (int r = 0; r < NW; ++r) a[r & 3] += Z[r * NZ + lane] * s1[r];
+      rz = (a[0] + a[1]) + (a[2] + a[3]);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane < NZ) s2[lane] = rz;
+    __builtin_amdgcn_wave_barrier();
+    wave_trsv(NZ, true, L, NZ, 1, L, NZ + 1, s2);   // L y = rz
+    wave_trsv(NZ, false, L, 1, NZ, L, NZ + 1, s2);  // L^T p_z = y
+    __builtin_amdgcn_wave_barrier();
+    // dw = Y p_y + Z p_z
+    if (rw) {
+      double a[2] = {0.0, 0.0};
+#pragma unroll
+      for (int c = 0; c < NZ; ++c) a[c & 1] += Z[lane * NZ + c] * s2[c];
+      x += a[0] + a[1];
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (rw) s2[lane] = x;
+    __builtin_amdgcn_wave_barrier();
+  }
+  *dwv = x;
+  // u = q1 - (M + dW I) dw  ->  Y^T u = (Q^T u)[0, m)  ->  R dy = Y^T u
+  const double mx = col_dot_u<NW>(M + lc, NW, s2);
+  const double u = chain_Qt<NW, MM>(rw ? q1v - dW * x - mx : 0.0, QR, bl, cl);
+  __builtin_amdgcn_wave_barrier();
+  if (lane < MM) s1[lane] = u;
+  __builtin_amdgcn_wave_barrier();
+  wave_trsv(MM, false, QR, 1, NW, QR, NW + 1, s1);  // R[i][k] = QR[k * NW + i]
+  __builtin_amdgcn_wave_barrier();
+  *dyv = lane < MM ? s1[lane] : 0.0;
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int NW, int MM>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void cpl_kkt_wave_kernel(
+    int mode, int64_t batch, const double* __restrict__ Mg, const double* __restrict__ Ag,
+    const double* __restrict__ r1g, const double* __restrict__ r2g, const double* __restrict__ mug,
+    const double* __restrict__ dw_last, const uint8_t* __restrict__ active, double* __restrict__ dwg,
+    double* __restrict__ dyg, double* __restrict__ dWg, double* __restrict__ dCg, int32_t* __restrict__ info,
+    double* __restrict__ ws) {
+  using W = KktWave<NW, MM>;
+  constexpr int NZ = W::NZ, NP = W::NP, NFAC = W::NFAC;
+  constexpr int T8 = (NW + 7) / 8;   // QR update: rows per lane (8 lanes per column)
+  constexpr int P8 = (MM + 6) / 8;   // QR update: passes of 8 columns at j = 0 (MM - 1 columns)
+  constexpr int T4 = (NW + 3) / 4;   // Z: rows per lane (4 lanes per column)
+  constexpr int P4 = (NZ + 15) / 16; // Z: passes of 16 columns
+  extern __shared__ __align__(16) double sm[];
+  const int lane = threadIdx.x & 63;
+  const int64_t b = blockIdx.x;
+  if (b >= batch) return;
+  double* QR = sm;                 // [MM][NW]
+  double* Z = QR + MM * NW;        // [NW][NZ]
+  double* L = Z + NW * NZ;         // [NZ][NZ]
+  double* beta = L + NZ * NZ;      // [MM]
+  double* cp = beta + MM;          // [NP + 1]
+  double* s1 = sm + NFAC;          // [NW] scratch
+  double* s2 = s1 + NW;            // [NW] scratch
+  double* dwl = s2 + NW;           // [NW] dw (broadcast copy)
+  double* dyl = dwl + NW;          // [MM] dy (broadcast copy)
+  const double* M = Mg + b * NW * NW;
+  const double* Ab = Ag + b * MM * NW;
+  double* wsb = ws + b * kkt_ws_per(NW, MM);
+  const bool rw = lane < NW;
+  const int lc = rw ? lane : 0;
+  const double q1v = rw ? r1g[b * NW + lane] : 0.0;
+  const double q2v = lane < MM ? r2g[b * MM + lane] : 0.0;
+
+  if (active && !active[b]) {
+    if (rw) dwg[b * NW + lane] = 0.0;
+    if (lane < MM) dyg[b * MM + lane] = 0.0;
+    if (lane == 0 && mode == 0) { dWg[b] = 0.0; dCg[b] = 0.0; info[b] = 0; }
+    return;
+  }
+  if (mode == 1) {  // re-solve with the kept factors
+    for (int i = lane; i < NFAC; i += 64) sm[i] = wsb[i];
+    const double dW = wsb[NFAC];
+    __builtin_amdgcn_wave_barrier();
+    double dwv, dyv;
+    wave_null_solve_t<NW, MM>(QR, Z, L, beta, cp, M, dW, q1v, q2v, s1, s2, &dwv, &dyv);
+    if (rw) dwg[b * NW + lane] = dwv;
+    if (lane < MM) dyg[b * MM + lane] = dyv;
+    return;
+  }
+
+  // ---- Householder QR of A^T (row j of QR = column j of A^T)
+  for (int i = lane; i < MM * NW; i += 64) QR[i] = Ab[i];
+  __builtin_amdgcn_wave_barrier();
+  KKT_MARK(0);
+  #pragma unroll 1
+  for (int j = 0; j < MM; ++j) {
+    double* x = QR + j * NW;
+    const bool below = lane > j && lane < NW;
+    const double xi = below ? x[lane] : 0.0;
+    const double alpha = x[j];
+    const double sig = wave_sum(xi * xi);
+    double bj = 0.0;
+    if (sig != 0.0) {
+      const double nrm = sqrt(alpha * alpha + sig);
+      const double v0 = alpha <= 0.0 ? alpha - nrm : -sig / (alpha + nrm);
+      const double rv0 = 1.0 / v0;
+      if (below) x[lane] = xi * rv0;
+      bj = 2.0 * v0 * v0 / (sig + v0 * v0);
+      if (lane == 0) x[j] = nrm;  // R_jj on the diagonal
+    }
+    if (lane == 0) beta[j] = bj;
+    if (bj != 0.0 && j + 1 < MM) {
+      // columns k > j: 8 lanes per column, 8 columns per pass, every pass's loads issued first;
+      // the lane's rows i = j + part + 8t, its reflector entries from the other lanes' vi
+      __builtin_amdgcn_wave_barrier();
+      const int part = lane & 7, cl8 = lane >> 3;
+      double vrow[T8];
+#pragma unroll
+      for (int t = 0; t < T8; ++t) {
+        const int i = j + part + 8 * t;
+        vrow[t] = i == j ? 1.0 : (i < NW ? x[i] : 0.0);
+      }
+      double yr[P8][T8];
+      double a[P8];
+#pragma unroll
+      for (int p = 0; p < P8; ++p) {
+        const int k = j + 1 + 8 * p + cl8;
+        const double* y = QR + (k < MM ? k : j) * NW;
+        a[p] = 0.0;
+#pragma unroll
+        for (int t = 0; t < T8; ++t) {
+          const int i = j + part + 8 * t;
+          yr[p][t] = i < NW ? y[i] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < P8; ++p) {
+#pragma unroll
+        for (int t = 0; t < T8; ++t) a[p] += vrow[t] * yr[p][t];
+        a[p] = bj * group8_sum(a[p]);
+      }
+#pragma unroll
+      for (int p = 0; p < P8; ++p) {
+        const int k = j + 1 + 8 * p + cl8;
+        if (k < MM) {
+          double* y = QR + k * NW;
+#pragma unroll
+          for (int t = 0; t < T8; ++t) {
+            const int i = j + part + 8 * t;
+            if (i < NW) y[i] = yr[p][t] - a[p] * vrow[t];
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  KKT_MARK(1);
+  // c_p = v_{2p}^T v_{2p+1} for the paired chains (lane p keeps c_p)
+  {
+    double cl = 0.0;
+    #pragma unroll 1
+    for (int p = 0; p < NP; ++p) {
+      const double c = wave_sum(refl_entry<NW>(QR, 2 * p) * refl_entry<NW>(QR, 2 * p + 1));
+      if (lane == p) cl = c;
+    }
+    if (lane < NP) cp[lane] = cl;
+  }
+  // ---- Z = H_0 ... H_{m-1} [0; I]: backward, 4 lanes per column, 16 columns per pass (rows < j of
+  // Z are still zero at step j); the lane's reflector entries come from the other lanes' vr
+  for (int e = lane; e < NW * NZ; e += 64) {
+    const int r = e / NZ, c = e - r * NZ;
+    Z[e] = r == MM + c ? 1.0 : 0.0;
+  }
+  __builtin_amdgcn_wave_barrier();
+  #pragma unroll 1
+  for (int j = MM - 1; j >= 0; --j) {
+    const double bj = beta[j];
+    if (bj == 0.0) continue;
+    const double* v = QR + j * NW;
+    const int part = lane & 3, c16 = lane >> 2;
+    double vrow[T4];
+#pragma unroll
+    for (int t = 0; t < T4; ++t) {
+      const int i = j + part + 4 * t;
+      vrow[t] = i == j ? 1.0 : (i < NW ? v[i] : 0.0);
+    }
+    double zr[P4][T4];
+    double a[P4];
+#pragma unroll
+    for (int p = 0; p < P4; ++p) {
+      const int c = 16 * p + c16;
+      const int cc = c < NZ ? c : 0;
+      a[p] = 0.0;
+#pragma unroll
+      for (int t = 0; t < T4; ++t) {
+        const int i = j + part + 4 * t;
+        zr[p][t] = i < NW ? Z[i * NZ + cc] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < P4; ++p) {
+#pragma unroll
+      for (int t = 0; t < T4; ++t) a[p] += vrow[t] * zr[p][t];
+      a[p] = bj * group4_sum(a[p]);
+    }
+#pragma unroll
+    for (int p = 0; p < P4; ++p) {
+      const int c = 16 * p + c16;
+      if (c < NZ) {
+#pragma unroll
+        for (int t = 0; t < T4; ++t) {
+          const int i = j + part + 4 * t;
+          if (i < NW) Z[i * NZ + c] = zr[p][t] - a[p] * vrow[t];
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  KKT_MARK(2);
+  // ---- rank deficiency: delta_c on R's diagonal
+  double dC = 0.0;
+  bool rank_def = false;
+  {
+    const double rjj = lane < MM ? QR[lane * NW + lane] : 0.0;
+    const double rmax = wave_max(fabs(rjj));
+    const bool defl = lane < MM && (!(fabs(rjj) >= 1e-10 * rmax) || rmax == 0.0);
+    rank_def = __ballot(defl) != 0ull;
+    if (rank_def) {
+      const double dc = 1e-8 * pow(mug[b], 0.25) * (rmax > 0.0 ? rmax : 1.0);
+      if (defl) QR[lane * NW + lane] = rjj < 0.0 ? rjj - dc : rjj + dc;
+      dC = dc;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  // ---- reduced Hessian Hr = Z^T (M Z): M Z a lane per row through the global workspace (L2),
+  // Hr's upper triangle a lane per entry, mirrored; the unshifted copy stays in the workspace
+  double dW = 0.0;
+  int32_t inf = 0;
+  if constexpr (NZ > 0) {
+    double* MZ = wsb;             // [NW][NZ] scratch (the factors overwrite it at the end)
+    double* Hs = wsb + NW * NZ;   // [NZ][NZ] scratch
+    {
+      // a lane per row r: acc[c] = sum_k M[k][r] Z[k][c]; M's column in chunks of 8, the next chunk's
+      // loads issued before the current chunk's FMAs
+      double acc[NZ];
+#pragma unroll
+      for (int c = 0; c < NZ; ++c) acc[c] = 0.0;
+      const double* mc = M + lc;  // column `lane` = row `lane` (M symmetric)
+      double mk[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) mk[u] = mc[u * NW];
+      #pragma unroll 1
+      for (int k0 = 0; k0 < NW; k0 += 8) {
+        double mn[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) mn[u] = k0 + 8 + u < NW ? mc[(k0 + 8 + u) * NW] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (k0 + u < NW) {
+            const double* zk = Z + (k0 + u) * NZ;
+#pragma unroll
+            for (int c = 0; c < NZ; ++c) acc[c] += mk[u] * zk[c];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) mk[u] = mn[u];
+      }
+      if (rw) {
+#pragma unroll
+        for (int c = 0; c < NZ; ++c) MZ[lane * NZ + c] = acc[c];
+      }
+    }
+    __threadfence_block();  // the lanes' M Z stores before the other lanes' loads
+    constexpr int NTRI = NZ * (NZ + 1) / 2;
+    for (int e = lane; e < NTRI; e += 64) {
+      int a = 0, rem = e;
+      while (rem >= NZ - a) { rem -= NZ - a; ++a; }
+      const int c = a + rem;
+      const double h = col_dot_u<NW>(MZ + c, NZ, Z + a, NZ);
+      Hs[a * NZ + c] = h;
+      Hs[c * NZ + a] = h;
+      L[a * NZ + c] = h;
+      L[c * NZ + a] = h;
+    }
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    KKT_MARK(3);
+    // ---- inertia correction: Cholesky of Hr + delta_w I, IPOPT's delta_w schedule (as the
+    // workgroup kernel: pivots at or below DBL_EPSILON max|M_ii| count as zero)
+    const double last = dw_last ? dw_last[b] : 0.0;
+    const double mmax = wave_max(rw ? fabs(M[lane * NW + lane]) : 0.0);
+    const double pivot_min = 2.220446049250313e-16 * mmax;
+    #pragma unroll 1
+    for (int attempt = 0; attempt < 64; ++attempt) {
+      if (attempt > 0) {
+        for (int e = lane; e < NZ * NZ; e += 64) L[e] = Hs[e] + ((e / NZ == e % NZ) ? dW : 0.0);
+        __builtin_amdgcn_wave_barrier();
+      }
+      if (wave_cholesky(L, NZ, pivot_min)) break;
+      if (dW == 0.0) dW = last == 0.0 ? 1e-4 : fmax(1e-20, last / 3.0);
+      else dW *= last == 0.0 ? 100.0 : 8.0;
+      if (dW > 1e40) { inf = 1; break; }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (lane == 0 && info) info[b] = inf;
+  KKT_MARK(4);
+  // ---- solve, then one step of iterative refinement on the unregularised system (one inlined
+  // copy of the solve: pass 1 solves for the correction of pass 0's residual)
+  double dwv = 0.0, dyv = 0.0;
+  double r1v = q1v, r2v = q2v;
+  #pragma unroll 1
+  for (int pass = 0; pass < 2; ++pass) {
+    double c1, c2;
+    wave_null_solve_t<NW, MM>(QR, Z, L, beta, cp, M, dW, r1v, r2v, s1, s2, &c1, &c2);
+    if (pass == 0) {
+      dwv = c1;
+      dyv = c2;
+    } else {
+      dwv += c1;
+      dyv += c2;
+    }
+    KKT_MARK(5);
+    if (pass == 1 || rank_def) break;
+    if (rw) dwl[lane] = dwv;
+    if (lane < MM) dyl[lane] = dyv;
+    __builtin_amdgcn_wave_barrier();
+    // e1 = q1 - dW dw - A^T dy - M dw,  e2 = q2 - A dw
+    const double aty = col_dot_u<MM>(Ab + lc, NW, dyl);
+    const double mdw = col_dot_u<NW>(M + lc, NW, dwl);
+    const double e1 = rw ? q1v - dW * dwv - aty - mdw : 0.0;
+    const double adw = col_dot_u<NW>(Ab + (lane < MM ? lane : 0) * NW, 1, dwl);
+    const double e2 = lane < MM ? q2v - adw : 0.0;
+    const double rmax = wave_max(fmax(fabs(e1), fabs(e2)));
+    const double qmax = wave_max(fmax(fabs(q1v), fabs(q2v)));
+    if (rmax <= 1e-13 * qmax) break;  // refine only above 1e-13 of the right-hand side
+    r1v = e1;
+    r2v = e2;
+    __builtin_amdgcn_wave_barrier();
+  }
+  KKT_MARK(6);
+  if (rw) dwg[b * NW + lane] = dwv;
+  if (lane < MM) dyg[b * MM + lane] = dyv;
+  if (lane == 0) { dWg[b] = dW; dCg[b] = dC; }
+  // keep the factors for mode 1 (every scratch read above is done: same wave, program order)
+  __threadfence_block();
+  for (int i = lane; i < NFAC; i += 64) wsb[i] = sm[i];
+  if (lane == 0) { wsb[NFAC] = dW; wsb[NFAC + 1] = dC; }
+  KKT_MARK(7);
+}
+
 }  // namespace cpl
 
 using namespace cpl;
@@ -711,6 +1218,23 @@ using KktKernel = void (*)(int, int64_t, int, int, const double*, const double*,
 static inline KktKernel kkt_kernel_for(int nw, int m) {
   if (nw == 47 && m == 30) return cpl_kkt_kernel<47, 30>;
   return cpl_kkt_kernel<0, 0>;
+}
+using KktWaveKernel = void (*)(int, int64_t, const double*, const double*, const double*, const double*,
+                              const double*, const double*, const uint8_t*, double*, double*, double*, double*,
+                              int32_t*, double*);
+
+// The one-wave kernel for the sizes it is specialised for (the 4-contact solve loop's nw 47, m 30),
+// nullptr otherwise.  CPL_KKT_KERNEL=block forces the workgroup kernel (a measurement-only switch,
+// read once).  Both kernels keep their factors in the same workspace size but in their own
+// layouts: a mode 1 call follows a mode 0 call of the same kernel (the choice is per size).
+static KktWaveKernel kkt_wave_kernel_for(int nw, int m) {
+  static const bool forced_block = [] {
+    const char* e = std::getenv("CPL_KKT_KERNEL");
+    return e && std::string(e) == "block";
+  }();
+  if (forced_block) return nullptr;
+  if (nw == 47 && m == 30) return cpl_kkt_wave_kernel<47, 30>;
+  return nullptr;
 }
 
 extern "C" {
@@ -751,11 +1275,17 @@ int32_t cpl_kkt_solve(int32_t mode, int64_t batch, int32_t nw, int32_t m, const 
   if (mode == 0 && (!d_mu || !d_delta_w || !d_delta_c || !d_info))
     return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_solve: factorisation needs mu, delta_w, delta_c, info");
   if (batch > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_solve: batch too large");
-  const size_t lds = sizeof(double) * (size_t)kkt_launch_lds_doubles(nw, m, mode);
-  if (lds > 160 * 1024) return fail(CPL_ERR_UNSUPPORTED, "cpl_kkt_solve: system too large for one LDS image");
-  hipLaunchKernelGGL(kkt_kernel_for(nw, m), dim3((unsigned)batch), dim3(KKT_THREADS), lds, (hipStream_t)stream, (int)mode,
-                     batch, (int)nw, (int)m, d_M, d_A, d_r1, d_r2, d_mu, d_delta_w_last, d_active, d_dw, d_dy,
-                     d_delta_w, d_delta_c, d_info, d_ws);
+  if (KktWaveKernel wk = kkt_wave_kernel_for(nw, m)) {
+    const size_t lds = sizeof(double) * (size_t)kktw_lds_doubles(nw, m);
+    hipLaunchKernelGGL(wk, dim3((unsigned)batch), dim3(64), lds, (hipStream_t)stream, (int)mode, batch, d_M, d_A, d_r1,
+                       d_r2, d_mu, d_delta_w_last, d_active, d_dw, d_dy, d_delta_w, d_delta_c, d_info, d_ws);
+  } else {
+    const size_t lds = sizeof(double) * (size_t)kkt_launch_lds_doubles(nw, m, mode);
+    if (lds > 160 * 1024) return fail(CPL_ERR_UNSUPPORTED, "cpl_kkt_solve: system too large for one LDS image");
+    hipLaunchKernelGGL(kkt_kernel_for(nw, m), dim3((unsigned)batch), dim3(KKT_THREADS), lds, (hipStream_t)stream,
+                       (int)mode, batch, (int)nw, (int)m, d_M, d_A, d_r1, d_r2, d_mu, d_delta_w_last, d_active, d_dw,
+                       d_dy, d_delta_w, d_delta_c, d_info, d_ws);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_kkt_kernel launch: ") + hipGetErrorString(e));
   return CPL_OK;

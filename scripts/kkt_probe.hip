@@ -91,8 +91,12 @@ int main(int argc, char** argv) {
     if (mode == 0) {
       std::vector<long long> prof((size_t)B * 8);
       CK(hipMemcpy(prof.data(), dprof, prof.size() * 8, hipMemcpyDeviceToHost));
-      const char* names[7] = {"QR", "Q accumulation", "rank + Z^T M Z", "inertia/Cholesky", "solve",
-                              "refinement", "store factors"};
+      const char* block_names[7] = {"QR", "Q accumulation", "rank + Z^T M Z", "inertia/Cholesky", "solve",
+                                    "refinement", "store factors"};
+      const char* wave_names[7] = {"QR", "Z accumulation", "rank + Z^T M Z", "inertia/Cholesky", "solve",
+                                   "refinement", "store factors"};
+      const char* const* names = kkt_wave_kernel_for(nw, m) ? wave_names : block_names;
+      std::printf("  (%s kernel)\n", kkt_wave_kernel_for(nw, m) ? "one-wave" : "workgroup");
       for (int p = 0; p < 7; ++p) {
         double s = 0.0;
         for (int b = 0; b < B; ++b) s += (double)(prof[(size_t)b * 8 + p + 1] - prof[(size_t)b * 8 + p]);
