@@ -22,7 +22,10 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <string>
+#include <tuple>
 
 #include "cpl_status.hpp"
 #include "cpl_wave.hpp"
@@ -1223,18 +1226,51 @@ using KktWaveKernel = void (*)(int, int64_t, const double*, const double*, const
                               const double*, const double*, const uint8_t*, double*, double*, double*, double*,
                               int32_t*, double*);
 
-// The one-wave kernel for the sizes it is specialised for (the 4-contact solve loop's nw 47, m 30),
-// nullptr otherwise.  CPL_KKT_KERNEL=block forces the workgroup kernel (a measurement-only switch,
-// read once).  Both kernels keep their factors in the same workspace size but in their own
-// layouts: a mode 1 call follows a mode 0 call of the same kernel (the choice is per size).
-static KktWaveKernel kkt_wave_kernel_for(int nw, int m) {
-  static const bool forced_block = [] {
+// The one-wave kernel for the sizes it is specialised for (the 4-contact solve loop's nw 47, m 30)
+// when it finishes first, nullptr otherwise.  Both kernels are latency-bound per system: a round of
+// resident systems takes ~0.12 ms on the workgroup kernel (4 per CU) and ~0.14 ms on the one-wave
+// kernel (7 per CU), so the workgroup kernel wins when the batch fits in as few of its rounds
+// (measured: B <= 1,024 and 2,048 on 256 CUs; the one-wave kernel from 1,536 and past 2,048).
+// The choice depends on (nw, m, batch) only, so a mode 1 call follows a mode 0 call of the same
+// kernel (their factor layouts differ).  CPL_KKT_KERNEL=block|wave forces one (measurement only).
+static KktWaveKernel kkt_wave_kernel_for(int nw, int m, int64_t batch) {
+  static const int forced = [] {
     const char* e = std::getenv("CPL_KKT_KERNEL");
-    return e && std::string(e) == "block";
+    if (!e) return 0;
+    return std::string(e) == "block" ? 1 : (std::string(e) == "wave" ? 2 : 0);
   }();
-  if (forced_block) return nullptr;
-  if (nw == 47 && m == 30) return cpl_kkt_wave_kernel<47, 30>;
-  return nullptr;
+  KktWaveKernel wk = nullptr;
+  if (nw == 47 && m == 30) wk = cpl_kkt_wave_kernel<47, 30>;
+  if (!wk || forced == 1) return nullptr;
+  if (forced == 2) return wk;
+  struct Occ {
+    int cus = 0, per_block = 0, per_wave = 0;
+  };
+  static std::mutex mu;
+  static std::map<std::tuple<int, int, int>, Occ> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return wk;
+  Occ o;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find({dev, nw, m});
+    if (it != cache.end()) {
+      o = it->second;
+    } else {
+      if (hipDeviceGetAttribute(&o.cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per_block, reinterpret_cast<const void*>(kkt_kernel_for(nw, m)),
+                                                       KKT_THREADS, sizeof(double) * kkt_launch_lds_doubles(nw, m, 0)) !=
+              hipSuccess ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per_wave, reinterpret_cast<const void*>(wk), 64,
+                                                       sizeof(double) * kktw_lds_doubles(nw, m)) != hipSuccess)
+        return wk;
+      cache[{dev, nw, m}] = o;
+    }
+  }
+  if (o.cus <= 0 || o.per_block <= 0 || o.per_wave <= 0) return wk;
+  const int64_t rb = (batch + (int64_t)o.cus * o.per_block - 1) / ((int64_t)o.cus * o.per_block);
+  const int64_t rw = (batch + (int64_t)o.cus * o.per_wave - 1) / ((int64_t)o.cus * o.per_wave);
+  return 1.17 * (double)rw < (double)rb ? wk : nullptr;
 }
 
 extern "C" {
@@ -1275,7 +1311,7 @@ int32_t cpl_kkt_solve(int32_t mode, int64_t batch, int32_t nw, int32_t m, const 
   if (mode == 0 && (!d_mu || !d_delta_w || !d_delta_c || !d_info))
     return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_solve: factorisation needs mu, delta_w, delta_c, info");
   if (batch > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_solve: batch too large");
-  if (KktWaveKernel wk = kkt_wave_kernel_for(nw, m)) {
+  if (KktWaveKernel wk = kkt_wave_kernel_for(nw, m, batch)) {
     const size_t lds = sizeof(double) * (size_t)kktw_lds_doubles(nw, m);
     hipLaunchKernelGGL(wk, dim3((unsigned)batch), dim3(64), lds, (hipStream_t)stream, (int)mode, batch, d_M, d_A, d_r1,
                        d_r2, d_mu, d_delta_w_last, d_active, d_dw, d_dy, d_delta_w, d_delta_c, d_info, d_ws);

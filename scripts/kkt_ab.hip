@@ -93,7 +93,7 @@ int main(int argc, char** argv) {
                              m, dM, dA, dr1, dr2, dmu, dlast, nullptr, dw[v], dy[v], dW[v], dC[v], info[v], dws);
         } else {
           const size_t lds = sizeof(double) * (size_t)kktw_lds_doubles(nw, m);
-          hipLaunchKernelGGL(kkt_wave_kernel_for(nw, m), dim3((unsigned)B), dim3(64), lds, 0, mode, (int64_t)B, dM, dA,
+          hipLaunchKernelGGL(kkt_wave_kernel_for(nw, m, 1 << 30), dim3((unsigned)B), dim3(64), lds, 0, mode, (int64_t)B, dM, dA,
                              dr1, dr2, dmu, dlast, nullptr, dw[v], dy[v], dW[v], dC[v], info[v], dws);
         }
         CK(hipGetLastError());
@@ -108,7 +108,7 @@ int main(int argc, char** argv) {
         CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kkt_kernel_for(nw, m)),
                                                         KKT_THREADS, sizeof(double) * kkt_launch_lds_doubles(nw, m, mode)));
       else
-        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kkt_wave_kernel_for(nw, m)),
+        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kkt_wave_kernel_for(nw, m, 1 << 30)),
                                                         64, sizeof(double) * kktw_lds_doubles(nw, m)));
       std::printf("%-5s mode %d: %.3f ms for %d systems (nw %d, m %d), %d workgroups/CU\n", names[v], mode, best, B, nw,
                   m, per_cu);
@@ -120,7 +120,7 @@ int main(int argc, char** argv) {
                          dA, dr1, dr2, dmu, dlast, nullptr, dw[v], dy[v], dW[v], dC[v], info[v], dws);
     } else {
       const size_t lds = sizeof(double) * (size_t)kktw_lds_doubles(nw, m);
-      hipLaunchKernelGGL(kkt_wave_kernel_for(nw, m), dim3((unsigned)B), dim3(64), lds, 0, 0, (int64_t)B, dM, dA, dr1,
+      hipLaunchKernelGGL(kkt_wave_kernel_for(nw, m, 1 << 30), dim3((unsigned)B), dim3(64), lds, 0, 0, (int64_t)B, dM, dA, dr1,
                          dr2, dmu, dlast, nullptr, dw[v], dy[v], dW[v], dC[v], info[v], dws);
     }
     CK(hipDeviceSynchronize());

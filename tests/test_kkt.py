@@ -1,6 +1,11 @@
 """cpl_kkt_solve (csrc/cpl_kkt.hip): the solve loop's batched Newton step on the GPU, against a dense
 numpy solve of the same KKT systems (float64; tolerance 1e-9 relative to the solution's scale, the
-systems' condition numbers are ~1e3-1e5)."""
+systems' condition numbers are ~1e3-1e5).
+
+The library picks the workgroup kernel or, for the 4-contact size (nw 47, m 30), the one-wave kernel
+by batch size (the workgroup kernel up to ~1k systems on 256 CUs, the one-wave kernel at 4,096 and
+8,192): the (47, 30) cases run at both B = 64 / 300 and B = 4,096 so that both kernels are covered
+(the dense check on a sample of the large batches)."""
 import ctypes
 
 import numpy as np
@@ -70,16 +75,22 @@ def _dense(M, A, r1, r2, dW=None):
     return out[:, :nw], out[:, nw:]
 
 
+def _sample(B):
+    return np.unique(np.concatenate([np.arange(min(B, 200)), np.arange(max(B - 100, 0), B)]))
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("nw,m", [(47, 30), (39, 14), (12, 12), (20, 0), (91, 54), (100, 70)])
-def test_kkt_matches_dense_solve(nw, m):
+@pytest.mark.parametrize("nw,m,B", [(47, 30, 300), (47, 30, 4096), (39, 14, 300), (12, 12, 300), (20, 0, 300),
+                                    (91, 54, 300), (100, 70, 300)])
+def test_kkt_matches_dense_solve(nw, m, B):
     nz = nw - m
     if 8 * (nw * nw + m * nw + nz * nz + nw + m + max(2 * nw, 3 * m) + 8) > 160 * 1024:
         pytest.skip("LDS image above 160 KiB: rejected by design")
-    B = 300
     M, A, r1, r2 = _systems(B, nw, m, seed=nw + m)
     dw, dy, dW, dC, info, _ = _run(0, M, A, r1, r2, np.full(B, 0.1))
     assert (info == 0).all() and (dW == 0).all() and (dC == 0).all()
+    idx = _sample(B)
+    M, A, r1, r2, dw, dy = M[idx], A[idx], r1[idx], r2[idx], dw[idx], dy[idx]
     rw, ry = _dense(M, A, r1, r2)
     np.testing.assert_allclose(dw, rw, rtol=0, atol=1e-9 * np.abs(rw).max())
     if m:
@@ -87,14 +98,16 @@ def test_kkt_matches_dense_solve(nw, m):
 
 
 @pytest.mark.gpu
-def test_kkt_inertia_correction_and_resolve():
-    B, nw, m = 64, 47, 30
+@pytest.mark.parametrize("B", [64, 4096])
+def test_kkt_inertia_correction_and_resolve(B):
+    nw, m = 47, 30
     M, A, r1, r2 = _systems(B, nw, m, seed=3, indefinite=True)
     dw, dy, dW, dC, info, ws = _run(0, M, A, r1, r2, np.full(B, 0.1))
     assert (info == 0).all() and (dW > 0).all()
+    idx = _sample(B)
     # the returned step solves the system with delta_w added (IPOPT's corrected system)
-    rw, ry = _dense(M, A, r1, r2, dW)
-    np.testing.assert_allclose(dw, rw, rtol=0, atol=1e-8 * np.abs(rw).max())
+    rw, ry = _dense(M[idx], A[idx], r1[idx], r2[idx], dW[idx])
+    np.testing.assert_allclose(dw[idx], rw, rtol=0, atol=1e-8 * np.abs(rw).max())
     # and the reduced Hessian of the corrected system is positive definite
     for b in range(4):
         q, _ = np.linalg.qr(A[b].T, mode="complete")
@@ -103,13 +116,14 @@ def test_kkt_inertia_correction_and_resolve():
     # mode 1: another r2 with the kept factors == a dense solve of the corrected system
     r2b = np.random.default_rng(9).normal(size=(B, m))
     dw1, dy1, *_ = _run(1, M, A, r1, r2b, np.full(B, 0.1), ws=ws)
-    rw1, _ = _dense(M, A, r1, r2b, dW)
-    np.testing.assert_allclose(dw1, rw1, rtol=0, atol=1e-7 * np.abs(rw1).max())
+    rw1, _ = _dense(M[idx], A[idx], r1[idx], r2b[idx], dW[idx])
+    np.testing.assert_allclose(dw1[idx], rw1, rtol=0, atol=1e-7 * np.abs(rw1).max())
 
 
 @pytest.mark.gpu
-def test_kkt_rank_deficient_gets_delta_c():
-    B, nw, m = 32, 47, 30
+@pytest.mark.parametrize("B", [32, 4096])
+def test_kkt_rank_deficient_gets_delta_c(B):
+    nw, m = 47, 30
     M, A, r1, r2 = _systems(B, nw, m, seed=4, rank_def=True)
     r2[:, -1] = r2[:, 0] + r2[:, 1]  # consistent right-hand side
     dw, dy, dW, dC, info, _ = _run(0, M, A, r1, r2, np.full(B, 1e-2))
