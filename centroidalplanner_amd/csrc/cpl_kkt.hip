@@ -830,6 +830,55 @@ __device__ __forceinline__ double col_dot_u(const double* a, int stride, const d
   return (s[0] + s[1]) + (s[2] + s[3]);
 }
 
+// Triangular solve T x = b on one wave with the lane's row of T in registers (one LDS round trip
+// for the whole row instead of one per step): lane r holds x_r (b_r on entry, r < N); T(r, k) =
+// T[r * si + k * sk], diagonal D[r * sd].  The same arithmetic as wave_trsv (x_i = a_i * (1 / D_i),
+// a_r -= T(r, i) x_i), so the same result bit for bit.
+template <int N, bool LOWER>
+__device__ __forceinline__ double wave_trsv_reg(const double* T, int si, int sk, const double* D, int sd, double x) {
+  const int lane = threadIdx.x & 63;
+  const bool act = lane < N;
+  const int lr = act ? lane : 0;
+  double t[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) t[k] = T[lr * si + k * sk];
+  const double inv = act ? 1.0 / D[lr * sd] : 0.0;
+#pragma unroll
+  for (int s = 0; s < N; ++s) {
+    const int i = LOWER ? s : N - 1 - s;
+    const double xi = wave_bcast(x, i) * wave_bcast(inv, i);
+    if (lane == i) x = xi;
+    if (LOWER ? (act && lane > i) : (lane < i)) x -= t[i] * xi;
+  }
+  return act ? x : 0.0;
+}
+
+// Right-looking Cholesky on one wave with lane r holding row r of the N x N matrix in a[] (the
+// lower factor replaces the lower triangle; the upper triangle is left as it was).  The same
+// operations in the same order as wave_cholesky (l_ik = a_ik * (1 / l_kk), a_ij -= l_ik l_jk), so
+// the same factor bit for bit, with no LDS round trips.  false (wave-uniform) on a pivot at or
+// below pivot_min or non-finite.
+template <int N>
+__device__ __forceinline__ bool wave_cholesky_reg(double (&a)[N], double pivot_min) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    const double d = wave_bcast(a[k], k);
+    if (!(d > pivot_min) || !(d < INFINITY)) return false;
+    const double lkk = sqrt(d);
+    const double inv = 1.0 / lkk;
+    const double lik = lane > k ? a[k] * inv : 0.0;
+    if (lane == k) a[k] = lkk;
+    if (lane > k) a[k] = lik;
+#pragma unroll
+    for (int j = k + 1; j < N; ++j) {
+      const double ljk = wave_bcast(lik, j);
+      if (lane >= j) a[j] -= lik * ljk;
+    }
+  }
+  return true;
+}
+
 // The null-space solve on one wave.  q1v (lanes < NW), q2v (lanes < MM): the right-hand sides in
 // registers; returns dw in *dwv (lanes < NW) and dy in *dyv (lanes < MM).  s1, s2: LDS scratch of NW
 // doubles.  M: the system's (symmetric) M in global memory, read by columns.
@@ -846,12 +895,9 @@ __device__ __forceinline__ void wave_null_solve_t(const double* QR, const double
   const bool rw = lane < NW;
   const int lc = rw ? lane : 0;
   // R^T p_y = q2   ((R^T)[i][k] = QR[i * NW + k])
-  if (lane < MM) s1[lane] = q2v;
-  __builtin_amdgcn_wave_barrier();
-  wave_trsv(MM, true, QR, NW, 1, QR, NW + 1, s1);
-  __builtin_amdgcn_wave_barrier();
+  const double py = wave_trsv_reg<MM, true>(QR, NW, 1, QR, NW + 1, lane < MM ? q2v : 0.0);
   // x = Y p_y = Q [p_y; 0]
-  double x = chain_Q<NW, MM>(lane < MM ? s1[lane] : 0.0, QR, bl, cl);
+  double x = chain_Q<NW, MM>(py, QR, bl, cl);
   if (rw) s2[lane] = x;
   __builtin_amdgcn_wave_barrier();
   if constexpr (NZ > 0) {
@@ -866,11 +912,10 @@ __device__ __forceinline__ void wave_null_solve_t(const double* QR, const double
       for (int r = 0; r < NW; ++r) a[r & 3] += Z[r * NZ + lane] * s1[r];
       rz = (a[0] + a[1]) + (a[2] + a[3]);
     }
+    const double yz = wave_trsv_reg<NZ, true>(L, NZ, 1, L, NZ + 1, rz);   // L y = rz
+    const double pz = wave_trsv_reg<NZ, false>(L, 1, NZ, L, NZ + 1, yz);  // L^T p_z = y
     __builtin_amdgcn_wave_barrier();
-    if (lane < NZ) s2[lane] = rz;
-    __builtin_amdgcn_wave_barrier();
-    wave_trsv(NZ, true, L, NZ, 1, L, NZ + 1, s2);   // L y = rz
-    wave_trsv(NZ, false, L, 1, NZ, L, NZ + 1, s2);  // L^T p_z = y
+    if (lane < NZ) s2[lane] = pz;
     __builtin_amdgcn_wave_barrier();
     // dw = Y p_y + Z p_z
     if (rw) {
@@ -887,12 +932,7 @@ __device__ __forceinline__ void wave_null_solve_t(const double* QR, const double
   // u = q1 - (M + dW I) dw  ->  Y^T u = (Q^T u)[0, m)  ->  R dy = Y^T u
   const double mx = col_dot_u<NW>(M + lc, NW, s2);
   const double u = chain_Qt<NW, MM>(rw ? q1v - dW * x - mx : 0.0, QR, bl, cl);
-  __builtin_amdgcn_wave_barrier();
-  if (lane < MM) s1[lane] = u;
-  __builtin_amdgcn_wave_barrier();
-  wave_trsv(MM, false, QR, 1, NW, QR, NW + 1, s1);  // R[i][k] = QR[k * NW + i]
-  __builtin_amdgcn_wave_barrier();
-  *dyv = lane < MM ? s1[lane] : 0.0;
+  *dyv = wave_trsv_reg<MM, false>(QR, 1, NW, QR, NW + 1, lane < MM ? u : 0.0);  // R[i][k] = QR[k * NW + i]
   __builtin_amdgcn_wave_barrier();
 }
 
@@ -1092,12 +1132,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     __builtin_amdgcn_wave_barrier();
   }
   // ---- reduced Hessian Hr = Z^T (M Z): M Z a lane per row through the global workspace (L2),
-  // Hr's upper triangle a lane per entry, mirrored; the unshifted copy stays in the workspace
+  // Hr's upper triangle a lane per entry, mirrored into L; the Cholesky keeps the unshifted rows in
+  // registers for its delta_w retries
   double dW = 0.0;
   int32_t inf = 0;
   if constexpr (NZ > 0) {
     double* MZ = wsb;             // [NW][NZ] scratch (the factors overwrite it at the end)
-    double* Hs = wsb + NW * NZ;   // [NZ][NZ] scratch
     {
       // a lane per row r: acc[c] = sum_k M[k][r] Z[k][c]; M's column in chunks of 8, the next chunk's
       // loads issued before the current chunk's FMAs
@@ -1136,8 +1176,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       while (rem >= NZ - a) { rem -= NZ - a; ++a; }
       const int c = a + rem;
       const double h = col_dot_u<NW>(MZ + c, NZ, Z + a, NZ);
-      Hs[a * NZ + c] = h;
-      Hs[c * NZ + a] = h;
       L[a * NZ + c] = h;
       L[c * NZ + a] = h;
     }
@@ -1149,16 +1187,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     const double last = dw_last ? dw_last[b] : 0.0;
     const double mmax = wave_max(rw ? fabs(M[lane * NW + lane]) : 0.0);
     const double pivot_min = 2.220446049250313e-16 * mmax;
+    // the lane's row of Hr in registers (from the L image just written), the factor in place
+    const int lr = lane < NZ ? lane : 0;
+    double hs[NZ], a[NZ];
+#pragma unroll
+    for (int c = 0; c < NZ; ++c) hs[c] = L[lr * NZ + c];
     #pragma unroll 1
     for (int attempt = 0; attempt < 64; ++attempt) {
-      if (attempt > 0) {
-        for (int e = lane; e < NZ * NZ; e += 64) L[e] = Hs[e] + ((e / NZ == e % NZ) ? dW : 0.0);
-        __builtin_amdgcn_wave_barrier();
-      }
-      if (wave_cholesky(L, NZ, pivot_min)) break;
+#pragma unroll
+      for (int c = 0; c < NZ; ++c) a[c] = lane < NZ ? hs[c] + (c == lane ? dW : 0.0) : 0.0;
+      if (wave_cholesky_reg<NZ>(a, pivot_min)) break;
       if (dW == 0.0) dW = last == 0.0 ? 1e-4 : fmax(1e-20, last / 3.0);
       else dW *= last == 0.0 ? 100.0 : 8.0;
       if (dW > 1e40) { inf = 1; break; }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane < NZ) {
+#pragma unroll
+      for (int c = 0; c < NZ; ++c) L[lane * NZ + c] = a[c];
     }
     __builtin_amdgcn_wave_barrier();
   }
