@@ -948,7 +948,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   constexpr int T8 = (NW + 7) / 8;   // QR update: rows per lane (8 lanes per column)
   constexpr int P8 = (MM + 6) / 8;   // QR update: passes of 8 columns at j = 0 (MM - 1 columns)
   constexpr int T4 = (NW + 3) / 4;   // Z: rows per lane (4 lanes per column)
-  constexpr int P4 = (NZ + 15) / 16; // Z: passes of 16 columns
+  constexpr int P4F = NZ / 16;       // Z: full passes of 16 columns (the rest a row per lane)
   extern __shared__ __align__(16) double sm[];
   const int lane = threadIdx.x & 63;
   const int64_t b = blockIdx.x;
@@ -1010,43 +1010,54 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     if (lane == 0) beta[j] = bj;
     if (bj != 0.0 && j + 1 < MM) {
       // columns k > j: 8 lanes per column, 8 columns per pass, every pass's loads issued first;
-      // the lane's rows i = j + part + 8t, its reflector entries from the other lanes' vi
+      // the lane's rows i = j + part + 8t.  Passes past the last column and row blocks past the
+      // last row are skipped by wave-uniform branches (the trailing matrix shrinks with j).
       __builtin_amdgcn_wave_barrier();
       const int part = lane & 7, cl8 = lane >> 3;
+      const int ncol = MM - 1 - j;  // trailing columns
       double vrow[T8];
 #pragma unroll
       for (int t = 0; t < T8; ++t) {
         const int i = j + part + 8 * t;
-        vrow[t] = i == j ? 1.0 : (i < NW ? x[i] : 0.0);
+        vrow[t] = 0.0;
+        if (j + 8 * t < NW) vrow[t] = i == j ? 1.0 : (i < NW ? x[i] : 0.0);
       }
       double yr[P8][T8];
       double a[P8];
 #pragma unroll
       for (int p = 0; p < P8; ++p) {
-        const int k = j + 1 + 8 * p + cl8;
-        const double* y = QR + (k < MM ? k : j) * NW;
         a[p] = 0.0;
+        if (8 * p < ncol) {
+          const int k = j + 1 + 8 * p + cl8;
+          const double* y = QR + (k < MM ? k : j) * NW;
 #pragma unroll
-        for (int t = 0; t < T8; ++t) {
-          const int i = j + part + 8 * t;
-          yr[p][t] = i < NW ? y[i] : 0.0;
+          for (int t = 0; t < T8; ++t) {
+            const int i = j + part + 8 * t;
+            yr[p][t] = 0.0;
+            if (j + 8 * t < NW) yr[p][t] = i < NW ? y[i] : 0.0;
+          }
         }
       }
 #pragma unroll
       for (int p = 0; p < P8; ++p) {
+        if (8 * p < ncol) {
 #pragma unroll
-        for (int t = 0; t < T8; ++t) a[p] += vrow[t] * yr[p][t];
-        a[p] = bj * group8_sum(a[p]);
+          for (int t = 0; t < T8; ++t)
+            if (j + 8 * t < NW) a[p] += vrow[t] * yr[p][t];
+          a[p] = bj * group8_sum(a[p]);
+        }
       }
 #pragma unroll
       for (int p = 0; p < P8; ++p) {
-        const int k = j + 1 + 8 * p + cl8;
-        if (k < MM) {
-          double* y = QR + k * NW;
+        if (8 * p < ncol) {
+          const int k = j + 1 + 8 * p + cl8;
+          if (k < MM) {
+            double* y = QR + k * NW;
 #pragma unroll
-          for (int t = 0; t < T8; ++t) {
-            const int i = j + part + 8 * t;
-            if (i < NW) y[i] = yr[p][t] - a[p] * vrow[t];
+            for (int t = 0; t < T8; ++t) {
+              const int i = j + part + 8 * t;
+              if (j + 8 * t < NW && i < NW) y[i] = yr[p][t] - a[p] * vrow[t];
+            }
           }
         }
       }
@@ -1064,8 +1075,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     }
     if (lane < NP) cp[lane] = cl;
   }
-  // ---- Z = H_0 ... H_{m-1} [0; I]: backward, 4 lanes per column, 16 columns per pass (rows < j of
-  // Z are still zero at step j); the lane's reflector entries come from the other lanes' vr
+  // ---- Z = H_0 ... H_{m-1} [0; I]: backward (rows < j of Z are still zero at step j).  Full groups
+  // of 16 columns 4 lanes per column (row blocks past the last row skipped by wave-uniform
+  // branches, loads first); the NZ % 16 leftover columns a row per lane with a wave sum.
   for (int e = lane; e < NW * NZ; e += 64) {
     const int r = e / NZ, c = e - r * NZ;
     Z[e] = r == MM + c ? 1.0 : 0.0;
@@ -1076,41 +1088,53 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     const double bj = beta[j];
     if (bj == 0.0) continue;
     const double* v = QR + j * NW;
-    const int part = lane & 3, c16 = lane >> 2;
-    double vrow[T4];
-#pragma unroll
-    for (int t = 0; t < T4; ++t) {
-      const int i = j + part + 4 * t;
-      vrow[t] = i == j ? 1.0 : (i < NW ? v[i] : 0.0);
-    }
-    double zr[P4][T4];
-    double a[P4];
-#pragma unroll
-    for (int p = 0; p < P4; ++p) {
-      const int c = 16 * p + c16;
-      const int cc = c < NZ ? c : 0;
-      a[p] = 0.0;
+    if constexpr (P4F > 0) {
+      const int part = lane & 3, c16 = lane >> 2;
+      double vrow[T4];
 #pragma unroll
       for (int t = 0; t < T4; ++t) {
         const int i = j + part + 4 * t;
-        zr[p][t] = i < NW ? Z[i * NZ + cc] : 0.0;
+        vrow[t] = 0.0;
+        if (j + 4 * t < NW) vrow[t] = i == j ? 1.0 : (i < NW ? v[i] : 0.0);
       }
-    }
+      double zr[P4F][T4];
+      double a[P4F];
 #pragma unroll
-    for (int p = 0; p < P4; ++p) {
-#pragma unroll
-      for (int t = 0; t < T4; ++t) a[p] += vrow[t] * zr[p][t];
-      a[p] = bj * group4_sum(a[p]);
-    }
-#pragma unroll
-    for (int p = 0; p < P4; ++p) {
-      const int c = 16 * p + c16;
-      if (c < NZ) {
+      for (int p = 0; p < P4F; ++p) {
+        const int c = 16 * p + c16;
+        a[p] = 0.0;
 #pragma unroll
         for (int t = 0; t < T4; ++t) {
           const int i = j + part + 4 * t;
-          if (i < NW) Z[i * NZ + c] = zr[p][t] - a[p] * vrow[t];
+          zr[p][t] = 0.0;
+          if (j + 4 * t < NW) zr[p][t] = i < NW ? Z[i * NZ + c] : 0.0;
         }
+      }
+#pragma unroll
+      for (int p = 0; p < P4F; ++p) {
+#pragma unroll
+        for (int t = 0; t < T4; ++t)
+          if (j + 4 * t < NW) a[p] += vrow[t] * zr[p][t];
+        a[p] = bj * group4_sum(a[p]);
+      }
+#pragma unroll
+      for (int p = 0; p < P4F; ++p) {
+        const int c = 16 * p + c16;
+#pragma unroll
+        for (int t = 0; t < T4; ++t) {
+          const int i = j + part + 4 * t;
+          if (j + 4 * t < NW && i < NW) Z[i * NZ + c] = zr[p][t] - a[p] * vrow[t];
+        }
+      }
+    }
+    if constexpr (NZ % 16 != 0) {
+      const double vi = refl_entry<NW>(QR, j);
+      const int lr = lane < NW ? lane : 0;
+#pragma unroll
+      for (int c = 16 * P4F; c < NZ; ++c) {
+        const double zv = lane < NW ? Z[lr * NZ + c] : 0.0;
+        const double sc = bj * wave_sum(vi * zv);
+        if (lane >= j && lane < NW) Z[lane * NZ + c] = zv - sc * vi;
       }
     }
     __builtin_amdgcn_wave_barrier();
