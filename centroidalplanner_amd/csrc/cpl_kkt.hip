@@ -26,6 +26,7 @@
 #include <mutex>
 #include <string>
 #include <tuple>
+#include <type_traits>
 
 #include "cpl_status.hpp"
 #include "cpl_wave.hpp"
@@ -945,10 +946,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     double* __restrict__ ws) {
   using W = KktWave<NW, MM>;
   constexpr int NZ = W::NZ, NP = W::NP, NFAC = W::NFAC;
-  constexpr int T8 = (NW + 7) / 8;   // QR update: rows per lane (8 lanes per column)
-  constexpr int P8 = (MM + 6) / 8;   // QR update: passes of 8 columns at j = 0 (MM - 1 columns)
-  constexpr int T4 = (NW + 3) / 4;   // Z: rows per lane (4 lanes per column)
-  constexpr int P4F = NZ / 16;       // Z: full passes of 16 columns (the rest a row per lane)
   extern __shared__ __align__(16) double sm[];
   const int lane = threadIdx.x & 63;
   const int64_t b = blockIdx.x;
@@ -987,81 +984,113 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     return;
   }
 
-  // ---- Householder QR of A^T (row j of QR = column j of A^T)
-  for (int i = lane; i < MM * NW; i += 64) QR[i] = Ab[i];
-  __builtin_amdgcn_wave_barrier();
-  KKT_MARK(0);
-  #pragma unroll 1
-  for (int j = 0; j < MM; ++j) {
-    double* x = QR + j * NW;
-    const bool below = lane > j && lane < NW;
-    const double xi = below ? x[lane] : 0.0;
-    const double alpha = x[j];
-    const double sig = wave_sum(xi * xi);
-    double bj = 0.0;
-    if (sig != 0.0) {
-      const double nrm = sqrt(alpha * alpha + sig);
-      const double v0 = alpha <= 0.0 ? alpha - nrm : -sig / (alpha + nrm);
-      const double rv0 = 1.0 / v0;
-      if (below) x[lane] = xi * rv0;
-      bj = 2.0 * v0 * v0 / (sig + v0 * v0);
-      if (lane == 0) x[j] = nrm;  // R_jj on the diagonal
-    }
-    if (lane == 0) beta[j] = bj;
-    if (bj != 0.0 && j + 1 < MM) {
-      // columns k > j: 8 lanes per column, 8 columns per pass, every pass's loads issued first;
-      // the lane's rows i = j + part + 8t.  Passes past the last column and row blocks past the
-      // last row are skipped by wave-uniform branches (the trailing matrix shrinks with j).
+  // ---- Householder QR of A^T with the matrix register-resident: lane (g = lane >> 3, part =
+  // lane & 7) holds A^T[i][k] for the rows i = part + 8t and the columns k = g + 8q.  Per column j
+  // the 8 lanes of group j & 7 form the reflector (a group sum, two broadcasts) and publish its
+  // entries through a 47-double LDS buffer; every trailing column's dot is a group sum and its
+  // update stays in registers — 2 x 6 LDS operations per column instead of ~50.
+  {
+    constexpr int RT = (NW + 7) / 8;  // row blocks per lane
+    constexpr int CQ = (MM + 7) / 8;  // column blocks per lane
+    const int g = lane >> 3, part = lane & 7;
+    double a[CQ][RT];
+#pragma unroll
+    for (int q = 0; q < CQ; ++q)
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        const int k = g + 8 * q, i = part + 8 * t;
+        a[q][t] = (k < MM && i < NW) ? Ab[k * NW + i] : 0.0;
+      }
+    double* vbuf = s1;  // [NW] the current reflector's entries
+    KKT_MARK(0);
+    // column j = 8 QB + jj: its entries sit in block QB of group jj (rows block QB holds row j, at
+    // lane 9 jj), and the blocks q < QB (finished columns) and t < QB (rows above j) are skipped —
+    // compile-time per QB
+    auto step = [&](auto qbc, int jj) {
+      constexpr int QB = decltype(qbc)::value;
+      const int j = 8 * QB + jj;
+      const double* c = a[QB];
+      // sigma = sum_{i > j} x_i^2 (a group sum), alpha = x_j (lane 9 jj)
+      double ps = 0.0;
+#pragma unroll
+      for (int t = QB; t < RT; ++t) {
+        const int i = part + 8 * t;
+        if (i > j && i < NW) ps += c[t] * c[t];
+      }
+      ps = group8_sum(ps);
+      const double sig = wave_bcast(ps, 9 * jj);
+      const double alpha = wave_bcast(c[QB], 9 * jj);
+      // the reflector (LAPACK's dlarfg form): nrm = sqrt(alpha^2 + sigma), v0 = alpha - nrm
+      // (cancellation-free when alpha > 0), beta = 2 v0^2 / (sigma + v0^2)
+      double bj = 0.0, rv0 = 0.0, nrm = alpha;
+      if (sig != 0.0) {
+        nrm = sqrt(alpha * alpha + sig);
+        const double v0 = alpha <= 0.0 ? alpha - nrm : -sig / (alpha + nrm);
+        rv0 = 1.0 / v0;
+        bj = 2.0 * v0 * v0 / (sig + v0 * v0);
+      }
+      if (lane == 0) beta[j] = bj;
+      if (g == jj) {  // R_jj and the scaled reflector entries (zero when sigma = 0), kept and published
+#pragma unroll
+        for (int t = QB; t < RT; ++t) {
+          const int i = part + 8 * t;
+          if (i < NW && i >= j) {
+            const double nv = i == j ? nrm : (sig != 0.0 ? a[QB][t] * rv0 : a[QB][t]);
+            if (i > j) vbuf[i] = nv;
+            a[QB][t] = nv;
+          }
+        }
+      }
       __builtin_amdgcn_wave_barrier();
-      const int part = lane & 7, cl8 = lane >> 3;
-      const int ncol = MM - 1 - j;  // trailing columns
-      double vrow[T8];
+      if (bj != 0.0 && j + 1 < MM) {
+        double vl[RT];
 #pragma unroll
-      for (int t = 0; t < T8; ++t) {
-        const int i = j + part + 8 * t;
-        vrow[t] = 0.0;
-        if (j + 8 * t < NW) vrow[t] = i == j ? 1.0 : (i < NW ? x[i] : 0.0);
-      }
-      double yr[P8][T8];
-      double a[P8];
+        for (int t = QB; t < RT; ++t) {
+          const int i = part + 8 * t;
+          vl[t] = (i > j && i < NW) ? vbuf[i] : (i == j ? 1.0 : 0.0);
+        }
+        double d[CQ];
 #pragma unroll
-      for (int p = 0; p < P8; ++p) {
-        a[p] = 0.0;
-        if (8 * p < ncol) {
-          const int k = j + 1 + 8 * p + cl8;
-          const double* y = QR + (k < MM ? k : j) * NW;
+        for (int q = QB; q < CQ; ++q) {
+          d[q] = 0.0;
 #pragma unroll
-          for (int t = 0; t < T8; ++t) {
-            const int i = j + part + 8 * t;
-            yr[p][t] = 0.0;
-            if (j + 8 * t < NW) yr[p][t] = i < NW ? y[i] : 0.0;
+          for (int t = QB; t < RT; ++t) d[q] += vl[t] * a[q][t];
+        }
+#pragma unroll
+        for (int q = QB; q < CQ; ++q) {
+          const int k = g + 8 * q;
+          const double sk = bj * group8_sum(d[q]);
+          if (k > j && k < MM) {
+#pragma unroll
+            for (int t = QB; t < RT; ++t) a[q][t] -= sk * vl[t];
           }
         }
       }
-#pragma unroll
-      for (int p = 0; p < P8; ++p) {
-        if (8 * p < ncol) {
-#pragma unroll
-          for (int t = 0; t < T8; ++t)
-            if (j + 8 * t < NW) a[p] += vrow[t] * yr[p][t];
-          a[p] = bj * group8_sum(a[p]);
-        }
-      }
-#pragma unroll
-      for (int p = 0; p < P8; ++p) {
-        if (8 * p < ncol) {
-          const int k = j + 1 + 8 * p + cl8;
-          if (k < MM) {
-            double* y = QR + k * NW;
-#pragma unroll
-            for (int t = 0; t < T8; ++t) {
-              const int i = j + part + 8 * t;
-              if (j + 8 * t < NW && i < NW) y[i] = yr[p][t] - a[p] * vrow[t];
-            }
-          }
-        }
-      }
+      __builtin_amdgcn_wave_barrier();
+    };
+    static_assert(CQ <= 4, "nw 47, m <= 32");
+    #pragma unroll 1
+    for (int jj = 0; jj < 8; ++jj) step(std::integral_constant<int, 0>(), jj);
+    if constexpr (CQ > 1) {
+      #pragma unroll 1
+      for (int jj = 0; jj < 8 && 8 + jj < MM; ++jj) step(std::integral_constant<int, 1>(), jj);
     }
+    if constexpr (CQ > 2) {
+      #pragma unroll 1
+      for (int jj = 0; jj < 8 && 16 + jj < MM; ++jj) step(std::integral_constant<int, 2>(), jj);
+    }
+    if constexpr (CQ > 3) {
+      #pragma unroll 1
+      for (int jj = 0; jj < 8 && 24 + jj < MM; ++jj) step(std::integral_constant<int, 3>(), jj);
+    }
+    // the factored matrix into the LDS image (row k of QR = column k of A^T after the reflections)
+#pragma unroll
+    for (int q = 0; q < CQ; ++q)
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        const int k = g + 8 * q, i = part + 8 * t;
+        if (k < MM && i < NW) QR[k * NW + i] = a[q][t];
+      }
     __builtin_amdgcn_wave_barrier();
   }
   KKT_MARK(1);
@@ -1075,67 +1104,71 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     }
     if (lane < NP) cp[lane] = cl;
   }
-  // ---- Z = H_0 ... H_{m-1} [0; I]: backward (rows < j of Z are still zero at step j).  Full groups
-  // of 16 columns 4 lanes per column (row blocks past the last row skipped by wave-uniform
-  // branches, loads first); the NZ % 16 leftover columns a row per lane with a wave sum.
-  for (int e = lane; e < NW * NZ; e += 64) {
-    const int r = e / NZ, c = e - r * NZ;
-    Z[e] = r == MM + c ? 1.0 : 0.0;
-  }
-  __builtin_amdgcn_wave_barrier();
-  #pragma unroll 1
-  for (int j = MM - 1; j >= 0; --j) {
-    const double bj = beta[j];
-    if (bj == 0.0) continue;
-    const double* v = QR + j * NW;
-    if constexpr (P4F > 0) {
-      const int part = lane & 3, c16 = lane >> 2;
-      double vrow[T4];
+  // ---- Z = H_0 ... H_{m-1} [0; I], register-resident: lane (c = lane >> 2, part = lane & 3) holds
+  // Z[i][c] for the rows i = part + 4t of column c < 16, the columns past 16 a row per lane; per
+  // reflector (backward) a group-of-4 sum per column, the next reflector's entries loaded one step
+  // ahead.  Rows < j of Z are still zero at step j.
+  {
+    constexpr int ZT = (NW + 3) / 4;
+    constexpr int NZX = NZ > 16 ? NZ - 16 : 0;
+    const int c16 = lane >> 2, part = lane & 3;
+    double z[ZT];
 #pragma unroll
-      for (int t = 0; t < T4; ++t) {
-        const int i = j + part + 4 * t;
-        vrow[t] = 0.0;
-        if (j + 4 * t < NW) vrow[t] = i == j ? 1.0 : (i < NW ? v[i] : 0.0);
+    for (int t = 0; t < ZT; ++t) {
+      const int i = part + 4 * t;
+      z[t] = (c16 < NZ && i == MM + c16) ? 1.0 : 0.0;
+    }
+    double zx[NZX > 0 ? NZX : 1];
+#pragma unroll
+    for (int c = 0; c < NZX; ++c) zx[c] = lane == MM + 16 + c ? 1.0 : 0.0;
+    auto load_refl = [&](int j, double (&vl)[ZT], double& vx) {
+#pragma unroll
+      for (int t = 0; t < ZT; ++t) {
+        const int i = part + 4 * t;
+        vl[t] = (i > j && i < NW) ? QR[j * NW + i] : (i == j ? 1.0 : 0.0);
       }
-      double zr[P4F][T4];
-      double a[P4F];
+      vx = NZX > 0 ? refl_entry<NW>(QR, j) : 0.0;
+    };
+    double vl[ZT], vx;
+    load_refl(MM - 1, vl, vx);
+    double bj = beta[MM - 1];
+    #pragma unroll 1
+    for (int j = MM - 1; j >= 0; --j) {
+      double nl[ZT], nx = 0.0, nb = 0.0;
+      if (j > 0) {
+        load_refl(j - 1, nl, nx);
+        nb = beta[j - 1];
+      }
+      if (bj != 0.0) {
+        double d0 = 0.0, d1 = 0.0;
 #pragma unroll
-      for (int p = 0; p < P4F; ++p) {
-        const int c = 16 * p + c16;
-        a[p] = 0.0;
-#pragma unroll
-        for (int t = 0; t < T4; ++t) {
-          const int i = j + part + 4 * t;
-          zr[p][t] = 0.0;
-          if (j + 4 * t < NW) zr[p][t] = i < NW ? Z[i * NZ + c] : 0.0;
+        for (int t = 0; t < ZT; t += 2) {
+          d0 += vl[t] * z[t];
+          if (t + 1 < ZT) d1 += vl[t + 1] * z[t + 1];
         }
-      }
+        const double sc = bj * group4_sum(d0 + d1);
+        if (c16 < NZ) {
 #pragma unroll
-      for (int p = 0; p < P4F; ++p) {
-#pragma unroll
-        for (int t = 0; t < T4; ++t)
-          if (j + 4 * t < NW) a[p] += vrow[t] * zr[p][t];
-        a[p] = bj * group4_sum(a[p]);
-      }
-#pragma unroll
-      for (int p = 0; p < P4F; ++p) {
-        const int c = 16 * p + c16;
-#pragma unroll
-        for (int t = 0; t < T4; ++t) {
-          const int i = j + part + 4 * t;
-          if (j + 4 * t < NW && i < NW) Z[i * NZ + c] = zr[p][t] - a[p] * vrow[t];
+          for (int t = 0; t < ZT; ++t) z[t] -= sc * vl[t];
         }
+#pragma unroll
+        for (int c = 0; c < NZX; ++c) zx[c] -= bj * wave_sum(vx * zx[c]) * vx;
+      }
+#pragma unroll
+      for (int t = 0; t < ZT; ++t) vl[t] = j > 0 ? nl[t] : 0.0;
+      vx = nx;
+      bj = nb;
+    }
+    if (c16 < NZ && c16 < 16) {
+#pragma unroll
+      for (int t = 0; t < ZT; ++t) {
+        const int i = part + 4 * t;
+        if (i < NW) Z[i * NZ + c16] = z[t];
       }
     }
-    if constexpr (NZ % 16 != 0) {
-      const double vi = refl_entry<NW>(QR, j);
-      const int lr = lane < NW ? lane : 0;
+    if (lane < NW) {
 #pragma unroll
-      for (int c = 16 * P4F; c < NZ; ++c) {
-        const double zv = lane < NW ? Z[lr * NZ + c] : 0.0;
-        const double sc = bj * wave_sum(vi * zv);
-        if (lane >= j && lane < NW) Z[lane * NZ + c] = zv - sc * vi;
-      }
+      for (int c = 0; c < NZX; ++c) Z[lane * NZ + 16 + c] = zx[c];
     }
     __builtin_amdgcn_wave_barrier();
   }
