@@ -723,15 +723,16 @@ __global__ __launch_bounds__(256) void cpl_lagrangian_grad_kernel(int64_t total,
 template <int NW, int MM>
 struct KktWave {
   static constexpr int NZ = NW - MM;
+  static constexpr int ZS = NZ + (NZ & 1);          // Z row stride: even, so rows are 16-byte aligned
   static constexpr int NP = MM / 2;                 // reflector pairs (a lone last one when MM is odd)
-  static constexpr int NFAC = MM * NW + NW * NZ + NZ * NZ + MM + NP + 1;
+  static constexpr int NFAC = MM * NW + NW * ZS + NZ * NZ + MM + NP + 1;
   static constexpr int LDS = ((NFAC + 3 * NW + MM) + 1) & ~1;
   static_assert(NW <= 64 && MM <= NW, "one wave per system: nw <= 64");
 };
 
 __host__ __device__ inline int kktw_lds_doubles(int nw, int m) {
-  const int nz = nw - m;
-  return ((m * nw + nw * nz + nz * nz + m + m / 2 + 1 + 3 * nw + m) + 1) & ~1;
+  const int nz = nw - m, zs = nz + (nz & 1);
+  return ((m * nw + nw * zs + nz * nz + m + m / 2 + 1 + 3 * nw + m) + 1) & ~1;
 }
 
 // two wave sums, their DPP chains interleaved (the result in every lane)
@@ -889,6 +890,7 @@ __device__ __forceinline__ void wave_null_solve_t(const double* QR, const double
                                                   double dW, double q1v, double q2v, double* s1, double* s2,
                                                   double* dwv, double* dyv) {
   constexpr int NZ = NW - MM;
+  constexpr int ZS = KktWave<NW, MM>::ZS;
   const int lane = threadIdx.x & 63;
   // beta and c_p for the two chains (lanes j / p)
   const double bl = lane < MM ? beta[lane] : 0.0;
@@ -910,7 +912,7 @@ __device__ __forceinline__ void wave_null_solve_t(const double* QR, const double
     if (lane < NZ) {
       double a[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll 8
-      for (int r = 0; r < NW; ++r) a[r & 3] += Z[r * NZ + lane] * s1[r];
+      for (int r = 0; r < NW; ++r) a[r & 3] += Z[r * ZS + lane] * s1[r];
       rz = (a[0] + a[1]) + (a[2] + a[3]);
     }
     const double yz = wave_trsv_reg<NZ, true>(L, NZ, 1, L, NZ + 1, rz);   // L y = rz
@@ -922,7 +924,7 @@ __device__ __forceinline__ void wave_null_solve_t(const double* QR, const double
     if (rw) {
       double a[2] = {0.0, 0.0};
 #pragma unroll
-      for (int c = 0; c < NZ; ++c) a[c & 1] += Z[lane * NZ + c] * s2[c];
+      for (int c = 0; c < NZ; ++c) a[c & 1] += Z[lane * ZS + c] * s2[c];
       x += a[0] + a[1];
     }
     __builtin_amdgcn_wave_barrier();
@@ -945,14 +947,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     double* __restrict__ dyg, double* __restrict__ dWg, double* __restrict__ dCg, int32_t* __restrict__ info,
     double* __restrict__ ws) {
   using W = KktWave<NW, MM>;
-  constexpr int NZ = W::NZ, NP = W::NP, NFAC = W::NFAC;
+  constexpr int NZ = W::NZ, ZS = W::ZS, NP = W::NP, NFAC = W::NFAC;
   extern __shared__ __align__(16) double sm[];
   const int lane = threadIdx.x & 63;
   const int64_t b = blockIdx.x;
   if (b >= batch) return;
   double* QR = sm;                 // [MM][NW]
-  double* Z = QR + MM * NW;        // [NW][NZ]
-  double* L = Z + NW * NZ;         // [NZ][NZ]
+  double* Z = QR + MM * NW;        // [NW][ZS]
+  double* L = Z + NW * ZS;         // [NZ][NZ]
   double* beta = L + NZ * NZ;      // [MM]
   double* cp = beta + MM;          // [NP + 1]
   double* s1 = sm + NFAC;          // [NW] scratch
@@ -1132,8 +1134,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     double vl[ZT], vx;
     load_refl(MM - 1, vl, vx);
     double bj = beta[MM - 1];
-    #pragma unroll 1
-    for (int j = MM - 1; j >= 0; --j) {
+    // reflector j = 4 JB + jj (backward): rows below 4 JB are still zero, so the row blocks t < JB
+    // are skipped — compile-time per JB
+    auto zstep = [&](auto jbc, int j) {
+      constexpr int JB = decltype(jbc)::value;
       double nl[ZT], nx = 0.0, nb = 0.0;
       if (j > 0) {
         load_refl(j - 1, nl, nx);
@@ -1142,14 +1146,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       if (bj != 0.0) {
         double d0 = 0.0, d1 = 0.0;
 #pragma unroll
-        for (int t = 0; t < ZT; t += 2) {
+        for (int t = JB; t < ZT; t += 2) {
           d0 += vl[t] * z[t];
           if (t + 1 < ZT) d1 += vl[t + 1] * z[t + 1];
         }
         const double sc = bj * group4_sum(d0 + d1);
         if (c16 < NZ) {
 #pragma unroll
-          for (int t = 0; t < ZT; ++t) z[t] -= sc * vl[t];
+          for (int t = JB; t < ZT; ++t) z[t] -= sc * vl[t];
         }
 #pragma unroll
         for (int c = 0; c < NZX; ++c) zx[c] -= bj * wave_sum(vx * zx[c]) * vx;
@@ -1158,17 +1162,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       for (int t = 0; t < ZT; ++t) vl[t] = j > 0 ? nl[t] : 0.0;
       vx = nx;
       bj = nb;
-    }
+    };
+    static_assert((MM + 3) / 4 <= 8, "m <= 32");
+    auto zblock = [&](auto jbc) {
+      constexpr int JB = decltype(jbc)::value;
+      if constexpr (4 * JB < MM) {
+        #pragma unroll 1
+        for (int j = (4 * JB + 3 < MM ? 4 * JB + 3 : MM - 1); j >= 4 * JB; --j) zstep(jbc, j);
+      }
+    };
+    zblock(std::integral_constant<int, 7>());
+    zblock(std::integral_constant<int, 6>());
+    zblock(std::integral_constant<int, 5>());
+    zblock(std::integral_constant<int, 4>());
+    zblock(std::integral_constant<int, 3>());
+    zblock(std::integral_constant<int, 2>());
+    zblock(std::integral_constant<int, 1>());
+    zblock(std::integral_constant<int, 0>());
     if (c16 < NZ && c16 < 16) {
 #pragma unroll
       for (int t = 0; t < ZT; ++t) {
         const int i = part + 4 * t;
-        if (i < NW) Z[i * NZ + c16] = z[t];
+        if (i < NW) Z[i * ZS + c16] = z[t];
       }
     }
     if (lane < NW) {
 #pragma unroll
-      for (int c = 0; c < NZX; ++c) Z[lane * NZ + 16 + c] = zx[c];
+      for (int c = 0; c < NZX; ++c) Z[lane * ZS + 16 + c] = zx[c];
     }
     __builtin_amdgcn_wave_barrier();
   }
@@ -1213,7 +1233,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           if (k0 + u < NW) {
-            const double* zk = Z + (k0 + u) * NZ;
+            const double* zk = Z + (k0 + u) * ZS;
 #pragma unroll
             for (int c = 0; c < NZ; ++c) acc[c] += mk[u] * zk[c];
           }
@@ -1232,7 +1252,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       int a = 0, rem = e;
       while (rem >= NZ - a) { rem -= NZ - a; ++a; }
       const int c = a + rem;
-      const double h = col_dot_u<NW>(MZ + c, NZ, Z + a, NZ);
+      const double h = col_dot_u<NW>(MZ + c, NZ, Z + a, ZS);
       L[a * NZ + c] = h;
       L[c * NZ + a] = h;
     }
