@@ -1214,48 +1214,59 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   double dW = 0.0;
   int32_t inf = 0;
   if constexpr (NZ > 0) {
-    double* MZ = wsb;             // [NW][NZ] scratch (the factors overwrite it at the end)
-    {
-      // a lane per row r: acc[c] = sum_k M[k][r] Z[k][c]; M's column in chunks of 8, the next chunk's
-      // loads issued before the current chunk's FMAs
-      double acc[NZ];
+    // W = M Z and Hr = Z^T W on the FP64 matrix cores (v_mfma_f64_16x16x4f64: A lane l = A[l & 15]
+    // [k = l >> 4], B lane l = B[k = l >> 4][l & 15], D lane l reg q = D[(l >> 4) + 4q][l & 15]),
+    // padded to 16-row / 16-column tiles and 4-deep k-steps.  W's accumulator register q of row
+    // block kb / 4 is exactly Hr's B fragment of k-step kb, so W never leaves the registers; Z^T's
+    // A fragment of k-step kb is Z's B fragment.  Hr's upper triangle is mirrored into L.
+    static_assert(NW <= 48 && NZ <= 32, "MFMA tiling of Z^T M Z: nw <= 48, nz <= 32");
+    constexpr int KB = (NW + 3) / 4;    // k-steps
+    constexpr int RB = (NW + 15) / 16;  // row blocks of W
+    constexpr int CB = (NZ + 15) / 16;  // column blocks of W / Hr
+    typedef double f64x4 __attribute__((ext_vector_type(4)));
+    const int li = lane & 15, lk = lane >> 4;
+    double Zf[KB][CB];
 #pragma unroll
-      for (int c = 0; c < NZ; ++c) acc[c] = 0.0;
-      const double* mc = M + lc;  // column `lane` = row `lane` (M symmetric)
-      double mk[8];
+    for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-      for (int u = 0; u < 8; ++u) mk[u] = mc[u * NW];
-      #pragma unroll 1
-      for (int k0 = 0; k0 < NW; k0 += 8) {
-        double mn[8];
+      for (int cb = 0; cb < CB; ++cb) {
+        const int k = 4 * kb + lk, c = 16 * cb + li;
+        Zf[kb][cb] = (k < NW && c < NZ) ? Z[k * ZS + c] : 0.0;
+      }
+    f64x4 W[RB][CB];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) mn[u] = k0 + 8 + u < NW ? mc[(k0 + 8 + u) * NW] : 0.0;
+    for (int rb = 0; rb < RB; ++rb) {
+      double Mf[KB];
+      const int r = 16 * rb + li;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          if (k0 + u < NW) {
-            const double* zk = Z + (k0 + u) * ZS;
+      for (int kb = 0; kb < KB; ++kb) {
+        const int k = 4 * kb + lk;
+        Mf[kb] = (r < NW && k < NW) ? M[k * NW + r] : 0.0;  // M[r][k] (symmetric: the lanes read along a row)
+      }
 #pragma unroll
-            for (int c = 0; c < NZ; ++c) acc[c] += mk[u] * zk[c];
+      for (int cb = 0; cb < CB; ++cb) {
+        f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Mf[kb], Zf[kb][cb], acc, 0, 0, 0);
+        W[rb][cb] = acc;
+      }
+    }
+#pragma unroll
+    for (int ab = 0; ab < CB; ++ab)
+#pragma unroll
+      for (int cb = ab; cb < CB; ++cb) {
+        f64x4 h = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) h = __builtin_amdgcn_mfma_f64_16x16x4f64(Zf[kb][ab], W[kb / 4][cb][kb % 4], h, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int ar = 16 * ab + lk + 4 * q, c = 16 * cb + li;
+          if (ar < NZ && c < NZ && ar <= c) {
+            L[ar * NZ + c] = h[q];
+            L[c * NZ + ar] = h[q];
           }
         }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) mk[u] = mn[u];
       }
-      if (rw) {
-#pragma unroll
-        for (int c = 0; c < NZ; ++c) MZ[lane * NZ + c] = acc[c];
-      }
-    }
-    __threadfence_block();  // the lanes' M Z stores before the other lanes' loads
-    constexpr int NTRI = NZ * (NZ + 1) / 2;
-    for (int e = lane; e < NTRI; e += 64) {
-      int a = 0, rem = e;
-      while (rem >= NZ - a) { rem -= NZ - a; ++a; }
-      const int c = a + rem;
-      const double h = col_dot_u<NW>(MZ + c, NZ, Z + a, ZS);
-      L[a * NZ + c] = h;
-      L[c * NZ + a] = h;
-    }
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
     KKT_MARK(3);
