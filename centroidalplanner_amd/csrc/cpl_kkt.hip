@@ -881,14 +881,69 @@ __device__ __forceinline__ bool wave_cholesky_reg(double (&a)[N], double pivot_m
   return true;
 }
 
+// M as FP64-MFMA A fragments: Mf[rb][kb] = M[16 rb + (lane & 15)][4 kb + (lane >> 4)] (zero padded),
+// loaded once per factorisation (M symmetric: the lanes read along a row) and kept in registers
+template <int NW>
+struct MFrag {
+  static constexpr int KB = (NW + 3) / 4, RB = (NW + 15) / 16;
+};
+template <int NW>
+__device__ __forceinline__ void load_m_frags(const double* M, double (&Mf)[MFrag<NW>::RB][MFrag<NW>::KB]) {
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int rb = 0; rb < MFrag<NW>::RB; ++rb)
+#pragma unroll
+    for (int kb = 0; kb < MFrag<NW>::KB; ++kb) {
+      const int r = 16 * rb + li, k = 4 * kb + lk;
+      Mf[rb][kb] = (r < NW && k < NW) ? M[k * NW + r] : 0.0;
+    }
+}
+
+// y = M x on the matrix cores: B = [x 0 ... 0] (x in column 0, read from LDS xs), one D column per
+// 16-row block; the results (lanes 0, 16, 32, 48) go through LDS ys back to one element per lane.
+// ys may alias xs.  Returns y_lane (0 for lanes >= NW).
+template <int NW>
+__device__ __forceinline__ double mfma_matvec(const double (&Mf)[MFrag<NW>::RB][MFrag<NW>::KB], const double* xs,
+                                              double* ys) {
+  constexpr int KB = MFrag<NW>::KB, RB = MFrag<NW>::RB;
+  typedef double f64x4 __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+  double xf[KB];
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    const int k = 4 * kb + lk;
+    xf[kb] = (li == 0 && k < NW) ? xs[k] : 0.0;
+  }
+  f64x4 acc[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    acc[rb] = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) acc[rb] = __builtin_amdgcn_mfma_f64_16x16x4f64(Mf[rb][kb], xf[kb], acc[rb], 0, 0, 0);
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (li == 0) {
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 16 * rb + lk + 4 * q;
+        if (r < NW) ys[r] = acc[rb][q];
+      }
+  }
+  __builtin_amdgcn_wave_barrier();
+  return lane < NW ? ys[lane] : 0.0;
+}
+
 // The null-space solve on one wave.  q1v (lanes < NW), q2v (lanes < MM): the right-hand sides in
 // registers; returns dw in *dwv (lanes < NW) and dy in *dyv (lanes < MM).  s1, s2: LDS scratch of NW
 // doubles.  M: the system's (symmetric) M in global memory, read by columns.
 template <int NW, int MM>
 __device__ __forceinline__ void wave_null_solve_t(const double* QR, const double* Z, const double* L,
-                                                  const double* beta, const double* cp, const double* M,
-                                                  double dW, double q1v, double q2v, double* s1, double* s2,
-                                                  double* dwv, double* dyv) {
+                                                  const double* beta, const double* cp,
+                                                  const double (&Mf)[MFrag<NW>::RB][MFrag<NW>::KB], double dW,
+                                                  double q1v, double q2v, double* s1, double* s2, double* dwv,
+                                                  double* dyv) {
   constexpr int NZ = NW - MM;
   constexpr int ZS = KktWave<NW, MM>::ZS;
   const int lane = threadIdx.x & 63;
@@ -905,7 +960,7 @@ __device__ __forceinline__ void wave_null_solve_t(const double* QR, const double
   __builtin_amdgcn_wave_barrier();
   if constexpr (NZ > 0) {
     // t = q1 - (M + dW I) Y p_y  ->  rz = Z^T t  ->  L L^T p_z = rz
-    const double mx = col_dot_u<NW>(M + lc, NW, s2);
+    const double mx = mfma_matvec<NW>(Mf, s2, s1);
     if (rw) s1[lane] = q1v - dW * x - mx;
     __builtin_amdgcn_wave_barrier();
     double rz = 0.0;
@@ -933,7 +988,7 @@ __device__ __forceinline__ void wave_null_solve_t(const double* QR, const double
   }
   *dwv = x;
   // u = q1 - (M + dW I) dw  ->  Y^T u = (Q^T u)[0, m)  ->  R dy = Y^T u
-  const double mx = col_dot_u<NW>(M + lc, NW, s2);
+  const double mx = mfma_matvec<NW>(Mf, s2, s1);
   const double u = chain_Qt<NW, MM>(rw ? q1v - dW * x - mx : 0.0, QR, bl, cl);
   *dyv = wave_trsv_reg<MM, false>(QR, 1, NW, QR, NW + 1, lane < MM ? u : 0.0);  // R[i][k] = QR[k * NW + i]
   __builtin_amdgcn_wave_barrier();
@@ -979,8 +1034,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     for (int i = lane; i < NFAC; i += 64) sm[i] = wsb[i];
     const double dW = wsb[NFAC];
     __builtin_amdgcn_wave_barrier();
+    double Mf[MFrag<NW>::RB][MFrag<NW>::KB];
+    load_m_frags<NW>(M, Mf);
     double dwv, dyv;
-    wave_null_solve_t<NW, MM>(QR, Z, L, beta, cp, M, dW, q1v, q2v, s1, s2, &dwv, &dyv);
+    wave_null_solve_t<NW, MM>(QR, Z, L, beta, cp, Mf, dW, q1v, q2v, s1, s2, &dwv, &dyv);
     if (rw) dwg[b * NW + lane] = dwv;
     if (lane < MM) dyg[b * MM + lane] = dyv;
     return;
@@ -1213,6 +1270,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   // registers for its delta_w retries
   double dW = 0.0;
   int32_t inf = 0;
+  double Mf[MFrag<NW>::RB][MFrag<NW>::KB];  // M's MFMA fragments: Z^T M Z here, every M product later
+  load_m_frags<NW>(M, Mf);
   if constexpr (NZ > 0) {
     // W = M Z and Hr = Z^T W on the FP64 matrix cores (v_mfma_f64_16x16x4f64: A lane l = A[l & 15]
     // [k = l >> 4], B lane l = B[k = l >> 4][l & 15], D lane l reg q = D[(l >> 4) + 4q][l & 15]),
@@ -1236,18 +1295,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     f64x4 W[RB][CB];
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
-      double Mf[KB];
-      const int r = 16 * rb + li;
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb) {
-        const int k = 4 * kb + lk;
-        Mf[kb] = (r < NW && k < NW) ? M[k * NW + r] : 0.0;  // M[r][k] (symmetric: the lanes read along a row)
-      }
 #pragma unroll
       for (int cb = 0; cb < CB; ++cb) {
         f64x4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Mf[kb], Zf[kb][cb], acc, 0, 0, 0);
+        for (int kb = 0; kb < KB; ++kb)
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Mf[rb][kb], Zf[kb][cb], acc, 0, 0, 0);
         W[rb][cb] = acc;
       }
     }
@@ -1305,7 +1358,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   #pragma unroll 1
   for (int pass = 0; pass < 2; ++pass) {
     double c1, c2;
-    wave_null_solve_t<NW, MM>(QR, Z, L, beta, cp, M, dW, r1v, r2v, s1, s2, &c1, &c2);
+    wave_null_solve_t<NW, MM>(QR, Z, L, beta, cp, Mf, dW, r1v, r2v, s1, s2, &c1, &c2);
     if (pass == 0) {
       dwv = c1;
       dyv = c2;
@@ -1320,7 +1373,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     __builtin_amdgcn_wave_barrier();
     // e1 = q1 - dW dw - A^T dy - M dw,  e2 = q2 - A dw
     const double aty = col_dot_u<MM>(Ab + lc, NW, dyl);
-    const double mdw = col_dot_u<NW>(M + lc, NW, dwl);
+    const double mdw = mfma_matvec<NW>(Mf, dwl, s1);
     const double e1 = rw ? q1v - dW * dwv - aty - mdw : 0.0;
     const double adw = col_dot_u<NW>(Ab + (lane < MM ? lane : 0) * NW, 1, dwl);
     const double e2 = lane < MM ? q2v - adw : 0.0;
