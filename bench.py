@@ -417,7 +417,7 @@ def solve_bench(args):
             "config": {"workload": SOLVE_CONFIG.name, "contacts": 4, "environment": "ground", "batch_per_gpu": B,
                        "parallelism": f"instance-sharded x{world}",
                        "hessian": ("exact (analytic Lagrangian Hessian kernel)" if args.hessian == "exact"
-                                   else "limited-memory (damped BFGS, IFOPT's IpoptSolver default)"),
+                                   else "limited-memory (IPOPT's L-BFGS: 6 pairs, scalar1 initialisation; IFOPT's IpoptSolver default)"),
                        "max_ls": args.max_ls, "max_soc": args.max_soc},
             "solved": ok, "iterations_max": int(its.max().item()), "iterations_mean": float(its.mean().item()),
             "lockstep_iterations": r.iterations_run, "eval_launches_per_solve": r.evaluations,

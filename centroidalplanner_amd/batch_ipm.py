@@ -18,7 +18,7 @@ uses, batched over instances, with every per-instance quantity a row of a device
   * Hessian of the Lagrangian (hessian="exact", IPOPT's default): central differences of its
     exact gradient grad f + J^T y over x_free, the 2 n_free perturbed points of every instance
     evaluated as ONE batch of B * 2 n_free instances and J^T y formed on the device
-    (cpl_lagrangian_grad); or (hessian="limited-memory", what IFOPT configures) a dense damped BFGS
+    (cpl_lagrangian_grad); or (hessian="limited-memory", what IFOPT configures) IPOPT's limited-memory BFGS
     model initialised like IPOPT's scalar1 = s'y / s's;
   * Newton step (cpl_kkt_solve, csrc/cpl_kkt.hip): null-space method on a Householder QR of A^T
     (A = [J_free | -P]) with IPOPT's inertia correction on the device — the KKT matrix has inertia
@@ -54,6 +54,7 @@ Two implementations of the same iteration:
 from __future__ import annotations
 
 import ctypes
+import math
 from dataclasses import dataclass
 from typing import Callable, Optional
 
@@ -61,6 +62,9 @@ import numpy as np
 
 from . import _abi
 from ._abi import INF
+
+EPS = float(np.finfo(np.float64).eps)
+LM_HIST, LM_MAX_SKIP = 6, 2  # IPOPT limited_memory_max_history / limited_memory_max_skipping
 
 BIG = INF / 10.0  # |bound| >= 1e19 is infinite (IPOPT nlp_lower/upper_bound_inf)
 
@@ -219,7 +223,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     hessian: "exact" (the analytic Lagrangian Hessian, cpl_lagrangian_hessian, for Ground /
     no-environment problems on the device; batched central differences of the Lagrangian gradient
     otherwise), "fd" (always the central differences) or "limited-memory"
-    (damped BFGS).  graph: capture one iteration as a HIP graph (default: on for device tensors).
+    (IPOPT's L-BFGS, 6 pairs).  graph: capture one iteration as a HIP graph (default: on for device tensors).
     max_ls / max_soc: line-search trials / second-order corrections per iteration (fixed counts)."""
     if hessian not in ("exact", "fd", "limited-memory"):
         raise ValueError("hessian must be 'exact', 'fd' or 'limited-memory'")
@@ -478,7 +482,10 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         "f": cur0["f"].clone(), "grad": cur0["grad"].clone(), "g": cur0["g"].clone(), "J": cur0["J"].clone(),
         "d_inf": zeros_B.clone(),
         "Hq": eye_f.repeat(B, 1, 1) if use_bfgs else None,
-        "hq_init": torch.zeros(B, dtype=torch.bool, device=dev),
+        "lm_s": torch.zeros(B, LM_HIST, nf, dtype=dt, device=dev) if use_bfgs else None,
+        "lm_y": torch.zeros(B, LM_HIST, nf, dtype=dt, device=dev) if use_bfgs else None,
+        "lm_cnt": torch.zeros(B, dtype=torch.int64, device=dev),
+        "lm_skip": torch.zeros(B, dtype=torch.int64, device=dev),
     }
 
     def check(E):
@@ -496,6 +503,47 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         S["active"].copy_(active)
         S["d_inf"].copy_(E["d_inf"])
         return active
+
+    def lbfgs_update(active, sk, new, cur, y_new, failed):
+        """IPOPT's LimMemQuasiNewtonUpdater with IFOPT's defaults (bfgs, max_history 6, scalar1,
+        init_val 1 in [1e-8, 1e8], max_skipping 2) — the device's k_lbfgs (csrc/cpl_solver.hip); a failed
+        line search (the feasibility step, our restoration stand-in, was taken) restarts the model."""
+        JTy_new = (new["J"].transpose(1, 2) @ y_new.unsqueeze(2)).squeeze(2)
+        JTy_old = (cur["J"].transpose(1, 2) @ y_new.unsqueeze(2)).squeeze(2)
+        yk = (new["grad"] + JTy_new)[:, free] - (cur["grad"] + JTy_old)[:, free]
+        sy, ss, yy = (sk * yk).sum(1), (sk * sk).sum(1), (yk * yk).sum(1)
+        take = active & (sy > math.sqrt(EPS) * ss.sqrt() * yy.sqrt())
+        skip = active & ~take
+        skipped = torch.where(skip, S["lm_skip"] + 1, torch.zeros_like(S["lm_skip"]))
+        reset = (skip & (skipped > LM_MAX_SKIP)) | (active & failed)
+        take = take & ~reset
+        S["lm_skip"].copy_(torch.where(active, torch.where(reset, torch.zeros_like(skipped), skipped), S["lm_skip"]))
+        # memory: a full one shifts down by one (the oldest pair dropped), the new pair appended
+        cnt = S["lm_cnt"]
+        full = (cnt == LM_HIST)[:, None, None]
+        Ps = torch.where(full, S["lm_s"].roll(-1, 1), S["lm_s"])
+        Py = torch.where(full, S["lm_y"].roll(-1, 1), S["lm_y"])
+        last = torch.clamp(cnt, max=LM_HIST - 1)
+        slot = (torch.arange(LM_HIST, device=dev)[None, :] == last[:, None])[:, :, None]
+        Ps = torch.where(slot, sk[:, None, :], Ps)
+        Py = torch.where(slot, yk[:, None, :], Py)
+        nc = last + 1
+        S["lm_s"].copy_(torch.where(take[:, None, None], Ps, S["lm_s"]))
+        S["lm_y"].copy_(torch.where(take[:, None, None], Py, S["lm_y"]))
+        S["lm_cnt"].copy_(torch.where(take, nc, torch.where(reset, torch.zeros_like(cnt), cnt)))
+        # the dense model rebuilt from sigma I by the recursion over the stored pairs, oldest first
+        sigma = torch.clamp(sy / torch.where(ss > 0, ss, 1.0), min=1e-8, max=1e8)
+        H = sigma[:, None, None] * eye_f
+        for j in range(LM_HIST):
+            sj, yj = Ps[:, j], Py[:, j]
+            Hs = (H @ sj.unsqueeze(2)).squeeze(2)
+            sHs, sjy = (sj * Hs).sum(1), (sj * yj).sum(1)
+            ok = (j < nc) & (sHs > 0)
+            Hn = (H - Hs.unsqueeze(2) * Hs.unsqueeze(1) / torch.where(ok, sHs, 1.0)[:, None, None]) + \
+                yj.unsqueeze(2) * yj.unsqueeze(1) / torch.where(ok, sjy, 1.0)[:, None, None]
+            H = torch.where(ok[:, None, None], Hn, H)
+        Hq = torch.where(take[:, None, None], H, S["Hq"])
+        S["Hq"].copy_(torch.where(reset[:, None, None], eye_f.expand_as(Hq), Hq))
 
     def step():
         """One lock-step iteration of every instance; no host synchronisation (graph-capturable)."""
@@ -636,28 +684,8 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         zU_new = torch.where(act & hasU, torch.minimum(torch.maximum(zU_new, mu[:, None] / (1e10 * dun)),
                                                        1e10 * mu[:, None] / dun), zU_new)
 
-        if use_bfgs:  # damped BFGS update over x_free (both Lagrangian gradients at the new y)
-            Hq = S["Hq"]
-            sk = (w_new - w)[:, :nf]
-            JTy_new = (new["J"].transpose(1, 2) @ y_new.unsqueeze(2)).squeeze(2)
-            JTy_old = (cur["J"].transpose(1, 2) @ y_new.unsqueeze(2)).squeeze(2)
-            yk = (new["grad"] + JTy_new)[:, free] - (cur["grad"] + JTy_old)[:, free]
-            sy = (sk * yk).sum(1)
-            ss = (sk * sk).sum(1)
-            first = active & ~S["hq_init"] & (sy > 0) & (ss > 0)
-            sigma0 = torch.where(first, sy / torch.where(ss > 0, ss, 1.0), torch.ones_like(sy))
-            Hq = torch.where(first[:, None, None], sigma0[:, None, None] * eye_f, Hq)
-            S["hq_init"].copy_(S["hq_init"] | first)
-            Hs = (Hq @ sk.unsqueeze(2)).squeeze(2)
-            sHs = (sk * Hs).sum(1)
-            theta = torch.where(sy >= 0.2 * sHs, torch.ones_like(sy),
-                                0.8 * sHs / torch.where(sHs - sy != 0, sHs - sy, 1.0))
-            r = theta[:, None] * yk + (1.0 - theta[:, None]) * Hs
-            sr = (sk * r).sum(1)
-            upd = active & (ss > 1e-30) & (sHs > 0) & (sr > 0)
-            Hn = Hq - Hs.unsqueeze(2) * Hs.unsqueeze(1) / torch.where(upd, sHs, 1.0)[:, None, None] + \
-                r.unsqueeze(2) * r.unsqueeze(1) / torch.where(upd, sr, 1.0)[:, None, None]
-            S["Hq"].copy_(torch.where(upd[:, None, None], 0.5 * (Hn + Hn.transpose(1, 2)), Hq))
+        if use_bfgs:  # IPOPT's limited-memory BFGS over x_free (both Lagrangian gradients at the new y)
+            lbfgs_update(active, (w_new - w)[:, :nf], new, cur, y_new, failed)
 
         # ---- write the state back in place
         S["w"].copy_(torch.where(act, w_new, w))

@@ -951,7 +951,6 @@ __device__ __forceinline__ void wave_null_solve_t(const double* QR, const double
   const double bl = lane < MM ? beta[lane] : 0.0;
   const double cl = lane < MM / 2 ? cp[lane] : 0.0;
   const bool rw = lane < NW;
-  const int lc = rw ? lane : 0;
   // R^T p_y = q2   ((R^T)[i][k] = QR[i * NW + k])
   const double py = wave_trsv_reg<MM, true>(QR, NW, 1, QR, NW + 1, lane < MM ? q2v : 0.0);
   // x = Y p_y = Q [p_y; 0]

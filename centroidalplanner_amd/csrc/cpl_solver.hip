@@ -6,16 +6,17 @@
 // per-instance quantity a row of a device buffer:
 //   * callbacks: cpl_eval_batch(_ex) (values-only Jacobian records), the analytic Lagrangian Hessian
 //     (cpl_lagrangian_hessian) or central differences (cpl_ipm_fd_points + cpl_eval_lagrangian_grad
-//     + cpl_ipm_fd_hessian_raw), or a damped BFGS model (IFOPT's limited-memory default, the
-//     reference's configuration, src/CentroidalPlanner.cpp:22-29);
+//     + cpl_ipm_fd_hessian_raw), or IPOPT's limited-memory BFGS model (6 pairs, scalar1; IFOPT's
+//     IpoptSolver default, the reference's configuration, src/CentroidalPlanner.cpp:22-29);
 //   * per-instance iteration work: cpl_ipm_optimality / newton_setup / post_step / trial_point /
 //     judge_take / accept / max_step / dense_a / masked_rows, the Newton step cpl_kkt_solve;
 //   * the glue between them (the line-search state, second-order corrections, the feasibility step
-//     standing in for the restoration phase, BFGS) in the small kernels below — no framework ops.
+//     standing in for the restoration phase, L-BFGS) in the small kernels below — no framework ops.
 // One iteration (fixed trip counts, masked updates, no host synchronisation) is captured once as a
 // HIP graph and replayed; the host reads an "any instance active" byte one iteration behind.
 #include <hip/hip_runtime.h>
 
+#include <cfloat>
 #include <cmath>
 #include <cstring>
 #include <algorithm>
@@ -102,7 +103,7 @@ __global__ __launch_bounds__(256) void k_init_state(
     double* __restrict__ theta_min, double* __restrict__ mu, uint8_t* __restrict__ active,
     int64_t* __restrict__ status, int64_t* __restrict__ iters, int64_t* __restrict__ acc, double* __restrict__ filt_t,
     double* __restrict__ filt_p, int64_t* __restrict__ fcount, double* __restrict__ dwl, double* __restrict__ d_inf,
-    uint8_t* __restrict__ hq_init, double* __restrict__ r1, double* __restrict__ r2, double* __restrict__ M) {
+    uint8_t* __restrict__ lm_cnt, uint8_t* __restrict__ lm_skip, double* __restrict__ r1, double* __restrict__ r2, double* __restrict__ M) {
   const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
   if (b >= B) return;
   const int lane = threadIdx.x & 63;
@@ -142,7 +143,8 @@ __global__ __launch_bounds__(256) void k_init_state(
     fcount[b] = 0;
     dwl[b] = 0.0;
     d_inf[b] = 0.0;
-    hq_init[b] = 0;
+    lm_cnt[b] = 0;
+    lm_skip[b] = 0;
   }
 }
 
@@ -297,32 +299,56 @@ __global__ void k_rest(int64_t B, const uint8_t* __restrict__ failed, const uint
   alpha2[b] = 2.0 * alpha[b];
 }
 
-// damped BFGS update of the model over x_free (batch_ipm step(), use_bfgs), one workgroup per
-// active instance: s = dw_free, y_k = grad_w L(w_new, y_new) - grad_w L(w, y_new) (the Jacobian
-// parts from A = [J_free | -P] at both points), first update scaled like IPOPT's s'y / s's, Powell
-// damping (theta = 0.8 s'Hs / (s'Hs - s'y) when s'y < 0.2 s'Hs), symmetrised.
-__global__ __launch_bounds__(256) void k_bfgs(int64_t B, int m, int nf, int nw, const uint8_t* __restrict__ act,
-                                              const double* __restrict__ w_old, const double* __restrict__ w_new,
-                                              const double* __restrict__ y, const double* __restrict__ dy,
-                                              const double* __restrict__ alpha, const double* __restrict__ gw_old,
-                                              const double* __restrict__ A_old, const double* __restrict__ gw_new,
-                                              const double* __restrict__ A_new, double* __restrict__ Hq,
-                                              uint8_t* __restrict__ hq_init) {
+// IPOPT's limited-memory quasi-Newton model (LimMemQuasiNewtonUpdater [IPOPT] with the defaults
+// IFOPT's IpoptSolver leaves in place behind src/CentroidalPlanner.cpp:22-29: update type bfgs,
+// limited_memory_max_history 6, initialization scalar1, init_val 1 (bounds 1e-8 / 1e8),
+// max_skipping 2; every variable is nonlinear since IFOPT declares no linear ones), over x_free,
+// one workgroup per active instance (batch_ipm step(), use_bfgs):
+//   s = dw_free, y = grad_x L(w_new, y_new) - grad_x L(w, y_new)  (the Jacobian parts from A = [J_free | -P]);
+//   the pair is skipped when s'y <= sqrt(eps) |s| |y|; more than max_skipping consecutive skips
+//   reset the memory (model back to init_val I), and so does a failed line search (the step came
+//   from the feasibility step standing in for IPOPT's restoration phase, whose return restarts the
+//   quasi-Newton model; without it the degenerate TestBasic ground problem — force weight 0 —
+//   stalls on a model whose scalar1 sigma collapsed along a flat direction);
+//   otherwise the pair enters the memory (the oldest of 6 dropped), sigma = s'y / s's of the newest
+//   pair clamped to [1e-8, 1e8], and the dense model is rebuilt from sigma I by the BFGS recursion
+//   over the stored pairs, oldest first: B <- B - (Bs)(Bs)' / s'Bs + y y' / s'y  (mathematically the
+//   compact representation IPOPT applies; B stays bitwise symmetric: every update is an outer product).
+constexpr int LM_HIST = 6, LM_MAX_SKIP = 2;
+__global__ __launch_bounds__(256) void k_lbfgs(int64_t B, int m, int nf, int nw, const uint8_t* __restrict__ act,
+                                               const double* __restrict__ w_old, const double* __restrict__ w_new,
+                                               const double* __restrict__ y, const double* __restrict__ dy,
+                                               const double* __restrict__ alpha, const double* __restrict__ gw_old,
+                                               const double* __restrict__ A_old, const double* __restrict__ gw_new,
+                                               const double* __restrict__ A_new, double* __restrict__ lm_s,
+                                               double* __restrict__ lm_y, uint8_t* __restrict__ lm_cnt,
+                                               uint8_t* __restrict__ lm_skip, const uint8_t* __restrict__ failed,
+                                               double* __restrict__ Hq) {
   const int64_t b = blockIdx.x;
   if (b >= B || !act[b]) return;
-  __shared__ double s_k[128], y_k[128], Hs[128], rv[128], yn[256], red[8];
+  __shared__ double Ps[LM_HIST][128], Py[LM_HIST][128], Hs[128], yn[256], red[8];
   const int tid = threadIdx.x;
   const double al = alpha[b];
   for (int r = tid; r < m; r += blockDim.x) yn[r] = y[b * m + r] + al * dy[b * m + r];
+  // both counters read before any barrier: thread 0 rewrites them below
+  const int cnt = lm_cnt[b], skipped = lm_skip[b] + 1;
   __syncthreads();
+  // the new pair goes to slot `last`; a full memory shifts down by one (the oldest dropped)
+  const int shift = cnt == LM_HIST ? 1 : 0, last = cnt - shift;
+  double* gs = lm_s + b * (int64_t)LM_HIST * nf;
+  double* gy = lm_y + b * (int64_t)LM_HIST * nf;
   for (int k = tid; k < nf; k += blockDim.x) {
     double jn = 0.0, jo = 0.0;
     for (int r = 0; r < m; ++r) {
       jn += A_new[(b * m + r) * nw + k] * yn[r];
       jo += A_old[(b * m + r) * nw + k] * yn[r];
     }
-    s_k[k] = w_new[b * nw + k] - w_old[b * nw + k];
-    y_k[k] = (gw_new[b * nw + k] + jn) - (gw_old[b * nw + k] + jo);
+    Ps[last][k] = w_new[b * nw + k] - w_old[b * nw + k];
+    Py[last][k] = (gw_new[b * nw + k] + jn) - (gw_old[b * nw + k] + jo);
+    for (int j = 0; j < last; ++j) {
+      Ps[j][k] = gs[(j + shift) * nf + k];
+      Py[j][k] = gy[(j + shift) * nf + k];
+    }
   }
   __syncthreads();
   auto block_dot = [&](const double* a, const double* c) {
@@ -336,38 +362,51 @@ __global__ __launch_bounds__(256) void k_bfgs(int64_t B, int m, int nf, int nw, 
     for (int q = 0; q < (int)(blockDim.x >> 6); ++q) t += red[q];
     return t;
   };
-  const double sy = block_dot(s_k, y_k);
-  const double ss = block_dot(s_k, s_k);
+  const double sy = block_dot(Ps[last], Py[last]);
+  const double ss = block_dot(Ps[last], Ps[last]);
+  const double yy = block_dot(Py[last], Py[last]);
   double* H = Hq + b * (int64_t)nf * nf;
-  if (!hq_init[b] && sy > 0.0 && ss > 0.0) {
-    const double sigma0 = sy / ss;
-    for (int e = tid; e < nf * nf; e += blockDim.x) H[e] = (e / nf == e % nf) ? sigma0 : 0.0;
+  const bool skip = !(sy > sqrt(DBL_EPSILON) * sqrt(ss) * sqrt(yy));
+  if (skip || failed[b]) {  // (uniform branch)
+    if (!failed[b] && skipped <= LM_MAX_SKIP) {
+      if (tid == 0) lm_skip[b] = (uint8_t)skipped;
+      return;
+    }
+    for (int e = tid; e < nf * nf; e += blockDim.x) H[e] = (e / nf == e % nf) ? 1.0 : 0.0;
+    if (tid == 0) {
+      lm_skip[b] = 0;
+      lm_cnt[b] = 0;
+    }
+    return;
+  }
+  const int nc = last + 1;
+  for (int k = tid; k < nf; k += blockDim.x)
+    for (int j = 0; j < nc; ++j) {
+      gs[j * nf + k] = Ps[j][k];
+      gy[j * nf + k] = Py[j][k];
+    }
+  if (tid == 0) {
+    lm_skip[b] = 0;
+    lm_cnt[b] = (uint8_t)nc;
+  }
+  const double sigma = fmin(fmax(sy / ss, 1e-8), 1e8);
+  for (int e = tid; e < nf * nf; e += blockDim.x) H[e] = (e / nf == e % nf) ? sigma : 0.0;
+  __syncthreads();
+  for (int j = 0; j < nc; ++j) {
+    for (int i = tid; i < nf; i += blockDim.x) {
+      double v = 0.0;
+      for (int k = 0; k < nf; ++k) v += H[i * nf + k] * Ps[j][k];
+      Hs[i] = v;
+    }
     __syncthreads();
-    if (tid == 0) hq_init[b] = 1;
-  }
-  __syncthreads();
-  for (int i = tid; i < nf; i += blockDim.x) {
-    double v = 0.0;
-    for (int j = 0; j < nf; ++j) v += H[i * nf + j] * s_k[j];
-    Hs[i] = v;
-  }
-  __syncthreads();
-  const double sHs = block_dot(s_k, Hs);
-  const double theta = sy >= 0.2 * sHs ? 1.0 : 0.8 * sHs / ((sHs - sy) != 0.0 ? (sHs - sy) : 1.0);
-  for (int k = tid; k < nf; k += blockDim.x) rv[k] = theta * y_k[k] + (1.0 - theta) * Hs[k];
-  __syncthreads();
-  const double sr = block_dot(s_k, rv);
-  if (!(ss > 1e-30 && sHs > 0.0 && sr > 0.0)) return;  // (uniform)
-  // Hn = H - Hs Hs^T / sHs + r r^T / sr, symmetrised: H <- (Hn + Hn^T) / 2, written in place by
-  // (i <= j) pairs so each pair reads both old entries before writing them
-  for (int e = tid; e < nf * nf; e += blockDim.x) {
-    const int i = e / nf, j = e - i * nf;
-    if (j < i) continue;
-    const double hij = H[i * nf + j] - Hs[i] * Hs[j] / sHs + rv[i] * rv[j] / sr;
-    const double hji = H[j * nf + i] - Hs[j] * Hs[i] / sHs + rv[j] * rv[i] / sr;
-    const double v = 0.5 * (hij + hji);
-    H[i * nf + j] = v;
-    H[j * nf + i] = v;
+    const double sHs = block_dot(Ps[j], Hs);
+    const double sjy = block_dot(Ps[j], Py[j]);
+    if (!(sHs > 0.0)) continue;  // (uniform; cannot happen for a positive definite model)
+    for (int e = tid; e < nf * nf; e += blockDim.x) {
+      const int i = e / nf, c = e - i * nf;
+      H[e] = (H[e] - Hs[i] * Hs[c] / sHs) + Py[j][i] * Py[j][c] / sjy;
+    }
+    __syncthreads();
   }
 }
 
@@ -548,9 +587,10 @@ struct cpl_solver {
   uint8_t *is_fixed, *hasL, *hasU;
   double *xl, *xu, *gl, *gu, *wl0, *wu0, *zeros_w, *zeros_B;
   // state
-  double *Xbase, *w, *y, *zL, *zU, *mu, *filt_t, *filt_p, *dwl, *f, *grad, *g, *J, *d_inf, *Hq, *theta_max, *theta_min;
+  double *Xbase, *w, *y, *zL, *zU, *mu, *filt_t, *filt_p, *dwl, *f, *grad, *g, *J, *d_inf, *Hq, *lm_s, *lm_y, *theta_max,
+      *theta_min;
   int64_t *status, *iters, *acc, *fcount;
-  uint8_t *active, *hq_init, *d_any;
+  uint8_t *active, *lm_cnt, *lm_skip, *d_any;
   // iteration temporaries
   double *A, *A_new, *gradw, *gradw_new, *c, *err0, *base, *mu_o, *ft, *fp, *tau, *X, *H, *M, *Mr, *r1, *r2, *gphi,
       *mr_diag, *theta_k, *phi_k, *dw, *dy, *delta_w, *delta_c, *dzL, *dzU, *a_max, *a_z, *gd, *ws;
@@ -722,9 +762,10 @@ int32_t step(cpl_solver* S) {
     hipLaunchKernelGGL(k_prep, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->free32, S->row_slack, S->gl,
                        S->grad_n, S->g_n, S->st_w, S->gradw_new, nullptr);
     LAUNCHED("k_prep (new)");
-    hipLaunchKernelGGL(k_bfgs, dim3((unsigned)B), dim3(256), 0, st, B, m, nf, nw, S->act, S->w, S->st_w, S->y, S->dy,
-                       S->st_alpha, S->gradw, S->A, S->gradw_new, S->A_new, S->Hq, S->hq_init);
-    LAUNCHED("k_bfgs");
+    hipLaunchKernelGGL(k_lbfgs, dim3((unsigned)B), dim3(256), 0, st, B, m, nf, nw, S->act, S->w, S->st_w, S->y, S->dy,
+                       S->st_alpha, S->gradw, S->A, S->gradw_new, S->A_new, S->lm_s, S->lm_y, S->lm_cnt, S->lm_skip,
+                       S->failed, S->Hq);
+    LAUNCHED("k_lbfgs");
   }
   CK(cpl_ipm_accept(B, nw, m, FMAX, S->act, S->st_aug, S->failed, S->rest, S->st_alpha, S->a_z, S->theta_k, S->phi_k,
                     S->ft, S->fp, S->fc, S->st_w, S->dy, S->dzL, S->dzU, S->mu_o, S->hasL, S->hasU, S->wl0, S->wu0,
@@ -792,7 +833,11 @@ int32_t compact(cpl_solver* S, int64_t count, int64_t Bn) {
   CK(move(S->grad, n)); CK(move(S->g, m)); CK(move(S->J, S->nnz_rec)); CK(move(S->d_inf, 1));
   CK(move(S->theta_max, 1)); CK(move(S->theta_min, 1)); CK(move(S->Xbase, n));
   CK(move(S->status, 1)); CK(move(S->iters, 1)); CK(move(S->acc, 1)); CK(move(S->fcount, 1));
-  if (S->bfgs) CK(move(S->Hq, (int64_t)nf * nf));
+  if (S->bfgs) {
+    CK(move(S->Hq, (int64_t)nf * nf));
+    CK(move(S->lm_s, (int64_t)LM_HIST * nf));
+    CK(move(S->lm_y, (int64_t)LM_HIST * nf));
+  }
   if (S->mass) CK(move(S->mass_c, 1));
   // 1-byte and 4-byte rows
   auto move_bytes = [&](uint8_t* buf) -> int32_t {
@@ -803,7 +848,8 @@ int32_t compact(cpl_solver* S, int64_t count, int64_t Bn) {
     return CPL_OK;
   };
   CK(move_bytes(S->active));
-  CK(move_bytes(S->hq_init));
+  CK(move_bytes(S->lm_cnt));
+  CK(move_bytes(S->lm_skip));
   if (S->tag) CK(move_bytes(S->tag_c));
   hipLaunchKernelGGL(k_gather_i32, dim3(blocks_elems(count)), dim3(256), 0, st, count, S->pos, S->orig,
                      (int32_t*)S->scratch);
@@ -1001,10 +1047,11 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   S->filt_t = a.take<double>(Bz * FMAX); S->filt_p = a.take<double>(Bz * FMAX); S->dwl = a.take<double>(Bz);
   S->f = a.take<double>(Bz); S->grad = a.take<double>(Bz * n); S->g = a.take<double>(Bz * m);
   S->J = a.take<double>(Bz * nnz_rec); S->d_inf = a.take<double>(Bz); S->Hq = a.take<double>(Bz * nf * nf);
+  S->lm_s = a.take<double>(S->bfgs ? Bz * LM_HIST * nf : 0); S->lm_y = a.take<double>(S->bfgs ? Bz * LM_HIST * nf : 0);
   S->theta_max = a.take<double>(Bz); S->theta_min = a.take<double>(Bz);
   S->status = a.take<int64_t>(Bz); S->iters = a.take<int64_t>(Bz); S->acc = a.take<int64_t>(Bz);
   S->fcount = a.take<int64_t>(Bz); S->fc = a.take<int64_t>(Bz);
-  S->active = a.take<uint8_t>(Bz); S->hq_init = a.take<uint8_t>(Bz); S->d_any = a.take<uint8_t>(2);
+  S->active = a.take<uint8_t>(Bz); S->lm_cnt = a.take<uint8_t>(Bz); S->lm_skip = a.take<uint8_t>(Bz); S->d_any = a.take<uint8_t>(2);
   // temporaries
   S->A = a.take<double>(Bz * m * nw); S->A_new = a.take<double>(Bz * m * nw);
   S->gradw = a.take<double>(Bz * nw); S->gradw_new = a.take<double>(Bz * nw); S->c = a.take<double>(Bz * m);
@@ -1111,14 +1158,14 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
   hipLaunchKernelGGL(k_init_state, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->free32, S->ineq_row,
                      S->row_slack, S->gl, S->hasL, S->hasU, S->wl0, S->wu0, S->opt.mu_init, S->X, S->g, S->grad, S->w,
                      S->zL, S->zU, S->theta_max, S->theta_min, S->mu, S->active, S->status, S->iters, S->acc,
-                     S->filt_t, S->filt_p, S->fcount, S->dwl, S->d_inf, S->hq_init, S->r1, S->r2, S->M);
+                     S->filt_t, S->filt_p, S->fcount, S->dwl, S->d_inf, S->lm_cnt, S->lm_skip, S->r1, S->r2, S->M);
   LAUNCHED("k_init_state");
   CK(cpl_ipm_dense_a(B, m, nw, nf, S->nnz_rec, S->amap, S->row_slack, S->J, S->A, nullptr, st));
   CK(cpl_kkt_solve(0, B, nw, m, S->M, S->A, S->r1, S->r2, S->mu, S->zeros_B, nullptr, S->dw, S->dy, S->delta_w,
                    S->delta_c, S->info, S->ws, st));
   hipLaunchKernelGGL(k_y0, dim3(blocks_for(B)), dim3(256), 0, st, B, m, S->dy, S->info, S->y);
   LAUNCHED("k_y0");
-  if (S->bfgs) {  // model initialised to I, rescaled by the first update (IPOPT's scalar1 s'y / s's)
+  if (S->bfgs) {  // model initialised to init_val I (IPOPT's limited_memory_init_val = 1)
     hipLaunchKernelGGL(k_eye, dim3(blocks_elems(B * nf * nf)), dim3(256), 0, st, B * nf * nf, nf, S->Hq);
     LAUNCHED("k_eye");
   }

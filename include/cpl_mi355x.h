@@ -450,7 +450,7 @@ int32_t cpl_ipm_dense_a(int64_t batch, int32_t m, int32_t nw, int32_t nf, int32_
  * Converged instances stay in the batch (frozen) until every instance has stopped.
  */
 #define CPL_HESSIAN_EXACT 0          /* analytic Lagrangian Hessian (Ground / no environment), else FD */
-#define CPL_HESSIAN_LIMITED_MEMORY 1 /* damped BFGS: IFOPT's IpoptSolver default */
+#define CPL_HESSIAN_LIMITED_MEMORY 1 /* IPOPT's L-BFGS (6 pairs, scalar1): IFOPT's IpoptSolver default */
 #define CPL_HESSIAN_FD 2             /* central differences of grad f + J^T y */
 
 #define CPL_SOLVE_OPTIMAL 0

@@ -322,7 +322,7 @@ def test_batch_solve_gpu_eight_contacts():
 
 def test_batch_solve_limited_memory_oracle_cpu():
     """IFOPT's default Hessian mode (the reference's IpoptSolver keeps it: src/CentroidalPlanner.cpp:22-29):
-    the damped BFGS model, on the host path over the oracle's callbacks."""
+    IPOPT's limited-memory BFGS model (6 pairs, scalar1), on the host path over the oracle's callbacks."""
     cpl = solve_problem()
     prob = cpl.GetCplProblem()
     X0, mass = solve_inputs(prob, 4, seed=11)
@@ -335,7 +335,7 @@ def test_batch_solve_limited_memory_oracle_cpu():
 
 @pytest.mark.gpu
 def test_batch_solve_gpu_limited_memory():
-    """The limited-memory (BFGS) mode on the device with the kernel callbacks, graph-captured."""
+    """The limited-memory (L-BFGS) mode on the device with the kernel callbacks, graph-captured."""
     from centroidalplanner_amd.batch_ipm import KernelEvaluator
 
     cpl = solve_problem()

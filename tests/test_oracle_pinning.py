@@ -36,9 +36,9 @@ class OracleEvaluator:
 
 
 def _gpu_evaluator(problem):
-    from centroidalplanner_amd.solver import TorchEvaluator
-
-    return TorchEvaluator(problem)
+    """The product path: no evaluator injected, so Solve() runs the native solve engine (the whole
+    interior-point iteration in HIP kernels over the GPU callbacks)."""
+    return None
 
 
 def _start(planner, names, mass):
