@@ -83,7 +83,7 @@ def parse():
     ap.add_argument("--max-soc", type=int, default=1, help="solve5: second-order corrections per iteration")
     ap.add_argument("--hessian", default="exact", choices=["exact", "limited-memory"],
                     help="solve5: exact Lagrangian Hessian (analytic kernel) or IFOPT's limited-memory default")
-    ap.add_argument("--cpu-sample", type=int, default=64, help="solve5: instances in the CPU baseline's sample")
+    ap.add_argument("--cpu-sample", type=int, default=512, help="solve5: instances in the CPU baseline's sample")
     ap.add_argument("--pmc-child", default="", help=argparse.SUPPRESS)
     return ap.parse_args()
 
