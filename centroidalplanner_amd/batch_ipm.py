@@ -531,7 +531,9 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         S["lm_s"].copy_(torch.where(take[:, None, None], Ps, S["lm_s"]))
         S["lm_y"].copy_(torch.where(take[:, None, None], Py, S["lm_y"]))
         S["lm_cnt"].copy_(torch.where(take, nc, torch.where(reset, torch.zeros_like(cnt), cnt)))
-        # the dense model rebuilt from sigma I by the recursion over the stored pairs, oldest first
+        # the dense model rebuilt from sigma I by the recursion over the stored pairs, oldest first (the
+        # device's k_lbfgs evaluates the same model with the recursion unrolled onto vectors: equal up to
+        # rounding)
         sigma = torch.clamp(sy / torch.where(ss > 0, ss, 1.0), min=1e-8, max=1e8)
         H = sigma[:, None, None] * eye_f
         for j in range(LM_HIST):

@@ -326,7 +326,7 @@ __global__ __launch_bounds__(256) void k_lbfgs(int64_t B, int m, int nf, int nw,
                                                double* __restrict__ Hq) {
   const int64_t b = blockIdx.x;
   if (b >= B || !act[b]) return;
-  __shared__ double Ps[LM_HIST][128], Py[LM_HIST][128], Hs[128], yn[256], red[8];
+  __shared__ double Ps[LM_HIST][128], Py[LM_HIST][128], yn[256], red[8];
   const int tid = threadIdx.x;
   const double al = alpha[b];
   for (int r = tid; r < m; r += blockDim.x) yn[r] = y[b * m + r] + al * dy[b * m + r];
@@ -390,23 +390,48 @@ __global__ __launch_bounds__(256) void k_lbfgs(int64_t B, int m, int nf, int nw,
     lm_cnt[b] = (uint8_t)nc;
   }
   const double sigma = fmin(fmax(sy / ss, 1e-8), 1e8);
-  for (int e = tid; e < nf * nf; e += blockDim.x) H[e] = (e / nf == e % nf) ? sigma : 0.0;
+  // The recursion unrolled onto vectors: a_j = B_j s_j = sigma s_j + sum_{i<j} [y_i (y_i's_j) / s_i'y_i
+  // - a_i (a_i's_j) / s_i'a_i] (pair i taken when s_i'a_i > 0), on wave 0 with lanes over x_free
+  // (two entries per lane, wave sums: no barriers); then every entry of
+  // B = sigma I + sum_i [-(a_i a_i') / s_i'a_i + (y_i y_i') / s_i'y_i] once, straight to global
+  // memory.  Same model as the dense rank-2 recursion (which re-read and re-wrote B six times).
+  __shared__ double Pa[LM_HIST][128], s_sa[LM_HIST], s_sy[LM_HIST];
+  if (tid < 64) {
+    const int k0 = tid, k1 = tid + 64;
+    const bool h0 = k0 < nf, h1 = k1 < nf;
+    for (int j = 0; j < nc; ++j) {
+      const double s0 = h0 ? Ps[j][k0] : 0.0, s1 = h1 ? Ps[j][k1] : 0.0;
+      double v0 = sigma * s0, v1 = sigma * s1;
+      for (int i = 0; i < j; ++i) {
+        if (!(s_sa[i] > 0.0)) continue;  // (uniform)
+        const double a0 = h0 ? Pa[i][k0] : 0.0, a1 = h1 ? Pa[i][k1] : 0.0;
+        const double y0 = h0 ? Py[i][k0] : 0.0, y1 = h1 ? Py[i][k1] : 0.0;
+        const double as = wave_sum(a0 * s0 + a1 * s1) / s_sa[i];
+        const double ys = wave_sum(y0 * s0 + y1 * s1) / s_sy[i];
+        v0 = (v0 - a0 * as) + y0 * ys;
+        v1 = (v1 - a1 * as) + y1 * ys;
+      }
+      if (h0) Pa[j][k0] = v0;
+      if (h1) Pa[j][k1] = v1;
+      const double y0 = h0 ? Py[j][k0] : 0.0, y1 = h1 ? Py[j][k1] : 0.0;
+      const double sa = wave_sum(s0 * v0 + s1 * v1);
+      const double sjy = wave_sum(s0 * y0 + s1 * y1);
+      if (tid == 0) {
+        s_sa[j] = sa;
+        s_sy[j] = sjy;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // lane 0's s_sa / s_sy visible to the next j
+    }
+  }
   __syncthreads();
-  for (int j = 0; j < nc; ++j) {
-    for (int i = tid; i < nf; i += blockDim.x) {
-      double v = 0.0;
-      for (int k = 0; k < nf; ++k) v += H[i * nf + k] * Ps[j][k];
-      Hs[i] = v;
+  for (int e = tid; e < nf * nf; e += blockDim.x) {
+    const int r = e / nf, c = e - r * nf;
+    double v = r == c ? sigma : 0.0;
+    for (int i = 0; i < nc; ++i) {
+      if (!(s_sa[i] > 0.0)) continue;  // (uniform; cannot happen for a positive definite model)
+      v = (v - Pa[i][r] * Pa[i][c] / s_sa[i]) + Py[i][r] * Py[i][c] / s_sy[i];
     }
-    __syncthreads();
-    const double sHs = block_dot(Ps[j], Hs);
-    const double sjy = block_dot(Ps[j], Py[j]);
-    if (!(sHs > 0.0)) continue;  // (uniform; cannot happen for a positive definite model)
-    for (int e = tid; e < nf * nf; e += blockDim.x) {
-      const int i = e / nf, c = e - i * nf;
-      H[e] = (H[e] - Hs[i] * Hs[c] / sHs) + Py[j][i] * Py[j][c] / sjy;
-    }
-    __syncthreads();
+    H[e] = v;
   }
 }
 
