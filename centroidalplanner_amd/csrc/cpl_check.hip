@@ -12,6 +12,9 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <string>
 #include <mutex>
 #include <vector>
 
@@ -30,9 +33,18 @@ static int32_t hfail(hipError_t e, const char* what) {
 struct HostIo {
   std::mutex mu;
   hipStream_t stream = nullptr;
-  void* buf = nullptr;
+  void* buf = nullptr;  // device workspace (batches past the zero-copy limit)
   size_t bytes = 0;
+  void* pin = nullptr;  // pinned, device-mapped host staging (small batches: the kernel reads and writes it)
+  size_t pin_bytes = 0;
 };
+// Small batches (the single-instance TNLP callback path) skip the DMA copies: the host arrays are
+// memcpy'd into library-owned coherent pinned memory, the eval kernel reads x and writes g / jac there
+// directly over the host link, and the outputs are memcpy'd back after the stream drains — one launch
+// and one wait instead of 2 + #outputs DMA transfers (each a pageable-memory staging round trip):
+// 22.5 us per single-instance eval_g + eval_jac_g (Ground N = 4) against 31 us for the DMA-staged
+// path.  (Polling hipStreamQuery instead of hipStreamSynchronize measured 4 us slower.)
+constexpr size_t ZERO_COPY_MAX = (size_t)1 << 20;
 static std::mutex g_hostio_mutex;
 static HostIo* g_hostio[64] = {nullptr};  // per device, never freed (process lifetime)
 
@@ -180,6 +192,53 @@ int32_t cpl_eval_batch_host(const cpl_problem_desc* d, int64_t batch, const doub
   const size_t sf = h_f ? up256(8 * B) : 0, sd = h_grad ? up256(8 * B * n) : 0, sn = h_norms ? 256 : 0;
   const size_t need = sx + sm + st8 + sg + sj + sf + sd + sn;
   hipError_t e;
+  if (need <= ZERO_COPY_MAX) {
+    if (need > io->pin_bytes) {
+      if (io->pin) {
+        if ((e = hipStreamSynchronize(io->stream)) != hipSuccess) return hfail(e, "hipStreamSynchronize");
+        (void)hipHostFree(io->pin);
+        io->pin = nullptr;
+        io->pin_bytes = 0;
+      }
+      const size_t cap = std::max(need, (size_t)64 << 10);
+      if ((e = hipHostMalloc(&io->pin, cap, hipHostMallocCoherent | hipHostMallocMapped)) != hipSuccess)
+        return hfail(e, "hipHostMalloc host-io staging");
+      io->pin_bytes = cap;
+    }
+    void* dpin = nullptr;  // the device's address of the staging (the same address on this platform)
+    if ((e = hipHostGetDevicePointer(&dpin, io->pin, 0)) != hipSuccess) return hfail(e, "hipHostGetDevicePointer");
+    char* hp = static_cast<char*>(io->pin);
+    char* dp = static_cast<char*>(dpin);
+    size_t off = 0;
+    auto carve = [&](size_t sz, const void* src, size_t copy) {
+      if (!sz) return (void*)nullptr;
+      if (src && copy) memcpy(hp + off, src, copy);
+      void* r = dp + off;
+      off += sz;
+      return r;
+    };
+    const double* px = static_cast<const double*>(carve(sx, h_x, 8 * B * n));
+    const double* pm = static_cast<const double*>(carve(sm, h_mass, 8 * B));
+    const uint8_t* pt = static_cast<const uint8_t*>(carve(st8, h_env_tag, B));
+    const size_t og = off;
+    double* pg = static_cast<double*>(carve(sg, nullptr, 0));
+    const size_t oj = off;
+    double* pj = static_cast<double*>(carve(sj, nullptr, 0));
+    const size_t of = off;
+    double* pf = static_cast<double*>(carve(sf, nullptr, 0));
+    const size_t od = off;
+    double* pd = static_cast<double*>(carve(sd, nullptr, 0));
+    const size_t on = off;
+    double* pn = static_cast<double*>(carve(sn, nullptr, 0));
+    if ((st = cpl_eval_batch_ex(d, batch, px, pm, pt, pg, pj, pf, pd, pn, flags, io->stream))) return st;
+    if ((e = hipStreamSynchronize(io->stream)) != hipSuccess) return hfail(e, "hipStreamSynchronize");
+    if (pg) memcpy(h_g, hp + og, 8 * B * m);
+    if (pj) memcpy(h_jac, hp + oj, 8 * B * nnz);
+    if (pf) memcpy(h_f, hp + of, 8 * B);
+    if (pd) memcpy(h_grad, hp + od, 8 * B * n);
+    if (pn) memcpy(h_norms, hp + on, 16);
+    return CPL_OK;
+  }
   if (need > io->bytes) {
     if (io->buf) {
       e = hipStreamSynchronize(io->stream);

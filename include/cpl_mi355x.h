@@ -238,9 +238,11 @@ int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_t
 /* ---- host-buffer entry points ------------------------------------------------------------ */
 /*
  * cpl_eval_batch_ex on HOST arrays (SURVEY.md §8(b) cpl_eval_batch_host): the same arguments and
- * layouts with host pointers; the arrays are staged through a library-owned device workspace (one
- * per device, grown on demand, serialised by a lock) on a library-owned stream, and the call returns
- * when the outputs are back in host memory.  The computation is the GPU kernel of cpl_eval_batch —
+ * layouts with host pointers, on a library-owned stream (one per device, serialised by a lock); the
+ * call returns when the outputs are back in host memory.  Batches whose inputs + outputs fit 1 MiB
+ * (the single-instance callback path) are copied into library-owned pinned host memory that the
+ * kernel reads and writes directly (one launch, no DMA transfers); larger ones are staged through a
+ * library-owned device workspace (grown on demand) with DMA copies.  The computation is the GPU kernel of cpl_eval_batch —
  * the library has no CPU evaluator.  This is what a single-instance IPOPT TNLP adapter binds
  * (IpoptAdapter::eval_g / eval_jac_g / eval_f / eval_grad_f behind src/CentroidalPlanner.cpp:29
  * [IFOPT-ext] hand host arrays); h_norms, if not NULL, receives the 2 residual norms.

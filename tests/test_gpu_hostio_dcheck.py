@@ -52,8 +52,12 @@ def derivative_test_ref(prob, x, mass, tag, pert, tol):
     return flagged.reshape(B, -1).sum(axis=1), rel, approx, exact
 
 
+# batches whose inputs + outputs fit 1 MiB take the zero-copy path (pinned staging read / written by the
+# kernel), larger ones the device workspace with DMA copies; both must equal the device-array call
 @pytest.mark.parametrize("name,batch,folded", [("ground4_1m", 1000, False), ("ground4_1m", 333, True),
-                                               ("sq8", 64, False), ("mixed16", 40, True)])
+                                               ("sq8", 64, False), ("mixed16", 40, True),
+                                               ("ground4_1m", 1, False), ("ground4_1m", 1, True), ("sq8", 1, False),
+                                               ("mixed16", 1, False), ("sq8", 600, True), ("mixed16", 301, False)])
 def test_eval_batch_host_matches_device(name, batch, folded):
     prob, x, mass, tag = _inputs(name, batch)
     dev = torch.device("cuda:0")
