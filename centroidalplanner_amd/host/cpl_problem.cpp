@@ -202,20 +202,10 @@ void hip_check(hipError_t e, const char* what) {
 CplTNLP::CplTNLP(CplProblem::Ptr problem, int device) : _problem(std::move(problem)) {
   if (!_problem) throw std::invalid_argument("CplTNLP needs a problem");
   if (device >= 0) hip_check(hipSetDevice(device), "hipSetDevice");
-  const size_t len = (size_t)(_problem->n() + _problem->m() + _problem->nnz() + 1 + _problem->n());
-  hipStream_t s = nullptr;
-  hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
-  _stream = s;
-  hip_check(hipMalloc(reinterpret_cast<void**>(&_dx), sizeof(double) * len), "hipMalloc");
-  hip_check(hipHostMalloc(reinterpret_cast<void**>(&_hbuf), sizeof(double) * len, hipHostMallocDefault),
-            "hipHostMalloc");
+  _hbuf.assign((size_t)(_problem->n() + _problem->m() + _problem->nnz() + 1 + _problem->n()), 0.0);
 }
 
-CplTNLP::~CplTNLP() {
-  if (_dx) (void)hipFree(_dx);
-  if (_hbuf) (void)hipHostFree(_hbuf);
-  if (_stream) (void)hipStreamDestroy(static_cast<hipStream_t>(_stream));
-}
+CplTNLP::~CplTNLP() = default;
 
 bool CplTNLP::get_nlp_info(int32_t& n, int32_t& m, int32_t& nnz_jac_g, int32_t& nnz_h_lag) const {
   n = _problem->n();
@@ -240,17 +230,13 @@ bool CplTNLP::get_starting_point(int32_t n, bool init_x, double* x) const {
 bool CplTNLP::Evaluate(const double* x, bool new_x) {
   const int32_t n = _problem->n(), m = _problem->m(), nnz = _problem->nnz();
   if (!new_x && _valid && std::equal(_x_cached.begin(), _x_cached.end(), x)) return true;
-  hipStream_t s = static_cast<hipStream_t>(_stream);
-  std::memcpy(_hbuf, x, sizeof(double) * n);
-  const size_t len = (size_t)(n + m + nnz + 1 + n);
-  if (hipMemcpyAsync(_dx, _hbuf, sizeof(double) * n, hipMemcpyHostToDevice, s) != hipSuccess) return false;
-  double* g = _dx + n;
+  double* g = _hbuf.data() + n;
   double* jac = g + m;
   double* f = jac + nnz;
   double* grad = f + 1;
-  if (cpl_eval_batch(&_problem->Desc(), 1, _dx, nullptr, nullptr, g, jac, f, grad, s) != CPL_OK) return false;
-  if (hipMemcpyAsync(_hbuf + n, g, sizeof(double) * (len - n), hipMemcpyDeviceToHost, s) != hipSuccess) return false;
-  if (hipStreamSynchronize(s) != hipSuccess) return false;
+  std::copy(x, x + n, _hbuf.data());
+  if (cpl_eval_batch_host(&_problem->Desc(), 1, _hbuf.data(), nullptr, nullptr, g, jac, f, grad, nullptr, 0) != CPL_OK)
+    return false;
   _x_cached.assign(x, x + n);
   _valid = true;
   ++_launches;
@@ -265,14 +251,14 @@ bool CplTNLP::eval_f(int32_t n, const double* x, bool new_x, double& obj_value) 
 
 bool CplTNLP::eval_grad_f(int32_t n, const double* x, bool new_x, double* grad_f) {
   if (n != _problem->n() || !Evaluate(x, new_x)) return false;
-  const double* src = _hbuf + n + _problem->m() + _problem->nnz() + 1;
+  const double* src = _hbuf.data() + n + _problem->m() + _problem->nnz() + 1;
   std::copy(src, src + n, grad_f);
   return true;
 }
 
 bool CplTNLP::eval_g(int32_t n, const double* x, bool new_x, int32_t m, double* g) {
   if (n != _problem->n() || m != _problem->m() || !Evaluate(x, new_x)) return false;
-  std::copy(_hbuf + n, _hbuf + n + m, g);
+  std::copy(_hbuf.data() + n, _hbuf.data() + n + m, g);
   return true;
 }
 
@@ -281,7 +267,7 @@ bool CplTNLP::eval_jac_g(int32_t n, const double* x, bool new_x, int32_t m, int3
   if (n != _problem->n() || m != _problem->m() || nele_jac != _problem->nnz()) return false;
   if (!values) return cpl_structure(&_problem->Desc(), iRow, jCol, nullptr) == CPL_OK;
   if (!Evaluate(x, new_x)) return false;
-  const double* src = _hbuf + n + m;
+  const double* src = _hbuf.data() + n + m;
   std::copy(src, src + nele_jac, values);
   return true;
 }

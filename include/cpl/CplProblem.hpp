@@ -109,7 +109,8 @@ class CplProblem {
 
 // The IPOPT TNLP hooks IFOPT's IpoptAdapter exposes for a CplProblem [IFOPT-ext], with IPOPT's
 // argument meaning (C_STYLE indices, inf = 1e20, eval_jac_g(values == NULL) = structure).  Every
-// callback of one x runs ONE fused launch on the GPU (g, jac, f and grad together) and serves the
+// callback of one x runs ONE fused launch on the GPU (g, jac, f and grad together, through
+// cpl_eval_batch_host: zero-copy pinned staging at this size) and serves the
 // remaining callbacks of that x from the cached results, so IPOPT's eval_f / eval_grad_f /
 // eval_g / eval_jac_g sequence costs one launch per iterate.  A maintainer's Ipopt::TNLP
 // subclass forwards to these one-to-one.
@@ -137,9 +138,7 @@ class CplTNLP {
   bool Evaluate(const double* x, bool new_x);
 
   CplProblem::Ptr _problem;
-  void* _stream = nullptr;
-  double* _dx = nullptr;   // device: x | g | jac | f | grad (one allocation)
-  double* _hbuf = nullptr; // pinned host mirror of the same layout
+  std::vector<double> _hbuf;  // x | g | jac | f | grad of the cached iterate (host)
   std::vector<double> _x_cached;
   bool _valid = false;
   int64_t _launches = 0;
