@@ -248,6 +248,11 @@ __global__ __launch_bounds__(256) void cpl_ipm_max_step_kernel(int64_t batch, in
 //   r1 = -(grad_phi + A^T y), r2 = -c, M = diag(Sigma) + [H 0; 0 0] (H: nf x nf, may be NULL),
 //   theta = sum |c|, phi = f - mu (sum log(w - wl) + sum log(wu - w)),
 //   Mr_diag = Sigma + sqrt(mu) / max(1, |w|)^2 (the feasibility step's diagonal).
+// LM: the Hessian block comes as the compact limited-memory model of the native engine's k_lbfgs
+// (per instance [sigma, nv, U (lm_pairs x nf), W (lm_pairs x nf)]): H = sigma I + sum_{i < nv}
+// (-u_i u_i' + w_i w_i'), each entry evaluated here in the order the dense build used, staged per wave
+// in dynamic LDS — the dense nf x nf model never goes through memory.
+template <bool LM>
 __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
     int64_t batch, int nw, int m, int nf, const double* __restrict__ w, const double* __restrict__ zL,
     const double* __restrict__ zU, const double* __restrict__ gw, const double* __restrict__ A,
@@ -256,7 +261,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
     const double* __restrict__ wl0, const double* __restrict__ wu0, const double* __restrict__ H, int h_sym,
     double* __restrict__ M, double* __restrict__ r1, double* __restrict__ r2, double* __restrict__ gphi,
     double* __restrict__ mr_diag, double* __restrict__ theta, double* __restrict__ phi,
-    const uint8_t* __restrict__ active) {
+    const uint8_t* __restrict__ active, const double* __restrict__ Hc, int lm_pairs) {
   const int64_t b = (int64_t)blockIdx.x * IPM_WAVES + (threadIdx.x >> 6);
   if (b >= batch || (active && !active[b])) return;  // converged: its Newton system is never read
   const int lane = threadIdx.x & 63;
@@ -294,14 +299,41 @@ __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
   // the wave's own LDS row of Sigma needs no workgroup barrier, only the wave's LDS ordering
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS stores have landed
   __builtin_amdgcn_wave_barrier();
-  const double* Hb = H ? H + b * (int64_t)nf * nf : nullptr;
-  // h_sym: H is the raw central-difference matrix (cpl_ipm_fd_hessian_raw), symmetrised here as
-  // batch_ipm.py's fd_hessian does: 0.5 (H + H^T)
-  for (int e = lane; e < nw * nw; e += 64) {
-    const int k = e / nw, j = e - k * nw;
-    double v = (j == k) ? sg[k] : 0.0;
-    if (Hb && k < nf && j < nf) v += h_sym ? 0.5 * (Hb[k * nf + j] + Hb[j * nf + k]) : Hb[k * nf + j];
-    Mb[e] = v;
+  if (LM) {
+    extern __shared__ __align__(16) double lm_dyn[];
+    const int per = 2 * lm_pairs * nf;
+    double* UW = lm_dyn + (threadIdx.x >> 6) * per;  // this wave's U | W
+    const double* hc = Hc + b * (int64_t)(2 + per);
+    const double sigma = hc[0];
+    const int nv = (int)hc[1];
+    for (int e = lane; e < nv * nf; e += 64) {
+      UW[e] = hc[2 + e];
+      UW[lm_pairs * nf + e] = hc[2 + lm_pairs * nf + e];
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    const double* U = UW;
+    const double* W = UW + lm_pairs * nf;
+    for (int e = lane; e < nw * nw; e += 64) {
+      const int k = e / nw, j = e - k * nw;
+      double v = (j == k) ? sg[k] : 0.0;
+      if (k < nf && j < nf) {
+        double h = j == k ? sigma : 0.0;
+        for (int i = 0; i < nv; ++i) h = (h - U[i * nf + k] * U[i * nf + j]) + W[i * nf + k] * W[i * nf + j];
+        v += h;
+      }
+      Mb[e] = v;
+    }
+  } else {
+    const double* Hb = H ? H + b * (int64_t)nf * nf : nullptr;
+    // h_sym: H is the raw central-difference matrix (cpl_ipm_fd_hessian_raw), symmetrised here as
+    // batch_ipm.py's fd_hessian does: 0.5 (H + H^T)
+    for (int e = lane; e < nw * nw; e += 64) {
+      const int k = e / nw, j = e - k * nw;
+      double v = (j == k) ? sg[k] : 0.0;
+      if (Hb && k < nf && j < nf) v += h_sym ? 0.5 * (Hb[k * nf + j] + Hb[j * nf + k]) : Hb[k * nf + j];
+      Mb[e] = v;
+    }
   }
   double th = 0.0;
   for (int r = lane; r < m; r += 64) {
@@ -631,10 +663,11 @@ int32_t cpl_ipm_newton_setup(int64_t batch, int32_t nw, int32_t m, int32_t nf, c
   if (!d_w || !d_zL || !d_zU || !d_gw || (m > 0 && (!d_A || !d_y || !d_c || !d_r2)) || !d_f || !d_mu || !d_hasL ||
       !d_hasU || !d_wl0 || !d_wu0 || !d_M || !d_r1 || !d_gphi || !d_mr_diag || !d_theta || !d_phi)
     return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_newton_setup: missing buffer");
-  IPM_LAUNCH(cpl_ipm_newton_setup_kernel, "cpl_ipm_newton_setup", batch, (int)nw, (int)m, (int)nf, d_w, d_zL, d_zU,
-             d_gw, d_A, d_y, d_c, d_f, d_mu, d_hasL, d_hasU, d_wl0, d_wu0, d_H, (int)h_sym, d_M, d_r1, d_r2, d_gphi,
-             d_mr_diag, d_theta, d_phi, d_active);
+  IPM_LAUNCH(cpl_ipm_newton_setup_kernel<false>, "cpl_ipm_newton_setup", batch, (int)nw, (int)m, (int)nf, d_w, d_zL,
+             d_zU, d_gw, d_A, d_y, d_c, d_f, d_mu, d_hasL, d_hasU, d_wl0, d_wu0, d_H, (int)h_sym, d_M, d_r1, d_r2,
+             d_gphi, d_mr_diag, d_theta, d_phi, d_active, nullptr, 0);
 }
+
 
 int32_t cpl_ipm_post_step(int64_t batch, int32_t nw, const double* d_w, const double* d_dw, const double* d_zL,
                           const double* d_zU, const double* d_gphi, const double* d_mu, const double* d_tau,
@@ -738,3 +771,28 @@ int32_t cpl_ipm_fd_hessian_raw(int64_t batch, int32_t n, int32_t nf, const int64
 }
 
 }  // extern "C"
+
+namespace cpl {
+// The native engine's Newton setup over its compact limited-memory model (see the LM kernel above);
+// the arguments otherwise as cpl_ipm_newton_setup.
+int32_t ipm_newton_setup_lm(int64_t batch, int32_t nw, int32_t m, int32_t nf, const double* d_w, const double* d_zL,
+                            const double* d_zU, const double* d_gw, const double* d_A, const double* d_y,
+                            const double* d_c, const double* d_f, const double* d_mu, const uint8_t* d_hasL,
+                            const uint8_t* d_hasU, const double* d_wl0, const double* d_wu0, const double* d_Hc,
+                            int32_t lm_pairs, double* d_M, double* d_r1, double* d_r2, double* d_gphi,
+                            double* d_mr_diag, double* d_theta, double* d_phi, const uint8_t* d_active, void* stream) {
+  if (batch < 0 || nw <= 0 || nw > 128 || m < 0 || nf < 0 || nf > nw || lm_pairs <= 0 || !d_Hc)
+    return fail(CPL_ERR_INVALID_ARGUMENT, "ipm_newton_setup_lm: bad arguments");
+  if (batch == 0) return CPL_OK;
+  const int64_t blocks = (batch + IPM_WAVES - 1) / IPM_WAVES;
+  if (blocks > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "ipm_newton_setup_lm: batch too large");
+  const size_t lds = sizeof(double) * IPM_WAVES * 2 * (size_t)lm_pairs * nf;
+  hipLaunchKernelGGL(cpl_ipm_newton_setup_kernel<true>, dim3((unsigned)blocks), dim3(64 * IPM_WAVES), lds,
+                     (hipStream_t)stream, batch, (int)nw, (int)m, (int)nf, d_w, d_zL, d_zU, d_gw, d_A, d_y, d_c, d_f,
+                     d_mu, d_hasL, d_hasU, d_wl0, d_wu0, nullptr, 0, d_M, d_r1, d_r2, d_gphi, d_mr_diag, d_theta, d_phi,
+                     d_active, d_Hc, (int)lm_pairs);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("ipm_newton_setup_lm launch: ") + hipGetErrorString(e));
+  return CPL_OK;
+}
+}  // namespace cpl

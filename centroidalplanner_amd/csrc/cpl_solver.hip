@@ -29,6 +29,13 @@
 #include "cpl_status.hpp"
 
 namespace cpl {
+// cpl_ipm.hip: cpl_ipm_newton_setup over the engine's compact limited-memory model
+int32_t ipm_newton_setup_lm(int64_t batch, int32_t nw, int32_t m, int32_t nf, const double* d_w, const double* d_zL,
+                            const double* d_zU, const double* d_gw, const double* d_A, const double* d_y,
+                            const double* d_c, const double* d_f, const double* d_mu, const uint8_t* d_hasL,
+                            const uint8_t* d_hasU, const double* d_wl0, const double* d_wu0, const double* d_Hc,
+                            int32_t lm_pairs, double* d_M, double* d_r1, double* d_r2, double* d_gphi,
+                            double* d_mr_diag, double* d_theta, double* d_phi, const uint8_t* d_active, void* stream);
 namespace {
 
 constexpr int FMAX = 64;          // filter entries kept per instance (a ring), as batch_ipm.FMAX
@@ -315,12 +322,15 @@ __global__ void k_rest(int64_t B, const uint8_t* __restrict__ failed, const uint
 //   over the stored pairs, oldest first: B <- B - (Bs)(Bs)' / s'Bs + y y' / s'y  (mathematically the
 //   compact representation IPOPT applies; B stays bitwise symmetric: every update is an outer product).
 constexpr int LM_HIST = 6, LM_MAX_SKIP = 2;
-__global__ __launch_bounds__(256) void k_lbfgs(int64_t B, int m, int nf, int nw, const uint8_t* __restrict__ act,
+// doubles per instance of the compact model: sigma, the number of pairs nv, U [LM_HIST][nf], W [LM_HIST][nf]
+__host__ __device__ constexpr int64_t LMC(int nf) { return 2 + 2 * (int64_t)LM_HIST * nf; }
+__global__ __launch_bounds__(256) void k_lbfgs(int64_t B, int m, int nf, int nw, int nnz_rec,
+                                               const int32_t* __restrict__ amap, const uint8_t* __restrict__ act,
                                                const double* __restrict__ w_old, const double* __restrict__ w_new,
                                                const double* __restrict__ y, const double* __restrict__ dy,
                                                const double* __restrict__ alpha, const double* __restrict__ gw_old,
-                                               const double* __restrict__ A_old, const double* __restrict__ gw_new,
-                                               const double* __restrict__ A_new, double* __restrict__ lm_s,
+                                               const double* __restrict__ J_old, const double* __restrict__ gw_new,
+                                               const double* __restrict__ J_new, double* __restrict__ lm_s,
                                                double* __restrict__ lm_y, uint8_t* __restrict__ lm_cnt,
                                                uint8_t* __restrict__ lm_skip, const uint8_t* __restrict__ failed,
                                                double* __restrict__ Hq) {
@@ -337,17 +347,45 @@ __global__ __launch_bounds__(256) void k_lbfgs(int64_t B, int m, int nf, int nw,
   const int shift = cnt == LM_HIST ? 1 : 0, last = cnt - shift;
   double* gs = lm_s + b * (int64_t)LM_HIST * nf;
   double* gy = lm_y + b * (int64_t)LM_HIST * nf;
-  for (int k = tid; k < nf; k += blockDim.x) {
-    double jn = 0.0, jo = 0.0;
-    for (int r = 0; r < m; ++r) {
-      jn += A_new[(b * m + r) * nw + k] * yn[r];
-      jo += A_old[(b * m + r) * nw + k] * yn[r];
+  {  // J_free^T y at both points, straight from the values-only Jacobian records (the entries of A =
+     // [J_free | -P] as cpl_ipm_dense_a forms them: amap -1 = 0, -2 = constant 1, NaN = 0); the rows
+     // split over `parts` thread groups, partials summed in fixed order
+    __shared__ double pjn[4][128], pjo[4][128];
+    const int kp = nf <= 64 ? 64 : 128, parts = (int)blockDim.x / kp;
+    const int k = tid % kp, part = tid / kp;
+    if (k < nf && part < parts) {
+      const double* jnb = J_new + b * (int64_t)nnz_rec;
+      const double* job = J_old + b * (int64_t)nnz_rec;
+      double jn = 0.0, jo = 0.0;
+      for (int r = part; r < m; r += parts) {
+        const int q = amap[r * nf + k];
+        if (q == -1) continue;  // structural zero: A's entry is 0
+        double an = 1.0, ao = 1.0;
+        if (q >= 0) {
+          an = jnb[q];
+          ao = job[q];
+          an = an == an ? an : 0.0;
+          ao = ao == ao ? ao : 0.0;
+        }
+        jn += an * yn[r];
+        jo += ao * yn[r];
+      }
+      pjn[part][k] = jn;
+      pjo[part][k] = jo;
     }
-    Ps[last][k] = w_new[b * nw + k] - w_old[b * nw + k];
-    Py[last][k] = (gw_new[b * nw + k] + jn) - (gw_old[b * nw + k] + jo);
-    for (int j = 0; j < last; ++j) {
-      Ps[j][k] = gs[(j + shift) * nf + k];
-      Py[j][k] = gy[(j + shift) * nf + k];
+    __syncthreads();
+    for (int k2 = tid; k2 < nf; k2 += blockDim.x) {
+      double jn = pjn[0][k2], jo = pjo[0][k2];
+      for (int q = 1; q < parts; ++q) {
+        jn += pjn[q][k2];
+        jo += pjo[q][k2];
+      }
+      Ps[last][k2] = w_new[b * nw + k2] - w_old[b * nw + k2];
+      Py[last][k2] = (gw_new[b * nw + k2] + jn) - (gw_old[b * nw + k2] + jo);
+      for (int j = 0; j < last; ++j) {
+        Ps[j][k2] = gs[(j + shift) * nf + k2];
+        Py[j][k2] = gy[(j + shift) * nf + k2];
+      }
     }
   }
   __syncthreads();
@@ -365,15 +403,16 @@ __global__ __launch_bounds__(256) void k_lbfgs(int64_t B, int m, int nf, int nw,
   const double sy = block_dot(Ps[last], Py[last]);
   const double ss = block_dot(Ps[last], Ps[last]);
   const double yy = block_dot(Py[last], Py[last]);
-  double* H = Hq + b * (int64_t)nf * nf;
+  double* hc = Hq + b * (int64_t)LMC(nf);  // the compact model: [sigma, nv, U, W]
   const bool skip = !(sy > sqrt(DBL_EPSILON) * sqrt(ss) * sqrt(yy));
   if (skip || failed[b]) {  // (uniform branch)
     if (!failed[b] && skipped <= LM_MAX_SKIP) {
       if (tid == 0) lm_skip[b] = (uint8_t)skipped;
       return;
     }
-    for (int e = tid; e < nf * nf; e += blockDim.x) H[e] = (e / nf == e % nf) ? 1.0 : 0.0;
-    if (tid == 0) {
+    if (tid == 0) {  // the model back to init_val I
+      hc[0] = 1.0;
+      hc[1] = 0.0;
       lm_skip[b] = 0;
       lm_cnt[b] = 0;
     }
@@ -393,7 +432,8 @@ __global__ __launch_bounds__(256) void k_lbfgs(int64_t B, int m, int nf, int nw,
   // The recursion unrolled onto vectors: a_j = B_j s_j = sigma s_j + sum_{i<j} [y_i (y_i's_j) / s_i'y_i
   // - a_i (a_i's_j) / s_i'a_i] (pair i taken when s_i'a_i > 0), on wave 0 with lanes over x_free
   // (two entries per lane, wave sums: no barriers); then every entry of
-  // B = sigma I + sum_i [-(a_i a_i') / s_i'a_i + (y_i y_i') / s_i'y_i] once, straight to global
+  // B = sigma I + sum_i [-(a_i a_i') / s_i'a_i + (y_i y_i') / s_i'y_i] once (as products of the scaled
+  // vectors a_i / sqrt(s_i'a_i), y_i / sqrt(s_i'y_i)), straight to global
   // memory.  Same model as the dense rank-2 recursion (which re-read and re-wrote B six times).
   __shared__ double Pa[LM_HIST][128], s_sa[LM_HIST], s_sy[LM_HIST];
   if (tid < 64) {
@@ -422,16 +462,31 @@ __global__ __launch_bounds__(256) void k_lbfgs(int64_t B, int m, int nf, int nw,
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // lane 0's s_sa / s_sy visible to the next j
     }
+    // scaled in place, u_i = a_i / sqrt(s_i'a_i) and v_i = y_i / sqrt(s_i'y_i) (both > 0 for a taken
+    // pair), so that every model entry is a sum of products u_r u_c, v_r v_c: symmetric bit for bit
+    for (int i = 0; i < nc; ++i) {
+      if (!(s_sa[i] > 0.0)) continue;
+      const double qa = sqrt(s_sa[i]), qy = sqrt(s_sy[i]);
+      if (h0) { Pa[i][k0] /= qa; Py[i][k0] /= qy; }
+      if (h1) { Pa[i][k1] /= qa; Py[i][k1] /= qy; }
+    }
   }
   __syncthreads();
-  for (int e = tid; e < nf * nf; e += blockDim.x) {
-    const int r = e / nf, c = e - r * nf;
-    double v = r == c ? sigma : 0.0;
-    for (int i = 0; i < nc; ++i) {
-      if (!(s_sa[i] > 0.0)) continue;  // (uniform; cannot happen for a positive definite model)
-      v = (v - Pa[i][r] * Pa[i][c] / s_sa[i]) + Py[i][r] * Py[i][c] / s_sy[i];
-    }
-    H[e] = v;
+  // the taken pairs (s_i'a_i > 0: always, for a positive definite model) in order, as the compact
+  // model the Newton setup expands entry by entry (ipm_newton_setup_lm)
+  for (int e = tid; e < nc * nf; e += blockDim.x) {
+    const int i = e / nf, k = e - i * nf;
+    if (!(s_sa[i] > 0.0)) continue;
+    int pos = 0;
+    for (int q = 0; q < i; ++q) pos += s_sa[q] > 0.0;
+    hc[2 + pos * nf + k] = Pa[i][k];
+    hc[2 + LM_HIST * nf + pos * nf + k] = Py[i][k];
+  }
+  if (tid == 0) {
+    int nv = 0;
+    for (int q = 0; q < nc; ++q) nv += s_sa[q] > 0.0;
+    hc[0] = sigma;
+    hc[1] = (double)nv;
   }
 }
 
@@ -558,11 +613,12 @@ __global__ __launch_bounds__(256) void k_final(int64_t B, int m, const double* _
   }
 }
 
-__global__ void k_eye(int64_t total, int nf, double* __restrict__ H) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= total) return;
-  const int q = (int)(e % ((int64_t)nf * nf));
-  H[e] = (q / nf == q % nf) ? 1.0 : 0.0;
+// the compact limited-memory model of every instance at init_val I: sigma = 1, no pairs
+__global__ void k_lm_init(int64_t B, int nf, double* __restrict__ Hq) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  Hq[b * LMC(nf)] = 1.0;
+  Hq[b * LMC(nf) + 1] = 0.0;
 }
 
 __global__ void k_repeat(int64_t B, int rep, const double* __restrict__ src, double* __restrict__ dst,
@@ -617,7 +673,7 @@ struct cpl_solver {
   int64_t *status, *iters, *acc, *fcount;
   uint8_t *active, *lm_cnt, *lm_skip, *d_any;
   // iteration temporaries
-  double *A, *A_new, *gradw, *gradw_new, *c, *err0, *base, *mu_o, *ft, *fp, *tau, *X, *H, *M, *Mr, *r1, *r2, *gphi,
+  double *A, *gradw, *gradw_new, *c, *err0, *base, *mu_o, *ft, *fp, *tau, *X, *H, *M, *Mr, *r1, *r2, *gphi,
       *mr_diag, *theta_k, *phi_k, *dw, *dy, *delta_w, *delta_c, *dzL, *dzU, *a_max, *a_z, *gd, *ws;
   int64_t* fc;
   int32_t* info;
@@ -685,7 +741,7 @@ int32_t step(cpl_solver* S) {
   const double* Hblk = nullptr;
   int h_sym = 0;
   if (S->bfgs) {
-    Hblk = S->Hq;
+    // the compact model is expanded inside the Newton setup (ipm_newton_setup_lm below)
   } else if (S->analytic_H) {
     CK(cpl_lagrangian_hessian(&S->desc, B, S->X, S->y, S->act, S->free32, nf, S->H, st));
     Hblk = S->H;
@@ -710,9 +766,14 @@ int32_t step(cpl_solver* S) {
     h_sym = 1;
   }
   // Newton system, step, multiplier steps, fraction-to-the-boundary steps
-  CK(cpl_ipm_newton_setup(B, nw, m, nf, S->w, S->zL, S->zU, S->gradw, S->A, S->y, S->c, S->f, S->mu_o, S->hasL,
-                          S->hasU, S->wl0, S->wu0, Hblk, h_sym, S->M, S->r1, S->r2, S->gphi, S->mr_diag, S->theta_k,
-                          S->phi_k, S->bfgs ? nullptr : S->act, st));
+  if (S->bfgs)
+    CK(ipm_newton_setup_lm(B, nw, m, nf, S->w, S->zL, S->zU, S->gradw, S->A, S->y, S->c, S->f, S->mu_o, S->hasL,
+                           S->hasU, S->wl0, S->wu0, S->Hq, LM_HIST, S->M, S->r1, S->r2, S->gphi, S->mr_diag,
+                           S->theta_k, S->phi_k, nullptr, st));
+  else
+    CK(cpl_ipm_newton_setup(B, nw, m, nf, S->w, S->zL, S->zU, S->gradw, S->A, S->y, S->c, S->f, S->mu_o, S->hasL,
+                            S->hasU, S->wl0, S->wu0, Hblk, h_sym, S->M, S->r1, S->r2, S->gphi, S->mr_diag, S->theta_k,
+                            S->phi_k, S->act, st));
   CK(cpl_kkt_solve(0, B, nw, m, S->M, S->A, S->r1, S->r2, S->mu_o, S->dwl, S->act, S->dw, S->dy, S->delta_w,
                    S->delta_c, S->info, S->ws, st));
   CK(cpl_ipm_post_step(B, nw, S->w, S->dw, S->zL, S->zU, S->gphi, S->mu_o, S->tau, S->hasL, S->hasU, S->wl0, S->wu0,
@@ -783,12 +844,11 @@ int32_t step(cpl_solver* S) {
   LAUNCHED("k_unpack");
   CK(eval_full(S, S->Xn, S->f_n, S->grad_n, S->g_n, S->J_n));
   if (S->bfgs) {
-    CK(cpl_ipm_dense_a(B, m, nw, nf, S->nnz_rec, S->amap, S->row_slack, S->J_n, S->A_new, S->act, st));
     hipLaunchKernelGGL(k_prep, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->free32, S->row_slack, S->gl,
                        S->grad_n, S->g_n, S->st_w, S->gradw_new, nullptr);
     LAUNCHED("k_prep (new)");
-    hipLaunchKernelGGL(k_lbfgs, dim3((unsigned)B), dim3(256), 0, st, B, m, nf, nw, S->act, S->w, S->st_w, S->y, S->dy,
-                       S->st_alpha, S->gradw, S->A, S->gradw_new, S->A_new, S->lm_s, S->lm_y, S->lm_cnt, S->lm_skip,
+    hipLaunchKernelGGL(k_lbfgs, dim3((unsigned)B), dim3(256), 0, st, B, m, nf, nw, S->nnz_rec, S->amap, S->act, S->w, S->st_w, S->y, S->dy,
+                       S->st_alpha, S->gradw, S->J, S->gradw_new, S->J_n, S->lm_s, S->lm_y, S->lm_cnt, S->lm_skip,
                        S->failed, S->Hq);
     LAUNCHED("k_lbfgs");
   }
@@ -859,7 +919,7 @@ int32_t compact(cpl_solver* S, int64_t count, int64_t Bn) {
   CK(move(S->theta_max, 1)); CK(move(S->theta_min, 1)); CK(move(S->Xbase, n));
   CK(move(S->status, 1)); CK(move(S->iters, 1)); CK(move(S->acc, 1)); CK(move(S->fcount, 1));
   if (S->bfgs) {
-    CK(move(S->Hq, (int64_t)nf * nf));
+    CK(move(S->Hq, LMC(nf)));
     CK(move(S->lm_s, (int64_t)LM_HIST * nf));
     CK(move(S->lm_y, (int64_t)LM_HIST * nf));
   }
@@ -1054,7 +1114,7 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   const size_t nfd = S->fd ? Bz * 2 * nf : 0;
   {  // the widest per-instance row the compaction moves
     int64_t wmax = nnz_rec;
-    for (int64_t v : {(int64_t)n, (int64_t)nw, (int64_t)m, (int64_t)FMAX, S->bfgs ? (int64_t)nf * nf : 0}) wmax = std::max(wmax, v);
+    for (int64_t v : {(int64_t)n, (int64_t)nw, (int64_t)m, (int64_t)FMAX, S->bfgs ? LMC(nf) : 0}) wmax = std::max(wmax, v);
     S->scratch_words = wmax;
   }
   auto carve = [&](Arena& a) {
@@ -1071,14 +1131,14 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   S->zL = a.take<double>(Bz * nw); S->zU = a.take<double>(Bz * nw); S->mu = a.take<double>(Bz);
   S->filt_t = a.take<double>(Bz * FMAX); S->filt_p = a.take<double>(Bz * FMAX); S->dwl = a.take<double>(Bz);
   S->f = a.take<double>(Bz); S->grad = a.take<double>(Bz * n); S->g = a.take<double>(Bz * m);
-  S->J = a.take<double>(Bz * nnz_rec); S->d_inf = a.take<double>(Bz); S->Hq = a.take<double>(Bz * nf * nf);
+  S->J = a.take<double>(Bz * nnz_rec); S->d_inf = a.take<double>(Bz); S->Hq = a.take<double>(S->bfgs ? Bz * LMC(nf) : 0);
   S->lm_s = a.take<double>(S->bfgs ? Bz * LM_HIST * nf : 0); S->lm_y = a.take<double>(S->bfgs ? Bz * LM_HIST * nf : 0);
   S->theta_max = a.take<double>(Bz); S->theta_min = a.take<double>(Bz);
   S->status = a.take<int64_t>(Bz); S->iters = a.take<int64_t>(Bz); S->acc = a.take<int64_t>(Bz);
   S->fcount = a.take<int64_t>(Bz); S->fc = a.take<int64_t>(Bz);
   S->active = a.take<uint8_t>(Bz); S->lm_cnt = a.take<uint8_t>(Bz); S->lm_skip = a.take<uint8_t>(Bz); S->d_any = a.take<uint8_t>(2);
   // temporaries
-  S->A = a.take<double>(Bz * m * nw); S->A_new = a.take<double>(Bz * m * nw);
+  S->A = a.take<double>(Bz * m * nw);
   S->gradw = a.take<double>(Bz * nw); S->gradw_new = a.take<double>(Bz * nw); S->c = a.take<double>(Bz * m);
   S->err0 = a.take<double>(Bz); S->base = a.take<double>(Bz); S->mu_o = a.take<double>(Bz);
   S->ft = a.take<double>(Bz * FMAX); S->fp = a.take<double>(Bz * FMAX); S->tau = a.take<double>(Bz);
@@ -1191,8 +1251,8 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
   hipLaunchKernelGGL(k_y0, dim3(blocks_for(B)), dim3(256), 0, st, B, m, S->dy, S->info, S->y);
   LAUNCHED("k_y0");
   if (S->bfgs) {  // model initialised to init_val I (IPOPT's limited_memory_init_val = 1)
-    hipLaunchKernelGGL(k_eye, dim3(blocks_elems(B * nf * nf)), dim3(256), 0, st, B * nf * nf, nf, S->Hq);
-    LAUNCHED("k_eye");
+    hipLaunchKernelGGL(k_lm_init, dim3(blocks_elems(B)), dim3(256), 0, st, B, nf, S->Hq);
+    LAUNCHED("k_lm_init");
   }
   const int64_t per_step_full = (S->fd ? 1 : 0) + (S->opt.max_ls > 0 ? S->opt.max_ls : 1) + S->opt.max_soc + 2;
   int it = 0;
