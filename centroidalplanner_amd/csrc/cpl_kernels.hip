@@ -2007,15 +2007,12 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
     // the row-staged kernel has no fused epilogue: a separate pass over g
     return d_norms && finish ? cpl_residual_norms(d, batch, d_g, d_norms, stream) : CPL_OK;
   } else {
+    // records too large for 8 per 48 KiB tile (16 Superquadric / mixed contacts, ~10 KiB each) run as
+    // 4-instance tiles on 256 threads: 1 048 576 x 16 mixed 3.17 ms against 3.99 ms for the 2-instance
+    // tiles on 128 threads of round 1 and 4.18 ms for 8-instance tiles
+    // (profiles/r2_v7/sweep_tiles_mixed16_*.jsonl)
     st = plan_tile(K, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr);
-    int wg = g_wg;
-    if (!st && g_lds_budget == 0 && K.T < 8) {
-      // records too large for 8 per 48 KiB tile (e.g. 16 Superquadric / mixed contacts, ~10 KiB
-      // each): 2-instance tiles on 128-thread workgroups keep more tiles resident per CU, which the
-      // latency-bound power / division chains need (measured 1.7x over 8-instance tiles)
-      st = plan_tile(K, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr, 2);
-      wg = 128;
-    }
+    const int wg = g_wg;
     if (st) return st;
     K.ablate = g_ablate;
     const size_t lds = sizeof(double) * (size_t)(K.offI + 72);

@@ -227,8 +227,8 @@ int32_t cpl_time_eval_batch_ex(const cpl_problem_desc* d, int64_t batch, const d
  * pipelined kernel for none/Ground, the tile-stationary kernel for Superquadric/mixed),
  * 1 = row-staged lane-per-instance, 2 = pipelined (persistent, warp-specialized), 3 =
  * tile-stationary; tile_lds_kb = LDS budget of one workgroup (8..160 KiB; 0 = per-kernel
- * default: 48 KiB for both, and for the tile kernel 2-instance tiles on 128 threads when fewer
- * than 8 records fit); wg_threads = 128 or 256 for the tile kernel (default 256);
+ * default: 48 KiB for both: the largest power-of-two tile that fits, e.g. 8 instances of 8
+ * Superquadric contacts, 4 of 16); wg_threads = 128 or 256 for the tile kernel (default 256);
  * nt_stores = non-temporal output stores (default 1); ablate = measurement-only ablation
  * (0 = off, 1 = skip the compute phase, 2 = skip the output stores: results are then garbage).
  * Every variant computes bit-identical results.  Not thread-safe against concurrent launches. */
