@@ -492,6 +492,44 @@ __global__ __launch_bounds__(256) void k_lbfgs(int64_t B, int m, int nf, int nw,
 
 // the number of instances still active into one int (read by the host one iteration behind):
 // zeroed by k_count_zero at the iteration's start, one atomic per workgroup
+// up to COUNT1_MAX instances: one workgroup counts them and writes the count (no zeroing launch)
+constexpr int64_t COUNT1_MAX = 65536;
+__global__ __launch_bounds__(1024) void k_count1(int64_t B, const uint8_t* __restrict__ active,
+                                                 int32_t* __restrict__ count) {
+  __shared__ int s_w[16];
+  int c = 0;
+  for (int64_t b = threadIdx.x; b < B; b += 1024) c += active[b] ? 1 : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int q = 0; q < 16; ++q) t += s_w[q];
+    count[0] = t;
+  }
+}
+// the accepted point's f, grad, g and Jacobian records into the iterate's, active instances only:
+// one launch over the concatenated row [f | grad (n) | g (m) | J (nnz_rec)]
+__global__ __launch_bounds__(256) void k_accept_rows(int64_t B, int n, int m, int nnz, const uint8_t* __restrict__ act,
+                                                     const double* __restrict__ f_n, const double* __restrict__ grad_n,
+                                                     const double* __restrict__ g_n, const double* __restrict__ J_n,
+                                                     double* __restrict__ f, double* __restrict__ grad,
+                                                     double* __restrict__ g, double* __restrict__ J) {
+  const int64_t L = 1 + n + m + nnz;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B * L) return;
+  const int64_t b = e / L;
+  if (!act[b]) return;
+  int q = (int)(e - b * L);
+  if (q == 0) { f[b] = f_n[b]; return; }
+  q -= 1;
+  if (q < n) { grad[b * n + q] = grad_n[b * n + q]; return; }
+  q -= n;
+  if (q < m) { g[b * m + q] = g_n[b * m + q]; return; }
+  q -= m;
+  J[b * nnz + q] = J_n[b * nnz + q];
+}
 __global__ void k_count_zero(int32_t* __restrict__ count) {
   if (threadIdx.x == 0 && blockIdx.x == 0) count[0] = 0;
 }
@@ -724,8 +762,10 @@ int32_t step(cpl_solver* S) {
   hipStream_t st = S->stream;
   const cpl_solve_options& o = S->opt;
   // optimality error, convergence test, barrier update (filters reset where mu changed)
-  hipLaunchKernelGGL(k_count_zero, dim3(1), dim3(64), 0, st, S->d_count);
-  LAUNCHED("k_count_zero");
+  if (B > COUNT1_MAX) {  // (k_count accumulates with atomics; small batches use k_count1 at the end)
+    hipLaunchKernelGGL(k_count_zero, dim3(1), dim3(64), 0, st, S->d_count);
+    LAUNCHED("k_count_zero");
+  }
   CK(cpl_ipm_dense_a(B, m, nw, nf, S->nnz_rec, S->amap, S->row_slack, S->J, S->A, S->active, st));
   hipLaunchKernelGGL(k_prep, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->free32, S->row_slack, S->gl,
                      S->grad, S->g, S->w, S->gradw, S->c);
@@ -855,11 +895,13 @@ int32_t step(cpl_solver* S) {
   CK(cpl_ipm_accept(B, nw, m, FMAX, S->act, S->st_aug, S->failed, S->rest, S->st_alpha, S->a_z, S->theta_k, S->phi_k,
                     S->ft, S->fp, S->fc, S->st_w, S->dy, S->dzL, S->dzU, S->mu_o, S->hasL, S->hasU, S->wl0, S->wu0,
                     S->w, S->y, S->zL, S->zU, S->mu, S->iters, S->filt_t, S->filt_p, S->fcount, st));
-  CK(cpl_ipm_masked_rows(B, 1, S->act, S->f_n, S->f, st));
-  CK(cpl_ipm_masked_rows(B, n, S->act, S->grad_n, S->grad, st));
-  CK(cpl_ipm_masked_rows(B, m, S->act, S->g_n, S->g, st));
-  CK(cpl_ipm_masked_rows(B, S->nnz_rec, S->act, S->J_n, S->J, st));
-  hipLaunchKernelGGL(k_count, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->active, S->d_count);
+  hipLaunchKernelGGL(k_accept_rows, dim3(blocks_elems(B * (1 + n + m + S->nnz_rec))), dim3(256), 0, st, B, n, m,
+                     S->nnz_rec, S->act, S->f_n, S->grad_n, S->g_n, S->J_n, S->f, S->grad, S->g, S->J);
+  LAUNCHED("k_accept_rows");
+  if (B > COUNT1_MAX)
+    hipLaunchKernelGGL(k_count, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->active, S->d_count);
+  else
+    hipLaunchKernelGGL(k_count1, dim3(1), dim3(1024), 0, st, B, S->active, S->d_count);
   LAUNCHED("k_count");
   return CPL_OK;
 }
