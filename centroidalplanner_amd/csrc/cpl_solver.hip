@@ -221,13 +221,16 @@ __global__ __launch_bounds__(256) void k_ls_init(int64_t B, int m, int nw, const
                                                  uint8_t* __restrict__ searching, double* __restrict__ st_f,
                                                  double* __restrict__ st_g, double* __restrict__ st_w,
                                                  double* __restrict__ st_alpha, uint8_t* __restrict__ st_aug,
-                                                 double* __restrict__ alpha) {
+                                                 double* __restrict__ alpha, uint8_t* __restrict__ failed,
+                                                 uint8_t* __restrict__ rest) {
   const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
   if (b >= B) return;
   const int lane = threadIdx.x & 63;
   for (int r = lane; r < m; r += 64) st_g[b * m + r] = g[b * m + r];
   for (int k = lane; k < nw; k += 64) st_w[b * nw + k] = w[b * nw + k];
   if (lane == 0) {
+    failed[b] = 0;  // (set again by k_feas_prep / k_rest when the rest of the line search runs)
+    rest[b] = 0;
     searching[b] = act[b];
     st_f[b] = f[b];
     st_alpha[b] = 0.0;
@@ -276,6 +279,19 @@ __global__ void k_soc_after(int64_t B, uint8_t* __restrict__ soc, const uint8_t*
   if (b >= B) return;
   soc[b] = soc[b] && !ok[b] && th[b] <= 0.99 * th_old[b];  // kappa_soc = 0.99
   th_old[b] = th[b];
+}
+
+// any instance still searching after the first trial (small-batch split iterations): one workgroup
+__global__ __launch_bounds__(256) void k_any_searching(int64_t B, const uint8_t* __restrict__ searching,
+                                                       uint8_t* __restrict__ flag) {
+  __shared__ int s_any;
+  if (threadIdx.x == 0) s_any = 0;
+  __syncthreads();
+  int a = 0;
+  for (int64_t b = threadIdx.x; b < B; b += blockDim.x) a |= searching[b];
+  if (a) s_any = 1;
+  __syncthreads();
+  if (threadIdx.x == 0) flag[0] = (uint8_t)s_any;
 }
 
 __global__ void k_halve(int64_t B, const uint8_t* __restrict__ searching, double* __restrict__ alpha) {
@@ -755,74 +771,22 @@ int32_t eval_full(cpl_solver* S, const double* X, double* fo, double* grado, dou
                            S->stream);
 }
 
-// one lock-step iteration of every instance (graph-capturable: no host synchronisation)
+// One lock-step iteration of every instance (graph-capturable: no host synchronisation), in three
+// phases: A = the Newton step and the first line-search trial with its second-order correction
+// (+ the any-searching flag when `flag`), B = the remaining trials and the feasibility step, C = the
+// accepted point's evaluation and the state update.  Small batches run them as separate graphs and
+// skip B when no instance is still searching after A (the usual case: B is ~25 masked launches).
+int32_t step_phase(cpl_solver* S, int phase, bool flag);
 int32_t step(cpl_solver* S) {
+  CK(step_phase(S, 1, false));
+  CK(step_phase(S, 2, false));
+  return step_phase(S, 3, false);
+}
+int32_t step_phase(cpl_solver* S, int phase, bool flag) {
   const int64_t B = S->Bcur;
   const int n = S->n, m = S->m, nf = S->nf, nw = S->nw;
   hipStream_t st = S->stream;
   const cpl_solve_options& o = S->opt;
-  // optimality error, convergence test, barrier update (filters reset where mu changed)
-  if (B > COUNT1_MAX) {  // (k_count accumulates with atomics; small batches use k_count1 at the end)
-    hipLaunchKernelGGL(k_count_zero, dim3(1), dim3(64), 0, st, S->d_count);
-    LAUNCHED("k_count_zero");
-  }
-  CK(cpl_ipm_dense_a(B, m, nw, nf, S->nnz_rec, S->amap, S->row_slack, S->J, S->A, S->active, st));
-  hipLaunchKernelGGL(k_prep, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->free32, S->row_slack, S->gl,
-                     S->grad, S->g, S->w, S->gradw, S->c);
-  LAUNCHED("k_prep");
-  CK(cpl_ipm_optimality(B, nw, m, FMAX, S->nbounds, o.tol, o.acceptable_tol, o.acceptable_iter, S->A, S->gradw, S->c,
-                        S->w, S->y, S->zL, S->zU, S->hasL, S->hasU, S->wl0, S->wu0, S->mu, S->filt_t, S->filt_p,
-                        S->fcount, S->active, S->status, S->acc, S->d_inf, S->err0, S->base, S->mu_o, S->ft, S->fp,
-                        S->fc, st));
-  hipLaunchKernelGGL(k_unpack_tau, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, nw, S->freepos, S->Xbase,
-                     S->w, S->mu_o, S->active, S->X, S->tau, S->act);
-  LAUNCHED("k_unpack_tau");
-  // Hessian of the Lagrangian over x_free
-  const double* Hblk = nullptr;
-  int h_sym = 0;
-  if (S->bfgs) {
-    // the compact model is expanded inside the Newton setup (ipm_newton_setup_lm below)
-  } else if (S->analytic_H) {
-    CK(cpl_lagrangian_hessian(&S->desc, B, S->X, S->y, S->act, S->free32, nf, S->H, st));
-    Hblk = S->H;
-  } else {  // central differences of grad f + J^T y (the 2 nf points of every instance in one launch)
-    CK(cpl_ipm_fd_points(B, n, nf, o.fd_step, S->freepos, S->X, S->Xp, S->hfd, S->act, st));
-    int32_t rc = CPL_ERR_UNSUPPORTED;
-    if (S->fd_fused)
-      rc = cpl_eval_lagrangian_grad(&S->desc, B * 2 * nf, S->Xp, S->mass ? S->mass_fd : nullptr,
-                                    S->tag ? S->tag_fd : nullptr, S->col_ptr, S->csc_k, S->csc_row, S->y, 2 * nf,
-                                    S->act, S->gL, st);
-    if (rc == CPL_ERR_UNSUPPORTED) {  // Superquadric / mixed: eval + J^T y in two launches
-      S->fd_fused = false;
-      CK(cpl_eval_batch(&S->desc, B * 2 * nf, S->Xp, S->mass ? S->mass_fd : nullptr, S->tag ? S->tag_fd : nullptr,
-                        nullptr, S->jac_fd, nullptr, S->grad_fd, st));
-      CK(cpl_lagrangian_grad(B * 2 * nf, n, m, S->nnz, S->col_ptr, S->csc_k, S->csc_row, S->grad_fd, S->jac_fd, S->y,
-                             2 * nf, S->gL, st));
-    } else {
-      CK(rc);
-    }
-    CK(cpl_ipm_fd_hessian_raw(B, n, nf, S->free64, S->gL, S->hfd, S->H, S->act, st));
-    Hblk = S->H;
-    h_sym = 1;
-  }
-  // Newton system, step, multiplier steps, fraction-to-the-boundary steps
-  if (S->bfgs)
-    CK(ipm_newton_setup_lm(B, nw, m, nf, S->w, S->zL, S->zU, S->gradw, S->A, S->y, S->c, S->f, S->mu_o, S->hasL,
-                           S->hasU, S->wl0, S->wu0, S->Hq, LM_HIST, S->M, S->r1, S->r2, S->gphi, S->mr_diag,
-                           S->theta_k, S->phi_k, nullptr, st));
-  else
-    CK(cpl_ipm_newton_setup(B, nw, m, nf, S->w, S->zL, S->zU, S->gradw, S->A, S->y, S->c, S->f, S->mu_o, S->hasL,
-                            S->hasU, S->wl0, S->wu0, Hblk, h_sym, S->M, S->r1, S->r2, S->gphi, S->mr_diag, S->theta_k,
-                            S->phi_k, S->act, st));
-  CK(cpl_kkt_solve(0, B, nw, m, S->M, S->A, S->r1, S->r2, S->mu_o, S->dwl, S->act, S->dw, S->dy, S->delta_w,
-                   S->delta_c, S->info, S->ws, st));
-  CK(cpl_ipm_post_step(B, nw, S->w, S->dw, S->zL, S->zU, S->gphi, S->mu_o, S->tau, S->hasL, S->hasU, S->wl0, S->wu0,
-                       S->theta_k, S->theta_min, S->act, S->delta_w, S->dwl, S->dzL, S->dzU, S->a_max, S->a_z, S->gd,
-                       S->switch_ok, st));
-  // filter line search with a second-order correction on the first trial
-  hipLaunchKernelGGL(k_ls_init, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nw, S->act, S->f, S->g, S->w, S->a_max,
-                     S->searching, S->st_f, S->st_g, S->st_w, S->st_alpha, S->st_aug, S->alpha);
-  LAUNCHED("k_ls_init");
   auto judge = [&](const double* wt, const double* ft_, const double* gt_, const double* al, const uint8_t* extra,
                    double* th, uint8_t* ok, int mode) {
     return cpl_ipm_judge_take(B, nw, m, nf, FMAX, S->row_slack, S->gl, S->hasL, S->hasU, S->wl0, S->wu0, wt, ft_, gt_,
@@ -830,7 +794,9 @@ int32_t step(cpl_solver* S) {
                               extra, S->searching, S->st_f, S->st_g, S->st_w, S->st_alpha, S->st_aug, th, ok, mode,
                               st);
   };
-  for (int ls = 0; ls < (o.max_ls > 0 ? o.max_ls : 1); ++ls) {
+  const int nls = o.max_ls > 0 ? o.max_ls : 1;
+  // one trial of the filter line search (ls == 0: with the second-order correction), then the halving
+  auto trial = [&](int ls) -> int32_t {
     CK(cpl_ipm_trial_point(B, n, nf, nw, S->free64, S->fixed64, S->Xbase, S->w, S->dw, S->alpha, S->searching,
                            S->st_w, S->wt, S->Xt, st));
     CK(eval_fg(S, S->Xt, S->f_t, S->g_t));
@@ -861,23 +827,98 @@ int32_t step(cpl_solver* S) {
     }
     hipLaunchKernelGGL(k_halve, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->searching, S->alpha);
     LAUNCHED("k_halve");
+    return CPL_OK;
+  };
+  if (phase == 1) {
+    // optimality error, convergence test, barrier update (filters reset where mu changed)
+    if (B > COUNT1_MAX) {  // (k_count accumulates with atomics; small batches use k_count1 at the end)
+      hipLaunchKernelGGL(k_count_zero, dim3(1), dim3(64), 0, st, S->d_count);
+      LAUNCHED("k_count_zero");
+    }
+    CK(cpl_ipm_dense_a(B, m, nw, nf, S->nnz_rec, S->amap, S->row_slack, S->J, S->A, S->active, st));
+    hipLaunchKernelGGL(k_prep, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->free32, S->row_slack, S->gl,
+                       S->grad, S->g, S->w, S->gradw, S->c);
+    LAUNCHED("k_prep");
+    CK(cpl_ipm_optimality(B, nw, m, FMAX, S->nbounds, o.tol, o.acceptable_tol, o.acceptable_iter, S->A, S->gradw, S->c,
+                          S->w, S->y, S->zL, S->zU, S->hasL, S->hasU, S->wl0, S->wu0, S->mu, S->filt_t, S->filt_p,
+                          S->fcount, S->active, S->status, S->acc, S->d_inf, S->err0, S->base, S->mu_o, S->ft, S->fp,
+                          S->fc, st));
+    hipLaunchKernelGGL(k_unpack_tau, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, nw, S->freepos, S->Xbase,
+                       S->w, S->mu_o, S->active, S->X, S->tau, S->act);
+    LAUNCHED("k_unpack_tau");
+    // Hessian of the Lagrangian over x_free
+    const double* Hblk = nullptr;
+    int h_sym = 0;
+    if (S->bfgs) {
+      // the compact model is expanded inside the Newton setup (ipm_newton_setup_lm below)
+    } else if (S->analytic_H) {
+      CK(cpl_lagrangian_hessian(&S->desc, B, S->X, S->y, S->act, S->free32, nf, S->H, st));
+      Hblk = S->H;
+    } else {  // central differences of grad f + J^T y (the 2 nf points of every instance in one launch)
+      CK(cpl_ipm_fd_points(B, n, nf, o.fd_step, S->freepos, S->X, S->Xp, S->hfd, S->act, st));
+      int32_t rc = CPL_ERR_UNSUPPORTED;
+      if (S->fd_fused)
+        rc = cpl_eval_lagrangian_grad(&S->desc, B * 2 * nf, S->Xp, S->mass ? S->mass_fd : nullptr,
+                                      S->tag ? S->tag_fd : nullptr, S->col_ptr, S->csc_k, S->csc_row, S->y, 2 * nf,
+                                      S->act, S->gL, st);
+      if (rc == CPL_ERR_UNSUPPORTED) {  // Superquadric / mixed: eval + J^T y in two launches
+        S->fd_fused = false;
+        CK(cpl_eval_batch(&S->desc, B * 2 * nf, S->Xp, S->mass ? S->mass_fd : nullptr, S->tag ? S->tag_fd : nullptr,
+                          nullptr, S->jac_fd, nullptr, S->grad_fd, st));
+        CK(cpl_lagrangian_grad(B * 2 * nf, n, m, S->nnz, S->col_ptr, S->csc_k, S->csc_row, S->grad_fd, S->jac_fd, S->y,
+                               2 * nf, S->gL, st));
+      } else {
+        CK(rc);
+      }
+      CK(cpl_ipm_fd_hessian_raw(B, n, nf, S->free64, S->gL, S->hfd, S->H, S->act, st));
+      Hblk = S->H;
+      h_sym = 1;
+    }
+    // Newton system, step, multiplier steps, fraction-to-the-boundary steps
+    if (S->bfgs)
+      CK(ipm_newton_setup_lm(B, nw, m, nf, S->w, S->zL, S->zU, S->gradw, S->A, S->y, S->c, S->f, S->mu_o, S->hasL,
+                             S->hasU, S->wl0, S->wu0, S->Hq, LM_HIST, S->M, S->r1, S->r2, S->gphi, S->mr_diag,
+                             S->theta_k, S->phi_k, nullptr, st));
+    else
+      CK(cpl_ipm_newton_setup(B, nw, m, nf, S->w, S->zL, S->zU, S->gradw, S->A, S->y, S->c, S->f, S->mu_o, S->hasL,
+                              S->hasU, S->wl0, S->wu0, Hblk, h_sym, S->M, S->r1, S->r2, S->gphi, S->mr_diag, S->theta_k,
+                              S->phi_k, S->act, st));
+    CK(cpl_kkt_solve(0, B, nw, m, S->M, S->A, S->r1, S->r2, S->mu_o, S->dwl, S->act, S->dw, S->dy, S->delta_w,
+                     S->delta_c, S->info, S->ws, st));
+    CK(cpl_ipm_post_step(B, nw, S->w, S->dw, S->zL, S->zU, S->gphi, S->mu_o, S->tau, S->hasL, S->hasU, S->wl0, S->wu0,
+                         S->theta_k, S->theta_min, S->act, S->delta_w, S->dwl, S->dzL, S->dzU, S->a_max, S->a_z, S->gd,
+                         S->switch_ok, st));
+    // filter line search with a second-order correction on the first trial
+    hipLaunchKernelGGL(k_ls_init, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nw, S->act, S->f, S->g, S->w, S->a_max,
+                       S->searching, S->st_f, S->st_g, S->st_w, S->st_alpha, S->st_aug, S->alpha, S->failed, S->rest);
+    LAUNCHED("k_ls_init");
+    CK(trial(0));
+    if (flag) {
+      hipLaunchKernelGGL(k_any_searching, dim3(1), dim3(256), 0, st, B, S->searching, S->d_any);
+      LAUNCHED("k_any_searching");
+    }
+    return CPL_OK;
   }
-  // no acceptable trial: the feasibility step (min 1/2 dw^T (Sigma + sqrt(mu) D_R^2) dw s.t. A dw = -c)
-  // stands in for IPOPT's restoration phase, taken when it cuts the violation by 10 %; else the last trial
-  hipLaunchKernelGGL(k_feas_prep, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nw, S->searching, S->mr_diag, S->c,
-                     S->failed, S->Mr, S->negc);
-  LAUNCHED("k_feas_prep");
-  CK(cpl_kkt_solve(0, B, nw, m, S->Mr, S->A, S->zeros_w, S->negc, S->mu_o, S->zeros_B, S->failed, S->dwr, S->dyr,
-                   S->dwr_d, S->dcr, S->infor, S->ws, st));
-  CK(cpl_ipm_max_step(B, nw, S->w, S->dwr, nullptr, nullptr, S->hasL, S->hasU, S->wl0, S->wu0, S->tau, S->ar, st));
-  CK(cpl_ipm_trial_point(B, n, nf, nw, S->free64, S->fixed64, S->Xbase, S->w, S->dwr, S->ar, S->failed, S->st_w, S->wr,
-                         S->Xr, st));
-  CK(eval_fg(S, S->Xr, S->f_r, S->g_r));
-  CK(judge(S->wr, S->f_r, S->g_r, S->zeros_B, S->failed, S->th_r, S->ok_r, 1));
-  hipLaunchKernelGGL(k_rest, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->failed, S->ok_r, S->alpha, S->rest,
-                     S->alpha2);
-  LAUNCHED("k_rest");
-  CK(judge(S->wt, S->f_t, S->g_t, S->alpha2, nullptr, S->th, S->ok, 2));
+  if (phase == 2) {
+    for (int ls = 1; ls < nls; ++ls) CK(trial(ls));
+    // no acceptable trial: the feasibility step (min 1/2 dw^T (Sigma + sqrt(mu) D_R^2) dw s.t. A dw = -c)
+    // stands in for IPOPT's restoration phase, taken when it cuts the violation by 10 %; else the last trial
+    hipLaunchKernelGGL(k_feas_prep, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nw, S->searching, S->mr_diag, S->c,
+                       S->failed, S->Mr, S->negc);
+    LAUNCHED("k_feas_prep");
+    CK(cpl_kkt_solve(0, B, nw, m, S->Mr, S->A, S->zeros_w, S->negc, S->mu_o, S->zeros_B, S->failed, S->dwr, S->dyr,
+                     S->dwr_d, S->dcr, S->infor, S->ws, st));
+    CK(cpl_ipm_max_step(B, nw, S->w, S->dwr, nullptr, nullptr, S->hasL, S->hasU, S->wl0, S->wu0, S->tau, S->ar, st));
+    CK(cpl_ipm_trial_point(B, n, nf, nw, S->free64, S->fixed64, S->Xbase, S->w, S->dwr, S->ar, S->failed, S->st_w, S->wr,
+                           S->Xr, st));
+    CK(eval_fg(S, S->Xr, S->f_r, S->g_r));
+    CK(judge(S->wr, S->f_r, S->g_r, S->zeros_B, S->failed, S->th_r, S->ok_r, 1));
+    hipLaunchKernelGGL(k_rest, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->failed, S->ok_r, S->alpha, S->rest,
+                       S->alpha2);
+    LAUNCHED("k_rest");
+    CK(judge(S->wt, S->f_t, S->g_t, S->alpha2, nullptr, S->th, S->ok, 2));
+    return CPL_OK;
+  }
   // the accepted points with their derivatives: one full evaluation
   hipLaunchKernelGGL(k_unpack, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, nw, S->freepos, S->Xbase,
                      S->st_w, nullptr, nullptr, S->Xn);
@@ -907,12 +948,13 @@ int32_t step(cpl_solver* S) {
 }
 
 // the graph of one iteration at the current batch size (captured once per size, then replayed)
-int32_t graph_for(cpl_solver* S) {
-  const int64_t key = S->Bcur * 4 + (S->mass ? 2 : 0) + (S->tag ? 1 : 0);
+// phase 0: the whole iteration (S->graph / S->gexec); 1..3: the split iteration's phases (*ex)
+int32_t graph_for(cpl_solver* S, int phase = 0, hipGraphExec_t* ex_out = nullptr) {
+  const int64_t key = (S->Bcur * 4 + (S->mass ? 2 : 0) + (S->tag ? 1 : 0)) * 4 + phase;
   auto it = S->graphs.find(key);
   if (it == S->graphs.end()) {
     HK(hipStreamBeginCapture(S->stream, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
-    const int32_t rc = step(S);
+    const int32_t rc = phase == 0 ? step(S) : step_phase(S, phase, phase == 1);
     hipGraph_t gr = nullptr;
     const hipError_t e = hipStreamEndCapture(S->stream, &gr);
     if (rc != CPL_OK) {
@@ -928,8 +970,12 @@ int32_t graph_for(cpl_solver* S) {
     }
     it = S->graphs.emplace(key, std::make_pair(gr, ex)).first;
   }
-  S->graph = it->second.first;
-  S->gexec = it->second.second;
+  if (phase == 0) {
+    S->graph = it->second.first;
+    S->gexec = it->second.second;
+  } else {
+    *ex_out = it->second.second;
+  }
   return CPL_OK;
 }
 
@@ -1311,6 +1357,40 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
     HK(hipStreamSynchronize(st), "hipStreamSynchronize");
     int last = S->h_count[0] ? max_iter : it;
     int start = it;
+    // batches of at most SPLIT_MAX rows: the iteration as three graphs, the line search's later
+    // trials and feasibility step (phase B) launched only when an instance is still searching after
+    // the first trial (read back before the launch: one stream synchronisation per iteration, against
+    // ~25 masked launches skipped in most iterations)
+    constexpr int64_t SPLIT_MAX = 256;
+    auto split_loop = [&]() -> int32_t {
+      const int64_t evA = (S->fd ? 1 : 0) + 1 + S->opt.max_soc;
+      const int64_t evB = (S->opt.max_ls > 0 ? S->opt.max_ls : 1) - 1 + 1;
+      hipGraphExec_t ga = nullptr, gb = nullptr, gc = nullptr;
+      CK(graph_for(S, 1, &ga));
+      CK(graph_for(S, 2, &gb));
+      CK(graph_for(S, 3, &gc));
+      bool have_count = false;  // h_count[0] holds the count after the previous iteration
+      while (it < last) {
+        HK(hipGraphLaunch(ga, st), "hipGraphLaunch");
+        HK(hipMemcpyAsync(S->h_flag, S->d_any, 1, hipMemcpyDeviceToHost, st), "hipMemcpyAsync flag");
+        HK(hipStreamSynchronize(st), "hipStreamSynchronize");
+        ++it;
+        evals += evA + 1;
+        if (have_count && S->h_count[0] == 0) break;  // converged in the previous iteration (this one was idle)
+        if (S->h_flag[0]) {
+          HK(hipGraphLaunch(gb, st), "hipGraphLaunch");
+          evals += evB;
+        }
+        HK(hipGraphLaunch(gc, st), "hipGraphLaunch");
+        HK(hipMemcpyAsync(S->h_count, S->d_count, 4, hipMemcpyDeviceToHost, st), "hipMemcpyAsync count");
+        have_count = true;
+      }
+      return CPL_OK;
+    };
+    if (S->opt.use_graph && S->Bcur <= SPLIT_MAX) {
+      CK(split_loop());
+      last = it;
+    }
     while (it < last) {
       if (S->opt.use_graph) HK(hipGraphLaunch(S->gexec, st), "hipGraphLaunch");
       else CK(step(S));
@@ -1332,6 +1412,10 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
           while (Bn / 2 >= now && Bn / 2 >= min_rows) Bn = (Bn + 1) / 2;
           if (Bn < S->Bcur) {
             CK(compact(S, now, Bn));
+            if (Bn <= SPLIT_MAX) {  // the rest of the solve as split iterations
+              CK(split_loop());
+              break;
+            }
             CK(graph_for(S));
             start = it;  // the flag pipeline restarts at the new size
           }
