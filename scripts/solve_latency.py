@@ -19,14 +19,19 @@ from centroidalplanner_amd.workload import solve_inputs, solve_problem  # noqa: 
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=20)
+ap.add_argument("--only", default="", help="run one case, e.g. limited-memory:1 (for a kernel trace)")
 args = ap.parse_args()
 
 prob = solve_problem().GetCplProblem()
 dev = torch.device("cuda:0")
 X0, mass = solve_inputs(prob, 64, seed=0xC910 + 5)
 out = {}
-for hessian in ("limited-memory", "exact"):
-    for B in (1, 64):
+cases = [(h, B) for h in ("limited-memory", "exact") for B in (1, 64)]
+if args.only:
+    h, b = args.only.split(":")
+    cases = [(h, int(b))]
+for hessian, B in cases:
+    if True:
         Xt, mt = torch.tensor(X0[:B], device=dev), torch.tensor(mass[:B], device=dev)
         r = batch_ipm_solve(prob, Xt, mt, max_iter=1000, hessian=hessian)  # warm: engine + graphs
         torch.cuda.synchronize()
