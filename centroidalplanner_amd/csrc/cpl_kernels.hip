@@ -1737,14 +1737,35 @@ static void fill_params(const cpl_problem_desc* d, KParams& K, const double* d_x
   for (int j = 0; j < 6; ++j) K.wrench[j] = d->wrench[j];
   K.mu = d->mu;
   K.ground_z = d->ground_z;
+  // the instance-independent Superquadric factors (15 glibc pow calls): only for the environments
+  // that read them, and cached per thread for the last (R, P) seen (the launch path is on the
+  // single-instance callback's critical path)
+  const bool sq = d->env_kind == CPL_ENV_SUPERQUADRIC || d->env_kind == CPL_ENV_MIXED;
+  struct SqFactors {
+    double R[3], P[3], EJ[3], Ka[3], Kb[3], Rm2[3], Rp2[3];
+    bool valid = false;
+  };
+  thread_local SqFactors cache;
+  if (sq && !(cache.valid && std::memcmp(cache.R, d->sq_R, sizeof(cache.R)) == 0 &&
+              std::memcmp(cache.P, d->sq_P, sizeof(cache.P)) == 0)) {
+    for (int a = 0; a < 3; ++a) {
+      const double R = d->sq_R[a], P = d->sq_P[a];
+      cache.R[a] = R; cache.P[a] = P;
+      cache.EJ[a] = P / std::pow(R, P);
+      cache.Ka[a] = P * std::pow(R, -P);
+      cache.Kb[a] = (P * P) * std::pow(R, P * -2.0);
+      cache.Rm2[a] = std::pow(R, -(P * 2.0));
+      cache.Rp2[a] = std::pow(R, P * 2.0);
+    }
+    cache.valid = true;
+  }
   for (int a = 0; a < 3; ++a) {
     const double C = d->sq_C[a], R = d->sq_R[a], P = d->sq_P[a];
     K.C[a] = C; K.R[a] = R; K.P[a] = P;
-    K.EJ[a] = P / std::pow(R, P);
-    K.Ka[a] = P * std::pow(R, -P);
-    K.Kb[a] = (P * P) * std::pow(R, P * -2.0);
-    K.Rm2[a] = std::pow(R, -(P * 2.0));
-    K.Rp2[a] = std::pow(R, P * 2.0);
+    if (sq) {
+      K.EJ[a] = cache.EJ[a]; K.Ka[a] = cache.Ka[a]; K.Kb[a] = cache.Kb[a];
+      K.Rm2[a] = cache.Rm2[a]; K.Rp2[a] = cache.Rp2[a];
+    }
     K.Psq[a] = P * P;
     K.Pm1[a] = P - 1.0;
     K.P2[a] = P * 2.0;
