@@ -745,6 +745,7 @@ def main():
         print(json.dumps(res), flush=True)
 
     if world > 1:
+        dist.barrier()  # every rank leaves together (rank 0 ran the checker leg after the timing)
         dist.destroy_process_group()
 
 
