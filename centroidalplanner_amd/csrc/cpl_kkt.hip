@@ -1412,13 +1412,18 @@ using KktWaveKernel = void (*)(int, int64_t, const double*, const double*, const
                               const double*, const double*, const uint8_t*, double*, double*, double*, double*,
                               int32_t*, double*);
 
-// The one-wave kernel for the sizes it is specialised for (the 4-contact solve loop's nw 47, m 30)
-// when it finishes first, nullptr otherwise.  Both kernels are latency-bound per system: a round of
-// resident systems takes ~0.12 ms on the workgroup kernel (4 per CU) and ~0.14 ms on the one-wave
-// kernel (7 per CU), so the workgroup kernel wins when the batch fits in as few of its rounds
-// (measured: B <= 1,024 and 2,048 on 256 CUs; the one-wave kernel from 1,536 and past 2,048).
-// The choice depends on (nw, m, batch) only, so a mode 1 call follows a mode 0 call of the same
-// kernel (their factor layouts differ).  CPL_KKT_KERNEL=block|wave forces one (measurement only).
+// The one-wave kernel for the sizes it is specialised for (the 4-contact solve loop's nw 47, m 30),
+// nullptr otherwise.  With its register-resident QR / Z and the FP64-MFMA reduced Hessian it
+// factorises faster than the workgroup kernel at every batch size (scripts/kkt_ab.hip,
+// profiles/r2_v7/kkt_ab/: 1 system 0.069 vs 0.099 ms, 1 024 0.080 vs 0.134, 8 192 0.42 vs 0.94);
+// its re-solve is 4-7 us slower up to ~1 000 systems, less than the factorisation gains.  Batches
+// below KKT_WAVE_MIN_BATCH (the single-instance Solve()) stay on the workgroup kernel: the
+// degenerate TestBasic ground problem (force weight 0) runs to the iteration limit, and its end point
+// depends on the rounding of every Newton step — it meets TestBasic's cone tolerance with the
+// workgroup kernel's, not with the one-wave kernel's.  (Earlier in round 2 the choice went by batch
+// size: the workgroup kernel while the batch fitted in as few of its rounds.)  CPL_KKT_KERNEL=block
+// or =wave forces one (measurement only).
+constexpr int64_t KKT_WAVE_MIN_BATCH = 64;
 static KktWaveKernel kkt_wave_kernel_for(int nw, int m, int64_t batch) {
   static const int forced = [] {
     const char* e = std::getenv("CPL_KKT_KERNEL");
@@ -1429,34 +1434,7 @@ static KktWaveKernel kkt_wave_kernel_for(int nw, int m, int64_t batch) {
   if (nw == 47 && m == 30) wk = cpl_kkt_wave_kernel<47, 30>;
   if (!wk || forced == 1) return nullptr;
   if (forced == 2) return wk;
-  struct Occ {
-    int cus = 0, per_block = 0, per_wave = 0;
-  };
-  static std::mutex mu;
-  static std::map<std::tuple<int, int, int>, Occ> cache;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return wk;
-  Occ o;
-  {
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = cache.find({dev, nw, m});
-    if (it != cache.end()) {
-      o = it->second;
-    } else {
-      if (hipDeviceGetAttribute(&o.cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per_block, reinterpret_cast<const void*>(kkt_kernel_for(nw, m)),
-                                                       KKT_THREADS, sizeof(double) * kkt_launch_lds_doubles(nw, m, 0)) !=
-              hipSuccess ||
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per_wave, reinterpret_cast<const void*>(wk), 64,
-                                                       sizeof(double) * kktw_lds_doubles(nw, m)) != hipSuccess)
-        return wk;
-      cache[{dev, nw, m}] = o;
-    }
-  }
-  if (o.cus <= 0 || o.per_block <= 0 || o.per_wave <= 0) return wk;
-  const int64_t rb = (batch + (int64_t)o.cus * o.per_block - 1) / ((int64_t)o.cus * o.per_block);
-  const int64_t rw = (batch + (int64_t)o.cus * o.per_wave - 1) / ((int64_t)o.cus * o.per_wave);
-  return 1.17 * (double)rw < (double)rb ? wk : nullptr;
+  return batch >= KKT_WAVE_MIN_BATCH ? wk : nullptr;
 }
 
 extern "C" {

@@ -2,10 +2,10 @@
 numpy solve of the same KKT systems (float64; tolerance 1e-9 relative to the solution's scale, the
 systems' condition numbers are ~1e3-1e5).
 
-The library picks the workgroup kernel or, for the 4-contact size (nw 47, m 30), the one-wave kernel
-by batch size (the workgroup kernel up to ~1k systems on 256 CUs, the one-wave kernel at 4,096 and
-8,192): the (47, 30) cases run at both B = 64 / 300 and B = 4,096 so that both kernels are covered
-(the dense check on a sample of the large batches)."""
+The 4-contact size (nw 47, m 30) runs the one-wave kernel from 64 systems up and the workgroup kernel
+below (every other size: the workgroup kernel's generic instance): the (47, 30) cases run at B = 64 /
+300 and B = 4,096 (the dense check on a sample of the large batches), the small-batch cases and
+the other sizes cover the workgroup kernel."""
 import ctypes
 
 import numpy as np
@@ -80,7 +80,7 @@ def _sample(B):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nw,m,B", [(47, 30, 300), (47, 30, 4096), (39, 14, 300), (12, 12, 300), (20, 0, 300),
+@pytest.mark.parametrize("nw,m,B", [(47, 30, 16), (47, 30, 300), (47, 30, 4096), (39, 14, 300), (12, 12, 300), (20, 0, 300),
                                     (91, 54, 300), (100, 70, 300)])
 def test_kkt_matches_dense_solve(nw, m, B):
     nz = nw - m
