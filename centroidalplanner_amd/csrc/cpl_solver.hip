@@ -222,13 +222,14 @@ __global__ __launch_bounds__(256) void k_ls_init(int64_t B, int m, int nw, const
                                                  double* __restrict__ st_g, double* __restrict__ st_w,
                                                  double* __restrict__ st_alpha, uint8_t* __restrict__ st_aug,
                                                  double* __restrict__ alpha, uint8_t* __restrict__ failed,
-                                                 uint8_t* __restrict__ rest) {
+                                                 uint8_t* __restrict__ rest, uint8_t* __restrict__ any) {
   const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
   if (b >= B) return;
   const int lane = threadIdx.x & 63;
   for (int r = lane; r < m; r += 64) st_g[b * m + r] = g[b * m + r];
   for (int k = lane; k < nw; k += 64) st_w[b * nw + k] = w[b * nw + k];
   if (lane == 0) {
+    if (b == 0 && any) any[0] = 0;  // the any-searching flag of the split iteration
     failed[b] = 0;  // (set again by k_feas_prep / k_rest when the rest of the line search runs)
     rest[b] = 0;
     searching[b] = act[b];
@@ -239,22 +240,6 @@ __global__ __launch_bounds__(256) void k_ls_init(int64_t B, int m, int nw, const
   }
 }
 
-// second-order correction bookkeeping (batch_ipm step(): soc, c_soc, a_soc, th_old)
-__global__ __launch_bounds__(256) void k_soc_begin(int64_t B, int m, const uint8_t* __restrict__ searching,
-                                                   const double* __restrict__ th, const double* __restrict__ theta_k,
-                                                   const double* __restrict__ c, const double* __restrict__ alpha,
-                                                   uint8_t* __restrict__ soc, double* __restrict__ c_soc,
-                                                   double* __restrict__ a_soc, double* __restrict__ th_old) {
-  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
-  if (b >= B) return;
-  const int lane = threadIdx.x & 63;
-  for (int r = lane; r < m; r += 64) c_soc[b * m + r] = c[b * m + r];
-  if (lane == 0) {
-    soc[b] = searching[b] && th[b] >= theta_k[b];
-    a_soc[b] = alpha[b];
-    th_old[b] = theta_k[b];
-  }
-}
 
 // c_soc = a_soc c_soc + c(trial point); the correction's right-hand side r2 = -c_soc
 __global__ __launch_bounds__(256) void k_soc_rhs(int64_t B, int m, int nf, int nw, const int32_t* __restrict__ row_slack,
@@ -270,6 +255,49 @@ __global__ __launch_bounds__(256) void k_soc_rhs(int64_t B, int m, int nf, int n
     const double v = a * c_soc[b * m + r] + ct;
     c_soc[b * m + r] = v;
     r2[b * m + r] = -v;
+  }
+}
+
+// second-order correction bookkeeping (batch_ipm step(): soc, c_soc, a_soc, th_old) and the first
+// correction's right-hand side in one launch: c_soc = a_soc c + c(trial point), r2 = -c_soc
+__global__ __launch_bounds__(256) void k_soc_begin_rhs(int64_t B, int m, int nf, int nw, const uint8_t* __restrict__ searching,
+                                                       const double* __restrict__ th, const double* __restrict__ theta_k,
+                                                       const double* __restrict__ c, const double* __restrict__ alpha,
+                                                       const int32_t* __restrict__ row_slack, const double* __restrict__ gl,
+                                                       const double* __restrict__ g_t, const double* __restrict__ w_t,
+                                                       uint8_t* __restrict__ soc, double* __restrict__ c_soc,
+                                                       double* __restrict__ a_soc, double* __restrict__ th_old,
+                                                       double* __restrict__ r2) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  const double a = alpha[b];
+  for (int r = lane; r < m; r += 64) {
+    const double ct = cons_row(g_t + b * m, w_t + b * nw, nf, r, row_slack, gl);
+    const double v = a * c[b * m + r] + ct;
+    c_soc[b * m + r] = v;
+    r2[b * m + r] = -v;
+  }
+  if (lane == 0) {
+    soc[b] = searching[b] && th[b] >= theta_k[b];
+    a_soc[b] = a;
+    th_old[b] = theta_k[b];
+  }
+}
+
+// the last k_soc_after and the trial's halving in one launch; with `any`, instances still searching
+// also raise the any-searching flag (zeroed by k_ls_init)
+__global__ void k_soc_after_halve(int64_t B, uint8_t* __restrict__ soc, const uint8_t* __restrict__ ok,
+                                  const double* __restrict__ th, double* __restrict__ th_old,
+                                  const uint8_t* __restrict__ searching, double* __restrict__ alpha,
+                                  uint8_t* __restrict__ any) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  soc[b] = soc[b] && !ok[b] && th[b] <= 0.99 * th_old[b];  // kappa_soc = 0.99
+  th_old[b] = th[b];
+  if (searching[b]) {
+    alpha[b] = 0.5 * alpha[b];
+    if (any) any[0] = 1;
   }
 }
 
@@ -796,20 +824,24 @@ int32_t step_phase(cpl_solver* S, int phase, bool flag) {
   };
   const int nls = o.max_ls > 0 ? o.max_ls : 1;
   // one trial of the filter line search (ls == 0: with the second-order correction), then the halving
-  auto trial = [&](int ls) -> int32_t {
+  auto trial = [&](int ls, bool any) -> int32_t {
     CK(cpl_ipm_trial_point(B, n, nf, nw, S->free64, S->fixed64, S->Xbase, S->w, S->dw, S->alpha, S->searching,
                            S->st_w, S->wt, S->Xt, st));
     CK(eval_fg(S, S->Xt, S->f_t, S->g_t));
     CK(judge(S->wt, S->f_t, S->g_t, S->alpha, nullptr, S->th, S->ok, 0));
     if (ls == 0 && o.max_soc > 0) {
-      hipLaunchKernelGGL(k_soc_begin, dim3(blocks_for(B)), dim3(256), 0, st, B, m, S->searching, S->th, S->theta_k,
-                         S->c, S->alpha, S->soc, S->c_soc, S->a_soc, S->th_old);
-      LAUNCHED("k_soc_begin");
       const double *cg = S->g_t, *cw = S->wt;
       for (int q = 0; q < o.max_soc; ++q) {
-        hipLaunchKernelGGL(k_soc_rhs, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nf, nw, S->row_slack, S->gl, cg, cw,
-                           S->a_soc, S->c_soc, S->r2s);
-        LAUNCHED("k_soc_rhs");
+        if (q == 0) {
+          hipLaunchKernelGGL(k_soc_begin_rhs, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nf, nw, S->searching, S->th,
+                             S->theta_k, S->c, S->alpha, S->row_slack, S->gl, cg, cw, S->soc, S->c_soc, S->a_soc,
+                             S->th_old, S->r2s);
+          LAUNCHED("k_soc_begin_rhs");
+        } else {
+          hipLaunchKernelGGL(k_soc_rhs, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nf, nw, S->row_slack, S->gl, cg,
+                             cw, S->a_soc, S->c_soc, S->r2s);
+          LAUNCHED("k_soc_rhs");
+        }
         CK(cpl_kkt_solve(1, B, nw, m, S->M, S->A, S->r1, S->r2s, nullptr, nullptr, S->soc, S->dws, S->dys, nullptr,
                          nullptr, nullptr, S->ws, st));
         CK(cpl_ipm_max_step(B, nw, S->w, S->dws, nullptr, nullptr, S->hasL, S->hasU, S->wl0, S->wu0, S->tau, S->a_soc,
@@ -818,6 +850,12 @@ int32_t step_phase(cpl_solver* S, int phase, bool flag) {
                                S->ws_, S->Xs, st));
         CK(eval_fg(S, S->Xs, S->f_s, S->g_s));
         CK(judge(S->ws_, S->f_s, S->g_s, S->alpha, S->soc, S->th_s, S->ok_s, 0));
+        if (q + 1 == o.max_soc) {  // the last correction: its bookkeeping with the halving
+          hipLaunchKernelGGL(k_soc_after_halve, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->soc, S->ok_s, S->th_s,
+                             S->th_old, S->searching, S->alpha, any ? S->d_any : nullptr);
+          LAUNCHED("k_soc_after_halve");
+          return CPL_OK;
+        }
         hipLaunchKernelGGL(k_soc_after, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->soc, S->ok_s, S->th_s,
                            S->th_old);
         LAUNCHED("k_soc_after");
@@ -827,6 +865,10 @@ int32_t step_phase(cpl_solver* S, int phase, bool flag) {
     }
     hipLaunchKernelGGL(k_halve, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->searching, S->alpha);
     LAUNCHED("k_halve");
+    if (any) {
+      hipLaunchKernelGGL(k_any_searching, dim3(1), dim3(256), 0, st, B, S->searching, S->d_any);
+      LAUNCHED("k_any_searching");
+    }
     return CPL_OK;
   };
   if (phase == 1) {
@@ -890,17 +932,14 @@ int32_t step_phase(cpl_solver* S, int phase, bool flag) {
                          S->switch_ok, st));
     // filter line search with a second-order correction on the first trial
     hipLaunchKernelGGL(k_ls_init, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nw, S->act, S->f, S->g, S->w, S->a_max,
-                       S->searching, S->st_f, S->st_g, S->st_w, S->st_alpha, S->st_aug, S->alpha, S->failed, S->rest);
+                       S->searching, S->st_f, S->st_g, S->st_w, S->st_alpha, S->st_aug, S->alpha, S->failed, S->rest,
+                       flag ? S->d_any : nullptr);
     LAUNCHED("k_ls_init");
-    CK(trial(0));
-    if (flag) {
-      hipLaunchKernelGGL(k_any_searching, dim3(1), dim3(256), 0, st, B, S->searching, S->d_any);
-      LAUNCHED("k_any_searching");
-    }
+    CK(trial(0, flag));  // (with `flag`: the any-searching flag for the split iteration)
     return CPL_OK;
   }
   if (phase == 2) {
-    for (int ls = 1; ls < nls; ++ls) CK(trial(ls));
+    for (int ls = 1; ls < nls; ++ls) CK(trial(ls, false));
     // no acceptable trial: the feasibility step (min 1/2 dw^T (Sigma + sqrt(mu) D_R^2) dw s.t. A dw = -c)
     // stands in for IPOPT's restoration phase, taken when it cuts the violation by 10 %; else the last trial
     hipLaunchKernelGGL(k_feas_prep, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nw, S->searching, S->mr_diag, S->c,
