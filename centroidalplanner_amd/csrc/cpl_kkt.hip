@@ -709,14 +709,16 @@ __global__ __launch_bounds__(256) void cpl_lagrangian_grad_kernel(int64_t total,
 // runs on ONE wave — no workgroup barriers (the workgroup kernel parks ~75 % of its wave cycles on
 // them) — and each phase issues its memory operations in bulk before it computes, so that a step
 // pays one LDS / L2 round trip instead of one per pass:
-//   * nw-vectors live one element per lane; a lane keeps its row of every Householder vector in
-//     registers (vr[j] = v_j[lane]);
-//   * QR of A^T: reflector j by a wave sum, the trailing columns 8 lanes per column;
-//   * Z = H_0 ... H_{m-1} [0; I] (only Z, not the whole Q), 4 lanes per column;
+//   * nw-vectors live one element per lane;
+//   * QR of A^T register-resident (lane (g, part) holds rows part + 8t of columns g + 8q): each
+//     reflector from an 8-lane group sum, published through a 47-double LDS buffer, the trailing
+//     columns updated in registers (8 lanes per column);
+//   * Z = H_0 ... H_{m-1} [0; I] (only Z, not the whole Q), register-resident, 4 lanes per column;
 //   * Y p_y = Q [p_y; 0] and Y^T u = (Q^T u)[0, m) as reflector chains, two reflectors per wave
 //     sum (c_p = v_{2p}^T v_{2p+1} precomputed);
-//   * M Z a lane per row with M's column (symmetric M: coalesced) loaded 16 at a time; Z^T (M Z)
-//     a lane per upper-triangle entry through the L2-resident workspace.
+//   * W = M Z and Z^T W on the FP64 matrix cores (v_mfma_f64_16x16x4f64), W's accumulators reused
+//     as Z^T W's B fragments; M's fragments stay in registers for every later M product;
+//   * the inertia-correcting Cholesky and the triangular sweeps with the rows in registers.
 // LDS image QR | Z | L | beta | cp | 3 nw + m vector slots: 21.7 KiB at nw = 47, m = 30, i.e.
 // seven systems per CU.  Factor workspace (mode 1): QR | Z | L | beta | cp | dW, dC.
 // ==========================================================================================
