@@ -377,3 +377,28 @@ def test_active_set_compaction_is_exact(hessian):
     assert a.compactions >= 1 and b.compactions == 0
     for k in ("x", "y", "status", "iterations", "objective", "primal_inf", "dual_inf"):
         assert torch.equal(getattr(a, k), getattr(b, k)), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_ls,max_soc,hessian", [(4, 1, "limited-memory"), (4, 0, "exact"), (1, 1, "exact"),
+                                                    (2, 2, "limited-memory")])
+def test_split_small_batch_iterations_are_exact(max_ls, max_soc, hessian):
+    """Small batches run each iteration as three graphs and skip the later line-search trials and the
+    feasibility step when nothing is still searching after the first trial (its second-order
+    correction fused with the halving and the any-searching flag): bitwise the eager one-step
+    iteration, for every line-search / SOC configuration."""
+    from centroidalplanner_amd.batch_ipm import KernelEvaluator
+
+    cpl = solve_problem()
+    prob = cpl.GetCplProblem()
+    B = 32
+    X0, mass = solve_inputs(prob, B, seed=21)
+    dev = torch.device("cuda:0")
+    X0t, mt = torch.as_tensor(X0, device=dev), torch.as_tensor(mass, device=dev)
+    kw = dict(max_iter=1000, hessian=hessian, max_ls=max_ls, max_soc=max_soc)
+    a = batch_ipm_solve(prob, X0t, mt, evaluator=KernelEvaluator(prob), graph=True, **kw)
+    b = batch_ipm_solve(prob, X0t, mt, evaluator=KernelEvaluator(prob), graph=False, **kw)
+    assert a.graph and not b.graph
+    for k in ("x", "y", "status", "iterations", "objective"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    assert bool((a.status <= STATUS_ACCEPTABLE).all())
