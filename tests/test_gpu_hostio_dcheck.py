@@ -124,3 +124,33 @@ def test_derivative_test_superquadric(name, batch):
     diff = np.abs(got["flagged"].cpu().numpy() - cnt)
     assert diff.sum() <= 0.01 * cnt.sum() + 2
     assert got["max_rel_error"] == pytest.approx(rel.max(), rel=1e-3)
+
+
+def test_eval_batch_host_concurrent_threads():
+    """The host entry from several host threads at once (one library-owned staging buffer and
+    stream per device, serialised by a lock): every call returns its own inputs' results."""
+    import threading
+
+    prob, x, mass, tag = _inputs("ground4_1m", 64)
+    want = [prob.eval_batch_host(x[i:i + 1], mass[i:i + 1], None, outputs=("g", "jac")) for i in range(8)]
+    got, errors = {}, []
+
+    def worker(t):
+        try:
+            for rep in range(25):
+                i = (t + rep) % 8
+                r = prob.eval_batch_host(x[i:i + 1], mass[i:i + 1], None, outputs=("g", "jac"))
+                for k in ("g", "jac"):
+                    if not np.array_equal(r[k], want[i][k], equal_nan=True):
+                        errors.append((t, rep, k))
+            got[t] = True
+        except Exception as e:  # noqa: BLE001
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:5]
+    assert len(got) == 4
