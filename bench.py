@@ -25,6 +25,10 @@ Rank 0 prints one JSON line.  Fields beyond the driver contract:
   jac_folded    the same batch with values-only Jacobian records (CPL_EVAL_JAC_FOLDED: structural
                 constants skipped), kernel time and bytes
   configs1_65k  BASELINE.json configs[1] (65,536 x 4 Ground) kernel time on the same GPU
+  configs2_sq8  BASELINE.json configs[2] (262,144 x 8 Superquadric): kernel time, HBM fraction, VALU
+                roofline (PMC), checker sample
+  configs4_solve5_lbfgs  BASELINE.json configs[4] (8,192 concurrent solves) in the reference's Hessian
+                mode (IPOPT's L-BFGS): solves/s, iterations, a small CPU sample of the same solver
 """
 from __future__ import annotations
 
@@ -337,24 +341,161 @@ def checker_leg(prob, env, xt, mt, tt, out, batch, sample):
     import pyoracle
     from parity_util import check_outputs
 
-    stride = max(1, batch // max(1, sample))
-    idx = torch.arange(0, batch, stride, device=xt.device)
-    idx = torch.unique(torch.cat([idx, torch.tensor([batch - 1], device=xt.device)]))  # include the tail
-    x = xt[idx].cpu().numpy()
-    mass = mt[idx].cpu().numpy() if mt is not None else None
-    tag = tt[idx].cpu().numpy() if tt is not None else None
-    got = {k: out[k][idx].cpu().numpy() for k in ("g", "jac")}
-    ref = pyoracle.eval_batch(prob.desc(), x, mass, tag, outputs=("g", "jac"))
-    res = {"instances": int(idx.numel()), "stride": stride, "policy": "tests/parity_util.py"}
-    try:
-        rep = check_outputs(prob, env, x, got, ref, tag)
-        res["ok"] = True
-        res["bitwise_frac"] = {k: v["bitwise_frac"] for k, v in rep.items()}
-    except AssertionError as e:
-        res["ok"] = False
-        res["error"] = str(e)[:400]
-    res["finite"] = bool(np.isfinite(got["g"]).all() and np.isfinite(got["jac"]).all())
+    dev = xt.device
+    if tt is None:  # one kind: a strided sample of the batch plus its tail
+        stride = max(1, batch // max(1, sample))
+        groups = {env: torch.unique(torch.cat([torch.arange(0, batch, stride, device=dev),
+                                               torch.tensor([batch - 1], device=dev)]))}
+    else:  # mixed batch: a strided sample of EACH environment kind (plus each kind's last instance)
+        kinds = {1: "ground", 2: "superquadric"}
+        groups = {}
+        for code, name in kinds.items():
+            members = torch.nonzero(tt == code).flatten()
+            if members.numel() == 0:
+                continue
+            stride = max(1, members.numel() // max(1, sample // len(kinds)))
+            pick = torch.unique(torch.cat([torch.arange(0, members.numel(), stride, device=dev),
+                                           torch.tensor([members.numel() - 1], device=dev)]))
+            groups[name] = members[pick]
+    res = {"instances": 0, "policy": "tests/parity_util.py", "ok": True, "per_kind": {}}
+    finite = True
+    for kind, idx in groups.items():
+        x = xt[idx].cpu().numpy()
+        mass = mt[idx].cpu().numpy() if mt is not None else None
+        tag = tt[idx].cpu().numpy() if tt is not None else None
+        got = {k: out[k][idx].cpu().numpy() for k in ("g", "jac")}
+        ref = pyoracle.eval_batch(prob.desc(), x, mass, tag, outputs=("g", "jac"))
+        part = {"instances": int(idx.numel())}
+        try:
+            rep = check_outputs(prob, env, x, got, ref, tag)
+            part["ok"] = True
+            part["bitwise_frac"] = {k: v["bitwise_frac"] for k, v in rep.items()}
+        except AssertionError as e:
+            part["ok"] = False
+            part["error"] = str(e)[:400]
+        res["per_kind"][kind] = part
+        res["instances"] += part["instances"]
+        res["ok"] = res["ok"] and part["ok"]
+        finite = finite and bool(np.isfinite(got["g"]).all() and np.isfinite(got["jac"]).all())
+    if len(groups) == 1:  # (the single-kind line keeps its flat fields)
+        only = next(iter(res["per_kind"].values()))
+        res.update({k: v for k, v in only.items() if k != "instances"})
+    res["finite"] = finite
     return res
+
+
+# ------------------------------------------------------------------------------------------
+# side fields of the default run: the other BASELINE.json configs on the driver's clock
+# ------------------------------------------------------------------------------------------
+def side_sq8(dev, stream, valu_counters, check_sample=1024):
+    """BASELINE.json configs[2] (262,144 x 8 Superquadric) on the same GPU: the eval kernel's time
+    (HIP events on the launch stream), its HBM fraction, its VALU roofline (PMC passes collected
+    before this process touched the GPU) and a checker sample of every kernel output."""
+    import ctypes
+
+    import torch
+
+    from centroidalplanner_amd import _abi
+    from centroidalplanner_amd.workload import CONFIGS, generate, make_problem
+
+    cfg = CONFIGS["sq8"]
+    B = cfg.batch
+    prob = make_problem(cfg.n_contacts, cfg.env)
+    x, mass, tag = generate(cfg.n_contacts, cfg.env, B, 0xC910 + cfg.config_id)
+    xt, mt = torch.tensor(x, device=dev), torch.tensor(mass, device=dev)
+    del x, mass
+    out = prob.eval_batch(xt, mt, outputs=("g", "jac", "norms"))
+    ms = ctypes.c_double()
+    p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    _abi.check(_abi.lib.cpl_time_eval_batch(ctypes.byref(prob.desc()), B, p(xt), p(mt), None, p(out["g"]),
+                                            p(out["jac"]), None, None, p(out["norms"]),
+                                            ctypes.c_void_p(stream.cuda_stream), 30, ctypes.byref(ms)))
+    bytes_inst, m = algorithmic_bytes(cfg.n_contacts, cfg.env)
+    res = {"workload": cfg.name, "kernel_ms": ms.value, "rows_per_s": B * m / (ms.value * 1e-3),
+           "hbm_gbps": bytes_inst * B / (ms.value * 1e-3) / 1e9,
+           "frac_of_peak": bytes_inst * B / (ms.value * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+           "bytes_per_instance": bytes_inst}
+    if isinstance(valu_counters, dict):
+        v = valu_roofline(valu_counters, ms.value)
+        res["roofline_valu"] = {k: v[k] for k in ("achieved", "peak", "unit", "frac", "issue_frac", "wait_frac",
+                                                  "valu_active_frac")}
+    elif valu_counters:
+        res["roofline_valu"] = {"error": valu_counters}
+    try:
+        res["check"] = checker_leg(prob, cfg.env, xt, mt, None, out, B, check_sample)
+    except Exception as e:  # noqa: BLE001
+        res["check"] = {"ok": False, "error": f"checker leg failed: {e}"}
+    del out, xt, mt
+    torch.cuda.empty_cache()
+    return res
+
+
+def run_solve5(dev, batch, hessian, steps, warm, max_ls, max_soc, cpu_sample, rank=0, world=1, barrier=None):
+    """BASELINE.json configs[4]: `steps` complete batched solves of `batch` TestBasic ground instances
+    (centroidalplanner_amd/batch_ipm.py -> the native engine), after `warm` untimed ones.  Returns
+    (dt seconds for the timed solves, the last result, the CPU leg or None)."""
+    import torch
+
+    from centroidalplanner_amd.batch_ipm import KernelEvaluator, batch_ipm_solve
+    from centroidalplanner_amd.workload import solve_inputs, solve_problem
+
+    prob = solve_problem().GetCplProblem()
+    X0, mass = solve_inputs(prob, batch, seed=0xC910 + 5 + 7919 * rank)
+    X0t, mt = torch.tensor(X0, device=dev), torch.tensor(mass, device=dev)
+    opts = dict(max_iter=300 if hessian == "exact" else 1000, max_ls=max_ls, max_soc=max_soc, hessian=hessian)
+    for _ in range(warm):
+        batch_ipm_solve(prob, X0t, mt, **opts)
+    torch.cuda.synchronize()
+    if barrier:
+        barrier()
+    ev = KernelEvaluator(prob)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r = batch_ipm_solve(prob, X0t, mt, evaluator=ev, **opts)
+    torch.cuda.synchronize()
+    if barrier:
+        barrier()
+    dt = time.perf_counter() - t0
+    cpu = None
+    if rank == 0 and world == 1 and cpu_sample > 0:
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            from test_batch_solve import OracleBatchEvaluator
+
+            info = host_cpu_info()
+            threads = info["threads"]
+            torch.set_num_threads(threads)
+            Bc = min(cpu_sample, batch)
+            tc = time.perf_counter()
+            rc = batch_ipm_solve(prob, torch.tensor(X0[:Bc]), torch.tensor(mass[:Bc]),
+                                 evaluator=OracleBatchEvaluator(prob, nthreads=threads), **opts)
+            tc = time.perf_counter() - tc
+            okc = int((rc.status <= 1).sum().item())
+            cpu = {"value": Bc / tc, "unit": "solves/s", "cores": threads, "kind": "port",
+                   "sample": f"the first {Bc} of the {batch} instances: the same batched solver (hessian={hessian}; "
+                             f"exact = the oracle's restatement of the analytic Hessian kernel) over the oracle's "
+                             f"callbacks on CPU torch, {threads} threads ({rc.iterations_run} iterations, {okc}/{Bc} "
+                             f"solved, {tc:.1f} s)",
+                   **{k: info[k] for k in ("cpu_model", "affinity", "omp_num_threads")}}
+        except Exception as e:  # noqa: BLE001
+            cpu = {"error": str(e)}
+    return dt, r, cpu
+
+
+def side_solve5(dev, cpu_sample=64):
+    """configs[4] in the reference's Hessian mode (IFOPT's limited-memory default) as a side field:
+    one timed batched solve of 8,192 instances after one warm-up, and a small CPU sample."""
+    from centroidalplanner_amd.workload import SOLVE_CONFIG
+
+    B = SOLVE_CONFIG.batch
+    dt, r, cpu = run_solve5(dev, B, "limited-memory", 1, 1, 4, 1, cpu_sample)
+    its = r.iterations.double()
+    return {"workload": SOLVE_CONFIG.name, "hessian": "limited-memory (IPOPT's L-BFGS, IFOPT's default)",
+            "solves_per_s": B / dt, "ms_per_solve_batch": dt * 1e3, "batch": B,
+            "solved": int((r.status <= 1).sum().item()), "iterations_max": int(its.max().item()),
+            "iterations_mean": float(its.mean().item()), "lockstep_iterations": r.iterations_run,
+            "cpu_baseline": cpu}
 
 
 # ------------------------------------------------------------------------------------------
@@ -366,8 +507,7 @@ def solve_bench(args):
     (CPU torch), a bounded sample of the instances."""
     import torch
 
-    from centroidalplanner_amd.batch_ipm import KernelEvaluator, batch_ipm_solve
-    from centroidalplanner_amd.workload import SOLVE_CONFIG, solve_inputs, solve_problem
+    from centroidalplanner_amd.workload import SOLVE_CONFIG
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -379,57 +519,17 @@ def solve_bench(args):
     if world > 1:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
     B = args.batch or SOLVE_CONFIG.batch
-    prob = solve_problem().GetCplProblem()
-    X0, mass = solve_inputs(prob, B, seed=0xC910 + 5 + 7919 * rank)
-    X0t, mt = torch.tensor(X0, device=dev), torch.tensor(mass, device=dev)
     steps = max(1, min(args.steps, 5))
     warm = 1 if args.warmup > 0 else 0
-    opts = dict(max_iter=300 if args.hessian == "exact" else 1000, max_ls=args.max_ls, max_soc=args.max_soc,
-                hessian=args.hessian)
-    for _ in range(warm):
-        batch_ipm_solve(prob, X0t, mt, **opts)
-    torch.cuda.synchronize()
-    print(f"[solve5] warmup done", file=sys.stderr, flush=True)
-    if world > 1:
-        dist.barrier()
-    ev = KernelEvaluator(prob)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        r = batch_ipm_solve(prob, X0t, mt, evaluator=ev, **opts)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
+    dt, r, cpu = run_solve5(dev, B, args.hessian, steps, warm, args.max_ls, args.max_soc,
+                            0 if args.no_cpu else args.cpu_sample, rank, world,
+                            barrier=dist.barrier if world > 1 else None)
     if world > 1:
         tdt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tdt, op=dist.ReduceOp.MAX)
         dt = float(tdt.item())
     ok = int((r.status <= 1).sum().item())
     its = r.iterations.double()
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        try:
-            sys.path.insert(0, os.path.join(ROOT, "oracle"))
-            sys.path.insert(0, os.path.join(ROOT, "tests"))
-            from test_batch_solve import OracleBatchEvaluator
-
-            info = host_cpu_info()
-            threads = info["threads"]
-            torch.set_num_threads(threads)
-            Bc = min(args.cpu_sample, B)
-            tc = time.perf_counter()
-            rc = batch_ipm_solve(prob, torch.tensor(X0[:Bc]), torch.tensor(mass[:Bc]),
-                                 evaluator=OracleBatchEvaluator(prob, nthreads=threads), **opts)
-            tc = time.perf_counter() - tc
-            okc = int((rc.status <= 1).sum().item())
-            cpu = {"value": Bc / tc, "unit": "solves/s", "cores": threads, "kind": "port",
-                   "sample": f"the first {Bc} of the {B} instances: the same batched solver (hessian={args.hessian}; "
-                             f"exact = the oracle's restatement of the analytic Hessian kernel) over the oracle's "
-                             f"callbacks on CPU torch, {threads} threads ({rc.iterations_run} iterations, {okc}/{Bc} "
-                             f"solved, {tc:.1f} s)",
-                   **{k: info[k] for k in ("cpu_model", "affinity", "omp_num_threads")}}
-        except Exception as e:  # noqa: BLE001
-            cpu = {"error": str(e)}
     if rank == 0:
         print(json.dumps({
             "metric": "concurrent CentroidalPlanner solves per second (full interior-point solve loop, GPU callbacks)",
@@ -481,6 +581,12 @@ def main():
                 valu_counters = collect_valu_counters(args)
             except Exception as e:  # noqa: BLE001
                 valu_counters = f"VALU PMC passes failed: {e}"
+    sq8_counters = None
+    if world == 1 and not args.no_side and args.config == "ground4_1m" and not args.no_pmc:
+        try:  # configs[2]'s VALU counters for its side field (PMC passes run before the GPU is touched)
+            sq8_counters = collect_valu_counters(argparse.Namespace(config="sq8", batch=0))
+        except Exception as e:  # noqa: BLE001
+            sq8_counters = f"VALU PMC passes failed: {e}"
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -514,9 +620,10 @@ def main():
     # per-step host cost is neither a graph launch nor an RCCL enqueue).  Each step still evaluates
     # the whole batch and writes its own norms row.
     S = max(1, min(args.bucket, K))
-    norms = [torch.zeros(S, 2, dtype=torch.float64, device=dev) for _ in range(2)]  # double-buffered buckets
 
     import ctypes
+
+    from centroidalplanner_amd.distributed import BucketedNormGather
 
     def launch(nb, count):
         # `count` steps' device work: per step the fused eval (values + CSR Jacobian values +
@@ -527,10 +634,11 @@ def main():
             out["norms"] = nb[s]
             prob.eval_batch(xt, mt, tt, outputs=("g", "jac", "norms"), out=out, stream=torch.cuda.current_stream(dev))
 
-    def buckets(steps):
-        return [S] * (steps // S) + ([steps % S] if steps % S else [])
-
-    sizes = sorted(set(buckets(K) + buckets(W)))
+    # the bucketed step loop with its asynchronous all-gather (distributed.BucketedNormGather: the
+    # same code the gloo world-2 tests drive on the CPU)
+    runner = BucketedNormGather(world, S, dev, launch, stream=stream)
+    norms = runner.norms
+    sizes = sorted(set(runner.sizes(K) + runner.sizes(W)))
     with torch.cuda.stream(stream):  # warm the launch path (per-stream workspaces) before capture
         for nb in norms:
             launch(nb, 1)
@@ -544,44 +652,19 @@ def main():
                     launch(nb, c)
                 graphs[(j, c)] = gr
         torch.cuda.synchronize()
-    pending = [None, None]
-    gathered = []
+        runner.replay = {key: gr.replay for key, gr in graphs.items()}
     gather_info = None
 
-    def run_bucket(i, count):
-        j = i % 2
-        with torch.cuda.stream(stream):
-            if pending[j] is not None:
-                # the all-gather of two buckets ago may still be reading norms[j]: on RCCL, wait()
-                # orders the CURRENT stream (the launch stream here) after the collective, so the
-                # replay below cannot overwrite norms[j] under it
-                pending[j].wait()
-                pending[j] = None
-            if graphs:
-                graphs[(j, count)].replay()
-            else:
-                launch(norms[j], count)
-            if world > 1:
-                from centroidalplanner_amd.distributed import all_gather_norms
-
-                # RCCL over xGMI on the collective stream, overlapping the next bucket
-                out_norms, work = all_gather_norms(norms[j][:count], async_op=True)
-                pending[j] = work
-                gathered.append((out_norms, count))
-                return work
-        return None
-
-    for i, c in enumerate(buckets(W)):
-        w = run_bucket(i, c)
+    for w in runner.run(W):
         if w is not None:
             w.wait()
     torch.cuda.synchronize()
-    gathered.clear()
+    runner.reset()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    works = [run_bucket(i, c) for i, c in enumerate(buckets(K))]
+    works = runner.run(K)
     for w in works:
         if w is not None:
             w.wait()
@@ -595,16 +678,9 @@ def main():
         dist.all_reduce(tdt, op=dist.ReduceOp.MAX)
         dt = float(tdt.item())
         # every timed step's norms reached every rank: the last bucket's gather holds one row per
-        # (rank, step); combined over ranks it is the whole job's residual for that step
-        from centroidalplanner_amd.distributed import combine_bucket
-
-        last, cnt = gathered[-1]
-        step_norms = combine_bucket(last, world, cnt)
-        # this rank's rows of the gathered bucket must be the norms it computed locally
-        local = norms[(len(buckets(K)) - 1) % 2][:cnt]
-        mine = last.view(world, cnt, 2)[rank]  # rank-major [world * cnt, 2]
-        gather_info = {"steps_in_last_bucket": cnt, "last_step_global_norms": list(step_norms[-1]),
-                       "local_rows_match": bool(torch.equal(mine.to(local.device), local))}
+        # (rank, step); combined over ranks it is the whole job's residual for that step, and this
+        # rank's rows must be the norms it computed locally
+        gather_info = runner.last_bucket_report(rank, K)
 
     # live kernel timing: HIP events on the launch stream around back-to-back eval launches only
     ms = ctypes.c_double()
@@ -692,6 +768,17 @@ def main():
             "note": "128 MB working set: fits the 256 MiB Infinity Cache",
         }
 
+    sq8 = solve5 = None
+    if rank == 0 and world == 1 and not args.no_side and args.config == "ground4_1m":
+        try:
+            sq8 = side_sq8(dev, stream, sq8_counters)
+        except Exception as e:  # noqa: BLE001
+            sq8 = {"error": str(e)}
+        try:
+            solve5 = side_solve5(dev, 0 if args.no_cpu else 64)
+        except Exception as e:  # noqa: BLE001
+            solve5 = {"error": str(e)}
+
     if rank == 0:
         res = {
             "metric": METRIC,
@@ -715,6 +802,8 @@ def main():
                 "parallelism": f"instance-sharded x{world}" + (" + RCCL all-gather of residual norms" if world > 1 else ""),
                 "launch": (f"hip-graph, {S} steps per replay" if graphs else "eager")
                 + (f", one all-gather per {S} steps" if world > 1 else ""),
+                "rank_inputs": "distinct per rank (seed 0xC910 + config + 7919 * rank): weak scaling over "
+                               "different instances, no data-path exchange",
             },
             "instances_per_s": batch * world * K / dt,
             "residual_gather": gather_info,
@@ -742,6 +831,10 @@ def main():
             res["configs1_65k"] = side
         if single:
             res["single_instance"] = single
+        if sq8:
+            res["configs2_sq8"] = sq8
+        if solve5:
+            res["configs4_solve5_lbfgs"] = solve5
         print(json.dumps(res), flush=True)
 
     if world > 1:

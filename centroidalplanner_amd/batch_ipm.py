@@ -174,7 +174,16 @@ class NativeSolver:
         if X0.shape != (B, n) or X0.dtype != torch.float64 or not X0.is_cuda:
             raise ValueError(f"X0 must be a float64 CUDA tensor [{B}, {n}]")
         X0 = X0.contiguous()
-        mass = None if mass is None else mass.to(torch.float64).contiguous()
+        # the engine copies the masses / tags device-to-device: same device as X0, one per instance
+        if mass is not None:
+            if not torch.is_tensor(mass) or mass.device != dev or tuple(mass.shape) != (B,):
+                raise ValueError(f"mass must be a tensor [{B}] on {dev}")
+            mass = mass.to(torch.float64).contiguous()
+        if env_tag is not None:
+            if (not torch.is_tensor(env_tag) or env_tag.device != dev or tuple(env_tag.shape) != (B,)
+                    or env_tag.dtype != torch.uint8):
+                raise ValueError(f"env_tag must be a uint8 tensor [{B}] on {dev}")
+            env_tag = env_tag.contiguous()
         x = torch.empty(B, n, dtype=torch.float64, device=dev)
         y = torch.empty(B, m, dtype=torch.float64, device=dev)
         status = torch.empty(B, dtype=torch.int32, device=dev)

@@ -1,14 +1,21 @@
 // cpl_kernels.hip — the hot path on gfx950: batched eval_g + eval_jac_g + eval_f + eval_grad_f
-// of CentroidalPlanner's IFOPT problem, one wave-lane per instance.
+// of CentroidalPlanner's IFOPT problem for many independent instances per launch.
 //
-// Mapping (memory-bound pointwise work, no MFMA):
-//   * one workgroup = one wave = a tile of 64 consecutive instances;
-//   * the tile's decision vectors (64*n doubles, contiguous in HBM) are streamed into LDS with
-//     16-byte coalesced loads; each lane then reads its own instance row from LDS;
-//   * each lane evaluates its instance in IFOPT order (values / CSR Jacobian / dense gradient)
-//     and "emits" every output double into a per-lane LDS row of CHUNK slots; when the chunk is
-//     full the wave writes the 64 x CHUNK block back with 16-byte stores, so every store wave-
-//     instruction covers 8 contiguous 128-byte runs of instance records (AoS, IFOPT layout).
+// Kernels the product dispatches (memory-bound pointwise work, no MFMA):
+//   * cpl_eval_pipe_kernel<ENV> — none / Ground environments (the north-star path): persistent,
+//     warp-specialised workgroups walking tiles blockIdx, blockIdx + grid, ...; one loader wave DMAs
+//     the NEXT tile's decision vectors into the other half of a double-buffered LDS image
+//     (global_load_lds_dwordx4) while three compute waves evaluate the current tile's work items
+//     (contact blocks in std::map order, statics values + force rows, torque rows, cost) into the
+//     tile's AoS output image in LDS and copy it out with 16-byte non-temporal stores, so every
+//     128-byte line of g / jac is written once, whole;
+//   * cpl_eval_tile_kernel<ENV> — Superquadric and mixed batches: one 256-thread workgroup per tile
+//     of T consecutive instances (T sized to the LDS budget), the same work items, Superquadric
+//     contacts in two barrier-separated phases (per (contact, axis) double-double power ladders into
+//     an LDS scratch, then per (contact, row) the normal-Jacobian entries); mixed tiles compacted by
+//     environment kind with a wave ballot;
+//   * cpl_eval_kernel — the first design (one wave-lane per instance, per-lane LDS rows written
+//     back 64 x CHUNK at a time), kept for A/B measurements only.
 // Arithmetic: IEEE binary64 with -ffp-contract=off and the reference's operation order
 // (see the oracle, oracle/cpl_oracle.c, and DESIGN.md §Numerics); integer and half-integer pow
 // exponents go through a double-double power (correctly rounded), instance-independent

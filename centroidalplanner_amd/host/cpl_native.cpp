@@ -4,6 +4,8 @@
 // src/CentroidalPlanner.cpp:22-34 (ifopt::IpoptSolver::Solve), with IFOPT's defaults.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 
@@ -37,12 +39,14 @@ BatchSolver::BatchSolver(CplProblem::Ptr problem, int64_t batch, const SolveOpti
     hip_check(hipMalloc(&_dstatus, 4 * B), "hipMalloc");
     hip_check(hipMalloc(&_diters, 4 * B), "hipMalloc");
   } catch (...) {
-    this->~BatchSolver();
+    release();  // (the destructor does not run for a constructor that throws)
     throw;
   }
 }
 
-BatchSolver::~BatchSolver() {
+BatchSolver::~BatchSolver() { release(); }
+
+void BatchSolver::release() {
   for (void* p : {(void*)_dx0, (void*)_dmass, (void*)_dx, (void*)_dy, (void*)_dobj, (void*)_dpinf, (void*)_dstatus,
                   (void*)_diters})
     if (p) (void)hipFree(p);
@@ -78,9 +82,14 @@ void BatchSolver::Solve(const double* x0, const double* mass, double* x, double*
 
 bool NativeSolver::Solve(CplTNLP& nlp) {
   const CplProblem::Ptr& prob = nlp.problem();
-  const int32_t n = prob->n();
+  const int32_t n = prob->n(), m = prob->m();
   std::vector<double> x0(n), x(n);
   nlp.get_starting_point(n, true, x0.data());
+  {  // the derivative test runs where the solve starts: x0 inside the variable bounds
+    std::vector<double> xl(n), xu(n), gl(m), gu(m);
+    nlp.get_bounds_info(n, xl.data(), xu.data(), m, gl.data(), gu.data());
+    for (int32_t j = 0; j < n; ++j) x0[j] = std::fmin(std::fmax(x0[j], xl[j]), xu[j]);
+  }
   _dreport = cpl_derivative_report{};
   if (_opt.derivative_test) {  // IPOPT checks the first derivatives before it iterates
     double* dx = nullptr;
@@ -94,8 +103,15 @@ bool NativeSolver::Solve(CplTNLP& nlp) {
     hip_check(e, "hipMemcpy x0");
     engine_check(st);
   }
-  BatchSolver bs(prob, 1, _opt);
-  bs.Solve(x0.data(), nullptr, x.data(), nullptr, &_status, &_iterations, nullptr, &_primal_inf);
+  // the engine handle (device buffers, captured iteration graphs) is kept between solves of the same
+  // problem template; a changed template (any setter since the last solve) gets a new one
+  if (!_bs || _bs_problem != prob.get() || std::memcmp(&_bs_desc, &prob->Desc(), sizeof(_bs_desc)) != 0) {
+    _bs.reset();
+    _bs.reset(new BatchSolver(prob, 1, _opt));
+    _bs_problem = prob.get();
+    _bs_desc = prob->Desc();
+  }
+  _bs->Solve(x0.data(), nullptr, x.data(), nullptr, &_status, &_iterations, nullptr, &_primal_inf);
   nlp.finalize_solution(n, x.data());
   return _status == CPL_SOLVE_OPTIMAL || _status == CPL_SOLVE_ACCEPTABLE;
 }

@@ -22,29 +22,57 @@ from .solver import solve
 
 @dataclass
 class ContactValues:
-    """include/CentroidalPlanner/Ifopt/Types.h:8-13"""
+    """include/CentroidalPlanner/Ifopt/Types.h:8-13; pycpl's read-only names force / position /
+    normal (bindings/python/pyCpl.cpp:34-37) are aliases of the C++ member names."""
 
     force_value: np.ndarray
     position_value: np.ndarray
     normal_value: np.ndarray
 
+    @property
+    def force(self) -> np.ndarray:
+        return self.force_value
+
+    @property
+    def position(self) -> np.ndarray:
+        return self.position_value
+
+    @property
+    def normal(self) -> np.ndarray:
+        return self.normal_value
+
+
+def _eigen_row(v) -> str:
+    """Eigen's default IOFormat for a row vector (what `ss << v.transpose()` prints): every
+    coefficient in the stream's default format (%g, 6 significant digits), right-aligned to the
+    widest coefficient, separated by one space."""
+    cells = [f"{float(c):g}" for c in np.asarray(v, dtype=np.float64).reshape(-1)]
+    w = max((len(c) for c in cells), default=0)
+    return " ".join(c.rjust(w) for c in cells)
+
 
 @dataclass
 class Solution:
-    """include/CentroidalPlanner/Ifopt/Types.h:15-21 (contact_values_map iterates in name order)."""
+    """include/CentroidalPlanner/Ifopt/Types.h:15-21 (contact_values_map iterates in name order);
+    pycpl's ``com`` (bindings/python/pyCpl.cpp:39-42) aliases com_sol, and ``repr`` is operator<<."""
 
     com_sol: np.ndarray
     contact_values_map: Dict[str, ContactValues] = field(default_factory=dict)
     success: bool = True
     message: str = ""
 
+    @property
+    def com(self) -> np.ndarray:
+        return self.com_sol
+
     def __str__(self) -> str:  # operator<< (src/CplProblem.cpp:321-344)
-        fmt = lambda v: " ".join(f"{c:g}" for c in v)  # noqa: E731
-        lines = [f"CoM: {fmt(self.com_sol)}"]
-        lines += [f"F_{k}: {fmt(v.force_value)}" for k, v in self.contact_values_map.items()]
-        lines += [f"p_{k}: {fmt(v.position_value)}" for k, v in self.contact_values_map.items()]
-        lines += [f"n_{k}: {fmt(v.normal_value)}" for k, v in self.contact_values_map.items()]
+        lines = [f"CoM: {_eigen_row(self.com_sol)}"]
+        lines += [f"F_{k}: {_eigen_row(v.force_value)}" for k, v in self.contact_values_map.items()]
+        lines += [f"p_{k}: {_eigen_row(v.position_value)}" for k, v in self.contact_values_map.items()]
+        lines += [f"n_{k}: {_eigen_row(v.normal_value)}" for k, v in self.contact_values_map.items()]
         return "\n".join(lines) + "\n"
+
+    __repr__ = __str__  # pyCpl.cpp:38 binds __repr__ to operator<<
 
 
 def _v3(v) -> np.ndarray:

@@ -28,22 +28,6 @@ class SolveResult:
     derivative_report: Optional[dict] = None  # derivative_test = "first-order" (cpl_derivative_test)
 
 
-class TorchEvaluator:
-    """Batched callbacks on the GPU through CplProblem.eval_batch (host arrays in and out)."""
-
-    def __init__(self, problem):
-        import torch
-
-        self.problem = problem
-        self.torch = torch
-        self.dev = torch.device("cuda", torch.cuda.current_device())
-
-    def eval_batch(self, X):
-        t = self.torch.as_tensor(np.ascontiguousarray(np.atleast_2d(X), dtype=np.float64), device=self.dev)
-        out = self.problem.eval_batch(t, outputs=("g", "jac", "f", "grad"))
-        return {k: v.cpu().numpy() for k, v in out.items()}
-
-
 class _HostBatchEvaluator:
     """An eval_batch(X) evaluator as batch_ipm's callback (CPU tensors in and out); forwards an
     analytic `hessian(X, y, free)` when the evaluator has one."""

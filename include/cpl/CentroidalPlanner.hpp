@@ -62,6 +62,7 @@ class BatchSolver {
   bool graph_captured() const;
 
  private:
+  void release();  // frees every device resource (idempotent: pointers nulled)
   CplProblem::Ptr _problem;
   int64_t _batch;
   cpl_solver* _solver = nullptr;
@@ -85,6 +86,9 @@ class NativeSolver : public NlpSolver {
 
  private:
   SolveOptions _opt;
+  std::unique_ptr<BatchSolver> _bs;  // kept between solves of the same template (_bs_desc)
+  const CplProblem* _bs_problem = nullptr;
+  cpl_problem_desc _bs_desc{};
   int32_t _status = -1, _iterations = 0;
   double _primal_inf = 0.0;
   cpl_derivative_report _dreport{};

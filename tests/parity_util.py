@@ -129,6 +129,47 @@ def sq_params(prob):
     return np.array(d.sq_C[:]), np.array(d.sq_R[:]), np.array(d.sq_P[:])
 
 
+def plain_rel_off_diagonals(prob, env, x, got, ref, tag=None):
+    """Plain relative error |gpu - ref| / |ref| of every pow-bearing entry EXCEPT the three
+    normal-Jacobian diagonals of each Superquadric contact (whose expanded numerators cancel,
+    src/Superquadric.cpp:98-100,152-154,206-208, and are graded on the scale of check_outputs):
+    the environment value / normal residual entries of g and the environment-gradient and
+    off-diagonal normal-Jacobian entries of jac.  Returns {"g": max, "jac": max, "entries": count,
+    "hist": decades} (NaN positions are compared by check_outputs, skipped here)."""
+    from centroidalplanner_amd import ENV_SUPERQUADRIC
+
+    N = len(prob.contact_names)
+    n, m, nnz = prob.get_nlp_info()
+    B = x.shape[0]
+    sq_inst = (np.ones(B, dtype=bool) if env == "superquadric" else
+               (tag == ENV_SUPERQUADRIC) if env == "mixed" else np.zeros(B, dtype=bool))
+    jm, gm = sq_entry_mask(N, prob.map_order, nnz, m, sq_inst)
+    for jo, _, _ in contact_offsets(N, True, prob.map_order):
+        for a in range(3):
+            jm[:, jo + 3 + 4 * a + a] = False  # the diagonal of normal-Jacobian row a
+    out = {"entries": 0, "hist": {"bitwise": 0, "lt1e-15": 0, "lt1e-13": 0, "lt1e-12": 0, "lt1e-10": 0,
+                                  "ge1e-10": 0}}
+    for k, mask in (("g", gm), ("jac", jm)):
+        gv, rv = np.asarray(got[k]), np.asarray(ref[k])
+        sel = mask & ~(np.isnan(gv) | np.isnan(rv))
+        with np.errstate(all="ignore"):
+            err = np.where(sel & (gv != rv), np.abs(gv - rv), 0.0)
+            rel = np.where(err > 0, err / np.where(np.abs(rv) > 0, np.abs(rv), 0.0), 0.0)
+        rel = np.where(sel & (err > 0) & (rv == 0), np.inf, rel)
+        v = rel[sel]
+        out[k] = float(v.max()) if v.size else 0.0
+        out["entries"] += int(sel.sum())
+        nz = v[v > 0]
+        h = out["hist"]
+        h["bitwise"] += int((v == 0).sum())
+        h["lt1e-15"] += int((nz < 1e-15).sum())
+        h["lt1e-13"] += int(((nz >= 1e-15) & (nz < 1e-13)).sum())
+        h["lt1e-12"] += int(((nz >= 1e-13) & (nz < 1e-12)).sum())
+        h["lt1e-10"] += int(((nz >= 1e-12) & (nz < 1e-10)).sum())
+        h["ge1e-10"] += int((nz >= 1e-10).sum())
+    return out
+
+
 def check_outputs(prob, env, x, got, ref, tag=None, raise_on_fail=True):
     """Apply the policy above to every output; returns {output: stats}; raises AssertionError
     (raise_on_fail=False: every output is checked and stats["ok"] says whether it passed)."""

@@ -133,3 +133,75 @@ def test_bucketed_norms_gloo_world2():
     assert np.array_equal(res[0][1], res[1][1])
     steps = combine_bucket(res[0][1], world, 3)
     assert steps == [(10.0 + s, (0.0 + s) + (100.0 + s)) for s in range(3)]
+
+
+def _loop_worker(rank, world, port, steps, bucket, q):
+    """The bench's bucketed step loop (distributed.BucketedNormGather, the code bench.py runs on
+    N GPUs) under gloo: every step writes synthetic per-rank norms rows; the handles are waited in
+    REVERSE issue order (out-of-order completion), then the gathered buckets are checked."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import torch.distributed as dist
+
+    from centroidalplanner_amd.distributed import BucketedNormGather, combine_bucket
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    step_no = [0]
+    written = []
+
+    def launch(rows, count):  # stands in for `count` eval steps writing their [max, sumsq] rows
+        for s in range(count):
+            k = step_no[0]
+            rows[s, 0] = 10.0 * rank + k       # max violation of this rank's shard at step k
+            rows[s, 1] = 1.0 + rank + 0.5 * k  # sum of squares
+            written.append((k, rows[s].clone()))
+            step_no[0] += 1
+
+    run = BucketedNormGather(world, bucket, torch.device("cpu"), launch)
+    for w in run.run(3):  # warm-up buckets, then forgotten
+        if w is not None:
+            w.wait()
+    run.reset()
+    step_no[0] = 0
+    written.clear()
+    works = run.run(steps)
+    for w in reversed(works):
+        if w is not None:
+            w.wait()
+    report = run.last_bucket_report(rank, steps)
+    per_step = []
+    for out, cnt in run.gathered:
+        per_step += combine_bucket(out, world, cnt)
+    q.put((rank, [c for _, c in run.gathered], per_step, report))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("steps,bucket", [(23, 10), (4, 10), (9, 1)])
+def test_bucketed_gather_loop_gloo_world2(steps, bucket):
+    """Every timed step's norms reach every rank, combined per step (max over ranks, sum over ranks);
+    the last bucket's own rows match what the rank computed; bucket sizes cover the steps."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_loop_worker, args=(r, world, port, steps, bucket, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, counts, per_step, report in res:
+        assert sum(counts) == steps and all(c <= bucket for c in counts)
+        assert len(per_step) == steps
+        for k, (gmax, gsum) in enumerate(per_step):
+            assert gmax == 10.0 * (world - 1) + k
+            assert gsum == sum(1.0 + r + 0.5 * k for r in range(world))
+        assert report["local_rows_match"]
+        assert report["steps_in_last_bucket"] == counts[-1]
+    assert res[0][2] == res[1][2]

@@ -112,4 +112,5 @@ def test_solution_print_format():
     sol.contact_values_map["c1"] = ContactValues(np.array([0, 0, 981.0]), np.array([0, 0, 0.1]), np.array([0, 0, 1.0]))
     s = str(sol)
     assert s.splitlines()[0] == "CoM: 0 0 1"
-    assert "F_c1: 0 0 981" in s and "p_c1: 0 0 0.1" in s and "n_c1: 0 0 1" in s
+    # Eigen's row format: every coefficient right-aligned to the widest one
+    assert "F_c1:   0   0 981" in s and "p_c1:   0   0 0.1" in s and "n_c1: 0 0 1" in s

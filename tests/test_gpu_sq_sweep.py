@@ -9,8 +9,10 @@ double-double, general exponents through the device's pow).  Sets covered:
   * P = 80 (outside the ladder) and mixed per-axis P;
   * N = 32 (CPL_MAX_CONTACTS), Superquadric, Ground, mixed and no environment.
 Parity policy: tests/parity_util.py (bit-exact off the pow-bearing entries, 1e-10 of the
-conditioning-aware scale on them, NaN positions identical).  The plain relative-error histogram of
-the pow-bearing entries is written to gpurun_out/sq_sweep_hist.json next to the scaled figure.
+conditioning-aware scale on them, NaN positions identical), and every pow-bearing entry off the three
+normal-Jacobian diagonals within 1e-10 PLAIN relative error (asserted).  The plain relative-error
+histogram of the pow-bearing entries is written to gpurun_out/sq_sweep_hist.json next to the scaled
+figure.
 """
 import json
 import os
@@ -19,7 +21,7 @@ import numpy as np
 import pytest
 
 import pyoracle
-from parity_util import check_outputs
+from parity_util import RTOL, check_outputs, plain_rel_off_diagonals
 
 torch = pytest.importorskip("torch")
 
@@ -103,8 +105,11 @@ def test_superquadric_parameter_sweep(name, N):
     x, mass = _sq_points(prob, 1501, 17 + N)
     got, ref = _run(prob, x, mass)
     rep = check_outputs(prob, "superquadric", x, got, ref, raise_on_fail=False)
-    _REPORT[f"{name}/N{N}"] = _summary(rep)
+    plain = plain_rel_off_diagonals(prob, "superquadric", x, got, ref)
+    _REPORT[f"{name}/N{N}"] = dict(_summary(rep), plain_off_diagonal=plain)
     assert all(rep[k]["ok"] for k in rep), (name, N, rep)
+    # the north-star bound as a PLAIN relative error on every pow-bearing entry off the diagonals
+    assert plain["g"] <= RTOL and plain["jac"] <= RTOL, (name, N, plain)
     if name in ("P2.5", "P3.7"):  # negative bases: NaN (glibc pow), at the same positions
         assert np.isnan(ref["jac"]).any()
 
@@ -118,8 +123,10 @@ def test_max_contacts(env):
     x, mass, tag = generate(32, env, 203, 321)
     got, ref = _run(prob, x, mass, tag)
     rep = check_outputs(prob, env, x, got, ref, tag, raise_on_fail=False)
-    _REPORT[f"N32/{env}"] = _summary(rep)
+    plain = plain_rel_off_diagonals(prob, env, x, got, ref, tag)
+    _REPORT[f"N32/{env}"] = dict(_summary(rep), plain_off_diagonal=plain)
     assert all(rep[k]["ok"] for k in rep), (env, rep)
+    assert plain["g"] <= RTOL and plain["jac"] <= RTOL, (env, plain)
 
 
 def test_write_report():
