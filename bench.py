@@ -83,8 +83,8 @@ def parse():
     ap.add_argument("--bucket", type=int, default=10,
                     help="steps per HIP-graph replay and per residual-norm all-gather (1 = per step)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--max-ls", type=int, default=4, help="solve5: line-search trials per iteration")
-    ap.add_argument("--max-soc", type=int, default=1, help="solve5: second-order corrections per iteration")
+    ap.add_argument("--max-ls", type=int, default=40, help="solve5: backtracking trials per iteration at most")
+    ap.add_argument("--max-soc", type=int, default=4, help="solve5: second-order corrections on the first trial")
     ap.add_argument("--hessian", default="exact", choices=["exact", "limited-memory"],
                     help="solve5: exact Lagrangian Hessian (analytic kernel) or IFOPT's limited-memory default")
     ap.add_argument("--cpu-sample", type=int, default=512, help="solve5: instances in the CPU baseline's sample")
@@ -489,7 +489,7 @@ def side_solve5(dev, cpu_sample=64):
     from centroidalplanner_amd.workload import SOLVE_CONFIG
 
     B = SOLVE_CONFIG.batch
-    dt, r, cpu = run_solve5(dev, B, "limited-memory", 1, 1, 4, 1, cpu_sample)
+    dt, r, cpu = run_solve5(dev, B, "limited-memory", 1, 1, 40, 4, cpu_sample)
     its = r.iterations.double()
     return {"workload": SOLVE_CONFIG.name, "hessian": "limited-memory (IPOPT's L-BFGS, IFOPT's default)",
             "solves_per_s": B / dt, "ms_per_solve_batch": dt * 1e3, "batch": B,

@@ -177,6 +177,7 @@ SIGNATURES = {
         [c_int64, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
          c_void_p, c_void_p],
     ),
+    "cpl_kkt_qd_solve": (c_int32, [c_int64, c_int32, c_int32] + [c_void_p] * 12),
     "cpl_kkt_solve": (
         c_int32,
         [c_int32, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -209,6 +210,7 @@ SIGNATURES = {
     "cpl_solver_solve": (c_int32, [c_void_p] + [c_void_p] * 10 + [POINTER(c_int32), POINTER(c_int64), c_void_p]),
     "cpl_solver_dims": (c_int32, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     "cpl_solver_stats": (c_int32, [c_void_p, POINTER(c_int32), POINTER(c_int64)]),
+    "cpl_solver_restorations": (c_int32, [c_void_p, c_void_p, c_void_p]),
 }
 
 

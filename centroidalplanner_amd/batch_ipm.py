@@ -71,7 +71,27 @@ BIG = INF / 10.0  # |bound| >= 1e19 is infinite (IPOPT nlp_lower/upper_bound_inf
 STATUS_OPTIMAL = 0
 STATUS_ACCEPTABLE = 1
 STATUS_MAX_ITER = 2
-STATUS_NAMES = {STATUS_OPTIMAL: "optimal", STATUS_ACCEPTABLE: "acceptable", STATUS_MAX_ITER: "max_iter"}
+STATUS_INFEASIBLE = 3     # the restoration phase converged: a point of local infeasibility
+STATUS_RESTO_FAILED = 4   # the restoration phase's line search failed
+STATUS_NAMES = {STATUS_OPTIMAL: "optimal", STATUS_ACCEPTABLE: "acceptable", STATUS_MAX_ITER: "max_iter",
+                STATUS_INFEASIBLE: "local_infeasibility", STATUS_RESTO_FAILED: "restoration_failed"}
+
+# IPOPT's defaults (Waechter & Biegler 2006; IpFilterLSAcceptor / IpBacktrackingLineSearch /
+# IpMonotoneMuUpdate / IpRestoMinC_1Nrm option defaults) that the iteration restates
+GAMMA_TH, GAMMA_PHI, DELTA_SW, S_TH, S_PHI, ETA_PHI = 1e-5, 1e-8, 1.0, 1.1, 2.3, 1e-8  # filter / switching / Armijo
+ALPHA_MIN_FRAC = 0.05      # alpha_min_frac
+KAPPA_SOC = 0.99           # kappa_soc
+OBJ_MAX_INC = 5.0          # obj_max_inc
+KAPPA_SIGMA = 1e10         # kappa_sigma
+BARRIER_TOL_FACTOR = 10.0  # barrier_tol_factor (kappa_epsilon)
+COMPL_INF_TOL = 1e-4       # compl_inf_tol (the barrier parameter's floor: min(tol, compl_inf_tol) / 11)
+MU_ROUNDS = 6              # barrier decreases per iteration (mu_allow_fast_monotone_decrease; 0.1 -> floor in 6)
+TINY_STEP_TOL, TINY_STEP_Y_TOL = 10.0 * EPS, 1e-2  # tiny_step_tol, tiny_step_y_tol
+RHO_R = 1000.0             # resto_penalty_parameter
+KAPPA_RESTO = 0.9          # required_infeasibility_reduction
+BOUND_MULT_RESET = 1000.0  # bound_mult_reset_threshold
+SOFT_RESTO_FACTOR = 0.9999  # soft_resto_pderror_reduction_factor
+MAX_SOFT_RESTO = 10         # max_soft_resto_iters
 
 FMAX = 64  # filter entries kept per instance (a ring)
 
@@ -130,6 +150,7 @@ class BatchSolveResult:
     iterations_run: int  # lock-step iterations of the batch
     graph: bool          # the iteration ran as a captured HIP graph
     compactions: int = 0  # active-set compactions of the native engine (the batch shrank this often)
+    restorations: object = None  # [B] int: restoration-phase entries per instance
 
     @property
     def success(self):
@@ -145,7 +166,7 @@ class NativeSolver:
     once, the iteration captured once as a HIP graph and replayed on every solve."""
 
     def __init__(self, problem, batch, tol=1e-8, max_iter=3000, mu_init=0.1, acceptable_tol=1e-6,
-                 acceptable_iter=15, max_ls=4, max_soc=1, hessian="exact", fd_step=1e-6, graph=True, compact=True):
+                 acceptable_iter=15, max_ls=40, max_soc=4, hessian="exact", fd_step=1e-6, graph=True, compact=True):
         o = _abi.SolveOptions()
         _abi.lib.cpl_solve_options_default(ctypes.byref(o))
         o.max_iter, o.max_ls, o.max_soc, o.acceptable_iter = int(max_iter), int(max_ls), int(max_soc), int(acceptable_iter)
@@ -200,9 +221,13 @@ class NativeSolver:
         nc, rows = ctypes.c_int32(), ctypes.c_int64()
         _abi.check(_abi.lib.cpl_solver_stats(self.handle, ctypes.byref(nc), ctypes.byref(rows)))
         self.compactions, self.final_rows = int(nc.value), int(rows.value)
+        resto = torch.empty(B, dtype=torch.int64, device=dev)
+        _abi.check(_abi.lib.cpl_solver_restorations(self.handle, _ptr(resto),
+                                                    ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
         return BatchSolveResult(x=x, y=y, status=status.to(torch.int64), iterations=iters.to(torch.int64),
                                 objective=obj, primal_inf=pinf, dual_inf=dinf, evaluations=int(ev.value),
-                                iterations_run=int(it.value), graph=bool(g.value), compactions=int(nc.value))
+                                iterations_run=int(it.value), graph=bool(g.value), compactions=int(nc.value),
+                                restorations=resto)
 
 
 _NATIVE_CACHE = {}
@@ -221,9 +246,9 @@ def _native(problem, B, **opts):
 
 def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None, tol: float = 1e-8,
                     max_iter: int = 3000, mu_init: float = 0.1, acceptable_tol: float = 1e-6,
-                    acceptable_iter: int = 15, max_ls: int = 4, max_soc: int = 1, hessian: str = "exact",
+                    acceptable_iter: int = 15, max_ls: int = 40, max_soc: int = 4, hessian: str = "exact",
                     fd_step: float = 1e-6, graph: Optional[bool] = None, check_every: int = 4,
-                    verbose: int = 0, compact: bool = True) -> BatchSolveResult:
+                    verbose: int = 0, compact: bool = True, verbose_instance: int = 0) -> BatchSolveResult:
     """Solve B instances of `problem`'s template from the starting points X0 [B, n] (torch float64,
     device tensor), per-instance robot masses `mass` [B] (None: the template's).
 
@@ -233,7 +258,8 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     no-environment problems on the device; batched central differences of the Lagrangian gradient
     otherwise), "fd" (always the central differences) or "limited-memory"
     (IPOPT's L-BFGS, 6 pairs).  graph: capture one iteration as a HIP graph (default: on for device tensors).
-    max_ls / max_soc: line-search trials / second-order corrections per iteration (fixed counts)."""
+    max_ls / max_soc: at most this many backtracking trials per iteration (the search also stops below
+    IPOPT's alpha_min) / second-order corrections on the first trial (IPOPT max_soc 4)."""
     if hessian not in ("exact", "fd", "limited-memory"):
         raise ValueError("hessian must be 'exact', 'fd' or 'limited-memory'")
     use_bfgs = hessian == "limited-memory"
@@ -300,7 +326,8 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     eye_f = torch.eye(nf, dtype=dt, device=dev)
     fslot = torch.arange(FMAX, device=dev)[None, :]
     fd_cols = torch.arange(nf, device=dev)
-
+    mu_min = min(tol, COMPL_INF_TOL) / (BARRIER_TOL_FACTOR + 1.0)  # IPOPT MonotoneMuUpdate's floor
+    xmask = torch.cat([torch.ones(nf, dtype=torch.bool, device=dev), torch.zeros(nI, dtype=torch.bool, device=dev)])
 
     def push(v):  # IPOPT bound_push = bound_frac = 1e-2 (absolute and relative to the range)
         k = 1e-2
@@ -348,7 +375,9 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         du_ = torch.where(hasU, wu0 - wv, torch.ones_like(wv))
         return -muv * (torch.log(dl_).sum(1) + torch.log(du_).sum(1))
 
-    def fd_hessian(Xc, yv):
+    def fd_hessian(Xc, yv, with_grad=True):
+        """Central differences of grad f + J^T y (with_grad False: of J^T y alone — the restoration
+        phase's constraint curvature) over x_free."""
         nonlocal n_eval
         h = fd_step * torch.clamp(Xc[:, free].abs(), min=1.0)                       # [B, nf]
         Xp = Xc.unsqueeze(1).repeat(1, 2 * nf, 1)                                   # [B, 2nf, n]
@@ -356,11 +385,51 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         Xp[:, nf + fd_cols, free] -= h
         n_eval += 1
         o = ev(Xp.view(B * 2 * nf, n), Mass_fd, outputs=("jac", "grad"))
-        gL = o["grad"].clone()
+        gL = o["grad"].clone() if with_grad else torch.zeros_like(o["grad"])
         gL.index_add_(1, jCol_t, torch.nan_to_num(o["jac"], nan=0.0) * yv.repeat_interleave(2 * nf, 0)[:, iRow_t])
         gL = gL.view(B, 2 * nf, n)[:, :, free]
         H = (gL[:, :nf] - gL[:, nf:]) / (2.0 * h[:, :, None])
         return 0.5 * (H + H.transpose(1, 2))
+
+    def hessian_blk(wv, yv, constraints_only=False):
+        """Hessian of the Lagrangian over x_free at unpack(wv): the evaluator's analytic one when it has
+        one (hessian="exact"), else central differences; constraints_only: of y^T g alone (the
+        restoration phase: its objective's curvature is the proximity term, added by the caller)."""
+        Xc = unpack(wv)
+        if hessian == "exact" and hasattr(ev, "hessian"):
+            Hb = ev.hessian(Xc, yv, free, zero_cost=True) if constraints_only else ev.hessian(Xc, yv, free)
+            if Hb is not None:
+                return Hb
+        return fd_hessian(Xc, yv, with_grad=not constraints_only)
+
+    def chol_inertia(K, dwl, mask):
+        """Cholesky of K + delta_w I with IPOPT's inertia-correction schedule (first 1e-4, or
+        dwl / 3 when the last correction was dwl; x100 / x8 growth); pivots at or below
+        _PIVOT_REL max|K_ii| count as zero eigenvalues."""
+        nzz = K.shape[1]
+        eye_z = torch.eye(nzz, dtype=dt, device=dev)
+        piv_tol = _PIVOT_REL * K.diagonal(dim1=1, dim2=2).abs().amax(1)
+
+        def chol(dw_):
+            Lf, inf_ = torch.linalg.cholesky_ex(K + dw_[:, None, None] * eye_z)
+            if nzz:
+                inf_ = torch.where((inf_ == 0) & ((Lf.diagonal(dim1=1, dim2=2) ** 2).amin(1) <= piv_tol),
+                                   torch.ones_like(inf_), inf_)
+            return Lf, inf_
+
+        delta_w = zeros_B.clone()
+        L1, info1 = chol(delta_w)
+        for _ in range(64):
+            bad = (info1 != 0) & mask
+            if not bool(bad.any()):
+                break
+            first_dw = torch.where(dwl == 0, torch.full_like(delta_w, 1e-4), torch.clamp(dwl / 3.0, min=1e-20))
+            grow = delta_w * torch.where(dwl == 0, 100.0, 8.0)
+            delta_w = torch.where(bad, torch.where(delta_w == 0, first_dw, grow), delta_w)
+            L1n, info1n = chol(delta_w)
+            L1 = torch.where(bad[:, None, None], L1n, L1)
+            info1 = torch.where(bad, info1n, info1)
+        return L1, delta_w
 
     def kkt_host(M, A, r1, r2, mu, dwl, active):
         """The same step as cpl_kkt_solve from torch's dense factorisations (host tensors), step for
@@ -376,33 +445,36 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         dc = 1e-8 * mu ** 0.25 * torch.where(rmax > 0, rmax, torch.ones_like(rmax))
         small = ~(Rd.abs() >= 1e-10 * rmax[:, None]) | (rmax[:, None] == 0)
         rank_def = small.any(1) if m else torch.zeros(B, dtype=torch.bool)
-        delta_c = torch.where(rank_def, dc, zeros_B)
         Rd.copy_(torch.where(small, Rd + torch.where(Rd < 0, -dc[:, None], dc[:, None]), Rd))
         Hr = Z.transpose(1, 2) @ M @ Z
         Hr = 0.5 * (Hr + Hr.transpose(1, 2))
         nz = nw - m
-        eye_z = torch.eye(nz, dtype=dt)
-        piv_tol = _PIVOT_REL * M.diagonal(dim1=1, dim2=2).abs().amax(1)
+        # the inertia test pivots against the full system's M (its largest diagonal entry)
+        piv_scale = M.diagonal(dim1=1, dim2=2).abs().amax(1)
+        if nz:
+            eye_z = torch.eye(nz, dtype=dt)
+            piv_tol = _PIVOT_REL * piv_scale
 
-        def chol(dw_):
-            Lf, inf_ = torch.linalg.cholesky_ex(Hr + dw_[:, None, None] * eye_z)
-            if nz:
+            def chol(dw_):
+                Lf, inf_ = torch.linalg.cholesky_ex(Hr + dw_[:, None, None] * eye_z)
                 inf_ = torch.where((inf_ == 0) & ((Lf.diagonal(dim1=1, dim2=2) ** 2).amin(1) <= piv_tol),
                                    torch.ones_like(inf_), inf_)
-            return Lf, inf_
+                return Lf, inf_
 
-        delta_w = zeros_B.clone()
-        L1, info1 = chol(delta_w)
-        for _ in range(64):
-            bad = info1 != 0
-            if not bool(bad.any()):
-                break
-            first_dw = torch.where(dwl == 0, torch.full_like(delta_w, 1e-4), torch.clamp(dwl / 3.0, min=1e-20))
-            grow = delta_w * torch.where(dwl == 0, 100.0, 8.0)
-            delta_w = torch.where(bad, torch.where(delta_w == 0, first_dw, grow), delta_w)
-            L1n, info1n = chol(delta_w)
-            L1 = torch.where(bad[:, None, None], L1n, L1)
-            info1 = torch.where(bad, info1n, info1)
+            delta_w = zeros_B.clone()
+            L1, info1 = chol(delta_w)
+            for _ in range(64):
+                bad = info1 != 0
+                if not bool(bad.any()):
+                    break
+                first_dw = torch.where(dwl == 0, torch.full_like(delta_w, 1e-4), torch.clamp(dwl / 3.0, min=1e-20))
+                grow = delta_w * torch.where(dwl == 0, 100.0, 8.0)
+                delta_w = torch.where(bad, torch.where(delta_w == 0, first_dw, grow), delta_w)
+                L1n, info1n = chol(delta_w)
+                L1 = torch.where(bad[:, None, None], L1n, L1)
+                info1 = torch.where(bad, info1n, info1)
+        else:
+            delta_w, L1 = zeros_B.clone(), None
         Mw = M + delta_w[:, None, None] * eye_w
 
         def solve(q1, q2):
@@ -425,8 +497,19 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         dw, dy = refined(r1, r2)
         return dw, dy, delta_w, lambda r2v, mask=None: refined(r1, r2v)[0]
 
-    kkt = kkt_host
-
+    def kkt_qd(W, A, Dinv, r1, r2, dwl, mask):
+        """The restoration phase's Newton system after p and n are eliminated (as IPOPT's
+        AugRestoSystemSolver reduces it): [[W, A^T], [A, -D]] [dw; dy] = [r1; r2], D = 1 / Dinv > 0
+        diagonal.  The primal Schur complement K = W + A^T Dinv A is factorised with the inertia
+        correction (the full system has the right inertia iff K is positive definite);
+        dw = K^-1 (r1 + A^T Dinv r2), dy = Dinv (A dw - r2)."""
+        K = W + A.transpose(1, 2) @ (Dinv[:, :, None] * A)
+        K = 0.5 * (K + K.transpose(1, 2))
+        L1, delta_w = chol_inertia(K, dwl, mask)
+        rhs = r1 + (A.transpose(1, 2) @ (Dinv * r2).unsqueeze(2)).squeeze(2)
+        dw = torch.cholesky_solve(rhs.unsqueeze(2), L1).squeeze(2)
+        dy = Dinv * ((A @ dw.unsqueeze(2)).squeeze(2) - r2)
+        return dw, dy, delta_w
 
     def errors(o, wv, yv, zl, zu):
         A_ = jac_w(o["J"])
@@ -442,23 +525,68 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         d_inf = dual.abs().amax(1)
         c_inf = c_.abs().amax(1) if m else zeros_B
         base = torch.maximum(d_inf / sd, c_inf)
-        return {"A": A_, "gw": gw, "c": c_, "d_inf": d_inf, "base": base, "cl": cl, "cu": cu, "sc": sc,
-                "err0": torch.maximum(base, torch.maximum(cl.amax(1), cu.amax(1)) / sc)}
+        return {"A": A_, "gw": gw, "c": c_, "d_inf": d_inf, "c_inf": c_inf, "base": base, "cl": cl, "cu": cu,
+                "sc": sc, "err0": torch.maximum(base, torch.maximum(cl.amax(1), cu.amax(1)) / sc)}
 
     def err_mu(E, muv):
         comp_mu = torch.maximum((E["cl"] - torch.where(hasL, muv[:, None], 0.0)).abs().amax(1),
                                 (E["cu"] - torch.where(hasU, muv[:, None], 0.0)).abs().amax(1))
         return torch.maximum(E["base"], comp_mu / E["sc"])
 
+    def pd_error(o, wv, yv, zl, zu, muv):
+        """IPOPT's primal-dual system error of the barrier problem (1-norms of the dual residual, the
+        constraint residual and the mu-complementarity; the soft restoration phase's measure)."""
+        A_ = jac_w(o["J"])
+        gw = torch.cat([o["grad"][:, free], zeros_I], 1)
+        dual = gw + (A_.transpose(1, 2) @ yv.unsqueeze(2)).squeeze(2) - zl + zu
+        c_ = cons(o["g"], wv[:, nf:])
+        cl = torch.where(hasL, (wv - wl0) * zl - muv[:, None], torch.zeros_like(wv))
+        cu = torch.where(hasU, (wu0 - wv) * zu - muv[:, None], torch.zeros_like(wv))
+        return dual.abs().sum(1) + c_.abs().sum(1) + cl.abs().sum(1) + cu.abs().sum(1)
+
     def reset_filter(mask, ft, fp, fc):
         return (torch.where(mask[:, None], torch.full_like(ft, float("inf")), ft),
                 torch.where(mask[:, None], torch.full_like(fp, float("inf")), fp),
                 torch.where(mask, torch.zeros_like(fc), fc))
 
+    def augment_filter(mask, ft, fp, fc, th, ph):
+        """IPOPT's AugmentFilter: the entry ((1 - gamma_theta) theta, phi - gamma_phi theta) into the ring."""
+        fi = fslot == torch.remainder(fc, FMAX)[:, None]
+        ft = torch.where(mask[:, None] & fi, ((1.0 - GAMMA_TH) * th)[:, None], ft)
+        fp = torch.where(mask[:, None] & fi, (ph - GAMMA_PHI * th)[:, None], fp)
+        return ft, fp, fc + mask.to(fc.dtype)
+
     def max_step(v, dv, lo_mask, lo, tau):
         r = torch.where(lo_mask & (dv < 0), -tau[:, None] * (v - lo) / torch.where(dv < 0, dv, -1.0),
                         torch.full_like(v, float("inf")))
         return torch.clamp(r.amin(1), max=1.0)
+
+    def alpha_min_of(theta_k, gd, theta_min):
+        """IPOPT FilterLSAcceptor::CalculateAlphaMin: the smallest trial step before the line search
+        gives up (alpha_min_frac 0.05)."""
+        ngd = torch.where(gd < 0, -gd, torch.ones_like(gd))
+        a = torch.minimum(torch.full_like(gd, GAMMA_TH), GAMMA_PHI * theta_k / ngd)
+        a = torch.where(theta_k <= theta_min, torch.minimum(a, DELTA_SW * theta_k ** S_TH / ngd ** S_PHI), a)
+        return ALPHA_MIN_FRAC * torch.where(gd < 0, a, torch.full_like(gd, GAMMA_TH))
+
+    def acceptable(th, ph, theta_k, phi_k, gd, al, switch_ok, theta_max, ft, fp, from_resto=False):
+        """IPOPT FilterLSAcceptor::CheckAcceptabilityOfTrialPoint: theta_max, then Armijo on the
+        barrier objective for an f-type step (switching condition, theta_k <= theta_min) or the
+        sufficient decrease of theta or phi against the current iterate (with the obj_max_inc guard),
+        then the filter (entries stored with their margins).  Returns (ok, h_type)."""
+        fin = torch.isfinite(ph) & torch.isfinite(th)
+        in_filter = ((th[:, None] <= ft) | (ph[:, None] <= fp)).all(1)
+        ftype = switch_ok & (al * torch.where(gd < 0, -gd, torch.zeros_like(gd)) ** S_PHI > DELTA_SW * theta_k ** S_TH)
+        armijo = ph <= phi_k + ETA_PHI * al * gd
+        suff = (th <= (1.0 - GAMMA_TH) * theta_k) | (ph <= phi_k - GAMMA_PHI * theta_k)
+        if not from_resto:  # obj_max_inc = 5: the barrier objective may not jump by 5 orders of magnitude
+            base = torch.where(phi_k.abs() > 10.0, torch.log10(phi_k.abs().clamp(min=1e-300)), torch.ones_like(phi_k))
+            inc = ph - phi_k
+            big = (inc > 0) & (torch.log10(inc.clamp(min=1e-300)) > OBJ_MAX_INC + base)
+            suff = suff & ~big
+            armijo = armijo & ~big
+        ok = fin & (th <= theta_max) & in_filter & torch.where(ftype, armijo, suff)
+        return ok, ~(ftype & armijo)
 
     # ---- starting point: x pushed into its bounds, slacks = g_I(x) pushed into theirs
     Xs = unpack(push(torch.cat([Xbase[:, free], zeros_I], 1)))
@@ -476,7 +604,11 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     y0 = -torch.cholesky_solve(A0 @ (gw0 - zL0 + zU0).unsqueeze(2), L0).squeeze(2)
     y0 = torch.where(((y0.abs().amax(1) <= 1e3) & (info0 == 0)).unsqueeze(1), y0, torch.zeros_like(y0))
 
-    # persistent state: the (captured) iteration reads these and writes them back in place
+    zB = lambda: zeros_B.clone()  # noqa: E731
+    zBm = lambda: torch.zeros(B, m, dtype=dt, device=dev)  # noqa: E731
+    zBw = lambda: torch.zeros(B, nw, dtype=dt, device=dev)  # noqa: E731
+    bool_B = lambda: torch.zeros(B, dtype=torch.bool, device=dev)  # noqa: E731
+    # persistent state: the iteration reads these and writes them back in place
     S = {
         "w": w0.contiguous(), "y": y0.contiguous(), "zL": zL0, "zU": zU0,
         "mu": torch.full((B,), mu_init, dtype=dt, device=dev),
@@ -487,45 +619,63 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         "filt_t": torch.full((B, FMAX), float("inf"), dtype=dt, device=dev),
         "filt_p": torch.full((B, FMAX), float("inf"), dtype=dt, device=dev),
         "fcount": torch.zeros(B, dtype=torch.int64, device=dev),
-        "dwl": zeros_B.clone(),
+        "dwl": zB(),
         "f": cur0["f"].clone(), "grad": cur0["grad"].clone(), "g": cur0["g"].clone(), "J": cur0["J"].clone(),
-        "d_inf": zeros_B.clone(),
+        "d_inf": zB(),
+        "tiny_last": bool_B(), "tiny_flag": bool_B(),
+        "in_soft": bool_B(), "soft_cnt": torch.zeros(B, dtype=torch.int64, device=dev),
         "Hq": eye_f.repeat(B, 1, 1) if use_bfgs else None,
         "lm_s": torch.zeros(B, LM_HIST, nf, dtype=dt, device=dev) if use_bfgs else None,
         "lm_y": torch.zeros(B, LM_HIST, nf, dtype=dt, device=dev) if use_bfgs else None,
         "lm_cnt": torch.zeros(B, dtype=torch.int64, device=dev),
         "lm_skip": torch.zeros(B, dtype=torch.int64, device=dev),
+        # restoration phase (IPOPT's MinC_1NrmRestorationPhase): per instance, a second interior-point
+        # problem in the same lock-step iteration
+        "resto": bool_B(), "wR": zBw(), "p": zBm(), "n": zBm(), "zp": zBm(), "zn": zBm(), "zLR": zBw(),
+        "zUR": zBw(), "muR": zB(), "ftR": torch.full((B, FMAX), float("inf"), dtype=dt, device=dev),
+        "fpR": torch.full((B, FMAX), float("inf"), dtype=dt, device=dev),
+        "fcR": torch.zeros(B, dtype=torch.int64, device=dev), "th_o0": zB(), "ph_o0": zB(), "dwlR": zB(),
+        "thmaxR": zB(), "thminR": zB(), "n_resto": torch.zeros(B, dtype=torch.int64, device=dev),
     }
 
-    def check(E):
-        """Convergence test at the current iterate; updates status / active / acc; returns active."""
+    def check(E, mask):
+        """Convergence test at the current iterate of the instances in `mask`; updates status /
+        active / acc."""
         active = S["active"]
         e0 = E["err0"]
-        done_now = active & (e0 <= tol)
-        acc = torch.where(active & (e0 <= acceptable_tol), S["acc"] + 1, torch.zeros_like(S["acc"]))
-        acc_now = active & ~done_now & (acc >= acceptable_iter)
+        act = active & mask
+        done_now = act & (e0 <= tol)
+        acc = torch.where(act & (e0 <= acceptable_tol), S["acc"] + 1, torch.where(act, 0, S["acc"]))
+        acc_now = act & ~done_now & (acc >= acceptable_iter)
         status = torch.where(done_now, torch.full_like(S["status"], STATUS_OPTIMAL),
                              torch.where(acc_now, torch.full_like(S["status"], STATUS_ACCEPTABLE), S["status"]))
-        active = active & ~done_now & ~acc_now
         S["acc"].copy_(acc)
         S["status"].copy_(status)
-        S["active"].copy_(active)
-        S["d_inf"].copy_(E["d_inf"])
-        return active
+        S["active"].copy_(active & ~done_now & ~acc_now)
+        S["d_inf"].copy_(torch.where(mask, E["d_inf"], S["d_inf"]))
 
-    def lbfgs_update(active, sk, new, cur, y_new, failed):
+    def lbfgs_reset(mask):
+        if use_bfgs:
+            S["lm_skip"].copy_(torch.where(mask, 0, S["lm_skip"]))
+            S["lm_cnt"].copy_(torch.where(mask, 0, S["lm_cnt"]))
+            S["Hq"].copy_(torch.where(mask[:, None, None], eye_f.expand_as(S["Hq"]), S["Hq"]))
+
+    def lbfgs_update(active, sk, new, cur, y_new, with_grad=True):
         """IPOPT's LimMemQuasiNewtonUpdater with IFOPT's defaults (bfgs, max_history 6, scalar1,
-        init_val 1 in [1e-8, 1e8], max_skipping 2) — the device's k_lbfgs (csrc/cpl_solver.hip); a failed
-        line search (the feasibility step, our restoration stand-in, was taken) restarts the model."""
+        init_val 1 in [1e-8, 1e8], max_skipping 2) — the device's k_lbfgs (csrc/cpl_solver.hip).
+        with_grad False: the pair from J^T y alone (the restoration phase's model of its
+        constraint curvature; its proximity term's Hessian is exact and added separately)."""
         JTy_new = (new["J"].transpose(1, 2) @ y_new.unsqueeze(2)).squeeze(2)
         JTy_old = (cur["J"].transpose(1, 2) @ y_new.unsqueeze(2)).squeeze(2)
-        yk = (new["grad"] + JTy_new)[:, free] - (cur["grad"] + JTy_old)[:, free]
+        if with_grad:
+            yk = (new["grad"] + JTy_new)[:, free] - (cur["grad"] + JTy_old)[:, free]
+        else:
+            yk = (0.0 + JTy_new)[:, free] - (0.0 + JTy_old)[:, free]
         sy, ss, yy = (sk * yk).sum(1), (sk * sk).sum(1), (yk * yk).sum(1)
         take = active & (sy > math.sqrt(EPS) * ss.sqrt() * yy.sqrt())
         skip = active & ~take
         skipped = torch.where(skip, S["lm_skip"] + 1, torch.zeros_like(S["lm_skip"]))
-        reset = (skip & (skipped > LM_MAX_SKIP)) | (active & failed)
-        take = take & ~reset
+        reset = skip & (skipped > LM_MAX_SKIP)
         S["lm_skip"].copy_(torch.where(active, torch.where(reset, torch.zeros_like(skipped), skipped), S["lm_skip"]))
         # memory: a full one shifts down by one (the oldest pair dropped), the new pair appended
         cnt = S["lm_cnt"]
@@ -556,32 +706,44 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         Hq = torch.where(take[:, None, None], H, S["Hq"])
         S["Hq"].copy_(torch.where(reset[:, None, None], eye_f.expand_as(Hq), Hq))
 
-    def step():
-        """One lock-step iteration of every instance; no host synchronisation (graph-capturable)."""
-        w, y, zL, zU, mu = S["w"], S["y"], S["zL"], S["zU"], S["mu"]
+    def trial_ls(wv, d, al, mask, st):
+        """A trial point w + al d for the instances in mask (others: their line-search state's point)."""
+        wt_ = wv + al[:, None] * d
+        return wt_, evaluate_fg(unpack(torch.where(mask[:, None], wt_, st["w"])))
+
+    def take(st, mask, wt, o, al, aug_mask, extra=None):
+        st["f"] = torch.where(mask, o["f"], st["f"])
+        st["g"] = torch.where(mask[:, None], o["g"], st["g"])
+        st["w"] = torch.where(mask[:, None], wt, st["w"])
+        st["alpha"] = torch.where(mask, al, st["alpha"])
+        st["aug"] = torch.where(mask, aug_mask, st["aug"])
+        st["found"] = st["found"] | mask
+        st["searching"] = st["searching"] & ~mask
+        if extra is not None:
+            for k, v in extra.items():
+                st[k] = torch.where(mask.view(-1, *([1] * (v.dim() - 1))), v, st[k])
+
+    # ------------------------------------------------------------------------------------------
+    def regular_step(E, act):
+        """One IPOPT iteration of the instances in `act` (not in the restoration phase)."""
+        w, y, zL, zU, mu = S["w"], S["y"], S["zL"], S["zU"], S["mu"].clone()
         cur = {"f": S["f"], "grad": S["grad"], "g": S["g"], "J": S["J"]}
-        E = errors(cur, w, y, zL, zU)
-        active = check(E).clone()
         A, gradw, c = E["A"], E["gw"], E["c"]
-        # ---- monotone barrier update (two rounds per iteration), filter reset where mu changed
+        # ---- monotone barrier update (IPOPT MonotoneMuUpdate with mu_allow_fast_monotone_decrease: as
+        # long as the barrier problem is solved to kappa_eps mu, or once after two tiny steps), the
+        # filter reset where mu changed
         ft, fp, fc = S["filt_t"], S["filt_p"], S["fcount"]
-        for _ in range(2):
-            upd = active & (err_mu(E, mu) <= 10.0 * mu) & (mu > tol / 10.0)
-            mu = torch.where(upd, torch.clamp(torch.minimum(0.2 * mu, mu ** 1.5), min=tol / 10.0), mu)
+        force = S["tiny_flag"] & act
+        for r in range(MU_ROUNDS):
+            upd = act & ((err_mu(E, mu) <= BARRIER_TOL_FACTOR * mu) | (force if r == 0 else False)) & (mu > mu_min)
+            mu = torch.where(upd, torch.clamp(torch.minimum(0.2 * mu, mu ** 1.5), min=mu_min), mu)
             ft, fp, fc = reset_filter(upd, ft, fp, fc)
         tau = torch.clamp(1.0 - mu, min=0.99)
 
         def primal_step(d):  # fraction to the boundary along d from w
             return torch.minimum(max_step(w, d, hasL, wl0, tau), max_step(-w, -d, hasU, -wu0, tau))
 
-        if use_bfgs:
-            Hblk = S["Hq"]
-        else:
-            # host path: the evaluator's own analytic Hessian when it has one (the oracle's restatement
-            # of cpl_lagrangian_hessian, so the CPU solve takes the device's exact-Hessian steps)
-            Hblk = ev.hessian(unpack(w), y, free) if (hessian == "exact" and hasattr(ev, "hessian")) else None
-            if Hblk is None:
-                Hblk = fd_hessian(unpack(w), y)
+        Hblk = S["Hq"] if use_bfgs else hessian_blk(w, y)
         dl = torch.where(hasL, w - wl0, torch.ones_like(w))
         du = torch.where(hasU, wu0 - w, torch.ones_like(w))
         Sig = torch.where(hasL, zL / dl, torch.zeros_like(w)) + torch.where(hasU, zU / du, torch.zeros_like(w))
@@ -591,135 +753,403 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         r2 = -c
         M = torch.diag_embed(Sig)
         M[:, :nf, :nf] += Hblk
-        mr_diag = Sig + mu.sqrt()[:, None] * torch.clamp(w.abs(), min=1.0) ** -2
         theta_k = c.abs().sum(1)
         phi_k = cur["f"] + barrier(w, mu)
-        dw, dy, delta_w, solve_primal = kkt(M, A, r1, r2, mu, S["dwl"], active)
-        dwl = torch.where(active, delta_w, S["dwl"])
+        dw, dy, delta_w, solve_primal = kkt_host(M, A, r1, r2, mu, S["dwl"], act)
+        dwl = torch.where(act, delta_w, S["dwl"])
         dzL = torch.where(hasL, mu[:, None] / dl - zL - zL / dl * dw, torch.zeros_like(w))
         dzU = torch.where(hasU, mu[:, None] / du - zU + zU / du * dw, torch.zeros_like(w))
         a_max = primal_step(dw)
         a_z = torch.minimum(max_step(zL, dzL, hasL, 0.0, tau), max_step(zU, dzU, hasU, 0.0, tau))
         gd = (gphi * dw).sum(1)
         switch_ok = (theta_k <= theta_min) & (gd < 0)
+        # IPOPT DetectTinyStep: the step is below 10 eps relative in every primal component, the
+        # multiplier step below 1e-2, the point feasible to 1e-4: taken whole without a line search;
+        # two in a row force the next barrier decrease
+        tiny = act & ((dw.abs() / (1.0 + w.abs())).amax(1) < TINY_STEP_TOL) & \
+            (dy.abs().amax(1) < TINY_STEP_Y_TOL) & (E["c_inf"] < 1e-4)
+        S["tiny_flag"].copy_(torch.where(act, tiny & S["tiny_last"], S["tiny_flag"]))
+        S["tiny_last"].copy_(torch.where(act, tiny & ~S["tiny_last"], S["tiny_last"]))
+        a_min = alpha_min_of(theta_k, gd, theta_min)
+        soft_now = act & S["in_soft"] & ~tiny
 
-        # ---- filter line search (IPOPT: gamma_theta 1e-5, gamma_phi 1e-8, delta 1, s_theta 1.1,
-        # s_phi 2.3, eta_phi 1e-8, theta_min/max = 1e-4/1e4 max(1, theta_0)), second-order
-        # corrections on the first trial; fixed trip counts, masked acceptance
-        # line-search state (fresh tensors: the device path updates them in place)
-        st = {"searching": active.clone(), "f": cur["f"].clone(), "g": cur["g"].clone(), "w": w.clone(),
-              "alpha": zeros_B.clone(), "aug": torch.zeros(B, dtype=torch.bool, device=dev)}
+        # ---- IPOPT's backtracking filter line search: trials alpha_max, alpha_max / 2, ... while
+        # alpha > alpha_min (at most max_ls), up to max_soc second-order corrections on the first;
+        # in IPOPT's soft restoration phase the backtracking is skipped: only the full primal-dual
+        # step is tried (at most max_soft_resto_iters iterations in a row)
+        S["soft_cnt"].copy_(S["soft_cnt"] + soft_now.to(torch.int64))
+        st = {"searching": act & ~tiny & ~soft_now, "found": bool_B(), "f": cur["f"].clone(),
+              "g": cur["g"].clone(), "w": w.clone(), "alpha": zB(), "aug": bool_B()}
 
-        def judge(wt, o, al):  # o: {"f", "g"} at the trial points
-            th = cons(o["g"], wt[:, nf:]).abs().sum(1)
-            ph = o["f"] + barrier(wt, mu)
-            fin = torch.isfinite(ph) & torch.isfinite(th)
-            in_filter = ((th[:, None] <= (1.0 - 1e-5) * ft) | (ph[:, None] <= fp - 1e-8 * ft)).all(1)
-            ftype = switch_ok & (al * (-gd).clamp(min=0.0) ** 2.3 > theta_k ** 1.1)
-            armijo = ph <= phi_k + 1e-8 * al * gd
-            suff = (th <= (1.0 - 1e-5) * theta_k) | (ph <= phi_k - 1e-8 * theta_k)
-            ok = fin & (th <= theta_max) & in_filter & torch.where(ftype, armijo, suff)
-            return ok, ~(ftype & armijo), th
-
-        def take(mask, wt, o, al, aug_mask):
-            st["f"] = torch.where(mask, o["f"], st["f"])
-            st["g"] = torch.where(mask[:, None], o["g"], st["g"])
-            st["w"] = torch.where(mask[:, None], wt, st["w"])
-            st["alpha"] = torch.where(mask, al, st["alpha"])
-            st["aug"] = torch.where(mask, aug_mask, st["aug"])
-            st["searching"] = st["searching"] & ~mask
-
-        def trial(d, al, mask):
-            wt_ = w + al[:, None] * d
-            return wt_, evaluate_fg(unpack(torch.where(mask[:, None], wt_, st["w"])))
-
-        def judge_take(wt_, o_, al, extra=None):
-            ok_, augm_, th_ = judge(wt_, o_, al)
-            take(st["searching"] & ok_ & (True if extra is None else extra), wt_, o_, al, augm_)
+        def judge_take(wt_, o_, al, extra_mask=None):
+            th_ = cons(o_["g"], wt_[:, nf:]).abs().sum(1)
+            ph_ = o_["f"] + barrier(wt_, mu)
+            ok_, h_ = acceptable(th_, ph_, theta_k, phi_k, gd, al, switch_ok, theta_max, ft, fp)
+            sel = st["searching"] & ok_
+            if extra_mask is not None:
+                sel = sel & extra_mask
+            take(st, sel, wt_, o_, al, h_)
             return ok_, th_
 
-        alpha = a_max
-        wt, o = w, cur
+        alpha = a_max.clone()
         for ls in range(max(1, max_ls)):
-            wt, o = trial(dw, alpha, st["searching"])
+            if not bool(st["searching"].any()):
+                break
+            wt, o = trial_ls(w, dw, alpha, st["searching"], st)
             ok, th = judge_take(wt, o, alpha)
-            if ls == 0 and max_soc > 0:
-                soc = st["searching"] & (th >= theta_k)
-                c_soc, a_soc, th_old = c, alpha, theta_k
-                ct = cons(o["g"], wt[:, nf:])
-                for _ in range(max_soc):
-                    c_soc = a_soc[:, None] * c_soc + ct
-                    dws = solve_primal(-c_soc, soc)  # only the instances that try a correction
-                    a_soc = primal_step(dws)
-                    ws, os_ = trial(dws, a_soc, soc)
-                    oks, ths = judge_take(ws, os_, alpha, soc)
-                    soc = soc & ~oks & (ths <= 0.99 * th_old)  # kappa_soc = 0.99
-                    th_old = ths
-                    ct = cons(os_["g"], ws[:, nf:])
+            if ls == 0:
+                if max_soc > 0:
+                    soc = st["searching"] & (th >= theta_k)
+                    c_soc, a_soc, th_old = c, alpha, th
+                    ct = cons(o["g"], wt[:, nf:])
+                    for _ in range(max_soc):
+                        if not bool(soc.any()):
+                            break
+                        c_soc = a_soc[:, None] * c_soc + ct
+                        dws = solve_primal(-c_soc, soc)
+                        a_soc = primal_step(dws)
+                        ws, os_ = trial_ls(w, dws, a_soc, soc, st)
+                        oks, ths = judge_take(ws, os_, alpha, soc)
+                        soc = soc & ~oks & (ths <= KAPPA_SOC * th_old)  # kappa_soc = 0.99
+                        th_old = ths
+                        ct = cons(os_["g"], ws[:, nf:])
             alpha = torch.where(st["searching"], 0.5 * alpha, alpha)
-        # no acceptable trial: a feasibility step stands in for IPOPT's restoration phase —
-        # min 1/2 dw^T (Sigma + sqrt(mu) D_R^2) dw s.t. A dw = -c (D_R = diag(1 / max(1, |w|)),
-        # IPOPT's restoration proximity weight), fraction to the boundary, taken when it cuts the
-        # violation by 10 %; the multipliers stay.  Otherwise the last trial.  Either way the
-        # instance's filter restarts.  (The KKT kernel skips the instances outside the mask.)
-        failed = st["searching"].clone()
-        Mr = torch.diag_embed(mr_diag)
-        dwr = kkt(Mr, A, torch.zeros_like(w), -c, mu, zeros_B, failed)[0]
-        ar = primal_step(dwr)
-        wr, orr = trial(dwr, ar, failed)
-        thr = cons(orr["g"], wr[:, nf:]).abs().sum(1)
-        rest = failed & torch.isfinite(thr) & torch.isfinite(orr["f"]) & (thr <= 0.9 * theta_k)
-        take(rest, wr, orr, zeros_B, torch.zeros_like(failed))
-        take(st["searching"], wt, o, 2.0 * alpha, torch.zeros_like(failed))
+            st["searching"] = st["searching"] & (alpha > a_min)  # IPOPT: the next trial only above alpha_min
+        # tiny steps: the whole fraction-to-the-boundary step
+        w_tiny = w + a_max[:, None] * dw
+        st["w"] = torch.where(tiny[:, None], w_tiny, st["w"])
+        st["alpha"] = torch.where(tiny, a_max, st["alpha"])
+        # ---- IPOPT's soft restoration step (TrySoftRestoStep): when the backtracking failed (or in the
+        # soft restoration phase) the full primal-dual step alpha = min(alpha_primal_max, alpha_dual_max)
+        # for every variable, taken when the original filter / current iterate accept it, or when it
+        # cuts the primal-dual error of the barrier problem (1-norms) by soft_resto_pderror_reduction_factor
+        bt_failed = act & ~tiny & ~soft_now & ~st["found"]
+        soft_try = (soft_now & (S["soft_cnt"] <= MAX_SOFT_RESTO)) | bt_failed
+        a_soft = torch.minimum(a_max, a_z)
+        soft_ok = bool_B()
+        if bool(soft_try.any()):
+            ws = w + a_soft[:, None] * dw
+            os_ = evaluate(unpack(torch.where(soft_try[:, None], ws, w)))
+            th_s = cons(os_["g"], ws[:, nf:]).abs().sum(1)
+            ph_s = os_["f"] + barrier(ws, mu)
+            orig_ok, _ = acceptable(th_s, ph_s, theta_k, phi_k, gd, zB(), switch_ok, theta_max, ft, fp)
+            ys = y + a_soft[:, None] * dy
+            zLs = torch.where(hasL, zL + a_soft[:, None] * dzL, zL)
+            zUs = torch.where(hasU, zU + a_soft[:, None] * dzU, zU)
+            fin_s = torch.isfinite(th_s) & torch.isfinite(ph_s)
+            better = pd_error(os_, ws, ys, zLs, zUs, mu) <= SOFT_RESTO_FACTOR * pd_error(cur, w, y, zL, zU, mu)
+            soft_ok = soft_try & fin_s & (orig_ok | better)
+            take(st, soft_ok, ws, os_, a_soft, bool_B())
+            left = soft_ok & orig_ok  # the original criterion holds: the soft phase ends
+            S["in_soft"].copy_(torch.where(left, False, torch.where(soft_ok, True, S["in_soft"])))
+            S["soft_cnt"].copy_(torch.where(left | (soft_ok & ~soft_now), 0, S["soft_cnt"]))
+        failed = act & ~tiny & ~st["found"]  # -> the restoration phase
+        S["in_soft"].copy_(S["in_soft"] & ~failed)
+        S["soft_cnt"].copy_(torch.where(failed, 0, S["soft_cnt"]))
+        moved = act & ~failed
         w_new = st["w"]
         al = st["alpha"]
+        a_z = torch.where(soft_ok, a_soft, a_z)  # the soft step moves the bound multipliers by alpha too
         # the accepted points with their derivatives: one full evaluation (trials carried f and g only)
         new = evaluate(unpack(w_new))
-        a_z = torch.where(rest, zeros_B, a_z)
-        addm = st["aug"] & active
-        fi = fslot == torch.remainder(fc, FMAX)[:, None]
-        ft = torch.where(addm[:, None] & fi, ((1.0 - 1e-5) * theta_k)[:, None], ft)
-        fp = torch.where(addm[:, None] & fi, (phi_k - 1e-8 * theta_k)[:, None], fp)
-        fc = fc + addm.to(fc.dtype)
-        ft, fp, fc = reset_filter(failed, ft, fp, fc)
+        addm = st["aug"] & moved
+        ft, fp, fc = augment_filter(addm, ft, fp, fc, theta_k, phi_k)
 
         # ---- accept: primal, multipliers, bound multipliers (kappa_Sigma safeguard)
-        act = active[:, None]
-        y_new = torch.where(act, y + al[:, None] * dy, y)
-        zL_new = torch.where(act & hasL, zL + a_z[:, None] * dzL, zL)
-        zU_new = torch.where(act & hasU, zU + a_z[:, None] * dzU, zU)
+        mv = moved[:, None]
+        y_new = torch.where(mv, y + al[:, None] * dy, y)
+        zL_new = torch.where(mv & hasL, zL + a_z[:, None] * dzL, zL)
+        zU_new = torch.where(mv & hasU, zU + a_z[:, None] * dzU, zU)
         dln = torch.where(hasL, w_new - wl0, torch.ones_like(w))
         dun = torch.where(hasU, wu0 - w_new, torch.ones_like(w))
-        zL_new = torch.where(act & hasL, torch.minimum(torch.maximum(zL_new, mu[:, None] / (1e10 * dln)),
-                                                       1e10 * mu[:, None] / dln), zL_new)
-        zU_new = torch.where(act & hasU, torch.minimum(torch.maximum(zU_new, mu[:, None] / (1e10 * dun)),
-                                                       1e10 * mu[:, None] / dun), zU_new)
-
+        zL_new = torch.where(mv & hasL, torch.minimum(torch.maximum(zL_new, mu[:, None] / (KAPPA_SIGMA * dln)),
+                                                      KAPPA_SIGMA * mu[:, None] / dln), zL_new)
+        zU_new = torch.where(mv & hasU, torch.minimum(torch.maximum(zU_new, mu[:, None] / (KAPPA_SIGMA * dun)),
+                                                      KAPPA_SIGMA * mu[:, None] / dun), zU_new)
         if use_bfgs:  # IPOPT's limited-memory BFGS over x_free (both Lagrangian gradients at the new y)
-            lbfgs_update(active, (w_new - w)[:, :nf], new, cur, y_new, failed)
+            lbfgs_update(moved, (w_new - w)[:, :nf], new, cur, y_new)
 
-        # ---- write the state back in place
-        S["w"].copy_(torch.where(act, w_new, w))
-        S["y"].copy_(y_new)
+        # ---- the restoration phase starts where the line search failed (IPOPT: PrepareRestoPhaseStart
+        # augments the filter with the current point; MinC_1NrmRestorationPhase / RestoIterateInitializer)
+        ft, fp, fc = augment_filter(failed, ft, fp, fc, theta_k, phi_k)
+        if bool(failed.any()):
+            enter_resto(failed, w, mu, c, A, zL, zU, cur["f"])
+        S["w"].copy_(torch.where(mv, w_new, w))
+        S["y"].copy_(torch.where(failed[:, None], S["y"], y_new))
         S["zL"].copy_(zL_new)
         S["zU"].copy_(zU_new)
-        S["mu"].copy_(mu)
-        S["iters"].copy_(S["iters"] + active.to(torch.int64))
+        S["mu"].copy_(torch.where(act, mu, S["mu"]))
+        S["iters"].copy_(S["iters"] + act.to(torch.int64))
         S["filt_t"].copy_(ft)
         S["filt_p"].copy_(fp)
         S["fcount"].copy_(fc)
         S["dwl"].copy_(dwl)
         for k in ("f", "grad", "g", "J"):
-            S[k].copy_(torch.where(active.view(-1, *([1] * (S[k].dim() - 1))), new[k], S[k]))
+            S[k].copy_(torch.where(moved.view(-1, *([1] * (S[k].dim() - 1))), new[k], S[k]))
         if verbose > 1:
-            verbose_line(E, mu, a_max, al, dw, dy, delta_w, cur)
+            verbose_line(E, mu, a_max, al, dw, dy, delta_w, cur, failed)
 
-    def verbose_line(E, mu, a_max, al, dw, dy, delta_w, cur):
-        b = int(verbose) - 2
+
+    def enter_resto(mask, w, mu, c, A, zL, zU, f0):
+        """RestoIterateInitializer: x_R = the current point, D_R = diag(1 / max(1, |x_R|)),
+        mu_R = max(mu, |c|_inf), p / n from the closed form of the barrier subproblem at fixed x
+        (p - n = c, both positive), their bound multipliers mu_R / p, mu_R / n, the x-bound
+        multipliers min(rho, z), least-squares constraint multipliers (<= constr_mult_init_max),
+        an empty filter and a fresh quasi-Newton model."""
+        mk, mw, mm = mask, mask[:, None], mask[:, None]
+        c_inf = c.abs().amax(1) if m else zeros_B
+        muR = torch.maximum(mu, c_inf)
+        a = (muR[:, None] - RHO_R * c) / (2.0 * RHO_R)
+        nn = a + torch.sqrt(a * a + muR[:, None] * c / (2.0 * RHO_R))
+        pp = c + nn
+        zp = muR[:, None] / pp
+        zn = muR[:, None] / nn
+        zLR = torch.where(hasL, torch.clamp(zL, max=RHO_R), torch.zeros_like(zL))
+        zUR = torch.where(hasU, torch.clamp(zU, max=RHO_R), torch.zeros_like(zU))
+        # least-squares multipliers of the restoration problem (IPOPT's estimate with M = I over
+        # (w, p, n): the same p / n elimination as the Newton step, Sigma_p = Sigma_n = 1), kept when
+        # |y|max <= constr_mult_init_max = 1e3
+        _, yR, _ = kkt_qd(eye_w.expand(B, nw, nw), A, torch.full_like(c, 0.5), zLR - zUR, zp - zn, zeros_B, mask)
+        yR = torch.where((yR.abs().amax(1) <= 1e3).unsqueeze(1), yR, torch.zeros_like(yR))
+        thR0 = (c - pp + nn).abs().sum(1)
+        S["resto"].copy_(S["resto"] | mk)
+        S["n_resto"].copy_(S["n_resto"] + mk.to(torch.int64))
+        for k, v in (("wR", w), ("p", pp), ("n", nn), ("zp", zp), ("zn", zn), ("zLR", zLR), ("zUR", zUR)):
+            S[k].copy_(torch.where(mw, v, S[k]))
+        S["y"].copy_(torch.where(mm, yR, S["y"]))
+        S["muR"].copy_(torch.where(mk, muR, S["muR"]))
+        S["ftR"].copy_(torch.where(mw, float("inf"), S["ftR"]))
+        S["fpR"].copy_(torch.where(mw, float("inf"), S["fpR"]))
+        S["fcR"].copy_(torch.where(mk, 0, S["fcR"]))
+        S["thmaxR"].copy_(torch.where(mk, 1e4 * thR0.clamp(min=1.0), S["thmaxR"]))
+        S["thminR"].copy_(torch.where(mk, 1e-4 * thR0.clamp(min=1.0), S["thminR"]))
+        S["th_o0"].copy_(torch.where(mk, c.abs().sum(1), S["th_o0"]))
+        S["ph_o0"].copy_(torch.where(mk, f0 + barrier(w, mu), S["ph_o0"]))
+        S["dwlR"].copy_(torch.where(mk, 0.0, S["dwlR"]))
+        lbfgs_reset(mk)
+
+    def resto_step(actR):
+        """One iteration of the restoration phase (IPOPT's MinC_1NrmRestorationPhase: the same
+        interior-point method on  min rho sum(p + n) + eta/2 |D_R (x - x_R)|^2  s.t.  c(w) - p + n = 0,
+        w within its bounds, p, n >= 0, eta = sqrt(mu_R)) for the instances in actR; then the test
+        for the return to the regular iteration (RestoConvergenceCheck: the original infeasibility cut
+        to kappa_resto = 0.9 of its value at the start, the point acceptable to the original filter
+        and to the iterate where the phase began)."""
+        w, y, mu = S["w"], S["y"], S["mu"]
+        pp, nn, zp, zn, zLR, zUR, muR = S["p"], S["n"], S["zp"], S["zn"], S["zLR"], S["zUR"], S["muR"].clone()
+        cur = {"f": S["f"], "grad": S["grad"], "g": S["g"], "J": S["J"]}
+        A = jac_w(cur["J"])
+        c = cons(cur["g"], w[:, nf:])
+        DR2 = torch.where(xmask, 1.0 / torch.clamp(S["wR"].abs(), min=1.0) ** 2, torch.zeros_like(w))
+
+        def terms(muv):
+            eta = torch.sqrt(muv)
+            gfw = torch.where(xmask, eta[:, None] * DR2 * (w - S["wR"]), torch.zeros_like(w))
+            return eta, gfw
+
+        # ---- the restoration problem's optimality error: converged = a point of local infeasibility
+        cR = c - pp + nn
+        eta, gfw = terms(muR)
+        dual_w = gfw + (A.transpose(1, 2) @ y.unsqueeze(2)).squeeze(2) - zLR + zUR
+        d_inf = torch.maximum(dual_w.abs().amax(1), torch.maximum((RHO_R - y - zp).abs().amax(1),
+                                                                  (RHO_R + y - zn).abs().amax(1)))
+        cl = torch.where(hasL, (w - torch.where(hasL, wl0, 0.0)) * zLR, torch.zeros_like(w))
+        cu = torch.where(hasU, (torch.where(hasU, wu0, 0.0) - w) * zUR, torch.zeros_like(w))
+        cp, cn = pp * zp, nn * zn
+        nbR = nbounds + 2 * m
+        zsum = zLR.abs().sum(1) + zUR.abs().sum(1) + zp.abs().sum(1) + zn.abs().sum(1)
+        sd = torch.clamp((y.abs().sum(1) + zsum) / max(m + nbR, 1), min=100.0) / 100.0
+        sc = torch.clamp(zsum / max(nbR, 1), min=100.0) / 100.0
+        base = torch.maximum(d_inf / sd, cR.abs().amax(1))
+        cmax = torch.maximum(torch.maximum(cl.amax(1), cu.amax(1)), torch.maximum(cp.amax(1), cn.amax(1)))
+        errR0 = torch.maximum(base, cmax / sc)
+        conv = actR & (errR0 <= tol)
+        S["status"].copy_(torch.where(conv, STATUS_INFEASIBLE, S["status"]))
+        S["active"].copy_(S["active"] & ~conv)
+        actR = actR & ~conv
+
+        def errR_mu(muv):
+            cm = torch.maximum(
+                torch.maximum((cl - torch.where(hasL, muv[:, None], 0.0)).abs().amax(1),
+                              (cu - torch.where(hasU, muv[:, None], 0.0)).abs().amax(1)),
+                torch.maximum((cp - muv[:, None]).abs().amax(1), (cn - muv[:, None]).abs().amax(1)))
+            return torch.maximum(base, cm / sc)
+
+        ftR, fpR, fcR = S["ftR"], S["fpR"], S["fcR"]
+        for _ in range(MU_ROUNDS):
+            upd = actR & (errR_mu(muR) <= BARRIER_TOL_FACTOR * muR) & (muR > mu_min)
+            muR = torch.where(upd, torch.clamp(torch.minimum(0.2 * muR, muR ** 1.5), min=mu_min), muR)
+            ftR, fpR, fcR = reset_filter(upd, ftR, fpR, fcR)
+        tauR = torch.clamp(1.0 - muR, min=0.99)
+        eta, gfw = terms(muR)
+
+        def phiR(wv, pv, nv):
+            prox = torch.where(xmask, DR2 * (wv - S["wR"]) ** 2, torch.zeros_like(wv)).sum(1)
+            return RHO_R * (pv.sum(1) + nv.sum(1)) + 0.5 * eta * prox + barrier(wv, muR) - \
+                muR * (torch.log(pv).sum(1) + torch.log(nv).sum(1))
+
+        # ---- Newton step with p, n eliminated
+        if use_bfgs:
+            Hc = S["Hq"]
+        else:
+            Hc = hessian_blk(w, y, constraints_only=True)
+        dl = torch.where(hasL, w - wl0, torch.ones_like(w))
+        du = torch.where(hasU, wu0 - w, torch.ones_like(w))
+        Sig = torch.where(hasL, zLR / dl, torch.zeros_like(w)) + torch.where(hasU, zUR / du, torch.zeros_like(w))
+        gphi = gfw - torch.where(hasL, muR[:, None] / dl, torch.zeros_like(w)) + \
+            torch.where(hasU, muR[:, None] / du, torch.zeros_like(w))
+        r1 = -(gphi + (A.transpose(1, 2) @ y.unsqueeze(2)).squeeze(2))
+        Sp, Sn = zp / pp, zn / nn
+        rp = -((RHO_R - muR[:, None] / pp) - y)
+        rn = -((RHO_R - muR[:, None] / nn) + y)
+        Dinv = 1.0 / (1.0 / Sp + 1.0 / Sn)
+        r2 = -cR + rp / Sp - rn / Sn
+        W = torch.diag_embed(Sig + torch.where(xmask, eta[:, None] * DR2, torch.zeros_like(w)))
+        W[:, :nf, :nf] += Hc
+        dw, dy, dWR = kkt_qd(W, A, Dinv, r1, r2, S["dwlR"], actR)
+        S["dwlR"].copy_(torch.where(actR, dWR, S["dwlR"]))
+        dp = (rp + dy) / Sp
+        dn = (rn - dy) / Sn
+        dzL = torch.where(hasL, muR[:, None] / dl - zLR - zLR / dl * dw, torch.zeros_like(w))
+        dzU = torch.where(hasU, muR[:, None] / du - zUR + zUR / du * dw, torch.zeros_like(w))
+        dzp = muR[:, None] / pp - zp - zp / pp * dp
+        dzn = muR[:, None] / nn - zn - zn / nn * dn
+        allm = torch.ones(B, m, dtype=torch.bool, device=dev)
+        a_max = torch.minimum(torch.minimum(max_step(w, dw, hasL, wl0, tauR), max_step(-w, -dw, hasU, -wu0, tauR)),
+                              torch.minimum(max_step(pp, dp, allm, 0.0, tauR), max_step(nn, dn, allm, 0.0, tauR)))
+        a_z = torch.minimum(torch.minimum(max_step(zLR, dzL, hasL, 0.0, tauR), max_step(zUR, dzU, hasU, 0.0, tauR)),
+                            torch.minimum(max_step(zp, dzp, allm, 0.0, tauR), max_step(zn, dzn, allm, 0.0, tauR)))
+        gd = (gphi * dw).sum(1) + ((RHO_R - muR[:, None] / pp) * dp).sum(1) + ((RHO_R - muR[:, None] / nn) * dn).sum(1)
+        thetaR = cR.abs().sum(1)
+        phR_k = phiR(w, pp, nn)
+        switch_ok = (thetaR <= S["thminR"]) & (gd < 0)
+        a_min = alpha_min_of(thetaR, gd, S["thminR"])
+
+        # ---- filter line search on the restoration problem (no second-order correction)
+        st = {"searching": actR.clone(), "found": bool_B(), "f": cur["f"].clone(), "g": cur["g"].clone(),
+              "w": w.clone(), "alpha": zB(), "aug": bool_B(), "p": pp.clone(), "n": nn.clone()}
+        alpha = a_max.clone()
+        for ls in range(max(1, max_ls)):
+            if not bool(st["searching"].any()):
+                break
+            wt, o = trial_ls(w, dw, alpha, st["searching"], st)
+            pt = pp + alpha[:, None] * dp
+            nt = nn + alpha[:, None] * dn
+            th_t = (cons(o["g"], wt[:, nf:]) - pt + nt).abs().sum(1)
+            ph_t = phiR(wt, pt, nt)
+            ok, h = acceptable(th_t, ph_t, thetaR, phR_k, gd, alpha, switch_ok, S["thmaxR"], ftR, fpR)
+            take(st, st["searching"] & ok, wt, o, alpha, h, extra={"p": pt, "n": nt})
+            alpha = torch.where(st["searching"], 0.5 * alpha, alpha)
+            st["searching"] = st["searching"] & (alpha > a_min)
+        failedR = actR & ~st["found"]
+        S["status"].copy_(torch.where(failedR, STATUS_RESTO_FAILED, S["status"]))
+        S["active"].copy_(S["active"] & ~failedR)
+        moved = actR & st["found"]
+        mv = moved[:, None]
+        w_new, al = st["w"], st["alpha"]
+        new = evaluate(unpack(w_new))
+        ftR, fpR, fcR = augment_filter(st["aug"] & moved, ftR, fpR, fcR, thetaR, phR_k)
+        # accept: multipliers (alpha_y = alpha), bound multipliers with the kappa_Sigma safeguard (mu_R)
+        y_new = torch.where(mv, y + al[:, None] * dy, y)
+
+        def safeguard(zv, dz, slack, has):
+            zv2 = zv + a_z[:, None] * dz
+            zv2 = torch.minimum(torch.maximum(zv2, muR[:, None] / (KAPPA_SIGMA * slack)),
+                                KAPPA_SIGMA * muR[:, None] / slack)
+            return torch.where(mv & has, zv2, zv)
+
+        p_new, n_new = st["p"], st["n"]
+        dln = torch.where(hasL, w_new - wl0, torch.ones_like(w))
+        dun = torch.where(hasU, wu0 - w_new, torch.ones_like(w))
+        zLR_n = safeguard(zLR, dzL, dln, hasL)
+        zUR_n = safeguard(zUR, dzU, dun, hasU)
+        zp_n = safeguard(zp, dzp, p_new, allm)
+        zn_n = safeguard(zn, dzn, n_new, allm)
+        if use_bfgs:  # the restoration phase's own model: pairs from J^T y (its constraint curvature)
+            lbfgs_update(moved, (w_new - w)[:, :nf], new, cur, y_new, with_grad=False)
+        for k, v in (("p", p_new), ("n", n_new), ("zp", zp_n), ("zn", zn_n), ("zLR", zLR_n), ("zUR", zUR_n)):
+            S[k].copy_(torch.where(mv, v, S[k]))
+        S["w"].copy_(torch.where(mv, w_new, w))
+        S["y"].copy_(y_new)
+        S["muR"].copy_(torch.where(actR, muR, S["muR"]))
+        S["ftR"].copy_(ftR)
+        S["fpR"].copy_(fpR)
+        S["fcR"].copy_(fcR)
+        S["iters"].copy_(S["iters"] + actR.to(torch.int64))
+        for k in ("f", "grad", "g", "J"):
+            S[k].copy_(torch.where(moved.view(-1, *([1] * (S[k].dim() - 1))), new[k], S[k]))
+
+        # ---- back to the regular iteration? (RestoConvergenceCheck / TestOrigProgress)
+        c_o = cons(new["g"], w_new[:, nf:])
+        th_o = c_o.abs().sum(1)
+        ph_o = new["f"] + barrier(w_new, mu)
+        fin = torch.isfinite(th_o) & torch.isfinite(ph_o)
+        in_filter = ((th_o[:, None] <= S["filt_t"]) | (ph_o[:, None] <= S["filt_p"])).all(1)
+        vs_start = (th_o <= (1.0 - GAMMA_TH) * S["th_o0"]) | (ph_o <= S["ph_o0"] - GAMMA_PHI * S["th_o0"])
+        back = moved & fin & (th_o <= KAPPA_RESTO * S["th_o0"]) & in_filter & vs_start
+        if verbose > 1:
+            b = verbose_instance
+            if bool(actR[b] | failedR[b]):
+                print(f"   [{b}] RESTO muR={float(muR[b]):.2e} errR={float(errR0[b]):.2e} thR={float(thetaR[b]):.2e} "
+                      f"a_max={float(a_max[b]):.2e} alpha={float(al[b]):.2e} th_o={float(th_o[b]):.2e} "
+                      f"th_o0={float(S['th_o0'][b]):.2e} ph_o={float(ph_o[b]):.6e} ph_o0={float(S['ph_o0'][b]):.6e} "
+                      f"filter={bool(in_filter[b])} start={bool(vs_start[b])} back={bool(back[b])} "
+                      f"failed={bool(failedR[b])} dWR={float(dWR[b]):.1e}")
+        if bool(back.any()):
+            leave_resto(back, w_new, mu)
+
+    def leave_resto(mask, w_new, mu):
+        """The return to the regular iteration (MinC_1NrmRestorationPhase::PerformRestoration after
+        convergence): the original bound multipliers take the primal-dual step to the new point
+        (ComputeBoundMultiplierStep, dual fraction to the boundary), all of them reset to 1 when any
+        exceeds bound_mult_reset_threshold = 1000; the constraint multipliers reset to 0
+        (constr_mult_reset_threshold = 0); the quasi-Newton model restarts."""
+        mw = mask[:, None]
+        zL, zU = S["zL"], S["zU"]
+        wR = S["wR"]
+        tau = torch.clamp(1.0 - mu, min=0.99)
+        slL0 = torch.where(hasL, wR - wl0, torch.ones_like(wR))
+        slU0 = torch.where(hasU, wu0 - wR, torch.ones_like(wR))
+        slL1 = torch.where(hasL, w_new - wl0, torch.ones_like(wR))
+        slU1 = torch.where(hasU, wu0 - w_new, torch.ones_like(wR))
+        dzL = torch.where(hasL, (zL * (slL0 - slL1) + mu[:, None]) / slL0 - zL, torch.zeros_like(zL))
+        dzU = torch.where(hasU, (zU * (slU0 - slU1) + mu[:, None]) / slU0 - zU, torch.zeros_like(zU))
+        a_d = torch.minimum(max_step(zL, dzL, hasL, 0.0, tau), max_step(zU, dzU, hasU, 0.0, tau))
+        zLn = torch.where(hasL, zL + a_d[:, None] * dzL, zL)
+        zUn = torch.where(hasU, zU + a_d[:, None] * dzU, zU)
+        big = torch.maximum(zLn.amax(1), zUn.amax(1)) > BOUND_MULT_RESET
+        zLn = torch.where(big[:, None] & hasL, torch.ones_like(zLn), zLn)
+        zUn = torch.where(big[:, None] & hasU, torch.ones_like(zUn), zUn)
+        S["zL"].copy_(torch.where(mw, zLn, zL))
+        S["zU"].copy_(torch.where(mw, zUn, zU))
+        S["y"].copy_(torch.where(mw, 0.0, S["y"]))
+        S["resto"].copy_(S["resto"] & ~mask)
+        S["acc"].copy_(torch.where(mask, 0, S["acc"]))
+        lbfgs_reset(mask)
+
+    def step():
+        """One lock-step iteration: the regular iteration of the instances outside the restoration
+        phase and a restoration-phase iteration of those inside it."""
+        cur = {"f": S["f"], "grad": S["grad"], "g": S["g"], "J": S["J"]}
+        E = errors(cur, S["w"], S["y"], S["zL"], S["zU"])
+        check(E, ~S["resto"])
+        actR = S["active"] & S["resto"]
+        act = S["active"] & ~S["resto"]
+        if bool(act.any()):
+            regular_step(E, act)
+        if bool(actR.any()):
+            resto_step(actR)
+
+    def verbose_line(E, mu, a_max, al, dw, dy, delta_w, cur, failed):
+        b = verbose_instance
         print(f"   [{b}] mu={float(mu[b]):.2e} err0={float(E['err0'][b]):.2e} a_max={float(a_max[b]):.2e} "
               f"alpha={float(al[b]):.2e} dw={float(dw[b].abs().max()):.2e} dy={float(dy[b].abs().max()):.2e} "
               f"dW={float(delta_w[b]):.1e} f={float(cur['f'][b]):.6e} d_inf={float(E['d_inf'][b]):.2e} "
-              f"c_inf={float(E['base'][b]):.2e} argdw={int(dw[b].abs().argmax())}")
+              f"c_inf={float(E['c_inf'][b]):.2e} resto_next={bool(failed[b])} tiny={bool(S['tiny_last'][b])}")
+        if verbose > 2 and n >= 12:
+            Xb = unpack(S["w"])[b]
+            print("        F:", " ".join(f"({float(Xb[3+9*i]):.3g},{float(Xb[4+9*i]):.3g},{float(Xb[5+9*i]):.3g})"
+                                       for i in range((n - 3) // 9)))
 
     # ---- drive the iterations
     it_run = 0
@@ -729,15 +1159,18 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         step()
         it_run += 1
         if verbose:
-            print(f"it {it_run:4d} active {int(S['active'].sum())}")
-    # final convergence test at the last iterate
-    check(errors({"f": S["f"], "grad": S["grad"], "g": S["g"], "J": S["J"]}, S["w"], S["y"], S["zL"], S["zU"]))
+            print(f"it {it_run:4d} active {int(S['active'].sum())} resto {int((S['resto'] & S['active']).sum())}")
+    # final convergence test at the last iterate (instances still in the restoration phase keep max_iter)
+    check(errors({"f": S["f"], "grad": S["grad"], "g": S["g"], "J": S["J"]}, S["w"], S["y"], S["zL"], S["zU"]),
+          ~S["resto"])
     # IPOPT honor_original_bounds: the final point is projected back into the unrelaxed bounds and
     # its objective / constraint values reported there
     Xf = torch.minimum(torch.maximum(unpack(S["w"]), xl), xu).contiguous()
     fin = evaluate_fg(Xf)
     g = fin["g"]
     viol = torch.clamp(torch.maximum(gl - g, g - gu), min=0.0).amax(1) if m else zeros_B
-    return BatchSolveResult(x=Xf, y=S["y"], status=S["status"], iterations=S["iters"],
-                            objective=fin["f"].clone(), primal_inf=viol, dual_inf=S["d_inf"], evaluations=n_eval,
-                            iterations_run=it_run, graph=False)
+    res = BatchSolveResult(x=Xf, y=S["y"], status=S["status"], iterations=S["iters"],
+                           objective=fin["f"].clone(), primal_inf=viol, dual_inf=S["d_inf"], evaluations=n_eval,
+                           iterations_run=it_run, graph=False)
+    res.restorations = S["n_resto"]
+    return res

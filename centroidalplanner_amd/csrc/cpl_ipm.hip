@@ -17,6 +17,7 @@
 namespace cpl {
 
 constexpr int IPM_WAVES = 4;  // instances per 256-thread workgroup
+constexpr int IPM_MU_ROUNDS = 6;  // barrier decreases per iteration (0.1 -> the floor at tol 1e-8 takes 6)
 
 __device__ __forceinline__ double ipm_wave_sum(double v) { return wave_sum(v); }
 
@@ -73,22 +74,26 @@ __global__ __launch_bounds__(256) void cpl_ipm_judge_take_kernel(
   th = ipm_wave_sum(th);
   lg = ipm_wave_sum(lg);
   const double ph = f_t[b] - mu[b] * lg;
+  // filter entries are stored with their margins ((1 - gamma_theta) theta, phi - gamma_phi theta):
+  // acceptable when, for every entry, theta or phi is not larger (IPOPT's Filter::Acceptable)
   bool rejected = false;
   for (int k = lane; k < nfilt; k += 64) {
     const double ft = filt_t[b * nfilt + k], fp = filt_p[b * nfilt + k];
-    rejected |= !((th <= (1.0 - 1e-5) * ft) || (ph <= fp - 1e-8 * ft));
+    rejected |= !((th <= ft) || (ph <= fp));
   }
   const bool in_filter = __ballot(rejected) == 0;
   const double al = alpha[b], tk = theta_k[b], pk = phi_k[b], g = gd[b];
   const bool fin = isfinite(ph) && isfinite(th);
   const bool ftype = switch_ok[b] && (al * pow(fmax(-g, 0.0), 2.3) > pow(tk, 1.1));
-  const bool armijo = ph <= pk + 1e-8 * al * g;
-  const bool suff = (th <= (1.0 - 1e-5) * tk) || (ph <= pk - 1e-8 * tk);
-  // mode 0: the filter test; 1: the feasibility (restoration stand-in) step, taken when it cuts
-  // theta by 10 %; 2: unconditional (the last trial of a failed search)
-  const bool ok = mode == 0 ? (fin && th <= theta_max[b] && in_filter && (ftype ? armijo : suff))
-                : mode == 1 ? (isfinite(th) && isfinite(f_t[b]) && th <= 0.9 * tk)
-                            : true;
+  bool armijo = ph <= pk + 1e-8 * al * g;
+  bool suff = (th <= (1.0 - 1e-5) * tk) || (ph <= pk - 1e-8 * tk);
+  // obj_max_inc = 5: a barrier objective more than 5 orders of magnitude above the current one is
+  // rejected (IPOPT FilterLSAcceptor::IsAcceptableToCurrentIterate)
+  if (ph > pk) {
+    const double basval = fabs(pk) > 10.0 ? log10(fabs(pk)) : 1.0;
+    if (log10(ph - pk) > 5.0 + basval) armijo = suff = false;
+  }
+  const bool ok = fin && th <= theta_max[b] && in_filter && (ftype ? armijo : suff);
   const bool take = ok && searching[b] && (extra_mask == nullptr || extra_mask[b]);
   if (take) {
     for (int r = lane; r < m; r += 64) st_g[b * m + r] = gb[r];
@@ -100,7 +105,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_judge_take_kernel(
     if (take) {
       st_f[b] = f_t[b];
       st_alpha[b] = al;
-      st_aug[b] = (mode == 0 && !(ftype && armijo)) ? 1 : 0;
+      st_aug[b] = !(ftype && armijo) ? 1 : 0;
       searching[b] = 0;
     }
   }
@@ -123,10 +128,22 @@ __global__ __launch_bounds__(256) void cpl_ipm_optimality_kernel(
     uint8_t* __restrict__ active, int64_t* __restrict__ status, int64_t* __restrict__ acc,
     double* __restrict__ d_inf_out, double* __restrict__ err0_out, double* __restrict__ base_out,
     double* __restrict__ mu_out, double* __restrict__ filt_t_out, double* __restrict__ filt_p_out,
-    int64_t* __restrict__ fcount_out) {
+    int64_t* __restrict__ fcount_out, int mu_rounds, double mu_min, const uint8_t* __restrict__ tiny_flag,
+    const uint8_t* __restrict__ skip) {
   const int64_t b = (int64_t)blockIdx.x * IPM_WAVES + (threadIdx.x >> 6);
   if (b >= batch) return;
   const int lane = threadIdx.x & 63;
+  if (skip && skip[b]) {  // (an instance in the restoration phase: its own test and barrier update)
+    for (int k = lane; k < nfilt; k += 64) {
+      filt_t_out[b * nfilt + k] = filt_t[b * nfilt + k];
+      filt_p_out[b * nfilt + k] = filt_p[b * nfilt + k];
+    }
+    if (lane == 0) {
+      mu_out[b] = mu_in[b];
+      fcount_out[b] = fcount[b];
+    }
+    return;
+  }
   const double* Ab = A + b * (int64_t)m * nw;
   const double* yb = y + b * m;
   // lanes own w entries k = lane, lane + 64 (nw <= 128)
@@ -171,10 +188,12 @@ __global__ __launch_bounds__(256) void cpl_ipm_optimality_kernel(
   const int64_t acc_new = (act && err0 <= acc_tol) ? acc[b] + 1 : 0;
   const bool acc_now = act && !done_now && acc_new >= acc_iter;
   act = act && !done_now && !acc_now;
-  // barrier update, two rounds
+  // barrier update (IPOPT MonotoneMuUpdate, mu_allow_fast_monotone_decrease): while the barrier
+  // problem is solved to kappa_eps mu (or once after two tiny steps), at most mu_rounds times
   double mu = mu_in[b];
   bool reset = false;
-  for (int round = 0; round < 2; ++round) {
+  const bool force = tiny_flag && tiny_flag[b];
+  for (int round = 0; round < mu_rounds; ++round) {
     double em = 0.0;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -186,8 +205,8 @@ __global__ __launch_bounds__(256) void cpl_ipm_optimality_kernel(
     }
     em = wave_max(em);
     const double err_mu = fmax(base, em / sc);
-    if (act && err_mu <= 10.0 * mu && mu > tol / 10.0) {
-      mu = fmax(fmin(0.2 * mu, pow(mu, 1.5)), tol / 10.0);
+    if (act && (err_mu <= 10.0 * mu || (force && round == 0)) && mu > mu_min) {
+      mu = fmax(fmin(0.2 * mu, pow(mu, 1.5)), mu_min);
       reset = true;
     }
   }
@@ -417,7 +436,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_accept_kernel(
   const int lane = threadIdx.x & 63;
   const bool act = active[b] != 0;
   const bool addm = act && aug[b];
-  const bool fail = failed[b] != 0;
+  const bool fail = failed && failed[b] != 0;
   const int64_t fc = fcount_in[b];
   const int slot = (int)(fc % nfilt);
   const double tk = theta[b], pk = phi[b];
@@ -431,7 +450,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_accept_kernel(
     filt_t[b * nfilt + k] = ft;
     filt_p[b * nfilt + k] = fp;
   }
-  const double al = alpha[b], az = rest[b] ? 0.0 : a_z[b], mub = mu[b];
+  const double al = alpha[b], az = (rest && rest[b]) ? 0.0 : a_z[b], mub = mu[b];
   for (int r = lane; r < m; r += 64)
     if (act) y[b * m + r] += al * dy[b * m + r];
   for (int k = lane; k < nw; k += 64) {
@@ -543,6 +562,35 @@ __global__ __launch_bounds__(256) void cpl_ipm_fd_hessian_raw_kernel(int64_t tot
   H[e] = (gb[(int64_t)k * n + c] - gb[(int64_t)(nf + k) * n + c]) / (2.0 * h[b * nf + k]);
 }
 
+
+// the barrier parameter's floor of IPOPT's MonotoneMuUpdate: min(tol, compl_inf_tol = 1e-4) /
+// (barrier_tol_factor + 1)
+double ipm_mu_min(double tol) { return fmin(tol, 1e-4) / 11.0; }
+
+// cpl_ipm_optimality with the engine's extras: mu_rounds barrier decreases at most, the floor
+// mu_min, tiny_flag (a forced first decrease after two tiny steps) and skip (instances in the
+// restoration phase, left untouched: their own test and barrier update run in its kernels)
+int32_t ipm_optimality_ex(int64_t batch, int32_t nw, int32_t m, int32_t nfilt, int32_t nbounds, double tol,
+                          double acc_tol, int32_t acc_iter, const double* d_A, const double* d_gw, const double* d_c,
+                          const double* d_w, const double* d_y, const double* d_zL, const double* d_zU,
+                          const uint8_t* d_hasL, const uint8_t* d_hasU, const double* d_wl0, const double* d_wu0,
+                          const double* d_mu, const double* d_filt_t, const double* d_filt_p, const int64_t* d_fcount,
+                          uint8_t* d_active, int64_t* d_status, int64_t* d_acc, double* d_d_inf, double* d_err0,
+                          double* d_base, double* d_mu_out, double* d_filt_t_out, double* d_filt_p_out,
+                          int64_t* d_fcount_out, int32_t mu_rounds, double mu_min, const uint8_t* d_tiny_flag,
+                          const uint8_t* d_skip, void* stream) {
+  const int64_t blocks = (batch + IPM_WAVES - 1) / IPM_WAVES;
+  if (batch == 0) return CPL_OK;
+  hipLaunchKernelGGL(cpl_ipm_optimality_kernel, dim3((unsigned)blocks), dim3(64 * IPM_WAVES), 0, (hipStream_t)stream,
+                     batch, (int)nw, (int)m, (int)nfilt, (int)nbounds, tol, acc_tol, (int)acc_iter, d_A, d_gw, d_c, d_w,
+                     d_y, d_zL, d_zU, d_hasL, d_hasU, d_wl0, d_wu0, d_mu, d_filt_t, d_filt_p, d_fcount, d_active,
+                     d_status, d_acc, d_d_inf, d_err0, d_base, d_mu_out, d_filt_t_out, d_filt_p_out, d_fcount_out,
+                     (int)mu_rounds, mu_min, d_tiny_flag, d_skip);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_ipm_optimality launch: ") + hipGetErrorString(e));
+  return CPL_OK;
+}
+
 }  // namespace cpl
 
 using namespace cpl;
@@ -577,8 +625,8 @@ int32_t cpl_ipm_judge_take(int64_t batch, int32_t nw, int32_t m, int32_t nf, int
                            const double* d_filt_t, const double* d_filt_p, const uint8_t* d_extra_mask,
                            uint8_t* d_searching, double* d_st_f, double* d_st_g, double* d_st_w, double* d_st_alpha,
                            uint8_t* d_st_aug, double* d_th_out, uint8_t* d_ok_out, int32_t mode, void* stream) {
-  if (batch < 0 || nw <= 0 || m < 0 || nf < 0 || nf > nw || nfilt < 0 || mode < 0 || mode > 2)
-    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_judge_take: bad sizes");
+  if (batch < 0 || nw <= 0 || m < 0 || nf < 0 || nf > nw || nfilt < 0 || mode != 0)
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_judge_take: bad sizes (mode must be 0)");
   if (batch == 0) return CPL_OK;
   if ((m > 0 && (!d_row_slack || !d_gl || !d_g_t || !d_st_g)) || !d_hasL || !d_hasU || !d_wl0 || !d_wu0 || !d_wt ||
       !d_f_t || !d_alpha || !d_mu || !d_theta_k || !d_phi_k || !d_gd || !d_switch_ok || !d_theta_max ||
@@ -614,13 +662,10 @@ int32_t cpl_ipm_optimality(int64_t batch, int32_t nw, int32_t m, int32_t nfilt, 
     return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_optimality: missing buffer");
   const int64_t blocks = (batch + IPM_WAVES - 1) / IPM_WAVES;
   if (blocks > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_optimality: batch too large");
-  hipLaunchKernelGGL(cpl_ipm_optimality_kernel, dim3((unsigned)blocks), dim3(64 * IPM_WAVES), 0, (hipStream_t)stream,
-                     batch, (int)nw, (int)m, (int)nfilt, (int)nbounds, tol, acc_tol, (int)acc_iter, d_A, d_gw, d_c, d_w,
-                     d_y, d_zL, d_zU, d_hasL, d_hasU, d_wl0, d_wu0, d_mu, d_filt_t, d_filt_p, d_fcount, d_active,
-                     d_status, d_acc, d_d_inf, d_err0, d_base, d_mu_out, d_filt_t_out, d_filt_p_out, d_fcount_out);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_ipm_optimality launch: ") + hipGetErrorString(e));
-  return CPL_OK;
+  return ipm_optimality_ex(batch, nw, m, nfilt, nbounds, tol, acc_tol, acc_iter, d_A, d_gw, d_c, d_w, d_y, d_zL, d_zU,
+                           d_hasL, d_hasU, d_wl0, d_wu0, d_mu, d_filt_t, d_filt_p, d_fcount, d_active, d_status, d_acc,
+                           d_d_inf, d_err0, d_base, d_mu_out, d_filt_t_out, d_filt_p_out, d_fcount_out, IPM_MU_ROUNDS,
+                           ipm_mu_min(tol), nullptr, nullptr, stream);
 }
 
 int32_t cpl_ipm_max_step(int64_t batch, int32_t nw, const double* d_v, const double* d_dir, const double* d_v2,

@@ -1396,6 +1396,96 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   KKT_MARK(7);
 }
 
+
+// ---- the restoration phase's Newton system (quasi-definite) -------------------------------
+// IPOPT's restoration problem (min rho sum(p + n) + eta/2 |D_R (x - x_R)|^2 s.t. c(w) - p + n = 0,
+// p, n >= 0) with p and n eliminated, as IPOPT's AugRestoSystemSolver reduces it:
+//     [ W   A^T ] [dw]   [r1]      D = 1/Sigma_p + 1/Sigma_n > 0 (diagonal, m)
+//     [ A   -D  ] [dy] = [r2]
+// has the right inertia iff K = W + A^T D^-1 A is positive definite, so its Cholesky is the inertia
+// test and dW follows IPOPT's schedule (first 1e-4, or dW_last / 3; x100 / x8).  Then
+// dw = K^-1 (r1 + A^T D^-1 r2), dy = D^-1 (A dw - r2).  One workgroup per instance: K formed once
+// (lower triangle, mirrored: bitwise symmetric) into the global workspace, each attempt factorised
+// by one wave in LDS (batch_ipm.py kkt_qd restates it).  Pivots at or below eps max|K_ii| count as
+// zero eigenvalues.
+__global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_qd_kernel(
+    int64_t batch, int nw, int m, const double* __restrict__ W, const double* __restrict__ A,
+    const double* __restrict__ Dinv, const double* __restrict__ r1, const double* __restrict__ r2,
+    const uint8_t* __restrict__ active, double* __restrict__ dwl, double* __restrict__ dw_out,
+    double* __restrict__ dy_out, double* __restrict__ delta_w_out, double* __restrict__ Kws) {
+  const int64_t b = blockIdx.x;
+  if (b >= batch || (active && !active[b])) return;
+  extern __shared__ __align__(16) double qd_lds[];
+  double* L = qd_lds;              // [nw][nw]
+  double* v = L + nw * nw;         // [nw]: rhs -> solution
+  double* t = v + nw;              // [m]: D^-1 r2
+  __shared__ double s_red[KKT_THREADS / 64];
+  __shared__ int s_ok;
+  const int tid = threadIdx.x;
+  const double* Wb = W + b * (int64_t)nw * nw;
+  const double* Ab = A + b * (int64_t)m * nw;
+  const double* Db = Dinv + b * m;
+  double* Kb = Kws + b * (int64_t)nw * nw;
+  // K = W + A^T D^-1 A, lower triangle (i >= j) summed over the rows in order, mirrored
+  double dmax = 0.0;
+  for (int e = tid; e < nw * nw; e += KKT_THREADS) {
+    const int i = e / nw, j = e - i * nw;
+    if (j > i) continue;
+    double s = 0.0;
+    for (int r = 0; r < m; ++r) s += (Ab[r * nw + i] * Db[r]) * Ab[r * nw + j];
+    const double k = Wb[i * nw + j] + s;
+    Kb[i * nw + j] = k;
+    Kb[j * nw + i] = k;
+    if (i == j) dmax = fmax(dmax, fabs(k));
+  }
+  for (int r = tid; r < m; r += KKT_THREADS) t[r] = Db[r] * r2[b * m + r];
+  dmax = wave_max(dmax);
+  if ((tid & 63) == 0) s_red[tid >> 6] = dmax;
+  __syncthreads();  // (also orders the global K stores before the copies below)
+  double kmax = 0.0;
+  for (int q = 0; q < KKT_THREADS / 64; ++q) kmax = fmax(kmax, s_red[q]);
+  const double piv_tol = 2.220446049250313e-16 * kmax;
+  const double last = dwl[b];
+  double dW = 0.0;
+  for (int attempt = 0; attempt < 64; ++attempt) {
+    for (int e = tid; e < nw * nw; e += KKT_THREADS) {
+      const int i = e / nw, j = e - i * nw;
+      L[e] = Kb[e] + (i == j ? dW : 0.0);
+    }
+    __syncthreads();
+    if (tid < 64) {
+      const bool ok = wave_cholesky(L, nw, piv_tol);
+      if (tid == 0) s_ok = ok ? 1 : 0;
+    }
+    __syncthreads();
+    if (s_ok) break;
+    dW = dW == 0.0 ? (last == 0.0 ? 1e-4 : fmax(last / 3.0, 1e-20)) : dW * (last == 0.0 ? 100.0 : 8.0);
+    __syncthreads();
+  }
+  // rhs = r1 + A^T (D^-1 r2)
+  for (int k = tid; k < nw; k += KKT_THREADS) {
+    double s = 0.0;
+    for (int r = 0; r < m; ++r) s += Ab[r * nw + k] * t[r];
+    v[k] = r1[b * nw + k] + s;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    wave_trsv(nw, true, L, nw, 1, L, nw + 1, v);   // L u = rhs
+    wave_trsv(nw, false, L, 1, nw, L, nw + 1, v);  // L^T dw = u
+  }
+  __syncthreads();
+  for (int k = tid; k < nw; k += KKT_THREADS) dw_out[b * nw + k] = v[k];
+  for (int r = tid; r < m; r += KKT_THREADS) {
+    double s = 0.0;
+    for (int k = 0; k < nw; ++k) s += Ab[r * nw + k] * v[k];
+    dy_out[b * m + r] = Db[r] * (s - r2[b * m + r]);
+  }
+  if (tid == 0) {
+    if (delta_w_out) delta_w_out[b] = dW;
+    dwl[b] = dW;
+  }
+}
+
 }  // namespace cpl
 
 using namespace cpl;
@@ -1418,15 +1508,12 @@ using KktWaveKernel = void (*)(int, int64_t, const double*, const double*, const
 // nullptr otherwise.  With its register-resident QR / Z and the FP64-MFMA reduced Hessian it
 // factorises faster than the workgroup kernel at every batch size (scripts/kkt_ab.hip,
 // profiles/r2_v7/kkt_ab/: 1 system 0.069 vs 0.099 ms, 1 024 0.080 vs 0.134, 8 192 0.42 vs 0.94);
-// its re-solve is 4-7 us slower up to ~1 000 systems, less than the factorisation gains.  Batches
-// below KKT_WAVE_MIN_BATCH (the single-instance Solve()) stay on the workgroup kernel: the
-// degenerate TestBasic ground problem (force weight 0) runs to the iteration limit, and its end point
-// depends on the rounding of every Newton step — it meets TestBasic's cone tolerance with the
-// workgroup kernel's, not with the one-wave kernel's.  (Earlier in round 2 the choice went by batch
-// size: the workgroup kernel while the batch fitted in as few of its rounds.)  CPL_KKT_KERNEL=block
-// or =wave forces one (measurement only).
-constexpr int64_t KKT_WAVE_MIN_BATCH = 64;
-static KktWaveKernel kkt_wave_kernel_for(int nw, int m, int64_t batch) {
+// its re-solve is 4-7 us slower up to ~1 000 systems, less than the factorisation gains, so the
+// choice depends on the system size only: every batch size, the single-instance Solve() included,
+// runs the same kernel and an instance's iterates do not depend on the batch it is solved in
+// (tests/test_gpu_solve_engine.py: B = 1 vs inside B = 64).  CPL_KKT_KERNEL=block or =wave forces
+// one (measurement only).
+static KktWaveKernel kkt_wave_kernel_for(int nw, int m) {
   static const int forced = [] {
     const char* e = std::getenv("CPL_KKT_KERNEL");
     if (!e) return 0;
@@ -1435,8 +1522,7 @@ static KktWaveKernel kkt_wave_kernel_for(int nw, int m, int64_t batch) {
   KktWaveKernel wk = nullptr;
   if (nw == 47 && m == 30) wk = cpl_kkt_wave_kernel<47, 30>;
   if (!wk || forced == 1) return nullptr;
-  if (forced == 2) return wk;
-  return batch >= KKT_WAVE_MIN_BATCH ? wk : nullptr;
+  return wk;
 }
 
 extern "C" {
@@ -1477,7 +1563,7 @@ int32_t cpl_kkt_solve(int32_t mode, int64_t batch, int32_t nw, int32_t m, const 
   if (mode == 0 && (!d_mu || !d_delta_w || !d_delta_c || !d_info))
     return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_solve: factorisation needs mu, delta_w, delta_c, info");
   if (batch > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_solve: batch too large");
-  if (KktWaveKernel wk = kkt_wave_kernel_for(nw, m, batch)) {
+  if (KktWaveKernel wk = kkt_wave_kernel_for(nw, m)) {
     const size_t lds = sizeof(double) * (size_t)kktw_lds_doubles(nw, m);
     hipLaunchKernelGGL(wk, dim3((unsigned)batch), dim3(64), lds, (hipStream_t)stream, (int)mode, batch, d_M, d_A, d_r1,
                        d_r2, d_mu, d_delta_w_last, d_active, d_dw, d_dy, d_delta_w, d_delta_c, d_info, d_ws);
@@ -1490,6 +1576,26 @@ int32_t cpl_kkt_solve(int32_t mode, int64_t batch, int32_t nw, int32_t m, const 
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_kkt_kernel launch: ") + hipGetErrorString(e));
+  return CPL_OK;
+}
+
+
+int32_t cpl_kkt_qd_solve(int64_t batch, int32_t nw, int32_t m, const double* d_W, const double* d_A,
+                         const double* d_Dinv, const double* d_r1, const double* d_r2, const uint8_t* d_active,
+                         double* d_delta_w_last, double* d_dw, double* d_dy, double* d_delta_w, double* d_ws,
+                         void* stream) {
+  if (batch < 0 || nw <= 0 || m < 0 || nw > KKT_MAX_NW)
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_qd_solve: need 0 <= m, 0 < nw <= 128");
+  if (batch == 0) return CPL_OK;
+  if (!d_W || (m > 0 && (!d_A || !d_Dinv || !d_r2 || !d_dy)) || !d_r1 || !d_dw || !d_delta_w_last || !d_ws)
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_qd_solve: missing buffer");
+  if (batch > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_qd_solve: batch too large");
+  const size_t lds = sizeof(double) * ((size_t)nw * nw + nw + (m > 0 ? m : 1));
+  hipLaunchKernelGGL(cpl_kkt_qd_kernel, dim3((unsigned)batch), dim3(KKT_THREADS), lds, (hipStream_t)stream, batch,
+                     (int)nw, (int)m, d_W, d_A, d_Dinv, d_r1, d_r2, d_active, d_delta_w_last, d_dw, d_dy, d_delta_w,
+                     d_ws);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_kkt_qd_kernel launch: ") + hipGetErrorString(e));
   return CPL_OK;
 }
 

@@ -36,6 +36,18 @@ int32_t ipm_newton_setup_lm(int64_t batch, int32_t nw, int32_t m, int32_t nf, co
                             const uint8_t* d_hasU, const double* d_wl0, const double* d_wu0, const double* d_Hc,
                             int32_t lm_pairs, double* d_M, double* d_r1, double* d_r2, double* d_gphi,
                             double* d_mr_diag, double* d_theta, double* d_phi, const uint8_t* d_active, void* stream);
+// cpl_ipm.hip: the optimality test + monotone barrier update with IPOPT's per-iteration rounds
+double ipm_mu_min(double tol);
+int32_t ipm_optimality_ex(int64_t batch, int32_t nw, int32_t m, int32_t fmax, int32_t nbounds, double tol,
+                          double acceptable_tol, int32_t acceptable_iter, const double* d_A, const double* d_gw,
+                          const double* d_c, const double* d_w, const double* d_y, const double* d_zL,
+                          const double* d_zU, const uint8_t* d_hasL, const uint8_t* d_hasU, const double* d_wl0,
+                          const double* d_wu0, const double* d_mu, const double* d_filt_t, const double* d_filt_p,
+                          const int64_t* d_fcount,
+                          uint8_t* d_active, int64_t* d_status, int64_t* d_acc, double* d_dinf, double* d_err0,
+                          double* d_base, double* d_mu_o, double* d_ft, double* d_fp, int64_t* d_fc,
+                          int32_t mu_rounds, double mu_min, const uint8_t* d_tiny_flag, const uint8_t* d_skip,
+                          void* stream);
 namespace {
 
 constexpr int FMAX = 64;          // filter entries kept per instance (a ring), as batch_ipm.FMAX
@@ -187,7 +199,8 @@ __global__ __launch_bounds__(256) void k_prep(int64_t B, int n, int m, int nf, i
 __global__ void k_unpack_tau(int64_t total, int n, int nw, const int32_t* __restrict__ freepos,
                              const double* __restrict__ Xbase, const double* __restrict__ w,
                              const double* __restrict__ mu, const uint8_t* __restrict__ active,
-                             double* __restrict__ X, double* __restrict__ tau, uint8_t* __restrict__ act) {
+                             const uint8_t* __restrict__ in_resto, double* __restrict__ X, double* __restrict__ tau,
+                             uint8_t* __restrict__ act) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total) return;
   const int64_t b = e / n;
@@ -196,7 +209,7 @@ __global__ void k_unpack_tau(int64_t total, int n, int nw, const int32_t* __rest
   X[e] = k >= 0 ? w[b * nw + k] : Xbase[e];
   if (j == 0) {
     tau[b] = fmax(1.0 - mu[b], 0.99);
-    act[b] = active[b];
+    act[b] = active[b] && !in_resto[b];  // the restoration phase's instances take their own step
   }
 }
 
@@ -214,32 +227,98 @@ __global__ void k_unpack(int64_t total, int n, int nw, const int32_t* __restrict
   X[e] = v;
 }
 
-// line-search state at the current iterate, the first trial step = the fraction-to-the-boundary one
-__global__ __launch_bounds__(256) void k_ls_init(int64_t B, int m, int nw, const uint8_t* __restrict__ act,
-                                                 const double* __restrict__ f, const double* __restrict__ g,
-                                                 const double* __restrict__ w, const double* __restrict__ a_max,
-                                                 uint8_t* __restrict__ searching, double* __restrict__ st_f,
-                                                 double* __restrict__ st_g, double* __restrict__ st_w,
-                                                 double* __restrict__ st_alpha, uint8_t* __restrict__ st_aug,
-                                                 double* __restrict__ alpha, uint8_t* __restrict__ failed,
-                                                 uint8_t* __restrict__ rest, uint8_t* __restrict__ any) {
+// ---- IPOPT constants of the line search / restoration phase (batch_ipm.py restates them) ------
+constexpr double GAMMA_TH = 1e-5, GAMMA_PHI = 1e-8, DELTA_SW = 1.0, S_TH = 1.1, S_PHI = 2.3, ETA_PHI = 1e-8;
+constexpr double ALPHA_MIN_FRAC = 0.05, KAPPA_SOC = 0.99, OBJ_MAX_INC = 5.0, KAPPA_SIGMA = 1e10;
+constexpr double TINY_STEP_TOL = 10.0 * DBL_EPSILON, TINY_STEP_Y_TOL = 1e-2;
+constexpr double RHO_R = 1000.0, KAPPA_RESTO = 0.9, BOUND_MULT_RESET = 1000.0, SOFT_RESTO_FACTOR = 0.9999;
+constexpr int MAX_SOFT_RESTO = 10, MU_ROUNDS = 6;
+
+__device__ __forceinline__ double wave_min_d(double v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+  return v;
+}
+
+// IPOPT FilterLSAcceptor::CalculateAlphaMin (alpha_min_frac 0.05)
+__device__ __forceinline__ double alpha_min_of(double theta, double gd, double theta_min) {
+  if (!(gd < 0.0)) return ALPHA_MIN_FRAC * GAMMA_TH;
+  double a = fmin(GAMMA_TH, GAMMA_PHI * theta / -gd);
+  if (theta <= theta_min) a = fmin(a, DELTA_SW * pow(theta, S_TH) / pow(-gd, S_PHI));
+  return ALPHA_MIN_FRAC * a;
+}
+
+// IPOPT FilterLSAcceptor::CheckAcceptabilityOfTrialPoint on one wave: theta_max, the filter (entries
+// stored with their margins), switching condition / Armijo / sufficient decrease against the
+// reference point with the obj_max_inc guard.  Returns ok; *h_type = the step augments the filter.
+__device__ __forceinline__ bool acceptable_wave(double th, double ph, double tk, double pk, double g, double al,
+                                                bool switch_ok, double theta_max, const double* ft, const double* fp,
+                                                bool* h_type) {
+  const int lane = threadIdx.x & 63;
+  bool rejected = false;
+  for (int k = lane; k < FMAX; k += 64) rejected |= !((th <= ft[k]) || (ph <= fp[k]));
+  const bool in_filter = __ballot(rejected) == 0;
+  const bool fin = isfinite(ph) && isfinite(th);
+  const bool ftype = switch_ok && (al * pow(fmax(-g, 0.0), S_PHI) > DELTA_SW * pow(tk, S_TH));
+  bool armijo = ph <= pk + ETA_PHI * al * g;
+  bool suff = (th <= (1.0 - GAMMA_TH) * tk) || (ph <= pk - GAMMA_PHI * tk);
+  if (ph > pk) {
+    const double basval = fabs(pk) > 10.0 ? log10(fabs(pk)) : 1.0;
+    if (log10(ph - pk) > OBJ_MAX_INC + basval) armijo = suff = false;
+  }
+  if (h_type) *h_type = !(ftype && armijo);
+  return fin && th <= theta_max && in_filter && (ftype ? armijo : suff);
+}
+
+// After the Newton step (batch_ipm.py regular_step): IPOPT's tiny-step test (every primal component
+// below 10 eps relative, the multiplier step below 1e-2, the point feasible to 1e-4; two in a row
+// force the next barrier decrease), the soft restoration phase's counter, alpha_min, and the line
+// search state (searching unless tiny or in the soft phase; a tiny step is taken whole: alpha_max).
+__global__ __launch_bounds__(256) void k_ls_setup(
+    int64_t B, int m, int nw, const uint8_t* __restrict__ act, const double* __restrict__ w,
+    const double* __restrict__ dw, const double* __restrict__ dy, const double* __restrict__ c,
+    const double* __restrict__ f, const double* __restrict__ g, const double* __restrict__ theta_k,
+    const double* __restrict__ gd, const double* __restrict__ theta_min, const double* __restrict__ a_max,
+    uint8_t* __restrict__ in_soft, int32_t* __restrict__ soft_cnt, uint8_t* __restrict__ tiny_last,
+    uint8_t* __restrict__ tiny_flag, uint8_t* __restrict__ tiny_now, uint8_t* __restrict__ soft_now,
+    double* __restrict__ a_min, uint8_t* __restrict__ searching, double* __restrict__ st_f, double* __restrict__ st_g,
+    double* __restrict__ st_w, double* __restrict__ st_alpha, uint8_t* __restrict__ st_aug, double* __restrict__ alpha,
+    uint8_t* __restrict__ any) {
   const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
   if (b >= B) return;
   const int lane = threadIdx.x & 63;
+  const bool a = act[b] != 0;
+  double rel = 0.0, dym = 0.0, cin = 0.0;
+  for (int k = lane; k < nw; k += 64) rel = fmax(rel, fabs(dw[b * nw + k]) / (1.0 + fabs(w[b * nw + k])));
+  for (int r = lane; r < m; r += 64) {
+    dym = fmax(dym, fabs(dy[b * m + r]));
+    cin = fmax(cin, fabs(c[b * m + r]));
+  }
+  rel = wave_max(rel);
+  dym = wave_max(dym);
+  cin = wave_max(cin);
+  const bool tiny = a && rel < TINY_STEP_TOL && dym < TINY_STEP_Y_TOL && cin < 1e-4;
+  const bool sn = a && in_soft[b] && !tiny;
+  const double am = a_max[b];
   for (int r = lane; r < m; r += 64) st_g[b * m + r] = g[b * m + r];
-  for (int k = lane; k < nw; k += 64) st_w[b * nw + k] = w[b * nw + k];
+  for (int k = lane; k < nw; k += 64) st_w[b * nw + k] = tiny ? w[b * nw + k] + am * dw[b * nw + k] : w[b * nw + k];
   if (lane == 0) {
-    if (b == 0 && any) any[0] = 0;  // the any-searching flag of the split iteration
-    failed[b] = 0;  // (set again by k_feas_prep / k_rest when the rest of the line search runs)
-    rest[b] = 0;
-    searching[b] = act[b];
+    if (b == 0 && any) any[0] = any[1] = 0;
+    if (a) {
+      const bool tl = tiny_last[b] != 0;
+      tiny_flag[b] = (tiny && tl) ? 1 : 0;
+      tiny_last[b] = (tiny && !tl) ? 1 : 0;
+    }
+    tiny_now[b] = tiny ? 1 : 0;
+    soft_now[b] = sn ? 1 : 0;
+    if (sn) soft_cnt[b] += 1;
+    a_min[b] = alpha_min_of(theta_k[b], gd[b], theta_min[b]);
+    searching[b] = (a && !tiny && !sn) ? 1 : 0;
     st_f[b] = f[b];
-    st_alpha[b] = 0.0;
+    st_alpha[b] = tiny ? am : 0.0;
     st_aug[b] = 0;
-    alpha[b] = a_max[b];
+    alpha[b] = am;
   }
 }
-
 
 // c_soc = a_soc c_soc + c(trial point); the correction's right-hand side r2 = -c_soc
 __global__ __launch_bounds__(256) void k_soc_rhs(int64_t B, int m, int nf, int nw, const int32_t* __restrict__ row_slack,
@@ -258,8 +337,8 @@ __global__ __launch_bounds__(256) void k_soc_rhs(int64_t B, int m, int nf, int n
   }
 }
 
-// second-order correction bookkeeping (batch_ipm step(): soc, c_soc, a_soc, th_old) and the first
-// correction's right-hand side in one launch: c_soc = a_soc c + c(trial point), r2 = -c_soc
+// second-order correction bookkeeping (batch_ipm.py: soc, c_soc, a_soc, th_old = theta of the first
+// trial point as IPOPT's TrySecondOrderCorrection) and the first correction's right-hand side
 __global__ __launch_bounds__(256) void k_soc_begin_rhs(int64_t B, int m, int nf, int nw, const uint8_t* __restrict__ searching,
                                                        const double* __restrict__ th, const double* __restrict__ theta_k,
                                                        const double* __restrict__ c, const double* __restrict__ alpha,
@@ -281,23 +360,7 @@ __global__ __launch_bounds__(256) void k_soc_begin_rhs(int64_t B, int m, int nf,
   if (lane == 0) {
     soc[b] = searching[b] && th[b] >= theta_k[b];
     a_soc[b] = a;
-    th_old[b] = theta_k[b];
-  }
-}
-
-// the last k_soc_after and the trial's halving in one launch; with `any`, instances still searching
-// also raise the any-searching flag (zeroed by k_ls_init)
-__global__ void k_soc_after_halve(int64_t B, uint8_t* __restrict__ soc, const uint8_t* __restrict__ ok,
-                                  const double* __restrict__ th, double* __restrict__ th_old,
-                                  const uint8_t* __restrict__ searching, double* __restrict__ alpha,
-                                  uint8_t* __restrict__ any) {
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  soc[b] = soc[b] && !ok[b] && th[b] <= 0.99 * th_old[b];  // kappa_soc = 0.99
-  th_old[b] = th[b];
-  if (searching[b]) {
-    alpha[b] = 0.5 * alpha[b];
-    if (any) any[0] = 1;
+    th_old[b] = th[b];
   }
 }
 
@@ -305,49 +368,181 @@ __global__ void k_soc_after(int64_t B, uint8_t* __restrict__ soc, const uint8_t*
                             const double* __restrict__ th, double* __restrict__ th_old) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  soc[b] = soc[b] && !ok[b] && th[b] <= 0.99 * th_old[b];  // kappa_soc = 0.99
+  soc[b] = soc[b] && !ok[b] && th[b] <= KAPPA_SOC * th_old[b];
   th_old[b] = th[b];
 }
 
-// any instance still searching after the first trial (small-batch split iterations): one workgroup
-__global__ __launch_bounds__(256) void k_any_searching(int64_t B, const uint8_t* __restrict__ searching,
-                                                       uint8_t* __restrict__ flag) {
-  __shared__ int s_any;
-  if (threadIdx.x == 0) s_any = 0;
-  __syncthreads();
-  int a = 0;
-  for (int64_t b = threadIdx.x; b < B; b += blockDim.x) a |= searching[b];
-  if (a) s_any = 1;
-  __syncthreads();
-  if (threadIdx.x == 0) flag[0] = (uint8_t)s_any;
-}
-
-__global__ void k_halve(int64_t B, const uint8_t* __restrict__ searching, double* __restrict__ alpha) {
+// after a trial: alpha halved where still searching, the search given up below alpha_min (IPOPT
+// tries the next point only while alpha > alpha_min); flags (zeroed by k_ls_setup / k_resto_post):
+// any[fi] = an instance is still searching; with soft_now, any[1] = an instance has no accepted
+// point yet and will try the soft restoration step
+__global__ void k_halve2(int64_t B, uint8_t* __restrict__ searching, double* __restrict__ alpha,
+                         const double* __restrict__ a_min, const uint8_t* __restrict__ act,
+                         const uint8_t* __restrict__ tiny, const uint8_t* __restrict__ soft_now,
+                         const int32_t* __restrict__ soft_cnt, const double* __restrict__ st_alpha,
+                         uint8_t* __restrict__ any, int fi) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  if (searching[b]) alpha[b] = 0.5 * alpha[b];
+  bool s = searching[b] != 0;
+  if (s) {
+    const double a = 0.5 * alpha[b];
+    alpha[b] = a;
+    if (!(a > a_min[b])) s = false;
+    searching[b] = s ? 1 : 0;
+  }
+  if (s) any[fi] = 1;
+  if (soft_now && act[b] && !tiny[b] &&
+      ((soft_now[b] && soft_cnt[b] <= MAX_SOFT_RESTO) || (!soft_now[b] && !(st_alpha[b] > 0.0))))
+    any[1] = 1;
 }
 
-// the feasibility step's system: failed = still searching; Mr = diag(mr_diag) (its zero off-diagonal
-// part set once); r2 = -c
-__global__ __launch_bounds__(256) void k_feas_prep(int64_t B, int m, int nw, const uint8_t* __restrict__ searching,
-                                                   const double* __restrict__ mr_diag, const double* __restrict__ c,
-                                                   uint8_t* __restrict__ failed, double* __restrict__ Mr,
-                                                   double* __restrict__ negc) {
+// IPOPT's soft restoration step, part 1 (BacktrackingLineSearch::TrySoftRestoStep): the instances
+// without an accepted trial (or in the soft phase, at most max_soft_resto_iters times) try the full
+// primal-dual step alpha = min(alpha_primal_max, alpha_dual_max): its point w + alpha dw and X
+__global__ __launch_bounds__(256) void k_soft_begin(
+    int64_t B, int n, int nf, int nw, const uint8_t* __restrict__ act, const uint8_t* __restrict__ tiny,
+    const uint8_t* __restrict__ soft_now, const int32_t* __restrict__ soft_cnt, const double* __restrict__ st_alpha,
+    const double* __restrict__ a_max, const double* __restrict__ a_z, const double* __restrict__ w,
+    const double* __restrict__ dw, const int32_t* __restrict__ freepos, const double* __restrict__ Xbase,
+    uint8_t* __restrict__ soft_try, double* __restrict__ a_soft, double* __restrict__ ws, double* __restrict__ X) {
   const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
   if (b >= B) return;
   const int lane = threadIdx.x & 63;
-  for (int k = lane; k < nw; k += 64) Mr[(b * nw + k) * nw + k] = mr_diag[b * nw + k];
-  for (int r = lane; r < m; r += 64) negc[b * m + r] = -c[b * m + r];
-  if (lane == 0) failed[b] = searching[b];
+  const bool t = act[b] && !tiny[b] &&
+                 ((soft_now[b] && soft_cnt[b] <= MAX_SOFT_RESTO) || (!soft_now[b] && !(st_alpha[b] > 0.0)));
+  const double as = fmin(a_max[b], a_z[b]);
+  for (int k = lane; k < nw; k += 64) ws[b * nw + k] = w[b * nw + k] + (t ? as : 0.0) * dw[b * nw + k];
+  for (int j = lane; j < n; j += 64) {
+    const int k = freepos[j];
+    X[b * n + j] = k >= 0 ? w[b * nw + k] + (t ? as : 0.0) * dw[b * nw + k] : Xbase[b * n + j];
+  }
+  if (lane == 0) {
+    soft_try[b] = t ? 1 : 0;
+    a_soft[b] = as;
+  }
 }
 
-__global__ void k_rest(int64_t B, const uint8_t* __restrict__ failed, const uint8_t* __restrict__ ok_r,
-                       const double* __restrict__ alpha, uint8_t* __restrict__ rest, double* __restrict__ alpha2) {
+// IPOPT's primal-dual error of the barrier problem (1-norms of the dual residual, the constraint
+// residual and the mu-complementarity) of one instance on one wave.  A row r, column k: from the
+// dense A (Ad != NULL) or from the values-only Jacobian records through amap (as cpl_ipm_dense_a).
+__device__ __forceinline__ double pd_error_wave(int m, int nf, int nw, const double* Ad, const double* Jrec,
+                                                const int32_t* amap, const int32_t* row_slack, const double* gw_free,
+                                                int gw_stride_n, const int32_t* free32, const double* c,
+                                                const double* w, const double* y, const double* zL, const double* zU,
+                                                const double* alpha_dy, const double* dy, const double* dzL,
+                                                const double* dzU, double a, const uint8_t* hasL, const uint8_t* hasU,
+                                                const double* wl0, const double* wu0, double mu) {
+  const int lane = threadIdx.x & 63;
+  double s = 0.0;
+  for (int k = lane; k < nw; k += 64) {
+    double dual = k < nf ? (gw_stride_n ? gw_free[free32[k]] : gw_free[k]) : 0.0;
+    for (int r = 0; r < m; ++r) {
+      double akr;
+      if (Ad) {
+        akr = Ad[r * nw + k];
+      } else if (k < nf) {
+        const int q = amap[r * nf + k];
+        akr = q == -1 ? 0.0 : (q == -2 ? 1.0 : Jrec[q]);
+        akr = akr == akr ? akr : 0.0;
+      } else {
+        akr = row_slack[r] == k - nf ? -1.0 : 0.0;
+      }
+      const double yr = dy ? y[r] + a * dy[r] : y[r];
+      dual += akr * yr;
+    }
+    const double zl = hasL[k] ? (dzL ? zL[k] + a * dzL[k] : zL[k]) : 0.0;
+    const double zu = hasU[k] ? (dzU ? zU[k] + a * dzU[k] : zU[k]) : 0.0;
+    dual = dual - zl + zu;
+    s += fabs(dual);
+    if (hasL[k]) s += fabs((w[k] - wl0[k]) * zl - mu);
+    if (hasU[k]) s += fabs((wu0[k] - w[k]) * zu - mu);
+  }
+  for (int r = lane; r < m; r += 64) s += fabs(c[r]);
+  (void)alpha_dy;
+  return wave_sum(s);
+}
+
+// part 2: the soft step is taken when the original filter / current iterate accept it (the soft
+// phase ends) or when it cuts the primal-dual error by soft_resto_pderror_reduction_factor (the
+// soft phase starts or continues); the step's alpha then also moves the bound multipliers
+__global__ __launch_bounds__(256) void k_soft_judge(
+    int64_t B, int n, int m, int nf, int nw, int nnz_rec, const uint8_t* __restrict__ soft_try,
+    const uint8_t* __restrict__ soft_now, const double* __restrict__ a_soft, const int32_t* __restrict__ amap,
+    const int32_t* __restrict__ row_slack, const int32_t* __restrict__ free32, const double* __restrict__ gl,
+    const uint8_t* __restrict__ hasL, const uint8_t* __restrict__ hasU, const double* __restrict__ wl0,
+    const double* __restrict__ wu0, const double* __restrict__ ws, const double* __restrict__ f_s,
+    const double* __restrict__ grad_s, const double* __restrict__ g_s, const double* __restrict__ J_s,
+    const double* __restrict__ A, const double* __restrict__ gradw, const double* __restrict__ c,
+    const double* __restrict__ w, const double* __restrict__ y, const double* __restrict__ zL,
+    const double* __restrict__ zU, const double* __restrict__ dy, const double* __restrict__ dzL,
+    const double* __restrict__ dzU, const double* __restrict__ mu, const double* __restrict__ theta_k,
+    const double* __restrict__ phi_k, const double* __restrict__ gd, const uint8_t* __restrict__ switch_ok,
+    const double* __restrict__ theta_max, const double* __restrict__ ft, const double* __restrict__ fp,
+    double* __restrict__ cs_tmp, uint8_t* __restrict__ in_soft, int32_t* __restrict__ soft_cnt,
+    double* __restrict__ st_f, double* __restrict__ st_g, double* __restrict__ st_w, double* __restrict__ st_alpha,
+    uint8_t* __restrict__ st_aug, double* __restrict__ a_z) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B || !soft_try[b]) return;
+  const int lane = threadIdx.x & 63;
+  const double* wb = ws + b * nw;
+  const double mub = mu[b], as = a_soft[b];
+  double th = 0.0, lg = 0.0;
+  for (int r = lane; r < m; r += 64) {
+    const double cr = cons_row(g_s + b * m, wb, nf, r, row_slack, gl);
+    cs_tmp[b * m + r] = cr;
+    th += fabs(cr);
+  }
+  for (int k = lane; k < nw; k += 64) {
+    if (hasL[k]) lg += log(wb[k] - wl0[k]);
+    if (hasU[k]) lg += log(wu0[k] - wb[k]);
+  }
+  th = wave_sum(th);
+  lg = wave_sum(lg);
+  const double ph = f_s[b] - mub * lg;
+  const bool orig_ok = acceptable_wave(th, ph, theta_k[b], phi_k[b], gd[b], 0.0, switch_ok[b], theta_max[b],
+                                       ft + b * FMAX, fp + b * FMAX, nullptr);
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  const double pd_t = pd_error_wave(m, nf, nw, nullptr, J_s + b * (int64_t)nnz_rec, amap, row_slack, grad_s + b * n, 1,
+                                    free32, cs_tmp + b * m, wb, y + b * m, zL + b * nw, zU + b * nw, nullptr,
+                                    dy + b * m, dzL + b * nw, dzU + b * nw, as, hasL, hasU, wl0, wu0, mub);
+  const double pd_c = pd_error_wave(m, nf, nw, A + b * (int64_t)m * nw, nullptr, amap, row_slack, gradw + b * nw, 0,
+                                    free32, c + b * m, w + b * nw, y + b * m, zL + b * nw, zU + b * nw, nullptr,
+                                    nullptr, nullptr, nullptr, 0.0, hasL, hasU, wl0, wu0, mub);
+  const bool ok = isfinite(th) && isfinite(ph) && (orig_ok || pd_t <= SOFT_RESTO_FACTOR * pd_c);
+  if (ok) {
+    for (int r = lane; r < m; r += 64) st_g[b * m + r] = g_s[b * m + r];
+    for (int k = lane; k < nw; k += 64) st_w[b * nw + k] = wb[k];
+  }
+  if (lane == 0) {
+    if (ok) {
+      st_f[b] = f_s[b];
+      st_alpha[b] = as;
+      st_aug[b] = 0;
+      a_z[b] = as;
+    }
+    const bool left = ok && orig_ok;
+    if (left) in_soft[b] = 0;
+    else if (ok) in_soft[b] = 1;
+    if (left || (ok && !soft_now[b])) soft_cnt[b] = 0;
+  }
+}
+
+// the end of the regular line search: failed = no accepted point (-> the restoration phase),
+// moved = an accepted one; a failed search leaves the soft phase
+__global__ void k_fail(int64_t B, const uint8_t* __restrict__ act, const double* __restrict__ st_alpha,
+                       uint8_t* __restrict__ failed, uint8_t* __restrict__ moved, uint8_t* __restrict__ in_soft,
+                       int32_t* __restrict__ soft_cnt) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  rest[b] = failed[b] && ok_r[b];
-  alpha2[b] = 2.0 * alpha[b];
+  const bool a = act[b] != 0;
+  const bool f = a && !(st_alpha[b] > 0.0);
+  failed[b] = f ? 1 : 0;
+  moved[b] = (a && !f) ? 1 : 0;
+  if (f) {
+    in_soft[b] = 0;
+    soft_cnt[b] = 0;
+  }
 }
 
 // IPOPT's limited-memory quasi-Newton model (LimMemQuasiNewtonUpdater [IPOPT] with the defaults
@@ -534,23 +729,591 @@ __global__ __launch_bounds__(256) void k_lbfgs(int64_t B, int m, int nf, int nw,
   }
 }
 
-// the number of instances still active into one int (read by the host one iteration behind):
-// zeroed by k_count_zero at the iteration's start, one atomic per workgroup
-// up to COUNT1_MAX instances: one workgroup counts them and writes the count (no zeroing launch)
+// ---- the restoration phase (IPOPT MinC_1NrmRestorationPhase; batch_ipm.py enter_resto /
+// resto_step / leave_resto restate these kernels) -------------------------------------------
+// The restoration problem of an instance whose line search failed at w_R:
+//   min rho sum(p + n) + eta/2 |D_R (x - x_R)|^2  s.t.  c(w) - p + n = 0,  w in its bounds, p, n >= 0,
+// eta = sqrt(mu_R), D_R = diag(1 / max(1, |x_R|)) over x_free; solved by the same interior-point
+// method (its own barrier parameter, filter and line search; p and n eliminated from the Newton
+// system) until the original infeasibility falls to kappa_resto of its value at the start and the
+// point is acceptable to the original filter and to the iterate where the phase began.
+
+// Entry (RestoIterateInitializer): x_R = w; mu_R = max(mu, |c|inf); p, n from the closed form of the
+// barrier subproblem at fixed x (p - n = c, both positive); their bound multipliers mu_R / p,
+// mu_R / n; the x-bound multipliers min(rho, z); the original filter augmented with the current
+// point (PrepareRestoPhaseStart); an empty restoration filter; a fresh quasi-Newton model; and the
+// least-squares system of the constraint multipliers (W = I, Sigma_p = Sigma_n = 1) for
+// cpl_kkt_qd_solve: r1 = zLR - zUR, r2 = zp - zn, D^-1 = 1/2.
+__global__ __launch_bounds__(256) void k_resto_enter(
+    int64_t B, int m, int nw, const uint8_t* __restrict__ failed, const double* __restrict__ c,
+    const double* __restrict__ w, const double* __restrict__ zL, const double* __restrict__ zU,
+    const double* __restrict__ mu, const double* __restrict__ theta_k, const double* __restrict__ phi_k,
+    const uint8_t* __restrict__ hasL, const uint8_t* __restrict__ hasU, double* __restrict__ filt_t,
+    double* __restrict__ filt_p, int64_t* __restrict__ fcount, int64_t* __restrict__ iters,
+    uint8_t* __restrict__ in_resto, int64_t* __restrict__ n_resto, double* __restrict__ wR, double* __restrict__ pR,
+    double* __restrict__ nR, double* __restrict__ zp, double* __restrict__ zn, double* __restrict__ zLR,
+    double* __restrict__ zUR, double* __restrict__ muR, double* __restrict__ ftR, double* __restrict__ fpR,
+    int64_t* __restrict__ fcR, double* __restrict__ thmaxR, double* __restrict__ thminR,
+    double* __restrict__ th_o0, double* __restrict__ ph_o0, double* __restrict__ dwlR, uint8_t* __restrict__ lm_cnt,
+    uint8_t* __restrict__ lm_skip, double* __restrict__ Hq, int64_t lmc, double* __restrict__ Mw,
+    double* __restrict__ r1, double* __restrict__ r2, double* __restrict__ Dinv) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B || !failed[b]) return;
+  const int lane = threadIdx.x & 63;
+  const double mub = mu[b];
+  double cinf = 0.0;
+  for (int r = lane; r < m; r += 64) cinf = fmax(cinf, fabs(c[b * m + r]));
+  cinf = wave_max(cinf);
+  const double mr = fmax(mub, cinf);
+  double th = 0.0;
+  for (int r = lane; r < m; r += 64) {
+    const double cr = c[b * m + r];
+    const double a = (mr - RHO_R * cr) / (2.0 * RHO_R);
+    const double nv = a + sqrt(a * a + mr * cr / (2.0 * RHO_R));
+    const double pv = cr + nv;
+    pR[b * m + r] = pv;
+    nR[b * m + r] = nv;
+    zp[b * m + r] = mr / pv;
+    zn[b * m + r] = mr / nv;
+    th += fabs(cr - pv + nv);
+    r2[b * m + r] = mr / pv - mr / nv;
+    Dinv[b * m + r] = 0.5;
+  }
+  th = wave_sum(th);
+  for (int k = lane; k < nw; k += 64) {
+    wR[b * nw + k] = w[b * nw + k];
+    const double zl = hasL[k] ? fmin(zL[b * nw + k], RHO_R) : 0.0;
+    const double zu = hasU[k] ? fmin(zU[b * nw + k], RHO_R) : 0.0;
+    zLR[b * nw + k] = zl;
+    zUR[b * nw + k] = zu;
+    r1[b * nw + k] = zl - zu;
+    for (int j = 0; j < nw; ++j) Mw[(b * nw + k) * nw + j] = j == k ? 1.0 : 0.0;
+  }
+  for (int k = lane; k < FMAX; k += 64) {
+    ftR[b * FMAX + k] = INFINITY;
+    fpR[b * FMAX + k] = INFINITY;
+  }
+  // the original filter augmented with the point where the phase begins
+  const int64_t fc = fcount[b];
+  const int slot = (int)(fc % FMAX);
+  const double tk = theta_k[b], pk = phi_k[b];
+  if (lane == 0) {
+    filt_t[b * FMAX + slot] = (1.0 - GAMMA_TH) * tk;
+    filt_p[b * FMAX + slot] = pk - GAMMA_PHI * tk;
+    fcount[b] = fc + 1;
+    iters[b] += 1;
+    in_resto[b] = 1;
+    n_resto[b] += 1;
+    muR[b] = mr;
+    fcR[b] = 0;
+    thmaxR[b] = 1e4 * fmax(th, 1.0);
+    thminR[b] = 1e-4 * fmax(th, 1.0);
+    th_o0[b] = tk;
+    ph_o0[b] = pk;
+    dwlR[b] = 0.0;
+    lm_cnt[b] = 0;
+    lm_skip[b] = 0;
+    if (Hq) {  // (limited-memory mode only)
+      Hq[b * lmc] = 1.0;
+      Hq[b * lmc + 1] = 0.0;
+    }
+  }
+}
+
+// the least-squares estimate kept when |y|max <= constr_mult_init_max = 1e3
+__global__ __launch_bounds__(256) void k_resto_y0(int64_t B, int m, const uint8_t* __restrict__ failed,
+                                                  const double* __restrict__ dy, double* __restrict__ y) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B || !failed[b]) return;
+  const int lane = threadIdx.x & 63;
+  double mx = 0.0;
+  for (int r = lane; r < m; r += 64) mx = fmax(mx, fabs(dy[b * m + r]));
+  mx = wave_max(mx);
+  for (int r = lane; r < m; r += 64) y[b * m + r] = mx <= 1e3 ? dy[b * m + r] : 0.0;
+}
+
+// the restoration problem's optimality error (converged: a point of local infeasibility), its
+// monotone barrier update (resetting its filter) and the proximity term's gradient over w
+__global__ __launch_bounds__(256) void k_resto_prep1(
+    int64_t B, int m, int nf, int nw, int nbounds, double tol, double mu_min, uint8_t* __restrict__ active,
+    const uint8_t* __restrict__ in_resto, uint8_t* __restrict__ actR, int64_t* __restrict__ status,
+    const double* __restrict__ A, const double* __restrict__ c, const double* __restrict__ w,
+    const double* __restrict__ y, const double* __restrict__ wR, const double* __restrict__ pR,
+    const double* __restrict__ nR, const double* __restrict__ zp, const double* __restrict__ zn,
+    const double* __restrict__ zLR, const double* __restrict__ zUR, const uint8_t* __restrict__ hasL,
+    const uint8_t* __restrict__ hasU, const double* __restrict__ wl0, const double* __restrict__ wu0,
+    double* __restrict__ muR, double* __restrict__ ftR, double* __restrict__ fpR, int64_t* __restrict__ fcR,
+    double* __restrict__ tauR, double* __restrict__ gfR) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  const bool a = active[b] && in_resto[b];
+  if (!a) {
+    if (lane == 0) actR[b] = 0;
+    return;
+  }
+  const double* Ab = A + b * (int64_t)m * nw;
+  double mu = muR[b];
+  double eta = sqrt(mu);
+  double dmax = 0.0, zs = 0.0, cmax = 0.0, ys = 0.0, crmax = 0.0;
+  double clv[2] = {0, 0}, cuv[2] = {0, 0};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k = lane + 64 * h;
+    if (k < nw) {
+      const double wk = w[b * nw + k];
+      const double dr = k < nf ? 1.0 / fmax(fabs(wR[b * nw + k]), 1.0) : 0.0;
+      double dual = k < nf ? eta * (dr * dr) * (wk - wR[b * nw + k]) : 0.0;
+      for (int r = 0; r < m; ++r) dual += Ab[r * nw + k] * y[b * m + r];
+      const double zl = zLR[b * nw + k], zu = zUR[b * nw + k];
+      dual = dual - zl + zu;
+      dmax = fmax(dmax, fabs(dual));
+      zs += fabs(zl) + fabs(zu);
+      clv[h] = hasL[k] ? (wk - wl0[k]) * zl : 0.0;
+      cuv[h] = hasU[k] ? (wu0[k] - wk) * zu : 0.0;
+      cmax = fmax(cmax, fmax(clv[h], cuv[h]));
+    }
+  }
+  double cp[2] = {0, 0}, cn[2] = {0, 0};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = lane + 64 * h;
+    if (r < m) {
+      const double yr = y[b * m + r], pv = pR[b * m + r], nv = nR[b * m + r], zpv = zp[b * m + r], znv = zn[b * m + r];
+      dmax = fmax(dmax, fmax(fabs(RHO_R - yr - zpv), fabs(RHO_R + yr - znv)));
+      zs += fabs(zpv) + fabs(znv);
+      ys += fabs(yr);
+      crmax = fmax(crmax, fabs(c[b * m + r] - pv + nv));
+      cp[h] = pv * zpv;
+      cn[h] = nv * znv;
+      cmax = fmax(cmax, fmax(cp[h], cn[h]));
+    }
+  }
+  dmax = wave_max(dmax);
+  cmax = wave_max(cmax);
+  crmax = wave_max(crmax);
+  zs = wave_sum(zs);
+  ys = wave_sum(ys);
+  const int nbR = nbounds + 2 * m;
+  const double sd = fmax((ys + zs) / (double)max(m + nbR, 1), 100.0) / 100.0;
+  const double sc = fmax(zs / (double)max(nbR, 1), 100.0) / 100.0;
+  const double base = fmax(dmax / sd, crmax);
+  const double err0 = fmax(base, cmax / sc);
+  if (err0 <= tol) {  // the restoration problem converged: a point of local infeasibility
+    if (lane == 0) {
+      status[b] = CPL_SOLVE_INFEASIBLE;
+      active[b] = 0;
+      actR[b] = 0;
+    }
+    return;
+  }
+  bool reset = false;
+  for (int round = 0; round < MU_ROUNDS; ++round) {
+    double em = 0.0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = lane + 64 * h;
+      if (k < nw) {
+        if (hasL[k]) em = fmax(em, fabs(clv[h] - mu));
+        if (hasU[k]) em = fmax(em, fabs(cuv[h] - mu));
+      }
+      if (lane + 64 * h < m) em = fmax(em, fmax(fabs(cp[h] - mu), fabs(cn[h] - mu)));
+    }
+    em = wave_max(em);
+    if (fmax(base, em / sc) <= 10.0 * mu && mu > mu_min) {
+      mu = fmax(fmin(0.2 * mu, pow(mu, 1.5)), mu_min);
+      reset = true;
+    }
+  }
+  if (reset) {
+    for (int k = lane; k < FMAX; k += 64) {
+      ftR[b * FMAX + k] = INFINITY;
+      fpR[b * FMAX + k] = INFINITY;
+    }
+  }
+  eta = sqrt(mu);
+  for (int k = lane; k < nw; k += 64) {
+    const double dr = k < nf ? 1.0 / fmax(fabs(wR[b * nw + k]), 1.0) : 0.0;
+    gfR[b * nw + k] = k < nf ? eta * (dr * dr) * (w[b * nw + k] - wR[b * nw + k]) : 0.0;
+  }
+  if (lane == 0) {
+    actR[b] = 1;
+    muR[b] = mu;
+    tauR[b] = fmax(1.0 - mu, 0.99);
+    if (reset) fcR[b] = 0;
+  }
+}
+
+// after the Newton setup (M = diag(Sigma_R) + H_c, r1 = -(grad phi_R,w + A^T y)): the proximity
+// term's Hessian eta D_R^2 on M's diagonal, the eliminated p / n blocks (Sigma_p = zp / p,
+// Sigma_n = zn / n, D^-1 = 1 / (1/Sigma_p + 1/Sigma_n), r2 = -(c - p + n) + r_p / Sigma_p - r_n / Sigma_n)
+// and the restoration problem's theta and barrier objective phi_R
+__global__ __launch_bounds__(256) void k_resto_prep2(
+    int64_t B, int m, int nf, int nw, const uint8_t* __restrict__ actR, const double* __restrict__ c,
+    const double* __restrict__ w, const double* __restrict__ y, const double* __restrict__ wR,
+    const double* __restrict__ pR, const double* __restrict__ nR, const double* __restrict__ zp,
+    const double* __restrict__ zn, const double* __restrict__ muR, const uint8_t* __restrict__ hasL,
+    const uint8_t* __restrict__ hasU, const double* __restrict__ wl0, const double* __restrict__ wu0,
+    double* __restrict__ M, double* __restrict__ rp, double* __restrict__ rn, double* __restrict__ Dinv,
+    double* __restrict__ r2, double* __restrict__ thetaR, double* __restrict__ phiR) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B || !actR[b]) return;
+  const int lane = threadIdx.x & 63;
+  const double mu = muR[b], eta = sqrt(mu);
+  double prox = 0.0, lg = 0.0, th = 0.0, pn = 0.0, lpn = 0.0;
+  for (int k = lane; k < nw; k += 64) {
+    const double wk = w[b * nw + k];
+    if (k < nf) {
+      const double dr = 1.0 / fmax(fabs(wR[b * nw + k]), 1.0);
+      const double d2 = dr * dr;
+      M[(b * nw + k) * nw + k] += eta * d2;
+      const double dx = wk - wR[b * nw + k];
+      prox += d2 * (dx * dx);
+    }
+    if (hasL[k]) lg += log(wk - wl0[k]);
+    if (hasU[k]) lg += log(wu0[k] - wk);
+  }
+  for (int r = lane; r < m; r += 64) {
+    const double pv = pR[b * m + r], nv = nR[b * m + r], yr = y[b * m + r];
+    const double sp = zp[b * m + r] / pv, sn = zn[b * m + r] / nv;
+    const double a = -((RHO_R - mu / pv) - yr), q = -((RHO_R - mu / nv) + yr);
+    const double cr = c[b * m + r] - pv + nv;
+    rp[b * m + r] = a;
+    rn[b * m + r] = q;
+    Dinv[b * m + r] = 1.0 / (1.0 / sp + 1.0 / sn);
+    r2[b * m + r] = -cr + a / sp - q / sn;
+    th += fabs(cr);
+    pn += pv + nv;
+    lpn += log(pv) + log(nv);
+  }
+  prox = wave_sum(prox);
+  lg = wave_sum(lg);
+  th = wave_sum(th);
+  pn = wave_sum(pn);
+  lpn = wave_sum(lpn);
+  if (lane == 0) {
+    thetaR[b] = th;
+    phiR[b] = RHO_R * pn + 0.5 * eta * prox - mu * lg - mu * lpn;
+  }
+}
+
+// after the restoration Newton step: dp, dn, the bound-multiplier steps, the fraction-to-the-boundary
+// steps (primal over w, p, n; dual over zLR, zUR, zp, zn), gd = grad phi_R . (dw, dp, dn), the
+// switching condition, alpha_min and the line search's state
+__global__ __launch_bounds__(256) void k_resto_post(
+    int64_t B, int m, int nw, const uint8_t* __restrict__ actR, const double* __restrict__ w,
+    const double* __restrict__ dw, const double* __restrict__ dy, const double* __restrict__ gphi,
+    const double* __restrict__ pR, const double* __restrict__ nR, const double* __restrict__ zp,
+    const double* __restrict__ zn, const double* __restrict__ zLR, const double* __restrict__ zUR,
+    const double* __restrict__ rp, const double* __restrict__ rn, const double* __restrict__ muR,
+    const double* __restrict__ tauR, const uint8_t* __restrict__ hasL, const uint8_t* __restrict__ hasU,
+    const double* __restrict__ wl0, const double* __restrict__ wu0, const double* __restrict__ thetaR,
+    const double* __restrict__ thminR, const double* __restrict__ f, const double* __restrict__ g,
+    double* __restrict__ dp, double* __restrict__ dn, double* __restrict__ dzL, double* __restrict__ dzU,
+    double* __restrict__ dzp, double* __restrict__ dzn, double* __restrict__ a_max, double* __restrict__ a_z,
+    double* __restrict__ gdR, uint8_t* __restrict__ switchR, double* __restrict__ a_min,
+    uint8_t* __restrict__ searching, double* __restrict__ st_f, double* __restrict__ st_g, double* __restrict__ st_w,
+    double* __restrict__ st_p, double* __restrict__ st_n, double* __restrict__ st_alpha, uint8_t* __restrict__ st_aug,
+    double* __restrict__ alpha, uint8_t* __restrict__ any) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  if (b == 0 && lane == 0 && any) any[2] = 0;
+  if (!actR[b]) return;
+  const double mu = muR[b], t = tauR[b];
+  double rpmax = INFINITY, rz = INFINITY, gd = 0.0;
+  for (int k = lane; k < nw; k += 64) {
+    const double wk = w[b * nw + k], dk = dw[b * nw + k];
+    gd += gphi[b * nw + k] * dk;
+    double dzl = 0.0, dzu = 0.0;
+    if (hasL[k]) {
+      const double dl = wk - wl0[k], zl = zLR[b * nw + k];
+      dzl = mu / dl - zl - zl / dl * dk;
+      if (dk < 0.0) rpmax = fmin(rpmax, -t * dl / dk);
+      if (dzl < 0.0) rz = fmin(rz, -t * zl / dzl);
+    }
+    if (hasU[k]) {
+      const double du = wu0[k] - wk, zu = zUR[b * nw + k];
+      dzu = mu / du - zu + zu / du * dk;
+      if (dk > 0.0) rpmax = fmin(rpmax, -t * du / -dk);
+      if (dzu < 0.0) rz = fmin(rz, -t * zu / dzu);
+    }
+    dzL[b * nw + k] = dzl;
+    dzU[b * nw + k] = dzu;
+    st_w[b * nw + k] = wk;
+  }
+  for (int r = lane; r < m; r += 64) {
+    const double pv = pR[b * m + r], nv = nR[b * m + r], zpv = zp[b * m + r], znv = zn[b * m + r];
+    const double dyr = dy[b * m + r];
+    const double sp = zpv / pv, sn = znv / nv;
+    const double dpv = (rp[b * m + r] + dyr) / sp, dnv = (rn[b * m + r] - dyr) / sn;
+    const double dzpv = mu / pv - zpv - zpv / pv * dpv, dznv = mu / nv - znv - znv / nv * dnv;
+    dp[b * m + r] = dpv;
+    dn[b * m + r] = dnv;
+    dzp[b * m + r] = dzpv;
+    dzn[b * m + r] = dznv;
+    gd += (RHO_R - mu / pv) * dpv + (RHO_R - mu / nv) * dnv;
+    if (dpv < 0.0) rpmax = fmin(rpmax, -t * pv / dpv);
+    if (dnv < 0.0) rpmax = fmin(rpmax, -t * nv / dnv);
+    if (dzpv < 0.0) rz = fmin(rz, -t * zpv / dzpv);
+    if (dznv < 0.0) rz = fmin(rz, -t * znv / dznv);
+    st_g[b * m + r] = g[b * m + r];
+    st_p[b * m + r] = pv;
+    st_n[b * m + r] = nv;
+  }
+  rpmax = wave_min_d(rpmax);
+  rz = wave_min_d(rz);
+  gd = wave_sum(gd);
+  if (lane == 0) {
+    const double am = fmin(rpmax, 1.0);
+    a_max[b] = am;
+    a_z[b] = fmin(rz, 1.0);
+    gdR[b] = gd;
+    const double th = thetaR[b];
+    switchR[b] = (th <= thminR[b] && gd < 0.0) ? 1 : 0;
+    a_min[b] = alpha_min_of(th, gd, thminR[b]);
+    searching[b] = 1;
+    st_f[b] = f[b];
+    st_alpha[b] = 0.0;
+    st_aug[b] = 0;
+    alpha[b] = am;
+  }
+}
+
+// the restoration line search's acceptance test at one trial point (p, n along with w) and the take
+__global__ __launch_bounds__(256) void k_resto_judge(
+    int64_t B, int m, int nf, int nw, const uint8_t* __restrict__ searching_in, const int32_t* __restrict__ row_slack,
+    const double* __restrict__ gl, const uint8_t* __restrict__ hasL, const uint8_t* __restrict__ hasU,
+    const double* __restrict__ wl0, const double* __restrict__ wu0, const double* __restrict__ wt,
+    const double* __restrict__ f_t, const double* __restrict__ g_t, const double* __restrict__ alpha,
+    const double* __restrict__ pR, const double* __restrict__ nR, const double* __restrict__ dp,
+    const double* __restrict__ dn, const double* __restrict__ wR, const double* __restrict__ muR,
+    const double* __restrict__ thetaR, const double* __restrict__ phiR, const double* __restrict__ gdR,
+    const uint8_t* __restrict__ switchR, const double* __restrict__ thmaxR, const double* __restrict__ ftR,
+    const double* __restrict__ fpR, uint8_t* __restrict__ searching, double* __restrict__ st_f,
+    double* __restrict__ st_g, double* __restrict__ st_w, double* __restrict__ st_p, double* __restrict__ st_n,
+    double* __restrict__ st_alpha, uint8_t* __restrict__ st_aug) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B || !searching_in[b]) return;
+  const int lane = threadIdx.x & 63;
+  const double al = alpha[b], mu = muR[b], eta = sqrt(mu);
+  const double* wb = wt + b * nw;
+  double th = 0.0, pn = 0.0, lpn = 0.0, prox = 0.0, lg = 0.0;
+  for (int r = lane; r < m; r += 64) {
+    const double pt = pR[b * m + r] + al * dp[b * m + r], nt = nR[b * m + r] + al * dn[b * m + r];
+    th += fabs(cons_row(g_t + b * m, wb, nf, r, row_slack, gl) - pt + nt);
+    pn += pt + nt;
+    lpn += log(pt) + log(nt);
+  }
+  for (int k = lane; k < nw; k += 64) {
+    if (k < nf) {
+      const double dr = 1.0 / fmax(fabs(wR[b * nw + k]), 1.0);
+      const double dx = wb[k] - wR[b * nw + k];
+      prox += (dr * dr) * (dx * dx);
+    }
+    if (hasL[k]) lg += log(wb[k] - wl0[k]);
+    if (hasU[k]) lg += log(wu0[k] - wb[k]);
+  }
+  th = wave_sum(th);
+  pn = wave_sum(pn);
+  lpn = wave_sum(lpn);
+  prox = wave_sum(prox);
+  lg = wave_sum(lg);
+  const double ph = RHO_R * pn + 0.5 * eta * prox - mu * lg - mu * lpn;
+  bool h = false;
+  const bool ok = acceptable_wave(th, ph, thetaR[b], phiR[b], gdR[b], al, switchR[b], thmaxR[b], ftR + b * FMAX,
+                                  fpR + b * FMAX, &h);
+  if (!ok) return;
+  for (int r = lane; r < m; r += 64) {
+    st_g[b * m + r] = g_t[b * m + r];
+    st_p[b * m + r] = pR[b * m + r] + al * dp[b * m + r];
+    st_n[b * m + r] = nR[b * m + r] + al * dn[b * m + r];
+  }
+  for (int k = lane; k < nw; k += 64) st_w[b * nw + k] = wb[k];
+  if (lane == 0) {
+    st_f[b] = f_t[b];
+    st_alpha[b] = al;
+    st_aug[b] = h ? 1 : 0;
+    searching[b] = 0;
+  }
+}
+
+// the restoration iteration's acceptance: a failed line search ends the instance (restoration
+// failed); otherwise y, the bound multipliers (kappa_Sigma safeguard at mu_R), p, n, w, the
+// restoration filter; then the return test (RestoConvergenceCheck: the original theta at most
+// kappa_resto of its value where the phase began, the point acceptable to the original filter and
+// to that iterate) and the return (ComputeBoundMultiplierStep for the original bound multipliers, a
+// reset to 1 when any exceeds 1000, y = 0, a fresh quasi-Newton model)
+__global__ __launch_bounds__(256) void k_resto_accept(
+    int64_t B, int m, int nf, int nw, const uint8_t* __restrict__ actR, uint8_t* __restrict__ movedR,
+    uint8_t* __restrict__ active, int64_t* __restrict__ status, int64_t* __restrict__ iters,
+    const double* __restrict__ st_alpha, const uint8_t* __restrict__ st_aug, const double* __restrict__ st_w,
+    const double* __restrict__ st_p, const double* __restrict__ st_n, const double* __restrict__ dy,
+    const double* __restrict__ dzL, const double* __restrict__ dzU, const double* __restrict__ dzp,
+    const double* __restrict__ dzn, const double* __restrict__ a_z, const double* __restrict__ muR,
+    const double* __restrict__ thetaR, const double* __restrict__ phiR, double* __restrict__ ftR,
+    double* __restrict__ fpR, int64_t* __restrict__ fcR, double* __restrict__ w, double* __restrict__ y,
+    double* __restrict__ pR, double* __restrict__ nR, double* __restrict__ zp, double* __restrict__ zn,
+    double* __restrict__ zLR, double* __restrict__ zUR, const uint8_t* __restrict__ hasL,
+    const uint8_t* __restrict__ hasU, const double* __restrict__ wl0, const double* __restrict__ wu0,
+    const int32_t* __restrict__ row_slack, const double* __restrict__ gl, const double* __restrict__ f_n,
+    const double* __restrict__ g_n, const double* __restrict__ mu, const double* __restrict__ filt_t,
+    const double* __restrict__ filt_p, const double* __restrict__ th_o0, const double* __restrict__ ph_o0,
+    const double* __restrict__ wR, double* __restrict__ zL, double* __restrict__ zU, uint8_t* __restrict__ in_resto,
+    int64_t* __restrict__ acc, uint8_t* __restrict__ lm_cnt, uint8_t* __restrict__ lm_skip, double* __restrict__ Hq,
+    int64_t lmc) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  if (!actR[b]) {
+    if (lane == 0) movedR[b] = 0;
+    return;
+  }
+  const double al = st_alpha[b];
+  if (!(al > 0.0)) {  // the restoration phase's line search failed
+    if (lane == 0) {
+      movedR[b] = 0;
+      status[b] = CPL_SOLVE_RESTO_FAILED;
+      active[b] = 0;
+      iters[b] += 1;
+    }
+    return;
+  }
+  const double mur = muR[b], az = a_z[b];
+  for (int r = lane; r < m; r += 64) {
+    y[b * m + r] += al * dy[b * m + r];
+    const double pn = st_p[b * m + r], nn = st_n[b * m + r];
+    zp[b * m + r] = fmin(fmax(zp[b * m + r] + az * dzp[b * m + r], mur / (KAPPA_SIGMA * pn)), KAPPA_SIGMA * mur / pn);
+    zn[b * m + r] = fmin(fmax(zn[b * m + r] + az * dzn[b * m + r], mur / (KAPPA_SIGMA * nn)), KAPPA_SIGMA * mur / nn);
+    pR[b * m + r] = pn;
+    nR[b * m + r] = nn;
+  }
+  for (int k = lane; k < nw; k += 64) {
+    const double wn = st_w[b * nw + k];
+    if (hasL[k]) {
+      const double dl = wn - wl0[k];
+      zLR[b * nw + k] = fmin(fmax(zLR[b * nw + k] + az * dzL[b * nw + k], mur / (KAPPA_SIGMA * dl)), KAPPA_SIGMA * mur / dl);
+    }
+    if (hasU[k]) {
+      const double du = wu0[k] - wn;
+      zUR[b * nw + k] = fmin(fmax(zUR[b * nw + k] + az * dzU[b * nw + k], mur / (KAPPA_SIGMA * du)), KAPPA_SIGMA * mur / du);
+    }
+    w[b * nw + k] = wn;
+  }
+  if (lane == 0) {
+    movedR[b] = 1;
+    iters[b] += 1;
+    if (st_aug[b]) {
+      const int64_t fc = fcR[b];
+      const int slot = (int)(fc % FMAX);
+      const double tk = thetaR[b], pk = phiR[b];
+      ftR[b * FMAX + slot] = (1.0 - GAMMA_TH) * tk;
+      fpR[b * FMAX + slot] = pk - GAMMA_PHI * tk;
+      fcR[b] = fc + 1;
+    }
+  }
+  // ---- back to the regular iteration?
+  const double mub = mu[b];
+  double th = 0.0, lg = 0.0;
+  for (int r = lane; r < m; r += 64) th += fabs(cons_row(g_n + b * m, st_w + b * nw, nf, r, row_slack, gl));
+  for (int k = lane; k < nw; k += 64) {
+    const double wn = st_w[b * nw + k];
+    if (hasL[k]) lg += log(wn - wl0[k]);
+    if (hasU[k]) lg += log(wu0[k] - wn);
+  }
+  th = wave_sum(th);
+  lg = wave_sum(lg);
+  const double ph = f_n[b] - mub * lg;
+  bool rejected = false;
+  for (int k = lane; k < FMAX; k += 64) rejected |= !((th <= filt_t[b * FMAX + k]) || (ph <= filt_p[b * FMAX + k]));
+  const bool in_filter = __ballot(rejected) == 0;
+  const double t0 = th_o0[b];
+  const bool vs_start = (th <= (1.0 - GAMMA_TH) * t0) || (ph <= ph_o0[b] - GAMMA_PHI * t0);
+  const bool back = isfinite(th) && isfinite(ph) && th <= KAPPA_RESTO * t0 && in_filter && vs_start;
+  if (!back) return;
+  const double tau = fmax(1.0 - mub, 0.99);
+  double ad = INFINITY;
+  double dzl[2] = {0, 0}, dzu[2] = {0, 0};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k = lane + 64 * h;
+    if (k < nw) {
+      const double wr = wR[b * nw + k], wn = st_w[b * nw + k];
+      if (hasL[k]) {
+        const double s0 = wr - wl0[k], s1 = wn - wl0[k], z = zL[b * nw + k];
+        dzl[h] = (z * (s0 - s1) + mub) / s0 - z;
+        if (dzl[h] < 0.0) ad = fmin(ad, -tau * z / dzl[h]);
+      }
+      if (hasU[k]) {
+        const double s0 = wu0[k] - wr, s1 = wu0[k] - wn, z = zU[b * nw + k];
+        dzu[h] = (z * (s0 - s1) + mub) / s0 - z;
+        if (dzu[h] < 0.0) ad = fmin(ad, -tau * z / dzu[h]);
+      }
+    }
+  }
+  ad = fmin(wave_min_d(ad), 1.0);
+  double zmax = -INFINITY, zl_n[2] = {0, 0}, zu_n[2] = {0, 0};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k = lane + 64 * h;
+    if (k < nw) {
+      zl_n[h] = hasL[k] ? zL[b * nw + k] + ad * dzl[h] : zL[b * nw + k];
+      zu_n[h] = hasU[k] ? zU[b * nw + k] + ad * dzu[h] : zU[b * nw + k];
+      zmax = fmax(zmax, fmax(zl_n[h], zu_n[h]));
+    }
+  }
+  zmax = wave_max(zmax);
+  const bool big = zmax > BOUND_MULT_RESET;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k = lane + 64 * h;
+    if (k < nw) {
+      zL[b * nw + k] = (big && hasL[k]) ? 1.0 : zl_n[h];
+      zU[b * nw + k] = (big && hasU[k]) ? 1.0 : zu_n[h];
+    }
+  }
+  for (int r = lane; r < m; r += 64) y[b * m + r] = 0.0;
+  if (lane == 0) {
+    in_resto[b] = 0;
+    acc[b] = 0;
+    lm_cnt[b] = 0;
+    lm_skip[b] = 0;
+    if (Hq) {  // (limited-memory mode only)
+      Hq[b * lmc] = 1.0;
+      Hq[b * lmc + 1] = 0.0;
+    }
+  }
+}
+
+// the number of instances still active, and of those in the restoration phase, into two ints
+// (read by the host after each iteration): up to COUNT1_MAX instances one workgroup counts them
 constexpr int64_t COUNT1_MAX = 65536;
 __global__ __launch_bounds__(1024) void k_count1(int64_t B, const uint8_t* __restrict__ active,
-                                                 int32_t* __restrict__ count) {
-  __shared__ int s_w[16];
-  int c = 0;
-  for (int64_t b = threadIdx.x; b < B; b += 1024) c += active[b] ? 1 : 0;
+                                                 const uint8_t* __restrict__ in_resto, int32_t* __restrict__ count) {
+  __shared__ int s_w[16], s_r[16];
+  int c = 0, cr = 0;
+  for (int64_t b = threadIdx.x; b < B; b += 1024) {
+    c += active[b] ? 1 : 0;
+    cr += (active[b] && in_resto[b]) ? 1 : 0;
+  }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c;
+  for (int o = 32; o > 0; o >>= 1) {
+    c += __shfl_xor(c, o);
+    cr += __shfl_xor(cr, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s_w[threadIdx.x >> 6] = c;
+    s_r[threadIdx.x >> 6] = cr;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    int t = 0;
-    for (int q = 0; q < 16; ++q) t += s_w[q];
+    int t = 0, tr = 0;
+    for (int q = 0; q < 16; ++q) {
+      t += s_w[q];
+      tr += s_r[q];
+    }
     count[0] = t;
+    count[1] = tr;
   }
 }
 // the accepted point's f, grad, g and Jacobian records into the iterate's, active instances only:
@@ -575,18 +1338,26 @@ __global__ __launch_bounds__(256) void k_accept_rows(int64_t B, int n, int m, in
   J[b * nnz + q] = J_n[b * nnz + q];
 }
 __global__ void k_count_zero(int32_t* __restrict__ count) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) count[0] = 0;
+  if (threadIdx.x == 0 && blockIdx.x == 0) count[0] = count[1] = 0;
 }
-__global__ __launch_bounds__(256) void k_count(int64_t B, const uint8_t* __restrict__ active, int32_t* __restrict__ count) {
-  __shared__ int s_cnt;
-  if (threadIdx.x == 0) s_cnt = 0;
+__global__ __launch_bounds__(256) void k_count(int64_t B, const uint8_t* __restrict__ active,
+                                               const uint8_t* __restrict__ in_resto, int32_t* __restrict__ count) {
+  __shared__ int s_cnt[2];
+  if (threadIdx.x < 2) s_cnt[threadIdx.x] = 0;
   __syncthreads();
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int a = (b < B && active[b]) ? 1 : 0;
-  const unsigned long long bal = __ballot(a);
-  if ((threadIdx.x & 63) == 0 && bal) atomicAdd(&s_cnt, __popcll(bal));
+  const int r = (a && in_resto[b]) ? 1 : 0;
+  const unsigned long long bal = __ballot(a), balr = __ballot(r);
+  if ((threadIdx.x & 63) == 0) {
+    if (bal) atomicAdd(&s_cnt[0], __popcll(bal));
+    if (balr) atomicAdd(&s_cnt[1], __popcll(balr));
+  }
   __syncthreads();
-  if (threadIdx.x == 0 && s_cnt) atomicAdd(count, s_cnt);
+  if (threadIdx.x == 0) {
+    if (s_cnt[0]) atomicAdd(count, s_cnt[0]);
+    if (s_cnt[1]) atomicAdd(count + 1, s_cnt[1]);
+  }
 }
 
 // ---- active-set compaction (the lock-step batch shrinks to its active instances) ----------
@@ -638,9 +1409,11 @@ __global__ __launch_bounds__(256) void k_scatter_final(int64_t rows, int n, int 
                                                        const double* __restrict__ w, const double* __restrict__ y,
                                                        const double* __restrict__ Xbase, const double* __restrict__ d_inf,
                                                        const int64_t* __restrict__ status, const int64_t* __restrict__ iters,
+                                                       const int64_t* __restrict__ n_resto,
                                                        double* __restrict__ fw, double* __restrict__ fy,
                                                        double* __restrict__ fX, double* __restrict__ fdinf,
-                                                       int64_t* __restrict__ fstatus, int64_t* __restrict__ fiters) {
+                                                       int64_t* __restrict__ fstatus, int64_t* __restrict__ fiters,
+                                                       int64_t* __restrict__ fresto) {
   const int64_t r = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
   if (r >= rows) return;
   const int32_t o = orig[r];
@@ -653,7 +1426,15 @@ __global__ __launch_bounds__(256) void k_scatter_final(int64_t rows, int n, int 
     fdinf[o] = d_inf[r];
     fstatus[o] = status[r];
     fiters[o] = iters[r];
+    fresto[o] = n_resto[r];
   }
+}
+
+// the restoration-phase instances whose trial was accepted in the current search
+__global__ void k_moved_r(int64_t B, const uint8_t* __restrict__ actR, const double* __restrict__ st_alpha,
+                          uint8_t* __restrict__ movedR) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) movedR[b] = actR[b] && st_alpha[b] > 0.0;
 }
 
 __global__ void k_gather_i32(int64_t k, const int32_t* __restrict__ pos, const int32_t* __restrict__ src,
@@ -729,50 +1510,56 @@ struct Arena {
 
 struct cpl_solver {
   cpl_problem_desc desc;
+  cpl_problem_desc desc_R;  // the template with zero cost weights: y^T g's Hessian for the restoration phase
   cpl_solve_options opt;
   int64_t B = 0;
   int64_t Bcur = 0;  // rows in play: B, shrunk by active-set compaction
   int n = 0, m = 0, nnz = 0, nnz_rec = 0, nf = 0, nI = 0, nw = 0, nbounds = 0;
   bool analytic_H = false, bfgs = false, fd = false, fd_fused = true;
+  double mu_min = 0.0;
   hipStream_t stream = nullptr;
-  hipGraph_t graph = nullptr;  // the graph of the current (Bcur, mass / tag presence)
-  hipGraphExec_t gexec = nullptr;
-  std::map<int64_t, std::pair<hipGraph_t, hipGraphExec_t>> graphs;  // every captured size
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  uint8_t* h_flag = nullptr;  // pinned, 2 bytes
+  bool captured = false;  // an iteration graph exists
+  std::map<int64_t, std::pair<hipGraph_t, hipGraphExec_t>> graphs;  // (size, inputs, phase) -> graph
+  uint8_t* h_flag = nullptr;  // pinned: the device's 4 flag bytes
   cpl::Arena arena;
   const double* mass = nullptr;       // per solve
   const uint8_t* tag = nullptr;
-  int64_t evals_per_step = 0;
   // problem constants (device)
   int32_t *free32, *ineq_row, *row_slack, *freepos, *amap, *col_ptr, *csc_k, *csc_row;
   int64_t *free64, *fixed64;
-  uint8_t *is_fixed, *hasL, *hasU;
+  uint8_t *is_fixed, *hasL, *hasU, *zeros_u8;
   double *xl, *xu, *gl, *gu, *wl0, *wu0, *zeros_w, *zeros_B;
   // state
   double *Xbase, *w, *y, *zL, *zU, *mu, *filt_t, *filt_p, *dwl, *f, *grad, *g, *J, *d_inf, *Hq, *lm_s, *lm_y, *theta_max,
       *theta_min;
-  int64_t *status, *iters, *acc, *fcount;
-  uint8_t *active, *lm_cnt, *lm_skip, *d_any;
+  int64_t *status, *iters, *acc, *fcount, *n_resto;
+  uint8_t *active, *lm_cnt, *lm_skip, *d_any, *in_soft, *tiny_last, *tiny_flag, *in_resto;
+  int32_t* soft_cnt;
+  // restoration state
+  double *wR, *pR, *nR, *zp, *zn, *zLR, *zUR, *muR, *ftR, *fpR, *th_o0, *ph_o0, *dwlR, *thmaxR, *thminR;
+  int64_t* fcR;
   // iteration temporaries
-  double *A, *gradw, *gradw_new, *c, *err0, *base, *mu_o, *ft, *fp, *tau, *X, *H, *M, *Mr, *r1, *r2, *gphi,
-      *mr_diag, *theta_k, *phi_k, *dw, *dy, *delta_w, *delta_c, *dzL, *dzU, *a_max, *a_z, *gd, *ws;
+  double *A, *gradw, *gradw_new, *c, *err0, *base, *mu_o, *ft, *fp, *tau, *X, *H, *M, *Kqd, *r1, *r2, *gphi,
+      *mr_diag, *theta_k, *phi_k, *dw, *dy, *delta_w, *delta_c, *dzL, *dzU, *a_max, *a_z, *gd, *ws, *a_min, *a_soft,
+      *cs_tmp, *scr1, *scr2;
   int64_t* fc;
   int32_t* info;
-  uint8_t *act, *switch_ok, *searching, *st_aug, *ok, *soc, *ok_s, *failed, *ok_r, *rest;
-  double *st_f, *st_g, *st_w, *st_alpha, *alpha, *alpha2, *th, *wt, *Xt, *f_t, *g_t;
+  uint8_t *act, *switch_ok, *searching, *st_aug, *ok, *soc, *ok_s, *failed, *moved, *tiny_now, *soft_now, *soft_try;
+  double *st_f, *st_g, *st_w, *st_alpha, *alpha, *th, *wt, *Xt, *f_t, *g_t;
   double *c_soc, *a_soc, *th_old, *r2s, *dws, *dys, *ws_, *Xs, *f_s, *g_s, *th_s;
-  double *negc, *dwr, *dyr, *dwr_d, *dcr, *ar, *wr, *Xr, *f_r, *g_r, *th_r;
-  int32_t* infor;
   double *Xn, *f_n, *grad_n, *g_n, *J_n, *Xp, *hfd, *gL, *mass_fd, *jac_fd, *grad_fd;
   uint8_t* tag_fd;
+  // restoration temporaries
+  double *gfR, *tauR, *rp, *rn, *Dinv, *dp, *dn, *dzp, *dzn, *st_p, *st_n, *thetaR, *phiR, *gdR, *a_maxR, *a_zR,
+      *a_minR, *alphaR;
+  uint8_t *actR, *movedR, *searchingR, *switchR;
   double *fin_f, *fin_g;
   int32_t *st32, *it32;
   // compaction: original instance of each row, compacted masses / tags, full-batch results
   int32_t *orig, *pos, *d_count, *h_count = nullptr;
   double *mass_c, *fw, *fy, *fX, *fdinf;
   uint8_t* tag_c;
-  int64_t *fstatus, *fiters;
+  int64_t *fstatus, *fiters, *fresto;
   uint64_t* scratch;
   int64_t scratch_words = 0;
   int32_t compactions = 0;
@@ -799,37 +1586,78 @@ int32_t eval_full(cpl_solver* S, const double* X, double* fo, double* grado, dou
                            S->stream);
 }
 
-// One lock-step iteration of every instance (graph-capturable: no host synchronisation), in three
-// phases: A = the Newton step and the first line-search trial with its second-order correction
-// (+ the any-searching flag when `flag`), B = the remaining trials and the feasibility step, C = the
-// accepted point's evaluation and the state update.  Small batches run them as separate graphs and
-// skip B when no instance is still searching after A (the usual case: B is ~25 masked launches).
-int32_t step_phase(cpl_solver* S, int phase, bool flag);
-int32_t step(cpl_solver* S) {
-  CK(step_phase(S, 1, false));
-  CK(step_phase(S, 2, false));
-  return step_phase(S, 3, false);
+// The phases of one lock-step iteration (each graph-capturable, no host synchronisation inside):
+//   P_NEWTON  the convergence test, barrier update, Newton step, tiny-step test, the first trial
+//             with its second-order corrections (flags: any still searching / any soft candidate)
+//   P_TRIAL   one more backtracking trial (launched while an instance is still searching)
+//   P_SOFT    IPOPT's soft restoration step (launched when an instance found no acceptable trial)
+//   P_ACCEPT  the accepted points' evaluation, L-BFGS, the state update, the restoration phase's
+//             entry for failed searches, the active / restoration counts
+//   P_RNEWTON the restoration phase's Newton step and first trial (launched when instances are in it)
+//   P_RTRIAL  one more restoration trial
+//   P_RACCEPT the restoration iteration's acceptance and the return test
+// Per iteration: P_NEWTON, P_TRIAL*, [P_SOFT], [P_RNEWTON, P_RTRIAL*, P_RACCEPT], P_ACCEPT.
+enum Phase { P_NEWTON = 1, P_TRIAL, P_SOFT, P_ACCEPT, P_RNEWTON, P_RTRIAL, P_RACCEPT, P_COUNT };
+
+int32_t hessian_into(cpl_solver* S, const cpl_problem_desc* d, const uint8_t* mask, const double** Hblk, int* h_sym) {
+  const int64_t B = S->Bcur;
+  const int n = S->n, nf = S->nf;
+  hipStream_t st = S->stream;
+  const cpl_solve_options& o = S->opt;
+  *Hblk = nullptr;
+  *h_sym = 0;
+  if (S->bfgs) return CPL_OK;  // the compact model is expanded inside the Newton setup
+  if (S->analytic_H) {
+    CK(cpl_lagrangian_hessian(d, B, S->X, S->y, mask, S->free32, nf, S->H, st));
+    *Hblk = S->H;
+    return CPL_OK;
+  }
+  // central differences of grad f + J^T y (the 2 nf points of every instance in one launch)
+  CK(cpl_ipm_fd_points(B, n, nf, o.fd_step, S->freepos, S->X, S->Xp, S->hfd, mask, st));
+  int32_t rc = CPL_ERR_UNSUPPORTED;
+  if (S->fd_fused)
+    rc = cpl_eval_lagrangian_grad(d, B * 2 * nf, S->Xp, S->mass ? S->mass_fd : nullptr, S->tag ? S->tag_fd : nullptr,
+                                  S->col_ptr, S->csc_k, S->csc_row, S->y, 2 * nf, mask, S->gL, st);
+  if (rc == CPL_ERR_UNSUPPORTED) {  // Superquadric / mixed: eval + J^T y in two launches
+    S->fd_fused = false;
+    CK(cpl_eval_batch(d, B * 2 * nf, S->Xp, S->mass ? S->mass_fd : nullptr, S->tag ? S->tag_fd : nullptr, nullptr,
+                      S->jac_fd, nullptr, S->grad_fd, st));
+    CK(cpl_lagrangian_grad(B * 2 * nf, n, S->m, S->nnz, S->col_ptr, S->csc_k, S->csc_row, S->grad_fd, S->jac_fd, S->y,
+                           2 * nf, S->gL, st));
+  } else {
+    CK(rc);
+  }
+  CK(cpl_ipm_fd_hessian_raw(B, n, nf, S->free64, S->gL, S->hfd, S->H, mask, st));
+  *Hblk = S->H;
+  *h_sym = 1;
+  return CPL_OK;
 }
-int32_t step_phase(cpl_solver* S, int phase, bool flag) {
+
+int32_t step_phase(cpl_solver* S, int phase) {
   const int64_t B = S->Bcur;
   const int n = S->n, m = S->m, nf = S->nf, nw = S->nw;
   hipStream_t st = S->stream;
   const cpl_solve_options& o = S->opt;
+  const int64_t lmc = S->bfgs ? LMC(nf) : 0;
   auto judge = [&](const double* wt, const double* ft_, const double* gt_, const double* al, const uint8_t* extra,
-                   double* th, uint8_t* ok, int mode) {
+                   double* th, uint8_t* ok) {
     return cpl_ipm_judge_take(B, nw, m, nf, FMAX, S->row_slack, S->gl, S->hasL, S->hasU, S->wl0, S->wu0, wt, ft_, gt_,
                               al, S->mu_o, S->theta_k, S->phi_k, S->gd, S->switch_ok, S->theta_max, S->ft, S->fp,
-                              extra, S->searching, S->st_f, S->st_g, S->st_w, S->st_alpha, S->st_aug, th, ok, mode,
-                              st);
+                              extra, S->searching, S->st_f, S->st_g, S->st_w, S->st_alpha, S->st_aug, th, ok, 0, st);
   };
-  const int nls = o.max_ls > 0 ? o.max_ls : 1;
-  // one trial of the filter line search (ls == 0: with the second-order correction), then the halving
-  auto trial = [&](int ls, bool any) -> int32_t {
+  auto halve = [&](uint8_t* searching, double* alpha, const double* a_min, int fi, bool soft) -> int32_t {
+    hipLaunchKernelGGL(k_halve2, dim3(blocks_elems(B)), dim3(256), 0, st, B, searching, alpha, a_min, S->act,
+                       S->tiny_now, soft ? S->soft_now : nullptr, S->soft_cnt, S->st_alpha, S->d_any, fi);
+    LAUNCHED("k_halve2");
+    return CPL_OK;
+  };
+  // one regular backtracking trial: the point, f and g there, IPOPT's acceptance test and the take
+  auto trial = [&](bool first) -> int32_t {
     CK(cpl_ipm_trial_point(B, n, nf, nw, S->free64, S->fixed64, S->Xbase, S->w, S->dw, S->alpha, S->searching,
                            S->st_w, S->wt, S->Xt, st));
     CK(eval_fg(S, S->Xt, S->f_t, S->g_t));
-    CK(judge(S->wt, S->f_t, S->g_t, S->alpha, nullptr, S->th, S->ok, 0));
-    if (ls == 0 && o.max_soc > 0) {
+    CK(judge(S->wt, S->f_t, S->g_t, S->alpha, nullptr, S->th, S->ok));
+    if (first && o.max_soc > 0) {  // second-order corrections on the first trial (IPOPT's max_soc)
       const double *cg = S->g_t, *cw = S->wt;
       for (int q = 0; q < o.max_soc; ++q) {
         if (q == 0) {
@@ -849,13 +1677,7 @@ int32_t step_phase(cpl_solver* S, int phase, bool flag) {
         CK(cpl_ipm_trial_point(B, n, nf, nw, S->free64, S->fixed64, S->Xbase, S->w, S->dws, S->a_soc, S->soc, S->st_w,
                                S->ws_, S->Xs, st));
         CK(eval_fg(S, S->Xs, S->f_s, S->g_s));
-        CK(judge(S->ws_, S->f_s, S->g_s, S->alpha, S->soc, S->th_s, S->ok_s, 0));
-        if (q + 1 == o.max_soc) {  // the last correction: its bookkeeping with the halving
-          hipLaunchKernelGGL(k_soc_after_halve, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->soc, S->ok_s, S->th_s,
-                             S->th_old, S->searching, S->alpha, any ? S->d_any : nullptr);
-          LAUNCHED("k_soc_after_halve");
-          return CPL_OK;
-        }
+        CK(judge(S->ws_, S->f_s, S->g_s, S->alpha, S->soc, S->th_s, S->ok_s));
         hipLaunchKernelGGL(k_soc_after, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->soc, S->ok_s, S->th_s,
                            S->th_old);
         LAUNCHED("k_soc_after");
@@ -863,137 +1685,192 @@ int32_t step_phase(cpl_solver* S, int phase, bool flag) {
         cw = S->ws_;
       }
     }
-    hipLaunchKernelGGL(k_halve, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->searching, S->alpha);
-    LAUNCHED("k_halve");
-    if (any) {
-      hipLaunchKernelGGL(k_any_searching, dim3(1), dim3(256), 0, st, B, S->searching, S->d_any);
-      LAUNCHED("k_any_searching");
-    }
-    return CPL_OK;
+    return halve(S->searching, S->alpha, S->a_min, 0, true);
   };
-  if (phase == 1) {
-    // optimality error, convergence test, barrier update (filters reset where mu changed)
-    if (B > COUNT1_MAX) {  // (k_count accumulates with atomics; small batches use k_count1 at the end)
-      hipLaunchKernelGGL(k_count_zero, dim3(1), dim3(64), 0, st, S->d_count);
-      LAUNCHED("k_count_zero");
+  // one restoration trial: the point (w along dw; p, n in the judge), f and g, the test and the take
+  auto rtrial = [&]() -> int32_t {
+    CK(cpl_ipm_trial_point(B, n, nf, nw, S->free64, S->fixed64, S->Xbase, S->w, S->dw, S->alphaR, S->searchingR,
+                           S->st_w, S->wt, S->Xt, st));
+    CK(eval_fg(S, S->Xt, S->f_t, S->g_t));
+    hipLaunchKernelGGL(k_resto_judge, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nf, nw, S->searchingR, S->row_slack,
+                       S->gl, S->hasL, S->hasU, S->wl0, S->wu0, S->wt, S->f_t, S->g_t, S->alphaR, S->pR, S->nR, S->dp,
+                       S->dn, S->wR, S->muR, S->thetaR, S->phiR, S->gdR, S->switchR, S->thmaxR, S->ftR, S->fpR,
+                       S->searchingR, S->st_f, S->st_g, S->st_w, S->st_p, S->st_n, S->st_alpha, S->st_aug);
+    LAUNCHED("k_resto_judge");
+    return halve(S->searchingR, S->alphaR, S->a_minR, 2, false);
+  };
+
+  switch (phase) {
+    case P_NEWTON: {
+      CK(cpl_ipm_dense_a(B, m, nw, nf, S->nnz_rec, S->amap, S->row_slack, S->J, S->A, S->active, st));
+      hipLaunchKernelGGL(k_prep, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->free32, S->row_slack,
+                         S->gl, S->grad, S->g, S->w, S->gradw, S->c);
+      LAUNCHED("k_prep");
+      CK(ipm_optimality_ex(B, nw, m, FMAX, S->nbounds, o.tol, o.acceptable_tol, o.acceptable_iter, S->A, S->gradw,
+                           S->c, S->w, S->y, S->zL, S->zU, S->hasL, S->hasU, S->wl0, S->wu0, S->mu, S->filt_t,
+                           S->filt_p, S->fcount, S->active, S->status, S->acc, S->d_inf, S->err0, S->base, S->mu_o,
+                           S->ft, S->fp, S->fc, MU_ROUNDS, S->mu_min, S->tiny_flag, S->in_resto, st));
+      hipLaunchKernelGGL(k_unpack_tau, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, nw, S->freepos, S->Xbase,
+                         S->w, S->mu_o, S->active, S->in_resto, S->X, S->tau, S->act);
+      LAUNCHED("k_unpack_tau");
+      const double* Hblk = nullptr;
+      int h_sym = 0;
+      CK(hessian_into(S, &S->desc, S->act, &Hblk, &h_sym));
+      if (S->bfgs)
+        CK(ipm_newton_setup_lm(B, nw, m, nf, S->w, S->zL, S->zU, S->gradw, S->A, S->y, S->c, S->f, S->mu_o, S->hasL,
+                               S->hasU, S->wl0, S->wu0, S->Hq, LM_HIST, S->M, S->r1, S->r2, S->gphi, S->mr_diag,
+                               S->theta_k, S->phi_k, S->act, st));
+      else
+        CK(cpl_ipm_newton_setup(B, nw, m, nf, S->w, S->zL, S->zU, S->gradw, S->A, S->y, S->c, S->f, S->mu_o, S->hasL,
+                                S->hasU, S->wl0, S->wu0, Hblk, h_sym, S->M, S->r1, S->r2, S->gphi, S->mr_diag,
+                                S->theta_k, S->phi_k, S->act, st));
+      CK(cpl_kkt_solve(0, B, nw, m, S->M, S->A, S->r1, S->r2, S->mu_o, S->dwl, S->act, S->dw, S->dy, S->delta_w,
+                       S->delta_c, S->info, S->ws, st));
+      CK(cpl_ipm_post_step(B, nw, S->w, S->dw, S->zL, S->zU, S->gphi, S->mu_o, S->tau, S->hasL, S->hasU, S->wl0,
+                           S->wu0, S->theta_k, S->theta_min, S->act, S->delta_w, S->dwl, S->dzL, S->dzU, S->a_max,
+                           S->a_z, S->gd, S->switch_ok, st));
+      hipLaunchKernelGGL(k_ls_setup, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nw, S->act, S->w, S->dw, S->dy, S->c,
+                         S->f, S->g, S->theta_k, S->gd, S->theta_min, S->a_max, S->in_soft, S->soft_cnt, S->tiny_last,
+                         S->tiny_flag, S->tiny_now, S->soft_now, S->a_min, S->searching, S->st_f, S->st_g, S->st_w,
+                         S->st_alpha, S->st_aug, S->alpha, S->d_any);
+      LAUNCHED("k_ls_setup");
+      return trial(true);
     }
-    CK(cpl_ipm_dense_a(B, m, nw, nf, S->nnz_rec, S->amap, S->row_slack, S->J, S->A, S->active, st));
-    hipLaunchKernelGGL(k_prep, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->free32, S->row_slack, S->gl,
-                       S->grad, S->g, S->w, S->gradw, S->c);
-    LAUNCHED("k_prep");
-    CK(cpl_ipm_optimality(B, nw, m, FMAX, S->nbounds, o.tol, o.acceptable_tol, o.acceptable_iter, S->A, S->gradw, S->c,
-                          S->w, S->y, S->zL, S->zU, S->hasL, S->hasU, S->wl0, S->wu0, S->mu, S->filt_t, S->filt_p,
-                          S->fcount, S->active, S->status, S->acc, S->d_inf, S->err0, S->base, S->mu_o, S->ft, S->fp,
-                          S->fc, st));
-    hipLaunchKernelGGL(k_unpack_tau, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, nw, S->freepos, S->Xbase,
-                       S->w, S->mu_o, S->active, S->X, S->tau, S->act);
-    LAUNCHED("k_unpack_tau");
-    // Hessian of the Lagrangian over x_free
-    const double* Hblk = nullptr;
-    int h_sym = 0;
-    if (S->bfgs) {
-      // the compact model is expanded inside the Newton setup (ipm_newton_setup_lm below)
-    } else if (S->analytic_H) {
-      CK(cpl_lagrangian_hessian(&S->desc, B, S->X, S->y, S->act, S->free32, nf, S->H, st));
-      Hblk = S->H;
-    } else {  // central differences of grad f + J^T y (the 2 nf points of every instance in one launch)
-      CK(cpl_ipm_fd_points(B, n, nf, o.fd_step, S->freepos, S->X, S->Xp, S->hfd, S->act, st));
-      int32_t rc = CPL_ERR_UNSUPPORTED;
-      if (S->fd_fused)
-        rc = cpl_eval_lagrangian_grad(&S->desc, B * 2 * nf, S->Xp, S->mass ? S->mass_fd : nullptr,
-                                      S->tag ? S->tag_fd : nullptr, S->col_ptr, S->csc_k, S->csc_row, S->y, 2 * nf,
-                                      S->act, S->gL, st);
-      if (rc == CPL_ERR_UNSUPPORTED) {  // Superquadric / mixed: eval + J^T y in two launches
-        S->fd_fused = false;
-        CK(cpl_eval_batch(&S->desc, B * 2 * nf, S->Xp, S->mass ? S->mass_fd : nullptr, S->tag ? S->tag_fd : nullptr,
-                          nullptr, S->jac_fd, nullptr, S->grad_fd, st));
-        CK(cpl_lagrangian_grad(B * 2 * nf, n, m, S->nnz, S->col_ptr, S->csc_k, S->csc_row, S->grad_fd, S->jac_fd, S->y,
-                               2 * nf, S->gL, st));
-      } else {
-        CK(rc);
+    case P_TRIAL:
+      return trial(false);
+    case P_SOFT: {
+      hipLaunchKernelGGL(k_soft_begin, dim3(blocks_for(B)), dim3(256), 0, st, B, n, nf, nw, S->act, S->tiny_now,
+                         S->soft_now, S->soft_cnt, S->st_alpha, S->a_max, S->a_z, S->w, S->dw, S->freepos, S->Xbase,
+                         S->soft_try, S->a_soft, S->ws_, S->Xs);
+      LAUNCHED("k_soft_begin");
+      CK(eval_full(S, S->Xs, S->f_n, S->grad_n, S->g_n, S->J_n));
+      hipLaunchKernelGGL(k_soft_judge, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->nnz_rec, S->soft_try,
+                         S->soft_now, S->a_soft, S->amap, S->row_slack, S->free32, S->gl, S->hasL, S->hasU, S->wl0,
+                         S->wu0, S->ws_, S->f_n, S->grad_n, S->g_n, S->J_n, S->A, S->gradw, S->c, S->w, S->y, S->zL,
+                         S->zU, S->dy, S->dzL, S->dzU, S->mu_o, S->theta_k, S->phi_k, S->gd, S->switch_ok,
+                         S->theta_max, S->ft, S->fp, S->cs_tmp, S->in_soft, S->soft_cnt, S->st_f, S->st_g, S->st_w,
+                         S->st_alpha, S->st_aug, S->a_z);
+      LAUNCHED("k_soft_judge");
+      return CPL_OK;
+    }
+    case P_ACCEPT: {
+      hipLaunchKernelGGL(k_fail, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->act, S->st_alpha, S->failed, S->moved,
+                         S->in_soft, S->soft_cnt);
+      LAUNCHED("k_fail");
+      // the accepted points with their derivatives: one full evaluation
+      hipLaunchKernelGGL(k_unpack, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, nw, S->freepos, S->Xbase,
+                         S->st_w, nullptr, nullptr, S->Xn);
+      LAUNCHED("k_unpack");
+      CK(eval_full(S, S->Xn, S->f_n, S->grad_n, S->g_n, S->J_n));
+      if (S->bfgs) {
+        hipLaunchKernelGGL(k_prep, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->free32, S->row_slack,
+                           S->gl, S->grad_n, S->g_n, S->st_w, S->gradw_new, nullptr);
+        LAUNCHED("k_prep (new)");
+        hipLaunchKernelGGL(k_lbfgs, dim3((unsigned)B), dim3(256), 0, st, B, m, nf, nw, S->nnz_rec, S->amap, S->moved,
+                           S->w, S->st_w, S->y, S->dy, S->st_alpha, S->gradw, S->J, S->gradw_new, S->J_n, S->lm_s,
+                           S->lm_y, S->lm_cnt, S->lm_skip, S->zeros_u8, S->Hq);
+        LAUNCHED("k_lbfgs");
       }
-      CK(cpl_ipm_fd_hessian_raw(B, n, nf, S->free64, S->gL, S->hfd, S->H, S->act, st));
-      Hblk = S->H;
-      h_sym = 1;
+      CK(cpl_ipm_accept(B, nw, m, FMAX, S->moved, S->st_aug, nullptr, nullptr, S->st_alpha, S->a_z, S->theta_k,
+                        S->phi_k, S->ft, S->fp, S->fc, S->st_w, S->dy, S->dzL, S->dzU, S->mu_o, S->hasL, S->hasU,
+                        S->wl0, S->wu0, S->w, S->y, S->zL, S->zU, S->mu, S->iters, S->filt_t, S->filt_p, S->fcount,
+                        st));
+      hipLaunchKernelGGL(k_accept_rows, dim3(blocks_elems(B * (1 + n + m + S->nnz_rec))), dim3(256), 0, st, B, n, m,
+                         S->nnz_rec, S->moved, S->f_n, S->grad_n, S->g_n, S->J_n, S->f, S->grad, S->g, S->J);
+      LAUNCHED("k_accept_rows");
+      // the restoration phase starts where the line search failed
+      hipLaunchKernelGGL(k_resto_enter, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nw, S->failed, S->c, S->w, S->zL,
+                         S->zU, S->mu_o, S->theta_k, S->phi_k, S->hasL, S->hasU, S->filt_t, S->filt_p, S->fcount,
+                         S->iters, S->in_resto, S->n_resto, S->wR, S->pR, S->nR, S->zp, S->zn, S->zLR, S->zUR, S->muR,
+                         S->ftR, S->fpR, S->fcR, S->thmaxR, S->thminR, S->th_o0, S->ph_o0, S->dwlR, S->lm_cnt,
+                         S->lm_skip, S->bfgs ? S->Hq : nullptr, lmc, S->M, S->r1, S->r2, S->Dinv);
+      LAUNCHED("k_resto_enter");
+      CK(cpl_kkt_qd_solve(B, nw, m, S->M, S->A, S->Dinv, S->r1, S->r2, S->failed, S->dwlR, S->dw, S->dy, S->scr1,
+                          S->Kqd, st));
+      hipLaunchKernelGGL(k_resto_y0, dim3(blocks_for(B)), dim3(256), 0, st, B, m, S->failed, S->dy, S->y);
+      LAUNCHED("k_resto_y0");
+      if (B > COUNT1_MAX) {
+        hipLaunchKernelGGL(k_count_zero, dim3(1), dim3(64), 0, st, S->d_count);
+        LAUNCHED("k_count_zero");
+        hipLaunchKernelGGL(k_count, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->active, S->in_resto, S->d_count);
+      } else {
+        hipLaunchKernelGGL(k_count1, dim3(1), dim3(1024), 0, st, B, S->active, S->in_resto, S->d_count);
+      }
+      LAUNCHED("k_count");
+      return CPL_OK;
     }
-    // Newton system, step, multiplier steps, fraction-to-the-boundary steps
-    if (S->bfgs)
-      CK(ipm_newton_setup_lm(B, nw, m, nf, S->w, S->zL, S->zU, S->gradw, S->A, S->y, S->c, S->f, S->mu_o, S->hasL,
-                             S->hasU, S->wl0, S->wu0, S->Hq, LM_HIST, S->M, S->r1, S->r2, S->gphi, S->mr_diag,
-                             S->theta_k, S->phi_k, nullptr, st));
-    else
-      CK(cpl_ipm_newton_setup(B, nw, m, nf, S->w, S->zL, S->zU, S->gradw, S->A, S->y, S->c, S->f, S->mu_o, S->hasL,
-                              S->hasU, S->wl0, S->wu0, Hblk, h_sym, S->M, S->r1, S->r2, S->gphi, S->mr_diag, S->theta_k,
-                              S->phi_k, S->act, st));
-    CK(cpl_kkt_solve(0, B, nw, m, S->M, S->A, S->r1, S->r2, S->mu_o, S->dwl, S->act, S->dw, S->dy, S->delta_w,
-                     S->delta_c, S->info, S->ws, st));
-    CK(cpl_ipm_post_step(B, nw, S->w, S->dw, S->zL, S->zU, S->gphi, S->mu_o, S->tau, S->hasL, S->hasU, S->wl0, S->wu0,
-                         S->theta_k, S->theta_min, S->act, S->delta_w, S->dwl, S->dzL, S->dzU, S->a_max, S->a_z, S->gd,
-                         S->switch_ok, st));
-    // filter line search with a second-order correction on the first trial
-    hipLaunchKernelGGL(k_ls_init, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nw, S->act, S->f, S->g, S->w, S->a_max,
-                       S->searching, S->st_f, S->st_g, S->st_w, S->st_alpha, S->st_aug, S->alpha, S->failed, S->rest,
-                       flag ? S->d_any : nullptr);
-    LAUNCHED("k_ls_init");
-    CK(trial(0, flag));  // (with `flag`: the any-searching flag for the split iteration)
-    return CPL_OK;
+    case P_RNEWTON: {
+      hipLaunchKernelGGL(k_resto_prep1, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nf, nw, S->nbounds, o.tol,
+                         S->mu_min, S->active, S->in_resto, S->actR, S->status, S->A, S->c, S->w, S->y, S->wR, S->pR,
+                         S->nR, S->zp, S->zn, S->zLR, S->zUR, S->hasL, S->hasU, S->wl0, S->wu0, S->muR, S->ftR,
+                         S->fpR, S->fcR, S->tauR, S->gfR);
+      LAUNCHED("k_resto_prep1");
+      const double* Hblk = nullptr;
+      int h_sym = 0;
+      CK(hessian_into(S, &S->desc_R, S->actR, &Hblk, &h_sym));
+      if (S->bfgs)
+        CK(ipm_newton_setup_lm(B, nw, m, nf, S->w, S->zLR, S->zUR, S->gfR, S->A, S->y, S->c, S->f, S->muR, S->hasL,
+                               S->hasU, S->wl0, S->wu0, S->Hq, LM_HIST, S->M, S->r1, S->scr2, S->gphi, S->mr_diag,
+                               S->scr1, S->scr1 + S->B, S->actR, st));
+      else
+        CK(cpl_ipm_newton_setup(B, nw, m, nf, S->w, S->zLR, S->zUR, S->gfR, S->A, S->y, S->c, S->f, S->muR, S->hasL,
+                                S->hasU, S->wl0, S->wu0, Hblk, h_sym, S->M, S->r1, S->scr2, S->gphi, S->mr_diag,
+                                S->scr1, S->scr1 + S->B, S->actR, st));
+      hipLaunchKernelGGL(k_resto_prep2, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nf, nw, S->actR, S->c, S->w, S->y,
+                         S->wR, S->pR, S->nR, S->zp, S->zn, S->muR, S->hasL, S->hasU, S->wl0, S->wu0, S->M, S->rp,
+                         S->rn, S->Dinv, S->r2, S->thetaR, S->phiR);
+      LAUNCHED("k_resto_prep2");
+      CK(cpl_kkt_qd_solve(B, nw, m, S->M, S->A, S->Dinv, S->r1, S->r2, S->actR, S->dwlR, S->dw, S->dy, S->scr1,
+                          S->Kqd, st));
+      hipLaunchKernelGGL(k_resto_post, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nw, S->actR, S->w, S->dw, S->dy,
+                         S->gphi, S->pR, S->nR, S->zp, S->zn, S->zLR, S->zUR, S->rp, S->rn, S->muR, S->tauR, S->hasL,
+                         S->hasU, S->wl0, S->wu0, S->thetaR, S->thminR, S->f, S->g, S->dp, S->dn, S->dzL, S->dzU,
+                         S->dzp, S->dzn, S->a_maxR, S->a_zR, S->gdR, S->switchR, S->a_minR, S->searchingR, S->st_f,
+                         S->st_g, S->st_w, S->st_p, S->st_n, S->st_alpha, S->st_aug, S->alphaR, S->d_any);
+      LAUNCHED("k_resto_post");
+      return rtrial();
+    }
+    case P_RTRIAL:
+      return rtrial();
+    case P_RACCEPT: {
+      hipLaunchKernelGGL(k_unpack, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, nw, S->freepos, S->Xbase,
+                         S->st_w, nullptr, nullptr, S->Xn);
+      LAUNCHED("k_unpack (resto)");
+      CK(eval_full(S, S->Xn, S->f_n, S->grad_n, S->g_n, S->J_n));
+      if (S->bfgs) {  // the restoration phase's own model: pairs from J^T y (its constraint curvature)
+        hipLaunchKernelGGL(k_moved_r, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->actR, S->st_alpha, S->movedR);
+        LAUNCHED("k_moved_r");
+        hipLaunchKernelGGL(k_lbfgs, dim3((unsigned)B), dim3(256), 0, st, B, m, nf, nw, S->nnz_rec, S->amap, S->movedR,
+                           S->w, S->st_w, S->y, S->dy, S->st_alpha, S->zeros_w, S->J, S->zeros_w, S->J_n, S->lm_s,
+                           S->lm_y, S->lm_cnt, S->lm_skip, S->zeros_u8, S->Hq);
+        LAUNCHED("k_lbfgs (resto)");
+      }
+      hipLaunchKernelGGL(k_resto_accept, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nf, nw, S->actR, S->movedR,
+                         S->active, S->status, S->iters, S->st_alpha, S->st_aug, S->st_w, S->st_p, S->st_n, S->dy,
+                         S->dzL, S->dzU, S->dzp, S->dzn, S->a_zR, S->muR, S->thetaR, S->phiR, S->ftR, S->fpR, S->fcR,
+                         S->w, S->y, S->pR, S->nR, S->zp, S->zn, S->zLR, S->zUR, S->hasL, S->hasU, S->wl0, S->wu0,
+                         S->row_slack, S->gl, S->f_n, S->g_n, S->mu, S->filt_t, S->filt_p, S->th_o0, S->ph_o0, S->wR,
+                         S->zL, S->zU, S->in_resto, S->acc, S->lm_cnt, S->lm_skip, S->bfgs ? S->Hq : nullptr, lmc);
+      LAUNCHED("k_resto_accept");
+      hipLaunchKernelGGL(k_accept_rows, dim3(blocks_elems(B * (1 + n + m + S->nnz_rec))), dim3(256), 0, st, B, n, m,
+                         S->nnz_rec, S->movedR, S->f_n, S->grad_n, S->g_n, S->J_n, S->f, S->grad, S->g, S->J);
+      LAUNCHED("k_accept_rows (resto)");
+      return CPL_OK;
+    }
+    default:
+      return fail(CPL_ERR_INVALID_ARGUMENT, "step_phase: bad phase");
   }
-  if (phase == 2) {
-    for (int ls = 1; ls < nls; ++ls) CK(trial(ls, false));
-    // no acceptable trial: the feasibility step (min 1/2 dw^T (Sigma + sqrt(mu) D_R^2) dw s.t. A dw = -c)
-    // stands in for IPOPT's restoration phase, taken when it cuts the violation by 10 %; else the last trial
-    hipLaunchKernelGGL(k_feas_prep, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nw, S->searching, S->mr_diag, S->c,
-                       S->failed, S->Mr, S->negc);
-    LAUNCHED("k_feas_prep");
-    CK(cpl_kkt_solve(0, B, nw, m, S->Mr, S->A, S->zeros_w, S->negc, S->mu_o, S->zeros_B, S->failed, S->dwr, S->dyr,
-                     S->dwr_d, S->dcr, S->infor, S->ws, st));
-    CK(cpl_ipm_max_step(B, nw, S->w, S->dwr, nullptr, nullptr, S->hasL, S->hasU, S->wl0, S->wu0, S->tau, S->ar, st));
-    CK(cpl_ipm_trial_point(B, n, nf, nw, S->free64, S->fixed64, S->Xbase, S->w, S->dwr, S->ar, S->failed, S->st_w, S->wr,
-                           S->Xr, st));
-    CK(eval_fg(S, S->Xr, S->f_r, S->g_r));
-    CK(judge(S->wr, S->f_r, S->g_r, S->zeros_B, S->failed, S->th_r, S->ok_r, 1));
-    hipLaunchKernelGGL(k_rest, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->failed, S->ok_r, S->alpha, S->rest,
-                       S->alpha2);
-    LAUNCHED("k_rest");
-    CK(judge(S->wt, S->f_t, S->g_t, S->alpha2, nullptr, S->th, S->ok, 2));
-    return CPL_OK;
-  }
-  // the accepted points with their derivatives: one full evaluation
-  hipLaunchKernelGGL(k_unpack, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, nw, S->freepos, S->Xbase,
-                     S->st_w, nullptr, nullptr, S->Xn);
-  LAUNCHED("k_unpack");
-  CK(eval_full(S, S->Xn, S->f_n, S->grad_n, S->g_n, S->J_n));
-  if (S->bfgs) {
-    hipLaunchKernelGGL(k_prep, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->free32, S->row_slack, S->gl,
-                       S->grad_n, S->g_n, S->st_w, S->gradw_new, nullptr);
-    LAUNCHED("k_prep (new)");
-    hipLaunchKernelGGL(k_lbfgs, dim3((unsigned)B), dim3(256), 0, st, B, m, nf, nw, S->nnz_rec, S->amap, S->act, S->w, S->st_w, S->y, S->dy,
-                       S->st_alpha, S->gradw, S->J, S->gradw_new, S->J_n, S->lm_s, S->lm_y, S->lm_cnt, S->lm_skip,
-                       S->failed, S->Hq);
-    LAUNCHED("k_lbfgs");
-  }
-  CK(cpl_ipm_accept(B, nw, m, FMAX, S->act, S->st_aug, S->failed, S->rest, S->st_alpha, S->a_z, S->theta_k, S->phi_k,
-                    S->ft, S->fp, S->fc, S->st_w, S->dy, S->dzL, S->dzU, S->mu_o, S->hasL, S->hasU, S->wl0, S->wu0,
-                    S->w, S->y, S->zL, S->zU, S->mu, S->iters, S->filt_t, S->filt_p, S->fcount, st));
-  hipLaunchKernelGGL(k_accept_rows, dim3(blocks_elems(B * (1 + n + m + S->nnz_rec))), dim3(256), 0, st, B, n, m,
-                     S->nnz_rec, S->act, S->f_n, S->grad_n, S->g_n, S->J_n, S->f, S->grad, S->g, S->J);
-  LAUNCHED("k_accept_rows");
-  if (B > COUNT1_MAX)
-    hipLaunchKernelGGL(k_count, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->active, S->d_count);
-  else
-    hipLaunchKernelGGL(k_count1, dim3(1), dim3(1024), 0, st, B, S->active, S->d_count);
-  LAUNCHED("k_count");
-  return CPL_OK;
 }
 
-// the graph of one iteration at the current batch size (captured once per size, then replayed)
-// phase 0: the whole iteration (S->graph / S->gexec); 1..3: the split iteration's phases (*ex)
-int32_t graph_for(cpl_solver* S, int phase = 0, hipGraphExec_t* ex_out = nullptr) {
-  const int64_t key = (S->Bcur * 4 + (S->mass ? 2 : 0) + (S->tag ? 1 : 0)) * 4 + phase;
+// the graph of one phase at the current batch size (captured once per (size, inputs, phase), then
+// replayed); without graphs the phase is launched directly
+int32_t run_phase(cpl_solver* S, int phase) {
+  if (!S->opt.use_graph) return step_phase(S, phase);
+  const int64_t key = ((S->Bcur * 4 + (S->mass ? 2 : 0) + (S->tag ? 1 : 0)) * 8) + phase;
   auto it = S->graphs.find(key);
   if (it == S->graphs.end()) {
     HK(hipStreamBeginCapture(S->stream, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
-    const int32_t rc = phase == 0 ? step(S) : step_phase(S, phase, phase == 1);
+    const int32_t rc = step_phase(S, phase);
     hipGraph_t gr = nullptr;
     const hipError_t e = hipStreamEndCapture(S->stream, &gr);
     if (rc != CPL_OK) {
@@ -1008,13 +1885,16 @@ int32_t graph_for(cpl_solver* S, int phase = 0, hipGraphExec_t* ex_out = nullptr
       return hip_err(e2, "hipGraphInstantiate");
     }
     it = S->graphs.emplace(key, std::make_pair(gr, ex)).first;
+    S->captured = true;
   }
-  if (phase == 0) {
-    S->graph = it->second.first;
-    S->gexec = it->second.second;
-  } else {
-    *ex_out = it->second.second;
-  }
+  HK(hipGraphLaunch(it->second.second, S->stream), "hipGraphLaunch");
+  return CPL_OK;
+}
+
+// the device's flags (any still searching / soft candidates / restoration searching) to the host
+int32_t read_flags(cpl_solver* S) {
+  HK(hipMemcpyAsync(S->h_flag, S->d_any, 4, hipMemcpyDeviceToHost, S->stream), "hipMemcpyAsync flags");
+  HK(hipStreamSynchronize(S->stream), "hipStreamSynchronize");
   return CPL_OK;
 }
 
@@ -1026,8 +1906,8 @@ int32_t compact(cpl_solver* S, int64_t count, int64_t Bn) {
   const int64_t Bc = S->Bcur;
   const int n = S->n, m = S->m, nw = S->nw;
   hipLaunchKernelGGL(k_scatter_final, dim3(blocks_for(Bc)), dim3(256), 0, st, Bc, n, m, nw, true, S->orig, S->active,
-                     S->w, S->y, S->Xbase, S->d_inf, S->status, S->iters, S->fw, S->fy, S->fX, S->fdinf, S->fstatus,
-                     S->fiters);
+                     S->w, S->y, S->Xbase, S->d_inf, S->status, S->iters, S->n_resto, S->fw, S->fy, S->fX, S->fdinf,
+                     S->fstatus, S->fiters, S->fresto);
   LAUNCHED("k_scatter_final");
   hipLaunchKernelGGL(k_positions, dim3(1), dim3(1024), 0, st, Bc, S->active, S->pos);
   LAUNCHED("k_positions");
@@ -1044,7 +1924,12 @@ int32_t compact(cpl_solver* S, int64_t count, int64_t Bn) {
   CK(move(S->filt_t, FMAX)); CK(move(S->filt_p, FMAX)); CK(move(S->dwl, 1)); CK(move(S->f, 1));
   CK(move(S->grad, n)); CK(move(S->g, m)); CK(move(S->J, S->nnz_rec)); CK(move(S->d_inf, 1));
   CK(move(S->theta_max, 1)); CK(move(S->theta_min, 1)); CK(move(S->Xbase, n));
-  CK(move(S->status, 1)); CK(move(S->iters, 1)); CK(move(S->acc, 1)); CK(move(S->fcount, 1));
+  CK(move(S->status, 1)); CK(move(S->iters, 1)); CK(move(S->acc, 1)); CK(move(S->fcount, 1)); CK(move(S->n_resto, 1));
+  // the restoration phase's state
+  CK(move(S->wR, nw)); CK(move(S->pR, m)); CK(move(S->nR, m)); CK(move(S->zp, m)); CK(move(S->zn, m));
+  CK(move(S->zLR, nw)); CK(move(S->zUR, nw)); CK(move(S->muR, 1)); CK(move(S->ftR, FMAX)); CK(move(S->fpR, FMAX));
+  CK(move(S->fcR, 1)); CK(move(S->th_o0, 1)); CK(move(S->ph_o0, 1)); CK(move(S->dwlR, 1)); CK(move(S->thmaxR, 1));
+  CK(move(S->thminR, 1));
   if (S->bfgs) {
     CK(move(S->Hq, LMC(nf)));
     CK(move(S->lm_s, (int64_t)LM_HIST * nf));
@@ -1062,11 +1947,20 @@ int32_t compact(cpl_solver* S, int64_t count, int64_t Bn) {
   CK(move_bytes(S->active));
   CK(move_bytes(S->lm_cnt));
   CK(move_bytes(S->lm_skip));
+  CK(move_bytes(S->in_soft));
+  CK(move_bytes(S->tiny_last));
+  CK(move_bytes(S->tiny_flag));
+  CK(move_bytes(S->in_resto));
   if (S->tag) CK(move_bytes(S->tag_c));
-  hipLaunchKernelGGL(k_gather_i32, dim3(blocks_elems(count)), dim3(256), 0, st, count, S->pos, S->orig,
-                     (int32_t*)S->scratch);
-  LAUNCHED("k_gather_i32");
-  HK(hipMemcpyAsync(S->orig, S->scratch, 4 * (size_t)count, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
+  auto move_i32 = [&](int32_t* buf) -> int32_t {
+    hipLaunchKernelGGL(k_gather_i32, dim3(blocks_elems(count)), dim3(256), 0, st, count, S->pos, buf,
+                       (int32_t*)S->scratch);
+    LAUNCHED("k_gather_i32");
+    HK(hipMemcpyAsync(buf, S->scratch, 4 * (size_t)count, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
+    return CPL_OK;
+  };
+  CK(move_i32(S->orig));
+  CK(move_i32(S->soft_cnt));
   hipLaunchKernelGGL(k_pad, dim3(blocks_elems(Bn)), dim3(256), 0, st, count, Bn, S->active, S->orig);
   LAUNCHED("k_pad");
   S->Bcur = Bn;
@@ -1091,8 +1985,8 @@ void cpl_solve_options_default(cpl_solve_options* o) {
   std::memset(o, 0, sizeof(*o));
   o->max_iter = 3000;
   o->hessian = CPL_HESSIAN_EXACT;
-  o->max_ls = 4;
-  o->max_soc = 1;
+  o->max_ls = 40;   // backtracking trials at most (IPOPT stops at alpha_min, ~20 halvings typically)
+  o->max_soc = 4;   // IPOPT's max_soc
   o->acceptable_iter = 15;
   o->use_graph = 1;
   o->compact = 1;
@@ -1109,8 +2003,6 @@ int32_t cpl_solver_destroy(cpl_solver* S) {
     (void)hipGraphDestroy(g.second.first);
   }
   S->graphs.clear();
-  for (auto& e : S->ev)
-    if (e) (void)hipEventDestroy(e);
   if (S->h_flag) (void)hipHostFree(S->h_flag);
   if (S->h_count) (void)hipHostFree(S->h_count);
   if (S->arena.base) (void)hipFree(S->arena.base);
@@ -1123,7 +2015,7 @@ int32_t cpl_solver_dims(const cpl_solver* S, int32_t* nf, int32_t* n_ineq, int32
   if (!S) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_solver_dims: null solver");
   if (nf) *nf = S->nf;
   if (n_ineq) *n_ineq = S->nI;
-  if (graph_captured) *graph_captured = S->gexec != nullptr;
+  if (graph_captured) *graph_captured = S->captured ? 1 : 0;
   return CPL_OK;
 }
 
@@ -1131,6 +2023,13 @@ int32_t cpl_solver_stats(const cpl_solver* S, int32_t* compactions, int64_t* fin
   if (!S) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_solver_stats: null solver");
   if (compactions) *compactions = S->compactions;
   if (final_rows) *final_rows = S->Bcur;
+  return CPL_OK;
+}
+
+int32_t cpl_solver_restorations(const cpl_solver* S, int64_t* d_out, void* stream) {
+  if (!S || !d_out) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_solver_restorations: null argument");
+  HK(hipMemcpyAsync(d_out, S->fresto, 8 * (size_t)S->B, hipMemcpyDeviceToDevice, (hipStream_t)stream),
+     "hipMemcpyAsync restorations");
   return CPL_OK;
 }
 
@@ -1219,9 +2118,13 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
 
   cpl_solver* S = new cpl_solver();
   S->desc = *d;
+  S->desc_R = *d;  // zero cost weights: the Hessian of y^T g alone (the restoration phase)
+  S->desc_R.W_com = 0.0;
+  for (int i = 0; i < CPL_MAX_CONTACTS; ++i) S->desc_R.W_p[i] = S->desc_R.W_F[i] = 0.0;
   S->opt = opt;
   S->B = batch;
   S->n = n; S->m = m; S->nnz = nnz; S->nnz_rec = nnz_rec; S->nf = nf; S->nI = nI; S->nw = nw; S->nbounds = nbounds;
+  S->mu_min = ipm_mu_min(opt.tol);
   S->bfgs = opt.hessian == CPL_HESSIAN_LIMITED_MEMORY;
   S->analytic_H = opt.hessian == CPL_HESSIAN_EXACT && cpl_lagrangian_hessian(d, 0, nullptr, nullptr, nullptr, nullptr,
                                                                              nf > 0 ? nf : 1, nullptr, nullptr) == CPL_OK;
@@ -1232,9 +2135,7 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   };
   hipError_t e = hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking);
   if (e != hipSuccess) return bad(e, "hipStreamCreate");
-  for (auto& ev : S->ev)
-    if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
-  if ((e = hipHostMalloc(&S->h_flag, 2)) != hipSuccess) return bad(e, "hipHostMalloc");
+  if ((e = hipHostMalloc(&S->h_flag, 4)) != hipSuccess) return bad(e, "hipHostMalloc");
   if ((e = hipHostMalloc(&S->h_count, 2 * sizeof(int32_t))) != hipSuccess) return bad(e, "hipHostMalloc");
   // every device buffer carved from one allocation: a measuring pass, then the real one
   const size_t Bz = (size_t)batch, kws = (size_t)cpl_kkt_workspace_doubles(nw, m);
@@ -1251,6 +2152,7 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   S->col_ptr = a.take<int32_t>(n + 1); S->csc_k = a.take<int32_t>(nnz); S->csc_row = a.take<int32_t>(nnz);
   S->free64 = a.take<int64_t>(nf); S->fixed64 = a.take<int64_t>(fixed_idx.size());
   S->is_fixed = a.take<uint8_t>(n); S->hasL = a.take<uint8_t>(nw); S->hasU = a.take<uint8_t>(nw);
+  S->zeros_u8 = a.take<uint8_t>(Bz);
   S->xl = a.take<double>(n); S->xu = a.take<double>(n); S->gl = a.take<double>(m); S->gu = a.take<double>(m);
   S->wl0 = a.take<double>(nw); S->wu0 = a.take<double>(nw);
   // state
@@ -1262,39 +2164,55 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   S->lm_s = a.take<double>(S->bfgs ? Bz * LM_HIST * nf : 0); S->lm_y = a.take<double>(S->bfgs ? Bz * LM_HIST * nf : 0);
   S->theta_max = a.take<double>(Bz); S->theta_min = a.take<double>(Bz);
   S->status = a.take<int64_t>(Bz); S->iters = a.take<int64_t>(Bz); S->acc = a.take<int64_t>(Bz);
-  S->fcount = a.take<int64_t>(Bz); S->fc = a.take<int64_t>(Bz);
-  S->active = a.take<uint8_t>(Bz); S->lm_cnt = a.take<uint8_t>(Bz); S->lm_skip = a.take<uint8_t>(Bz); S->d_any = a.take<uint8_t>(2);
+  S->fcount = a.take<int64_t>(Bz); S->fc = a.take<int64_t>(Bz); S->n_resto = a.take<int64_t>(Bz);
+  S->active = a.take<uint8_t>(Bz); S->lm_cnt = a.take<uint8_t>(Bz); S->lm_skip = a.take<uint8_t>(Bz); S->d_any = a.take<uint8_t>(4);
+  S->in_soft = a.take<uint8_t>(Bz); S->tiny_last = a.take<uint8_t>(Bz); S->tiny_flag = a.take<uint8_t>(Bz);
+  S->in_resto = a.take<uint8_t>(Bz); S->soft_cnt = a.take<int32_t>(Bz);
+  // the restoration phase's state
+  S->wR = a.take<double>(Bz * nw); S->pR = a.take<double>(Bz * m); S->nR = a.take<double>(Bz * m);
+  S->zp = a.take<double>(Bz * m); S->zn = a.take<double>(Bz * m); S->zLR = a.take<double>(Bz * nw);
+  S->zUR = a.take<double>(Bz * nw); S->muR = a.take<double>(Bz); S->ftR = a.take<double>(Bz * FMAX);
+  S->fpR = a.take<double>(Bz * FMAX); S->fcR = a.take<int64_t>(Bz); S->th_o0 = a.take<double>(Bz);
+  S->ph_o0 = a.take<double>(Bz); S->dwlR = a.take<double>(Bz); S->thmaxR = a.take<double>(Bz);
+  S->thminR = a.take<double>(Bz);
   // temporaries
   S->A = a.take<double>(Bz * m * nw);
   S->gradw = a.take<double>(Bz * nw); S->gradw_new = a.take<double>(Bz * nw); S->c = a.take<double>(Bz * m);
   S->err0 = a.take<double>(Bz); S->base = a.take<double>(Bz); S->mu_o = a.take<double>(Bz);
   S->ft = a.take<double>(Bz * FMAX); S->fp = a.take<double>(Bz * FMAX); S->tau = a.take<double>(Bz);
   S->X = a.take<double>(Bz * n); S->H = a.take<double>(Bz * nf * nf); S->M = a.take<double>(Bz * nw * nw);
-  S->Mr = a.take<double>(Bz * nw * nw); S->r1 = a.take<double>(Bz * nw); S->r2 = a.take<double>(Bz * m);
+  S->Kqd = a.take<double>(Bz * nw * nw); S->r1 = a.take<double>(Bz * nw); S->r2 = a.take<double>(Bz * m);
   S->gphi = a.take<double>(Bz * nw); S->mr_diag = a.take<double>(Bz * nw); S->theta_k = a.take<double>(Bz);
   S->phi_k = a.take<double>(Bz); S->dw = a.take<double>(Bz * nw); S->dy = a.take<double>(Bz * m);
   S->delta_w = a.take<double>(Bz); S->delta_c = a.take<double>(Bz); S->dzL = a.take<double>(Bz * nw);
   S->dzU = a.take<double>(Bz * nw); S->a_max = a.take<double>(Bz); S->a_z = a.take<double>(Bz);
   S->gd = a.take<double>(Bz); S->ws = a.take<double>(Bz * kws); S->info = a.take<int32_t>(Bz);
+  S->a_min = a.take<double>(Bz); S->a_soft = a.take<double>(Bz); S->cs_tmp = a.take<double>(Bz * m);
+  S->scr1 = a.take<double>(2 * Bz); S->scr2 = a.take<double>(Bz * m);
   S->act = a.take<uint8_t>(Bz); S->switch_ok = a.take<uint8_t>(Bz); S->searching = a.take<uint8_t>(Bz);
   S->st_aug = a.take<uint8_t>(Bz); S->ok = a.take<uint8_t>(Bz); S->soc = a.take<uint8_t>(Bz);
-  S->ok_s = a.take<uint8_t>(Bz); S->failed = a.take<uint8_t>(Bz); S->ok_r = a.take<uint8_t>(Bz);
-  S->rest = a.take<uint8_t>(Bz);
+  S->ok_s = a.take<uint8_t>(Bz); S->failed = a.take<uint8_t>(Bz); S->moved = a.take<uint8_t>(Bz);
+  S->tiny_now = a.take<uint8_t>(Bz); S->soft_now = a.take<uint8_t>(Bz); S->soft_try = a.take<uint8_t>(Bz);
   S->st_f = a.take<double>(Bz); S->st_g = a.take<double>(Bz * m); S->st_w = a.take<double>(Bz * nw);
-  S->st_alpha = a.take<double>(Bz); S->alpha = a.take<double>(Bz); S->alpha2 = a.take<double>(Bz);
+  S->st_alpha = a.take<double>(Bz); S->alpha = a.take<double>(Bz);
   S->th = a.take<double>(Bz); S->wt = a.take<double>(Bz * nw); S->Xt = a.take<double>(Bz * n);
   S->f_t = a.take<double>(Bz); S->g_t = a.take<double>(Bz * m);
   S->c_soc = a.take<double>(Bz * m); S->a_soc = a.take<double>(Bz); S->th_old = a.take<double>(Bz);
   S->r2s = a.take<double>(Bz * m); S->dws = a.take<double>(Bz * nw); S->dys = a.take<double>(Bz * m);
   S->ws_ = a.take<double>(Bz * nw); S->Xs = a.take<double>(Bz * n); S->f_s = a.take<double>(Bz);
   S->g_s = a.take<double>(Bz * m); S->th_s = a.take<double>(Bz);
-  S->negc = a.take<double>(Bz * m); S->dwr = a.take<double>(Bz * nw); S->dyr = a.take<double>(Bz * m);
-  S->dwr_d = a.take<double>(Bz); S->dcr = a.take<double>(Bz); S->ar = a.take<double>(Bz);
-  S->wr = a.take<double>(Bz * nw); S->Xr = a.take<double>(Bz * n); S->f_r = a.take<double>(Bz);
-  S->g_r = a.take<double>(Bz * m); S->th_r = a.take<double>(Bz); S->infor = a.take<int32_t>(Bz);
   S->Xn = a.take<double>(Bz * n); S->f_n = a.take<double>(Bz); S->grad_n = a.take<double>(Bz * n);
   S->g_n = a.take<double>(Bz * m); S->J_n = a.take<double>(Bz * nnz_rec);
   S->zeros_w = a.take<double>(Bz * nw); S->zeros_B = a.take<double>(Bz);
+  // the restoration phase's temporaries
+  S->gfR = a.take<double>(Bz * nw); S->tauR = a.take<double>(Bz); S->rp = a.take<double>(Bz * m);
+  S->rn = a.take<double>(Bz * m); S->Dinv = a.take<double>(Bz * m); S->dp = a.take<double>(Bz * m);
+  S->dn = a.take<double>(Bz * m); S->dzp = a.take<double>(Bz * m); S->dzn = a.take<double>(Bz * m);
+  S->st_p = a.take<double>(Bz * m); S->st_n = a.take<double>(Bz * m); S->thetaR = a.take<double>(Bz);
+  S->phiR = a.take<double>(Bz); S->gdR = a.take<double>(Bz); S->a_maxR = a.take<double>(Bz);
+  S->a_zR = a.take<double>(Bz); S->a_minR = a.take<double>(Bz); S->alphaR = a.take<double>(Bz);
+  S->actR = a.take<uint8_t>(Bz); S->movedR = a.take<uint8_t>(Bz); S->searchingR = a.take<uint8_t>(Bz);
+  S->switchR = a.take<uint8_t>(Bz);
   S->fin_f = a.take<double>(Bz); S->fin_g = a.take<double>(Bz * m);
   S->st32 = a.take<int32_t>(Bz); S->it32 = a.take<int32_t>(Bz);
   S->Xp = a.take<double>(nfd * n); S->gL = a.take<double>(nfd * n); S->hfd = a.take<double>(Bz * nf);
@@ -1304,6 +2222,7 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   S->mass_c = a.take<double>(Bz); S->tag_c = a.take<uint8_t>(Bz);
   S->fw = a.take<double>(Bz * nw); S->fy = a.take<double>(Bz * m); S->fX = a.take<double>(Bz * n);
   S->fdinf = a.take<double>(Bz); S->fstatus = a.take<int64_t>(Bz); S->fiters = a.take<int64_t>(Bz);
+  S->fresto = a.take<int64_t>(Bz);
   S->scratch = a.take<uint64_t>(Bz * (size_t)S->scratch_words);
   };
   Arena probe;
@@ -1326,7 +2245,7 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   for (const Up& u : ups)
     if (u.bytes && (e = hipMemcpy(u.dst, u.src, u.bytes, hipMemcpyHostToDevice)) != hipSuccess) return bad(e, "hipMemcpy");
   if ((e = hipMemset(S->zeros_w, 0, 8 * Bz * nw)) != hipSuccess || (e = hipMemset(S->zeros_B, 0, 8 * Bz)) != hipSuccess ||
-      (e = hipMemset(S->Mr, 0, 8 * Bz * nw * nw)) != hipSuccess)
+      (e = hipMemset(S->zeros_u8, 0, Bz)) != hipSuccess)
     return bad(e, "hipMemset");
   *out = S;
   return CPL_OK;
@@ -1353,6 +2272,13 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
   if (d_env_tag) HK(hipMemcpyAsync(S->tag_c, d_env_tag, (size_t)B, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync tag");
   hipLaunchKernelGGL(k_iota, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->orig);
   LAUNCHED("k_iota");
+  // per-instance flags of the line search and the restoration phase start cleared
+  HK(hipMemsetAsync(S->in_soft, 0, (size_t)B, st), "hipMemsetAsync");
+  HK(hipMemsetAsync(S->tiny_last, 0, (size_t)B, st), "hipMemsetAsync");
+  HK(hipMemsetAsync(S->tiny_flag, 0, (size_t)B, st), "hipMemsetAsync");
+  HK(hipMemsetAsync(S->in_resto, 0, (size_t)B, st), "hipMemsetAsync");
+  HK(hipMemsetAsync(S->soft_cnt, 0, 4 * (size_t)B, st), "hipMemsetAsync");
+  HK(hipMemsetAsync(S->n_resto, 0, 8 * (size_t)B, st), "hipMemsetAsync");
   int64_t evals = 0;
   if (S->fd && (d_mass || d_env_tag)) {
     hipLaunchKernelGGL(k_repeat, dim3(blocks_elems(B * 2 * nf)), dim3(256), 0, st, B, 2 * nf, S->mass, S->mass_fd,
@@ -1381,85 +2307,52 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
     hipLaunchKernelGGL(k_lm_init, dim3(blocks_elems(B)), dim3(256), 0, st, B, nf, S->Hq);
     LAUNCHED("k_lm_init");
   }
-  const int64_t per_step_full = (S->fd ? 1 : 0) + (S->opt.max_ls > 0 ? S->opt.max_ls : 1) + S->opt.max_soc + 2;
+  const int nls = S->opt.max_ls > 0 ? S->opt.max_ls : 1;
+  const int64_t ev_newton = (S->fd ? 1 : 0) + 1 + S->opt.max_soc;
   int it = 0;
   const int max_iter = S->opt.max_iter;
   const bool compacting = S->opt.compact != 0 && S->opt.use_graph;
   const int64_t min_rows = 256;
-  if (max_iter > 0) {
-    // first iteration executed (warms per-stream state, the eval kernels' launch geometry)
-    CK(step(S));
-    ++it;
-    evals += per_step_full;
-    if (S->opt.use_graph) CK(graph_for(S));
-    HK(hipMemcpyAsync(S->h_count, S->d_count, 4, hipMemcpyDeviceToHost, st), "hipMemcpyAsync count");
-    HK(hipStreamSynchronize(st), "hipStreamSynchronize");
-    int last = S->h_count[0] ? max_iter : it;
-    int start = it;
-    // batches of at most SPLIT_MAX rows: the iteration as three graphs, the line search's later
-    // trials and feasibility step (phase B) launched only when an instance is still searching after
-    // the first trial (read back before the launch: one stream synchronisation per iteration, against
-    // ~25 masked launches skipped in most iterations)
-    constexpr int64_t SPLIT_MAX = 256;
-    auto split_loop = [&]() -> int32_t {
-      const int64_t evA = (S->fd ? 1 : 0) + 1 + S->opt.max_soc;
-      const int64_t evB = (S->opt.max_ls > 0 ? S->opt.max_ls : 1) - 1 + 1;
-      hipGraphExec_t ga = nullptr, gb = nullptr, gc = nullptr;
-      CK(graph_for(S, 1, &ga));
-      CK(graph_for(S, 2, &gb));
-      CK(graph_for(S, 3, &gc));
-      bool have_count = false;  // h_count[0] holds the count after the previous iteration
-      while (it < last) {
-        HK(hipGraphLaunch(ga, st), "hipGraphLaunch");
-        HK(hipMemcpyAsync(S->h_flag, S->d_any, 1, hipMemcpyDeviceToHost, st), "hipMemcpyAsync flag");
-        HK(hipStreamSynchronize(st), "hipStreamSynchronize");
-        ++it;
-        evals += evA + 1;
-        if (have_count && S->h_count[0] == 0) break;  // converged in the previous iteration (this one was idle)
-        if (S->h_flag[0]) {
-          HK(hipGraphLaunch(gb, st), "hipGraphLaunch");
-          evals += evB;
-        }
-        HK(hipGraphLaunch(gc, st), "hipGraphLaunch");
-        HK(hipMemcpyAsync(S->h_count, S->d_count, 4, hipMemcpyDeviceToHost, st), "hipMemcpyAsync count");
-        have_count = true;
-      }
-      return CPL_OK;
-    };
-    if (S->opt.use_graph && S->Bcur <= SPLIT_MAX) {
-      CK(split_loop());
-      last = it;
+  int32_t resto_rows = 0;  // instances in the restoration phase after the previous iteration
+  while (it < max_iter) {
+    CK(run_phase(S, P_NEWTON));
+    evals += ev_newton;
+    CK(read_flags(S));
+    // further backtracking trials while an instance is still searching (at most max_ls in all)
+    for (int ls = 1; S->h_flag[0] && ls < nls; ++ls) {
+      CK(run_phase(S, P_TRIAL));
+      ++evals;
+      CK(read_flags(S));
     }
-    while (it < last) {
-      if (S->opt.use_graph) HK(hipGraphLaunch(S->gexec, st), "hipGraphLaunch");
-      else CK(step(S));
-      ++it;
-      evals += per_step_full;
-      const int k = it & 1;
-      HK(hipMemcpyAsync(S->h_count + k, S->d_count, 4, hipMemcpyDeviceToHost, st), "hipMemcpyAsync count");
-      HK(hipEventRecord(S->ev[k], st), "hipEventRecord");
-      if (it - start >= 2) {  // the previous iteration's count (normally landed already)
-        HK(hipEventSynchronize(S->ev[k ^ 1]), "hipEventSynchronize");
-        const int64_t cnt = S->h_count[k ^ 1];
-        if (cnt == 0) break;
-        if (compacting && S->Bcur > min_rows && 2 * cnt <= S->Bcur) {
-          // shrink to the smallest halving of the current size that holds the active instances
-          HK(hipStreamSynchronize(st), "hipStreamSynchronize");
-          const int64_t now = S->h_count[k];
-          if (now == 0) break;
-          int64_t Bn = S->Bcur;
-          while (Bn / 2 >= now && Bn / 2 >= min_rows) Bn = (Bn + 1) / 2;
-          if (Bn < S->Bcur) {
-            CK(compact(S, now, Bn));
-            if (Bn <= SPLIT_MAX) {  // the rest of the solve as split iterations
-              CK(split_loop());
-              break;
-            }
-            CK(graph_for(S));
-            start = it;  // the flag pipeline restarts at the new size
-          }
-        }
+    if (S->h_flag[1] || S->h_flag[0]) {  // an instance found no acceptable trial: the soft restoration step
+      CK(run_phase(S, P_SOFT));
+      ++evals;
+    }
+    if (resto_rows > 0) {  // one restoration-phase iteration of the instances inside it
+      CK(run_phase(S, P_RNEWTON));
+      evals += (S->fd ? 1 : 0) + 1;
+      CK(read_flags(S));
+      for (int ls = 1; S->h_flag[2] && ls < nls; ++ls) {
+        CK(run_phase(S, P_RTRIAL));
+        ++evals;
+        CK(read_flags(S));
       }
+      CK(run_phase(S, P_RACCEPT));
+      ++evals;
+    }
+    CK(run_phase(S, P_ACCEPT));
+    ++evals;
+    ++it;
+    HK(hipMemcpyAsync(S->h_count, S->d_count, 8, hipMemcpyDeviceToHost, st), "hipMemcpyAsync count");
+    HK(hipStreamSynchronize(st), "hipStreamSynchronize");
+    const int64_t cnt = S->h_count[0];
+    resto_rows = S->h_count[1];
+    if (cnt == 0) break;
+    if (compacting && S->Bcur > min_rows && 2 * cnt <= S->Bcur) {
+      // shrink to the smallest halving of the current size that holds the active instances
+      int64_t Bn = S->Bcur;
+      while (Bn / 2 >= cnt && Bn / 2 >= min_rows) Bn = (Bn + 1) / 2;
+      if (Bn < S->Bcur) CK(compact(S, cnt, Bn));
     }
   }
   // final convergence test at the last iterate (the barrier update outputs go to scratch)
@@ -1468,14 +2361,14 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
   hipLaunchKernelGGL(k_prep, dim3(blocks_for(Bc)), dim3(256), 0, st, Bc, n, m, nf, nw, S->free32, S->row_slack, S->gl,
                      S->grad, S->g, S->w, S->gradw, S->c);
   LAUNCHED("k_prep");
-  CK(cpl_ipm_optimality(Bc, nw, m, FMAX, S->nbounds, S->opt.tol, S->opt.acceptable_tol, S->opt.acceptable_iter, S->A,
-                        S->gradw, S->c, S->w, S->y, S->zL, S->zU, S->hasL, S->hasU, S->wl0, S->wu0, S->mu, S->filt_t,
-                        S->filt_p, S->fcount, S->active, S->status, S->acc, S->d_inf, S->err0, S->base, S->mu_o, S->ft,
-                        S->fp, S->fc, st));
+  CK(ipm_optimality_ex(Bc, nw, m, FMAX, S->nbounds, S->opt.tol, S->opt.acceptable_tol, S->opt.acceptable_iter, S->A,
+                       S->gradw, S->c, S->w, S->y, S->zL, S->zU, S->hasL, S->hasU, S->wl0, S->wu0, S->mu, S->filt_t,
+                       S->filt_p, S->fcount, S->active, S->status, S->acc, S->d_inf, S->err0, S->base, S->mu_o, S->ft,
+                       S->fp, S->fc, MU_ROUNDS, S->mu_min, nullptr, S->in_resto, st));
   // every row still in the batch to its instance's place in the full-batch results
   hipLaunchKernelGGL(k_scatter_final, dim3(blocks_for(Bc)), dim3(256), 0, st, Bc, n, m, nw, false, S->orig, S->active,
-                     S->w, S->y, S->Xbase, S->d_inf, S->status, S->iters, S->fw, S->fy, S->fX, S->fdinf, S->fstatus,
-                     S->fiters);
+                     S->w, S->y, S->Xbase, S->d_inf, S->status, S->iters, S->n_resto, S->fw, S->fy, S->fX, S->fdinf,
+                     S->fstatus, S->fiters, S->fresto);
   LAUNCHED("k_scatter_final");
   // IPOPT honor_original_bounds: the final point projected into the original bounds, re-evaluated
   double* Xf = d_x ? d_x : S->Xn;

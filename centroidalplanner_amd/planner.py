@@ -60,6 +60,7 @@ class Solution:
     contact_values_map: Dict[str, ContactValues] = field(default_factory=dict)
     success: bool = True
     message: str = ""
+    iterations: int = 0  # the interior-point iterations the solve took (IPOPT's iteration count)
 
     @property
     def com(self) -> np.ndarray:
@@ -106,7 +107,7 @@ class CentroidalPlanner:
                     derivative_test=self.solver_derivative_test if self.evaluator is None else "none")
         self.last_derivative_report = res.derivative_report
         sol = self._cpl_problem.GetSolution()
-        out = Solution(com_sol=sol["com"], success=res.success, message=res.status)
+        out = Solution(com_sol=sol["com"], success=res.success, message=res.status, iterations=res.iterations)
         for name, cv in sol["contact_values_map"].items():
             out.contact_values_map[name] = ContactValues(cv["force"], cv["position"], cv["normal"])
         return out

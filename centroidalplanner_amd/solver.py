@@ -43,10 +43,10 @@ class _HostBatchEvaluator:
         o = self.ev.eval_batch(X.cpu().numpy())
         return {k: torch.as_tensor(np.asarray(o[k]), device=X.device) for k in outputs}
 
-    def _hessian(self, X, y, free):
+    def _hessian(self, X, y, free, zero_cost=False):
         import torch
 
-        H = self.ev.hessian(X.cpu().numpy(), y.cpu().numpy(), free.cpu().numpy())
+        H = self.ev.hessian(X.cpu().numpy(), y.cpu().numpy(), free.cpu().numpy(), zero_cost=zero_cost)
         return None if H is None else torch.as_tensor(np.asarray(H), device=X.device)
 
 

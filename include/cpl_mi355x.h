@@ -339,6 +339,21 @@ int32_t cpl_kkt_solve(int32_t mode, int64_t batch, int32_t nw, int32_t m, const 
                       const double* d_r1, const double* d_r2, const double* d_mu, const double* d_delta_w_last,
                       const uint8_t* d_active, double* d_dw, double* d_dy, double* d_delta_w, double* d_delta_c,
                       int32_t* d_info, double* d_ws, void* stream);
+/*
+ * The restoration phase's Newton system with p and n eliminated (IPOPT's restoration problem, as
+ * its AugRestoSystemSolver reduces it; no reference counterpart — IPOPT's work behind
+ * src/CentroidalPlanner.cpp:29): per instance
+ *     [ W   A^T ] [dw]   [r1]     W [nw, nw] symmetric, A [m, nw], D = 1 / d_Dinv > 0 (diagonal)
+ *     [ A   -D  ] [dy] = [r2]
+ * through K = W + A^T D^-1 A with IPOPT's inertia correction (K + dW I positive definite; first
+ * dW 1e-4 or d_delta_w_last / 3, growth x100 / x8): dw = K^-1 (r1 + A^T D^-1 r2), dy = D^-1 (A dw - r2).
+ * d_delta_w_last is updated in place (the correction used); d_ws: nw * nw doubles per instance.
+ * d_active [batch] uint8 or NULL: inactive instances are skipped.  nw <= 128.
+ */
+int32_t cpl_kkt_qd_solve(int64_t batch, int32_t nw, int32_t m, const double* d_W, const double* d_A,
+                         const double* d_Dinv, const double* d_r1, const double* d_r2, const uint8_t* d_active,
+                         double* d_delta_w_last, double* d_dw, double* d_dy, double* d_delta_w, double* d_ws,
+                         void* stream);
 
 /*
  * Solve-loop line search, fused per instance (csrc/cpl_ipm.hip; no reference counterpart — the
@@ -458,12 +473,14 @@ int32_t cpl_ipm_dense_a(int64_t batch, int32_t m, int32_t nw, int32_t nf, int32_
 #define CPL_SOLVE_OPTIMAL 0
 #define CPL_SOLVE_ACCEPTABLE 1
 #define CPL_SOLVE_MAX_ITER 2
+#define CPL_SOLVE_INFEASIBLE 3   /* restoration phase converged to a point of local infeasibility */
+#define CPL_SOLVE_RESTO_FAILED 4 /* the restoration phase's line search failed */
 
 typedef struct cpl_solve_options {
   int32_t max_iter;        /* 3000 (IPOPT's default) */
   int32_t hessian;         /* CPL_HESSIAN_*, default CPL_HESSIAN_EXACT */
-  int32_t max_ls;          /* line-search trials per iteration, 4 */
-  int32_t max_soc;         /* second-order corrections on the first trial, 1 */
+  int32_t max_ls;          /* backtracking trials per iteration at most (also alpha_min), 40 */
+  int32_t max_soc;         /* second-order corrections on the first trial, 4 (IPOPT max_soc) */
   int32_t acceptable_iter; /* 15 */
   int32_t use_graph;       /* capture the iteration as a HIP graph, 1 */
   int32_t compact;         /* active-set compaction, 1: once at most half of the batch is still
@@ -499,6 +516,8 @@ int32_t cpl_solver_solve(cpl_solver* s, const double* d_x0, const double* d_mass
 int32_t cpl_solver_dims(const cpl_solver* s, int32_t* nf, int32_t* n_ineq, int32_t* graph_captured);
 /* the last solve's active-set compactions and its final lock-step batch size */
 int32_t cpl_solver_stats(const cpl_solver* s, int32_t* compactions, int64_t* final_rows);
+/* the last solve's restoration-phase entries per instance into d_out [batch] (device int64) */
+int32_t cpl_solver_restorations(const cpl_solver* s, int64_t* d_out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -36,10 +36,19 @@ class OracleBatchEvaluator:
                                 None, outputs=tuple(outputs), nthreads=self.nthreads)
         return {k: torch.as_tensor(v, device=X.device) for k, v in o.items()}
 
-    def hessian(self, X, y, free):
+    def hessian(self, X, y, free, zero_cost=False):
+        """zero_cost: the Hessian of y^T g alone (the template with zero cost weights — the
+        restoration phase's constraint curvature)."""
         if self.problem.desc().env_kind not in (0, 1):
             return None
-        H = pyoracle.lagrangian_hessian(self.problem.desc(), X.cpu().numpy(), y.cpu().numpy(), free.cpu().numpy())
+        d = self.problem.desc()
+        if zero_cost:
+            d = type(d).from_buffer_copy(d)
+            d.W_com = 0.0
+            for i in range(len(d.W_F)):
+                d.W_F[i] = 0.0
+                d.W_p[i] = 0.0
+        H = pyoracle.lagrangian_hessian(d, X.cpu().numpy(), y.cpu().numpy(), free.cpu().numpy())
         return torch.as_tensor(H, device=X.device)
 
 
@@ -222,13 +231,19 @@ def _certify_scenario(which, prob, x, mass, wrench):
         np.testing.assert_array_equal(x[3 + 27: 6 + 27], 0.0)
 
 
+# the Hessian mode per scenario: IPOPT's exact Hessian on the exponent-10 superquadric surface (the
+# limited-memory model stalls there), IFOPT's limited-memory model on CoMPlanner (whose held contact
+# sits on the cone's kink at zero tangential force, where the exact Hessian of |F_t| is unbounded)
+_HESSIAN = {"superquadric": "exact", "com": "limited-memory"}
+
+
 @pytest.mark.parametrize("which", ["superquadric", "com"])
 def test_batch_solve_other_scenarios_oracle_cpu(which):
     prob, x0, wrench = _scenario(which)
     B = 4
     mass = np.random.default_rng(3).uniform(80.0, 150.0, B)
     r = batch_ipm_solve(prob, torch.as_tensor(np.tile(x0, (B, 1))), torch.as_tensor(mass),
-                        evaluator=OracleBatchEvaluator(prob), max_iter=300)
+                        evaluator=OracleBatchEvaluator(prob), max_iter=300, hessian=_HESSIAN[which])
     assert bool((r.status <= STATUS_ACCEPTABLE).all()), r.status
     for b in range(B):
         _certify_scenario(which, prob, r.x[b].numpy(), mass[b], wrench)
@@ -242,17 +257,11 @@ def test_batch_solve_other_scenarios_gpu(which):
     mass = np.random.default_rng(4).uniform(80.0, 150.0, B)
     dev = torch.device("cuda:0")
     r = batch_ipm_solve(prob, torch.as_tensor(np.tile(x0, (B, 1)), device=dev), torch.as_tensor(mass, device=dev),
-                        max_iter=1000)
+                        max_iter=1000, hessian=_HESSIAN[which])
     assert r.graph
     st = r.status.cpu().numpy()
     ok = st <= STATUS_ACCEPTABLE
-    if which == "superquadric":
-        assert ok.all(), np.bincount(st)
-    else:
-        # CoMPlanner: the contact held at its force threshold ends at zero tangential force, where
-        # |F_t| - mu F_n is not differentiable (the reference's Jacobian is 0/0 there): Newton
-        # converges slowly around the kink (30-800 iterations on the CPU sample)
-        assert ok.mean() >= 0.97, np.bincount(st)
+    assert ok.all(), np.bincount(st)
     X = r.x.cpu().numpy()
     for b in np.flatnonzero(ok)[::17]:
         _certify_scenario(which, prob, X[b], mass[b], wrench)

@@ -1,0 +1,78 @@
+"""The native solve engine (csrc/cpl_solver.hip) against itself and against the host restatement
+(batch_ipm.py over the oracle's callbacks) on the paths the round-3 iteration added: IPOPT's
+restoration phase, soft restoration and tiny steps.
+
+* batch independence: every kernel of the iteration works on one instance per wave / workgroup and
+  the KKT kernel is chosen by the system size alone (cpl_kkt.hip kkt_wave_kernel_for), so an
+  instance solved alone and the same instance inside a batch of 64 take bitwise the same iterates;
+* the restoration phase on the device: TestBasic's superquadric scenario from x = 0 enters it on its
+  first iteration (the 0/0 cone Jacobian makes the first Newton step useless); the device solve
+  ends like the host restatement (same status, same number of restoration phases, objective to the
+  rounding of the two evaluators: the eval kernel and the oracle differ in the last bits of pow).
+"""
+import numpy as np
+import pytest
+import torch
+
+from centroidalplanner_amd.batch_ipm import STATUS_ACCEPTABLE, batch_ipm_solve
+from centroidalplanner_amd.workload import solve_inputs, solve_problem
+
+from test_batch_solve import OracleBatchEvaluator, _HESSIAN, _scenario
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hessian", ["exact", "limited-memory"])
+def test_instance_alone_is_bitwise_the_instance_in_a_batch(hessian):
+    prob = solve_problem().GetCplProblem()
+    B = 64
+    X0, mass = solve_inputs(prob, B, seed=31)
+    dev = torch.device("cuda:0")
+    full = batch_ipm_solve(prob, torch.as_tensor(X0, device=dev), torch.as_tensor(mass, device=dev), max_iter=1000,
+                           hessian=hessian)
+    assert bool((full.status <= STATUS_ACCEPTABLE).all())
+    for k in (0, 17, 63):
+        one = batch_ipm_solve(prob, torch.as_tensor(X0[k:k + 1], device=dev), torch.as_tensor(mass[k:k + 1], device=dev),
+                              max_iter=1000, hessian=hessian)
+        assert int(one.status[0]) == int(full.status[k]) and int(one.iterations[0]) == int(full.iterations[k])
+        assert torch.equal(one.x[0], full.x[k]) and torch.equal(one.y[0], full.y[k])
+
+
+def _zero_start(prob):
+    xl, xu, _, _ = prob.get_bounds_info()
+    return np.clip(np.zeros(prob.n), xl, xu)
+
+
+@pytest.mark.gpu
+def test_restoration_phase_device_matches_host():
+    prob, _, _ = _scenario("superquadric")
+    x0 = _zero_start(prob)
+    mass = np.array([100.0, 96.57673546])
+    B = mass.size
+    dev = torch.device("cuda:0")
+    d = batch_ipm_solve(prob, torch.as_tensor(np.tile(x0, (B, 1)), device=dev), torch.as_tensor(mass, device=dev),
+                        max_iter=1000, hessian=_HESSIAN["superquadric"])
+    h = batch_ipm_solve(prob, torch.as_tensor(np.tile(x0, (B, 1))), torch.as_tensor(mass),
+                        evaluator=OracleBatchEvaluator(prob), max_iter=1000, hessian=_HESSIAN["superquadric"])
+    assert d.restorations is not None and d.restorations.dtype == torch.int64
+    rd, rh = d.restorations.cpu().numpy(), h.restorations.numpy()
+    assert (rh >= 1).all()  # x = 0: the restoration phase from the first iteration
+    np.testing.assert_array_equal(d.status.cpu().numpy(), h.status.numpy())
+    np.testing.assert_array_equal(rd, rh)
+    assert bool((h.status <= STATUS_ACCEPTABLE).all())
+    np.testing.assert_allclose(d.objective.cpu().numpy(), h.objective.numpy(), rtol=1e-6)
+
+
+@pytest.mark.gpu
+def test_com_planner_from_zero_device_matches_host():
+    """CoMPlanner from x = 0 (limited-memory): no restoration phase, converged on both paths."""
+    prob, _, _ = _scenario("com")
+    x0 = _zero_start(prob)
+    mass = np.random.default_rng(3).uniform(80.0, 150.0, 8)
+    B = mass.size
+    dev = torch.device("cuda:0")
+    d = batch_ipm_solve(prob, torch.as_tensor(np.tile(x0, (B, 1)), device=dev), torch.as_tensor(mass, device=dev),
+                        max_iter=1000, hessian="limited-memory")
+    h = batch_ipm_solve(prob, torch.as_tensor(np.tile(x0, (B, 1))), torch.as_tensor(mass),
+                        evaluator=OracleBatchEvaluator(prob), max_iter=1000, hessian="limited-memory")
+    assert bool((d.status <= STATUS_ACCEPTABLE).all()) and bool((h.status <= STATUS_ACCEPTABLE).all())
+    np.testing.assert_allclose(d.objective.cpu().numpy(), h.objective.numpy(), rtol=1e-6, atol=1e-9)

@@ -194,12 +194,15 @@ def test_optimality_error_convergence_and_barrier_update():
     acc_now = active & ~done & (acc_new >= acc_iter)
     st_ref = np.where(done, 0, np.where(acc_now, 1, status))
     act = active & ~done & ~acc_now
+    # IPOPT's monotone update: up to 6 decreases per iteration (mu_allow_fast_monotone_decrease), floor
+    # min(tol, compl_inf_tol 1e-4) / (barrier_tol_factor 10 + 1)
+    mu_min = min(tol, 1e-4) / 11.0
     mu_r, reset = mu.copy(), np.zeros(B, dtype=bool)
-    for _ in range(2):
+    for _ in range(6):
         em = np.maximum(np.abs(cl - np.where(hasL, mu_r[:, None], 0.0)).max(1),
                         np.abs(cu - np.where(hasU, mu_r[:, None], 0.0)).max(1))
-        upd = act & (np.maximum(base, em / sc) <= 10.0 * mu_r) & (mu_r > tol / 10.0)
-        mu_r = np.where(upd, np.maximum(np.minimum(0.2 * mu_r, mu_r ** 1.5), tol / 10.0), mu_r)
+        upd = act & (np.maximum(base, em / sc) <= 10.0 * mu_r) & (mu_r > mu_min)
+        mu_r = np.where(upd, np.maximum(np.minimum(0.2 * mu_r, mu_r ** 1.5), mu_min), mu_r)
         reset |= upd
     T = {k: _t(v) for k, v in dict(A=A, gw=gw, c=c, w=w, y=y, zL=zL, zU=zU, wl0=wl0, wu0=wu0, mu=mu, ft=ft,
                                     fp=fp).items()}
