@@ -143,12 +143,14 @@ def plain_rel_off_diagonals(prob, env, x, got, ref, tag=None):
     B = x.shape[0]
     sq_inst = (np.ones(B, dtype=bool) if env == "superquadric" else
                (tag == ENV_SUPERQUADRIC) if env == "mixed" else np.zeros(B, dtype=bool))
+    out = {"entries": 0, "g": 0.0, "jac": 0.0,
+           "hist": {"bitwise": 0, "lt1e-15": 0, "lt1e-13": 0, "lt1e-12": 0, "lt1e-10": 0, "ge1e-10": 0}}
+    if not sq_inst.any():  # no Superquadric contact rows in this layout: no pow-bearing entries
+        return out
     jm, gm = sq_entry_mask(N, prob.map_order, nnz, m, sq_inst)
     for jo, _, _ in contact_offsets(N, True, prob.map_order):
         for a in range(3):
             jm[:, jo + 3 + 4 * a + a] = False  # the diagonal of normal-Jacobian row a
-    out = {"entries": 0, "hist": {"bitwise": 0, "lt1e-15": 0, "lt1e-13": 0, "lt1e-12": 0, "lt1e-10": 0,
-                                  "ge1e-10": 0}}
     for k, mask in (("g", gm), ("jac", jm)):
         gv, rv = np.asarray(got[k]), np.asarray(ref[k])
         sel = mask & ~(np.isnan(gv) | np.isnan(rv))
