@@ -419,7 +419,8 @@ __global__ __launch_bounds__(256) void cpl_ipm_post_step_kernel(
 // Acceptance (batch_ipm.py step, "accept" + state write-back, in place): filter augmentation after
 // h-type steps (ring slot fcount mod nfilt), filter reset of failed searches, y += alpha dy,
 // z += a_z dz with the kappa_Sigma = 1e10 safeguard at the new point, w <- w_new, mu, iters.
-// a_z is taken as 0 where rest (the feasibility step keeps the multipliers).
+// a_z is taken as 0 where rest (the feasibility step keeps the multipliers).  failed / rest may be
+// NULL (no filter resets / no multiplier-keeping rows: the solve engine's restoration phase).
 __global__ __launch_bounds__(256) void cpl_ipm_accept_kernel(
     int64_t batch, int nw, int m, int nfilt, const uint8_t* __restrict__ active, const uint8_t* __restrict__ aug,
     const uint8_t* __restrict__ failed, const uint8_t* __restrict__ rest, const double* __restrict__ alpha,
@@ -741,7 +742,7 @@ int32_t cpl_ipm_accept(int64_t batch, int32_t nw, int32_t m, int32_t nfilt, cons
                        double* d_filt_t, double* d_filt_p, int64_t* d_fcount, void* stream) {
   if (batch < 0 || nw <= 0 || m < 0 || nfilt <= 0) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_accept: bad sizes");
   if (batch == 0) return CPL_OK;
-  if (!d_active || !d_aug || !d_failed || !d_rest || !d_alpha || !d_a_z || !d_theta || !d_phi || !d_filt_t_in ||
+  if (!d_active || !d_aug || !d_alpha || !d_a_z || !d_theta || !d_phi || !d_filt_t_in ||
       !d_filt_p_in || !d_fcount_in || !d_w_new || (m > 0 && (!d_dy || !d_y)) || !d_dzL || !d_dzU || !d_mu ||
       !d_hasL || !d_hasU || !d_wl0 || !d_wu0 || !d_w || !d_zL || !d_zU || !d_mu_state || !d_iters || !d_filt_t ||
       !d_filt_p || !d_fcount)

@@ -416,7 +416,7 @@ int32_t cpl_ipm_max_step(int64_t batch, int32_t nw, const double* d_v, const dou
  * cpl_ipm_post_step: dzL, dzU from the primal step, the primal and dual fraction-to-the-boundary
  *   steps, gd = grad_phi . dw, the switching-condition flag, delta_w_last on active instances.
  * cpl_ipm_accept: filter augmentation / reset, y, z (kappa_Sigma safeguard), w, mu and iteration
- *   counters written back in place.
+ *   counters written back in place (d_failed: filter reset rows, d_rest: rows keeping z; both optional).
  * cpl_ipm_masked_rows: dst[b, :] = src[b, :] where mask[b].
  * d_active (optional, where present): instances with active[b] == 0 are skipped — their outputs
  * are left unwritten (converged instances of the solve loop, whose Newton data is never read).
