@@ -577,8 +577,10 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         fin = torch.isfinite(ph) & torch.isfinite(th)
         in_filter = ((th[:, None] <= ft) | (ph[:, None] <= fp)).all(1)
         ftype = switch_ok & (al * torch.where(gd < 0, -gd, torch.zeros_like(gd)) ** S_PHI > DELTA_SW * theta_k ** S_TH)
-        armijo = ph <= phi_k + ETA_PHI * al * gd
-        suff = (th <= (1.0 - GAMMA_TH) * theta_k) | (ph <= phi_k - GAMMA_PHI * theta_k)
+        # IPOPT's Compare_le(lhs, rhs, base): lhs - rhs <= 10 eps |base| (round-off of the reference values)
+        ro_p, ro_t = 10.0 * EPS * phi_k.abs(), 10.0 * EPS * theta_k.abs()
+        armijo = (ph - phi_k) - ETA_PHI * al * gd <= ro_p
+        suff = (th - (1.0 - GAMMA_TH) * theta_k <= ro_t) | ((ph - phi_k) - (-GAMMA_PHI * theta_k) <= ro_p)
         if not from_resto:  # obj_max_inc = 5: the barrier objective may not jump by 5 orders of magnitude
             base = torch.where(phi_k.abs() > 10.0, torch.log10(phi_k.abs().clamp(min=1e-300)), torch.ones_like(phi_k))
             inc = ph - phi_k
@@ -844,9 +846,17 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
             S["in_soft"].copy_(torch.where(left, False, torch.where(soft_ok, True, S["in_soft"])))
             S["soft_cnt"].copy_(torch.where(left | (soft_ok & ~soft_now), 0, S["soft_cnt"]))
         failed = act & ~tiny & ~st["found"]  # -> the restoration phase
+        # IPOPT calls no restoration phase at an acceptable point (BacktrackingLineSearch: "Restoration
+        # phase called at acceptable point" -> STOP_AT_ACCEPTABLE_POINT): the solve ends there
+        at_acc = failed & (E["err0"] <= acceptable_tol)
+        act_it = act & ~at_acc  # the instances whose iteration counts
+        if bool(at_acc.any()):
+            S["status"].copy_(torch.where(at_acc, STATUS_ACCEPTABLE, S["status"]))
+            S["active"].copy_(S["active"] & ~at_acc)
+            failed = failed & ~at_acc
         S["in_soft"].copy_(S["in_soft"] & ~failed)
         S["soft_cnt"].copy_(torch.where(failed, 0, S["soft_cnt"]))
-        moved = act & ~failed
+        moved = act_it & ~failed
         w_new = st["w"]
         al = st["alpha"]
         a_z = torch.where(soft_ok, a_soft, a_z)  # the soft step moves the bound multipliers by alpha too
@@ -879,7 +889,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         S["zL"].copy_(zL_new)
         S["zU"].copy_(zU_new)
         S["mu"].copy_(torch.where(act, mu, S["mu"]))
-        S["iters"].copy_(S["iters"] + act.to(torch.int64))
+        S["iters"].copy_(S["iters"] + act_it.to(torch.int64))
         S["filt_t"].copy_(ft)
         S["filt_p"].copy_(fp)
         S["fcount"].copy_(fc)
@@ -1085,7 +1095,9 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         ph_o = new["f"] + barrier(w_new, mu)
         fin = torch.isfinite(th_o) & torch.isfinite(ph_o)
         in_filter = ((th_o[:, None] <= S["filt_t"]) | (ph_o[:, None] <= S["filt_p"])).all(1)
-        vs_start = (th_o <= (1.0 - GAMMA_TH) * S["th_o0"]) | (ph_o <= S["ph_o0"] - GAMMA_PHI * S["th_o0"])
+        t0, p0 = S["th_o0"], S["ph_o0"]
+        vs_start = (th_o - (1.0 - GAMMA_TH) * t0 <= 10.0 * EPS * t0.abs()) | \
+            ((ph_o - p0) - (-GAMMA_PHI * t0) <= 10.0 * EPS * p0.abs())
         back = moved & fin & (th_o <= KAPPA_RESTO * S["th_o0"]) & in_filter & vs_start
         if verbose > 1:
             b = verbose_instance

@@ -7,6 +7,8 @@
 // a different order (last-bit differences only).
 #include <hip/hip_runtime.h>
 
+#include <cfloat>
+
 #include <cmath>
 #include <cstdint>
 #include <string>
@@ -85,8 +87,10 @@ __global__ __launch_bounds__(256) void cpl_ipm_judge_take_kernel(
   const double al = alpha[b], tk = theta_k[b], pk = phi_k[b], g = gd[b];
   const bool fin = isfinite(ph) && isfinite(th);
   const bool ftype = switch_ok[b] && (al * pow(fmax(-g, 0.0), 2.3) > pow(tk, 1.1));
-  bool armijo = ph <= pk + 1e-8 * al * g;
-  bool suff = (th <= (1.0 - 1e-5) * tk) || (ph <= pk - 1e-8 * tk);
+  // IPOPT's Compare_le(lhs, rhs, base): lhs - rhs <= 10 eps |base| (round-off of the reference values)
+  const double ro_p = 10.0 * DBL_EPSILON * fabs(pk), ro_t = 10.0 * DBL_EPSILON * fabs(tk);
+  bool armijo = (ph - pk) - 1e-8 * al * g <= ro_p;
+  bool suff = (th - (1.0 - 1e-5) * tk <= ro_t) || ((ph - pk) - (-1e-8 * tk) <= ro_p);
   // obj_max_inc = 5: a barrier objective more than 5 orders of magnitude above the current one is
   // rejected (IPOPT FilterLSAcceptor::IsAcceptableToCurrentIterate)
   if (ph > pk) {

@@ -259,8 +259,10 @@ __device__ __forceinline__ bool acceptable_wave(double th, double ph, double tk,
   const bool in_filter = __ballot(rejected) == 0;
   const bool fin = isfinite(ph) && isfinite(th);
   const bool ftype = switch_ok && (al * pow(fmax(-g, 0.0), S_PHI) > DELTA_SW * pow(tk, S_TH));
-  bool armijo = ph <= pk + ETA_PHI * al * g;
-  bool suff = (th <= (1.0 - GAMMA_TH) * tk) || (ph <= pk - GAMMA_PHI * tk);
+  // IPOPT's Compare_le(lhs, rhs, base): lhs - rhs <= 10 eps |base| (round-off of the reference values)
+  const double ro_p = 10.0 * DBL_EPSILON * fabs(pk), ro_t = 10.0 * DBL_EPSILON * fabs(tk);
+  bool armijo = (ph - pk) - ETA_PHI * al * g <= ro_p;
+  bool suff = (th - (1.0 - GAMMA_TH) * tk <= ro_t) || ((ph - pk) - (-GAMMA_PHI * tk) <= ro_p);
   if (ph > pk) {
     const double basval = fabs(pk) > 10.0 ? log10(fabs(pk)) : 1.0;
     if (log10(ph - pk) > OBJ_MAX_INC + basval) armijo = suff = false;
@@ -529,14 +531,24 @@ __global__ __launch_bounds__(256) void k_soft_judge(
 }
 
 // the end of the regular line search: failed = no accepted point (-> the restoration phase),
-// moved = an accepted one; a failed search leaves the soft phase
+// moved = an accepted one; a failed search leaves the soft phase.  IPOPT calls no restoration phase
+// at an acceptable point (BacktrackingLineSearch: "Restoration phase called at acceptable point" ->
+// STOP_AT_ACCEPTABLE_POINT): an instance whose search failed there ends with status acceptable.
 __global__ void k_fail(int64_t B, const uint8_t* __restrict__ act, const double* __restrict__ st_alpha,
-                       uint8_t* __restrict__ failed, uint8_t* __restrict__ moved, uint8_t* __restrict__ in_soft,
-                       int32_t* __restrict__ soft_cnt) {
+                       const double* __restrict__ err0, double acc_tol, uint8_t* __restrict__ failed,
+                       uint8_t* __restrict__ moved, uint8_t* __restrict__ in_soft, int32_t* __restrict__ soft_cnt,
+                       int64_t* __restrict__ status, uint8_t* __restrict__ active) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const bool a = act[b] != 0;
-  const bool f = a && !(st_alpha[b] > 0.0);
+  bool f = a && !(st_alpha[b] > 0.0);
+  if (f && err0[b] <= acc_tol) {
+    status[b] = CPL_SOLVE_ACCEPTABLE;
+    active[b] = 0;
+    failed[b] = 0;
+    moved[b] = 0;
+    return;
+  }
   failed[b] = f ? 1 : 0;
   moved[b] = (a && !f) ? 1 : 0;
   if (f) {
@@ -1228,7 +1240,9 @@ __global__ __launch_bounds__(256) void k_resto_accept(
   for (int k = lane; k < FMAX; k += 64) rejected |= !((th <= filt_t[b * FMAX + k]) || (ph <= filt_p[b * FMAX + k]));
   const bool in_filter = __ballot(rejected) == 0;
   const double t0 = th_o0[b];
-  const bool vs_start = (th <= (1.0 - GAMMA_TH) * t0) || (ph <= ph_o0[b] - GAMMA_PHI * t0);
+  const double p0 = ph_o0[b];
+  const bool vs_start = (th - (1.0 - GAMMA_TH) * t0 <= 10.0 * DBL_EPSILON * fabs(t0)) ||
+                        ((ph - p0) - (-GAMMA_PHI * t0) <= 10.0 * DBL_EPSILON * fabs(p0));
   const bool back = isfinite(th) && isfinite(ph) && th <= KAPPA_RESTO * t0 && in_filter && vs_start;
   if (!back) return;
   const double tau = fmax(1.0 - mub, 0.99);
@@ -1754,8 +1768,8 @@ int32_t step_phase(cpl_solver* S, int phase) {
       return CPL_OK;
     }
     case P_ACCEPT: {
-      hipLaunchKernelGGL(k_fail, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->act, S->st_alpha, S->failed, S->moved,
-                         S->in_soft, S->soft_cnt);
+      hipLaunchKernelGGL(k_fail, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->act, S->st_alpha, S->err0,
+                         o.acceptable_tol, S->failed, S->moved, S->in_soft, S->soft_cnt, S->status, S->active);
       LAUNCHED("k_fail");
       // the accepted points with their derivatives: one full evaluation
       hipLaunchKernelGGL(k_unpack, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, nw, S->freepos, S->Xbase,
