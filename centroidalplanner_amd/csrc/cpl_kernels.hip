@@ -1178,41 +1178,28 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
   const int n_gr = valid - n_sq;
   const bool compute = K.ablate != 1;
 
-  // ---- phase 1 (Superquadric): per-axis power ladders into the LDS scratch
-  if (HAS_SQ && compute && n_sq > 0 && (K.want_g || K.want_j)) {
-    const int items1 = 3 * N * n_sq;
-    for (int it = tid; it < items1; it += WG) {
-      const int j = it % n_sq, ka = it / n_sq;
-      const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
-      const int k = ka / 3, a = ka - 3 * k;
-      sq_axis_item(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m);
-    }
-    __syncthreads();
-  }
-
-  // ---- phase 2: SQ rows | Ground / no-env contacts | statics | cost
+  // ---- phase 1: the Superquadric power ladders (into the LDS scratch); phase 2: the Superquadric
+  // rows.  The items that do not read the scratch (Ground / no-env contacts, statics, cost) join
+  // phase 1 for Superquadric batches, so that the two barrier-separated phases carry comparable work
+  // (sq8 0.347 -> 0.329 ms), and phase 2 for mixed batches, where the tile's Ground contacts then
+  // overlap the Superquadric rows (3.50 -> 3.44 ms for mixed16; profiles/r3/ab_*).  SQ items run
+  // axis-major (item -> (axis, contact, instance)).
+  constexpr bool OTHERS_FIRST = ENVK != CPL_ENV_MIXED;
+  const bool wgj = K.want_g || K.want_j;
   if (compute) {
-    const int r_sq = (HAS_SQ && (K.want_g || K.want_j)) ? 3 * N * n_sq : 0;
-    const int r_gr = (ENVK != CPL_ENV_SUPERQUADRIC && (K.want_g || K.want_j)) ? N * n_gr : 0;
-    const int r_st = (K.want_g || K.want_j) ? 4 * valid : 0;
+    const int r_ax = (HAS_SQ && wgj) ? 3 * N * n_sq : 0;
+    const int r_gr = (ENVK != CPL_ENV_SUPERQUADRIC && wgj) ? N * n_gr : 0;
+    const int r_st = wgj ? 4 * valid : 0;
     const int r_co = K.cost_seg >= 0 ? valid : 0;
-    const int items2 = r_sq + r_gr + r_st + r_co;
-    for (int it = tid; it < items2; it += WG) {
-      int e = it;
-      if (e < r_sq) {
-        const int j = e % n_sq, ka = e / n_sq;
-        const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
-        const int k = ka / 3, a = ka - 3 * k;
-        sq_row_item(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m, Jt + r * nnz);
-        continue;
-      }
-      e -= r_sq;
+    const int r_oth = r_gr + r_st + r_co;
+    const int per_axis = N * n_sq;
+    auto other_item = [&](int e) {
       if (e < r_gr) {
         const int j = e % n_gr, k = e / n_gr;
         const int r = ENVK == CPL_ENV_MIXED ? lists[64 + j] : j;
         contact_item<ENVK == CPL_ENV_NONE ? CPL_ENV_NONE : CPL_ENV_GROUND>(K, X + r * n, CPL_ENV_GROUND, k,
                                                                           Gt + r * m, Jt + r * nnz);
-        continue;
+        return;
       }
       e -= r_gr;
       if (e < r_st) {
@@ -1220,10 +1207,34 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
         const double* xr = X + r * n;
         if (sg == 0) statics_values_item(K, xr, mass ? mass[b0 + r] : mass_def, Gt + r * m, Jt + r * nnz);
         else if (K.want_j) statics_row_item(K, xr, sg - 1, Jt + r * nnz);
-        continue;
+        return;
       }
       e -= r_st;
       cost_item(K, X + e * n, f_out ? f_out + b0 + e : nullptr, Dt + e * n);
+    };
+    const int items1 = r_ax + (OTHERS_FIRST ? r_oth : 0);
+    for (int it = tid; it < items1; it += WG) {
+      if (HAS_SQ && it < r_ax) {
+        const int a = it / per_axis, kj = it - a * per_axis;
+        const int k = kj / n_sq, j = kj - k * n_sq;
+        const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
+        sq_axis_item(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m);
+      } else {
+        other_item(it - r_ax);
+      }
+    }
+    if (HAS_SQ && n_sq > 0 && wgj) __syncthreads();
+    const int r_rows = r_ax;
+    const int items2 = r_rows + (OTHERS_FIRST ? 0 : r_oth);
+    for (int it = tid; it < items2; it += WG) {
+      if (HAS_SQ && it < r_rows) {
+        const int a = it / per_axis, kj = it - a * per_axis;
+        const int k = kj / n_sq, j = kj - k * n_sq;
+        const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
+        sq_row_item(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m, Jt + r * nnz);
+      } else {
+        other_item(it - r_rows);
+      }
     }
   }
   __syncthreads();
@@ -1412,36 +1423,26 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
     const int n_gr = valid - n_sq;
     const bool wgj = K.want_g || K.want_j;
 
-    // ---- phase 1 (Superquadric power ladders)
-    if (HAS_SQ) {
-      if (n_sq > 0 && wgj && K.ablate != 1) {
-        const int items1 = 3 * N * n_sq;
-        for (int it = tid; it < items1; it += CT) {
-          const int j = it % n_sq, ka = it / n_sq;
-          const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
-          const int k = ka / 3, a = ka - 3 * k;
-          sq_axis_item(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m);
-        }
-      }
-      lds_barrier();
-    }
-    // ---- phase 2
+    // ---- phase 1: the Superquadric power ladders with every item that does not read their scratch
+    // (contacts without Superquadric, statics, cost); phase 2: the Superquadric rows (as the tile
+    // kernel; SQ items axis-major)
     if (K.ablate != 1) {
-      const int r_sq = (HAS_SQ && wgj) ? 3 * N * n_sq : 0;
+      const int r_ax = (HAS_SQ && wgj) ? 3 * N * n_sq : 0;
       const int r_gr = (ENVK != CPL_ENV_SUPERQUADRIC && wgj) ? N * n_gr : 0;
       const int r_st = wgj ? 4 * valid : 0;
       const int r_co = K.cost_seg >= 0 ? valid : 0;
-      const int items2 = r_sq + r_gr + r_st + r_co;
-      for (int it = tid; it < items2; it += CT) {
+      const int items1 = r_ax + r_gr + r_st + r_co;
+      const int per_axis = N * n_sq;
+      for (int it = tid; it < items1; it += CT) {
         int e = it;
-        if (HAS_SQ && e < r_sq) {
-          const int j = e % n_sq, ka = e / n_sq;
+        if (HAS_SQ && e < r_ax) {
+          const int a = e / per_axis, kj = e - a * per_axis;
+          const int k = kj / n_sq, j = kj - k * n_sq;
           const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
-          const int k = ka / 3, a = ka - 3 * k;
-          sq_row_item(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m, Jt + r * nnz);
+          sq_axis_item(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m);
           continue;
         }
-        e -= r_sq;
+        e -= r_ax;
         if (e < r_gr) {
           const int j = e % n_gr, k = e / n_gr;
           const int r = ENVK == CPL_ENV_MIXED ? lists[64 + j] : j;
@@ -1463,6 +1464,20 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
         if (!HAS_SQ && K.lg_active && !K.lg_active[(b0 + e) / K.y_repeat]) continue;
         cost_item(K, X + e * n, f_out ? f_out + b0 + e : nullptr, Dt + e * n);
       }
+      if (HAS_SQ) {
+        lds_barrier();
+        if (wgj) {
+          const int items2 = 3 * per_axis;
+          for (int it = tid; it < items2; it += CT) {
+            const int a = it / per_axis, kj = it - a * per_axis;
+            const int k = kj / n_sq, j = kj - k * n_sq;
+            const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
+            sq_row_item(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m, Jt + r * nnz);
+          }
+        }
+      }
+    } else if (HAS_SQ) {
+      lds_barrier();
     }
     lds_barrier();  // the tile image is complete
     if (K.want_lgrad) {

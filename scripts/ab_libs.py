@@ -31,9 +31,10 @@ libs = {}
 for tag in args.libs.split(","):
     path = tag
     lib = ctypes.CDLL(os.path.abspath(path), mode=ctypes.RTLD_LOCAL)
-    fn = lib.cpl_time_eval_batch
-    res, sig = _abi.SIGNATURES["cpl_time_eval_batch"]
-    fn.restype, fn.argtypes = res, sig
+    for name in ("cpl_time_eval_batch", "cpl_eval_batch"):
+        fn = getattr(lib, name)
+        res, sig = _abi.SIGNATURES[name]
+        fn.restype, fn.argtypes = res, sig
     libs[tag] = lib
 
 cfg = CONFIGS[args.config]
@@ -53,6 +54,18 @@ for _ in range(args.rounds):
                                            None, None, p(out["norms"]), ctypes.c_void_p(stream.cuda_stream), args.reps,
                                            ctypes.byref(ms)))
         times[k].append(ms.value)
+# every library's outputs on the same inputs, compared bit for bit with the first one's
+ref = None
+for k, lib in libs.items():
+    g, jac = torch.full_like(out["g"], float("nan")), torch.full_like(out["jac"], float("nan"))
+    _abi.check(lib.cpl_eval_batch(ctypes.byref(prob.desc()), B, p(xt), p(mt), p(tt), p(g), p(jac), None, None,
+                                  ctypes.c_void_p(stream.cuda_stream)))
+    torch.cuda.synchronize()
+    if ref is None:
+        ref = (k, g, jac)
+    else:
+        same = all(bool(((a == b) | (torch.isnan(a) & torch.isnan(b))).all()) for a, b in ((g, ref[1]), (jac, ref[2])))
+        print(json.dumps({"lib": k, "bitwise_equal_to": ref[0], "equal": same}), flush=True)
 bpi, m = algorithmic_bytes(cfg.n_contacts, cfg.env)
 for k, ts in times.items():
     med = statistics.median(ts)
