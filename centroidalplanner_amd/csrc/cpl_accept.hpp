@@ -1,0 +1,89 @@
+// cpl_accept.hpp — IPOPT's filter line-search acceptance test on one wave (FilterLSAcceptor
+// [IPOPT]; batch_ipm.py `acceptable` restates it), shared by the solve engine's kernels
+// (cpl_ipm.hip's judge, cpl_solver.hip's soft / restoration judges, cpl_kernels.hip's backtracking
+// kernel), and the argument block of that backtracking kernel (cpl_kernels.hip ls_backtrack, called
+// by cpl_solver.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+
+namespace cpl {
+
+// gamma_theta, gamma_phi, delta, s_theta, s_phi, eta_phi, obj_max_inc [IPOPT defaults]
+constexpr double LS_GAMMA_TH = 1e-5, LS_GAMMA_PHI = 1e-8, LS_DELTA = 1.0, LS_S_TH = 1.1, LS_S_PHI = 2.3;
+constexpr double LS_ETA_PHI = 1e-8, LS_OBJ_MAX_INC = 5.0;
+constexpr int LS_MAX_SOFT_RESTO = 10;  // max_soft_resto_iters
+
+// theta_max; the filter (entries stored with their margins ((1 - gamma_theta) theta, phi - gamma_phi
+// theta): acceptable when, for every entry, theta or phi is not larger — IPOPT's Filter::Acceptable);
+// the switching condition; Armijo on the barrier objective for an f-type step, else sufficient
+// decrease of theta or phi against the reference point, both with IPOPT's round-off tolerance
+// Compare_le(lhs, rhs, base) = lhs - rhs <= 10 eps |base|; obj_max_inc.  *h_type: the step augments
+// the filter.  Every lane of the wave must call it (a ballot).
+__device__ __forceinline__ bool ls_acceptable_wave(double th, double ph, double tk, double pk, double g, double al,
+                                                   bool switch_ok, double theta_max, const double* ft,
+                                                   const double* fp, int nfilt, bool* h_type) {
+  const int lane = threadIdx.x & 63;
+  bool rejected = false;
+  for (int k = lane; k < nfilt; k += 64) rejected |= !((th <= ft[k]) || (ph <= fp[k]));
+  const bool in_filter = __ballot(rejected) == 0;
+  const bool fin = isfinite(ph) && isfinite(th);
+  const bool ftype = switch_ok && (al * pow(fmax(-g, 0.0), LS_S_PHI) > LS_DELTA * pow(tk, LS_S_TH));
+  const double ro_p = 10.0 * DBL_EPSILON * fabs(pk), ro_t = 10.0 * DBL_EPSILON * fabs(tk);
+  bool armijo = (ph - pk) - LS_ETA_PHI * al * g <= ro_p;
+  bool suff = (th - (1.0 - LS_GAMMA_TH) * tk <= ro_t) || ((ph - pk) - (-LS_GAMMA_PHI * tk) <= ro_p);
+  if (ph > pk) {  // IsAcceptableToCurrentIterate: no jump of more than obj_max_inc orders of magnitude
+    const double basval = fabs(pk) > 10.0 ? log10(fabs(pk)) : 1.0;
+    if (log10(ph - pk) > LS_OBJ_MAX_INC + basval) armijo = suff = false;
+  }
+  if (h_type) *h_type = !(ftype && armijo);
+  return fin && th <= theta_max && in_filter && (ftype ? armijo : suff);
+}
+
+// The rest of the regular backtracking line search of every instance still searching after its
+// first trial (and that trial's second-order corrections), in one launch: trials at alpha, alpha / 2,
+// ... until one is acceptable, alpha falls to alpha_min, or max_trials more trials were made
+// (batch_ipm.py regular_step, trials ls = 1 .. max_ls - 1).  Device pointers, rows of the batch.
+struct LsBacktrackArgs {
+  int64_t batch;
+  int32_t n, m, nf, nw, nfilt, max_trials;
+  const uint8_t* act;         // the instance iterates this iteration (active, not in restoration)
+  const uint8_t* tiny;        // tiny step this iteration (no line search)
+  const uint8_t* soft_now;    // in the soft restoration phase this iteration
+  const int32_t* soft_cnt;
+  uint8_t* searching;         // in/out
+  double* alpha;              // in/out: the next trial's step
+  const double* a_min;
+  const double* w;            // [batch, nw] the iterate
+  const double* dw;           // [batch, nw] the Newton step
+  const double* Xbase;        // [batch, n] fixed variables
+  const int32_t* freepos;     // [n] position in w of each variable, -1 fixed
+  const int32_t* row_slack;   // [m] slack of each inequality row, -1 equality
+  const double* gl;
+  const uint8_t* hasL;
+  const uint8_t* hasU;
+  const double* wl0;
+  const double* wu0;
+  const double* mu;
+  const double* theta_k;
+  const double* phi_k;
+  const double* gd;
+  const uint8_t* switch_ok;
+  const double* theta_max;
+  const double* filt_t;       // [batch, nfilt] the filter (after this iteration's barrier update)
+  const double* filt_p;
+  const double* mass;         // [batch] or NULL
+  const uint8_t* env_tag;     // [batch] (mixed batches) or NULL
+  double* st_f;               // the accepted trial: f, g, w, alpha, filter-augmenting
+  double* st_g;
+  double* st_w;
+  double* st_alpha;
+  uint8_t* st_aug;
+  uint8_t* any;               // any[0] |= still searching (trials exhausted), any[1] |= soft candidate
+};
+
+}  // namespace cpl

@@ -14,6 +14,7 @@
 #include <string>
 
 #include "cpl_status.hpp"
+#include "cpl_accept.hpp"
 #include "cpl_wave.hpp"
 
 namespace cpl {
@@ -76,28 +77,10 @@ __global__ __launch_bounds__(256) void cpl_ipm_judge_take_kernel(
   th = ipm_wave_sum(th);
   lg = ipm_wave_sum(lg);
   const double ph = f_t[b] - mu[b] * lg;
-  // filter entries are stored with their margins ((1 - gamma_theta) theta, phi - gamma_phi theta):
-  // acceptable when, for every entry, theta or phi is not larger (IPOPT's Filter::Acceptable)
-  bool rejected = false;
-  for (int k = lane; k < nfilt; k += 64) {
-    const double ft = filt_t[b * nfilt + k], fp = filt_p[b * nfilt + k];
-    rejected |= !((th <= ft) || (ph <= fp));
-  }
-  const bool in_filter = __ballot(rejected) == 0;
-  const double al = alpha[b], tk = theta_k[b], pk = phi_k[b], g = gd[b];
-  const bool fin = isfinite(ph) && isfinite(th);
-  const bool ftype = switch_ok[b] && (al * pow(fmax(-g, 0.0), 2.3) > pow(tk, 1.1));
-  // IPOPT's Compare_le(lhs, rhs, base): lhs - rhs <= 10 eps |base| (round-off of the reference values)
-  const double ro_p = 10.0 * DBL_EPSILON * fabs(pk), ro_t = 10.0 * DBL_EPSILON * fabs(tk);
-  bool armijo = (ph - pk) - 1e-8 * al * g <= ro_p;
-  bool suff = (th - (1.0 - 1e-5) * tk <= ro_t) || ((ph - pk) - (-1e-8 * tk) <= ro_p);
-  // obj_max_inc = 5: a barrier objective more than 5 orders of magnitude above the current one is
-  // rejected (IPOPT FilterLSAcceptor::IsAcceptableToCurrentIterate)
-  if (ph > pk) {
-    const double basval = fabs(pk) > 10.0 ? log10(fabs(pk)) : 1.0;
-    if (log10(ph - pk) > 5.0 + basval) armijo = suff = false;
-  }
-  const bool ok = fin && th <= theta_max[b] && in_filter && (ftype ? armijo : suff);
+  const double al = alpha[b];
+  bool aug = false;
+  const bool ok = ls_acceptable_wave(th, ph, theta_k[b], phi_k[b], gd[b], al, switch_ok[b] != 0, theta_max[b],
+                                     filt_t + b * nfilt, filt_p + b * nfilt, nfilt, &aug);
   const bool take = ok && searching[b] && (extra_mask == nullptr || extra_mask[b]);
   if (take) {
     for (int r = lane; r < m; r += 64) st_g[b * m + r] = gb[r];
@@ -109,7 +92,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_judge_take_kernel(
     if (take) {
       st_f[b] = f_t[b];
       st_alpha[b] = al;
-      st_aug[b] = !(ftype && armijo) ? 1 : 0;
+      st_aug[b] = aug ? 1 : 0;
       searching[b] = 0;
     }
   }

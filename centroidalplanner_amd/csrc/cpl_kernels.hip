@@ -32,7 +32,9 @@
 #include <tuple>
 #include <vector>
 
+#include "cpl_accept.hpp"
 #include "cpl_layout.hpp"
+#include "cpl_wave.hpp"
 #include "cpl_status.hpp"
 
 namespace cpl {
@@ -2080,6 +2082,141 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "cpl_eval_kernel launch");
+  return CPL_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// The solve engine's backtracking line search after the first trial (cpl_accept.hpp
+// LsBacktrackArgs): one wave per instance, the instances not searching leave at once.  A trial point
+// x_t = unpack(w + alpha dw) is evaluated (f and g) by the eval work items of the tile kernel on this
+// one instance (contacts, statics values, cost; Superquadric axis ladders, then rows) — the same
+// arithmetic as the batched eval launch — and judged by ls_acceptable_wave exactly as
+// cpl_ipm_judge_take judges the first trial.  The whole search runs in the kernel: the engine's
+// iteration no longer waits for the host between trials (one trial per graph launch and a flag read
+// back per trial cost ~55 us each; the lock-step batch makes as many trials as its slowest instance).
+template <int ENVK>
+__global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, const LsBacktrackArgs A) {
+  extern __shared__ __align__(16) double smem[];
+  __shared__ double s_f;
+  const int64_t b = blockIdx.x;
+  if (b >= A.batch) return;
+  const int lane = threadIdx.x;
+  const bool act = A.act[b] != 0;
+  bool searching = act && A.searching[b] != 0;
+  double al = A.alpha[b];
+  double st_alpha = A.st_alpha[b];
+  if (searching && A.max_trials > 0) {
+    const int n = A.n, m = A.m, nf = A.nf, nw = A.nw, N = K.N;
+    double* X = smem;
+    double* G = X + n;
+    double* wt = G + m;
+    double* L = wt + nw;  // [N][SQ_L] Superquadric scratch
+    load_ctab(K);
+    __syncthreads();
+    const double* wb = A.w + b * nw;
+    const double* db = A.dw + b * nw;
+    const double* Xb = A.Xbase + b * n;
+    const double m_i = A.mass ? A.mass[b] : K.mass_default;
+    const bool sq = ENVK == CPL_ENV_SUPERQUADRIC ||
+                    (ENVK == CPL_ENV_MIXED && A.env_tag[b] == CPL_ENV_SUPERQUADRIC);
+    const double a_min = A.a_min[b], mub = A.mu[b], tk = A.theta_k[b], pk = A.phi_k[b], g = A.gd[b];
+    const bool sw = A.switch_ok[b] != 0;
+    const double thmax = A.theta_max[b];
+    const double* ft = A.filt_t + b * A.nfilt;
+    const double* fp = A.filt_p + b * A.nfilt;
+    for (int trial = 0; trial < A.max_trials && searching; ++trial) {
+      // the trial point (cpl_ipm_trial_point's arithmetic)
+      for (int k = lane; k < nw; k += 64) wt[k] = wb[k] + al * db[k];
+      for (int j = lane; j < n; j += 64) {
+        const int k = A.freepos[j];
+        X[j] = k >= 0 ? wb[k] + al * db[k] : Xb[j];
+      }
+      __syncthreads();
+      // f and g of the trial point: the eval work items of one instance
+      if (ENVK != CPL_ENV_NONE && ENVK != CPL_ENV_GROUND && sq) {
+        for (int it = lane; it < 3 * N + 2; it += 64) {
+          if (it < 3 * N) sq_axis_item(K, X, it / 3, it % 3, L + (it / 3) * SQ_L, G);
+          else if (it == 3 * N) statics_values_item(K, X, m_i, G, G);
+          else cost_item(K, X, &s_f, nullptr);
+        }
+        __syncthreads();
+        for (int it = lane; it < 3 * N; it += 64) sq_row_item(K, X, it / 3, it % 3, L + (it / 3) * SQ_L, G, G);
+      } else {
+        for (int it = lane; it < N + 2; it += 64) {
+          if (it < N)
+            contact_item<ENVK == CPL_ENV_NONE ? CPL_ENV_NONE : CPL_ENV_GROUND>(K, X, CPL_ENV_GROUND, it, G, G);
+          else if (it == N) statics_values_item(K, X, m_i, G, G);
+          else cost_item(K, X, &s_f, nullptr);
+        }
+      }
+      __syncthreads();
+      // theta, the barrier objective, the acceptance test (cpl_ipm_judge_take's arithmetic)
+      double th = 0.0;
+      for (int r = lane; r < m; r += 64) {
+        const int s = A.row_slack[r];
+        th += fabs(s < 0 ? G[r] - A.gl[r] : G[r] - wt[nf + s]);
+      }
+      double lg = 0.0;
+      for (int k = lane; k < nw; k += 64) {
+        if (A.hasL[k]) lg += log(wt[k] - A.wl0[k]);
+        if (A.hasU[k]) lg += log(A.wu0[k] - wt[k]);
+      }
+      th = wave_sum(th);
+      lg = wave_sum(lg);
+      const double fv = s_f;
+      const double ph = fv - mub * lg;
+      bool aug = false;
+      const bool ok = ls_acceptable_wave(th, ph, tk, pk, g, al, sw, thmax, ft, fp, A.nfilt, &aug);
+      if (ok) {  // take it
+        for (int r = lane; r < m; r += 64) A.st_g[b * m + r] = G[r];
+        for (int k = lane; k < nw; k += 64) A.st_w[b * nw + k] = wt[k];
+        if (lane == 0) {
+          A.st_f[b] = fv;
+          A.st_alpha[b] = al;
+          A.st_aug[b] = aug ? 1 : 0;
+        }
+        st_alpha = al;
+        searching = false;
+      } else {  // IPOPT: the next trial only above alpha_min
+        al = 0.5 * al;
+        searching = al > a_min;
+      }
+      __syncthreads();  // the LDS images are rewritten by the next trial
+    }
+  }
+  if (lane == 0) {
+    if (act) {
+      A.searching[b] = searching ? 1 : 0;
+      A.alpha[b] = al;
+    }
+    if (searching) A.any[0] = 1;
+    // a soft restoration candidate: no accepted trial (or in the soft phase, within its budget)
+    const bool sn = A.soft_now[b] != 0;
+    if (act && !A.tiny[b] && ((sn && A.soft_cnt[b] <= LS_MAX_SOFT_RESTO) || (!sn && !(st_alpha > 0.0))))
+      A.any[1] = 1;
+  }
+}
+
+int32_t ls_backtrack(const cpl_problem_desc* d, const LsBacktrackArgs& a, hipStream_t stream) {
+  if (a.batch <= 0) return CPL_OK;
+  if (a.batch > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "ls_backtrack: batch too large");
+  KParams K;
+  fill_params(d, K, a.w);
+  if (K.n != a.n || K.m != a.m) return fail(CPL_ERR_INVALID_ARGUMENT, "ls_backtrack: problem dimensions differ");
+  K.want_g = 1;
+  K.want_f = 1;
+  K.want_j = 0;
+  K.want_grad = 0;
+  K.fold = FOLD_NONE;
+  const bool sq = d->env_kind == CPL_ENV_SUPERQUADRIC || d->env_kind == CPL_ENV_MIXED;
+  if (d->env_kind == CPL_ENV_MIXED && !a.env_tag) return fail(CPL_ERR_INVALID_ARGUMENT, "ls_backtrack: mixed needs tags");
+  const size_t lds = sizeof(double) * ((size_t)a.n + a.m + a.nw + (sq ? (size_t)K.N * SQ_L : 0) + 2);
+  using KernT = void (*)(const KParams, const LsBacktrackArgs);
+  static const KernT table[4] = {cpl_ls_backtrack_kernel<CPL_ENV_NONE>, cpl_ls_backtrack_kernel<CPL_ENV_GROUND>,
+                                 cpl_ls_backtrack_kernel<CPL_ENV_SUPERQUADRIC>, cpl_ls_backtrack_kernel<CPL_ENV_MIXED>};
+  hipLaunchKernelGGL(table[K.env_kind], dim3((unsigned)a.batch), dim3(64), lds, stream, K, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_fail(e, "cpl_ls_backtrack_kernel launch");
   return CPL_OK;
 }
 

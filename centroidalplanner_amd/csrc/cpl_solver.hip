@@ -25,6 +25,7 @@
 #include <utility>
 #include <vector>
 
+#include "cpl_accept.hpp"
 #include "cpl_layout.hpp"
 #include "cpl_status.hpp"
 
@@ -36,6 +37,8 @@ int32_t ipm_newton_setup_lm(int64_t batch, int32_t nw, int32_t m, int32_t nf, co
                             const uint8_t* d_hasU, const double* d_wl0, const double* d_wu0, const double* d_Hc,
                             int32_t lm_pairs, double* d_M, double* d_r1, double* d_r2, double* d_gphi,
                             double* d_mr_diag, double* d_theta, double* d_phi, const uint8_t* d_active, void* stream);
+// cpl_kernels.hip: the backtracking line search after the first trial, one wave per instance
+int32_t ls_backtrack(const cpl_problem_desc* d, const LsBacktrackArgs& a, hipStream_t stream);
 // cpl_ipm.hip: the optimality test + monotone barrier update with IPOPT's per-iteration rounds
 double ipm_mu_min(double tol);
 int32_t ipm_optimality_ex(int64_t batch, int32_t nw, int32_t m, int32_t fmax, int32_t nbounds, double tol,
@@ -228,11 +231,12 @@ __global__ void k_unpack(int64_t total, int n, int nw, const int32_t* __restrict
 }
 
 // ---- IPOPT constants of the line search / restoration phase (batch_ipm.py restates them) ------
-constexpr double GAMMA_TH = 1e-5, GAMMA_PHI = 1e-8, DELTA_SW = 1.0, S_TH = 1.1, S_PHI = 2.3, ETA_PHI = 1e-8;
-constexpr double ALPHA_MIN_FRAC = 0.05, KAPPA_SOC = 0.99, OBJ_MAX_INC = 5.0, KAPPA_SIGMA = 1e10;
+// (the acceptance test itself: cpl_accept.hpp)
+constexpr double GAMMA_TH = LS_GAMMA_TH, GAMMA_PHI = LS_GAMMA_PHI, DELTA_SW = LS_DELTA, S_TH = LS_S_TH, S_PHI = LS_S_PHI;
+constexpr double ALPHA_MIN_FRAC = 0.05, KAPPA_SOC = 0.99, KAPPA_SIGMA = 1e10;
 constexpr double TINY_STEP_TOL = 10.0 * DBL_EPSILON, TINY_STEP_Y_TOL = 1e-2;
 constexpr double RHO_R = 1000.0, KAPPA_RESTO = 0.9, BOUND_MULT_RESET = 1000.0, SOFT_RESTO_FACTOR = 0.9999;
-constexpr int MAX_SOFT_RESTO = 10, MU_ROUNDS = 6;
+constexpr int MAX_SOFT_RESTO = LS_MAX_SOFT_RESTO, MU_ROUNDS = 6;
 
 __device__ __forceinline__ double wave_min_d(double v) {
   for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
@@ -253,22 +257,7 @@ __device__ __forceinline__ double alpha_min_of(double theta, double gd, double t
 __device__ __forceinline__ bool acceptable_wave(double th, double ph, double tk, double pk, double g, double al,
                                                 bool switch_ok, double theta_max, const double* ft, const double* fp,
                                                 bool* h_type) {
-  const int lane = threadIdx.x & 63;
-  bool rejected = false;
-  for (int k = lane; k < FMAX; k += 64) rejected |= !((th <= ft[k]) || (ph <= fp[k]));
-  const bool in_filter = __ballot(rejected) == 0;
-  const bool fin = isfinite(ph) && isfinite(th);
-  const bool ftype = switch_ok && (al * pow(fmax(-g, 0.0), S_PHI) > DELTA_SW * pow(tk, S_TH));
-  // IPOPT's Compare_le(lhs, rhs, base): lhs - rhs <= 10 eps |base| (round-off of the reference values)
-  const double ro_p = 10.0 * DBL_EPSILON * fabs(pk), ro_t = 10.0 * DBL_EPSILON * fabs(tk);
-  bool armijo = (ph - pk) - ETA_PHI * al * g <= ro_p;
-  bool suff = (th - (1.0 - GAMMA_TH) * tk <= ro_t) || ((ph - pk) - (-GAMMA_PHI * tk) <= ro_p);
-  if (ph > pk) {
-    const double basval = fabs(pk) > 10.0 ? log10(fabs(pk)) : 1.0;
-    if (log10(ph - pk) > OBJ_MAX_INC + basval) armijo = suff = false;
-  }
-  if (h_type) *h_type = !(ftype && armijo);
-  return fin && th <= theta_max && in_filter && (ftype ? armijo : suff);
+  return ls_acceptable_wave(th, ph, tk, pk, g, al, switch_ok, theta_max, ft, fp, FMAX, h_type);
 }
 
 // After the Newton step (batch_ipm.py regular_step): IPOPT's tiny-step test (every primal component
@@ -1748,7 +1737,23 @@ int32_t step_phase(cpl_solver* S, int phase) {
                          S->tiny_flag, S->tiny_now, S->soft_now, S->a_min, S->searching, S->st_f, S->st_g, S->st_w,
                          S->st_alpha, S->st_aug, S->alpha, S->d_any);
       LAUNCHED("k_ls_setup");
-      return trial(true);
+      CK(trial(true));
+      if (o.max_ls > 1) {  // the remaining trials of every instance still searching, in one launch
+        HK(hipMemsetAsync(S->d_any, 0, 2, st), "hipMemsetAsync flags");
+        LsBacktrackArgs la;
+        la.batch = B; la.n = n; la.m = m; la.nf = nf; la.nw = nw; la.nfilt = FMAX; la.max_trials = o.max_ls - 1;
+        la.act = S->act; la.tiny = S->tiny_now; la.soft_now = S->soft_now; la.soft_cnt = S->soft_cnt;
+        la.searching = S->searching; la.alpha = S->alpha; la.a_min = S->a_min;
+        la.w = S->w; la.dw = S->dw; la.Xbase = S->Xbase; la.freepos = S->freepos; la.row_slack = S->row_slack;
+        la.gl = S->gl; la.hasL = S->hasL; la.hasU = S->hasU; la.wl0 = S->wl0; la.wu0 = S->wu0;
+        la.mu = S->mu_o; la.theta_k = S->theta_k; la.phi_k = S->phi_k; la.gd = S->gd; la.switch_ok = S->switch_ok;
+        la.theta_max = S->theta_max; la.filt_t = S->ft; la.filt_p = S->fp;
+        la.mass = S->mass; la.env_tag = S->tag;
+        la.st_f = S->st_f; la.st_g = S->st_g; la.st_w = S->st_w; la.st_alpha = S->st_alpha; la.st_aug = S->st_aug;
+        la.any = S->d_any;
+        CK(ls_backtrack(&S->desc, la, st));
+      }
+      return CPL_OK;
     }
     case P_TRIAL:
       return trial(false);
@@ -2329,15 +2334,9 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
   const int64_t min_rows = 256;
   int32_t resto_rows = 0;  // instances in the restoration phase after the previous iteration
   while (it < max_iter) {
-    CK(run_phase(S, P_NEWTON));
+    CK(run_phase(S, P_NEWTON));  // the Newton step and the whole regular line search
     evals += ev_newton;
     CK(read_flags(S));
-    // further backtracking trials while an instance is still searching (at most max_ls in all)
-    for (int ls = 1; S->h_flag[0] && ls < nls; ++ls) {
-      CK(run_phase(S, P_TRIAL));
-      ++evals;
-      CK(read_flags(S));
-    }
     if (S->h_flag[1] || S->h_flag[0]) {  // an instance found no acceptable trial: the soft restoration step
       CK(run_phase(S, P_SOFT));
       ++evals;
