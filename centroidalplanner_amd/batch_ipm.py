@@ -28,26 +28,29 @@ uses, batched over instances, with every per-instance quantity a row of a device
     iterative refinement.  Host tensors (the solver's logic under test on the CPU) take the same
     step from torch's dense factorisations (projector form of the null-space method);
   * fraction-to-the-boundary rule (tau = max(0.99, 1 - mu)), monotone Fiacco-McCormick barrier
-    update (kappa_mu = 0.2, theta_mu = 1.5, kappa_eps = 10) with a filter reset, IPOPT's filter
-    line search (switching condition, Armijo on the barrier objective for f-type steps, filter
-    augmentation after h-type steps) with second-order corrections on the first trial,
-    kappa_Sigma = 1e10 safeguard on the bound multipliers; no restoration phase: an instance whose
-    line search finds no acceptable point takes one feasibility (min-norm Gauss-Newton) step when
-    that cuts its violation, else the last trial, and restarts its filter;
+    update (kappa_mu = 0.2, theta_mu = 1.5, kappa_eps = 10, up to 6 decreases per iteration, floor
+    min(tol, 1e-4) / 11) with a filter reset, IPOPT's filter line search (switching condition, Armijo
+    on the barrier objective for f-type steps, filter augmentation after h-type steps, Compare_le
+    round-off tolerance, obj_max_inc) backtracking while alpha > alpha_min with up to max_soc
+    second-order corrections on the first trial, tiny steps, the soft restoration step, and IPOPT's
+    restoration phase (MinC_1Nrm: min rho |p + n|_1 + eta/2 |D_R (x - x_R)|^2 s.t. c(w) - p + n = 0
+    with its own barrier parameter, filter and line search) where the search fails — unless the
+    point is already acceptable, where the solve stops (STOP_AT_ACCEPTABLE_POINT);
+    kappa_Sigma = 1e10 safeguard on the bound multipliers;
   * termination on IPOPT's scaled optimality error (s_max = 100) <= tol, or <= acceptable_tol
     (1e-6) for 15 consecutive iterations.
 
 Every evaluation — the iterate, each line-search trial point, the finite-difference points — is ONE
-batched call of the evaluator for all instances.  Instances that converged stay in the batch
-(frozen), so every launch keeps its shape; one iteration has no host synchronisation at all (fixed
-trip counts, masked updates).
+batched call of the evaluator for all instances (the device engine runs the trials after the first
+inside one kernel, per instance).  Instances that converged stay in the batch (frozen), so every
+launch keeps its shape.
 
 Two implementations of the same iteration:
   * device tensors -> the native engine (csrc/cpl_solver.hip, C-ABI cpl_solver_*, NativeSolver
     below): the product callbacks (cpl_eval_batch with values-only Jacobian records), the Newton
     step in cpl_kkt_solve, the per-instance work in the cpl_ipm_* kernels and the glue in the
-    engine's own kernels; the iteration captured once as a HIP graph and replayed, the host reading
-    an "any active" flag one iteration behind.  No framework ops on the path;
+    engine's own kernels; the phases of the iteration captured once as HIP graphs and replayed, the
+    host reading a few flag bytes per iteration.  No framework ops on the path;
   * host tensors -> this module's torch restatement over any evaluator's callbacks (the tests drive
     it with the oracle's): the checker of the device path — the same algorithm, step for step.
 """
