@@ -84,6 +84,18 @@ struct LsBacktrackArgs {
   double* st_alpha;
   uint8_t* st_aug;
   uint8_t* any;               // any[0] |= still searching (trials exhausted), any[1] |= soft candidate
+  // restoration-phase search (resto != 0; batch_ipm.py resto_step): the trial also moves p, n along
+  // dp, dn; theta = sum |c(w_t) - p_t + n_t|, phi = rho sum(p_t + n_t) + eta/2 |D_R (x_t - x_R)|^2 -
+  // mu_R (sum log slacks + sum log p_t n_t); the flag is any[2]; no soft restoration
+  int32_t resto;
+  double rho;
+  const double* pR;
+  const double* nR;
+  const double* dp;
+  const double* dn;
+  const double* wR;
+  double* st_p;
+  double* st_n;
 };
 
 }  // namespace cpl

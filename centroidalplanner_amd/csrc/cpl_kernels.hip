@@ -2094,7 +2094,7 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
 // cpl_ipm_judge_take judges the first trial.  The whole search runs in the kernel: the engine's
 // iteration no longer waits for the host between trials (one trial per graph launch and a flag read
 // back per trial cost ~55 us each; the lock-step batch makes as many trials as its slowest instance).
-template <int ENVK>
+template <int ENVK, bool RESTO>
 __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, const LsBacktrackArgs A) {
   extern __shared__ __align__(16) double smem[];
   __shared__ double s_f;
@@ -2161,15 +2161,42 @@ __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, c
         if (A.hasL[k]) lg += log(wt[k] - A.wl0[k]);
         if (A.hasU[k]) lg += log(A.wu0[k] - wt[k]);
       }
+      double pn = 0.0, lpn = 0.0, prox = 0.0;
+      if (RESTO) {  // (k_resto_judge's terms; th above is replaced by the restoration problem's)
+        th = 0.0;
+        for (int r = lane; r < m; r += 64) {
+          const int s = A.row_slack[r];
+          const double pt = A.pR[b * m + r] + al * A.dp[b * m + r], nt = A.nR[b * m + r] + al * A.dn[b * m + r];
+          th += fabs((s < 0 ? G[r] - A.gl[r] : G[r] - wt[nf + s]) - pt + nt);
+          pn += pt + nt;
+          lpn += log(pt) + log(nt);
+        }
+        for (int k = lane; k < nf; k += 64) {
+          const double dr = 1.0 / fmax(fabs(A.wR[b * nw + k]), 1.0);
+          const double dx = wt[k] - A.wR[b * nw + k];
+          prox += (dr * dr) * (dx * dx);
+        }
+      }
       th = wave_sum(th);
       lg = wave_sum(lg);
       const double fv = s_f;
-      const double ph = fv - mub * lg;
+      double ph = fv - mub * lg;
+      if (RESTO) {
+        pn = wave_sum(pn);
+        lpn = wave_sum(lpn);
+        prox = wave_sum(prox);
+        ph = A.rho * pn + 0.5 * sqrt(mub) * prox - mub * lg - mub * lpn;
+      }
       bool aug = false;
       const bool ok = ls_acceptable_wave(th, ph, tk, pk, g, al, sw, thmax, ft, fp, A.nfilt, &aug);
       if (ok) {  // take it
         for (int r = lane; r < m; r += 64) A.st_g[b * m + r] = G[r];
         for (int k = lane; k < nw; k += 64) A.st_w[b * nw + k] = wt[k];
+        if (RESTO)
+          for (int r = lane; r < m; r += 64) {
+            A.st_p[b * m + r] = A.pR[b * m + r] + al * A.dp[b * m + r];
+            A.st_n[b * m + r] = A.nR[b * m + r] + al * A.dn[b * m + r];
+          }
         if (lane == 0) {
           A.st_f[b] = fv;
           A.st_alpha[b] = al;
@@ -2189,11 +2216,15 @@ __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, c
       A.searching[b] = searching ? 1 : 0;
       A.alpha[b] = al;
     }
-    if (searching) A.any[0] = 1;
-    // a soft restoration candidate: no accepted trial (or in the soft phase, within its budget)
-    const bool sn = A.soft_now[b] != 0;
-    if (act && !A.tiny[b] && ((sn && A.soft_cnt[b] <= LS_MAX_SOFT_RESTO) || (!sn && !(st_alpha > 0.0))))
-      A.any[1] = 1;
+    if (RESTO) {
+      if (searching) A.any[2] = 1;
+    } else {
+      if (searching) A.any[0] = 1;
+      // a soft restoration candidate: no accepted trial (or in the soft phase, within its budget)
+      const bool sn = A.soft_now[b] != 0;
+      if (act && !A.tiny[b] && ((sn && A.soft_cnt[b] <= LS_MAX_SOFT_RESTO) || (!sn && !(st_alpha > 0.0))))
+        A.any[1] = 1;
+    }
   }
 }
 
@@ -2212,9 +2243,14 @@ int32_t ls_backtrack(const cpl_problem_desc* d, const LsBacktrackArgs& a, hipStr
   if (d->env_kind == CPL_ENV_MIXED && !a.env_tag) return fail(CPL_ERR_INVALID_ARGUMENT, "ls_backtrack: mixed needs tags");
   const size_t lds = sizeof(double) * ((size_t)a.n + a.m + a.nw + (sq ? (size_t)K.N * SQ_L : 0) + 2);
   using KernT = void (*)(const KParams, const LsBacktrackArgs);
-  static const KernT table[4] = {cpl_ls_backtrack_kernel<CPL_ENV_NONE>, cpl_ls_backtrack_kernel<CPL_ENV_GROUND>,
-                                 cpl_ls_backtrack_kernel<CPL_ENV_SUPERQUADRIC>, cpl_ls_backtrack_kernel<CPL_ENV_MIXED>};
-  hipLaunchKernelGGL(table[K.env_kind], dim3((unsigned)a.batch), dim3(64), lds, stream, K, a);
+  static const KernT table[2][4] = {
+      {cpl_ls_backtrack_kernel<CPL_ENV_NONE, false>, cpl_ls_backtrack_kernel<CPL_ENV_GROUND, false>,
+       cpl_ls_backtrack_kernel<CPL_ENV_SUPERQUADRIC, false>, cpl_ls_backtrack_kernel<CPL_ENV_MIXED, false>},
+      {cpl_ls_backtrack_kernel<CPL_ENV_NONE, true>, cpl_ls_backtrack_kernel<CPL_ENV_GROUND, true>,
+       cpl_ls_backtrack_kernel<CPL_ENV_SUPERQUADRIC, true>, cpl_ls_backtrack_kernel<CPL_ENV_MIXED, true>}};
+  if (a.resto && (!a.pR || !a.nR || !a.dp || !a.dn || !a.wR || !a.st_p || !a.st_n))
+    return fail(CPL_ERR_INVALID_ARGUMENT, "ls_backtrack: restoration search without its buffers");
+  hipLaunchKernelGGL(table[a.resto ? 1 : 0][K.env_kind], dim3((unsigned)a.batch), dim3(64), lds, stream, K, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "cpl_ls_backtrack_kernel launch");
   return CPL_OK;

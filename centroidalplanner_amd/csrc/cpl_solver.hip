@@ -1590,17 +1590,19 @@ int32_t eval_full(cpl_solver* S, const double* X, double* fo, double* grado, dou
 }
 
 // The phases of one lock-step iteration (each graph-capturable, no host synchronisation inside):
-//   P_NEWTON  the convergence test, barrier update, Newton step, tiny-step test, the first trial
-//             with its second-order corrections (flags: any still searching / any soft candidate)
-//   P_TRIAL   one more backtracking trial (launched while an instance is still searching)
-//   P_SOFT    IPOPT's soft restoration step (launched when an instance found no acceptable trial)
-//   P_ACCEPT  the accepted points' evaluation, L-BFGS, the state update, the restoration phase's
-//             entry for failed searches, the active / restoration counts
-//   P_RNEWTON the restoration phase's Newton step and first trial (launched when instances are in it)
-//   P_RTRIAL  one more restoration trial
-//   P_RACCEPT the restoration iteration's acceptance and the return test
-// Per iteration: P_NEWTON, P_TRIAL*, [P_SOFT], [P_RNEWTON, P_RTRIAL*, P_RACCEPT], P_ACCEPT.
-enum Phase { P_NEWTON = 1, P_TRIAL, P_SOFT, P_ACCEPT, P_RNEWTON, P_RTRIAL, P_RACCEPT, P_COUNT };
+//   P_NEWTON    the convergence test, barrier update, Newton step, tiny-step test, the first trial
+//               with its second-order corrections, then the rest of every instance's backtracking
+//               search in one kernel (cpl_kernels.hip ls_backtrack); flags: any instance with no
+//               accepted trial (a soft-restoration candidate) / still searching
+//   P_SOFT      IPOPT's soft restoration step (launched when a flag was raised)
+//   P_RNEWTON   one restoration-phase iteration of the instances inside it: Newton step, first trial,
+//               the rest of the search in one kernel, the acceptance and the return test (P_RACCEPT)
+//   P_ACCEPT    the accepted points' evaluation, L-BFGS, the state update, the restoration phase's
+//               entry for failed searches, the active / restoration counts; P_ACCEPT_NR the same
+//               without the entry (no flag raised: no instance can have failed)
+// Per iteration: P_NEWTON, [P_SOFT], [P_RNEWTON], P_ACCEPT | P_ACCEPT_NR; the host reads the flag
+// bytes after P_NEWTON and the two counts after the accept.
+enum Phase { P_NEWTON = 1, P_SOFT, P_ACCEPT, P_RNEWTON, P_RACCEPT, P_ACCEPT_NR };
 
 int32_t hessian_into(cpl_solver* S, const cpl_problem_desc* d, const uint8_t* mask, const double** Hblk, int* h_sym) {
   const int64_t B = S->Bcur;
@@ -1654,13 +1656,14 @@ int32_t step_phase(cpl_solver* S, int phase) {
     LAUNCHED("k_halve2");
     return CPL_OK;
   };
-  // one regular backtracking trial: the point, f and g there, IPOPT's acceptance test and the take
-  auto trial = [&](bool first) -> int32_t {
+  // the first regular trial: the point, f and g there, IPOPT's acceptance test and the take, its
+  // second-order corrections, the halving
+  auto first_trial = [&]() -> int32_t {
     CK(cpl_ipm_trial_point(B, n, nf, nw, S->free64, S->fixed64, S->Xbase, S->w, S->dw, S->alpha, S->searching,
                            S->st_w, S->wt, S->Xt, st));
     CK(eval_fg(S, S->Xt, S->f_t, S->g_t));
     CK(judge(S->wt, S->f_t, S->g_t, S->alpha, nullptr, S->th, S->ok));
-    if (first && o.max_soc > 0) {  // second-order corrections on the first trial (IPOPT's max_soc)
+    if (o.max_soc > 0) {  // second-order corrections on the first trial (IPOPT's max_soc)
       const double *cg = S->g_t, *cw = S->wt;
       for (int q = 0; q < o.max_soc; ++q) {
         if (q == 0) {
@@ -1690,7 +1693,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
     }
     return halve(S->searching, S->alpha, S->a_min, 0, true);
   };
-  // one restoration trial: the point (w along dw; p, n in the judge), f and g, the test and the take
+  // the first restoration trial: the point (w along dw; p, n in the judge), f and g, the test and the take
   auto rtrial = [&]() -> int32_t {
     CK(cpl_ipm_trial_point(B, n, nf, nw, S->free64, S->fixed64, S->Xbase, S->w, S->dw, S->alphaR, S->searchingR,
                            S->st_w, S->wt, S->Xt, st));
@@ -1737,7 +1740,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
                          S->tiny_flag, S->tiny_now, S->soft_now, S->a_min, S->searching, S->st_f, S->st_g, S->st_w,
                          S->st_alpha, S->st_aug, S->alpha, S->d_any);
       LAUNCHED("k_ls_setup");
-      CK(trial(true));
+      CK(first_trial());
       if (o.max_ls > 1) {  // the remaining trials of every instance still searching, in one launch
         HK(hipMemsetAsync(S->d_any, 0, 2, st), "hipMemsetAsync flags");
         LsBacktrackArgs la;
@@ -1751,12 +1754,14 @@ int32_t step_phase(cpl_solver* S, int phase) {
         la.mass = S->mass; la.env_tag = S->tag;
         la.st_f = S->st_f; la.st_g = S->st_g; la.st_w = S->st_w; la.st_alpha = S->st_alpha; la.st_aug = S->st_aug;
         la.any = S->d_any;
+        la.resto = 0;
+        la.rho = 0.0;
+        la.pR = la.nR = la.dp = la.dn = la.wR = nullptr;
+        la.st_p = la.st_n = nullptr;
         CK(ls_backtrack(&S->desc, la, st));
       }
       return CPL_OK;
     }
-    case P_TRIAL:
-      return trial(false);
     case P_SOFT: {
       hipLaunchKernelGGL(k_soft_begin, dim3(blocks_for(B)), dim3(256), 0, st, B, n, nf, nw, S->act, S->tiny_now,
                          S->soft_now, S->soft_cnt, S->st_alpha, S->a_max, S->a_z, S->w, S->dw, S->freepos, S->Xbase,
@@ -1772,7 +1777,8 @@ int32_t step_phase(cpl_solver* S, int phase) {
       LAUNCHED("k_soft_judge");
       return CPL_OK;
     }
-    case P_ACCEPT: {
+    case P_ACCEPT:
+    case P_ACCEPT_NR: {
       hipLaunchKernelGGL(k_fail, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->act, S->st_alpha, S->err0,
                          o.acceptable_tol, S->failed, S->moved, S->in_soft, S->soft_cnt, S->status, S->active);
       LAUNCHED("k_fail");
@@ -1797,6 +1803,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
       hipLaunchKernelGGL(k_accept_rows, dim3(blocks_elems(B * (1 + n + m + S->nnz_rec))), dim3(256), 0, st, B, n, m,
                          S->nnz_rec, S->moved, S->f_n, S->grad_n, S->g_n, S->J_n, S->f, S->grad, S->g, S->J);
       LAUNCHED("k_accept_rows");
+      if (phase == P_ACCEPT_NR) goto count;  // no instance can have failed its search: no entry
       // the restoration phase starts where the line search failed
       hipLaunchKernelGGL(k_resto_enter, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nw, S->failed, S->c, S->w, S->zL,
                          S->zU, S->mu_o, S->theta_k, S->phi_k, S->hasL, S->hasU, S->filt_t, S->filt_p, S->fcount,
@@ -1808,6 +1815,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
                           S->Kqd, st));
       hipLaunchKernelGGL(k_resto_y0, dim3(blocks_for(B)), dim3(256), 0, st, B, m, S->failed, S->dy, S->y);
       LAUNCHED("k_resto_y0");
+    count:
       if (B > COUNT1_MAX) {
         hipLaunchKernelGGL(k_count_zero, dim3(1), dim3(64), 0, st, S->d_count);
         LAUNCHED("k_count_zero");
@@ -1847,10 +1855,28 @@ int32_t step_phase(cpl_solver* S, int phase) {
                          S->dzp, S->dzn, S->a_maxR, S->a_zR, S->gdR, S->switchR, S->a_minR, S->searchingR, S->st_f,
                          S->st_g, S->st_w, S->st_p, S->st_n, S->st_alpha, S->st_aug, S->alphaR, S->d_any);
       LAUNCHED("k_resto_post");
-      return rtrial();
+      CK(rtrial());
+      if (o.max_ls > 1) {  // the restoration search's remaining trials, in one launch
+        HK(hipMemsetAsync(S->d_any + 2, 0, 1, st), "hipMemsetAsync flag");
+        LsBacktrackArgs la;
+        la.batch = B; la.n = n; la.m = m; la.nf = nf; la.nw = nw; la.nfilt = FMAX; la.max_trials = o.max_ls - 1;
+        la.act = S->actR; la.tiny = S->tiny_now; la.soft_now = S->soft_now; la.soft_cnt = S->soft_cnt;
+        la.searching = S->searchingR; la.alpha = S->alphaR; la.a_min = S->a_minR;
+        la.w = S->w; la.dw = S->dw; la.Xbase = S->Xbase; la.freepos = S->freepos; la.row_slack = S->row_slack;
+        la.gl = S->gl; la.hasL = S->hasL; la.hasU = S->hasU; la.wl0 = S->wl0; la.wu0 = S->wu0;
+        la.mu = S->muR; la.theta_k = S->thetaR; la.phi_k = S->phiR; la.gd = S->gdR; la.switch_ok = S->switchR;
+        la.theta_max = S->thmaxR; la.filt_t = S->ftR; la.filt_p = S->fpR;
+        la.mass = S->mass; la.env_tag = S->tag;
+        la.st_f = S->st_f; la.st_g = S->st_g; la.st_w = S->st_w; la.st_alpha = S->st_alpha; la.st_aug = S->st_aug;
+        la.any = S->d_any;
+        la.resto = 1;
+        la.rho = RHO_R;
+        la.pR = S->pR; la.nR = S->nR; la.dp = S->dp; la.dn = S->dn; la.wR = S->wR;
+        la.st_p = S->st_p; la.st_n = S->st_n;
+        CK(ls_backtrack(&S->desc, la, st));
+      }
+      return step_phase(S, P_RACCEPT);
     }
-    case P_RTRIAL:
-      return rtrial();
     case P_RACCEPT: {
       hipLaunchKernelGGL(k_unpack, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, nw, S->freepos, S->Xbase,
                          S->st_w, nullptr, nullptr, S->Xn);
@@ -1885,7 +1911,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
 // replayed); without graphs the phase is launched directly
 int32_t run_phase(cpl_solver* S, int phase) {
   if (!S->opt.use_graph) return step_phase(S, phase);
-  const int64_t key = ((S->Bcur * 4 + (S->mass ? 2 : 0) + (S->tag ? 1 : 0)) * 8) + phase;
+  const int64_t key = ((S->Bcur * 4 + (S->mass ? 2 : 0) + (S->tag ? 1 : 0)) * 16) + phase;
   auto it = S->graphs.find(key);
   if (it == S->graphs.end()) {
     HK(hipStreamBeginCapture(S->stream, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
@@ -2326,7 +2352,6 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
     hipLaunchKernelGGL(k_lm_init, dim3(blocks_elems(B)), dim3(256), 0, st, B, nf, S->Hq);
     LAUNCHED("k_lm_init");
   }
-  const int nls = S->opt.max_ls > 0 ? S->opt.max_ls : 1;
   const int64_t ev_newton = (S->fd ? 1 : 0) + 1 + S->opt.max_soc;
   int it = 0;
   const int max_iter = S->opt.max_iter;
@@ -2341,19 +2366,12 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
       CK(run_phase(S, P_SOFT));
       ++evals;
     }
+    const bool may_fail = S->h_flag[1] || S->h_flag[0];
     if (resto_rows > 0) {  // one restoration-phase iteration of the instances inside it
       CK(run_phase(S, P_RNEWTON));
-      evals += (S->fd ? 1 : 0) + 1;
-      CK(read_flags(S));
-      for (int ls = 1; S->h_flag[2] && ls < nls; ++ls) {
-        CK(run_phase(S, P_RTRIAL));
-        ++evals;
-        CK(read_flags(S));
-      }
-      CK(run_phase(S, P_RACCEPT));
-      ++evals;
+      evals += (S->fd ? 1 : 0) + 3;
     }
-    CK(run_phase(S, P_ACCEPT));
+    CK(run_phase(S, may_fail ? P_ACCEPT : P_ACCEPT_NR));
     ++evals;
     ++it;
     HK(hipMemcpyAsync(S->h_count, S->d_count, 8, hipMemcpyDeviceToHost, st), "hipMemcpyAsync count");

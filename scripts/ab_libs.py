@@ -25,6 +25,7 @@ ap.add_argument("--batch", type=int, default=0)
 ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--libs", default="centroidalplanner_amd/libcpl_mi355x.so,build/libcpl_old.so")
+ap.add_argument("--tuning", default="", help="variant:lds_kb:wg:nt passed to every library's cpl_set_tuning")
 args = ap.parse_args()
 
 libs = {}
@@ -35,6 +36,10 @@ for tag in args.libs.split(","):
         fn = getattr(lib, name)
         res, sig = _abi.SIGNATURES[name]
         fn.restype, fn.argtypes = res, sig
+    if args.tuning:
+        v = [int(t) for t in args.tuning.split(":")]
+        lib.cpl_set_tuning.restype = ctypes.c_int32
+        _abi.check(lib.cpl_set_tuning(*[ctypes.c_int32(t) for t in (v + [0] * (5 - len(v)))]))
     libs[tag] = lib
 
 cfg = CONFIGS[args.config]
@@ -69,5 +74,5 @@ for k, lib in libs.items():
 bpi, m = algorithmic_bytes(cfg.n_contacts, cfg.env)
 for k, ts in times.items():
     med = statistics.median(ts)
-    print(json.dumps({"config": args.config, "batch": B, "lib": k, "median_ms": med, "min_ms": min(ts),
+    print(json.dumps({"config": args.config, "batch": B, "lib": k, "tuning": args.tuning, "median_ms": med, "min_ms": min(ts),
                       "GBps": bpi * B / (med * 1e-3) / 1e9}), flush=True)

@@ -17,7 +17,8 @@ IFOPT's defaults — the limited-memory Hessian, max_iter 3000).
 
 TestBasic's ground scenario (force weight 0) is degenerate: its optimum unloads two contacts, whose
 forces then sit at the apex of the cone |F_t| - mu F.n <= 0, where the constraint is not
-differentiable; neither Hessian mode converges to tol there.  That test pins the
+differentiable; neither Hessian mode converges to tol there ("Why TestBasic's ground
+scenario does not converge").  That test pins the
 documented outcome instead of success.
 """
 import numpy as np
