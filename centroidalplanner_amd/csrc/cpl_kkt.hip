@@ -1408,6 +1408,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 // (lower triangle, mirrored: bitwise symmetric) into the global workspace, each attempt factorised
 // by one wave in LDS (batch_ipm.py kkt_qd restates it).  Pivots at or below eps max|K_ii| count as
 // zero eigenvalues.
+// One factorisation attempt of the quasi-definite system's K + dW I on one wave: for the 4-contact
+// size the rows live in registers (wave_cholesky_reg: bitwise the LDS factor, no LDS round trips:
+// the restoration phase's factorisations took 150-350 us with the LDS version's read-modify-writes
+// over the trailing square); the factor goes to L for the triangular solves.
+template <int N>
+__device__ __forceinline__ bool qd_factor_reg(const double* __restrict__ K, double dW, double piv, double* L) {
+  const int lane = threadIdx.x & 63;
+  double a[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) a[k] = lane < N ? K[lane * N + k] + (lane == k ? dW : 0.0) : 0.0;
+  const bool ok = wave_cholesky_reg<N>(a, piv);
+  if (ok && lane < N) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) L[lane * N + k] = a[k];
+  }
+  return ok;
+}
+
 __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_qd_kernel(
     int64_t batch, int nw, int m, const double* __restrict__ W, const double* __restrict__ A,
     const double* __restrict__ Dinv, const double* __restrict__ r1, const double* __restrict__ r2,
@@ -1423,8 +1441,13 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_qd_kernel(
   __shared__ int s_ok;
   const int tid = threadIdx.x;
   const double* Wb = W + b * (int64_t)nw * nw;
-  const double* Ab = A + b * (int64_t)m * nw;
-  const double* Db = Dinv + b * m;
+  double* As = t + m;             // [m][nw]: A staged in LDS
+  double* Ds = As + m * nw;       // [m]: D^-1
+  for (int e = tid; e < m * nw; e += KKT_THREADS) As[e] = A[b * (int64_t)m * nw + e];
+  for (int r = tid; r < m; r += KKT_THREADS) Ds[r] = Dinv[b * m + r];
+  __syncthreads();
+  const double* Ab = As;
+  const double* Db = Ds;
   double* Kb = Kws + b * (int64_t)nw * nw;
   // K = W + A^T D^-1 A, lower triangle (i >= j) summed over the rows in order, mirrored
   double dmax = 0.0;
@@ -1448,14 +1471,21 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_qd_kernel(
   const double last = dwl[b];
   double dW = 0.0;
   for (int attempt = 0; attempt < 64; ++attempt) {
-    for (int e = tid; e < nw * nw; e += KKT_THREADS) {
-      const int i = e / nw, j = e - i * nw;
-      L[e] = Kb[e] + (i == j ? dW : 0.0);
-    }
-    __syncthreads();
-    if (tid < 64) {
-      const bool ok = wave_cholesky(L, nw, piv_tol);
-      if (tid == 0) s_ok = ok ? 1 : 0;
+    if (nw == 47) {  // (K's global copy was written by this workgroup before the barrier above)
+      if (tid < 64) {
+        const bool ok = qd_factor_reg<47>(Kb, dW, piv_tol, L);
+        if (tid == 0) s_ok = ok ? 1 : 0;
+      }
+    } else {
+      for (int e = tid; e < nw * nw; e += KKT_THREADS) {
+        const int i = e / nw, j = e - i * nw;
+        L[e] = Kb[e] + (i == j ? dW : 0.0);
+      }
+      __syncthreads();
+      if (tid < 64) {
+        const bool ok = wave_cholesky(L, nw, piv_tol);
+        if (tid == 0) s_ok = ok ? 1 : 0;
+      }
     }
     __syncthreads();
     if (s_ok) break;
@@ -1590,7 +1620,7 @@ int32_t cpl_kkt_qd_solve(int64_t batch, int32_t nw, int32_t m, const double* d_W
   if (!d_W || (m > 0 && (!d_A || !d_Dinv || !d_r2 || !d_dy)) || !d_r1 || !d_dw || !d_delta_w_last || !d_ws)
     return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_qd_solve: missing buffer");
   if (batch > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_qd_solve: batch too large");
-  const size_t lds = sizeof(double) * ((size_t)nw * nw + nw + (m > 0 ? m : 1));
+  const size_t lds = sizeof(double) * ((size_t)nw * nw + nw + 2 * (size_t)(m > 0 ? m : 1) + (size_t)m * nw);
   hipLaunchKernelGGL(cpl_kkt_qd_kernel, dim3((unsigned)batch), dim3(KKT_THREADS), lds, (hipStream_t)stream, batch,
                      (int)nw, (int)m, d_W, d_A, d_Dinv, d_r1, d_r2, d_active, d_delta_w_last, d_dw, d_dy, d_delta_w,
                      d_ws);
