@@ -1601,8 +1601,13 @@ int32_t eval_full(cpl_solver* S, const double* X, double* fo, double* grado, dou
 //               entry for failed searches, the active / restoration counts; P_ACCEPT_NR the same
 //               without the entry (no flag raised: no instance can have failed)
 // Per iteration: P_NEWTON, [P_SOFT], [P_RNEWTON], P_ACCEPT | P_ACCEPT_NR; the host reads the flag
-// bytes after P_NEWTON and the two counts after the accept.
-enum Phase { P_NEWTON = 1, P_SOFT, P_ACCEPT, P_RNEWTON, P_RACCEPT, P_ACCEPT_NR };
+// bytes after P_NEWTON and the two counts after the accept.  Small batches (at most FUSE_ROWS rows,
+// where every launch is latency and a host round trip costs as much as several kernels) run the
+// whole iteration as one graph instead, P_FUSED = P_NEWTON + P_SOFT + P_ACCEPT (P_FUSED_R with the
+// restoration iteration as well): the soft step's kernels and the restoration entry's run masked
+// whether or not an instance needs them, and the host reads only the counts.
+constexpr int64_t FUSE_ROWS = 256;  // (see the phase list above)
+enum Phase { P_NEWTON = 1, P_SOFT, P_ACCEPT, P_RNEWTON, P_RACCEPT, P_ACCEPT_NR, P_FUSED, P_FUSED_R };
 
 int32_t hessian_into(cpl_solver* S, const cpl_problem_desc* d, const uint8_t* mask, const double** Hblk, int* h_sym) {
   const int64_t B = S->Bcur;
@@ -1902,6 +1907,12 @@ int32_t step_phase(cpl_solver* S, int phase) {
       LAUNCHED("k_accept_rows (resto)");
       return CPL_OK;
     }
+    case P_FUSED:
+    case P_FUSED_R:
+      CK(step_phase(S, P_NEWTON));
+      CK(step_phase(S, P_SOFT));
+      if (phase == P_FUSED_R) CK(step_phase(S, P_RNEWTON));
+      return step_phase(S, P_ACCEPT);
     default:
       return fail(CPL_ERR_INVALID_ARGUMENT, "step_phase: bad phase");
   }
@@ -2359,20 +2370,25 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
   const int64_t min_rows = 256;
   int32_t resto_rows = 0;  // instances in the restoration phase after the previous iteration
   while (it < max_iter) {
-    CK(run_phase(S, P_NEWTON));  // the Newton step and the whole regular line search
-    evals += ev_newton;
-    CK(read_flags(S));
-    if (S->h_flag[1] || S->h_flag[0]) {  // an instance found no acceptable trial: the soft restoration step
-      CK(run_phase(S, P_SOFT));
+    if (S->Bcur <= FUSE_ROWS && S->opt.use_graph) {  // one graph, one host round trip
+      CK(run_phase(S, resto_rows > 0 ? P_FUSED_R : P_FUSED));
+      evals += ev_newton + 2 + (resto_rows > 0 ? (S->fd ? 1 : 0) + 3 : 0);
+    } else {
+      CK(run_phase(S, P_NEWTON));  // the Newton step and the whole regular line search
+      evals += ev_newton;
+      CK(read_flags(S));
+      if (S->h_flag[1] || S->h_flag[0]) {  // an instance found no acceptable trial: the soft restoration step
+        CK(run_phase(S, P_SOFT));
+        ++evals;
+      }
+      const bool may_fail = S->h_flag[1] || S->h_flag[0];
+      if (resto_rows > 0) {  // one restoration-phase iteration of the instances inside it
+        CK(run_phase(S, P_RNEWTON));
+        evals += (S->fd ? 1 : 0) + 3;
+      }
+      CK(run_phase(S, may_fail ? P_ACCEPT : P_ACCEPT_NR));
       ++evals;
     }
-    const bool may_fail = S->h_flag[1] || S->h_flag[0];
-    if (resto_rows > 0) {  // one restoration-phase iteration of the instances inside it
-      CK(run_phase(S, P_RNEWTON));
-      evals += (S->fd ? 1 : 0) + 3;
-    }
-    CK(run_phase(S, may_fail ? P_ACCEPT : P_ACCEPT_NR));
-    ++evals;
     ++it;
     HK(hipMemcpyAsync(S->h_count, S->d_count, 8, hipMemcpyDeviceToHost, st), "hipMemcpyAsync count");
     HK(hipStreamSynchronize(st), "hipStreamSynchronize");
