@@ -94,6 +94,8 @@ struct KParams {
   // cstride = offset of the first contact block and length of one, in the (folded) record
   int32_t fold, jbase, cstride;
   int32_t soa;               // outputs entry-major ([m][B], [nnz][B], [n][B]) instead of instance-major
+  int32_t jdirect;           // tile kernel: the Jacobian items write their entries straight to the
+                             // output records instead of the LDS tile image (smaller tiles' LDS)
 };
 static_assert(sizeof(KParams) < 4096, "kernel parameters must fit the kernarg segment");
 
@@ -1154,7 +1156,8 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
   const int valid = (int)((batch - b0) < T ? (batch - b0) : T);
   double* X = smem;
   double* Gt = smem + K.offG;
-  double* Jt = smem + K.offJ;
+  // the Jacobian rows: the LDS tile image, or (jdirect) the output records themselves
+  double* Jt = K.jdirect ? jac_out + b0 * K.nnz : smem + K.offJ;
   double* Dt = smem + K.offD;
   double* L = smem + K.offL;                                    // [T][LR] (SQ / mixed)
   int* lists = reinterpret_cast<int*>(smem + K.offI);          // sq_list[64], gr_list[64], n_sq
@@ -1246,7 +1249,7 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
     if (K.want_grad) copy_out_soa<WG, NT>(grad_out + b0, batch, Dt, n, valid, tid);
   } else if (K.ablate != 2) {
     if (K.want_g) copy_out<WG, NT>(g_out + b0 * m, Gt, valid * m, tid);
-    if (K.want_j) copy_out<WG, NT>(jac_out + b0 * nnz, Jt, valid * nnz, tid);
+    if (K.want_j && !K.jdirect) copy_out<WG, NT>(jac_out + b0 * nnz, Jt, valid * nnz, tid);
     if (K.want_grad) copy_out<WG, NT>(grad_out + b0 * n, Dt, valid * n, tid);
   }
   if (K.want_norms) {
@@ -1820,8 +1823,9 @@ static size_t eval_lds_bytes(int n) { return sizeof(double) * (size_t)(TILE * n 
 // Tuning knobs (cpl_set_tuning): kernel variant and the LDS budget of one workgroup.
 // Variant 0 (auto, the default) takes the pipelined kernel for the HBM-bound environments (none,
 // Ground) and the tile-stationary kernel for the VALU-bound ones (Superquadric, mixed), where the
-// pipelined kernel's three compute waves per workgroup leave the FP64 pipes under-filled.
-enum { VAR_AUTO = 0, VAR_ROWSTAGE = 1, VAR_PIPE = 2, VAR_TILE = 3 };
+// pipelined kernel's three compute waves per workgroup leave the FP64 pipes under-filled; mixed
+// batches with the Jacobian written straight to the records (variant 4 forces that everywhere).
+enum { VAR_AUTO = 0, VAR_ROWSTAGE = 1, VAR_PIPE = 2, VAR_TILE = 3, VAR_TILE_JD = 4 };
 static int g_variant = VAR_AUTO;
 static size_t g_lds_budget = 0;    // 0 = per-kernel default (tile 32 KiB, pipelined 48 KiB)
 static int g_wg = 256;             // threads per tile workgroup (128 or 256)
@@ -1841,8 +1845,8 @@ static int32_t plan_tile(KParams& K, bool g, bool j, bool f, bool grad, int t_ma
   K.want_g = g; K.want_j = j; K.want_f = f; K.want_grad = grad;
   const bool sq = K.env_kind == CPL_ENV_SUPERQUADRIC || K.env_kind == CPL_ENV_MIXED;
   K.LR = K.N * SQ_L + 1;  // odd instance stride of the SQ scratch: conflict-free LDS banks
-  const size_t per = sizeof(double) * (size_t)(K.n + (g ? K.m : 0) + (j ? K.nnz : 0) + (grad ? K.n : 0) +
-                                               (sq ? K.LR : 0));
+  const size_t per = sizeof(double) * (size_t)(K.n + (g ? K.m : 0) + (j && !K.jdirect ? K.nnz : 0) +
+                                               (grad ? K.n : 0) + (sq ? K.LR : 0));
   const size_t fixed = sizeof(double) * 72 + sizeof(CTab);  // index lists + parameter table
   int T = 64, logT = 6;
   while (T > t_max) { T >>= 1; --logT; }
@@ -1856,7 +1860,7 @@ static int32_t plan_tile(KParams& K, bool g, bool j, bool f, bool grad, int t_ma
   K.S = K.N + 4 + ((f || grad) ? 1 : 0);
   K.offG = T * K.n;
   K.offJ = K.offG + (g ? T * K.m : 0);
-  K.offD = K.offJ + (j ? T * K.nnz : 0);
+  K.offD = K.offJ + (j && !K.jdirect ? T * K.nnz : 0);
   K.offL = K.offD + (grad ? T * K.n : 0);
   K.offI = K.offL + (sq ? T * K.LR : 0);
   K.offI = (K.offI + 1) & ~1;
@@ -2056,6 +2060,12 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
     // 4-instance tiles on 256 threads: 1 048 576 x 16 mixed 3.17 ms against 3.99 ms for the 2-instance
     // tiles on 128 threads of round 1 and 4.18 ms for 8-instance tiles
     // (profiles/r2_v7/sweep_tiles_mixed16_*.jsonl)
+    // mixed batches write the Jacobian straight to the output records (their ~10 KiB records leave
+    // 4 instances per 48 KiB tile otherwise; without the Jacobian image the tile holds 8): mixed16
+    // 4.23 -> 3.47 ms, interleaved A/B in one process (profiles/r3/abk_mixed16.jsonl); the
+    // Superquadric records are small enough that the staged copy-out wins there (0.32 vs 0.42 ms)
+    const bool jd = g_variant == VAR_TILE_JD || (g_variant == VAR_AUTO && K.env_kind == CPL_ENV_MIXED);
+    K.jdirect = (jd && d_jac && !K.soa) ? 1 : 0;
     st = plan_tile(K, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr);
     const int wg = g_wg;
     if (st) return st;
@@ -2323,7 +2333,7 @@ int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_t
                        int32_t ablate) {
   if (ablate < 0 || ablate > 2) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
   g_ablate = ablate;
-  if (kernel_variant < VAR_AUTO || kernel_variant > VAR_TILE) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown kernel variant");
+  if (kernel_variant < VAR_AUTO || kernel_variant > VAR_TILE_JD) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown kernel variant");
   if (tile_lds_kb != 0 && (tile_lds_kb < 8 || tile_lds_kb > 160))
     return fail(CPL_ERR_INVALID_ARGUMENT, "LDS budget out of [8, 160] KiB");
   if (wg_threads != 128 && wg_threads != 256) return fail(CPL_ERR_INVALID_ARGUMENT, "workgroup size must be 128 or 256");
