@@ -1841,16 +1841,20 @@ static bool use_pipe(const KParams& K) {
   return g_variant == VAR_AUTO && (K.env_kind == CPL_ENV_NONE || K.env_kind == CPL_ENV_GROUND);
 }
 
-static int32_t plan_tile(KParams& K, bool g, bool j, bool f, bool grad, int t_max = 64) {
+// size_without_j: the tile size is chosen as if the Jacobian were written straight to the records
+// (the layouts that cannot, SoA, then stage it in a larger LDS image) so that every layout of a batch
+// runs the same tiles and the fused per-tile residual partials reduce in the same order
+static int32_t plan_tile(KParams& K, bool g, bool j, bool f, bool grad, int t_max = 64, bool size_without_j = false) {
   K.want_g = g; K.want_j = j; K.want_f = f; K.want_grad = grad;
   const bool sq = K.env_kind == CPL_ENV_SUPERQUADRIC || K.env_kind == CPL_ENV_MIXED;
   K.LR = K.N * SQ_L + 1;  // odd instance stride of the SQ scratch: conflict-free LDS banks
   const size_t per = sizeof(double) * (size_t)(K.n + (g ? K.m : 0) + (j && !K.jdirect ? K.nnz : 0) +
                                                (grad ? K.n : 0) + (sq ? K.LR : 0));
+  const size_t per_t = size_without_j ? per - sizeof(double) * (size_t)(j && !K.jdirect ? K.nnz : 0) : per;
   const size_t fixed = sizeof(double) * 72 + sizeof(CTab);  // index lists + parameter table
   int T = 64, logT = 6;
   while (T > t_max) { T >>= 1; --logT; }
-  while (T > 2 && (size_t)T * per + fixed > tile_budget()) { T >>= 1; --logT; }
+  while (T > 2 && (size_t)T * per_t + fixed > tile_budget()) { T >>= 1; --logT; }
   // (T >= 2 is even, so every tile of every record array starts on a 16-byte boundary; below 8 the
   // tile boundaries no longer fall on 128-byte lines — the price of more resident workgroups for
   // the large VALU-bound records)
@@ -2066,7 +2070,7 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
     // Superquadric records are small enough that the staged copy-out wins there (0.32 vs 0.42 ms)
     const bool jd = g_variant == VAR_TILE_JD || (g_variant == VAR_AUTO && K.env_kind == CPL_ENV_MIXED);
     K.jdirect = (jd && d_jac && !K.soa) ? 1 : 0;
-    st = plan_tile(K, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr);
+    st = plan_tile(K, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr, 64, jd && d_jac);
     const int wg = g_wg;
     if (st) return st;
     K.ablate = g_ablate;
