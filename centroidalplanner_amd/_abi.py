@@ -85,7 +85,7 @@ class SolveOptions(ctypes.Structure):
         ("acceptable_iter", c_int32),
         ("use_graph", c_int32),
         ("compact", c_int32),
-        ("reserved1", c_int32),
+        ("ls_kernel", c_int32),
         ("tol", c_double),
         ("acceptable_tol", c_double),
         ("mu_init", c_double),

@@ -169,7 +169,8 @@ class NativeSolver:
     once, the iteration captured once as a HIP graph and replayed on every solve."""
 
     def __init__(self, problem, batch, tol=1e-8, max_iter=3000, mu_init=0.1, acceptable_tol=1e-6,
-                 acceptable_iter=15, max_ls=40, max_soc=4, hessian="exact", fd_step=1e-6, graph=True, compact=True):
+                 acceptable_iter=15, max_ls=40, max_soc=4, hessian="exact", fd_step=1e-6, graph=True, compact=True,
+                 ls_kernel=1):
         o = _abi.SolveOptions()
         _abi.lib.cpl_solve_options_default(ctypes.byref(o))
         o.max_iter, o.max_ls, o.max_soc, o.acceptable_iter = int(max_iter), int(max_ls), int(max_soc), int(acceptable_iter)
@@ -178,6 +179,7 @@ class NativeSolver:
                      "fd": _abi.HESSIAN_FD}[hessian]
         o.use_graph = 1 if graph else 0
         o.compact = 1 if compact else 0
+        o.ls_kernel = int(ls_kernel)
         self.problem, self.batch = problem, int(batch)
         self.desc = problem.desc()
         self.handle = ctypes.c_void_p()
@@ -251,7 +253,8 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                     max_iter: int = 3000, mu_init: float = 0.1, acceptable_tol: float = 1e-6,
                     acceptable_iter: int = 15, max_ls: int = 40, max_soc: int = 4, hessian: str = "exact",
                     fd_step: float = 1e-6, graph: Optional[bool] = None, check_every: int = 4,
-                    verbose: int = 0, compact: bool = True, verbose_instance: int = 0) -> BatchSolveResult:
+                    verbose: int = 0, compact: bool = True, verbose_instance: int = 0,
+                    ls_kernel: int = 1) -> BatchSolveResult:
     """Solve B instances of `problem`'s template from the starting points X0 [B, n] (torch float64,
     device tensor), per-instance robot masses `mass` [B] (None: the template's).
 
@@ -262,7 +265,10 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     otherwise), "fd" (always the central differences) or "limited-memory"
     (IPOPT's L-BFGS, 6 pairs).  graph: capture one iteration as a HIP graph (default: on for device tensors).
     max_ls / max_soc: at most this many backtracking trials per iteration (the search also stops below
-    IPOPT's alpha_min) / second-order corrections on the first trial (IPOPT max_soc 4)."""
+    IPOPT's alpha_min) / second-order corrections on the first trial (IPOPT max_soc 4).
+    ls_kernel (device engine): the whole line search (first trial, its corrections, backtracking) in
+    one launch for 47 x 30 systems — 1: batches of at most 256 rows, 2: always, 0: never; the same
+    iterates bit for bit."""
     if hessian not in ("exact", "fd", "limited-memory"):
         raise ValueError("hessian must be 'exact', 'fd' or 'limited-memory'")
     use_bfgs = hessian == "limited-memory"
@@ -274,7 +280,8 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                              "host tensors")
         ns = _native(problem, X0.shape[0], tol=tol, max_iter=max_iter, mu_init=mu_init, acceptable_tol=acceptable_tol,
                      acceptable_iter=acceptable_iter, max_ls=max_ls, max_soc=max_soc, hessian=hessian,
-                     fd_step=fd_step, graph=True if graph is None else bool(graph), compact=compact)
+                     fd_step=fd_step, graph=True if graph is None else bool(graph), compact=compact,
+                     ls_kernel=ls_kernel)
         r = ns.solve(X0, mass, None if evaluator is None else evaluator.env_tag)
         if evaluator is not None:
             evaluator.calls += r.evaluations

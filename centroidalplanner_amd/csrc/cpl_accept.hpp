@@ -17,6 +17,7 @@ namespace cpl {
 constexpr double LS_GAMMA_TH = 1e-5, LS_GAMMA_PHI = 1e-8, LS_DELTA = 1.0, LS_S_TH = 1.1, LS_S_PHI = 2.3;
 constexpr double LS_ETA_PHI = 1e-8, LS_OBJ_MAX_INC = 5.0;
 constexpr int LS_MAX_SOFT_RESTO = 10;  // max_soft_resto_iters
+constexpr double LS_KAPPA_SOC = 0.99;  // kappa_soc
 
 // theta_max; the filter (entries stored with their margins ((1 - gamma_theta) theta, phi - gamma_phi
 // theta): acceptable when, for every entry, theta or phi is not larger — IPOPT's Filter::Acceptable);
@@ -96,6 +97,17 @@ struct LsBacktrackArgs {
   const double* wR;
   double* st_p;
   double* st_n;
+  // first != 0 (regular search; systems the one-wave KKT kernel factorises): the kernel also makes
+  // the first trial at alpha (alpha_max) and its up to max_soc second-order corrections (batch_ipm.py
+  // regular_step, IPOPT's TrySecondOrderCorrection), re-solving with the factors the iteration's
+  // factorisation kept (kkt_ws), before it backtracks — one launch for the whole search
+  int32_t first;
+  int32_t max_soc;
+  const double* c;            // [batch, m] c(w) at the iterate
+  const double* M;            // [batch, nw, nw] the Newton system's M
+  const double* r1;           // [batch, nw] its first right-hand side
+  const double* kkt_ws;       // cpl_kkt_solve's factor workspace (mode 0 of this iteration)
+  const double* tau;          // [batch] fraction-to-the-boundary parameter
 };
 
 }  // namespace cpl

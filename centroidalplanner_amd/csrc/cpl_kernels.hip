@@ -33,6 +33,7 @@
 #include <vector>
 
 #include "cpl_accept.hpp"
+#include "cpl_kkt_wave.hpp"
 #include "cpl_layout.hpp"
 #include "cpl_wave.hpp"
 #include "cpl_status.hpp"
@@ -2108,7 +2109,7 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
 // cpl_ipm_judge_take judges the first trial.  The whole search runs in the kernel: the engine's
 // iteration no longer waits for the host between trials (one trial per graph launch and a flag read
 // back per trial cost ~55 us each; the lock-step batch makes as many trials as its slowest instance).
-template <int ENVK, bool RESTO>
+template <int ENVK, bool RESTO, bool FIRST>
 __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, const LsBacktrackArgs A) {
   extern __shared__ __align__(16) double smem[];
   __shared__ double s_f;
@@ -2119,12 +2120,16 @@ __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, c
   bool searching = act && A.searching[b] != 0;
   double al = A.alpha[b];
   double st_alpha = A.st_alpha[b];
-  if (searching && A.max_trials > 0) {
+  if (searching && (FIRST || A.max_trials > 0)) {
     const int n = A.n, m = A.m, nf = A.nf, nw = A.nw, N = K.N;
+    constexpr bool SQK = ENVK == CPL_ENV_SUPERQUADRIC || ENVK == CPL_ENV_MIXED;
+    const int nL = SQK ? N * SQ_L : 0;
     double* X = smem;
     double* G = X + n;
     double* wt = G + m;
     double* L = wt + nw;  // [N][SQ_L] Superquadric scratch
+    double* Dv = L + nL;  // (FIRST) the second-order correction's step
+    double* kk = smem + ((n + m + 2 * nw + nL + 1) & ~1);  // (FIRST) the KKT re-solve's LDS image
     load_ctab(K);
     __syncthreads();
     const double* wb = A.w + b * nw;
@@ -2138,12 +2143,15 @@ __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, c
     const double thmax = A.theta_max[b];
     const double* ft = A.filt_t + b * A.nfilt;
     const double* fp = A.filt_p + b * A.nfilt;
-    for (int trial = 0; trial < A.max_trials && searching; ++trial) {
-      // the trial point (cpl_ipm_trial_point's arithmetic)
-      for (int k = lane; k < nw; k += 64) wt[k] = wb[k] + al * db[k];
+    // One trial: the point w + step dir (cpl_ipm_trial_point's arithmetic), f and g there, theta and
+    // the barrier objective, the acceptance test with the step al_j (cpl_ipm_judge_take's arithmetic).
+    // Leaves the trial's g in G, its w in wt, its f in s_f.
+    auto trial = [&](const double* dir, double step, double al_j, double& th_out, bool& aug) -> bool {
+      __syncthreads();  // the LDS images of the previous trial are read no more
+      for (int k = lane; k < nw; k += 64) wt[k] = wb[k] + step * dir[k];
       for (int j = lane; j < n; j += 64) {
         const int k = A.freepos[j];
-        X[j] = k >= 0 ? wb[k] + al * db[k] : Xb[j];
+        X[j] = k >= 0 ? wb[k] + step * dir[k] : Xb[j];
       }
       __syncthreads();
       // f and g of the trial point: the eval work items of one instance
@@ -2164,7 +2172,6 @@ __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, c
         }
       }
       __syncthreads();
-      // theta, the barrier objective, the acceptance test (cpl_ipm_judge_take's arithmetic)
       double th = 0.0;
       for (int r = lane; r < m; r += 64) {
         const int s = A.row_slack[r];
@@ -2180,7 +2187,7 @@ __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, c
         th = 0.0;
         for (int r = lane; r < m; r += 64) {
           const int s = A.row_slack[r];
-          const double pt = A.pR[b * m + r] + al * A.dp[b * m + r], nt = A.nR[b * m + r] + al * A.dn[b * m + r];
+          const double pt = A.pR[b * m + r] + al_j * A.dp[b * m + r], nt = A.nR[b * m + r] + al_j * A.dn[b * m + r];
           th += fabs((s < 0 ? G[r] - A.gl[r] : G[r] - wt[nf + s]) - pt + nt);
           pn += pt + nt;
           lpn += log(pt) + log(nt);
@@ -2193,36 +2200,89 @@ __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, c
       }
       th = wave_sum(th);
       lg = wave_sum(lg);
-      const double fv = s_f;
-      double ph = fv - mub * lg;
+      double ph = s_f - mub * lg;
       if (RESTO) {
         pn = wave_sum(pn);
         lpn = wave_sum(lpn);
         prox = wave_sum(prox);
         ph = A.rho * pn + 0.5 * sqrt(mub) * prox - mub * lg - mub * lpn;
       }
-      bool aug = false;
-      const bool ok = ls_acceptable_wave(th, ph, tk, pk, g, al, sw, thmax, ft, fp, A.nfilt, &aug);
-      if (ok) {  // take it
-        for (int r = lane; r < m; r += 64) A.st_g[b * m + r] = G[r];
-        for (int k = lane; k < nw; k += 64) A.st_w[b * nw + k] = wt[k];
-        if (RESTO)
-          for (int r = lane; r < m; r += 64) {
-            A.st_p[b * m + r] = A.pR[b * m + r] + al * A.dp[b * m + r];
-            A.st_n[b * m + r] = A.nR[b * m + r] + al * A.dn[b * m + r];
-          }
-        if (lane == 0) {
-          A.st_f[b] = fv;
-          A.st_alpha[b] = al;
-          A.st_aug[b] = aug ? 1 : 0;
+      th_out = th;
+      return ls_acceptable_wave(th, ph, tk, pk, g, al_j, sw, thmax, ft, fp, A.nfilt, &aug);
+    };
+    // the take of an accepted trial: its f, g, w (p, n) and step into the line-search state
+    auto take = [&](double al_j, bool aug) {
+      for (int r = lane; r < m; r += 64) A.st_g[b * m + r] = G[r];
+      for (int k = lane; k < nw; k += 64) A.st_w[b * nw + k] = wt[k];
+      if (RESTO)
+        for (int r = lane; r < m; r += 64) {
+          A.st_p[b * m + r] = A.pR[b * m + r] + al_j * A.dp[b * m + r];
+          A.st_n[b * m + r] = A.nR[b * m + r] + al_j * A.dn[b * m + r];
         }
-        st_alpha = al;
-        searching = false;
-      } else {  // IPOPT: the next trial only above alpha_min
-        al = 0.5 * al;
-        searching = al > a_min;
+      if (lane == 0) {
+        A.st_f[b] = s_f;
+        A.st_alpha[b] = al_j;
+        A.st_aug[b] = aug ? 1 : 0;
       }
-      __syncthreads();  // the LDS images are rewritten by the next trial
+      st_alpha = al_j;
+      searching = false;
+    };
+    // The search as one loop with one trial call site (the trial is large: one inlined copy).
+    // FIRST: the first trial at alpha_max, then IPOPT's second-order corrections of it: c_soc =
+    // a c_k + c(trial) (accumulated a_soc c_soc + c(correction) from the second on), the step of
+    // [M A^T; A 0] [dw; dy] = [r1; -c_soc] from the kept factors, its own fraction to the boundary,
+    // the corrected point judged with the first trial's alpha; the next correction only while the
+    // last one cut theta by kappa_soc (k_soc_begin_rhs / k_soc_rhs / k_soc_after's bookkeeping);
+    // then alpha halved (k_halve2) and the backtracking trials (at most max_trials more).
+    constexpr int KNW = 47, KM = 30;
+    enum { S_FIRST, S_SOC, S_BACK };
+    int stage = (FIRST && !RESTO) ? S_FIRST : S_BACK;
+    int q = 0, tr = 0;
+    double csoc = 0.0, a_soc = 0.0, th_old = 0.0;
+    const int s_l = lane < m ? A.row_slack[lane] : -1;
+    const double gl_l = lane < m ? A.gl[lane] : 0.0;
+    auto cons = [&]() { return s_l >= 0 ? G[lane] - wt[nf + s_l] : G[lane] - gl_l; };  // lane < m
+    while (searching && (stage != S_BACK || tr < A.max_trials)) {
+      const double* dir = db;
+      double step = al;
+      if (FIRST && !RESTO && stage == S_SOC) {
+        if (q > 0 && lane < m) csoc = a_soc * csoc + cons();
+        double dwv, dyv;
+        kkt_wave_resolve<KNW, KM>(A.M + b * KNW * KNW, A.kkt_ws + b * kkt_ws_per(KNW, KM),
+                                  lane < KNW ? A.r1[b * KNW + lane] : 0.0, lane < KM ? -csoc : 0.0, kk, &dwv, &dyv);
+        if (lane < nw) Dv[lane] = dwv;
+        double r = INFINITY;  // cpl_ipm_max_step (primal)
+        const double t = A.tau[b];
+        for (int k = lane; k < nw; k += 64) {
+          const double vk = wb[k], dk = dwv;
+          if (A.hasL[k] && dk < 0.0) r = fmin(r, -t * (vk - A.wl0[k]) / dk);
+          if (A.hasU[k] && dk > 0.0) r = fmin(r, -t * (A.wu0[k] - vk) / -dk);
+        }
+        a_soc = fmin(wave_min(r), 1.0);
+        dir = Dv;
+        step = a_soc;
+      }
+      double th;
+      bool aug = false;
+      if (trial(dir, step, al, th, aug)) {
+        take(al, aug);
+        break;
+      }
+      if (stage == S_FIRST && A.max_soc > 0 && th >= tk) {
+        if (lane < m) csoc = al * A.c[b * m + lane] + cons();
+        a_soc = al;
+        th_old = th;
+        stage = S_SOC;
+        continue;
+      }
+      if (stage == S_SOC && ++q < A.max_soc && th <= LS_KAPPA_SOC * th_old) {
+        th_old = th;
+        continue;
+      }
+      if (stage == S_BACK) ++tr;
+      stage = S_BACK;
+      al = 0.5 * al;  // IPOPT: the next trial only above alpha_min
+      searching = al > a_min;
     }
   }
   if (lane == 0) {
@@ -2255,16 +2315,23 @@ int32_t ls_backtrack(const cpl_problem_desc* d, const LsBacktrackArgs& a, hipStr
   K.fold = FOLD_NONE;
   const bool sq = d->env_kind == CPL_ENV_SUPERQUADRIC || d->env_kind == CPL_ENV_MIXED;
   if (d->env_kind == CPL_ENV_MIXED && !a.env_tag) return fail(CPL_ERR_INVALID_ARGUMENT, "ls_backtrack: mixed needs tags");
-  const size_t lds = sizeof(double) * ((size_t)a.n + a.m + a.nw + (sq ? (size_t)K.N * SQ_L : 0) + 2);
+  const bool first = a.first != 0;
+  if (first && (a.resto || a.nw != 47 || a.m != 30 || !a.c || !a.M || !a.r1 || !a.kkt_ws || !a.tau))
+    return fail(CPL_ERR_INVALID_ARGUMENT, "ls_backtrack: the fused first trial needs a 47 x 30 system and its buffers");
+  const size_t nL = sq ? (size_t)K.N * SQ_L : 0;
+  size_t lds = sizeof(double) * ((size_t)a.n + a.m + a.nw + nL + 2);
+  if (first) lds = sizeof(double) * ((((size_t)a.n + a.m + 2 * (size_t)a.nw + nL + 1) & ~(size_t)1) + KktWave<47, 30>::LDS);
   using KernT = void (*)(const KParams, const LsBacktrackArgs);
-  static const KernT table[2][4] = {
-      {cpl_ls_backtrack_kernel<CPL_ENV_NONE, false>, cpl_ls_backtrack_kernel<CPL_ENV_GROUND, false>,
-       cpl_ls_backtrack_kernel<CPL_ENV_SUPERQUADRIC, false>, cpl_ls_backtrack_kernel<CPL_ENV_MIXED, false>},
-      {cpl_ls_backtrack_kernel<CPL_ENV_NONE, true>, cpl_ls_backtrack_kernel<CPL_ENV_GROUND, true>,
-       cpl_ls_backtrack_kernel<CPL_ENV_SUPERQUADRIC, true>, cpl_ls_backtrack_kernel<CPL_ENV_MIXED, true>}};
+#define CPL_LS_KERNELS(R, F)                                                                                   \
+  {cpl_ls_backtrack_kernel<CPL_ENV_NONE, R, F>, cpl_ls_backtrack_kernel<CPL_ENV_GROUND, R, F>,                 \
+   cpl_ls_backtrack_kernel<CPL_ENV_SUPERQUADRIC, R, F>, cpl_ls_backtrack_kernel<CPL_ENV_MIXED, R, F>}
+  static const KernT table[3][4] = {CPL_LS_KERNELS(false, false), CPL_LS_KERNELS(true, false),
+                                    CPL_LS_KERNELS(false, true)};
+#undef CPL_LS_KERNELS
   if (a.resto && (!a.pR || !a.nR || !a.dp || !a.dn || !a.wR || !a.st_p || !a.st_n))
     return fail(CPL_ERR_INVALID_ARGUMENT, "ls_backtrack: restoration search without its buffers");
-  hipLaunchKernelGGL(table[a.resto ? 1 : 0][K.env_kind], dim3((unsigned)a.batch), dim3(64), lds, stream, K, a);
+  hipLaunchKernelGGL(table[first ? 2 : (a.resto ? 1 : 0)][K.env_kind], dim3((unsigned)a.batch), dim3(64), lds, stream,
+                     K, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "cpl_ls_backtrack_kernel launch");
   return CPL_OK;

@@ -39,6 +39,7 @@ int32_t ipm_newton_setup_lm(int64_t batch, int32_t nw, int32_t m, int32_t nf, co
                             double* d_mr_diag, double* d_theta, double* d_phi, const uint8_t* d_active, void* stream);
 // cpl_kernels.hip: the backtracking line search after the first trial, one wave per instance
 int32_t ls_backtrack(const cpl_problem_desc* d, const LsBacktrackArgs& a, hipStream_t stream);
+bool kkt_wave_size(int nw, int m);
 // cpl_ipm.hip: the optimality test + monotone barrier update with IPOPT's per-iteration rounds
 double ipm_mu_min(double tol);
 int32_t ipm_optimality_ex(int64_t batch, int32_t nw, int32_t m, int32_t fmax, int32_t nbounds, double tol,
@@ -1519,6 +1520,7 @@ struct cpl_solver {
   int64_t Bcur = 0;  // rows in play: B, shrunk by active-set compaction
   int n = 0, m = 0, nnz = 0, nnz_rec = 0, nf = 0, nI = 0, nw = 0, nbounds = 0;
   bool analytic_H = false, bfgs = false, fd = false, fd_fused = true;
+  bool ls_fusable = false;  // the one-wave KKT size: the fused line-search kernel can re-solve with its factors
   double mu_min = 0.0;
   hipStream_t stream = nullptr;
   bool captured = false;  // an iteration graph exists
@@ -1745,8 +1747,32 @@ int32_t step_phase(cpl_solver* S, int phase) {
                          S->tiny_flag, S->tiny_now, S->soft_now, S->a_min, S->searching, S->st_f, S->st_g, S->st_w,
                          S->st_alpha, S->st_aug, S->alpha, S->d_any);
       LAUNCHED("k_ls_setup");
-      CK(first_trial());
-      if (o.max_ls > 1) {  // the remaining trials of every instance still searching, in one launch
+      // the whole search in one launch (first trial, its corrections, the backtracking), or the
+      // first trial step by step and the remaining trials in one launch
+      const bool fused = o.ls_kernel == 2 || (o.ls_kernel == 1 && B <= FUSE_ROWS);
+      if (!(fused && S->ls_fusable)) CK(first_trial());
+      if (fused && S->ls_fusable) {
+        LsBacktrackArgs la;
+        la.batch = B; la.n = n; la.m = m; la.nf = nf; la.nw = nw; la.nfilt = FMAX; la.max_trials = o.max_ls - 1;
+        if (la.max_trials < 0) la.max_trials = 0;
+        la.act = S->act; la.tiny = S->tiny_now; la.soft_now = S->soft_now; la.soft_cnt = S->soft_cnt;
+        la.searching = S->searching; la.alpha = S->alpha; la.a_min = S->a_min;
+        la.w = S->w; la.dw = S->dw; la.Xbase = S->Xbase; la.freepos = S->freepos; la.row_slack = S->row_slack;
+        la.gl = S->gl; la.hasL = S->hasL; la.hasU = S->hasU; la.wl0 = S->wl0; la.wu0 = S->wu0;
+        la.mu = S->mu_o; la.theta_k = S->theta_k; la.phi_k = S->phi_k; la.gd = S->gd; la.switch_ok = S->switch_ok;
+        la.theta_max = S->theta_max; la.filt_t = S->ft; la.filt_p = S->fp;
+        la.mass = S->mass; la.env_tag = S->tag;
+        la.st_f = S->st_f; la.st_g = S->st_g; la.st_w = S->st_w; la.st_alpha = S->st_alpha; la.st_aug = S->st_aug;
+        la.any = S->d_any;
+        la.resto = 0;
+        la.rho = 0.0;
+        la.pR = la.nR = la.dp = la.dn = la.wR = nullptr;
+        la.st_p = la.st_n = nullptr;
+        la.first = 1;
+        la.max_soc = o.max_soc;
+        la.c = S->c; la.M = S->M; la.r1 = S->r1; la.kkt_ws = S->ws; la.tau = S->tau;
+        CK(ls_backtrack(&S->desc, la, st));
+      } else if (o.max_ls > 1) {  // the remaining trials of every instance still searching, in one launch
         HK(hipMemsetAsync(S->d_any, 0, 2, st), "hipMemsetAsync flags");
         LsBacktrackArgs la;
         la.batch = B; la.n = n; la.m = m; la.nf = nf; la.nw = nw; la.nfilt = FMAX; la.max_trials = o.max_ls - 1;
@@ -1763,6 +1789,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
         la.rho = 0.0;
         la.pR = la.nR = la.dp = la.dn = la.wR = nullptr;
         la.st_p = la.st_n = nullptr;
+        la.first = 0; la.max_soc = 0; la.c = la.M = la.r1 = la.kkt_ws = la.tau = nullptr;
         CK(ls_backtrack(&S->desc, la, st));
       }
       return CPL_OK;
@@ -1878,6 +1905,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
         la.rho = RHO_R;
         la.pR = S->pR; la.nR = S->nR; la.dp = S->dp; la.dn = S->dn; la.wR = S->wR;
         la.st_p = S->st_p; la.st_n = S->st_n;
+        la.first = 0; la.max_soc = 0; la.c = la.M = la.r1 = la.kkt_ws = la.tau = nullptr;
         CK(ls_backtrack(&S->desc, la, st));
       }
       return step_phase(S, P_RACCEPT);
@@ -2046,6 +2074,7 @@ void cpl_solve_options_default(cpl_solve_options* o) {
   o->acceptable_iter = 15;
   o->use_graph = 1;
   o->compact = 1;
+  o->ls_kernel = 1;
   o->tol = 1e-8;
   o->acceptable_tol = 1e-6;
   o->mu_init = 0.1;
@@ -2099,7 +2128,7 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   cpl_solve_options_default(&opt);
   if (o) opt = *o;
   if (opt.hessian < CPL_HESSIAN_EXACT || opt.hessian > CPL_HESSIAN_FD || opt.max_iter < 0 || opt.max_soc < 0 ||
-      opt.max_ls < 0 || !(opt.tol > 0.0))
+      opt.max_ls < 0 || !(opt.tol > 0.0) || opt.ls_kernel < 0 || opt.ls_kernel > 2)
     return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_solver_create: bad options");
   int32_t n, m, nnz;
   CK(cpl_dims(d, &n, &m, &nnz));
@@ -2180,6 +2209,7 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   S->opt = opt;
   S->B = batch;
   S->n = n; S->m = m; S->nnz = nnz; S->nnz_rec = nnz_rec; S->nf = nf; S->nI = nI; S->nw = nw; S->nbounds = nbounds;
+  S->ls_fusable = kkt_wave_size(nw, m);
   S->mu_min = ipm_mu_min(opt.tol);
   S->bfgs = opt.hessian == CPL_HESSIAN_LIMITED_MEMORY;
   S->analytic_H = opt.hessian == CPL_HESSIAN_EXACT && cpl_lagrangian_hessian(d, 0, nullptr, nullptr, nullptr, nullptr,

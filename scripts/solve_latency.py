@@ -20,6 +20,7 @@ from centroidalplanner_amd.workload import solve_inputs, solve_problem  # noqa: 
 ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--only", default="", help="run one case, e.g. limited-memory:1 (for a kernel trace)")
+ap.add_argument("--ls-kernel", type=int, default=1, help="the engine's ls_kernel option (0 / 1 / 2)")
 args = ap.parse_args()
 
 prob = solve_problem().GetCplProblem()
@@ -33,11 +34,11 @@ if args.only:
 for hessian, B in cases:
     if True:
         Xt, mt = torch.tensor(X0[:B], device=dev), torch.tensor(mass[:B], device=dev)
-        r = batch_ipm_solve(prob, Xt, mt, max_iter=1000, hessian=hessian)  # warm: engine + graphs
+        r = batch_ipm_solve(prob, Xt, mt, max_iter=1000, hessian=hessian, ls_kernel=args.ls_kernel)  # warm: engine + graphs
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.reps):
-            r = batch_ipm_solve(prob, Xt, mt, max_iter=1000, hessian=hessian)
+            r = batch_ipm_solve(prob, Xt, mt, max_iter=1000, hessian=hessian, ls_kernel=args.ls_kernel)
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / args.reps
         its = r.iterations.double()

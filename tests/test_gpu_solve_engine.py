@@ -81,3 +81,25 @@ def test_com_planner_from_zero_device_matches_host():
     assert bool((d.status <= STATUS_ACCEPTABLE).all()) and bool((h.status <= STATUS_ACCEPTABLE).all())
     # converged to tol 1e-8 (scaled): objectives of ~3e-4 agree to the solver's tolerance
     np.testing.assert_allclose(d.objective.cpu().numpy(), h.objective.numpy(), rtol=1e-6, atol=1e-8)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hessian,max_ls,max_soc,seed", [("limited-memory", 40, 4, 3), ("exact", 40, 4, 5),
+                                                         ("limited-memory", 4, 1, 7), ("exact", 1, 2, 9)])
+def test_fused_line_search_is_bitwise_the_stepwise_search(hessian, max_ls, max_soc, seed):
+    """The whole line search in one launch (cpl_ls_backtrack_kernel FIRST: the first trial, its
+    second-order corrections re-solved with the kept one-wave KKT factors, the backtracking) takes
+    bitwise the iterates of the step-by-step search (trial point / eval / judge / SOC launches):
+    every batch size then solves an instance the same way whichever path its size selects."""
+    prob = solve_problem().GetCplProblem()
+    B = 48
+    X0, mass = solve_inputs(prob, B, seed=seed)
+    dev = torch.device("cuda:0")
+    X0t, mt = torch.as_tensor(X0, device=dev), torch.as_tensor(mass, device=dev)
+    kw = dict(max_iter=1000, hessian=hessian, max_ls=max_ls, max_soc=max_soc)
+    a = batch_ipm_solve(prob, X0t, mt, ls_kernel=2, **kw)
+    b = batch_ipm_solve(prob, X0t, mt, ls_kernel=0, **kw)
+    for k in ("x", "y", "status", "iterations", "objective", "restorations"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    if max_ls == 40:
+        assert bool((a.status <= STATUS_ACCEPTABLE).all())
