@@ -104,9 +104,12 @@ static_assert(sizeof(KParams) < 4096, "kernel parameters must fit the kernarg se
 // axis index.  A kernarg read with a divergent index is a vector memory load, and its vmcnt wait
 // would also drain the wave's in-flight output stores; an LDS read waits on lgkmcnt only.
 constexpr int CPL_MAX_ROWS = 6 + 6 * CPL_MAX_CONTACTS;
+// The Superquadric per-axis factors too (the two-phase items index them with a lane-varying axis).
+enum { AX_C, AX_R, AX_P, AX_EJ, AX_KA, AX_KB, AX_RM2, AX_RP2, AX_PSQ, AX_PM1, AX_P2, AX_P2M2, AX_P2M3, AX_N };
 struct CTab {
   int32_t map_order[CPL_MAX_CONTACTS];
   double F_thr[CPL_MAX_CONTACTS];
+  double ax[AX_N][3];          // KParams' C, R, P, EJ, Ka, Kb, Rm2, Rp2, Psq, Pm1, P2, P2m2, P2m3
   uint8_t cone[CPL_MAX_ROWS];  // row r of g is a FrictionCone row (bounds (-inf, 0]) — residual norms
 };
 __shared__ CTab s_ct;
@@ -117,6 +120,26 @@ __device__ __forceinline__ void load_ctab(const KParams& K) {
   if (t < CPL_MAX_CONTACTS) {
     s_ct.map_order[t] = K.map_order[t];
     s_ct.F_thr[t] = K.F_thr[t];
+  }
+  if (t < 3 * AX_N) {  // (no pointers into K: an address-taken kernarg struct is copied to scratch)
+    const int f = t / 3, a = t - 3 * (t / 3);
+    double v;
+    switch (f) {
+      case AX_C: v = K.C[a]; break;
+      case AX_R: v = K.R[a]; break;
+      case AX_P: v = K.P[a]; break;
+      case AX_EJ: v = K.EJ[a]; break;
+      case AX_KA: v = K.Ka[a]; break;
+      case AX_KB: v = K.Kb[a]; break;
+      case AX_RM2: v = K.Rm2[a]; break;
+      case AX_RP2: v = K.Rp2[a]; break;
+      case AX_PSQ: v = K.Psq[a]; break;
+      case AX_PM1: v = K.Pm1[a]; break;
+      case AX_P2: v = K.P2[a]; break;
+      case AX_P2M2: v = K.P2m2[a]; break;
+      default: v = K.P2m3[a]; break;
+    }
+    s_ct.ax[f][a] = v;
   }
   for (int r = t; r < K.m; r += blockDim.x)
     s_ct.cone[r] = r >= 6 && ((r - 6) % K.contact_rows) >= K.contact_rows - 2;
@@ -183,6 +206,18 @@ __device__ __forceinline__ void block_norms(const NormAcc& a, double& bm, double
 // 65 536 x 4: its store-ack / atomic / reload round trips sit on the kernel's tail.)
 constexpr int NORM_HDR = 128;
 
+
+// partial pair per WAVE (tile kernel): DPP wave reductions and no barrier, so the reduction adds no
+// synchronisation to a workgroup's critical path (the block reduction with its two barriers cost the
+// latency-bound Superquadric tiles 14 %); pair index blockIdx.x * waves + wave
+__device__ __forceinline__ void partial_norms_waves(const NormAcc& a, double* __restrict__ part) {
+  const double bm = wave_max(a.vmax), bs = wave_sum(a.vsum);
+  if ((threadIdx.x & 63) == 0) {
+    const int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    part[2 * i] = bm;
+    part[2 * i + 1] = bs;
+  }
+}
 
 // partial pair per workgroup with plain stores (the kernel boundary is the coherence point)
 __device__ void partial_norms(const NormAcc& a, double* __restrict__ part) {
@@ -401,6 +436,55 @@ __device__ __forceinline__ void axis_powers(const KParams& K, int a, double d, A
   o.p2Pm3 = cpow(d, K.P2m3[a]);
   o.p2Pm2 = cpow(d, K.P2m2[a]);
   o.p2P = cpow(d, K.P2[a]);
+}
+
+// A per-axis Superquadric factor with a lane-varying axis a: from the block's LDS table (AXL) or
+// from the kernel arguments (a vector load from the kernarg segment).  Mixed batches take the LDS
+// table (the kernarg loads' vmcnt waits also waited for the Jacobian rows' global stores: 3.65 ->
+// 3.41 ms at 1M x 16); Superquadric batches keep the kernarg loads (the LDS table raised their
+// kernel from 113 to 145 VGPRs, three waves per SIMD instead of four: 0.32 -> 0.39 ms at 262k x 8).
+template <bool AXL>
+__device__ __forceinline__ double axv(const KParams& K, int f, int a) {
+  if (AXL) return s_ct.ax[f][a];
+  switch (f) {
+    case AX_C: return K.C[a];
+    case AX_R: return K.R[a];
+    case AX_P: return K.P[a];
+    case AX_EJ: return K.EJ[a];
+    case AX_KA: return K.Ka[a];
+    case AX_KB: return K.Kb[a];
+    case AX_RM2: return K.Rm2[a];
+    case AX_RP2: return K.Rp2[a];
+    case AX_PSQ: return K.Psq[a];
+    case AX_PM1: return K.Pm1[a];
+    case AX_P2: return K.P2[a];
+    case AX_P2M2: return K.P2m2[a];
+    default: return K.P2m3[a];
+  }
+}
+
+// axis_powers with the exponents through axv (the two-phase items: lane-varying a)
+template <bool AXL>
+__device__ __forceinline__ void axis_powers_ax(const KParams& K, bool ladder, int a, double d, AxisPowers& o) {
+  if (ladder) {
+    const dd B = dd_ipow(d, (unsigned)axv<AXL>(K, AX_P, a) - 2u);
+    const dd A = dd_mul_d(B, d);
+    const dd Q = dd_mul_d(A, d);
+    const double q2 = dd_sqr(Q).hi;
+    if (q2 == q2 && fabs(q2) >= DD_TINY && fabs(q2) <= DD_HUGE) {  // every chain member in range
+      o.pm1 = A.hi;
+      o.pP = Q.hi;
+      o.p2Pm3 = dd_mul(B, A).hi;
+      o.p2Pm2 = dd_sqr(A).hi;
+      o.p2P = q2;
+      return;
+    }
+  }
+  o.pm1 = cpow(d, axv<AXL>(K, AX_PM1, a));
+  o.pP = cpow(d, axv<AXL>(K, AX_P, a));
+  o.p2Pm3 = cpow(d, axv<AXL>(K, AX_P2M3, a));
+  o.p2Pm2 = cpow(d, axv<AXL>(K, AX_P2M2, a));
+  o.p2P = cpow(d, axv<AXL>(K, AX_P2, a));
 }
 
 __device__ __forceinline__ void superquadric_contact(const KParams& K, double p0, double p1, double p2,
@@ -979,36 +1063,37 @@ __device__ __forceinline__ void cost_item(const KParams& K, const double* __rest
 constexpr int SQ_L = 18;  // per contact: 3 axes x {pm1, pP, p2Pm3, p2Pm2, p2P, inv}
 enum { L_PM1 = 0, L_PP, L_P2PM3, L_P2PM2, L_P2P, L_INV, L_AXIS };
 
+template <bool AXL>
 __device__ __forceinline__ void sq_axis_item(const KParams& K, const double* __restrict__ xr, int k, int a,
                                              double* __restrict__ Lc, double* __restrict__ Gr) {
   const int i = s_ct.map_order[k];
   const double pa = xr[6 + 9 * i + a];
-  const double d = -K.C[a] + pa;
+  const double d = -axv<AXL>(K, AX_C, a) + pa;
   double* o = Lc + a * L_AXIS;
   if (K.want_g) {
     // src/Superquadric.cpp:45  pow((p-C)/R, P)
-    const double u = (pa - K.C[a]) / K.R[a];
+    const double u = (pa - axv<AXL>(K, AX_C, a)) / axv<AXL>(K, AX_R, a);
     double w;
     if (K.sq_ladder && fabs(u) >= DD_TINY && fabs(u) <= 0x1p+40) {
-      w = dd_ipow(u, (unsigned)K.P[a]).hi;
-      if (!(fabs(w) >= DD_TINY && fabs(w) <= DD_HUGE)) w = cpow(u, K.P[a]);
+      w = dd_ipow(u, (unsigned)axv<AXL>(K, AX_P, a)).hi;
+      if (!(fabs(w) >= DD_TINY && fabs(w) <= DD_HUGE)) w = cpow(u, axv<AXL>(K, AX_P, a));
     } else {
-      w = cpow(u, K.P[a]);
+      w = cpow(u, axv<AXL>(K, AX_P, a));
     }
     Gr[6 + 6 * k + 1 + a] = w;
   }
   if (K.want_j) {
     AxisPowers ap;
-    axis_powers(K, a, d, ap);
+    axis_powers_ax<AXL>(K, K.sq_ladder != 0, a, d, ap);
     o[L_PM1] = ap.pm1;
     o[L_PP] = ap.pP;
     o[L_P2PM3] = ap.p2Pm3;
     o[L_P2PM2] = ap.p2Pm2;
     o[L_P2P] = ap.p2P;
-    const double t = K.C[a] - pa;
+    const double t = axv<AXL>(K, AX_C, a) - pa;
     o[L_INV] = 1.0 / (t * t);
   } else {
-    o[L_PM1] = cpow(d, K.Pm1[a]);  // src/Superquadric.cpp:54-56 (normal value only)
+    o[L_PM1] = cpow(d, axv<AXL>(K, AX_PM1, a));  // src/Superquadric.cpp:54-56 (normal value only)
   }
 }
 
@@ -1044,6 +1129,7 @@ __device__ __forceinline__ void cone_rows(const KParams& K, int i, const double*
   }
 }
 
+template <bool AXL>
 __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __restrict__ xr, int k, int a,
                                             const double* __restrict__ Lc, double* __restrict__ Gr,
                                             double* __restrict__ Jr) {
@@ -1062,9 +1148,9 @@ __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __re
       v += gk[3];
       v -= 1.0;
     }
-    const double ej0 = K.EJ[0] * Lc[0 * L_AXIS + L_PM1];
-    const double ej1 = K.EJ[1] * Lc[1 * L_AXIS + L_PM1];
-    const double ej2 = K.EJ[2] * Lc[2 * L_AXIS + L_PM1];
+    const double ej0 = axv<AXL>(K, AX_EJ, 0) * Lc[0 * L_AXIS + L_PM1];
+    const double ej1 = axv<AXL>(K, AX_EJ, 1) * Lc[1 * L_AXIS + L_PM1];
+    const double ej2 = axv<AXL>(K, AX_EJ, 2) * Lc[2 * L_AXIS + L_PM1];
     const double nrm = sqrt((ej0 * ej0 + ej1 * ej1) + ej2 * ej2);
     if (K.want_g) {
       gk[0] = v;
@@ -1086,25 +1172,25 @@ __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __re
   const double p_b = q[3 + b], p_c = q[3 + c];
   double out[3];
   {  // diagonal (a, a)
-    double lead = K.Ka[a];
+    double lead = axv<AXL>(K, AX_KA, a);
 #pragma unroll
     for (int kk = 0; kk < 3; ++kk) {
-      lead = lead * (kk == a ? La[L_PP] : K.Rm2[kk]);
+      lead = lead * (kk == a ? La[L_PP] : axv<AXL>(K, AX_RM2, kk));
       lead = lead * Lc[kk * L_AXIS + L_INV];
     }
-    lead = lead * K.Pm1[a];
+    lead = lead * axv<AXL>(K, AX_PM1, a);
     lead = lead * 1.0;
-    const double Tb = ((K.Rm2[b] * Lb[L_INV]) * K.Psq[b]) * Lb[L_P2P];
-    const double Tc = ((K.Rm2[c] * Lcc[L_INV]) * K.Psq[c]) * Lcc[L_P2P];
-    const double Dg = (K.Kb[a] * La[L_P2P]) * La[L_INV];
+    const double Tb = ((axv<AXL>(K, AX_RM2, b) * Lb[L_INV]) * axv<AXL>(K, AX_PSQ, b)) * Lb[L_P2P];
+    const double Tc = ((axv<AXL>(K, AX_RM2, c) * Lcc[L_INV]) * axv<AXL>(K, AX_PSQ, c)) * Lcc[L_P2P];
+    const double Dg = (axv<AXL>(K, AX_KB, a) * La[L_P2P]) * La[L_INV];
     const double S = (Tb + Tc) + Dg;
     const double p2Pb = Lb[L_P2P], p2Pc = Lcc[L_P2P];
-    const double E = (((((((K.C[b] * K.C[b]) * K.Psq[c]) * p2Pc) * K.Rp2[b] +
-                         (((K.C[c] * K.C[c]) * K.Psq[b]) * p2Pb) * K.Rp2[c]) +
-                        (((p_b * p_b) * K.Psq[c]) * p2Pc) * K.Rp2[b]) +
-                       (((p_c * p_c) * K.Psq[b]) * p2Pb) * K.Rp2[c]) -
-                      ((((K.C[b] * p_b) * K.Psq[c]) * p2Pc) * K.Rp2[b]) * 2.0) -
-                     ((((K.C[c] * p_c) * K.Psq[b]) * p2Pb) * K.Rp2[c]) * 2.0;
+    const double E = (((((((axv<AXL>(K, AX_C, b) * axv<AXL>(K, AX_C, b)) * axv<AXL>(K, AX_PSQ, c)) * p2Pc) * axv<AXL>(K, AX_RP2, b) +
+                         (((axv<AXL>(K, AX_C, c) * axv<AXL>(K, AX_C, c)) * axv<AXL>(K, AX_PSQ, b)) * p2Pb) * axv<AXL>(K, AX_RP2, c)) +
+                        (((p_b * p_b) * axv<AXL>(K, AX_PSQ, c)) * p2Pc) * axv<AXL>(K, AX_RP2, b)) +
+                       (((p_c * p_c) * axv<AXL>(K, AX_PSQ, b)) * p2Pb) * axv<AXL>(K, AX_RP2, c)) -
+                      ((((axv<AXL>(K, AX_C, b) * p_b) * axv<AXL>(K, AX_PSQ, c)) * p2Pc) * axv<AXL>(K, AX_RP2, b)) * 2.0) -
+                     ((((axv<AXL>(K, AX_C, c) * p_c) * axv<AXL>(K, AX_PSQ, b)) * p2Pb) * axv<AXL>(K, AX_RP2, c)) * 2.0;
     out[a] = lead / pow_three_halves(S) * E;
   }
 #pragma unroll
@@ -1112,22 +1198,22 @@ __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __re
     if (bb == a) continue;
     const int oo = 3 - a - bb;
     const double* Lbb = Lc + bb * L_AXIS;
-    double lead = K.Ka[a];
+    double lead = axv<AXL>(K, AX_KA, a);
     if (a < bb) {  // src/Superquadric.cpp:109, 119, 163
       lead = lead * La[L_PM1];
-      lead = lead * K.Psq[bb];
+      lead = lead * axv<AXL>(K, AX_PSQ, bb);
       lead = lead * Lbb[L_P2PM3];
-      lead = lead * K.P2m2[bb];
+      lead = lead * axv<AXL>(K, AX_P2M2, bb);
     } else {       // src/Superquadric.cpp:129, 173, 183
-      lead = lead * K.Psq[bb];
+      lead = lead * axv<AXL>(K, AX_PSQ, bb);
       lead = lead * Lbb[L_P2PM3];
-      lead = lead * K.P2m2[bb];
+      lead = lead * axv<AXL>(K, AX_P2M2, bb);
       lead = lead * La[L_PM1];
     }
-    lead = lead * K.Rm2[bb];
+    lead = lead * axv<AXL>(K, AX_RM2, bb);
     lead = lead * 1.0;
-    const double S = (K.Kb[oo] * Lc[oo * L_AXIS + L_P2PM2] + K.Kb[a] * La[L_P2PM2]) +
-                     (K.Psq[bb] * Lbb[L_P2PM2]) * K.Rm2[bb];
+    const double S = (axv<AXL>(K, AX_KB, oo) * Lc[oo * L_AXIS + L_P2PM2] + axv<AXL>(K, AX_KB, a) * La[L_P2PM2]) +
+                     (axv<AXL>(K, AX_PSQ, bb) * Lbb[L_P2PM2]) * axv<AXL>(K, AX_RM2, bb);
     out[bb] = lead / pow_three_halves(S) * (-1.0 / 2.0);
   }
   double* row = jk + 3 + (fold ? 3 : 4) * a;
@@ -1135,7 +1221,11 @@ __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __re
   if (!fold) row[3] = 1.0;
 }
 
-template <int ENVK, int WG, bool NT>
+// JD: the Jacobian items write their entries straight to the output records (K.jdirect); a
+// compile-time choice, so that every Jacobian store is a plain LDS or a plain global store: through a
+// generic pointer they were FLAT stores, which count on lgkmcnt too — every later LDS wait of the
+// thread then waited for its in-flight global stores.
+template <int ENVK, int WG, bool NT, bool JD>
 __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int64_t batch,
                                                             const double* __restrict__ x,
                                                             const double* __restrict__ mass,
@@ -1158,7 +1248,7 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
   double* X = smem;
   double* Gt = smem + K.offG;
   // the Jacobian rows: the LDS tile image, or (jdirect) the output records themselves
-  double* Jt = K.jdirect ? jac_out + b0 * K.nnz : smem + K.offJ;
+  double* Jt = JD ? jac_out + b0 * K.nnz : smem + K.offJ;
   double* Dt = smem + K.offD;
   double* L = smem + K.offL;                                    // [T][LR] (SQ / mixed)
   int* lists = reinterpret_cast<int*>(smem + K.offI);          // sq_list[64], gr_list[64], n_sq
@@ -1224,12 +1314,14 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
         const int a = it / per_axis, kj = it - a * per_axis;
         const int k = kj / n_sq, j = kj - k * n_sq;
         const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
-        sq_axis_item(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m);
+        sq_axis_item<ENVK == CPL_ENV_MIXED>(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m);
       } else {
         other_item(it - r_ax);
       }
     }
-    if (HAS_SQ && n_sq > 0 && wgj) __syncthreads();
+    // LDS-only barriers from here on: the phases exchange LDS data only, and a __syncthreads would
+    // first wait for every global store the items issued (f, and with jdirect the Jacobian rows)
+    if (HAS_SQ && n_sq > 0 && wgj) lds_barrier();
     const int r_rows = r_ax;
     const int items2 = r_rows + (OTHERS_FIRST ? 0 : r_oth);
     for (int it = tid; it < items2; it += WG) {
@@ -1237,27 +1329,27 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
         const int a = it / per_axis, kj = it - a * per_axis;
         const int k = kj / n_sq, j = kj - k * n_sq;
         const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
-        sq_row_item(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m, Jt + r * nnz);
+        sq_row_item<ENVK == CPL_ENV_MIXED>(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m, Jt + r * nnz);
       } else {
         other_item(it - r_rows);
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
   if (K.ablate != 2 && K.soa) {
     if (K.want_g) copy_out_soa<WG, NT>(g_out + b0, batch, Gt, m, valid, tid);
     if (K.want_j) copy_out_soa<WG, NT>(jac_out + b0, batch, Jt, nnz, valid, tid);
     if (K.want_grad) copy_out_soa<WG, NT>(grad_out + b0, batch, Dt, n, valid, tid);
   } else if (K.ablate != 2) {
     if (K.want_g) copy_out<WG, NT>(g_out + b0 * m, Gt, valid * m, tid);
-    if (K.want_j && !K.jdirect) copy_out<WG, NT>(jac_out + b0 * nnz, Jt, valid * nnz, tid);
+    if (K.want_j && !JD) copy_out<WG, NT>(jac_out + b0 * nnz, Jt, valid * nnz, tid);
     if (K.want_grad) copy_out<WG, NT>(grad_out + b0 * n, Dt, valid * n, tid);
   }
   if (K.want_norms) {
     NormAcc acc;
     acc.init(tid, WG, m);
     acc.add_tile(Gt, valid * m, tid, WG, m);
-    partial_norms(acc, norms_ws + NORM_HDR);
+    partial_norms_waves(acc, norms_ws + NORM_HDR);
   }
 }
 
@@ -1445,7 +1537,7 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
           const int a = e / per_axis, kj = e - a * per_axis;
           const int k = kj / n_sq, j = kj - k * n_sq;
           const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
-          sq_axis_item(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m);
+          sq_axis_item<ENVK == CPL_ENV_MIXED>(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m);
           continue;
         }
         e -= r_ax;
@@ -1478,7 +1570,7 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
             const int a = it / per_axis, kj = it - a * per_axis;
             const int k = kj / n_sq, j = kj - k * n_sq;
             const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
-            sq_row_item(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m, Jt + r * nnz);
+            sq_row_item<ENVK == CPL_ENV_MIXED>(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m, Jt + r * nnz);
           }
         }
       }
@@ -2070,29 +2162,31 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
     // 4.23 -> 3.47 ms, interleaved A/B in one process (profiles/r3/abk_mixed16.jsonl); the
     // Superquadric records are small enough that the staged copy-out wins there (0.32 vs 0.42 ms)
     const bool jd = g_variant == VAR_TILE_JD || (g_variant == VAR_AUTO && K.env_kind == CPL_ENV_MIXED);
-    K.jdirect = (jd && d_jac && !K.soa) ? 1 : 0;
+    K.jdirect = (jd && d_jac && !K.soa && g_wg == 256) ? 1 : 0;
     st = plan_tile(K, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr, 64, jd && d_jac);
     const int wg = g_wg;
     if (st) return st;
     K.ablate = g_ablate;
     const size_t lds = sizeof(double) * (size_t)(K.offI + 72);
     const unsigned grid = (unsigned)((batch + K.T - 1) / K.T);
-    if (K.want_norms && (st = norm_workspace(stream, grid, &ws))) return st;
+    const size_t nparts = (size_t)grid * (wg / 64);  // one partial pair per wave
+    if (K.want_norms && (st = norm_workspace(stream, nparts, &ws))) return st;
     using KernT = void (*)(const KParams, int64_t, const double*, const double*, const uint8_t*, double*, double*,
                            double*, double*, double*);
 #define CPL_TILE_KERNELS(E) \
-  {cpl_eval_tile_kernel<E, 128, false>, cpl_eval_tile_kernel<E, 128, true>, cpl_eval_tile_kernel<E, 256, false>, \
-   cpl_eval_tile_kernel<E, 256, true>}
-    static const KernT table[4][4] = {CPL_TILE_KERNELS(CPL_ENV_NONE), CPL_TILE_KERNELS(CPL_ENV_GROUND),
+  {cpl_eval_tile_kernel<E, 128, false, false>, cpl_eval_tile_kernel<E, 128, true, false>,        \
+   cpl_eval_tile_kernel<E, 256, false, false>, cpl_eval_tile_kernel<E, 256, true, false>,        \
+   cpl_eval_tile_kernel<E, 256, false, true>, cpl_eval_tile_kernel<E, 256, true, true>}
+    static const KernT table[4][6] = {CPL_TILE_KERNELS(CPL_ENV_NONE), CPL_TILE_KERNELS(CPL_ENV_GROUND),
                                       CPL_TILE_KERNELS(CPL_ENV_SUPERQUADRIC), CPL_TILE_KERNELS(CPL_ENV_MIXED)};
 #undef CPL_TILE_KERNELS
-    const KernT kern = table[K.env_kind][(wg == 256 ? 2 : 0) + (g_nt ? 1 : 0)];
+    const KernT kern = table[K.env_kind][(K.jdirect ? 4 : (wg == 256 ? 2 : 0)) + (g_nt ? 1 : 0)];
     hipLaunchKernelGGL(kern, dim3(grid), dim3(wg), lds, stream, K, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f,
                        d_grad, ws);
     if (K.want_norms) {  // per-tile partials -> final pair
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return hip_fail(e, "cpl_eval_tile_kernel launch");
-      if (finish) launch_residual_final((int)grid, ws + NORM_HDR, d_norms, stream);
+      if (finish) launch_residual_final((int)nparts, ws + NORM_HDR, d_norms, stream);
     }
   }
   hipError_t e = hipGetLastError();
@@ -2157,12 +2251,12 @@ __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, c
       // f and g of the trial point: the eval work items of one instance
       if (ENVK != CPL_ENV_NONE && ENVK != CPL_ENV_GROUND && sq) {
         for (int it = lane; it < 3 * N + 2; it += 64) {
-          if (it < 3 * N) sq_axis_item(K, X, it / 3, it % 3, L + (it / 3) * SQ_L, G);
+          if (it < 3 * N) sq_axis_item<ENVK == CPL_ENV_MIXED>(K, X, it / 3, it % 3, L + (it / 3) * SQ_L, G);
           else if (it == 3 * N) statics_values_item(K, X, m_i, G, G);
           else cost_item(K, X, &s_f, nullptr);
         }
         __syncthreads();
-        for (int it = lane; it < 3 * N; it += 64) sq_row_item(K, X, it / 3, it % 3, L + (it / 3) * SQ_L, G, G);
+        for (int it = lane; it < 3 * N; it += 64) sq_row_item<ENVK == CPL_ENV_MIXED>(K, X, it / 3, it % 3, L + (it / 3) * SQ_L, G, G);
       } else {
         for (int it = lane; it < N + 2; it += 64) {
           if (it < N)

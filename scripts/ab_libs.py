@@ -26,6 +26,7 @@ ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--libs", default="centroidalplanner_amd/libcpl_mi355x.so,build/libcpl_old.so")
 ap.add_argument("--tuning", default="", help="variant:lds_kb:wg:nt passed to every library's cpl_set_tuning")
+ap.add_argument("--no-norms", action="store_true", help="time the eval kernel without the fused residual norms")
 args = ap.parse_args()
 
 libs = {}
@@ -56,7 +57,8 @@ for _ in range(args.rounds):
     for k, lib in libs.items():
         ms = ctypes.c_double()
         _abi.check(lib.cpl_time_eval_batch(ctypes.byref(prob.desc()), B, p(xt), p(mt), p(tt), p(out["g"]), p(out["jac"]),
-                                           None, None, p(out["norms"]), ctypes.c_void_p(stream.cuda_stream), args.reps,
+                                           None, None, None if args.no_norms else p(out["norms"]),
+                                           ctypes.c_void_p(stream.cuda_stream), args.reps,
                                            ctypes.byref(ms)))
         times[k].append(ms.value)
 # every library's outputs on the same inputs, compared bit for bit with the first one's
@@ -74,5 +76,6 @@ for k, lib in libs.items():
 bpi, m = algorithmic_bytes(cfg.n_contacts, cfg.env)
 for k, ts in times.items():
     med = statistics.median(ts)
-    print(json.dumps({"config": args.config, "batch": B, "lib": k, "tuning": args.tuning, "median_ms": med, "min_ms": min(ts),
+    print(json.dumps({"config": args.config, "batch": B, "lib": k, "tuning": args.tuning, "norms": not args.no_norms,
+                      "median_ms": med, "min_ms": min(ts),
                       "GBps": bpi * B / (med * 1e-3) / 1e9}), flush=True)
