@@ -1308,7 +1308,10 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
       e -= r_st;
       cost_item(K, X + e * n, f_out ? f_out + b0 + e : nullptr, Dt + e * n);
     };
-    const int items1 = r_ax + (OTHERS_FIRST ? r_oth : 0);
+    // mixed: the statics / cost items join phase 1 (beside the Superquadric ladders), the Ground
+    // contacts phase 2 (beside the Superquadric rows) — with 8-instance tiles both phases then fit
+    // one pass of the workgroup (232 and 256 items at the 1:1 mix)
+    const int items1 = r_ax + (OTHERS_FIRST ? r_oth : r_oth - r_gr);
     for (int it = tid; it < items1; it += WG) {
       if (HAS_SQ && it < r_ax) {
         const int a = it / per_axis, kj = it - a * per_axis;
@@ -1316,14 +1319,14 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
         const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
         sq_axis_item<ENVK == CPL_ENV_MIXED>(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m);
       } else {
-        other_item(it - r_ax);
+        other_item(it - r_ax + (OTHERS_FIRST ? 0 : r_gr));
       }
     }
     // LDS-only barriers from here on: the phases exchange LDS data only, and a __syncthreads would
     // first wait for every global store the items issued (f, and with jdirect the Jacobian rows)
     if (HAS_SQ && n_sq > 0 && wgj) lds_barrier();
     const int r_rows = r_ax;
-    const int items2 = r_rows + (OTHERS_FIRST ? 0 : r_oth);
+    const int items2 = r_rows + (OTHERS_FIRST ? 0 : r_gr);
     for (int it = tid; it < items2; it += WG) {
       if (HAS_SQ && it < r_rows) {
         const int a = it / per_axis, kj = it - a * per_axis;
