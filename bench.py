@@ -28,7 +28,9 @@ Rank 0 prints one JSON line.  Fields beyond the driver contract:
   configs2_sq8  BASELINE.json configs[2] (262,144 x 8 Superquadric): kernel time, HBM fraction, VALU
                 roofline (PMC), checker sample
   configs4_solve5_lbfgs  BASELINE.json configs[4] (8,192 concurrent solves) in the reference's Hessian
-                mode (IPOPT's L-BFGS): solves/s, iterations, a small CPU sample of the same solver
+                mode (IPOPT's L-BFGS): solves/s, iterations, a small CPU sample of the same solver;
+                .single_solve: one instance solved alone (CentroidalPlanner::Solve()'s batch of one):
+                GPU ms per solve beside the host restatement on one core
 """
 from __future__ import annotations
 
@@ -498,6 +500,57 @@ def side_solve5(dev, cpu_sample=64):
             "cpu_baseline": cpu}
 
 
+def side_single_solve(dev, reps=7):
+    """The facade's primary call, CentroidalPlanner::Solve() (src/CentroidalPlanner.cpp:22-34): ONE
+    instance of the solve workload solved in IFOPT's limited-memory mode by the native engine (B = 1:
+    every kernel of an iteration is launch latency), median of `reps` solves after a warm-up, beside the
+    same solver over the oracle's callbacks on one CPU core (the host restatement, batch_ipm.py)."""
+    import statistics
+
+    import torch
+
+    from centroidalplanner_amd.batch_ipm import batch_ipm_solve
+    from centroidalplanner_amd.workload import solve_inputs, solve_problem
+
+    prob = solve_problem().GetCplProblem()
+    X0, mass = solve_inputs(prob, 1, seed=0xC910 + 5)
+    X0t, mt = torch.tensor(X0, device=dev), torch.tensor(mass, device=dev)
+    opts = dict(max_iter=1000, hessian="limited-memory")
+    r = batch_ipm_solve(prob, X0t, mt, **opts)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        r = batch_ipm_solve(prob, X0t, mt, **opts)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    ms = statistics.median(ts) * 1e3
+    res = {"workload": "one instance of the solve workload (4-contact Ground), IFOPT's limited-memory Hessian",
+           "gpu_ms_per_solve": ms, "iterations": int(r.iterations[0].item()), "status": int(r.status[0].item()),
+           "us_per_iteration": ms * 1e3 / max(1, int(r.iterations_run))}
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from test_batch_solve import OracleBatchEvaluator
+
+        nt = torch.get_num_threads()
+        torch.set_num_threads(1)
+        try:
+            tc = time.perf_counter()
+            rc = batch_ipm_solve(prob, torch.tensor(X0), torch.tensor(mass), evaluator=OracleBatchEvaluator(prob, nthreads=1),
+                                 **opts)
+            tc = time.perf_counter() - tc
+        finally:
+            torch.set_num_threads(nt)
+        res["cpu_baseline"] = {"value": tc * 1e3, "unit": "ms per solve", "cores": 1, "kind": "port",
+                               "sample": f"the same instance: the host restatement of the solver (batch_ipm.py, CPU "
+                                         f"torch) over the oracle's callbacks, one thread ({int(rc.iterations[0])} "
+                                         f"iterations, status {int(rc.status[0])})"}
+    except Exception as e:  # noqa: BLE001
+        res["cpu_baseline"] = {"error": str(e)}
+    return res
+
+
 # ------------------------------------------------------------------------------------------
 def solve_bench(args):
     """BASELINE.json configs[4]: the full solve loop, 8,192 concurrent 4-contact Ground instances on
@@ -778,6 +831,10 @@ def main():
             solve5 = side_solve5(dev, 0 if args.no_cpu else 64)
         except Exception as e:  # noqa: BLE001
             solve5 = {"error": str(e)}
+        try:
+            solve5["single_solve"] = side_single_solve(dev)
+        except Exception as e:  # noqa: BLE001
+            solve5["single_solve"] = {"error": str(e)}
 
     if rank == 0:
         res = {
