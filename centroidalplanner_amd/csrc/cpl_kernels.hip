@@ -97,6 +97,7 @@ struct KParams {
   int32_t soa;               // outputs entry-major ([m][B], [nnz][B], [n][B]) instead of instance-major
   int32_t jdirect;           // tile kernel: the Jacobian items write their entries straight to the
                              // output records instead of the LDS tile image (smaller tiles' LDS)
+  int32_t offA;              // (jdirect) doubles offset of the statics CoM-pair scratch [T][6]
 };
 static_assert(sizeof(KParams) < 4096, "kernel parameters must fit the kernarg segment");
 
@@ -958,8 +959,20 @@ __device__ __forceinline__ void contact_item(const KParams& K, const double* __r
 // CentroidalStatics::GetValues (src/Constraints/CentroidalStatics.cpp:37-61) and Jacobian rows 0-2
 // (the I3 of every F_i, :93-95)
 __device__ __forceinline__ void statics_values_item(const KParams& K, const double* __restrict__ xr, double m_i,
-                                                    double* __restrict__ Gr, double* __restrict__ Jr) {
+                                                    double* __restrict__ Gr, double* __restrict__ Jr,
+                                                    bool with_j = true, double* __restrict__ com6 = nullptr) {
   const int N = K.N;
+  if (com6) {  // the torque rows' CoM pairs (statics_row_item's a1, a2 for rows 3, 4, 5), map order
+    double a[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int k = 0; k < N; ++k) {
+      const double* F = xr + 3 + 9 * s_ct.map_order[k];
+      a[0] -= -(-1.0) * F[2]; a[1] -= -(1.0) * F[1];   // row 3: (e1, s1) = (2, -), (e2, s2) = (1, +)
+      a[2] -= -(1.0) * F[2];  a[3] -= -(-1.0) * F[0];  // row 4: (2, +), (0, -)
+      a[4] -= -(-1.0) * F[1]; a[5] -= -(1.0) * F[0];   // row 5: (1, -), (0, +)
+    }
+#pragma unroll
+    for (int t = 0; t < 6; ++t) com6[t] = a[t];
+  }
   if (K.want_g) {
     const double c0 = xr[0], c1 = xr[1], c2 = xr[2];
     double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0, v4 = 0.0, v5 = 0.0;
@@ -977,8 +990,43 @@ __device__ __forceinline__ void statics_values_item(const KParams& K, const doub
     v0 += m_i * K.gravity[0]; v1 += m_i * K.gravity[1]; v2 += m_i * K.gravity[2];
     Gr[0] = v0; Gr[1] = v1; Gr[2] = v2; Gr[3] = v3; Gr[4] = v4; Gr[5] = v5;
   }
-  if (K.want_j && K.fold == FOLD_NONE)  // folded layouts skip the constant I3 blocks
+  if (with_j && K.want_j && K.fold == FOLD_NONE)  // folded layouts skip the constant I3 blocks
     for (int e = 0; e < 3 * N; ++e) Jr[e] = 1.0;
+}
+
+// The statics Jacobian rows of one instance (statics_values_item's I3 blocks and statics_row_item's
+// three torque rows), entry by entry with the lanes along the record: every value is the expression
+// the two items compute (the CoM pairs' sums in map order), but consecutive lanes write consecutive
+// doubles — where the records are written straight to HBM (tile kernel JD) one thread per row issued
+// 50-70 stores to 50-70 different lines per wave instruction.
+__device__ __forceinline__ void statics_rows_coop(const KParams& K, const double* __restrict__ xr,
+                                                  const double* __restrict__ com6, double* __restrict__ Jr, int tid,
+                                                  int nthreads) {
+  const int N = K.N;
+  const int RL = 2 + 4 * N;
+  const int I3 = K.fold == FOLD_NONE ? 3 * N : 0;
+  const int SJ = I3 + 3 * RL;
+  for (int e = tid; e < SJ; e += nthreads) {
+    double v = 1.0;
+    if (e >= I3) {
+      int w = e - I3;
+      const int q = w >= 2 * RL ? 2 : (w >= RL ? 1 : 0);
+      w -= q * RL;
+      const int e1 = q == 2 ? 1 : 2;
+      const int e2 = q == 0 ? 1 : 0;
+      const double s1 = q == 1 ? 1.0 : -1.0;
+      const double s2 = q == 1 ? -1.0 : 1.0;
+      if (w < 2) {  // the CoM pair (summed by statics_values_item in map order)
+        v = com6[2 * q + w];
+      } else {
+        const int i = (w - 2) >> 2, c = (w - 2) & 3;
+        const double* F = xr + 3 + 9 * i;
+        const double* p = F + 3;
+        v = c == 0 ? s1 * (p[e1] - xr[e1]) : c == 1 ? s2 * (p[e2] - xr[e2]) : c == 2 ? -s1 * F[e1] : -s2 * F[e2];
+      }
+    }
+    Jr[e] = v;
+  }
 }
 
 // Torque row 3+q of CentroidalStatics::FillJacobianBlock (src/Constraints/CentroidalStatics.cpp:75-137):
@@ -1285,7 +1333,8 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
   if (compute) {
     const int r_ax = (HAS_SQ && wgj) ? 3 * N * n_sq : 0;
     const int r_gr = (ENVK != CPL_ENV_SUPERQUADRIC && wgj) ? N * n_gr : 0;
-    const int r_st = wgj ? 4 * valid : 0;
+    const int r_st = wgj ? (JD ? 1 : 4) * valid : 0;  // (JD: the statics J rows by statics_rows_coop)
+    double* com6 = smem + K.offA;                        // (JD) [T][6]
     const int r_co = K.cost_seg >= 0 ? valid : 0;
     const int r_oth = r_gr + r_st + r_co;
     const int per_axis = N * n_sq;
@@ -1301,7 +1350,9 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
       if (e < r_st) {
         const int r = e % valid, sg = e / valid;
         const double* xr = X + r * n;
-        if (sg == 0) statics_values_item(K, xr, mass ? mass[b0 + r] : mass_def, Gt + r * m, Jt + r * nnz);
+        if (sg == 0)
+          statics_values_item(K, xr, mass ? mass[b0 + r] : mass_def, Gt + r * m, Jt + r * nnz, !JD,
+                              JD && K.want_j ? com6 + 6 * r : nullptr);
         else if (K.want_j) statics_row_item(K, xr, sg - 1, Jt + r * nnz);
         return;
       }
@@ -1336,6 +1387,10 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
       } else {
         other_item(it - r_rows);
       }
+    }
+    if (JD && K.want_j) {  // the statics Jacobian rows, lanes along each record
+      lds_barrier();  // (the CoM pairs of the values items)
+      for (int r = 0; r < valid; ++r) statics_rows_coop(K, X + r * n, com6 + 6 * r, Jt + r * nnz, tid, WG);
     }
   }
   lds_barrier();
@@ -1945,7 +2000,7 @@ static int32_t plan_tile(KParams& K, bool g, bool j, bool f, bool grad, int t_ma
   const bool sq = K.env_kind == CPL_ENV_SUPERQUADRIC || K.env_kind == CPL_ENV_MIXED;
   K.LR = K.N * SQ_L + 1;  // odd instance stride of the SQ scratch: conflict-free LDS banks
   const size_t per = sizeof(double) * (size_t)(K.n + (g ? K.m : 0) + (j && !K.jdirect ? K.nnz : 0) +
-                                               (grad ? K.n : 0) + (sq ? K.LR : 0));
+                                               (grad ? K.n : 0) + (sq ? K.LR : 0) + (j && K.jdirect ? 6 : 0));
   const size_t per_t = size_without_j ? per - sizeof(double) * (size_t)(j && !K.jdirect ? K.nnz : 0) : per;
   const size_t fixed = sizeof(double) * 72 + sizeof(CTab);  // index lists + parameter table
   int T = 64, logT = 6;
@@ -1962,7 +2017,8 @@ static int32_t plan_tile(KParams& K, bool g, bool j, bool f, bool grad, int t_ma
   K.offJ = K.offG + (g ? T * K.m : 0);
   K.offD = K.offJ + (j && !K.jdirect ? T * K.nnz : 0);
   K.offL = K.offD + (grad ? T * K.n : 0);
-  K.offI = K.offL + (sq ? T * K.LR : 0);
+  K.offA = K.offL + (sq ? T * K.LR : 0);
+  K.offI = K.offA + (j && K.jdirect ? 6 * T : 0);
   K.offI = (K.offI + 1) & ~1;
   return CPL_OK;
 }
