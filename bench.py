@@ -87,6 +87,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--max-ls", type=int, default=40, help="solve5: backtracking trials per iteration at most")
     ap.add_argument("--max-soc", type=int, default=4, help="solve5: second-order corrections on the first trial")
+    ap.add_argument("--ls-kernel", type=int, default=2, help="solve5: the engine's ls_kernel option (0 / 1 / 2)")
     ap.add_argument("--hessian", default="exact", choices=["exact", "limited-memory"],
                     help="solve5: exact Lagrangian Hessian (analytic kernel) or IFOPT's limited-memory default")
     ap.add_argument("--cpu-sample", type=int, default=512, help="solve5: instances in the CPU baseline's sample")
@@ -436,7 +437,8 @@ def side_sq8(dev, stream, valu_counters, check_sample=1024):
     return res
 
 
-def run_solve5(dev, batch, hessian, steps, warm, max_ls, max_soc, cpu_sample, rank=0, world=1, barrier=None):
+def run_solve5(dev, batch, hessian, steps, warm, max_ls, max_soc, cpu_sample, rank=0, world=1, barrier=None,
+               ls_kernel=2):
     """BASELINE.json configs[4]: `steps` complete batched solves of `batch` TestBasic ground instances
     (centroidalplanner_amd/batch_ipm.py -> the native engine), after `warm` untimed ones.  Returns
     (dt seconds for the timed solves, the last result, the CPU leg or None)."""
@@ -448,7 +450,8 @@ def run_solve5(dev, batch, hessian, steps, warm, max_ls, max_soc, cpu_sample, ra
     prob = solve_problem().GetCplProblem()
     X0, mass = solve_inputs(prob, batch, seed=0xC910 + 5 + 7919 * rank)
     X0t, mt = torch.tensor(X0, device=dev), torch.tensor(mass, device=dev)
-    opts = dict(max_iter=300 if hessian == "exact" else 1000, max_ls=max_ls, max_soc=max_soc, hessian=hessian)
+    opts = dict(max_iter=300 if hessian == "exact" else 1000, max_ls=max_ls, max_soc=max_soc, hessian=hessian,
+                ls_kernel=ls_kernel)
     for _ in range(warm):
         batch_ipm_solve(prob, X0t, mt, **opts)
     torch.cuda.synchronize()
@@ -580,7 +583,7 @@ def solve_bench(args):
     warm = 1 if args.warmup > 0 else 0
     dt, r, cpu = run_solve5(dev, B, args.hessian, steps, warm, args.max_ls, args.max_soc,
                             0 if args.no_cpu else args.cpu_sample, rank, world,
-                            barrier=dist.barrier if world > 1 else None)
+                            barrier=dist.barrier if world > 1 else None, ls_kernel=args.ls_kernel)
     if world > 1:
         tdt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tdt, op=dist.ReduceOp.MAX)

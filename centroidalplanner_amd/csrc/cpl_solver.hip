@@ -524,12 +524,21 @@ __global__ __launch_bounds__(256) void k_soft_judge(
 // moved = an accepted one; a failed search leaves the soft phase.  IPOPT calls no restoration phase
 // at an acceptable point (BacktrackingLineSearch: "Restoration phase called at acceptable point" ->
 // STOP_AT_ACCEPTABLE_POINT): an instance whose search failed there ends with status acceptable.
-__global__ void k_fail(int64_t B, const uint8_t* __restrict__ act, const double* __restrict__ st_alpha,
-                       const double* __restrict__ err0, double acc_tol, uint8_t* __restrict__ failed,
-                       uint8_t* __restrict__ moved, uint8_t* __restrict__ in_soft, int32_t* __restrict__ soft_cnt,
-                       int64_t* __restrict__ status, uint8_t* __restrict__ active) {
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+// ... in the same launch as the accepted points' X = unpack(st_w) (an element per thread; the first
+// element of each instance also does that instance's bookkeeping — which does not touch st_w)
+__global__ void k_fail_unpack(int64_t total, int n, int nw, const int32_t* __restrict__ freepos,
+                              const double* __restrict__ Xbase, const double* __restrict__ st_w, double* __restrict__ X,
+                              const uint8_t* __restrict__ act, const double* __restrict__ st_alpha,
+                              const double* __restrict__ err0, double acc_tol, uint8_t* __restrict__ failed,
+                              uint8_t* __restrict__ moved, uint8_t* __restrict__ in_soft, int32_t* __restrict__ soft_cnt,
+                              int64_t* __restrict__ status, uint8_t* __restrict__ active) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int64_t b = e / n;
+  const int j = (int)(e - b * n);
+  const int k = freepos[j];
+  X[e] = k >= 0 ? st_w[b * nw + k] : Xbase[e];
+  if (j != 0) return;
   const bool a = act[b] != 0;
   bool f = a && !(st_alpha[b] > 0.0);
   if (f && err0[b] <= acc_tol) {
@@ -570,7 +579,8 @@ __global__ __launch_bounds__(256) void k_lbfgs(int64_t B, int m, int nf, int nw,
                                                const double* __restrict__ w_old, const double* __restrict__ w_new,
                                                const double* __restrict__ y, const double* __restrict__ dy,
                                                const double* __restrict__ alpha, const double* __restrict__ gw_old,
-                                               const double* __restrict__ J_old, const double* __restrict__ gw_new,
+                                               const double* __restrict__ J_old, const double* __restrict__ grad_new,
+                                               const int32_t* __restrict__ free_idx, int n,
                                                const double* __restrict__ J_new, double* __restrict__ lm_s,
                                                double* __restrict__ lm_y, uint8_t* __restrict__ lm_cnt,
                                                uint8_t* __restrict__ lm_skip, const uint8_t* __restrict__ failed,
@@ -622,7 +632,9 @@ __global__ __launch_bounds__(256) void k_lbfgs(int64_t B, int m, int nf, int nw,
         jo += pjo[q][k2];
       }
       Ps[last][k2] = w_new[b * nw + k2] - w_old[b * nw + k2];
-      Py[last][k2] = (gw_new[b * nw + k2] + jn) - (gw_old[b * nw + k2] + jo);
+      // grad_w f at the new point: its free components (k_prep's gather), 0 without a cost (grad_new NULL)
+      const double gn = grad_new ? grad_new[b * n + free_idx[k2]] : 0.0;
+      Py[last][k2] = (gn + jn) - (gw_old[b * nw + k2] + jo);
       for (int j = 0; j < last; ++j) {
         Ps[j][k2] = gs[(j + shift) * nf + k2];
         Py[j][k2] = gy[(j + shift) * nf + k2];
@@ -740,6 +752,25 @@ __global__ __launch_bounds__(256) void k_lbfgs(int64_t B, int m, int nf, int nw,
 // system) until the original infeasibility falls to kappa_resto of its value at the start and the
 // point is acceptable to the original filter and to the iterate where the phase began.
 
+// The accepted point's rows [f | grad (n) | g (m) | J (nnz_rec)] into the iterate's (k_accept_rows),
+// entry q of instance b; k_resto_enter does it for the instances that moved (moved != NULL) in its
+// launch — one launch fewer per iteration.
+struct AcceptRows {
+  const uint8_t* moved;
+  int n, m, nnz;
+  const double *f_n, *grad_n, *g_n, *J_n;
+  double *f, *grad, *g, *J;
+};
+__device__ __forceinline__ void accept_row_entry(const AcceptRows& a, int64_t b, int64_t q) {
+  if (q == 0) { a.f[b] = a.f_n[b]; return; }
+  q -= 1;
+  if (q < a.n) { a.grad[b * a.n + q] = a.grad_n[b * a.n + q]; return; }
+  q -= a.n;
+  if (q < a.m) { a.g[b * a.m + q] = a.g_n[b * a.m + q]; return; }
+  q -= a.m;
+  a.J[b * a.nnz + q] = a.J_n[b * a.nnz + q];
+}
+
 // Entry (RestoIterateInitializer): x_R = w; mu_R = max(mu, |c|inf); p, n from the closed form of the
 // barrier subproblem at fixed x (p - n = c, both positive); their bound multipliers mu_R / p,
 // mu_R / n; the x-bound multipliers min(rho, z); the original filter augmented with the current
@@ -758,10 +789,16 @@ __global__ __launch_bounds__(256) void k_resto_enter(
     int64_t* __restrict__ fcR, double* __restrict__ thmaxR, double* __restrict__ thminR,
     double* __restrict__ th_o0, double* __restrict__ ph_o0, double* __restrict__ dwlR, uint8_t* __restrict__ lm_cnt,
     uint8_t* __restrict__ lm_skip, double* __restrict__ Hq, int64_t lmc, double* __restrict__ Mw,
-    double* __restrict__ r1, double* __restrict__ r2, double* __restrict__ Dinv) {
+    double* __restrict__ r1, double* __restrict__ r2, double* __restrict__ Dinv, const AcceptRows ar) {
   const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
-  if (b >= B || !failed[b]) return;
+  if (b >= B) return;
   const int lane = threadIdx.x & 63;
+  if (ar.moved && ar.moved[b]) {  // (k_accept_rows for the instances that moved, in the same launch)
+    const int64_t L = 1 + ar.n + ar.m + ar.nnz;
+    for (int64_t q = lane; q < L; q += 64) accept_row_entry(ar, b, q);
+    return;
+  }
+  if (!failed[b]) return;
   const double mub = mu[b];
   double cinf = 0.0;
   for (int r = lane; r < m; r += 64) cinf = fmax(cinf, fabs(c[b * m + r]));
@@ -1544,7 +1581,7 @@ struct cpl_solver {
   double *wR, *pR, *nR, *zp, *zn, *zLR, *zUR, *muR, *ftR, *fpR, *th_o0, *ph_o0, *dwlR, *thmaxR, *thminR;
   int64_t* fcR;
   // iteration temporaries
-  double *A, *gradw, *gradw_new, *c, *err0, *base, *mu_o, *ft, *fp, *tau, *X, *H, *M, *Kqd, *r1, *r2, *gphi,
+  double *A, *gradw, *c, *err0, *base, *mu_o, *ft, *fp, *tau, *X, *H, *M, *Kqd, *r1, *r2, *gphi,
       *mr_diag, *theta_k, *phi_k, *dw, *dy, *delta_w, *delta_c, *dzL, *dzU, *a_max, *a_z, *gd, *ws, *a_min, *a_soft,
       *cs_tmp, *scr1, *scr2;
   int64_t* fc;
@@ -1749,7 +1786,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
       LAUNCHED("k_ls_setup");
       // the whole search in one launch (first trial, its corrections, the backtracking), or the
       // first trial step by step and the remaining trials in one launch
-      const bool fused = o.ls_kernel == 2 || (o.ls_kernel == 1 && B <= FUSE_ROWS);
+      const bool fused = o.ls_kernel == 2 || (o.ls_kernel == 1 && B <= FUSE_ROWS);  // (2: the default)
       if (!(fused && S->ls_fusable)) CK(first_trial());
       if (fused && S->ls_fusable) {
         LsBacktrackArgs la;
@@ -1811,20 +1848,15 @@ int32_t step_phase(cpl_solver* S, int phase) {
     }
     case P_ACCEPT:
     case P_ACCEPT_NR: {
-      hipLaunchKernelGGL(k_fail, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->act, S->st_alpha, S->err0,
-                         o.acceptable_tol, S->failed, S->moved, S->in_soft, S->soft_cnt, S->status, S->active);
-      LAUNCHED("k_fail");
-      // the accepted points with their derivatives: one full evaluation
-      hipLaunchKernelGGL(k_unpack, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, nw, S->freepos, S->Xbase,
-                         S->st_w, nullptr, nullptr, S->Xn);
-      LAUNCHED("k_unpack");
+      // the failed-search bookkeeping and the accepted points, then one full evaluation there
+      hipLaunchKernelGGL(k_fail_unpack, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, nw, S->freepos,
+                         S->Xbase, S->st_w, S->Xn, S->act, S->st_alpha, S->err0, o.acceptable_tol, S->failed, S->moved,
+                         S->in_soft, S->soft_cnt, S->status, S->active);
+      LAUNCHED("k_fail_unpack");
       CK(eval_full(S, S->Xn, S->f_n, S->grad_n, S->g_n, S->J_n));
       if (S->bfgs) {
-        hipLaunchKernelGGL(k_prep, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->free32, S->row_slack,
-                           S->gl, S->grad_n, S->g_n, S->st_w, S->gradw_new, nullptr);
-        LAUNCHED("k_prep (new)");
         hipLaunchKernelGGL(k_lbfgs, dim3((unsigned)B), dim3(256), 0, st, B, m, nf, nw, S->nnz_rec, S->amap, S->moved,
-                           S->w, S->st_w, S->y, S->dy, S->st_alpha, S->gradw, S->J, S->gradw_new, S->J_n, S->lm_s,
+                           S->w, S->st_w, S->y, S->dy, S->st_alpha, S->gradw, S->J, S->grad_n, S->free32, n, S->J_n, S->lm_s,
                            S->lm_y, S->lm_cnt, S->lm_skip, S->zeros_u8, S->Hq);
         LAUNCHED("k_lbfgs");
       }
@@ -1832,17 +1864,20 @@ int32_t step_phase(cpl_solver* S, int phase) {
                         S->phi_k, S->ft, S->fp, S->fc, S->st_w, S->dy, S->dzL, S->dzU, S->mu_o, S->hasL, S->hasU,
                         S->wl0, S->wu0, S->w, S->y, S->zL, S->zU, S->mu, S->iters, S->filt_t, S->filt_p, S->fcount,
                         st));
-      hipLaunchKernelGGL(k_accept_rows, dim3(blocks_elems(B * (1 + n + m + S->nnz_rec))), dim3(256), 0, st, B, n, m,
-                         S->nnz_rec, S->moved, S->f_n, S->grad_n, S->g_n, S->J_n, S->f, S->grad, S->g, S->J);
-      LAUNCHED("k_accept_rows");
-      if (phase == P_ACCEPT_NR) goto count;  // no instance can have failed its search: no entry
+      AcceptRows ar{S->moved, n, m, S->nnz_rec, S->f_n, S->grad_n, S->g_n, S->J_n, S->f, S->grad, S->g, S->J};
+      if (phase == P_ACCEPT_NR) {  // no instance can have failed its search: no entry
+        hipLaunchKernelGGL(k_accept_rows, dim3(blocks_elems(B * (1 + n + m + S->nnz_rec))), dim3(256), 0, st, B, n,
+                           m, S->nnz_rec, S->moved, S->f_n, S->grad_n, S->g_n, S->J_n, S->f, S->grad, S->g, S->J);
+        LAUNCHED("k_accept_rows");
+        goto count;
+      }
       // the restoration phase starts where the line search failed
       hipLaunchKernelGGL(k_resto_enter, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nw, S->failed, S->c, S->w, S->zL,
                          S->zU, S->mu_o, S->theta_k, S->phi_k, S->hasL, S->hasU, S->filt_t, S->filt_p, S->fcount,
                          S->iters, S->in_resto, S->n_resto, S->wR, S->pR, S->nR, S->zp, S->zn, S->zLR, S->zUR, S->muR,
                          S->ftR, S->fpR, S->fcR, S->thmaxR, S->thminR, S->th_o0, S->ph_o0, S->dwlR, S->lm_cnt,
-                         S->lm_skip, S->bfgs ? S->Hq : nullptr, lmc, S->M, S->r1, S->r2, S->Dinv);
-      LAUNCHED("k_resto_enter");
+                         S->lm_skip, S->bfgs ? S->Hq : nullptr, lmc, S->M, S->r1, S->r2, S->Dinv, ar);
+      LAUNCHED("k_resto_enter (+ the accepted rows)");
       CK(cpl_kkt_qd_solve(B, nw, m, S->M, S->A, S->Dinv, S->r1, S->r2, S->failed, S->dwlR, S->dw, S->dy, S->scr1,
                           S->Kqd, st));
       hipLaunchKernelGGL(k_resto_y0, dim3(blocks_for(B)), dim3(256), 0, st, B, m, S->failed, S->dy, S->y);
@@ -1919,7 +1954,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
         hipLaunchKernelGGL(k_moved_r, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->actR, S->st_alpha, S->movedR);
         LAUNCHED("k_moved_r");
         hipLaunchKernelGGL(k_lbfgs, dim3((unsigned)B), dim3(256), 0, st, B, m, nf, nw, S->nnz_rec, S->amap, S->movedR,
-                           S->w, S->st_w, S->y, S->dy, S->st_alpha, S->zeros_w, S->J, S->zeros_w, S->J_n, S->lm_s,
+                           S->w, S->st_w, S->y, S->dy, S->st_alpha, S->zeros_w, S->J, nullptr, S->free32, n, S->J_n, S->lm_s,
                            S->lm_y, S->lm_cnt, S->lm_skip, S->zeros_u8, S->Hq);
         LAUNCHED("k_lbfgs (resto)");
       }
@@ -2074,7 +2109,7 @@ void cpl_solve_options_default(cpl_solve_options* o) {
   o->acceptable_iter = 15;
   o->use_graph = 1;
   o->compact = 1;
-  o->ls_kernel = 1;
+  o->ls_kernel = 2;
   o->tol = 1e-8;
   o->acceptable_tol = 1e-6;
   o->mu_init = 0.1;
@@ -2263,7 +2298,7 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   S->thminR = a.take<double>(Bz);
   // temporaries
   S->A = a.take<double>(Bz * m * nw);
-  S->gradw = a.take<double>(Bz * nw); S->gradw_new = a.take<double>(Bz * nw); S->c = a.take<double>(Bz * m);
+  S->gradw = a.take<double>(Bz * nw); S->c = a.take<double>(Bz * m);
   S->err0 = a.take<double>(Bz); S->base = a.take<double>(Bz); S->mu_o = a.take<double>(Bz);
   S->ft = a.take<double>(Bz * FMAX); S->fp = a.take<double>(Bz * FMAX); S->tau = a.take<double>(Bz);
   S->X = a.take<double>(Bz * n); S->H = a.take<double>(Bz * nf * nf); S->M = a.take<double>(Bz * nw * nw);

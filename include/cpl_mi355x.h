@@ -489,10 +489,9 @@ typedef struct cpl_solve_options {
                               size); the results come back in the instances' own order */
   int32_t ls_kernel;       /* the first line-search trial, its second-order corrections and the
                               backtracking in ONE launch (systems the one-wave KKT kernel factorises:
-                              nw = 47, m = 30): 1 (default) for lock-step batches of at most 256 rows
-                              (launch-bound: the single-instance Solve(), every solve's tail), 2 at
-                              every size, 0 never (one launch per step of the first trial) — the same
-                              iterates bit for bit either way */
+                              nw = 47, m = 30): 2 (default) at every batch size, 1 for lock-step
+                              batches of at most 256 rows, 0 never (one launch per step of the first
+                              trial) — the same iterates bit for bit either way */
   double tol;              /* 1e-8 */
   double acceptable_tol;   /* 1e-6 */
   double mu_init;          /* 0.1 */

@@ -20,7 +20,7 @@ from centroidalplanner_amd.workload import solve_inputs, solve_problem  # noqa: 
 ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--only", default="", help="run one case, e.g. limited-memory:1 (for a kernel trace)")
-ap.add_argument("--ls-kernel", type=int, default=1, help="the engine's ls_kernel option (0 / 1 / 2)")
+ap.add_argument("--ls-kernel", type=int, default=2, help="the engine's ls_kernel option (0 / 1 / 2)")
 args = ap.parse_args()
 
 prob = solve_problem().GetCplProblem()
