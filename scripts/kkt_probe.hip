@@ -95,8 +95,8 @@ int main(int argc, char** argv) {
                                     "refinement", "store factors"};
       const char* wave_names[7] = {"QR", "Z accumulation", "rank + Z^T M Z", "inertia/Cholesky", "solve",
                                    "refinement", "store factors"};
-      const char* const* names = kkt_wave_kernel_for(nw, m, 1 << 30) ? wave_names : block_names;
-      std::printf("  (%s kernel)\n", kkt_wave_kernel_for(nw, m, 1 << 30) ? "one-wave" : "workgroup");
+      const char* const* names = kkt_wave_kernel_for(nw, m) ? wave_names : block_names;
+      std::printf("  (%s kernel)\n", kkt_wave_kernel_for(nw, m) ? "one-wave" : "workgroup");
       for (int p = 0; p < 7; ++p) {
         double s = 0.0;
         for (int b = 0; b < B; ++b) s += (double)(prof[(size_t)b * 8 + p + 1] - prof[(size_t)b * 8 + p]);
