@@ -2401,8 +2401,9 @@ __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, c
       if (FIRST && !RESTO && stage == S_SOC) {
         if (q > 0 && lane < m) csoc = a_soc * csoc + cons();
         double dwv, dyv;
-        kkt_wave_resolve<KNW, KM>(A.M + b * KNW * KNW, A.kkt_ws + b * kkt_ws_per(KNW, KM),
-                                  lane < KNW ? A.r1[b * KNW + lane] : 0.0, lane < KM ? -csoc : 0.0, kk, &dwv, &dyv);
+        kkt_wave_resolve_g<KNW, KM>(A.M + b * KNW * KNW, A.kkt_ws + b * kkt_ws_per(KNW, KM),
+                                    lane < KNW ? A.r1[b * KNW + lane] : 0.0, lane < KM ? -csoc : 0.0, kk, &dwv,
+                                    &dyv);
         if (lane < nw) Dv[lane] = dwv;
         double r = INFINITY;  // cpl_ipm_max_step (primal)
         const double t = A.tau[b];

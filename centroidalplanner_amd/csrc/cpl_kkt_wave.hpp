@@ -209,15 +209,55 @@ __device__ __forceinline__ double mfma_matvec(const double (&Mf)[MFrag<NW>::RB][
   return lane < NW ? ys[lane] : 0.0;
 }
 
+// mfma_matvec with M's fragments loaded from memory (L2) just before their MFMAs instead of held in
+// registers: the same operands in the same order (bitwise the same y), without 72 VGPRs live across
+// the caller — for kernels whose occupancy the resident fragments would cost (the line-search kernel's
+// second-order corrections).
+template <int NW>
+__device__ __forceinline__ double mfma_matvec_g(const double* __restrict__ M, const double* xs, double* ys) {
+  constexpr int KB = MFrag<NW>::KB, RB = MFrag<NW>::RB;
+  typedef double f64x4 __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+  double xf[KB];
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    const int k = 4 * kb + lk;
+    xf[kb] = (li == 0 && k < NW) ? xs[k] : 0.0;
+  }
+  f64x4 acc[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    acc[rb] = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      const int r = 16 * rb + li, k = 4 * kb + lk;
+      const double mf = (r < NW && k < NW) ? M[k * NW + r] : 0.0;
+      acc[rb] = __builtin_amdgcn_mfma_f64_16x16x4f64(mf, xf[kb], acc[rb], 0, 0, 0);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (li == 0) {
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 16 * rb + lk + 4 * q;
+        if (r < NW) ys[r] = acc[rb][q];
+      }
+  }
+  __builtin_amdgcn_wave_barrier();
+  return lane < NW ? ys[lane] : 0.0;
+}
+
 // The null-space solve on one wave.  q1v (lanes < NW), q2v (lanes < MM): the right-hand sides in
 // registers; returns dw in *dwv (lanes < NW) and dy in *dyv (lanes < MM).  s1, s2: LDS scratch of NW
 // doubles.  M: the system's (symmetric) M in global memory, read by columns.
-template <int NW, int MM>
-__device__ __forceinline__ void wave_null_solve_t(const double* QR, const double* Z, const double* L,
-                                                  const double* beta, const double* cp,
-                                                  const double (&Mf)[MFrag<NW>::RB][MFrag<NW>::KB], double dW,
-                                                  double q1v, double q2v, double* s1, double* s2, double* dwv,
-                                                  double* dyv) {
+// the same with any M x product (mv(xs, ys): M xs through the LDS vectors, as mfma_matvec)
+template <int NW, int MM, class MV>
+__device__ __forceinline__ void wave_null_solve_mv(const double* QR, const double* Z, const double* L,
+                                                   const double* beta, const double* cp, MV&& mv, double dW,
+                                                   double q1v, double q2v, double* s1, double* s2, double* dwv,
+                                                   double* dyv) {
   constexpr int NZ = NW - MM;
   constexpr int ZS = KktWave<NW, MM>::ZS;
   const int lane = threadIdx.x & 63;
@@ -233,7 +273,7 @@ __device__ __forceinline__ void wave_null_solve_t(const double* QR, const double
   __builtin_amdgcn_wave_barrier();
   if constexpr (NZ > 0) {
     // t = q1 - (M + dW I) Y p_y  ->  rz = Z^T t  ->  L L^T p_z = rz
-    const double mx = mfma_matvec<NW>(Mf, s2, s1);
+    const double mx = mv(s2, s1);
     if (rw) s1[lane] = q1v - dW * x - mx;
     __builtin_amdgcn_wave_barrier();
     double rz = 0.0;
@@ -261,11 +301,22 @@ __device__ __forceinline__ void wave_null_solve_t(const double* QR, const double
   }
   *dwv = x;
   // u = q1 - (M + dW I) dw  ->  Y^T u = (Q^T u)[0, m)  ->  R dy = Y^T u
-  const double mx = mfma_matvec<NW>(Mf, s2, s1);
+  const double mx = mv(s2, s1);
   const double u = chain_Qt<NW, MM>(rw ? q1v - dW * x - mx : 0.0, QR, bl, cl);
   *dyv = wave_trsv_reg<MM, false>(QR, 1, NW, QR, NW + 1, lane < MM ? u : 0.0);  // R[i][k] = QR[k * NW + i]
   __builtin_amdgcn_wave_barrier();
 }
+
+template <int NW, int MM>
+__device__ __forceinline__ void wave_null_solve_t(const double* QR, const double* Z, const double* L,
+                                                  const double* beta, const double* cp,
+                                                  const double (&Mf)[MFrag<NW>::RB][MFrag<NW>::KB], double dW,
+                                                  double q1v, double q2v, double* s1, double* s2, double* dwv,
+                                                  double* dyv) {
+  wave_null_solve_mv<NW, MM>(QR, Z, L, beta, cp, [&](const double* xs, double* ys) { return mfma_matvec<NW>(Mf, xs, ys); },
+                             dW, q1v, q2v, s1, s2, dwv, dyv);
+}
+
 
 // Re-solve with the factors a factorisation kept (mode 1 of cpl_kkt_wave_kernel): the factor image
 // (NFAC doubles) copied from the instance's workspace wsb into LDS sm (W::LDS doubles: the image
@@ -290,6 +341,28 @@ __device__ __forceinline__ void kkt_wave_resolve(const double* __restrict__ M, c
   double Mf[MFrag<NW>::RB][MFrag<NW>::KB];
   load_m_frags<NW>(M, Mf);
   wave_null_solve_t<NW, MM>(QR, Z, L, beta, cp, Mf, dW, q1v, q2v, s1, s2, dwv, dyv);
+}
+
+// kkt_wave_resolve with M's fragments loaded per product (mfma_matvec_g): bitwise the same step, for
+// kernels that cannot keep 72 VGPRs of fragments resident (the line-search kernel)
+template <int NW, int MM>
+__device__ __forceinline__ void kkt_wave_resolve_g(const double* __restrict__ M, const double* __restrict__ wsb,
+                                                   double q1v, double q2v, double* sm, double* dwv, double* dyv) {
+  using W = KktWave<NW, MM>;
+  constexpr int NZ = W::NZ, ZS = W::ZS, NFAC = W::NFAC;
+  const int lane = threadIdx.x & 63;
+  double* QR = sm;
+  double* Z = QR + MM * NW;
+  double* L = Z + NW * ZS;
+  double* beta = L + NZ * NZ;
+  double* cp = beta + MM;
+  double* s1 = sm + NFAC;
+  double* s2 = s1 + NW;
+  for (int i = lane; i < NFAC; i += 64) sm[i] = wsb[i];
+  const double dW = wsb[NFAC];
+  __builtin_amdgcn_wave_barrier();
+  wave_null_solve_mv<NW, MM>(QR, Z, L, beta, cp, [&](const double* xs, double* ys) { return mfma_matvec_g<NW>(M, xs, ys); },
+                             dW, q1v, q2v, s1, s2, dwv, dyv);
 }
 
 }  // namespace cpl
