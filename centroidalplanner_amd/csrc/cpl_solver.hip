@@ -574,6 +574,9 @@ __global__ void k_fail_unpack(int64_t total, int n, int nw, const int32_t* __res
 constexpr int LM_HIST = 6, LM_MAX_SKIP = 2;
 // doubles per instance of the compact model: sigma, the number of pairs nv, U [LM_HIST][nf], W [LM_HIST][nf]
 __host__ __device__ constexpr int64_t LMC(int nf) { return 2 + 2 * (int64_t)LM_HIST * nf; }
+// NFX: the LDS row length of the pair vectors (64 for nf <= 64 — the 4-contact problem's 39 — else 128):
+// 28.5 -> 15.5 KiB of LDS per workgroup, twice the resident workgroups per CU
+template <int NFX>
 __global__ __launch_bounds__(256) void k_lbfgs(int64_t B, int m, int nf, int nw, int nnz_rec,
                                                const int32_t* __restrict__ amap, const uint8_t* __restrict__ act,
                                                const double* __restrict__ w_old, const double* __restrict__ w_new,
@@ -587,7 +590,7 @@ __global__ __launch_bounds__(256) void k_lbfgs(int64_t B, int m, int nf, int nw,
                                                double* __restrict__ Hq) {
   const int64_t b = blockIdx.x;
   if (b >= B || !act[b]) return;
-  __shared__ double Ps[LM_HIST][128], Py[LM_HIST][128], yn[256], red[8];
+  __shared__ double Ps[LM_HIST][NFX], Py[LM_HIST][NFX], yn[256], red[8];
   const int tid = threadIdx.x;
   const double al = alpha[b];
   for (int r = tid; r < m; r += blockDim.x) yn[r] = y[b * m + r] + al * dy[b * m + r];
@@ -601,7 +604,7 @@ __global__ __launch_bounds__(256) void k_lbfgs(int64_t B, int m, int nf, int nw,
   {  // J_free^T y at both points, straight from the values-only Jacobian records (the entries of A =
      // [J_free | -P] as cpl_ipm_dense_a forms them: amap -1 = 0, -2 = constant 1, NaN = 0); the rows
      // split over `parts` thread groups, partials summed in fixed order
-    __shared__ double pjn[4][128], pjo[4][128];
+    __shared__ double pjn[4][NFX], pjo[4][NFX];
     const int kp = nf <= 64 ? 64 : 128, parts = (int)blockDim.x / kp;
     const int k = tid % kp, part = tid / kp;
     if (k < nf && part < parts) {
@@ -688,7 +691,7 @@ __global__ __launch_bounds__(256) void k_lbfgs(int64_t B, int m, int nf, int nw,
   // B = sigma I + sum_i [-(a_i a_i') / s_i'a_i + (y_i y_i') / s_i'y_i] once (as products of the scaled
   // vectors a_i / sqrt(s_i'a_i), y_i / sqrt(s_i'y_i)), straight to global
   // memory.  Same model as the dense rank-2 recursion (which re-read and re-wrote B six times).
-  __shared__ double Pa[LM_HIST][128], s_sa[LM_HIST], s_sy[LM_HIST];
+  __shared__ double Pa[LM_HIST][NFX], s_sa[LM_HIST], s_sy[LM_HIST];
   if (tid < 64) {
     const int k0 = tid, k1 = tid + 64;
     const bool h0 = k0 < nf, h1 = k1 < nf;
@@ -1855,7 +1858,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
       LAUNCHED("k_fail_unpack");
       CK(eval_full(S, S->Xn, S->f_n, S->grad_n, S->g_n, S->J_n));
       if (S->bfgs) {
-        hipLaunchKernelGGL(k_lbfgs, dim3((unsigned)B), dim3(256), 0, st, B, m, nf, nw, S->nnz_rec, S->amap, S->moved,
+        hipLaunchKernelGGL(nf <= 64 ? k_lbfgs<64> : k_lbfgs<128>, dim3((unsigned)B), dim3(256), 0, st, B, m, nf, nw, S->nnz_rec, S->amap, S->moved,
                            S->w, S->st_w, S->y, S->dy, S->st_alpha, S->gradw, S->J, S->grad_n, S->free32, n, S->J_n, S->lm_s,
                            S->lm_y, S->lm_cnt, S->lm_skip, S->zeros_u8, S->Hq);
         LAUNCHED("k_lbfgs");
@@ -1953,7 +1956,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
       if (S->bfgs) {  // the restoration phase's own model: pairs from J^T y (its constraint curvature)
         hipLaunchKernelGGL(k_moved_r, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->actR, S->st_alpha, S->movedR);
         LAUNCHED("k_moved_r");
-        hipLaunchKernelGGL(k_lbfgs, dim3((unsigned)B), dim3(256), 0, st, B, m, nf, nw, S->nnz_rec, S->amap, S->movedR,
+        hipLaunchKernelGGL(nf <= 64 ? k_lbfgs<64> : k_lbfgs<128>, dim3((unsigned)B), dim3(256), 0, st, B, m, nf, nw, S->nnz_rec, S->amap, S->movedR,
                            S->w, S->st_w, S->y, S->dy, S->st_alpha, S->zeros_w, S->J, nullptr, S->free32, n, S->J_n, S->lm_s,
                            S->lm_y, S->lm_cnt, S->lm_skip, S->zeros_u8, S->Hq);
         LAUNCHED("k_lbfgs (resto)");
