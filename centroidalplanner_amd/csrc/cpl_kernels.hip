@@ -1362,32 +1362,32 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
     // mixed: the statics / cost items join phase 1 (beside the Superquadric ladders), the Ground
     // contacts phase 2 (beside the Superquadric rows) — with 8-instance tiles both phases then fit
     // one pass of the workgroup (232 and 256 items at the 1:1 mix)
+    // Each phase as two loops over the same item -> thread mapping (Superquadric items, then the
+    // others): one item function per loop body, so the register allocation of the two does not add up.
     const int items1 = r_ax + (OTHERS_FIRST ? r_oth : r_oth - r_gr);
-    for (int it = tid; it < items1; it += WG) {
-      if (HAS_SQ && it < r_ax) {
+    if (HAS_SQ)
+      for (int it = tid; it < r_ax; it += WG) {
         const int a = it / per_axis, kj = it - a * per_axis;
         const int k = kj / n_sq, j = kj - k * n_sq;
         const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
         sq_axis_item<ENVK == CPL_ENV_MIXED>(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m);
-      } else {
-        other_item(it - r_ax + (OTHERS_FIRST ? 0 : r_gr));
       }
-    }
+    for (int it = tid; it < items1; it += WG)
+      if (it >= r_ax) other_item(it - r_ax + (OTHERS_FIRST ? 0 : r_gr));
     // LDS-only barriers from here on: the phases exchange LDS data only, and a __syncthreads would
     // first wait for every global store the items issued (f, and with jdirect the Jacobian rows)
     if (HAS_SQ && n_sq > 0 && wgj) lds_barrier();
     const int r_rows = r_ax;
     const int items2 = r_rows + (OTHERS_FIRST ? 0 : r_gr);
-    for (int it = tid; it < items2; it += WG) {
-      if (HAS_SQ && it < r_rows) {
+    if (HAS_SQ)
+      for (int it = tid; it < r_rows; it += WG) {
         const int a = it / per_axis, kj = it - a * per_axis;
         const int k = kj / n_sq, j = kj - k * n_sq;
         const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
         sq_row_item<ENVK == CPL_ENV_MIXED>(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m, Jt + r * nnz);
-      } else {
-        other_item(it - r_rows);
       }
-    }
+    for (int it = tid; it < items2; it += WG)
+      if (it >= r_rows) other_item(it - r_rows);
     if (JD && K.want_j) {  // the statics Jacobian rows, lanes along each record
       lds_barrier();  // (the CoM pairs of the values items)
       for (int r = 0; r < valid; ++r) statics_rows_coop(K, X + r * n, com6 + 6 * r, Jt + r * nnz, tid, WG);
