@@ -27,6 +27,8 @@ Rank 0 prints one JSON line.  Fields beyond the driver contract:
   configs1_65k  BASELINE.json configs[1] (65,536 x 4 Ground) kernel time on the same GPU
   configs2_sq8  BASELINE.json configs[2] (262,144 x 8 Superquadric): kernel time, HBM fraction, VALU
                 roofline (PMC), checker sample
+  configs3_mixed16  BASELINE.json configs[3]'s 1,048,576 x 16 mixed batch on one GPU: kernel time, HBM
+                fraction, per-kind checker sample
   configs4_solve5_lbfgs  BASELINE.json configs[4] (8,192 concurrent solves) in the reference's Hessian
                 mode (IPOPT's L-BFGS): solves/s, iterations, a small CPU sample of the same solver;
                 .single_solve: one instance solved alone (CentroidalPlanner::Solve()'s batch of one):
@@ -437,6 +439,45 @@ def side_sq8(dev, stream, valu_counters, check_sample=1024):
     return res
 
 
+def side_mixed16(dev, stream, check_sample=512):
+    """BASELINE.json configs[3] (1,048,576 x 16 contacts, Ground / Superquadric tagged per instance) on
+    ONE GPU: the eval kernel's time (median of timed rounds, HIP events), its HBM fraction and a
+    per-kind checker sample (both environment kinds) of the outputs."""
+    import ctypes
+
+    import torch
+
+    from centroidalplanner_amd import _abi
+    from centroidalplanner_amd.workload import CONFIGS, config_inputs
+
+    cfg = CONFIGS["mixed16"]
+    prob, x, mass, tag = config_inputs(cfg)
+    B = x.shape[0]
+    xt, mt, tt = torch.tensor(x, device=dev), torch.tensor(mass, device=dev), torch.tensor(tag, device=dev)
+    del x, mass
+    out = prob.eval_batch(xt, mt, tt, outputs=("g", "jac", "norms"))
+    p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    ms = ctypes.c_double()
+    rounds = []
+    for _ in range(3):
+        _abi.check(_abi.lib.cpl_time_eval_batch(ctypes.byref(prob.desc()), B, p(xt), p(mt), p(tt), p(out["g"]),
+                                                p(out["jac"]), None, None, p(out["norms"]),
+                                                ctypes.c_void_p(stream.cuda_stream), 5, ctypes.byref(ms)))
+        rounds.append(ms.value)
+    kms = sorted(rounds)[1]
+    bytes_inst, m = algorithmic_bytes(cfg.n_contacts, cfg.env)
+    res = {"workload": cfg.name + " (one GPU)", "kernel_ms": kms, "rows_per_s": B * m / (kms * 1e-3),
+           "hbm_gbps": bytes_inst * B / (kms * 1e-3) / 1e9,
+           "frac_of_peak": bytes_inst * B / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, "bytes_per_instance": bytes_inst}
+    try:
+        res["check"] = checker_leg(prob, cfg.env, xt, mt, tt, out, B, check_sample)
+    except Exception as e:  # noqa: BLE001
+        res["check"] = {"ok": False, "error": f"checker leg failed: {e}"}
+    del out, xt, mt, tt
+    torch.cuda.empty_cache()
+    return res
+
+
 def run_solve5(dev, batch, hessian, steps, warm, max_ls, max_soc, cpu_sample, rank=0, world=1, barrier=None,
                ls_kernel=2):
     """BASELINE.json configs[4]: `steps` complete batched solves of `batch` TestBasic ground instances
@@ -828,12 +869,16 @@ def main():
             "note": "128 MB working set: fits the 256 MiB Infinity Cache",
         }
 
-    sq8 = solve5 = None
+    sq8 = solve5 = mixed = None
     if rank == 0 and world == 1 and not args.no_side and args.config == "ground4_1m":
         try:
             sq8 = side_sq8(dev, stream, sq8_counters)
         except Exception as e:  # noqa: BLE001
             sq8 = {"error": str(e)}
+        try:
+            mixed = side_mixed16(dev, stream)
+        except Exception as e:  # noqa: BLE001
+            mixed = {"error": str(e)}
         try:
             solve5 = side_solve5(dev, 0 if args.no_cpu else 64)
         except Exception as e:  # noqa: BLE001
@@ -897,6 +942,8 @@ def main():
             res["single_instance"] = single
         if sq8:
             res["configs2_sq8"] = sq8
+        if mixed is not None:
+            res["configs3_mixed16"] = mixed
         if solve5:
             res["configs4_solve5_lbfgs"] = solve5
         print(json.dumps(res), flush=True)
