@@ -1394,6 +1394,14 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
     }
   }
   lds_barrier();
+  // the residual partials first (from the LDS image), so that their stores are in flight with the
+  // copy-out's instead of after them on every workgroup's tail
+  if (K.want_norms) {
+    NormAcc acc;
+    acc.init(tid, WG, m);
+    acc.add_tile(Gt, valid * m, tid, WG, m);
+    partial_norms_waves(acc, norms_ws + NORM_HDR);
+  }
   if (K.ablate != 2 && K.soa) {
     if (K.want_g) copy_out_soa<WG, NT>(g_out + b0, batch, Gt, m, valid, tid);
     if (K.want_j) copy_out_soa<WG, NT>(jac_out + b0, batch, Jt, nnz, valid, tid);
@@ -1402,12 +1410,6 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
     if (K.want_g) copy_out<WG, NT>(g_out + b0 * m, Gt, valid * m, tid);
     if (K.want_j && !JD) copy_out<WG, NT>(jac_out + b0 * nnz, Jt, valid * nnz, tid);
     if (K.want_grad) copy_out<WG, NT>(grad_out + b0 * n, Dt, valid * n, tid);
-  }
-  if (K.want_norms) {
-    NormAcc acc;
-    acc.init(tid, WG, m);
-    acc.add_tile(Gt, valid * m, tid, WG, m);
-    partial_norms_waves(acc, norms_ws + NORM_HDR);
   }
 }
 
