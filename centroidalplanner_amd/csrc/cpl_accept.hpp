@@ -110,4 +110,46 @@ struct LsBacktrackArgs {
   const double* tau;          // [batch] fraction-to-the-boundary parameter
 };
 
+// The solve loop's per-iteration unpack after the optimality test, fused into that kernel's tail
+// (cpl_ipm.hip; was a launch of its own): X = unpack(w) (free columns from w, fixed ones from
+// Xbase), tau = max(0.99, 1 - mu) and the iteration's snapshot act = active && !in_resto.
+struct IpmUnpack {
+  int32_t n;
+  const int32_t* freepos;
+  const double* Xbase;
+  const uint8_t* in_resto;
+  double* X;
+  double* tau;
+  uint8_t* act;
+};
+
+// one entry e of A = dc/dw = [J_free | -P] (batch-major [B][m][nw]) from the CSR Jacobian values:
+// amap[r * nf + k] = CSR position of (row r, free column k), -1 (structural zero) or -2 (a
+// structural 1 the folded layout skips); NaN -> 0 (a cone at zero tangential force); the slack
+// block is -1 at (r, nf + row_slack[r]).  Shared by cpl_ipm_dense_a and the solver's fused launch.
+__device__ __forceinline__ void dense_a_entry(int64_t e, int m, int nw, int nf, int nnz,
+                                              const int32_t* __restrict__ amap,
+                                              const int32_t* __restrict__ row_slack,
+                                              const double* __restrict__ jac, double* __restrict__ A,
+                                              const uint8_t* __restrict__ active) {
+  const int per = m * nw;
+  const int64_t b = e / per;
+  if (active && !active[b]) return;
+  const int rc = (int)(e - b * per);
+  const int r = rc / nw, k = rc - r * nw;
+  double v = 0.0;
+  if (k < nf) {
+    const int q = amap[r * nf + k];
+    if (q >= 0) {
+      v = jac[b * nnz + q];
+      v = v == v ? v : 0.0;
+    } else if (q == -2) {
+      v = 1.0;
+    }
+  } else if (row_slack[r] == k - nf) {
+    v = -1.0;
+  }
+  A[e] = v;
+}
+
 }  // namespace cpl

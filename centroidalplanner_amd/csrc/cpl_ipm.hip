@@ -116,10 +116,22 @@ __global__ __launch_bounds__(256) void cpl_ipm_optimality_kernel(
     double* __restrict__ d_inf_out, double* __restrict__ err0_out, double* __restrict__ base_out,
     double* __restrict__ mu_out, double* __restrict__ filt_t_out, double* __restrict__ filt_p_out,
     int64_t* __restrict__ fcount_out, int mu_rounds, double mu_min, const uint8_t* __restrict__ tiny_flag,
-    const uint8_t* __restrict__ skip) {
+    const uint8_t* __restrict__ skip, const IpmUnpack up) {
   const int64_t b = (int64_t)blockIdx.x * IPM_WAVES + (threadIdx.x >> 6);
   if (b >= batch) return;
   const int lane = threadIdx.x & 63;
+  // the solve loop's unpack (IpmUnpack) at the iteration's barrier parameter and active flag
+  auto unpack = [&](double mu_v, bool act_v) {
+    if (!up.X) return;
+    for (int j = lane; j < up.n; j += 64) {
+      const int k = up.freepos[j];
+      up.X[b * up.n + j] = k >= 0 ? w[b * nw + k] : up.Xbase[b * up.n + j];
+    }
+    if (lane == 0) {
+      up.tau[b] = fmax(1.0 - mu_v, 0.99);
+      up.act[b] = act_v && !up.in_resto[b];
+    }
+  };
   if (skip && skip[b]) {  // (an instance in the restoration phase: its own test and barrier update)
     for (int k = lane; k < nfilt; k += 64) {
       filt_t_out[b * nfilt + k] = filt_t[b * nfilt + k];
@@ -129,6 +141,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_optimality_kernel(
       mu_out[b] = mu_in[b];
       fcount_out[b] = fcount[b];
     }
+    unpack(mu_in[b], active[b] != 0);
     return;
   }
   const double* Ab = A + b * (int64_t)m * nw;
@@ -212,6 +225,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_optimality_kernel(
     mu_out[b] = mu;
     fcount_out[b] = reset ? 0 : fcount[b];
   }
+  unpack(mu, act);
 }
 
 // Fraction-to-the-boundary step (batch_ipm.py max_step, both sides): the largest alpha <= 1 with
@@ -483,24 +497,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_dense_a_kernel(int64_t total, int
                                                               const uint8_t* __restrict__ active) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total) return;
-  const int per = m * nw;
-  const int64_t b = e / per;
-  if (active && !active[b]) return;
-  const int rc = (int)(e - b * per);
-  const int r = rc / nw, k = rc - r * nw;
-  double v = 0.0;
-  if (k < nf) {
-    const int q = amap[r * nf + k];
-    if (q >= 0) {
-      v = jac[b * nnz + q];
-      v = v == v ? v : 0.0;
-    } else if (q == -2) {  // a structural constant 1 the folded Jacobian layout skips
-      v = 1.0;
-    }
-  } else if (row_slack[r] == k - nf) {
-    v = -1.0;
-  }
-  A[e] = v;
+  dense_a_entry(e, m, nw, nf, nnz, amap, row_slack, jac, A, active);
 }
 
 // Central-difference points of the solve loop's Hessian (batch_ipm.py fd_hessian): for instance b
@@ -566,14 +563,16 @@ int32_t ipm_optimality_ex(int64_t batch, int32_t nw, int32_t m, int32_t nfilt, i
                           uint8_t* d_active, int64_t* d_status, int64_t* d_acc, double* d_d_inf, double* d_err0,
                           double* d_base, double* d_mu_out, double* d_filt_t_out, double* d_filt_p_out,
                           int64_t* d_fcount_out, int32_t mu_rounds, double mu_min, const uint8_t* d_tiny_flag,
-                          const uint8_t* d_skip, void* stream) {
+                          const uint8_t* d_skip, const IpmUnpack* unpack, void* stream) {
   const int64_t blocks = (batch + IPM_WAVES - 1) / IPM_WAVES;
+  IpmUnpack up{};
+  if (unpack) up = *unpack;
   if (batch == 0) return CPL_OK;
   hipLaunchKernelGGL(cpl_ipm_optimality_kernel, dim3((unsigned)blocks), dim3(64 * IPM_WAVES), 0, (hipStream_t)stream,
                      batch, (int)nw, (int)m, (int)nfilt, (int)nbounds, tol, acc_tol, (int)acc_iter, d_A, d_gw, d_c, d_w,
                      d_y, d_zL, d_zU, d_hasL, d_hasU, d_wl0, d_wu0, d_mu, d_filt_t, d_filt_p, d_fcount, d_active,
                      d_status, d_acc, d_d_inf, d_err0, d_base, d_mu_out, d_filt_t_out, d_filt_p_out, d_fcount_out,
-                     (int)mu_rounds, mu_min, d_tiny_flag, d_skip);
+                     (int)mu_rounds, mu_min, d_tiny_flag, d_skip, up);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_ipm_optimality launch: ") + hipGetErrorString(e));
   return CPL_OK;
@@ -653,7 +652,7 @@ int32_t cpl_ipm_optimality(int64_t batch, int32_t nw, int32_t m, int32_t nfilt, 
   return ipm_optimality_ex(batch, nw, m, nfilt, nbounds, tol, acc_tol, acc_iter, d_A, d_gw, d_c, d_w, d_y, d_zL, d_zU,
                            d_hasL, d_hasU, d_wl0, d_wu0, d_mu, d_filt_t, d_filt_p, d_fcount, d_active, d_status, d_acc,
                            d_d_inf, d_err0, d_base, d_mu_out, d_filt_t_out, d_filt_p_out, d_fcount_out, IPM_MU_ROUNDS,
-                           ipm_mu_min(tol), nullptr, nullptr, stream);
+                           ipm_mu_min(tol), nullptr, nullptr, nullptr, stream);
 }
 
 int32_t cpl_ipm_max_step(int64_t batch, int32_t nw, const double* d_v, const double* d_dir, const double* d_v2,

@@ -51,7 +51,7 @@ int32_t ipm_optimality_ex(int64_t batch, int32_t nw, int32_t m, int32_t fmax, in
                           uint8_t* d_active, int64_t* d_status, int64_t* d_acc, double* d_dinf, double* d_err0,
                           double* d_base, double* d_mu_o, double* d_ft, double* d_fp, int64_t* d_fc,
                           int32_t mu_rounds, double mu_min, const uint8_t* d_tiny_flag, const uint8_t* d_skip,
-                          void* stream);
+                          const IpmUnpack* unpack, void* stream);
 namespace {
 
 constexpr int FMAX = 64;          // filter entries kept per instance (a ring), as batch_ipm.FMAX
@@ -198,8 +198,31 @@ __global__ __launch_bounds__(256) void k_prep(int64_t B, int n, int m, int nf, i
     for (int r = lane; r < m; r += 64) c[b * m + r] = cons_row(g + b * m, w + b * nw, nf, r, row_slack, gl);
 }
 
+// A = [J_free | -P] (cpl_ipm_dense_a's entries) and k_prep in one launch: the first nblk_a
+// workgroups take A's entries, the rest k_prep's instances (independent outputs, no ordering)
+__global__ __launch_bounds__(256) void k_dense_a_prep(int64_t totalA, unsigned nblk_a, int m, int nw, int nf, int nnz,
+                                                      const int32_t* __restrict__ amap,
+                                                      const int32_t* __restrict__ row_slack,
+                                                      const double* __restrict__ jac, double* __restrict__ A,
+                                                      const uint8_t* __restrict__ active, int64_t B, int n, const int32_t* __restrict__ free_idx,
+                                                      const double* __restrict__ gl, const double* __restrict__ grad,
+                                                      const double* __restrict__ g, const double* __restrict__ w,
+                                                      double* __restrict__ gradw, double* __restrict__ c) {
+  if (blockIdx.x < nblk_a) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < totalA) dense_a_entry(e, m, nw, nf, nnz, amap, row_slack, jac, A, active);
+    return;
+  }
+  const int64_t b = (int64_t)(blockIdx.x - nblk_a) * WPB + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  for (int k = lane; k < nw; k += 64) gradw[b * nw + k] = k < nf ? grad[b * n + free_idx[k]] : 0.0;
+  for (int r = lane; r < m; r += 64) c[b * m + r] = cons_row(g + b * m, w + b * nw, nf, r, row_slack, gl);
+}
+
 // after the optimality kernel: tau = max(0.99, 1 - mu), the iteration's active snapshot, and the
-// evaluation point X = unpack(w) for the Hessian
+// evaluation point X = unpack(w) for the Hessian (the solve loop has it fused into the optimality
+// kernel: IpmUnpack)
 __global__ void k_unpack_tau(int64_t total, int n, int nw, const int32_t* __restrict__ freepos,
                              const double* __restrict__ Xbase, const double* __restrict__ w,
                              const double* __restrict__ mu, const uint8_t* __restrict__ active,
@@ -1330,11 +1353,27 @@ __global__ __launch_bounds__(256) void k_resto_accept(
 }
 
 // the number of instances still active, and of those in the restoration phase, into two ints
-// (read by the host after each iteration): up to COUNT1_MAX instances one workgroup counts them
+// (read by the host after each iteration): up to COUNT1_MAX instances one workgroup counts them.
+// With a mailbox (coherent pinned host memory: [count, resto, seq]) the two counts also go straight
+// to the host, then the iteration's sequence number (count[2], incremented here) behind a
+// system-scope fence: the host polls seq instead of a D2H copy + stream synchronisation (a blit
+// kernel and two host wake-ups per iteration, ~35 us of a single solve's ~200 us iteration).
 constexpr int64_t COUNT1_MAX = 65536;
 __global__ __launch_bounds__(1024) void k_count1(int64_t B, const uint8_t* __restrict__ active,
-                                                 const uint8_t* __restrict__ in_resto, int32_t* __restrict__ count) {
+                                                 const uint8_t* __restrict__ in_resto, int32_t* __restrict__ count,
+                                                 int32_t* __restrict__ mail, int m, const uint8_t* __restrict__ failed,
+                                                 const double* __restrict__ dy, double* __restrict__ y) {
   __shared__ int s_w[16], s_r[16];
+  if (failed) {  // k_resto_y0's work, a wave per instance (no dependence on the counts below)
+    const int lane = threadIdx.x & 63;
+    for (int64_t b = threadIdx.x >> 6; b < B; b += 16) {
+      if (!failed[b]) continue;
+      double mx = 0.0;
+      for (int r = lane; r < m; r += 64) mx = fmax(mx, fabs(dy[b * m + r]));
+      mx = wave_max(mx);
+      for (int r = lane; r < m; r += 64) y[b * m + r] = mx <= 1e3 ? dy[b * m + r] : 0.0;
+    }
+  }
   int c = 0, cr = 0;
   for (int64_t b = threadIdx.x; b < B; b += 1024) {
     c += active[b] ? 1 : 0;
@@ -1358,6 +1397,15 @@ __global__ __launch_bounds__(1024) void k_count1(int64_t B, const uint8_t* __res
     }
     count[0] = t;
     count[1] = tr;
+    if (mail) {
+      const int32_t seq = count[2] + 1;
+      count[2] = seq;
+      volatile int32_t* mb = mail;
+      mb[0] = t;
+      mb[1] = tr;
+      __threadfence_system();
+      mb[2] = seq;
+    }
   }
 }
 // the accepted point's f, grad, g and Jacobian records into the iterate's, active instances only:
@@ -1755,17 +1803,20 @@ int32_t step_phase(cpl_solver* S, int phase) {
 
   switch (phase) {
     case P_NEWTON: {
-      CK(cpl_ipm_dense_a(B, m, nw, nf, S->nnz_rec, S->amap, S->row_slack, S->J, S->A, S->active, st));
-      hipLaunchKernelGGL(k_prep, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->free32, S->row_slack,
-                         S->gl, S->grad, S->g, S->w, S->gradw, S->c);
-      LAUNCHED("k_prep");
+      {  // A (active instances) and k_prep's gradw / c in one launch
+        const int64_t totalA = B * (int64_t)m * nw;
+        const unsigned nblk_a = (unsigned)((totalA + 255) / 256);
+        hipLaunchKernelGGL(k_dense_a_prep, dim3(nblk_a + blocks_for(B)), dim3(256), 0, st, totalA, nblk_a, m, nw, nf,
+                           S->nnz_rec, S->amap, S->row_slack, S->J, S->A, S->active, B, n, S->free32, S->gl, S->grad, S->g, S->w,
+                           S->gradw, S->c);
+        LAUNCHED("k_dense_a_prep");
+      }
+      // (with k_unpack_tau's X = unpack(w), tau and the active snapshot fused into its tail)
+      const IpmUnpack unp{n, S->freepos, S->Xbase, S->in_resto, S->X, S->tau, S->act};
       CK(ipm_optimality_ex(B, nw, m, FMAX, S->nbounds, o.tol, o.acceptable_tol, o.acceptable_iter, S->A, S->gradw,
                            S->c, S->w, S->y, S->zL, S->zU, S->hasL, S->hasU, S->wl0, S->wu0, S->mu, S->filt_t,
                            S->filt_p, S->fcount, S->active, S->status, S->acc, S->d_inf, S->err0, S->base, S->mu_o,
-                           S->ft, S->fp, S->fc, MU_ROUNDS, S->mu_min, S->tiny_flag, S->in_resto, st));
-      hipLaunchKernelGGL(k_unpack_tau, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, nw, S->freepos, S->Xbase,
-                         S->w, S->mu_o, S->active, S->in_resto, S->X, S->tau, S->act);
-      LAUNCHED("k_unpack_tau");
+                           S->ft, S->fp, S->fc, MU_ROUNDS, S->mu_min, S->tiny_flag, S->in_resto, &unp, st));
       const double* Hblk = nullptr;
       int h_sym = 0;
       CK(hessian_into(S, &S->desc, S->act, &Hblk, &h_sym));
@@ -1883,15 +1934,19 @@ int32_t step_phase(cpl_solver* S, int phase) {
       LAUNCHED("k_resto_enter (+ the accepted rows)");
       CK(cpl_kkt_qd_solve(B, nw, m, S->M, S->A, S->Dinv, S->r1, S->r2, S->failed, S->dwlR, S->dw, S->dy, S->scr1,
                           S->Kqd, st));
-      hipLaunchKernelGGL(k_resto_y0, dim3(blocks_for(B)), dim3(256), 0, st, B, m, S->failed, S->dy, S->y);
-      LAUNCHED("k_resto_y0");
+      if (B > COUNT1_MAX) {
+        hipLaunchKernelGGL(k_resto_y0, dim3(blocks_for(B)), dim3(256), 0, st, B, m, S->failed, S->dy, S->y);
+        LAUNCHED("k_resto_y0");
+      }
     count:
       if (B > COUNT1_MAX) {
         hipLaunchKernelGGL(k_count_zero, dim3(1), dim3(64), 0, st, S->d_count);
         LAUNCHED("k_count_zero");
         hipLaunchKernelGGL(k_count, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->active, S->in_resto, S->d_count);
       } else {
-        hipLaunchKernelGGL(k_count1, dim3(1), dim3(1024), 0, st, B, S->active, S->in_resto, S->d_count);
+        // (with the restoration entry's multiplier reset fused in: P_ACCEPT)
+        hipLaunchKernelGGL(k_count1, dim3(1), dim3(1024), 0, st, B, S->active, S->in_resto, S->d_count, S->h_count, m,
+                           phase == P_ACCEPT ? S->failed : nullptr, S->dy, S->y);
       }
       LAUNCHED("k_count");
       return CPL_OK;
@@ -2014,6 +2069,26 @@ int32_t run_phase(cpl_solver* S, int phase) {
 }
 
 // the device's flags (any still searching / soft candidates / restoration searching) to the host
+// wait for iteration `seq`'s counts in the mailbox (k_count1), polling; the stream is queried
+// every 1024 polls so that a failed launch ends the wait with its error
+int32_t wait_mail(cpl_solver* S, int32_t seq) {
+  volatile int32_t* mb = S->h_count;
+  for (uint32_t k = 1;; ++k) {
+    if (mb[2] == seq) break;
+    if ((k & 1023u) == 0) {
+      const hipError_t q = hipStreamQuery(S->stream);
+      if (q == hipSuccess) {
+        if (mb[2] == seq) break;
+        return fail(CPL_ERR_RUNTIME, "cpl_solver_solve: the iteration's counts never reached the host");
+      }
+      if (q != hipErrorNotReady) return hip_err(q, "hipStreamQuery");
+    }
+    __builtin_ia32_pause();
+  }
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  return CPL_OK;
+}
+
 int32_t read_flags(cpl_solver* S) {
   HK(hipMemcpyAsync(S->h_flag, S->d_any, 4, hipMemcpyDeviceToHost, S->stream), "hipMemcpyAsync flags");
   HK(hipStreamSynchronize(S->stream), "hipStreamSynchronize");
@@ -2260,7 +2335,9 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   hipError_t e = hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking);
   if (e != hipSuccess) return bad(e, "hipStreamCreate");
   if ((e = hipHostMalloc(&S->h_flag, 4)) != hipSuccess) return bad(e, "hipHostMalloc");
-  if ((e = hipHostMalloc(&S->h_count, 2 * sizeof(int32_t))) != hipSuccess) return bad(e, "hipHostMalloc");
+  // [count, resto, seq, -]: the per-iteration mailbox k_count1 writes (coherent, GPU-mapped)
+  if ((e = hipHostMalloc(&S->h_count, 4 * sizeof(int32_t), hipHostMallocCoherent | hipHostMallocMapped)) != hipSuccess)
+    return bad(e, "hipHostMalloc");
   // every device buffer carved from one allocation: a measuring pass, then the real one
   const size_t Bz = (size_t)batch, kws = (size_t)cpl_kkt_workspace_doubles(nw, m);
   const size_t nfd = S->fd ? Bz * 2 * nf : 0;
@@ -2342,7 +2419,7 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   S->Xp = a.take<double>(nfd * n); S->gL = a.take<double>(nfd * n); S->hfd = a.take<double>(Bz * nf);
   S->mass_fd = a.take<double>(nfd); S->jac_fd = a.take<double>(nfd * nnz); S->grad_fd = a.take<double>(nfd * n);
   S->tag_fd = a.take<uint8_t>(nfd);
-  S->orig = a.take<int32_t>(Bz); S->pos = a.take<int32_t>(Bz); S->d_count = a.take<int32_t>(2);
+  S->orig = a.take<int32_t>(Bz); S->pos = a.take<int32_t>(Bz); S->d_count = a.take<int32_t>(4);
   S->mass_c = a.take<double>(Bz); S->tag_c = a.take<uint8_t>(Bz);
   S->fw = a.take<double>(Bz * nw); S->fy = a.take<double>(Bz * m); S->fX = a.take<double>(Bz * n);
   S->fdinf = a.take<double>(Bz); S->fstatus = a.take<int64_t>(Bz); S->fiters = a.take<int64_t>(Bz);
@@ -2437,6 +2514,11 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
   const bool compacting = S->opt.compact != 0 && S->opt.use_graph;
   const int64_t min_rows = 256;
   int32_t resto_rows = 0;  // instances in the restoration phase after the previous iteration
+  // the mailbox's sequence: the device counter restarts with this solve (the previous solve ended
+  // with a stream synchronisation, so nothing is still writing the host side)
+  int32_t seq = 0;
+  ((volatile int32_t*)S->h_count)[2] = 0;
+  HK(hipMemsetAsync(S->d_count + 2, 0, sizeof(int32_t), st), "hipMemsetAsync seq");
   while (it < max_iter) {
     if (S->Bcur <= FUSE_ROWS && S->opt.use_graph) {  // one graph, one host round trip
       CK(run_phase(S, resto_rows > 0 ? P_FUSED_R : P_FUSED));
@@ -2458,10 +2540,14 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
       ++evals;
     }
     ++it;
-    HK(hipMemcpyAsync(S->h_count, S->d_count, 8, hipMemcpyDeviceToHost, st), "hipMemcpyAsync count");
-    HK(hipStreamSynchronize(st), "hipStreamSynchronize");
-    const int64_t cnt = S->h_count[0];
-    resto_rows = S->h_count[1];
+    if (S->Bcur <= COUNT1_MAX) {  // k_count1 delivered the counts to the mailbox
+      CK(wait_mail(S, ++seq));
+    } else {
+      HK(hipMemcpyAsync(S->h_count, S->d_count, 8, hipMemcpyDeviceToHost, st), "hipMemcpyAsync count");
+      HK(hipStreamSynchronize(st), "hipStreamSynchronize");
+    }
+    const int64_t cnt = ((volatile int32_t*)S->h_count)[0];
+    resto_rows = ((volatile int32_t*)S->h_count)[1];
     if (cnt == 0) break;
     if (compacting && S->Bcur > min_rows && 2 * cnt <= S->Bcur) {
       // shrink to the smallest halving of the current size that holds the active instances
@@ -2479,7 +2565,7 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
   CK(ipm_optimality_ex(Bc, nw, m, FMAX, S->nbounds, S->opt.tol, S->opt.acceptable_tol, S->opt.acceptable_iter, S->A,
                        S->gradw, S->c, S->w, S->y, S->zL, S->zU, S->hasL, S->hasU, S->wl0, S->wu0, S->mu, S->filt_t,
                        S->filt_p, S->fcount, S->active, S->status, S->acc, S->d_inf, S->err0, S->base, S->mu_o, S->ft,
-                       S->fp, S->fc, MU_ROUNDS, S->mu_min, nullptr, S->in_resto, st));
+                       S->fp, S->fc, MU_ROUNDS, S->mu_min, nullptr, S->in_resto, nullptr, st));
   // every row still in the batch to its instance's place in the full-batch results
   hipLaunchKernelGGL(k_scatter_final, dim3(blocks_for(Bc)), dim3(256), 0, st, Bc, n, m, nw, false, S->orig, S->active,
                      S->w, S->y, S->Xbase, S->d_inf, S->status, S->iters, S->n_resto, S->fw, S->fy, S->fX, S->fdinf,
