@@ -480,8 +480,8 @@ __device__ __forceinline__ double pd_error_wave(int m, int nf, int nw, const dou
 // part 2: the soft step is taken when the original filter / current iterate accept it (the soft
 // phase ends) or when it cuts the primal-dual error by soft_resto_pderror_reduction_factor (the
 // soft phase starts or continues); the step's alpha then also moves the bound multipliers
-__global__ __launch_bounds__(256) void k_soft_judge(
-    int64_t B, int n, int m, int nf, int nw, int nnz_rec, const uint8_t* __restrict__ soft_try,
+__device__ __forceinline__ void soft_judge_wave(
+    int64_t b, int64_t B, int n, int m, int nf, int nw, int nnz_rec, const uint8_t* __restrict__ soft_try,
     const uint8_t* __restrict__ soft_now, const double* __restrict__ a_soft, const int32_t* __restrict__ amap,
     const int32_t* __restrict__ row_slack, const int32_t* __restrict__ free32, const double* __restrict__ gl,
     const uint8_t* __restrict__ hasL, const uint8_t* __restrict__ hasU, const double* __restrict__ wl0,
@@ -496,8 +496,6 @@ __global__ __launch_bounds__(256) void k_soft_judge(
     double* __restrict__ cs_tmp, uint8_t* __restrict__ in_soft, int32_t* __restrict__ soft_cnt,
     double* __restrict__ st_f, double* __restrict__ st_g, double* __restrict__ st_w, double* __restrict__ st_alpha,
     uint8_t* __restrict__ st_aug, double* __restrict__ a_z) {
-  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
-  if (b >= B || !soft_try[b]) return;
   const int lane = threadIdx.x & 63;
   const double* wb = ws + b * nw;
   const double mub = mu[b], as = a_soft[b];
@@ -543,25 +541,39 @@ __global__ __launch_bounds__(256) void k_soft_judge(
   }
 }
 
+__global__ __launch_bounds__(256) void k_soft_judge(
+    int64_t B, int n, int m, int nf, int nw, int nnz_rec, const uint8_t* __restrict__ soft_try,
+    const uint8_t* __restrict__ soft_now, const double* __restrict__ a_soft, const int32_t* __restrict__ amap,
+    const int32_t* __restrict__ row_slack, const int32_t* __restrict__ free32, const double* __restrict__ gl,
+    const uint8_t* __restrict__ hasL, const uint8_t* __restrict__ hasU, const double* __restrict__ wl0,
+    const double* __restrict__ wu0, const double* __restrict__ ws, const double* __restrict__ f_s,
+    const double* __restrict__ grad_s, const double* __restrict__ g_s, const double* __restrict__ J_s,
+    const double* __restrict__ A, const double* __restrict__ gradw, const double* __restrict__ c,
+    const double* __restrict__ w, const double* __restrict__ y, const double* __restrict__ zL,
+    const double* __restrict__ zU, const double* __restrict__ dy, const double* __restrict__ dzL,
+    const double* __restrict__ dzU, const double* __restrict__ mu, const double* __restrict__ theta_k,
+    const double* __restrict__ phi_k, const double* __restrict__ gd, const uint8_t* __restrict__ switch_ok,
+    const double* __restrict__ theta_max, const double* __restrict__ ft, const double* __restrict__ fp,
+    double* __restrict__ cs_tmp, uint8_t* __restrict__ in_soft, int32_t* __restrict__ soft_cnt,
+    double* __restrict__ st_f, double* __restrict__ st_g, double* __restrict__ st_w, double* __restrict__ st_alpha,
+    uint8_t* __restrict__ st_aug, double* __restrict__ a_z) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B || !soft_try[b]) return;
+  soft_judge_wave(b, B, n, m, nf, nw, nnz_rec, soft_try, soft_now, a_soft, amap, row_slack, free32, gl, hasL, hasU, wl0,
+                  wu0, ws, f_s, grad_s, g_s, J_s, A, gradw, c, w, y, zL, zU, dy, dzL, dzU, mu, theta_k, phi_k, gd,
+                  switch_ok, theta_max, ft, fp, cs_tmp, in_soft, soft_cnt, st_f, st_g, st_w, st_alpha, st_aug, a_z);
+}
+
 // the end of the regular line search: failed = no accepted point (-> the restoration phase),
 // moved = an accepted one; a failed search leaves the soft phase.  IPOPT calls no restoration phase
 // at an acceptable point (BacktrackingLineSearch: "Restoration phase called at acceptable point" ->
 // STOP_AT_ACCEPTABLE_POINT): an instance whose search failed there ends with status acceptable.
-// ... in the same launch as the accepted points' X = unpack(st_w) (an element per thread; the first
-// element of each instance also does that instance's bookkeeping — which does not touch st_w)
-__global__ void k_fail_unpack(int64_t total, int n, int nw, const int32_t* __restrict__ freepos,
-                              const double* __restrict__ Xbase, const double* __restrict__ st_w, double* __restrict__ X,
-                              const uint8_t* __restrict__ act, const double* __restrict__ st_alpha,
-                              const double* __restrict__ err0, double acc_tol, uint8_t* __restrict__ failed,
-                              uint8_t* __restrict__ moved, uint8_t* __restrict__ in_soft, int32_t* __restrict__ soft_cnt,
-                              int64_t* __restrict__ status, uint8_t* __restrict__ active) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= total) return;
-  const int64_t b = e / n;
-  const int j = (int)(e - b * n);
-  const int k = freepos[j];
-  X[e] = k >= 0 ? st_w[b * nw + k] : Xbase[e];
-  if (j != 0) return;
+// The bookkeeping of instance b:
+__device__ __forceinline__ void fail_book(int64_t b, const uint8_t* __restrict__ act,
+                                          const double* __restrict__ st_alpha, const double* __restrict__ err0,
+                                          double acc_tol, uint8_t* __restrict__ failed, uint8_t* __restrict__ moved,
+                                          uint8_t* __restrict__ in_soft, int32_t* __restrict__ soft_cnt,
+                                          int64_t* __restrict__ status, uint8_t* __restrict__ active) {
   const bool a = act[b] != 0;
   bool f = a && !(st_alpha[b] > 0.0);
   if (f && err0[b] <= acc_tol) {
@@ -577,6 +589,76 @@ __global__ void k_fail_unpack(int64_t total, int n, int nw, const int32_t* __res
     in_soft[b] = 0;
     soft_cnt[b] = 0;
   }
+}
+
+// ... in the same launch as the accepted points' X = unpack(st_w) (an element per thread; the first
+// element of each instance also does that instance's bookkeeping — which does not touch st_w)
+__global__ void k_fail_unpack(int64_t total, int n, int nw, const int32_t* __restrict__ freepos,
+                              const double* __restrict__ Xbase, const double* __restrict__ st_w, double* __restrict__ X,
+                              const uint8_t* __restrict__ act, const double* __restrict__ st_alpha,
+                              const double* __restrict__ err0, double acc_tol, uint8_t* __restrict__ failed,
+                              uint8_t* __restrict__ moved, uint8_t* __restrict__ in_soft, int32_t* __restrict__ soft_cnt,
+                              int64_t* __restrict__ status, uint8_t* __restrict__ active) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int64_t b = e / n;
+  const int j = (int)(e - b * n);
+  const int k = freepos[j];
+  X[e] = k >= 0 ? st_w[b * nw + k] : Xbase[e];
+  if (j != 0) return;
+  fail_book(b, act, st_alpha, err0, acc_tol, failed, moved, in_soft, soft_cnt, status, active);
+}
+
+// The small-batch iteration (P_FUSED) runs the soft step's judge and the end of the search as one
+// wave per instance: the judge (soft_try instances), then — its st_w / st_alpha / soft counters
+// written by the same wave, made visible to the wave's other lanes by a workgroup fence — the
+// accepted point's X = unpack(st_w) and the bookkeeping.  The same operations on the same values
+// as k_soft_judge + k_fail_unpack.
+struct FailTail {
+  const int32_t* freepos;
+  const double* Xbase;
+  double* X;
+  const uint8_t* act;
+  const double* err0;
+  double acc_tol;
+  uint8_t* failed;
+  uint8_t* moved;
+  int64_t* status;
+  uint8_t* active;
+};
+__global__ __launch_bounds__(256) void k_soft_judge_fail(
+    int64_t B, int n, int m, int nf, int nw, int nnz_rec, const uint8_t* __restrict__ soft_try,
+    const uint8_t* __restrict__ soft_now, const double* __restrict__ a_soft, const int32_t* __restrict__ amap,
+    const int32_t* __restrict__ row_slack, const int32_t* __restrict__ free32, const double* __restrict__ gl,
+    const uint8_t* __restrict__ hasL, const uint8_t* __restrict__ hasU, const double* __restrict__ wl0,
+    const double* __restrict__ wu0, const double* __restrict__ ws, const double* __restrict__ f_s,
+    const double* __restrict__ grad_s, const double* __restrict__ g_s, const double* __restrict__ J_s,
+    const double* __restrict__ A, const double* __restrict__ gradw, const double* __restrict__ c,
+    const double* __restrict__ w, const double* __restrict__ y, const double* __restrict__ zL,
+    const double* __restrict__ zU, const double* __restrict__ dy, const double* __restrict__ dzL,
+    const double* __restrict__ dzU, const double* __restrict__ mu, const double* __restrict__ theta_k,
+    const double* __restrict__ phi_k, const double* __restrict__ gd, const uint8_t* __restrict__ switch_ok,
+    const double* __restrict__ theta_max, const double* __restrict__ ft, const double* __restrict__ fp,
+    double* __restrict__ cs_tmp, uint8_t* __restrict__ in_soft, int32_t* __restrict__ soft_cnt,
+    double* __restrict__ st_f, double* __restrict__ st_g, double* __restrict__ st_w, double* __restrict__ st_alpha,
+    uint8_t* __restrict__ st_aug, double* __restrict__ a_z, const FailTail ft2) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B) return;
+  if (soft_try[b])
+    soft_judge_wave(b, B, n, m, nf, nw, nnz_rec, soft_try, soft_now, a_soft, amap, row_slack, free32, gl, hasL, hasU,
+                    wl0, wu0, ws, f_s, grad_s, g_s, J_s, A, gradw, c, w, y, zL, zU, dy, dzL, dzU, mu, theta_k, phi_k,
+                    gd, switch_ok, theta_max, ft, fp, cs_tmp, in_soft, soft_cnt, st_f, st_g, st_w, st_alpha, st_aug,
+                    a_z);
+  __threadfence_block();
+  __builtin_amdgcn_wave_barrier();
+  const int lane = threadIdx.x & 63;
+  for (int j = lane; j < n; j += 64) {
+    const int k = ft2.freepos[j];
+    ft2.X[b * n + j] = k >= 0 ? st_w[b * nw + k] : ft2.Xbase[b * n + j];
+  }
+  if (lane == 0)
+    fail_book(b, ft2.act, st_alpha, ft2.err0, ft2.acc_tol, ft2.failed, ft2.moved, in_soft, soft_cnt, ft2.status,
+              ft2.active);
 }
 
 // IPOPT's limited-memory quasi-Newton model (LimMemQuasiNewtonUpdater [IPOPT] with the defaults
@@ -1650,6 +1732,7 @@ struct cpl_solver {
   int32_t *st32, *it32;
   // compaction: original instance of each row, compacted masses / tags, full-batch results
   int32_t *orig, *pos, *d_count, *h_count = nullptr;
+  bool tail_fused = false;  // P_FUSED: the soft judge launch also ends the search (k_soft_judge_fail)
   double *mass_c, *fw, *fy, *fX, *fdinf;
   uint8_t* tag_c;
   int64_t *fstatus, *fiters, *fresto;
@@ -1891,6 +1974,18 @@ int32_t step_phase(cpl_solver* S, int phase) {
                          S->soft_try, S->a_soft, S->ws_, S->Xs);
       LAUNCHED("k_soft_begin");
       CK(eval_full(S, S->Xs, S->f_n, S->grad_n, S->g_n, S->J_n));
+      if (S->tail_fused) {
+        const FailTail tail{S->freepos, S->Xbase, S->Xn, S->act, S->err0, o.acceptable_tol, S->failed, S->moved,
+                            S->status, S->active};
+        hipLaunchKernelGGL(k_soft_judge_fail, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->nnz_rec,
+                           S->soft_try, S->soft_now, S->a_soft, S->amap, S->row_slack, S->free32, S->gl, S->hasL,
+                           S->hasU, S->wl0, S->wu0, S->ws_, S->f_n, S->grad_n, S->g_n, S->J_n, S->A, S->gradw, S->c,
+                           S->w, S->y, S->zL, S->zU, S->dy, S->dzL, S->dzU, S->mu_o, S->theta_k, S->phi_k, S->gd,
+                           S->switch_ok, S->theta_max, S->ft, S->fp, S->cs_tmp, S->in_soft, S->soft_cnt, S->st_f,
+                           S->st_g, S->st_w, S->st_alpha, S->st_aug, S->a_z, tail);
+        LAUNCHED("k_soft_judge_fail");
+        return CPL_OK;
+      }
       hipLaunchKernelGGL(k_soft_judge, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->nnz_rec, S->soft_try,
                          S->soft_now, S->a_soft, S->amap, S->row_slack, S->free32, S->gl, S->hasL, S->hasU, S->wl0,
                          S->wu0, S->ws_, S->f_n, S->grad_n, S->g_n, S->J_n, S->A, S->gradw, S->c, S->w, S->y, S->zL,
@@ -1902,11 +1997,14 @@ int32_t step_phase(cpl_solver* S, int phase) {
     }
     case P_ACCEPT:
     case P_ACCEPT_NR: {
-      // the failed-search bookkeeping and the accepted points, then one full evaluation there
-      hipLaunchKernelGGL(k_fail_unpack, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, nw, S->freepos,
-                         S->Xbase, S->st_w, S->Xn, S->act, S->st_alpha, S->err0, o.acceptable_tol, S->failed, S->moved,
-                         S->in_soft, S->soft_cnt, S->status, S->active);
-      LAUNCHED("k_fail_unpack");
+      // the failed-search bookkeeping and the accepted points (done by the soft judge's launch in
+      // P_FUSED), then one full evaluation there
+      if (!S->tail_fused) {
+        hipLaunchKernelGGL(k_fail_unpack, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, nw, S->freepos,
+                           S->Xbase, S->st_w, S->Xn, S->act, S->st_alpha, S->err0, o.acceptable_tol, S->failed,
+                           S->moved, S->in_soft, S->soft_cnt, S->status, S->active);
+        LAUNCHED("k_fail_unpack");
+      }
       CK(eval_full(S, S->Xn, S->f_n, S->grad_n, S->g_n, S->J_n));
       if (S->bfgs) {
         hipLaunchKernelGGL(nf <= 64 ? k_lbfgs<64> : k_lbfgs<128>, dim3((unsigned)B), dim3(256), 0, st, B, m, nf, nw, S->nnz_rec, S->amap, S->moved,
@@ -2029,11 +2127,16 @@ int32_t step_phase(cpl_solver* S, int phase) {
       return CPL_OK;
     }
     case P_FUSED:
-    case P_FUSED_R:
+    case P_FUSED_R: {
       CK(step_phase(S, P_NEWTON));
-      CK(step_phase(S, P_SOFT));
-      if (phase == P_FUSED_R) CK(step_phase(S, P_RNEWTON));
-      return step_phase(S, P_ACCEPT);
+      // P_SOFT and P_ACCEPT adjacent (no restoration iteration between): one launch ends the search
+      S->tail_fused = phase == P_FUSED;
+      int32_t rc = step_phase(S, P_SOFT);
+      if (rc == CPL_OK && phase == P_FUSED_R) rc = step_phase(S, P_RNEWTON);
+      if (rc == CPL_OK) rc = step_phase(S, P_ACCEPT);
+      S->tail_fused = false;
+      return rc;
+    }
     default:
       return fail(CPL_ERR_INVALID_ARGUMENT, "step_phase: bad phase");
   }
