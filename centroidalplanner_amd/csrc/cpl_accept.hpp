@@ -110,6 +110,80 @@ struct LsBacktrackArgs {
   const double* tau;          // [batch] fraction-to-the-boundary parameter
 };
 
+// IPOPT FilterLSAcceptor::CalculateAlphaMin (alpha_min_frac 0.05)
+constexpr double LS_ALPHA_MIN_FRAC = 0.05;
+__device__ __forceinline__ double ls_alpha_min_of(double theta, double gd, double theta_min) {
+  if (!(gd < 0.0)) return LS_ALPHA_MIN_FRAC * LS_GAMMA_TH;
+  double a = fmin(LS_GAMMA_TH, LS_GAMMA_PHI * theta / -gd);
+  if (theta <= theta_min) a = fmin(a, LS_DELTA * pow(theta, LS_S_TH) / pow(-gd, LS_S_PHI));
+  return LS_ALPHA_MIN_FRAC * a;
+}
+
+// IPOPT's tiny-step test tolerances (tiny_step_tol, tiny_step_y_tol)
+constexpr double LS_TINY_STEP_TOL = 10.0 * DBL_EPSILON, LS_TINY_STEP_Y_TOL = 1e-2;
+
+__device__ __forceinline__ double ls_xor_max(double v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  return v;
+}
+
+// After the Newton step (batch_ipm.py regular_step): IPOPT's tiny-step test (every primal component
+// below 10 eps relative, the multiplier step below 1e-2, the point feasible to 1e-4; two in a row
+// force the next barrier decrease), the soft restoration phase's counter, alpha_min, and the line
+// search state (searching unless tiny or in the soft phase; a tiny step is taken whole: alpha_max).
+// One wave per instance, at the end of cpl_ipm.hip's post-step kernel (am = alpha_max and gd = the
+// directional derivative it has just computed).
+struct LsSetupArgs {
+  int32_t m;
+  const uint8_t* act;
+  const double *w, *dw, *dy, *c, *f, *g, *theta_k, *theta_min;
+  uint8_t* in_soft;
+  int32_t* soft_cnt;
+  uint8_t *tiny_last, *tiny_flag, *tiny_now, *soft_now;
+  double* a_min;
+  uint8_t* searching;
+  double *st_f, *st_g, *st_w, *st_alpha;
+  uint8_t* st_aug;
+  double* alpha;
+  uint8_t* any;
+};
+__device__ __forceinline__ void ls_setup_wave(int64_t b, int nw, const LsSetupArgs& L, double am, double gd) {
+  const int m = L.m;
+  const int lane = threadIdx.x & 63;
+  const bool a = L.act[b] != 0;
+  double rel = 0.0, dym = 0.0, cin = 0.0;
+  for (int k = lane; k < nw; k += 64) rel = fmax(rel, fabs(L.dw[b * nw + k]) / (1.0 + fabs(L.w[b * nw + k])));
+  for (int r = lane; r < m; r += 64) {
+    dym = fmax(dym, fabs(L.dy[b * m + r]));
+    cin = fmax(cin, fabs(L.c[b * m + r]));
+  }
+  rel = ls_xor_max(rel);
+  dym = ls_xor_max(dym);
+  cin = ls_xor_max(cin);
+  const bool tiny = a && rel < LS_TINY_STEP_TOL && dym < LS_TINY_STEP_Y_TOL && cin < 1e-4;
+  const bool sn = a && L.in_soft[b] && !tiny;
+  for (int r = lane; r < m; r += 64) L.st_g[b * m + r] = L.g[b * m + r];
+  for (int k = lane; k < nw; k += 64)
+    L.st_w[b * nw + k] = tiny ? L.w[b * nw + k] + am * L.dw[b * nw + k] : L.w[b * nw + k];
+  if (lane == 0) {
+    if (b == 0 && L.any) L.any[0] = L.any[1] = 0;
+    if (a) {
+      const bool tl = L.tiny_last[b] != 0;
+      L.tiny_flag[b] = (tiny && tl) ? 1 : 0;
+      L.tiny_last[b] = (tiny && !tl) ? 1 : 0;
+    }
+    L.tiny_now[b] = tiny ? 1 : 0;
+    L.soft_now[b] = sn ? 1 : 0;
+    if (sn) L.soft_cnt[b] += 1;
+    L.a_min[b] = ls_alpha_min_of(L.theta_k[b], gd, L.theta_min[b]);
+    L.searching[b] = (a && !tiny && !sn) ? 1 : 0;
+    L.st_f[b] = L.f[b];
+    L.st_alpha[b] = tiny ? am : 0.0;
+    L.st_aug[b] = 0;
+    L.alpha[b] = am;
+  }
+}
+
 // The solve loop's per-iteration unpack after the optimality test, fused into that kernel's tail
 // (cpl_ipm.hip; was a launch of its own): X = unpack(w) (free columns from w, fixed ones from
 // Xbase), tau = max(0.99, 1 - mu) and the iteration's snapshot act = active && !in_resto.

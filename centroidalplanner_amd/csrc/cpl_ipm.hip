@@ -380,7 +380,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_post_step_kernel(
     const double* __restrict__ wl0, const double* __restrict__ wu0, const double* __restrict__ theta,
     const double* __restrict__ theta_min, const uint8_t* __restrict__ active, const double* __restrict__ delta_w,
     double* __restrict__ dwl, double* __restrict__ dzL, double* __restrict__ dzU, double* __restrict__ a_max,
-    double* __restrict__ a_z, double* __restrict__ gd_out, uint8_t* __restrict__ switch_ok) {
+    double* __restrict__ a_z, double* __restrict__ gd_out, uint8_t* __restrict__ switch_ok, const LsSetupArgs ls) {
   const int64_t b = (int64_t)blockIdx.x * IPM_WAVES + (threadIdx.x >> 6);
   if (b >= batch) return;
   const int lane = threadIdx.x & 63;
@@ -415,6 +415,9 @@ __global__ __launch_bounds__(256) void cpl_ipm_post_step_kernel(
     switch_ok[b] = (theta[b] <= theta_min[b] && gd < 0.0) ? 1 : 0;
     if (active[b]) dwl[b] = delta_w[b];
   }
+  // the solve loop's line-search setup (ls.act != NULL; was the next launch): no output of this
+  // kernel is among its inputs except alpha_max and gd, passed in registers
+  if (ls.act) ls_setup_wave(b, nw, ls, fmin(rp, 1.0), gd);
 }
 
 // Acceptance (batch_ipm.py step, "accept" + state write-back, in place): filter augmentation after
@@ -552,6 +555,32 @@ __global__ __launch_bounds__(256) void cpl_ipm_fd_hessian_raw_kernel(int64_t tot
 // (barrier_tol_factor + 1)
 double ipm_mu_min(double tol) { return fmin(tol, 1e-4) / 11.0; }
 
+#define IPM_LAUNCH(kernel, name, ...)                                                                   \
+  do {                                                                                                 \
+    const int64_t blocks_ = (batch + IPM_WAVES - 1) / IPM_WAVES;                                       \
+    if (blocks_ > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, name ": batch too large");       \
+    hipLaunchKernelGGL(kernel, dim3((unsigned)blocks_), dim3(64 * IPM_WAVES), 0, (hipStream_t)stream,   \
+                       __VA_ARGS__);                                                                   \
+    hipError_t e_ = hipGetLastError();                                                                 \
+    if (e_ != hipSuccess) return fail(CPL_ERR_HIP, std::string(name " launch: ") + hipGetErrorString(e_)); \
+    return CPL_OK;                                                                                     \
+  } while (0)
+
+
+// cpl_ipm_post_step with the solve loop's line-search setup fused in (ls != NULL: LsSetupArgs)
+int32_t ipm_post_step_ex(int64_t batch, int32_t nw, const double* d_w, const double* d_dw, const double* d_zL,
+                         const double* d_zU, const double* d_gphi, const double* d_mu, const double* d_tau,
+                         const uint8_t* d_hasL, const uint8_t* d_hasU, const double* d_wl0, const double* d_wu0,
+                         const double* d_theta, const double* d_theta_min, const uint8_t* d_active,
+                         const double* d_delta_w, double* d_dwl, double* d_dzL, double* d_dzU, double* d_a_max,
+                         double* d_a_z, double* d_gd, uint8_t* d_switch_ok, const LsSetupArgs* ls, void* stream) {
+  LsSetupArgs L{};
+  if (ls) L = *ls;
+  IPM_LAUNCH(cpl_ipm_post_step_kernel, "cpl_ipm_post_step", batch, (int)nw, d_w, d_dw, d_zL, d_zU, d_gphi, d_mu, d_tau,
+             d_hasL, d_hasU, d_wl0, d_wu0, d_theta, d_theta_min, d_active, d_delta_w, d_dwl, d_dzL, d_dzU, d_a_max,
+             d_a_z, d_gd, d_switch_ok, L);
+}
+
 // cpl_ipm_optimality with the engine's extras: mu_rounds barrier decreases at most, the floor
 // mu_min, tiny_flag (a forced first decrease after two tiny steps) and skip (instances in the
 // restoration phase, left untouched: their own test and barrier update run in its kernels)
@@ -671,16 +700,6 @@ int32_t cpl_ipm_max_step(int64_t batch, int32_t nw, const double* d_v, const dou
   return CPL_OK;
 }
 
-#define IPM_LAUNCH(kernel, name, ...)                                                                   \
-  do {                                                                                                 \
-    const int64_t blocks_ = (batch + IPM_WAVES - 1) / IPM_WAVES;                                       \
-    if (blocks_ > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, name ": batch too large");       \
-    hipLaunchKernelGGL(kernel, dim3((unsigned)blocks_), dim3(64 * IPM_WAVES), 0, (hipStream_t)stream,   \
-                       __VA_ARGS__);                                                                   \
-    hipError_t e_ = hipGetLastError();                                                                 \
-    if (e_ != hipSuccess) return fail(CPL_ERR_HIP, std::string(name " launch: ") + hipGetErrorString(e_)); \
-    return CPL_OK;                                                                                     \
-  } while (0)
 
 int32_t cpl_ipm_newton_setup(int64_t batch, int32_t nw, int32_t m, int32_t nf, const double* d_w, const double* d_zL,
                              const double* d_zU, const double* d_gw, const double* d_A, const double* d_y,
@@ -713,9 +732,9 @@ int32_t cpl_ipm_post_step(int64_t batch, int32_t nw, const double* d_w, const do
       !d_theta || !d_theta_min || !d_active || !d_delta_w || !d_dwl || !d_dzL || !d_dzU || !d_a_max || !d_a_z ||
       !d_gd || !d_switch_ok)
     return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_post_step: missing buffer");
-  IPM_LAUNCH(cpl_ipm_post_step_kernel, "cpl_ipm_post_step", batch, (int)nw, d_w, d_dw, d_zL, d_zU, d_gphi, d_mu, d_tau,
-             d_hasL, d_hasU, d_wl0, d_wu0, d_theta, d_theta_min, d_active, d_delta_w, d_dwl, d_dzL, d_dzU, d_a_max,
-             d_a_z, d_gd, d_switch_ok);
+  return ipm_post_step_ex(batch, nw, d_w, d_dw, d_zL, d_zU, d_gphi, d_mu, d_tau, d_hasL, d_hasU, d_wl0, d_wu0, d_theta,
+                          d_theta_min, d_active, d_delta_w, d_dwl, d_dzL, d_dzU, d_a_max, d_a_z, d_gd, d_switch_ok,
+                          nullptr, stream);
 }
 
 int32_t cpl_ipm_accept(int64_t batch, int32_t nw, int32_t m, int32_t nfilt, const uint8_t* d_active,

@@ -40,6 +40,13 @@ int32_t ipm_newton_setup_lm(int64_t batch, int32_t nw, int32_t m, int32_t nf, co
 // cpl_kernels.hip: the backtracking line search after the first trial, one wave per instance
 int32_t ls_backtrack(const cpl_problem_desc* d, const LsBacktrackArgs& a, hipStream_t stream);
 bool kkt_wave_size(int nw, int m);
+// cpl_ipm.hip: the post-step kernel with the line-search setup (LsSetupArgs) as its tail
+int32_t ipm_post_step_ex(int64_t batch, int32_t nw, const double* d_w, const double* d_dw, const double* d_zL,
+                         const double* d_zU, const double* d_gphi, const double* d_mu, const double* d_tau,
+                         const uint8_t* d_hasL, const uint8_t* d_hasU, const double* d_wl0, const double* d_wu0,
+                         const double* d_theta, const double* d_theta_min, const uint8_t* d_active,
+                         const double* d_delta_w, double* d_dwl, double* d_dzL, double* d_dzU, double* d_a_max,
+                         double* d_a_z, double* d_gd, uint8_t* d_switch_ok, const LsSetupArgs* ls, void* stream);
 // cpl_ipm.hip: the optimality test + monotone barrier update with IPOPT's per-iteration rounds
 double ipm_mu_min(double tol);
 int32_t ipm_optimality_ex(int64_t batch, int32_t nw, int32_t m, int32_t fmax, int32_t nbounds, double tol,
@@ -257,8 +264,7 @@ __global__ void k_unpack(int64_t total, int n, int nw, const int32_t* __restrict
 // ---- IPOPT constants of the line search / restoration phase (batch_ipm.py restates them) ------
 // (the acceptance test itself: cpl_accept.hpp)
 constexpr double GAMMA_TH = LS_GAMMA_TH, GAMMA_PHI = LS_GAMMA_PHI, DELTA_SW = LS_DELTA, S_TH = LS_S_TH, S_PHI = LS_S_PHI;
-constexpr double ALPHA_MIN_FRAC = 0.05, KAPPA_SOC = 0.99, KAPPA_SIGMA = 1e10;
-constexpr double TINY_STEP_TOL = 10.0 * DBL_EPSILON, TINY_STEP_Y_TOL = 1e-2;
+constexpr double KAPPA_SOC = 0.99, KAPPA_SIGMA = 1e10;
 constexpr double RHO_R = 1000.0, KAPPA_RESTO = 0.9, BOUND_MULT_RESET = 1000.0, SOFT_RESTO_FACTOR = 0.9999;
 constexpr int MAX_SOFT_RESTO = LS_MAX_SOFT_RESTO, MU_ROUNDS = 6;
 
@@ -267,12 +273,9 @@ __device__ __forceinline__ double wave_min_d(double v) {
   return v;
 }
 
-// IPOPT FilterLSAcceptor::CalculateAlphaMin (alpha_min_frac 0.05)
+// IPOPT FilterLSAcceptor::CalculateAlphaMin (cpl_accept.hpp)
 __device__ __forceinline__ double alpha_min_of(double theta, double gd, double theta_min) {
-  if (!(gd < 0.0)) return ALPHA_MIN_FRAC * GAMMA_TH;
-  double a = fmin(GAMMA_TH, GAMMA_PHI * theta / -gd);
-  if (theta <= theta_min) a = fmin(a, DELTA_SW * pow(theta, S_TH) / pow(-gd, S_PHI));
-  return ALPHA_MIN_FRAC * a;
+  return ls_alpha_min_of(theta, gd, theta_min);
 }
 
 // IPOPT FilterLSAcceptor::CheckAcceptabilityOfTrialPoint on one wave: theta_max, the filter (entries
@@ -284,56 +287,8 @@ __device__ __forceinline__ bool acceptable_wave(double th, double ph, double tk,
   return ls_acceptable_wave(th, ph, tk, pk, g, al, switch_ok, theta_max, ft, fp, FMAX, h_type);
 }
 
-// After the Newton step (batch_ipm.py regular_step): IPOPT's tiny-step test (every primal component
-// below 10 eps relative, the multiplier step below 1e-2, the point feasible to 1e-4; two in a row
-// force the next barrier decrease), the soft restoration phase's counter, alpha_min, and the line
-// search state (searching unless tiny or in the soft phase; a tiny step is taken whole: alpha_max).
-__global__ __launch_bounds__(256) void k_ls_setup(
-    int64_t B, int m, int nw, const uint8_t* __restrict__ act, const double* __restrict__ w,
-    const double* __restrict__ dw, const double* __restrict__ dy, const double* __restrict__ c,
-    const double* __restrict__ f, const double* __restrict__ g, const double* __restrict__ theta_k,
-    const double* __restrict__ gd, const double* __restrict__ theta_min, const double* __restrict__ a_max,
-    uint8_t* __restrict__ in_soft, int32_t* __restrict__ soft_cnt, uint8_t* __restrict__ tiny_last,
-    uint8_t* __restrict__ tiny_flag, uint8_t* __restrict__ tiny_now, uint8_t* __restrict__ soft_now,
-    double* __restrict__ a_min, uint8_t* __restrict__ searching, double* __restrict__ st_f, double* __restrict__ st_g,
-    double* __restrict__ st_w, double* __restrict__ st_alpha, uint8_t* __restrict__ st_aug, double* __restrict__ alpha,
-    uint8_t* __restrict__ any) {
-  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
-  if (b >= B) return;
-  const int lane = threadIdx.x & 63;
-  const bool a = act[b] != 0;
-  double rel = 0.0, dym = 0.0, cin = 0.0;
-  for (int k = lane; k < nw; k += 64) rel = fmax(rel, fabs(dw[b * nw + k]) / (1.0 + fabs(w[b * nw + k])));
-  for (int r = lane; r < m; r += 64) {
-    dym = fmax(dym, fabs(dy[b * m + r]));
-    cin = fmax(cin, fabs(c[b * m + r]));
-  }
-  rel = wave_max(rel);
-  dym = wave_max(dym);
-  cin = wave_max(cin);
-  const bool tiny = a && rel < TINY_STEP_TOL && dym < TINY_STEP_Y_TOL && cin < 1e-4;
-  const bool sn = a && in_soft[b] && !tiny;
-  const double am = a_max[b];
-  for (int r = lane; r < m; r += 64) st_g[b * m + r] = g[b * m + r];
-  for (int k = lane; k < nw; k += 64) st_w[b * nw + k] = tiny ? w[b * nw + k] + am * dw[b * nw + k] : w[b * nw + k];
-  if (lane == 0) {
-    if (b == 0 && any) any[0] = any[1] = 0;
-    if (a) {
-      const bool tl = tiny_last[b] != 0;
-      tiny_flag[b] = (tiny && tl) ? 1 : 0;
-      tiny_last[b] = (tiny && !tl) ? 1 : 0;
-    }
-    tiny_now[b] = tiny ? 1 : 0;
-    soft_now[b] = sn ? 1 : 0;
-    if (sn) soft_cnt[b] += 1;
-    a_min[b] = alpha_min_of(theta_k[b], gd[b], theta_min[b]);
-    searching[b] = (a && !tiny && !sn) ? 1 : 0;
-    st_f[b] = f[b];
-    st_alpha[b] = tiny ? am : 0.0;
-    st_aug[b] = 0;
-    alpha[b] = am;
-  }
-}
+// (the line-search setup after the Newton step: cpl_accept.hpp ls_setup_wave, run by the post-step
+// kernel)
 
 // c_soc = a_soc c_soc + c(trial point); the correction's right-hand side r2 = -c_soc
 __global__ __launch_bounds__(256) void k_soc_rhs(int64_t B, int m, int nf, int nw, const int32_t* __restrict__ row_slack,
@@ -388,7 +343,7 @@ __global__ void k_soc_after(int64_t B, uint8_t* __restrict__ soc, const uint8_t*
 }
 
 // after a trial: alpha halved where still searching, the search given up below alpha_min (IPOPT
-// tries the next point only while alpha > alpha_min); flags (zeroed by k_ls_setup / k_resto_post):
+// tries the next point only while alpha > alpha_min); flags (zeroed by ls_setup_wave / k_resto_post):
 // any[fi] = an instance is still searching; with soft_now, any[1] = an instance has no accepted
 // point yet and will try the soft restoration step
 __global__ void k_halve2(int64_t B, uint8_t* __restrict__ searching, double* __restrict__ alpha,
@@ -1913,14 +1868,17 @@ int32_t step_phase(cpl_solver* S, int phase) {
                                 S->theta_k, S->phi_k, S->act, st));
       CK(cpl_kkt_solve(0, B, nw, m, S->M, S->A, S->r1, S->r2, S->mu_o, S->dwl, S->act, S->dw, S->dy, S->delta_w,
                        S->delta_c, S->info, S->ws, st));
-      CK(cpl_ipm_post_step(B, nw, S->w, S->dw, S->zL, S->zU, S->gphi, S->mu_o, S->tau, S->hasL, S->hasU, S->wl0,
-                           S->wu0, S->theta_k, S->theta_min, S->act, S->delta_w, S->dwl, S->dzL, S->dzU, S->a_max,
-                           S->a_z, S->gd, S->switch_ok, st));
-      hipLaunchKernelGGL(k_ls_setup, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nw, S->act, S->w, S->dw, S->dy, S->c,
-                         S->f, S->g, S->theta_k, S->gd, S->theta_min, S->a_max, S->in_soft, S->soft_cnt, S->tiny_last,
-                         S->tiny_flag, S->tiny_now, S->soft_now, S->a_min, S->searching, S->st_f, S->st_g, S->st_w,
-                         S->st_alpha, S->st_aug, S->alpha, S->d_any);
-      LAUNCHED("k_ls_setup");
+      {  // the step's multipliers / fraction-to-the-boundary, then (same launch) the search's setup
+        LsSetupArgs ls;
+        ls.m = m; ls.act = S->act; ls.w = S->w; ls.dw = S->dw; ls.dy = S->dy; ls.c = S->c; ls.f = S->f; ls.g = S->g;
+        ls.theta_k = S->theta_k; ls.theta_min = S->theta_min; ls.in_soft = S->in_soft; ls.soft_cnt = S->soft_cnt;
+        ls.tiny_last = S->tiny_last; ls.tiny_flag = S->tiny_flag; ls.tiny_now = S->tiny_now; ls.soft_now = S->soft_now;
+        ls.a_min = S->a_min; ls.searching = S->searching; ls.st_f = S->st_f; ls.st_g = S->st_g; ls.st_w = S->st_w;
+        ls.st_alpha = S->st_alpha; ls.st_aug = S->st_aug; ls.alpha = S->alpha; ls.any = S->d_any;
+        CK(ipm_post_step_ex(B, nw, S->w, S->dw, S->zL, S->zU, S->gphi, S->mu_o, S->tau, S->hasL, S->hasU, S->wl0,
+                            S->wu0, S->theta_k, S->theta_min, S->act, S->delta_w, S->dwl, S->dzL, S->dzU, S->a_max,
+                            S->a_z, S->gd, S->switch_ok, &ls, st));
+      }
       // the whole search in one launch (first trial, its corrections, the backtracking), or the
       // first trial step by step and the remaining trials in one launch
       const bool fused = o.ls_kernel == 2 || (o.ls_kernel == 1 && B <= FUSE_ROWS);  // (2: the default)
