@@ -110,6 +110,27 @@ struct LsBacktrackArgs {
   const double* tau;          // [batch] fraction-to-the-boundary parameter
 };
 
+// s + sum_{r < m} a[r * stride] * v[r], accumulated in r order exactly as the plain loop
+// (s += a v: the same roundings), with the loads issued eight at a time: the plain loop's load ->
+// multiply -> add chain waited one L2 round trip per row (a one-wave-per-instance kernel at small
+// batch sizes is that chain)
+__device__ __forceinline__ double seq_dot_acc(double s, const double* __restrict__ a, int stride,
+                                              const double* __restrict__ v, int m) {
+  int r = 0;
+  for (; r + 8 <= m; r += 8) {
+    double av[8], vv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      av[u] = a[(r + u) * stride];
+      vv[u] = v[r + u];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += av[u] * vv[u];
+  }
+  for (; r < m; ++r) s += a[r * stride] * v[r];
+  return s;
+}
+
 // IPOPT FilterLSAcceptor::CalculateAlphaMin (alpha_min_frac 0.05)
 constexpr double LS_ALPHA_MIN_FRAC = 0.05;
 __device__ __forceinline__ double ls_alpha_min_of(double theta, double gd, double theta_min) {

@@ -154,7 +154,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_optimality_kernel(
     const int k = lane + 64 * h;
     if (k < nw) {
       double dual = gw[b * nw + k];
-      for (int r = 0; r < m; ++r) dual += Ab[r * nw + k] * yb[r];
+      dual = seq_dot_acc(dual, Ab + k, nw, yb, m);
       const double zl = zL[b * nw + k], zu = zU[b * nw + k], wk = w[b * nw + k];
       dual = dual - zl + zu;
       dmax = fmax(dmax, fabs(dual));
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
       lg += log(du);
     }
     double aty = 0.0;
-    for (int r = 0; r < m; ++r) aty += Ab[r * nw + k] * yb[r];
+    aty = seq_dot_acc(aty, Ab + k, nw, yb, m);
     gphi[b * nw + k] = gp;
     r1[b * nw + k] = -(gp + aty);
     const double aw = fmax(fabs(wk), 1.0);

@@ -966,7 +966,7 @@ __global__ __launch_bounds__(256) void k_resto_prep1(
       const double wk = w[b * nw + k];
       const double dr = k < nf ? 1.0 / fmax(fabs(wR[b * nw + k]), 1.0) : 0.0;
       double dual = k < nf ? eta * (dr * dr) * (wk - wR[b * nw + k]) : 0.0;
-      for (int r = 0; r < m; ++r) dual += Ab[r * nw + k] * y[b * m + r];
+      dual = seq_dot_acc(dual, Ab + k, nw, y + b * m, m);
       const double zl = zLR[b * nw + k], zu = zUR[b * nw + k];
       dual = dual - zl + zu;
       dmax = fmax(dmax, fabs(dual));
