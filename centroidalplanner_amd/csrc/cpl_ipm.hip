@@ -334,20 +334,42 @@ __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
     __builtin_amdgcn_wave_barrier();
     const double* U = UW;
     const double* W = UW + lm_pairs * nf;
-    for (int e = lane; e < nw * nw; e += 64) {
-      const int k = e / nw, j = e - k * nw;
-      double v = (j == k) ? sg[k] : 0.0;
-      if (k < nf && j < nf) {
-        double h = j == k ? sigma : 0.0;
-        for (int i = 0; i < nv; ++i) h = (h - U[i * nf + k] * U[i * nf + j]) + W[i * nf + k] * W[i * nf + j];
-        v += h;
+    // four entries per lane at a time (independent chains: their LDS reads overlap), each entry's
+    // operations in the order of the one-entry loop
+    constexpr int EU = 4;
+    for (int e0 = lane; e0 < nw * nw; e0 += 64 * EU) {
+      int kk[EU], jj[EU];
+      bool in[EU];
+      double h[EU];
+#pragma unroll
+      for (int u = 0; u < EU; ++u) {
+        const int e = e0 + 64 * u;
+        kk[u] = e / nw;
+        jj[u] = e - kk[u] * nw;
+        in[u] = e < nw * nw && kk[u] < nf && jj[u] < nf;
+        h[u] = jj[u] == kk[u] ? sigma : 0.0;
       }
-      Mb[e] = v;
+      for (int i = 0; i < nv; ++i) {
+#pragma unroll
+        for (int u = 0; u < EU; ++u)
+          if (in[u])
+            h[u] = (h[u] - U[i * nf + kk[u]] * U[i * nf + jj[u]]) + W[i * nf + kk[u]] * W[i * nf + jj[u]];
+      }
+#pragma unroll
+      for (int u = 0; u < EU; ++u) {
+        const int e = e0 + 64 * u;
+        if (e < nw * nw) {
+          double v = (jj[u] == kk[u]) ? sg[kk[u]] : 0.0;
+          if (in[u]) v += h[u];
+          Mb[e] = v;
+        }
+      }
     }
   } else {
     const double* Hb = H ? H + b * (int64_t)nf * nf : nullptr;
     // h_sym: H is the raw central-difference matrix (cpl_ipm_fd_hessian_raw), symmetrised here as
-    // batch_ipm.py's fd_hessian does: 0.5 (H + H^T)
+    // batch_ipm.py's fd_hessian does: 0.5 (H + H^T) (unrolled: four entries' loads in flight)
+#pragma unroll 4
     for (int e = lane; e < nw * nw; e += 64) {
       const int k = e / nw, j = e - k * nw;
       double v = (j == k) ? sg[k] : 0.0;
