@@ -108,6 +108,16 @@ struct LsBacktrackArgs {
   const double* r1;           // [batch, nw] its first right-hand side
   const double* kkt_ws;       // cpl_kkt_solve's factor workspace (mode 0 of this iteration)
   const double* tau;          // [batch] fraction-to-the-boundary parameter
+  // soft_ws != NULL (the small-batch iteration, P_FUSED): the kernel's tail also starts IPOPT's soft
+  // restoration step (the solver's k_soft_begin, which would be the next launch): soft_try = no
+  // accepted trial (or in the soft phase within its budget), a_soft = min(alpha_max, alpha_z), the
+  // point soft_ws = w + a_soft dw on those instances (= w elsewhere) and its X = unpack(soft_ws)
+  const double* a_max;
+  const double* a_z;
+  double* soft_ws;
+  double* soft_X;
+  uint8_t* soft_try;
+  double* a_soft;
 };
 
 // s + sum_{r < m} a[r * stride] * v[r], accumulated in r order exactly as the plain loop

@@ -2456,6 +2456,21 @@ __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, c
         A.any[1] = 1;
     }
   }
+  if (!RESTO && A.soft_ws) {  // the soft restoration step's start (LsBacktrackArgs::soft_ws)
+    const bool sn = A.soft_now[b] != 0;
+    const bool t = act && !A.tiny[b] && ((sn && A.soft_cnt[b] <= LS_MAX_SOFT_RESTO) || (!sn && !(st_alpha > 0.0)));
+    const double as = fmin(A.a_max[b], A.a_z[b]);
+    const int nw = A.nw, n = A.n;
+    for (int k = lane; k < nw; k += 64) A.soft_ws[b * nw + k] = A.w[b * nw + k] + (t ? as : 0.0) * A.dw[b * nw + k];
+    for (int j = lane; j < n; j += 64) {
+      const int k = A.freepos[j];
+      A.soft_X[b * n + j] = k >= 0 ? A.w[b * nw + k] + (t ? as : 0.0) * A.dw[b * nw + k] : A.Xbase[b * n + j];
+    }
+    if (lane == 0) {
+      A.soft_try[b] = t ? 1 : 0;
+      A.a_soft[b] = as;
+    }
+  }
 }
 
 int32_t ls_backtrack(const cpl_problem_desc* d, const LsBacktrackArgs& a, hipStream_t stream) {

@@ -1688,6 +1688,8 @@ struct cpl_solver {
   // compaction: original instance of each row, compacted masses / tags, full-batch results
   int32_t *orig, *pos, *d_count, *h_count = nullptr;
   bool tail_fused = false;  // P_FUSED: the soft judge launch also ends the search (k_soft_judge_fail)
+  bool soft_fused = false;  // P_FUSED(_R): the search kernel starts the soft step (no k_soft_begin)
+  bool soft_begun = false;  // ... and the Newton phase's search kernel did (P_SOFT skips k_soft_begin)
   double *mass_c, *fw, *fy, *fX, *fdinf;
   uint8_t* tag_c;
   int64_t *fstatus, *fiters, *fresto;
@@ -1903,6 +1905,12 @@ int32_t step_phase(cpl_solver* S, int phase) {
         la.first = 1;
         la.max_soc = o.max_soc;
         la.c = S->c; la.M = S->M; la.r1 = S->r1; la.kkt_ws = S->ws; la.tau = S->tau;
+        la.a_max = S->a_max; la.a_z = S->a_z;
+        la.soft_ws = la.soft_X = la.a_soft = nullptr; la.soft_try = nullptr;
+        if (S->soft_fused) {
+          la.soft_ws = S->ws_; la.soft_X = S->Xs; la.soft_try = S->soft_try; la.a_soft = S->a_soft;
+          S->soft_begun = true;
+        }
         CK(ls_backtrack(&S->desc, la, st));
       } else if (o.max_ls > 1) {  // the remaining trials of every instance still searching, in one launch
         HK(hipMemsetAsync(S->d_any, 0, 2, st), "hipMemsetAsync flags");
@@ -1922,15 +1930,18 @@ int32_t step_phase(cpl_solver* S, int phase) {
         la.pR = la.nR = la.dp = la.dn = la.wR = nullptr;
         la.st_p = la.st_n = nullptr;
         la.first = 0; la.max_soc = 0; la.c = la.M = la.r1 = la.kkt_ws = la.tau = nullptr;
+        la.a_max = la.a_z = nullptr; la.soft_ws = la.soft_X = la.a_soft = nullptr; la.soft_try = nullptr;
         CK(ls_backtrack(&S->desc, la, st));
       }
       return CPL_OK;
     }
     case P_SOFT: {
-      hipLaunchKernelGGL(k_soft_begin, dim3(blocks_for(B)), dim3(256), 0, st, B, n, nf, nw, S->act, S->tiny_now,
-                         S->soft_now, S->soft_cnt, S->st_alpha, S->a_max, S->a_z, S->w, S->dw, S->freepos, S->Xbase,
-                         S->soft_try, S->a_soft, S->ws_, S->Xs);
-      LAUNCHED("k_soft_begin");
+      if (!S->soft_begun) {  // (else the Newton phase's search kernel started the soft step)
+        hipLaunchKernelGGL(k_soft_begin, dim3(blocks_for(B)), dim3(256), 0, st, B, n, nf, nw, S->act, S->tiny_now,
+                           S->soft_now, S->soft_cnt, S->st_alpha, S->a_max, S->a_z, S->w, S->dw, S->freepos, S->Xbase,
+                           S->soft_try, S->a_soft, S->ws_, S->Xs);
+        LAUNCHED("k_soft_begin");
+      }
       CK(eval_full(S, S->Xs, S->f_n, S->grad_n, S->g_n, S->J_n));
       if (S->tail_fused) {
         const FailTail tail{S->freepos, S->Xbase, S->Xn, S->act, S->err0, o.acceptable_tol, S->failed, S->moved,
@@ -2055,6 +2066,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
         la.pR = S->pR; la.nR = S->nR; la.dp = S->dp; la.dn = S->dn; la.wR = S->wR;
         la.st_p = S->st_p; la.st_n = S->st_n;
         la.first = 0; la.max_soc = 0; la.c = la.M = la.r1 = la.kkt_ws = la.tau = nullptr;
+        la.a_max = la.a_z = nullptr; la.soft_ws = la.soft_X = la.a_soft = nullptr; la.soft_try = nullptr;
         CK(ls_backtrack(&S->desc, la, st));
       }
       return step_phase(S, P_RACCEPT);
@@ -2086,10 +2098,19 @@ int32_t step_phase(cpl_solver* S, int phase) {
     }
     case P_FUSED:
     case P_FUSED_R: {
-      CK(step_phase(S, P_NEWTON));
+      S->soft_fused = true;
+      S->soft_begun = false;
+      {
+        const int32_t rc0 = step_phase(S, P_NEWTON);
+        if (rc0 != CPL_OK) {
+          S->soft_fused = S->soft_begun = false;
+          return rc0;
+        }
+      }
       // P_SOFT and P_ACCEPT adjacent (no restoration iteration between): one launch ends the search
       S->tail_fused = phase == P_FUSED;
       int32_t rc = step_phase(S, P_SOFT);
+      S->soft_fused = S->soft_begun = false;
       if (rc == CPL_OK && phase == P_FUSED_R) rc = step_phase(S, P_RNEWTON);
       if (rc == CPL_OK) rc = step_phase(S, P_ACCEPT);
       S->tail_fused = false;
