@@ -671,18 +671,32 @@ __global__ __launch_bounds__(256) void k_lbfgs(int64_t B, int m, int nf, int nw,
       const double* jnb = J_new + b * (int64_t)nnz_rec;
       const double* job = J_old + b * (int64_t)nnz_rec;
       double jn = 0.0, jo = 0.0;
-      for (int r = part; r < m; r += parts) {
-        const int q = amap[r * nf + k];
-        if (q == -1) continue;  // structural zero: A's entry is 0
-        double an = 1.0, ao = 1.0;
-        if (q >= 0) {
-          an = jnb[q];
-          ao = job[q];
-          an = an == an ? an : 0.0;
-          ao = ao == ao ? ao : 0.0;
+      // rows r = part, part + parts, ... in order, eight at a time: the eight amap indices, then the
+      // eight record entries they name, are loads in flight together (one row at a time waited two
+      // dependent L2 round trips per row); the accumulation is the plain loop's
+      const int R = m > part ? (m - part + parts - 1) / parts : 0;
+      for (int t0 = 0; t0 < R; t0 += 8) {
+        int qv[8];
+        double anv[8], aov[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) qv[u] = t0 + u < R ? amap[(part + (t0 + u) * parts) * nf + k] : -1;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          anv[u] = qv[u] >= 0 ? jnb[qv[u]] : 1.0;
+          aov[u] = qv[u] >= 0 ? job[qv[u]] : 1.0;
         }
-        jn += an * yn[r];
-        jo += ao * yn[r];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (qv[u] == -1) continue;  // structural zero (or past the last row): A's entry is 0
+          double an = anv[u], ao = aov[u];
+          if (qv[u] >= 0) {
+            an = an == an ? an : 0.0;
+            ao = ao == ao ? ao : 0.0;
+          }
+          const int r = part + (t0 + u) * parts;
+          jn += an * yn[r];
+          jo += ao * yn[r];
+        }
       }
       pjn[part][k] = jn;
       pjo[part][k] = jo;
