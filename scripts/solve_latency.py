@@ -21,7 +21,12 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--only", default="", help="run one case, e.g. limited-memory:1 (for a kernel trace)")
 ap.add_argument("--ls-kernel", type=int, default=2, help="the engine's ls_kernel option (0 / 1 / 2)")
+ap.add_argument("--variant", type=int, default=0, help="eval kernel variant (cpl_set_tuning), 0 = auto")
 args = ap.parse_args()
+if args.variant:
+    from centroidalplanner_amd import _abi  # noqa: E402
+
+    _abi.check(_abi.lib.cpl_set_tuning(args.variant, 0, 256, 1, 0))
 
 prob = solve_problem().GetCplProblem()
 dev = torch.device("cuda:0")
