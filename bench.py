@@ -73,7 +73,8 @@ def algorithmic_bytes(N, env, outputs=("g", "jac"), with_mass=True):
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without WORLD_SIZE in the environment, N > 1 spawns N rank processes")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="ground4_1m", help="ground4_1m | ground4 | sq8 | mixed16 | none4 | solve5")
@@ -94,7 +95,179 @@ def parse():
                     help="solve5: exact Lagrangian Hessian (analytic kernel) or IFOPT's limited-memory default")
     ap.add_argument("--cpu-sample", type=int, default=512, help="solve5: instances in the CPU baseline's sample")
     ap.add_argument("--pmc-child", default="", help=argparse.SUPPRESS)
+    # CPU rehearsal of the multi-rank launch (tests only: gloo, the shard's evaluation supplied by a
+    # file the test names; never on a GPU run)
+    ap.add_argument("--rehearse-cpu", default="", help=argparse.SUPPRESS)
     return ap.parse_args()
+
+
+# ------------------------------------------------------------------------------------------
+# multi-rank launch: one process per GPU
+# ------------------------------------------------------------------------------------------
+def resolve_world(args):
+    """(world, rank, local_rank, spawn): WORLD_SIZE / RANK / LOCAL_RANK from the environment (the
+    driver's torch.distributed.run launch); without them, --gpus N > 1 asks this process to spawn the
+    N ranks itself.  A --gpus that disagrees with WORLD_SIZE is refused."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        world = int(env_world)
+        if args.gpus is not None and args.gpus != world:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world}")
+        return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")), False
+    n = 1 if args.gpus is None else int(args.gpus)
+    if n < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    return n, 0, 0, n > 1
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(world, argv=None, poll_s=0.5):
+    """`python bench.py --gpus N` with no WORLD_SIZE: start N fresh rank processes of this script
+    (RANK = LOCAL_RANK = r, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1, a free MASTER_PORT) — this parent
+    makes no GPU call, so every rank (rank 0's PMC passes and CPU leg included) starts from a clean
+    process.  Rank 0's stdout (the JSON line) is forwarded; the other ranks' stdout goes to stderr.
+    If a rank fails, the others are stopped and the exit code is non-zero."""
+    argv = sys.argv[1:] if argv is None else list(argv)
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL (the only kind the host supports)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(),
+                                      start_new_session=True))
+    import threading
+
+    lines = []
+
+    def pump():  # rank 0's stdout, read as it comes (a full pipe would stall the rank)
+        for raw in procs[0].stdout:
+            lines.append(raw.decode(errors="replace"))
+
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    failed = None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            failed = bad[0]
+            break
+        if all(c == 0 for c in codes):
+            break
+        time.sleep(poll_s)
+    if failed is not None:
+        import signal
+
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+    th.join(timeout=30)
+    for ln in lines:
+        if ln.lstrip().startswith("{"):
+            sys.stdout.write(ln)
+        else:
+            sys.stderr.write(ln)
+    sys.stdout.flush()
+    if failed is not None:
+        print(f"bench.py: rank {failed[0]} exited with {failed[1]}", file=sys.stderr)
+        return 1
+    return 0
+
+
+def rehearse_cpu(args, world, rank):
+    """CPU rehearsal of the multi-rank bench (tests: gloo on CPU ranks).  The same shard, bucketed
+    step loop (distributed.BucketedNormGather) and max-over-ranks timing as the GPU path; the shard's
+    per-step residual norms come from ``norms(prob, x, mass, tag) -> [max, sumsq]`` defined in the
+    file --rehearse-cpu names (a test file: the CPU stands in for the rank's GPU).  Prints the line
+    with roofline = null."""
+    import importlib.util
+
+    import torch
+    import torch.distributed as dist
+
+    from centroidalplanner_amd.distributed import BucketedNormGather, shard
+    from centroidalplanner_amd.workload import CONFIGS, generate, make_problem
+
+    spec = importlib.util.spec_from_file_location("_bench_rehearsal", args.rehearse_cpu)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    cfg = CONFIGS[args.config]
+    total = args.batch or cfg.batch
+    start, batch = shard(total, rank, world) if cfg.config_id == 4 and not args.batch else (0, total)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    prob = make_problem(cfg.n_contacts, cfg.env)
+    x, mass, tag = generate(cfg.n_contacts, cfg.env, batch, 0xC910 + cfg.config_id + 7919 * rank)
+    local = torch.tensor(mod.norms(prob, x, mass, tag), dtype=torch.float64)
+
+    def launch(rows, count):
+        for s in range(count):
+            rows[s].copy_(local)
+
+    K, W = args.steps, args.warmup
+    runner = BucketedNormGather(world, max(1, min(args.bucket, K)), torch.device("cpu"), launch)
+    for w in runner.run(W):
+        if w is not None:
+            w.wait()
+    runner.reset()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for w in runner.run(K):
+        if w is not None:
+            w.wait()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    gather = None
+    totals = torch.tensor([dt, float(batch)], dtype=torch.float64)
+    if world > 1:
+        t = totals[:1].clone()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        b = totals[1:].clone()
+        dist.all_reduce(b, op=dist.ReduceOp.SUM)
+        dt, total_rows = float(t.item()), int(b.item())
+        gather = runner.last_bucket_report(rank, K)
+    else:
+        total_rows = batch
+    _, m = algorithmic_bytes(cfg.n_contacts, cfg.env)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": total_rows * m * K / dt, "unit": "rows/s", "n_gpus": world,
+                          "steps": K, "warmup": W, "ms_per_step": dt / K * 1e3, "higher_is_better": True,
+                          "scaling": scaling_of(cfg, args), "vs_baseline": None, "dtype": "f64",
+                          "data": "synthetic (CPU rehearsal of the multi-rank launch)",
+                          "config": {"workload": cfg.name, "batch_per_gpu": batch, "batch_total": total_rows,
+                                     "parallelism": f"instance-sharded x{world} (gloo, CPU rehearsal)"},
+                          "residual_gather": gather, "roofline": None, "cpu_baseline": None}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def scaling_of(cfg, args):
+    """configs[3] is quoted as 1,048,576 instances over the node: sharded, its total is fixed (strong
+    scaling); every other config keeps its per-GPU batch (weak scaling)."""
+    return "strong" if cfg.config_id == 4 and not args.batch else "weak"
 
 
 # ------------------------------------------------------------------------------------------
@@ -656,14 +829,16 @@ def main():
     args = parse()
     if args.pmc_child:
         pmc_child(args)
-        return
+        return 0
+    world, rank, local_rank, spawn = resolve_world(args)
+    if spawn:  # before anything touches the GPU
+        return spawn_ranks(world)
+    if args.rehearse_cpu:
+        rehearse_cpu(args, world, rank)
+        return 0
     if args.config == "solve5":
         solve_bench(args)
-        return
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        return 0
 
     from centroidalplanner_amd.workload import CONFIGS
 
@@ -674,12 +849,16 @@ def main():
 
         batch = shard(cfg.batch, rank, world)[1]  # config 4 is quoted as 1,048,576 over the node
 
+    # rank 0's legs that run before this process touches the GPU (the other ranks wait for it in the
+    # process-group rendezvous): the PMC passes (child processes under rocprofv3, the per-rank batch)
+    # and the CPU baseline
     traffic, pmc_info, valu_counters = None, None, None
-    if world == 1 and not args.no_pmc:
-        traffic, pmc_info = collect_pmc(args)
+    if rank == 0 and not args.no_pmc:
+        pmc_args = argparse.Namespace(config=args.config, batch=batch if batch != cfg.batch else args.batch)
+        traffic, pmc_info = collect_pmc(pmc_args)
         if cfg.env in ("superquadric", "mixed"):  # VALU-bound kernels: the VALU roofline too
             try:
-                valu_counters = collect_valu_counters(args)
+                valu_counters = collect_valu_counters(pmc_args)
             except Exception as e:  # noqa: BLE001
                 valu_counters = f"VALU PMC passes failed: {e}"
     sq8_counters = None
@@ -690,7 +869,7 @@ def main():
             sq8_counters = f"VALU PMC passes failed: {e}"
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:
         try:
             cpu = cpu_baseline(cfg, args.cpu_seconds)
         except Exception as e:  # noqa: BLE001
@@ -774,10 +953,14 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    total_batch = batch
     if world > 1:
         tdt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tdt, op=dist.ReduceOp.MAX)
         dt = float(tdt.item())
+        tb = torch.tensor([batch], dtype=torch.int64, device=dev)
+        dist.all_reduce(tb, op=dist.ReduceOp.SUM)  # instances of the whole job (shards may differ by 1)
+        total_batch = int(tb.item())
         # every timed step's norms reached every rank: the last bucket's gather holds one row per
         # (rank, step); combined over ranks it is the whole job's residual for that step, and this
         # rank's rows must be the norms it computed locally
@@ -798,7 +981,7 @@ def main():
 
     bytes_inst, m = algorithmic_bytes(cfg.n_contacts, cfg.env)
     alg_bytes = bytes_inst * batch
-    rows_total = batch * m * world * K
+    rows_total = total_batch * m * K
     value = rows_total / dt
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
 
@@ -898,7 +1081,7 @@ def main():
             "warmup": W,
             "ms_per_step": dt / K * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling_of(cfg, args),
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded SURVEY.md §8(d) instances; no published reference number)",
@@ -907,6 +1090,7 @@ def main():
                 "contacts": cfg.n_contacts,
                 "environment": cfg.env,
                 "batch_per_gpu": batch,
+                "batch_total": total_batch,
                 "outputs": "g + jac (IFOPT CSR values), per-shard residual norms",
                 "parallelism": f"instance-sharded x{world}" + (" + RCCL all-gather of residual norms" if world > 1 else ""),
                 "launch": (f"hip-graph, {S} steps per replay" if graphs else "eager")
@@ -914,7 +1098,7 @@ def main():
                 "rank_inputs": "distinct per rank (seed 0xC910 + config + 7919 * rank): weak scaling over "
                                "different instances, no data-path exchange",
             },
-            "instances_per_s": batch * world * K / dt,
+            "instances_per_s": total_batch * K / dt,
             "residual_gather": gather_info,
             "roofline": {
                 "bound": "hbm",
@@ -954,4 +1138,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)
