@@ -90,6 +90,7 @@ class SolveOptions(ctypes.Structure):
         ("acceptable_tol", c_double),
         ("mu_init", c_double),
         ("fd_step", c_double),
+        ("fallback_viol_tol", c_double),
     ]
 
 
@@ -211,6 +212,7 @@ SIGNATURES = {
     "cpl_solver_dims": (c_int32, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     "cpl_solver_stats": (c_int32, [c_void_p, POINTER(c_int32), POINTER(c_int64)]),
     "cpl_solver_restorations": (c_int32, [c_void_p, c_void_p, c_void_p]),
+    "cpl_solver_fallbacks": (c_int32, [c_void_p, c_void_p, c_void_p]),
 }
 
 

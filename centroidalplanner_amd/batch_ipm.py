@@ -75,7 +75,7 @@ STATUS_OPTIMAL = 0
 STATUS_ACCEPTABLE = 1
 STATUS_MAX_ITER = 2
 STATUS_INFEASIBLE = 3     # the restoration phase converged: a point of local infeasibility
-STATUS_RESTO_FAILED = 4   # the restoration phase's line search failed
+STATUS_RESTO_FAILED = 4   # the restoration phase converged twice to a feasible point the filter rejects
 STATUS_NAMES = {STATUS_OPTIMAL: "optimal", STATUS_ACCEPTABLE: "acceptable", STATUS_MAX_ITER: "max_iter",
                 STATUS_INFEASIBLE: "local_infeasibility", STATUS_RESTO_FAILED: "restoration_failed"}
 
@@ -154,6 +154,7 @@ class BatchSolveResult:
     graph: bool          # the iteration ran as a captured HIP graph
     compactions: int = 0  # active-set compactions of the native engine (the batch shrank this often)
     restorations: object = None  # [B] int: restoration-phase entries per instance
+    fallback: object = None  # [B] bool: x is the best feasible iterate, not the last (fallback_viol_tol)
 
     @property
     def success(self):
@@ -170,7 +171,7 @@ class NativeSolver:
 
     def __init__(self, problem, batch, tol=1e-8, max_iter=3000, mu_init=0.1, acceptable_tol=1e-6,
                  acceptable_iter=15, max_ls=40, max_soc=4, hessian="exact", fd_step=1e-6, graph=True, compact=True,
-                 ls_kernel=2):
+                 ls_kernel=2, fallback_viol_tol=1e-9):
         o = _abi.SolveOptions()
         _abi.lib.cpl_solve_options_default(ctypes.byref(o))
         o.max_iter, o.max_ls, o.max_soc, o.acceptable_iter = int(max_iter), int(max_ls), int(max_soc), int(acceptable_iter)
@@ -180,6 +181,7 @@ class NativeSolver:
         o.use_graph = 1 if graph else 0
         o.compact = 1 if compact else 0
         o.ls_kernel = int(ls_kernel)
+        o.fallback_viol_tol = float(fallback_viol_tol)
         self.problem, self.batch = problem, int(batch)
         self.desc = problem.desc()
         self.handle = ctypes.c_void_p()
@@ -229,10 +231,13 @@ class NativeSolver:
         resto = torch.empty(B, dtype=torch.int64, device=dev)
         _abi.check(_abi.lib.cpl_solver_restorations(self.handle, _ptr(resto),
                                                     ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+        fb = torch.empty(B, dtype=torch.uint8, device=dev)
+        _abi.check(_abi.lib.cpl_solver_fallbacks(self.handle, _ptr(fb),
+                                                 ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
         return BatchSolveResult(x=x, y=y, status=status.to(torch.int64), iterations=iters.to(torch.int64),
                                 objective=obj, primal_inf=pinf, dual_inf=dinf, evaluations=int(ev.value),
                                 iterations_run=int(it.value), graph=bool(g.value), compactions=int(nc.value),
-                                restorations=resto)
+                                restorations=resto, fallback=fb.bool())
 
 
 _NATIVE_CACHE = {}
@@ -254,7 +259,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                     acceptable_iter: int = 15, max_ls: int = 40, max_soc: int = 4, hessian: str = "exact",
                     fd_step: float = 1e-6, graph: Optional[bool] = None, check_every: int = 4,
                     verbose: int = 0, compact: bool = True, verbose_instance: int = 0,
-                    ls_kernel: int = 2) -> BatchSolveResult:
+                    ls_kernel: int = 2, fallback_viol_tol: float = 1e-9) -> BatchSolveResult:
     """Solve B instances of `problem`'s template from the starting points X0 [B, n] (torch float64,
     device tensor), per-instance robot masses `mass` [B] (None: the template's).
 
@@ -268,7 +273,10 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     IPOPT's alpha_min) / second-order corrections on the first trial (IPOPT max_soc 4).
     ls_kernel (device engine): the whole line search (first trial, its corrections, backtracking) in
     one launch for 47 x 30 systems — 2 (default): always, 1: batches of at most 256 rows, 0: never;
-    the same iterates bit for bit."""
+    the same iterates bit for bit.
+    fallback_viol_tol (not IPOPT, which returns its last iterate; <= 0: off): an instance that stops
+    without converging at an iterate violating its original constraints by more than this returns the
+    lowest-objective iterate it met that satisfied them to this tolerance (result.fallback)."""
     if hessian not in ("exact", "fd", "limited-memory"):
         raise ValueError("hessian must be 'exact', 'fd' or 'limited-memory'")
     use_bfgs = hessian == "limited-memory"
@@ -281,7 +289,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         ns = _native(problem, X0.shape[0], tol=tol, max_iter=max_iter, mu_init=mu_init, acceptable_tol=acceptable_tol,
                      acceptable_iter=acceptable_iter, max_ls=max_ls, max_soc=max_soc, hessian=hessian,
                      fd_step=fd_step, graph=True if graph is None else bool(graph), compact=compact,
-                     ls_kernel=ls_kernel)
+                     ls_kernel=ls_kernel, fallback_viol_tol=fallback_viol_tol)
         r = ns.solve(X0, mass, None if evaluator is None else evaluator.env_tag)
         if evaluator is not None:
             evaluator.calls += r.evaluations
@@ -581,12 +589,16 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
 
     def acceptable(th, ph, theta_k, phi_k, gd, al, switch_ok, theta_max, ft, fp, from_resto=False):
         """IPOPT FilterLSAcceptor::CheckAcceptabilityOfTrialPoint: theta_max, then Armijo on the
-        barrier objective for an f-type step (switching condition, theta_k <= theta_min) or the
-        sufficient decrease of theta or phi against the current iterate (with the obj_max_inc guard),
-        then the filter (entries stored with their margins).  Returns (ok, h_type)."""
+        barrier objective for an f-type step (switching condition) at a reference point with
+        theta_k <= theta_min, or the sufficient decrease of theta or phi against the current iterate
+        (with the obj_max_inc guard), then the filter (entries stored with their margins).  switch_ok:
+        theta_k <= theta_min (gd < 0 is tested here).  Returns (ok, h_type): h_type = the step augments
+        the filter — UpdateForNextIteration: unless IsFtype (the switching condition alone, no
+        theta_min term) and Armijo hold."""
         fin = torch.isfinite(ph) & torch.isfinite(th)
         in_filter = ((th[:, None] <= ft) | (ph[:, None] <= fp)).all(1)
-        ftype = switch_ok & (al * torch.where(gd < 0, -gd, torch.zeros_like(gd)) ** S_PHI > DELTA_SW * theta_k ** S_TH)
+        is_ftype = (gd < 0) & (al * torch.where(gd < 0, -gd, torch.zeros_like(gd)) ** S_PHI > DELTA_SW * theta_k ** S_TH)
+        ftype = is_ftype & switch_ok
         # IPOPT's Compare_le(lhs, rhs, base): lhs - rhs <= 10 eps |base| (round-off of the reference values)
         ro_p, ro_t = 10.0 * EPS * phi_k.abs(), 10.0 * EPS * theta_k.abs()
         armijo = (ph - phi_k) - ETA_PHI * al * gd <= ro_p
@@ -598,7 +610,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
             suff = suff & ~big
             armijo = armijo & ~big
         ok = fin & (th <= theta_max) & in_filter & torch.where(ftype, armijo, suff)
-        return ok, ~(ftype & armijo)
+        return ok, ~(is_ftype & armijo)
 
     # ---- starting point: x pushed into its bounds, slacks = g_I(x) pushed into theirs
     Xs = unpack(push(torch.cat([Xbase[:, free], zeros_I], 1)))
@@ -648,7 +660,24 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         "fpR": torch.full((B, FMAX), float("inf"), dtype=dt, device=dev),
         "fcR": torch.zeros(B, dtype=torch.int64, device=dev), "th_o0": zB(), "ph_o0": zB(), "dwlR": zB(),
         "thmaxR": zB(), "thminR": zB(), "n_resto": torch.zeros(B, dtype=torch.int64, device=dev),
+        "resto_tight": bool_B(),
+        # the best iterate feasible to fallback_viol_tol (lowest f): the fallback result of a solve that
+        # stops without converging at an infeasible iterate (not IPOPT)
+        "best_w": zBw(), "best_f": torch.full((B,), float("inf"), dtype=dt, device=dev),
     }
+
+    def orig_violation(g):
+        """max violation of g against the original constraint bounds (NaN: infinite)."""
+        if not m:
+            return zeros_B
+        v = torch.clamp(torch.maximum(gl - g, g - gu), min=0.0).amax(1)
+        return torch.where(torch.isnan(g).any(1), torch.full_like(v, float("inf")), v)
+
+    def track_best():
+        v = orig_violation(S["g"])
+        upd = S["active"] & (v <= fallback_viol_tol) & (S["f"] < S["best_f"])
+        S["best_w"].copy_(torch.where(upd[:, None], S["w"], S["best_w"]))
+        S["best_f"].copy_(torch.where(upd, S["f"], S["best_f"]))
 
     def check(E, mask):
         """Convergence test at the current iterate of the instances in `mask`; updates status /
@@ -774,7 +803,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         a_max = primal_step(dw)
         a_z = torch.minimum(max_step(zL, dzL, hasL, 0.0, tau), max_step(zU, dzU, hasU, 0.0, tau))
         gd = (gphi * dw).sum(1)
-        switch_ok = (theta_k <= theta_min) & (gd < 0)
+        switch_ok = theta_k <= theta_min
         # IPOPT DetectTinyStep: the step is below 10 eps relative in every primal component, the
         # multiplier step below 1e-2, the point feasible to 1e-4: taken whole without a line search;
         # two in a row force the next barrier decrease
@@ -983,10 +1012,18 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         base = torch.maximum(d_inf / sd, cR.abs().amax(1))
         cmax = torch.maximum(torch.maximum(cl.amax(1), cu.amax(1)), torch.maximum(cp.amax(1), cn.amax(1)))
         errR0 = torch.maximum(base, cmax / sc)
-        conv = actR & (errR0 <= tol)
-        S["status"].copy_(torch.where(conv, STATUS_INFEASIBLE, S["status"]))
-        S["active"].copy_(S["active"] & ~conv)
-        actR = actR & ~conv
+        # converged (RestoConvergenceCheck): local infeasibility unless the original max |c| <= 1e2 tol;
+        # a feasible point unacceptable to the original filter tightens the restoration tolerance to
+        # 1e-2 tol once and goes on, the second time it ends the solve as a restoration failure
+        tight = S["resto_tight"]
+        conv = actR & (errR0 <= torch.where(tight, 1e-2 * tol, tol))
+        feas = (c.abs().amax(1) if m else zeros_B) <= 1e2 * tol
+        stop = conv & (~feas | tight)
+        S["status"].copy_(torch.where(stop & feas, STATUS_RESTO_FAILED,
+                                      torch.where(stop, STATUS_INFEASIBLE, S["status"])))
+        S["resto_tight"].copy_(tight | (conv & feas))
+        S["active"].copy_(S["active"] & ~stop)
+        actR = actR & ~stop
 
         def errR_mu(muv):
             cm = torch.maximum(
@@ -1042,7 +1079,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         gd = (gphi * dw).sum(1) + ((RHO_R - muR[:, None] / pp) * dp).sum(1) + ((RHO_R - muR[:, None] / nn) * dn).sum(1)
         thetaR = cR.abs().sum(1)
         phR_k = phiR(w, pp, nn)
-        switch_ok = (thetaR <= S["thminR"]) & (gd < 0)
+        switch_ok = thetaR <= S["thminR"]
         a_min = alpha_min_of(thetaR, gd, S["thminR"])
 
         # ---- filter line search on the restoration problem (no second-order correction)
@@ -1062,8 +1099,14 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
             alpha = torch.where(st["searching"], 0.5 * alpha, alpha)
             st["searching"] = st["searching"] & (alpha > a_min)
         failedR = actR & ~st["found"]
-        S["status"].copy_(torch.where(failedR, STATUS_RESTO_FAILED, S["status"]))
-        S["active"].copy_(S["active"] & ~failedR)
+        # the restoration problem's line search failed: IPOPT's RestoRestorationPhase — w and every
+        # multiplier stay, p and n take the closed-form minimisers of the barrier subproblem at the
+        # current c(w) and mu_R (as at the phase's start), and that is the next iterate
+        if bool(failedR.any()):
+            aR = (muR[:, None] - RHO_R * c) / (2.0 * RHO_R)
+            nR_ = aR + torch.sqrt(aR * aR + muR[:, None] * c / (2.0 * RHO_R))
+            S["n"].copy_(torch.where(failedR[:, None], nR_, S["n"]))
+            S["p"].copy_(torch.where(failedR[:, None], c + nR_, S["p"]))
         moved = actR & st["found"]
         mv = moved[:, None]
         w_new, al = st["w"], st["alpha"]
@@ -1161,6 +1204,8 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
             regular_step(E, act)
         if bool(actR.any()):
             resto_step(actR)
+        if fallback_viol_tol > 0:
+            track_best()
 
     def verbose_line(E, mu, a_max, al, dw, dy, delta_w, cur, failed):
         b = verbose_instance
@@ -1185,6 +1230,11 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     # final convergence test at the last iterate (instances still in the restoration phase keep max_iter)
     check(errors({"f": S["f"], "grad": S["grad"], "g": S["g"], "J": S["J"]}, S["w"], S["y"], S["zL"], S["zU"]),
           ~S["resto"])
+    fallback = bool_B()
+    if fallback_viol_tol > 0:  # an unconverged instance stopped at an infeasible iterate: its best feasible one
+        fallback = (S["status"] > STATUS_ACCEPTABLE) & (orig_violation(S["g"]) > fallback_viol_tol) & \
+            torch.isfinite(S["best_f"])
+        S["w"].copy_(torch.where(fallback[:, None], S["best_w"], S["w"]))
     # IPOPT honor_original_bounds: the final point is projected back into the unrelaxed bounds and
     # its objective / constraint values reported there
     Xf = torch.minimum(torch.maximum(unpack(S["w"]), xl), xu).contiguous()
@@ -1195,4 +1245,5 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                            objective=fin["f"].clone(), primal_inf=viol, dual_inf=S["d_inf"], evaluations=n_eval,
                            iterations_run=it_run, graph=False)
     res.restorations = S["n_resto"]
+    res.fallback = fallback
     return res

@@ -21,19 +21,27 @@ constexpr double LS_KAPPA_SOC = 0.99;  // kappa_soc
 
 // theta_max; the filter (entries stored with their margins ((1 - gamma_theta) theta, phi - gamma_phi
 // theta): acceptable when, for every entry, theta or phi is not larger — IPOPT's Filter::Acceptable);
-// the switching condition; Armijo on the barrier objective for an f-type step, else sufficient
-// decrease of theta or phi against the reference point, both with IPOPT's round-off tolerance
-// Compare_le(lhs, rhs, base) = lhs - rhs <= 10 eps |base|; obj_max_inc.  *h_type: the step augments
-// the filter.  Every lane of the wave must call it (a ballot).
+// the switching condition; Armijo on the barrier objective for an f-type step at a reference point
+// with theta <= theta_min, else sufficient decrease of theta or phi against the reference point, both
+// with IPOPT's round-off tolerance Compare_le(lhs, rhs, base) = lhs - rhs <= 10 eps |base|;
+// obj_max_inc.  *h_type: the step augments the filter — IPOPT's UpdateForNextIteration augments
+// unless the step is f-type (IsFtype: the switching condition alone, no theta_min term) AND Armijo
+// holds.  sw: LS_SW_DESCENT (grad phi . dw < 0) | LS_SW_THETA_MIN (theta_k <= theta_min), the
+// post-step kernel's flags.  Every lane of the wave must call it (a ballot).
+constexpr uint8_t LS_SW_DESCENT = 1, LS_SW_THETA_MIN = 2;
+__device__ __forceinline__ uint8_t ls_switch_flags(double theta, double theta_min, double gd) {
+  return (uint8_t)((gd < 0.0 ? LS_SW_DESCENT : 0) | (theta <= theta_min ? LS_SW_THETA_MIN : 0));
+}
 __device__ __forceinline__ bool ls_acceptable_wave(double th, double ph, double tk, double pk, double g, double al,
-                                                   bool switch_ok, double theta_max, const double* ft,
+                                                   uint8_t sw, double theta_max, const double* ft,
                                                    const double* fp, int nfilt, bool* h_type) {
   const int lane = threadIdx.x & 63;
   bool rejected = false;
   for (int k = lane; k < nfilt; k += 64) rejected |= !((th <= ft[k]) || (ph <= fp[k]));
   const bool in_filter = __ballot(rejected) == 0;
   const bool fin = isfinite(ph) && isfinite(th);
-  const bool ftype = switch_ok && (al * pow(fmax(-g, 0.0), LS_S_PHI) > LS_DELTA * pow(tk, LS_S_TH));
+  const bool is_ftype = (sw & LS_SW_DESCENT) && (al * pow(fmax(-g, 0.0), LS_S_PHI) > LS_DELTA * pow(tk, LS_S_TH));
+  const bool ftype = is_ftype && (sw & LS_SW_THETA_MIN);
   const double ro_p = 10.0 * DBL_EPSILON * fabs(pk), ro_t = 10.0 * DBL_EPSILON * fabs(tk);
   bool armijo = (ph - pk) - LS_ETA_PHI * al * g <= ro_p;
   bool suff = (th - (1.0 - LS_GAMMA_TH) * tk <= ro_t) || ((ph - pk) - (-LS_GAMMA_PHI * tk) <= ro_p);
@@ -41,7 +49,7 @@ __device__ __forceinline__ bool ls_acceptable_wave(double th, double ph, double 
     const double basval = fabs(pk) > 10.0 ? log10(fabs(pk)) : 1.0;
     if (log10(ph - pk) > LS_OBJ_MAX_INC + basval) armijo = suff = false;
   }
-  if (h_type) *h_type = !(ftype && armijo);
+  if (h_type) *h_type = !(is_ftype && armijo);
   return fin && th <= theta_max && in_filter && (ftype ? armijo : suff);
 }
 

@@ -79,7 +79,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_judge_take_kernel(
   const double ph = f_t[b] - mu[b] * lg;
   const double al = alpha[b];
   bool aug = false;
-  const bool ok = ls_acceptable_wave(th, ph, theta_k[b], phi_k[b], gd[b], al, switch_ok[b] != 0, theta_max[b],
+  const bool ok = ls_acceptable_wave(th, ph, theta_k[b], phi_k[b], gd[b], al, switch_ok[b], theta_max[b],
                                      filt_t + b * nfilt, filt_p + b * nfilt, nfilt, &aug);
   const bool take = ok && searching[b] && (extra_mask == nullptr || extra_mask[b]);
   if (take) {
@@ -393,7 +393,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
 
 // After the Newton step (batch_ipm.py step): bound-multiplier steps dzL = mu/dl - zL - zL/dl dw,
 // dzU = mu/du - zU + zU/du dw, their fraction-to-the-boundary step a_z, the primal one a_max,
-// gd = grad_phi . dw, switch_ok = theta <= theta_min & gd < 0, and delta_w_last <- delta_w on the
+// gd = grad_phi . dw, switch_ok = ls_switch_flags (gd < 0, theta <= theta_min), and delta_w_last <- delta_w on the
 // active instances.
 __global__ __launch_bounds__(256) void cpl_ipm_post_step_kernel(
     int64_t batch, int nw, const double* __restrict__ w, const double* __restrict__ dw, const double* __restrict__ zL,
@@ -434,7 +434,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_post_step_kernel(
     a_max[b] = fmin(rp, 1.0);
     a_z[b] = fmin(rz, 1.0);
     gd_out[b] = gd;
-    switch_ok[b] = (theta[b] <= theta_min[b] && gd < 0.0) ? 1 : 0;
+    switch_ok[b] = ls_switch_flags(theta[b], theta_min[b], gd);
     if (active[b]) dwl[b] = delta_w[b];
   }
   // the solve loop's line-search setup (ls.act != NULL; was the next launch): no output of this

@@ -98,6 +98,7 @@ struct KParams {
   int32_t jdirect;           // tile kernel: the Jacobian items write their entries straight to the
                              // output records instead of the LDS tile image (smaller tiles' LDS)
   int32_t offA;              // (jdirect) doubles offset of the statics CoM-pair scratch [T][6]
+  int32_t offRB, offCS, offST;  // entry kernel: row bases [2][T] (int64), cone scratch, statics scratch
 };
 static_assert(sizeof(KParams) < 4096, "kernel parameters must fit the kernarg segment");
 
@@ -876,6 +877,26 @@ __device__ __forceinline__ void copy_out(double* __restrict__ dst, const double*
   }
 }
 
+// Copy-out of a tile image [valid][rec] to the records of instances rowb[r] (rec even: every record
+// and every pair of it is 16-byte aligned), 16-byte stores, lanes along the records
+template <int WG, bool NT>
+__device__ __forceinline__ void copy_out_rows(double* __restrict__ dst, const long long* __restrict__ rowb,
+                                              const double* __restrict__ src, int rec, int valid, int tid) {
+  const int r2 = rec >> 1;
+  const double2* s2 = reinterpret_cast<const double2*>(src);
+  for (int e = tid; e < valid * r2; e += WG) {
+    const int r = e / r2, q = e - r * r2;
+    const double2 v = s2[e];
+    double2* d = reinterpret_cast<double2*>(dst + rowb[r] * rec) + q;
+    if (NT) {
+      __builtin_nontemporal_store(v.x, &d->x);
+      __builtin_nontemporal_store(v.y, &d->y);
+    } else {
+      *d = v;
+    }
+  }
+}
+
 // one contact block (map position k, vector index i): g rows env(1) normal(3) cone(2),
 // jac rows env p(3) | normal r: p(3) n_r(1) | cone 0: F(3) n(3) | cone 1: F(3) n(3)
 template <int ENVK>
@@ -1062,23 +1083,26 @@ __device__ __forceinline__ void statics_row_item(const KParams& K, const double*
 }
 
 // MinimizeCentroidalVariables::GetCost / FillJacobianBlock, src/MinimizeCentroidalVariables.cpp:124-192
+__device__ __forceinline__ double cost_value(const KParams& K, const double* __restrict__ xr) {
+  const int N = K.N;
+  double value = 0;
+  for (int k = 0; k < N; ++k) {
+    const int i = s_ct.map_order[k];
+    const double* q = xr + 3 + 9 * i;
+    const double e0 = q[3] - K.p_ref[i][0], e1 = q[4] - K.p_ref[i][1], e2 = q[5] - K.p_ref[i][2];
+    const double h0 = q[0] - K.F_ref[i][0], h1 = q[1] - K.F_ref[i][1], h2 = q[2] - K.F_ref[i][2];
+    value += 0.5 * K.W_p[i] * ((e0 * e0 + e1 * e1) + e2 * e2) + 0.5 * K.W_F[i] * ((h0 * h0 + h1 * h1) + h2 * h2);
+  }
+  const double r0 = xr[0] - K.com_ref[0], r1 = xr[1] - K.com_ref[1], r2 = xr[2] - K.com_ref[2];
+  value += 0.5 * K.W_com * ((r0 * r0 + r1 * r1) + r2 * r2);
+  return value;
+}
+
 __device__ __forceinline__ void cost_item(const KParams& K, const double* __restrict__ xr, double* __restrict__ f,
                                           double* __restrict__ Dr) {
   const int N = K.N;
   const double c0 = xr[0], c1 = xr[1], c2 = xr[2];
-  if (K.want_f) {
-    double value = 0;
-    for (int k = 0; k < N; ++k) {
-      const int i = s_ct.map_order[k];
-      const double* q = xr + 3 + 9 * i;
-      const double e0 = q[3] - K.p_ref[i][0], e1 = q[4] - K.p_ref[i][1], e2 = q[5] - K.p_ref[i][2];
-      const double h0 = q[0] - K.F_ref[i][0], h1 = q[1] - K.F_ref[i][1], h2 = q[2] - K.F_ref[i][2];
-      value += 0.5 * K.W_p[i] * ((e0 * e0 + e1 * e1) + e2 * e2) + 0.5 * K.W_F[i] * ((h0 * h0 + h1 * h1) + h2 * h2);
-    }
-    const double r0 = c0 - K.com_ref[0], r1 = c1 - K.com_ref[1], r2 = c2 - K.com_ref[2];
-    value += 0.5 * K.W_com * ((r0 * r0 + r1 * r1) + r2 * r2);
-    *f = value;
-  }
+  if (K.want_f) *f = cost_value(K, xr);
   if (K.want_grad) {
     Dr[0] = K.W_com * (c0 - K.com_ref[0]);
     Dr[1] = K.W_com * (c1 - K.com_ref[1]);
@@ -1273,11 +1297,16 @@ __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __re
 // compile-time choice, so that every Jacobian store is a plain LDS or a plain global store: through a
 // generic pointer they were FLAT stores, which count on lgkmcnt too — every later LDS wait of the
 // thread then waited for its in-flight global stores.
+// idx (optional, with d_count on the device): an instance list — tile position j evaluates instance
+// idx[j] and its records are written in place (the Superquadric half of a mixed batch, launched for
+// `batch` list entries at most; tiles past *d_count only write zero norm partials).  Not with JD / SoA.
 template <int ENVK, int WG, bool NT, bool JD>
 __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int64_t batch,
                                                             const double* __restrict__ x,
                                                             const double* __restrict__ mass,
                                                             const uint8_t* __restrict__ env_tag,
+                                                            const int32_t* __restrict__ idx,
+                                                            const int32_t* __restrict__ d_count,
                                                             double* __restrict__ g_out,
                                                             double* __restrict__ jac_out,
                                                             double* __restrict__ f_out,
@@ -1291,18 +1320,39 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
   const int tid = threadIdx.x;
   const int T = K.T;
   const int n = K.n, m = K.m, nnz = K.nnz, N = K.N;
-  const int64_t b0 = (int64_t)blockIdx.x * T;
-  const int valid = (int)((batch - b0) < T ? (batch - b0) : T);
+  const int64_t count = d_count ? (int64_t)*d_count : batch;
+  const int64_t ntiles = (count + T - 1) / T;
+  NormAcc nacc;
+  nacc.init(tid, WG, m);
+  // one tile per workgroup, or (list launches, a grid of the resident workgroups) tiles blockIdx,
+  // blockIdx + grid, ...
+  for (int64_t tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
+  const int64_t b0 = tl * T;
+  const int valid = (int)((count - b0) < T ? (count - b0) : T);
+  long long* rowb = reinterpret_cast<long long*>(smem + K.offRB);  // (idx) instance of each tile row
+  auto inst = [&](int r) -> int64_t { return idx ? (int64_t)rowb[r] : b0 + r; };
   double* X = smem;
   double* Gt = smem + K.offG;
   // the Jacobian rows: the LDS tile image, or (jdirect) the output records themselves
   double* Jt = JD ? jac_out + b0 * K.nnz : smem + K.offJ;
+  // row r's Jacobian: the LDS image's, or (JD) the output record itself — of instance rowb[r] in a
+  // list launch
+  auto JR = [&](int r) -> double* { return (JD && idx) ? jac_out + rowb[r] * nnz : Jt + r * nnz; };
   double* Dt = smem + K.offD;
   double* L = smem + K.offL;                                    // [T][LR] (SQ / mixed)
   int* lists = reinterpret_cast<int*>(smem + K.offI);          // sq_list[64], gr_list[64], n_sq
   constexpr bool HAS_SQ = ENVK == CPL_ENV_SUPERQUADRIC || ENVK == CPL_ENV_MIXED;
 
-  copy_in<WG>(X, x + b0 * n, valid * n, tid, K.x_aligned16 != 0);
+  if (idx) {
+    if (tid < valid) rowb[tid] = idx[b0 + tid];
+    __syncthreads();
+    for (int e = tid; e < valid * n; e += WG) {
+      const int r = e / n;
+      X[e] = x[rowb[r] * n + (e - r * n)];
+    }
+  } else {
+    copy_in<WG>(X, x + b0 * n, valid * n, tid, K.x_aligned16 != 0);
+  }
   int n_sq = ENVK == CPL_ENV_SUPERQUADRIC ? valid : 0;
   if (ENVK == CPL_ENV_MIXED) {
     // compact the tile's instances by environment kind so that every wave runs one code path
@@ -1343,7 +1393,7 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
         const int j = e % n_gr, k = e / n_gr;
         const int r = ENVK == CPL_ENV_MIXED ? lists[64 + j] : j;
         contact_item<ENVK == CPL_ENV_NONE ? CPL_ENV_NONE : CPL_ENV_GROUND>(K, X + r * n, CPL_ENV_GROUND, k,
-                                                                          Gt + r * m, Jt + r * nnz);
+                                                                          Gt + r * m, JR(r));
         return;
       }
       e -= r_gr;
@@ -1351,13 +1401,13 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
         const int r = e % valid, sg = e / valid;
         const double* xr = X + r * n;
         if (sg == 0)
-          statics_values_item(K, xr, mass ? mass[b0 + r] : mass_def, Gt + r * m, Jt + r * nnz, !JD,
+          statics_values_item(K, xr, mass ? mass[inst(r)] : mass_def, Gt + r * m, JR(r), !JD,
                               JD && K.want_j ? com6 + 6 * r : nullptr);
-        else if (K.want_j) statics_row_item(K, xr, sg - 1, Jt + r * nnz);
+        else if (K.want_j) statics_row_item(K, xr, sg - 1, JR(r));
         return;
       }
       e -= r_st;
-      cost_item(K, X + e * n, f_out ? f_out + b0 + e : nullptr, Dt + e * n);
+      cost_item(K, X + e * n, f_out ? f_out + inst(e) : nullptr, Dt + e * n);
     };
     // mixed: the statics / cost items join phase 1 (beside the Superquadric ladders), the Ground
     // contacts phase 2 (beside the Superquadric rows) — with 8-instance tiles both phases then fit
@@ -1384,25 +1434,32 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
         const int a = it / per_axis, kj = it - a * per_axis;
         const int k = kj / n_sq, j = kj - k * n_sq;
         const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
-        sq_row_item<ENVK == CPL_ENV_MIXED>(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m, Jt + r * nnz);
+        sq_row_item<ENVK == CPL_ENV_MIXED>(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m, JR(r));
       }
     for (int it = tid; it < items2; it += WG)
       if (it >= r_rows) other_item(it - r_rows);
     if (JD && K.want_j) {  // the statics Jacobian rows, lanes along each record
       lds_barrier();  // (the CoM pairs of the values items)
-      for (int r = 0; r < valid; ++r) statics_rows_coop(K, X + r * n, com6 + 6 * r, Jt + r * nnz, tid, WG);
+      for (int r = 0; r < valid; ++r) statics_rows_coop(K, X + r * n, com6 + 6 * r, JR(r), tid, WG);
     }
   }
   lds_barrier();
   // the residual partials first (from the LDS image), so that their stores are in flight with the
-  // copy-out's instead of after them on every workgroup's tail
+  // copy-out's instead of after them on every workgroup's tail (one tile per workgroup; list
+  // launches accumulate over their tiles and write after the loop)
   if (K.want_norms) {
-    NormAcc acc;
-    acc.init(tid, WG, m);
-    acc.add_tile(Gt, valid * m, tid, WG, m);
-    partial_norms_waves(acc, norms_ws + NORM_HDR);
+    nacc.add_tile(Gt, valid * m, tid, WG, m);
+    if (!idx) partial_norms_waves(nacc, norms_ws + NORM_HDR);
   }
-  if (K.ablate != 2 && K.soa) {
+  if (K.ablate != 2 && idx) {  // records written in place: row by row (g, jac rows are 16-byte aligned)
+    if (K.want_g) copy_out_rows<WG, NT>(g_out, rowb, Gt, m, valid, tid);
+    if (K.want_j && !JD) copy_out_rows<WG, NT>(jac_out, rowb, Jt, nnz, valid, tid);
+    if (K.want_grad)
+      for (int e = tid; e < valid * n; e += WG) {
+        const int r = e / n;
+        grad_out[rowb[r] * n + (e - r * n)] = Dt[e];
+      }
+  } else if (K.ablate != 2 && K.soa) {
     if (K.want_g) copy_out_soa<WG, NT>(g_out + b0, batch, Gt, m, valid, tid);
     if (K.want_j) copy_out_soa<WG, NT>(jac_out + b0, batch, Jt, nnz, valid, tid);
     if (K.want_grad) copy_out_soa<WG, NT>(grad_out + b0, batch, Dt, n, valid, tid);
@@ -1411,6 +1468,10 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
     if (K.want_j && !JD) copy_out<WG, NT>(jac_out + b0 * nnz, Jt, valid * nnz, tid);
     if (K.want_grad) copy_out<WG, NT>(grad_out + b0 * n, Dt, valid * n, tid);
   }
+  if (tl + gridDim.x < ntiles) __syncthreads();  // the next tile overwrites the LDS image
+  }  // tiles
+  // (list launches) the residual partials, one pair per wave — zeros from workgroups with no tile
+  if (K.want_norms && idx) partial_norms_waves(nacc, norms_ws + NORM_HDR);
 }
 
 
@@ -1673,6 +1734,326 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
 
 
 // ------------------------------------------------------------------------------------------
+// v4: table-driven records (Ground / no environment; IFOPT CSR values, instance-major).
+//   The pipelined kernel's loader wave (double-buffered LDS DMA of the next tile's x) with another
+//   compute side.  Every g / jac entry of these records is, up to its sign, one of: an element of x,
+//   a constant (0, 1), or a value of a short per-contact / per-instance prologue (p - c, the friction
+//   cone's values and row-1 derivatives, the Ground residuals, the statics sums).  So:
+//     * a per-block opcode table (built once per launch in LDS) maps record position -> (source
+//       area, offset, sign);
+//     * per tile, one thread per (instance, contact) and per instance computes the prologue values
+//       into an LDS scratch — the same operations in the same order as the work items of the other
+//       kernels (bitwise the same values);
+//     * the g and jac records are then a branch-free gather: lanes along the records, two entries per
+//       lane, 16-byte non-temporal stores straight to HBM.
+//   No output image lives in LDS, so large records (16 contacts: 6 KiB of outputs per instance) keep
+//   large tiles.  Optional instance list idx [count]: tile position j evaluates instance idx[j] and
+//   writes its records in place (the Ground half of a mixed batch); d_count: the list's length on the
+//   device (the grid is sized for `batch`, tiles past the count idle).  Records must have an even
+//   number of entries (m always; nnz = 6 + 42N with a surface, 6 + 27N without: even N).
+// ------------------------------------------------------------------------------------------
+// scratch per instance: [statics g (6) | CoM pairs (6) | per contact (vector order) ENT_PC values]
+constexpr int ENT_PC = 15;  // d = p - c (3), cone row 1 (6), cone g (2), env g (1), normal g (3)
+enum { EPC_D = 0, EPC_ROW1 = 3, EPC_CONEG = 9, EPC_ENVG = 11, EPC_NORMG = 12 };
+constexpr unsigned OP_X = 0u << 28, OP_S = 1u << 28, OP_C = 2u << 28, OP_NEG = 1u << 31;
+
+// the opcode of g entry q / jac entry q of the record (map order -> vector index via s_ct)
+template <int ENVK>
+__device__ __forceinline__ unsigned entry_op_g(int q, int S0) {
+  constexpr int CR = ENVK == CPL_ENV_NONE ? 2 : 6;
+  if (q < 6) return OP_S | (unsigned)q;
+  const int u = q - 6, k = u / CR, w = u - k * CR;
+  const unsigned ci = (unsigned)(S0 + ENT_PC * s_ct.map_order[k]);
+  if (ENVK == CPL_ENV_NONE) return OP_S | (ci + EPC_CONEG + w);
+  if (w == 0) return OP_S | (ci + EPC_ENVG);
+  if (w < 4) return OP_S | (ci + EPC_NORMG + (w - 1));
+  return OP_S | (ci + EPC_CONEG + (w - 4));
+}
+template <int ENVK>
+__device__ __forceinline__ unsigned entry_op_j(int q, int N, int S0) {
+  constexpr int CJ = ENVK == CPL_ENV_NONE ? 12 : 27;
+  const int RL = 2 + 4 * N, JC = 3 * N + 3 * RL;
+  if (q < 3 * N) return OP_C | 1u;  // the force-balance rows' I3 blocks (CentroidalStatics.cpp:93-95)
+  if (q < JC) {                     // torque row 3 + qq (CentroidalStatics.cpp:75-137)
+    int w = q - 3 * N;
+    const int qq = w >= 2 * RL ? 2 : (w >= RL ? 1 : 0);
+    w -= qq * RL;
+    if (w < 2) return OP_S | (unsigned)(6 + 2 * qq + w);  // the CoM pair
+    const int e1 = qq == 2 ? 1 : 2, e2 = qq == 0 ? 1 : 0;
+    const bool s1neg = qq != 1, s2neg = qq == 1;  // s1 = (qq == 1 ? 1 : -1), s2 = (qq == 1 ? -1 : 1)
+    const int i = (w - 2) >> 2, c = (w - 2) & 3;
+    const unsigned ci = (unsigned)(S0 + ENT_PC * i);
+    switch (c) {
+      case 0: return OP_S | (ci + EPC_D + e1) | (s1neg ? OP_NEG : 0u);   // s1 (p - c)[e1]
+      case 1: return OP_S | (ci + EPC_D + e2) | (s2neg ? OP_NEG : 0u);   // s2 (p - c)[e2]
+      case 2: return OP_X | (unsigned)(3 + 9 * i + e1) | (s1neg ? 0u : OP_NEG);  // -s1 F[e1]
+      default: return OP_X | (unsigned)(3 + 9 * i + e2) | (s2neg ? 0u : OP_NEG);  // -s2 F[e2]
+    }
+  }
+  const int u = q - JC, k = u / CJ;
+  int w = u - k * CJ;
+  const int i = s_ct.map_order[k];
+  if (ENVK != CPL_ENV_NONE) {
+    // src/Ground.cpp:30-50: gradient (0, 0, 1), zero normal Jacobian; EnvironmentNormal's n_r block 1
+    if (w < 3) return OP_C | (w == 2 ? 1u : 0u);
+    if (w < 15) return OP_C | (((w - 3) & 3) == 3 ? 1u : 0u);
+    w -= 15;
+  }
+  if (w < 3) return OP_X | (unsigned)(9 + 9 * i + w) | OP_NEG;  // cone row 0: -n (FrictionCone.cpp:79-81)
+  if (w < 6) return OP_X | (unsigned)(3 + 9 * i + (w - 3)) | OP_NEG;  // -F (:91-93)
+  return OP_S | (unsigned)(S0 + ENT_PC * i + EPC_ROW1 + (w - 6));   // row 1 (:82-101)
+}
+
+// loader wave: one row of `count` doubles (8-byte aligned source) into LDS with 4-byte DMA granules
+__device__ __forceinline__ void dma_row4(double* dst, const double* src, int count, int lane) {
+  const unsigned* s4 = reinterpret_cast<const unsigned*>(src);
+  unsigned* d4 = reinterpret_cast<unsigned*>(dst);
+  const int words = 2 * count;
+  for (int q = 0; q < words; q += 64)
+    if (q + lane < words) __builtin_amdgcn_global_load_lds((glb_void_t*)(s4 + q + lane), (lds_void_t*)(d4 + q), 4, 0, 0);
+}
+
+// the value of opcode op for tile row r: x row, scratch row or constant, sign applied as a sign-bit
+// flip (bitwise the unary minus of the other kernels)
+__device__ __forceinline__ double entry_value(unsigned op, const double* __restrict__ Xr, const double* __restrict__ Sr,
+                                              const double* __restrict__ C) {
+  const unsigned t = (op >> 28) & 3u;
+  const double* base = t == 0 ? Xr : (t == 1 ? Sr : C);
+  const double v = base[op & 0xffffffu];
+  long long bits = __double_as_longlong(v);
+  bits ^= (long long)(op & OP_NEG) << 32;
+  return __longlong_as_double(bits);
+}
+
+template <int ENVK, bool NT>
+__global__ __launch_bounds__(256) void cpl_eval_entry_kernel(const KParams K, int64_t batch,
+                                                             const double* __restrict__ x,
+                                                             const double* __restrict__ mass,
+                                                             const int32_t* __restrict__ idx,
+                                                             const int32_t* __restrict__ d_count,
+                                                             double* __restrict__ g_out,
+                                                             double* __restrict__ jac_out,
+                                                             double* __restrict__ f_out,
+                                                             double* __restrict__ grad_out,
+                                                             double* __restrict__ norms_ws) {
+  constexpr int NCW = 3, CT = 64 * NCW;  // compute waves + one loader wave
+  extern __shared__ __align__(16) double smem[];
+  load_ctab(K);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const bool loader = (tid >> 6) == NCW;
+  const int T = K.T;
+  const int n = K.n, m = K.m, nnz = K.nnz, N = K.N;
+  const int S = 12 + ENT_PC * N;  // scratch doubles per instance
+  auto XB = [&](int bi) { return smem + (bi ? K.offX1 : 0); };
+  auto MB = [&](int bi) { return smem + K.offMB + (bi ? T : 0); };
+  auto RB = [&](int bi) { return reinterpret_cast<long long*>(smem + K.offRB) + (bi ? T : 0); };
+  double* SC = smem + K.offCS;                                  // [T][S]
+  double* CN = smem + K.offST;                                  // constants 0, 1
+  unsigned* OPG = reinterpret_cast<unsigned*>(smem + K.offST + 2);  // [m] then [nnz] opcodes
+  unsigned* OPJ = OPG + m;
+  __syncthreads();  // (s_ct)
+  if (tid == 0) { CN[0] = 0.0; CN[1] = 1.0; }
+  for (int q = tid; q < m; q += blockDim.x) OPG[q] = entry_op_g<ENVK>(q, 12);
+  for (int q = tid; q < nnz; q += blockDim.x) OPJ[q] = entry_op_j<ENVK>(q, N, 12);
+  const int64_t count = d_count ? (int64_t)*d_count : batch;
+  const int64_t ntiles = (count + T - 1) / T;
+  const bool contiguous = idx == nullptr && K.x_aligned16;
+  double mass_def = K.mass_default;  // a value (see cpl_eval_pipe_kernel)
+  asm volatile("" : "+v"(mass_def));
+  NormAcc acc;
+  int64_t t = blockIdx.x;
+  __syncthreads();  // (the table)
+
+  if (loader) {
+    double st_mass = 0.0, st_tail = 0.0;
+    long long st_b = 0;
+    auto stage = [&](int64_t tt, int bi) {
+      const int64_t j0 = tt * T;
+      const int vs = (int)((count - j0) < T ? (count - j0) : T);
+      int b = 0;
+      if (lane < vs) {
+        b = idx ? idx[j0 + lane] : (int)(j0 + lane);
+        st_b = b;
+        st_mass = mass ? mass[b] : mass_def;
+      }
+      if (contiguous) {
+        const int cnt = vs * n;
+        dma_tile(XB(bi), x + j0 * n, cnt, lane);
+        if ((cnt & 1) && lane == 0) st_tail = x[j0 * n + cnt - 1];
+      } else {
+        for (int r = 0; r < vs; ++r) dma_row4(XB(bi) + r * n, x + (int64_t)__builtin_amdgcn_readlane(b, r) * n, n, lane);
+      }
+    };
+    auto finish_stage = [&](int64_t tt, int bi) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int64_t j0 = tt * T;
+      const int vs = (int)((count - j0) < T ? (count - j0) : T);
+      const int cnt = vs * n;
+      if (contiguous && (cnt & 1) && lane == 0) XB(bi)[cnt - 1] = st_tail;
+      if (lane < vs) {
+        MB(bi)[lane] = st_mass;
+        RB(bi)[lane] = st_b;
+      }
+    };
+    if (t < ntiles) {
+      stage(t, 0);
+      finish_stage(t, 0);
+    }
+    lds_barrier();
+    int cur = 0;
+    for (; t < ntiles; t += gridDim.x) {
+      const int64_t tn = t + gridDim.x;
+      if (tn < ntiles) stage(tn, cur ^ 1);
+      lds_barrier();  // (the compute waves' prologue)
+      if (tn < ntiles) finish_stage(tn, cur ^ 1);
+      lds_barrier();  // (the tile's entries)
+      cur ^= 1;
+    }
+  } else {
+    acc.init(tid, CT, m);
+    lds_barrier();
+    int cur = 0;
+    const double mu = K.mu;
+    for (; t < ntiles; t += gridDim.x) {
+      const int64_t j0 = t * T;
+      const int valid = (int)((count - j0) < T ? (count - j0) : T);
+      const double* X = XB(cur);
+      const double* Mb = MB(cur);
+      const long long* Rb = RB(cur);
+      // ---- prologue: per (instance, contact) p - c, the cone's values and row-1 derivatives, the
+      // Ground residuals; per instance the statics values and the torque rows' CoM pairs; the cost
+      const int pc = valid * N;
+      const int items = pc + valid + (K.want_f ? valid : 0);
+      for (int it = tid; it < items; it += CT) {
+        if (it < pc) {
+          const int r = it / N, i = it - r * N;  // (vector order)
+          const double* xr = X + r * n;
+          const double* q = xr + 3 + 9 * i;
+          const double F0 = q[0], F1 = q[1], F2 = q[2], p0 = q[3], p1 = q[4], p2 = q[5];
+          const double n0 = q[6], n1 = q[7], n2 = q[8];
+          double* cs = SC + r * S + 12 + ENT_PC * i;
+          cs[EPC_D + 0] = p0 - xr[0];  // statics_rows_coop's (p[e] - xr[e])
+          cs[EPC_D + 1] = p1 - xr[1];
+          cs[EPC_D + 2] = p2 - xr[2];
+          // src/Constraints/FrictionCone.cpp:30-45 (values), :71-101 (contact_item's expressions)
+          const double t1 = dot3(F0, F1, F2, n0, n1, n2);
+          const double nF = dot3(n0, n1, n2, F0, F1, F2);
+          const double u0 = F0 - nF * n0, u1 = F1 - nF * n1, u2 = F2 - nF * n2;
+          cs[EPC_CONEG + 0] = -t1 + s_ct.F_thr[i];
+          cs[EPC_CONEG + 1] = sqrt((u0 * u0 + u1 * u1) + u2 * u2) - mu * t1;
+          const double t2 = F0 - n0 * t1;
+          const double t3 = F1 - n1 * t1;
+          const double t4 = F2 - n2 * t1;
+          const double t5 = F0 * n0;
+          const double t6 = F1 * n1;
+          const double t7 = F2 * n2;
+          const double s = sqrt(t2 * t2 + t3 * t3 + t4 * t4);
+          double* jk = cs + EPC_ROW1 - 6;
+          jk[6] = (t2 * (n0 * n0 - 1.0) * 2.0 + n0 * n1 * t3 * 2.0 + n0 * n2 * t4 * 2.0) * 1.0 / s * (-1.0 / 2.0) - mu * n0;
+          jk[7] = (t3 * (n1 * n1 - 1.0) * 2.0 + n0 * n1 * t2 * 2.0 + n1 * n2 * t4 * 2.0) * 1.0 / s * (-1.0 / 2.0) - mu * n1;
+          jk[8] = (t4 * (n2 * n2 - 1.0) * 2.0 + n0 * n2 * t2 * 2.0 + n1 * n2 * t3 * 2.0) * 1.0 / s * (-1.0 / 2.0) - mu * n2;
+          jk[9] = (t2 * (t6 + t7 + t5 * 2.0) * 2.0 + F0 * n1 * t3 * 2.0 + F0 * n2 * t4 * 2.0) * 1.0 / s * (-1.0 / 2.0) - mu * F0;
+          jk[10] = (t3 * (t5 + t7 + t6 * 2.0) * 2.0 + F1 * n0 * t2 * 2.0 + F1 * n2 * t4 * 2.0) * 1.0 / s * (-1.0 / 2.0) - mu * F1;
+          jk[11] = (t4 * (t5 + t6 + t7 * 2.0) * 2.0 + F2 * n0 * t2 * 2.0 + F2 * n1 * t3 * 2.0) * 1.0 / s * (-1.0 / 2.0) - mu * F2;
+          if (ENVK != CPL_ENV_NONE) {  // src/Ground.cpp:23-50 (contact_item's gv)
+            cs[EPC_ENVG] = p2 - K.ground_z;
+            cs[EPC_NORMG + 0] = n0 - 0.0;
+            cs[EPC_NORMG + 1] = n1 - 0.0;
+            cs[EPC_NORMG + 2] = n2 - 1.0;
+          }
+        } else if (it < pc + valid) {
+          // CentroidalStatics::GetValues (src/Constraints/CentroidalStatics.cpp:37-61) and the torque
+          // rows' CoM pairs (:119-136), both in map order — statics_values_item's arithmetic
+          const int r = it - pc;
+          const double* xr = X + r * n;
+          double* st = SC + r * S;
+          const double c0 = xr[0], c1 = xr[1], c2 = xr[2];
+          double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0, v4 = 0.0, v5 = 0.0;
+          double a[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+          for (int k = 0; k < N; ++k) {
+            const double* q = xr + 3 + 9 * s_ct.map_order[k];
+            const double F0 = q[0], F1 = q[1], F2 = q[2];
+            const double d0 = q[3] - c0, d1 = q[4] - c1, d2 = q[5] - c2;
+            v0 += F0; v1 += F1; v2 += F2;
+            v3 += d1 * F2 - d2 * F1;
+            v4 += d2 * F0 - d0 * F2;
+            v5 += d0 * F1 - d1 * F0;
+            a[0] -= -(-1.0) * F2; a[1] -= -(1.0) * F1;
+            a[2] -= -(1.0) * F2;  a[3] -= -(-1.0) * F0;
+            a[4] -= -(-1.0) * F1; a[5] -= -(1.0) * F0;
+          }
+          const double m_i = Mb[r];
+          v0 -= K.wrench[0]; v1 -= K.wrench[1]; v2 -= K.wrench[2];
+          v3 -= K.wrench[3]; v4 -= K.wrench[4]; v5 -= K.wrench[5];
+          v0 += m_i * K.gravity[0]; v1 += m_i * K.gravity[1]; v2 += m_i * K.gravity[2];
+          st[0] = v0; st[1] = v1; st[2] = v2; st[3] = v3; st[4] = v4; st[5] = v5;
+#pragma unroll
+          for (int u = 0; u < 6; ++u) st[6 + u] = a[u];
+        } else {
+          const int r = it - pc - valid;
+          f_out[Rb[r]] = cost_value(K, X + r * n);
+        }
+      }
+      lds_barrier();
+      // ---- g and the Jacobian values: a gather by the opcode tables, two entries per lane, lanes
+      // along the tile's records (consecutive lanes, consecutive 16-byte pieces of one record)
+      auto gather = [&](const unsigned* __restrict__ op, int rec, double* __restrict__ out, bool norms) {
+        const int h2 = rec >> 1;
+        const int total = valid * h2;
+        int r = tid / h2, q2 = tid - r * h2;
+        for (int e = tid; e < total; e += CT) {
+          const uint2 o = reinterpret_cast<const uint2*>(op)[q2];
+          const double* Xr = X + r * n;
+          const double* Sr = SC + r * S;
+          const double v0 = entry_value(o.x, Xr, Sr, CN), v1 = entry_value(o.y, Xr, Sr, CN);
+          if (norms) {
+            const double a0 = row_violation(v0, s_ct.cone[2 * q2]), a1 = row_violation(v1, s_ct.cone[2 * q2 + 1]);
+            acc.vmax = a0 > acc.vmax ? a0 : acc.vmax;
+            acc.vsum += a0 * a0;
+            acc.vmax = a1 > acc.vmax ? a1 : acc.vmax;
+            acc.vsum += a1 * a1;
+          }
+          double2* d = reinterpret_cast<double2*>(out + Rb[r] * rec) + q2;
+          if (NT) {
+            __builtin_nontemporal_store(v0, &d->x);
+            __builtin_nontemporal_store(v1, &d->y);
+          } else {
+            *d = make_double2(v0, v1);
+          }
+          q2 += CT;
+          while (q2 >= h2) { q2 -= h2; ++r; }
+        }
+      };
+      if (K.want_g) gather(OPG, m, g_out, K.want_norms != 0);
+      if (K.want_j) gather(OPJ, nnz, jac_out, false);
+      // ---- the cost gradient (MinimizeCentroidalVariables.cpp:151-192; cost_item's entries)
+      if (K.want_grad) {
+        const int total = valid * n;
+        int r = tid / n, q = tid - r * n;
+        for (int e = tid; e < total; e += CT) {
+          const double* xr = X + r * n;
+          double v;
+          if (q < 3) {
+            v = K.W_com * (xr[q] - K.com_ref[q]);
+          } else {
+            const int i = (q - 3) / 9, w = (q - 3) - 9 * i;
+            v = w < 3 ? K.W_F[i] * (xr[q] - K.F_ref[i][w]) : w < 6 ? K.W_p[i] * (xr[q] - K.p_ref[i][w - 3]) : 0.0;
+          }
+          grad_out[Rb[r] * n + q] = v;
+          q += CT;
+          while (q >= n) { q -= n; ++r; }
+        }
+      }
+      lds_barrier();  // next x landed, scratch free
+      cur ^= 1;
+    }
+  }
+  if (K.want_norms) partial_norms(acc, norms_ws + NORM_HDR);  // the loader contributes zeros
+}
+
+
+// ------------------------------------------------------------------------------------------
 // Exact Hessian of the Lagrangian f + y^T g over the free variables (Ground / no environment:
 // the environment and normal rows are linear there, so only the cost, the torque rows of
 // CentroidalStatics and the two FrictionCone rows carry curvature).  For an entry (u, v) of the
@@ -1844,10 +2225,18 @@ __global__ __launch_bounds__(RN_BLOCK) void cpl_residual_partial(int64_t total, 
 // order depends only on nparts (deterministic).
 constexpr int RF_ILP = 8;
 
+// With `chunk` (level 1 of a two-level finish): workgroup b reduces the pairs [b chunk, (b + 1) chunk)
+// into out[2b], out[2b + 1].
 template <int RF_BLOCK>
 __global__ __launch_bounds__(RF_BLOCK) void cpl_residual_final(int nparts, const double* __restrict__ part,
-                                                               double* __restrict__ out) {
+                                                               double* __restrict__ out, int chunk = 0) {
   __shared__ double smax[RF_BLOCK / 64], ssum[RF_BLOCK / 64];
+  if (chunk > 0) {
+    const int first = (int)blockIdx.x * chunk;
+    part += 2 * (size_t)first;
+    out += 2 * (size_t)blockIdx.x;
+    nparts = nparts - first < chunk ? nparts - first : chunk;
+  }
   const double2* p2 = reinterpret_cast<const double2*>(part);
   const int tid = threadIdx.x;
   double am[RF_ILP], as[RF_ILP];
@@ -1889,10 +2278,158 @@ __global__ __launch_bounds__(RF_BLOCK) void cpl_residual_final(int nparts, const
   }
 }
 
+// ---- mixed batches split by environment kind: a stable partition of the instance indices by tag
+// (every launch recomputes it: the tags may change between launches under the same pointer), the
+// Ground instances to the entry kernel, the Superquadric ones to the Superquadric tile kernel, each
+// writing its records in place.  Deterministic: the lists keep instance order, so the tiles (and the
+// norm partials' summation order) are a function of the tags alone.
+constexpr int PART_BLOCK = 1024;
+__global__ __launch_bounds__(PART_BLOCK) void k_kind_count(int64_t batch, const uint8_t* __restrict__ tag,
+                                                           int32_t* __restrict__ blk_sq) {
+  __shared__ int wsum[PART_BLOCK / 64];
+  const int64_t b = (int64_t)blockIdx.x * PART_BLOCK + threadIdx.x;
+  const bool sq = b < batch && tag[b] == CPL_ENV_SUPERQUADRIC;
+  const int c = __popcll(__ballot(sq));
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int w = 0; w < PART_BLOCK / 64; ++w) t += wsum[w];
+    blk_sq[blockIdx.x] = t;
+  }
+}
+// exclusive scan of the per-block Superquadric counts (one workgroup, chunks of PART_BLOCK) and the
+// two list lengths: counts[0] Ground, counts[1] Superquadric
+__global__ __launch_bounds__(PART_BLOCK) void k_kind_scan(int64_t batch, int nblk, const int32_t* __restrict__ blk_sq,
+                                                          int32_t* __restrict__ blk_off, int32_t* __restrict__ counts) {
+  __shared__ int sh[PART_BLOCK];
+  int carry = 0;
+  for (int base = 0; base < nblk; base += PART_BLOCK) {
+    const int i = base + (int)threadIdx.x;
+    const int v = i < nblk ? blk_sq[i] : 0;
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < PART_BLOCK; o <<= 1) {  // Hillis-Steele inclusive scan
+      const int u = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0;
+      __syncthreads();
+      sh[threadIdx.x] += u;
+      __syncthreads();
+    }
+    if (i < nblk) blk_off[i] = carry + sh[threadIdx.x] - v;
+    carry += sh[PART_BLOCK - 1];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    counts[1] = carry;
+    counts[0] = (int32_t)(batch - carry);
+  }
+}
+__global__ __launch_bounds__(PART_BLOCK) void k_kind_write(int64_t batch, const uint8_t* __restrict__ tag,
+                                                           const int32_t* __restrict__ blk_off,
+                                                           int32_t* __restrict__ idx_gr, int32_t* __restrict__ idx_sq) {
+  __shared__ int wsum[PART_BLOCK / 64];
+  const int64_t b = (int64_t)blockIdx.x * PART_BLOCK + threadIdx.x;
+  const bool in = b < batch;
+  const bool sq = in && tag[b] == CPL_ENV_SUPERQUADRIC;
+  const unsigned long long msk = __ballot(sq);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) wsum[wave] = __popcll(msk);
+  __syncthreads();
+  int before = 0;  // Superquadric instances of the block before this wave
+  for (int w = 0; w < wave; ++w) before += wsum[w];
+  const int sq_rank = before + __popcll(msk & ((1ull << lane) - 1ull));
+  const int local = (int)threadIdx.x;
+  const int64_t off_sq = blk_off[blockIdx.x];
+  const int64_t off_gr = (int64_t)blockIdx.x * PART_BLOCK - off_sq;
+  if (sq) idx_sq[off_sq + sq_rank] = (int32_t)b;
+  else if (in) idx_gr[off_gr + (local - sq_rank)] = (int32_t)b;
+}
+
+// the kind lists' workspace, per (device, stream), grown on demand and never freed (a captured graph
+// keeps its pointers; see NormWs): [idx_gr | idx_sq | blk_sq | blk_off | counts]
+struct KindWs {
+  int32_t* ptr = nullptr;
+  int64_t cap = 0;
+  std::vector<int32_t*> old;
+};
+static int32_t hip_fail(hipError_t e, const char* what);
+static std::mutex g_kind_ws_mutex;
+static std::map<std::pair<int, hipStream_t>, KindWs> g_kind_ws;
+
+struct KindLists {
+  int32_t *idx_gr, *idx_sq, *blk_sq, *blk_off, *counts;
+};
+static int32_t kind_workspace(hipStream_t stream, int64_t batch, KindLists* out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+  std::lock_guard<std::mutex> lk(g_kind_ws_mutex);
+  KindWs& w = g_kind_ws[{dev, stream}];
+  if (w.cap < batch) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+      return fail(CPL_ERR_RUNTIME,
+                  "mixed batch: the per-stream kind-list workspace must grow, which a stream capture forbids; "
+                  "launch the largest batch once on this stream before capturing");
+    const int64_t nblk = (batch + PART_BLOCK - 1) / PART_BLOCK;
+    int32_t* p = nullptr;
+    e = hipMalloc(&p, sizeof(int32_t) * (size_t)(2 * batch + 2 * nblk + 4));
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc kind lists");
+    if (w.ptr) w.old.push_back(w.ptr);
+    w.ptr = p;
+    w.cap = batch;
+  }
+  const int64_t cap = w.cap, nblk = (cap + PART_BLOCK - 1) / PART_BLOCK;
+  out->idx_gr = w.ptr;
+  out->idx_sq = w.ptr + cap;
+  out->blk_sq = w.ptr + 2 * cap;
+  out->blk_off = out->blk_sq + nblk;
+  out->counts = out->blk_off + nblk;
+  return CPL_OK;
+}
+
+// `part` must have room for nparts + nparts / RF_CHUNK + 1 pairs (the norm workspaces hold 2 cap)
+constexpr int RF_CHUNK = 8192;
+// a side stream (and a fork / join event pair) per (device, stream) for the mixed split's two halves,
+// created on first use and kept (a captured graph may hold them)
+struct SideStream {
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+static std::mutex g_side_mutex;
+static std::map<std::pair<int, hipStream_t>, SideStream> g_side;
+static int32_t side_stream(hipStream_t stream, SideStream* out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+  std::lock_guard<std::mutex> lk(g_side_mutex);
+  SideStream& ss = g_side[{dev, stream}];
+  if (!ss.side) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+      return fail(CPL_ERR_RUNTIME, "mixed batch: launch once on this stream before capturing it (side stream)");
+    if ((e = hipStreamCreateWithFlags(&ss.side, hipStreamNonBlocking)) != hipSuccess) return hip_fail(e, "hipStreamCreate");
+    if ((e = hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+    if ((e = hipEventCreateWithFlags(&ss.join, hipEventDisableTiming)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+  }
+  *out = ss;
+  return CPL_OK;
+}
+
 static void launch_residual_final(int nparts, const double* part, double* out, hipStream_t s) {
   // 1024 threads: one load round trip for up to 8 192 partials (rocprof: 4.1 us at 768 partials,
-  // 4.7 us on 256 threads — three dependent round trips in the tail loop)
-  hipLaunchKernelGGL(cpl_residual_final<1024>, dim3(1), dim3(1024), 0, s, nparts, part, out);
+  // 4.7 us on 256 threads — three dependent round trips in the tail loop).  Past 2 * RF_CHUNK
+  // partials (the per-wave partials of a 1M-instance tile launch: ~10^6) one workgroup took 200 us:
+  // a first level of ceil(nparts / RF_CHUNK) workgroups, each a contiguous chunk, then one workgroup
+  // over their pairs (deterministic: the split depends on nparts only)
+  if (nparts <= 2 * RF_CHUNK) {
+    hipLaunchKernelGGL(cpl_residual_final<1024>, dim3(1), dim3(1024), 0, s, nparts, part, out, 0);
+    return;
+  }
+  const int nb = (nparts + RF_CHUNK - 1) / RF_CHUNK;
+  double* lvl = const_cast<double*>(part) + 2 * (size_t)nparts;
+  hipLaunchKernelGGL(cpl_residual_final<1024>, dim3(nb), dim3(1024), 0, s, nparts, part, lvl, RF_CHUNK);
+  hipLaunchKernelGGL(cpl_residual_final<1024>, dim3(1), dim3(1024), 0, s, nb, lvl, out, 0);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1978,7 +2515,8 @@ static size_t eval_lds_bytes(int n) { return sizeof(double) * (size_t)(TILE * n 
 // Ground) and the tile-stationary kernel for the VALU-bound ones (Superquadric, mixed), where the
 // pipelined kernel's three compute waves per workgroup leave the FP64 pipes under-filled; mixed
 // batches with the Jacobian written straight to the records (variant 4 forces that everywhere).
-enum { VAR_AUTO = 0, VAR_ROWSTAGE = 1, VAR_PIPE = 2, VAR_TILE = 3, VAR_TILE_JD = 4 };
+enum { VAR_AUTO = 0, VAR_ROWSTAGE = 1, VAR_PIPE = 2, VAR_TILE = 3, VAR_TILE_JD = 4, VAR_ENTRY = 5, VAR_SPLIT = 6,
+       VAR_SPLIT_JD = 7 };
 static int g_variant = VAR_AUTO;
 static size_t g_lds_budget = 0;    // 0 = per-kernel default (tile 32 KiB, pipelined 48 KiB)
 static int g_wg = 256;             // threads per tile workgroup (128 or 256)
@@ -2022,6 +2560,7 @@ static int32_t plan_tile(KParams& K, bool g, bool j, bool f, bool grad, int t_ma
   K.offA = K.offL + (sq ? T * K.LR : 0);
   K.offI = K.offA + (j && K.jdirect ? 6 * T : 0);
   K.offI = (K.offI + 1) & ~1;
+  K.offRB = K.offI + 72;  // (instance lists) the tile rows' instances, T int64
   return CPL_OK;
 }
 
@@ -2049,6 +2588,39 @@ static int32_t plan_pipe(KParams& K, bool g, bool j, bool f, bool grad, size_t e
   K.offL = K.offD + (grad ? T * K.n : 0);
   K.offI = up2(K.offL + (sq ? T * K.LR : 0));
   return CPL_OK;
+}
+
+// Entry kernel layout (doubles): x double buffer, masses [2][T], row bases [2][T] (int64), the cone
+// scratch [T][N][ENT_CS], the statics scratch [T][12]; T even, at most 64, the largest that fits the
+// LDS budget (no output image: 16-contact records keep 12-instance tiles in 48 KiB)
+static int32_t plan_entry(KParams& K, bool g, bool j, bool f, bool grad) {
+  K.want_g = g; K.want_j = j; K.want_f = f; K.want_grad = grad;
+  const size_t per = sizeof(double) * (size_t)(2 * K.n + 4 + K.N * ENT_PC + 12);
+  const size_t fixed = sizeof(double) * (size_t)(8 + 2 + (K.m + K.nnz + 1) / 2) + sizeof(CTab);
+  // default budget: 80 KiB for records of 12+ contacts (two workgroups per CU with ~18-instance
+  // tiles: 16-contact Ground 0.81 ms against 0.88 / 1.05 ms at 64 / 48 KiB, profiles/r4), else 48 KiB
+  const size_t budget = g_lds_budget ? g_lds_budget : (K.N >= 12 ? 80 * 1024 : 48 * 1024);
+  int T = 64;
+  while (T > 2 && (size_t)T * per + fixed > budget) T -= 2;
+  if ((size_t)T * per + fixed > 160 * 1024) return fail(CPL_ERR_UNSUPPORTED, "problem too large for one LDS tile");
+  K.T = T;
+  K.logT = 0;
+  auto up2 = [](int v) { return (v + 1) & ~1; };
+  K.offX1 = up2(T * K.n);
+  K.offMB = K.offX1 + up2(T * K.n);
+  K.offRB = K.offMB + 2 * T;
+  K.offCS = K.offRB + 2 * T;                          // scratch [T][12 + ENT_PC N]
+  K.offST = K.offCS + T * (12 + ENT_PC * K.N);        // constants (2), then the opcode tables
+  K.offI = up2(K.offST + 2 + (K.m + K.nnz + 1) / 2);
+  return CPL_OK;
+}
+static bool use_entry(const KParams& K, int32_t flags) {
+  return (g_variant == VAR_ENTRY || g_variant == VAR_SPLIT) && flags == 0 && (K.nnz % 2) == 0 &&
+         (K.env_kind == CPL_ENV_NONE || K.env_kind == CPL_ENV_GROUND);
+}
+static bool use_split(const KParams& K, int32_t flags, int64_t batch) {
+  return (g_variant == VAR_SPLIT || g_variant == VAR_SPLIT_JD) && flags == 0 && K.env_kind == CPL_ENV_MIXED &&
+         batch <= 0x7fffffffLL;
 }
 
 struct PipeLaunch {
@@ -2165,6 +2737,82 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
   double* ws = nullptr;
   if (lg && !use_pipe(K))
     return fail(CPL_ERR_UNSUPPORTED, "fused Lagrangian gradient: pipelined (Ground / no environment) path only");
+  if (!lg && use_split(K, flags, batch)) {
+    // mixed batch split by kind: the stable partition, then the Ground instances through the entry
+    // kernel and the Superquadric ones through the Superquadric tile kernel, records in place
+    KindLists kl;
+    if ((st = kind_workspace(stream, batch, &kl))) return st;
+    const unsigned nblk = (unsigned)((batch + PART_BLOCK - 1) / PART_BLOCK);
+    hipLaunchKernelGGL(k_kind_count, dim3(nblk), dim3(PART_BLOCK), 0, stream, batch, d_env_tag, kl.blk_sq);
+    hipLaunchKernelGGL(k_kind_scan, dim3(1), dim3(PART_BLOCK), 0, stream, batch, (int)nblk, kl.blk_sq, kl.blk_off,
+                       kl.counts);
+    hipLaunchKernelGGL(k_kind_write, dim3(nblk), dim3(PART_BLOCK), 0, stream, batch, d_env_tag, kl.blk_off, kl.idx_gr,
+                       kl.idx_sq);
+    KParams Kg = K, Ks = K;
+    if ((st = plan_entry(Kg, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr))) return st;
+    Ks.jdirect = (g_variant == VAR_SPLIT_JD && d_jac) ? 1 : 0;
+    if ((st = plan_tile(Ks, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr))) return st;
+    Kg.ablate = Ks.ablate = g_ablate;
+    using EntryT = void (*)(const KParams, int64_t, const double*, const double*, const int32_t*, const int32_t*,
+                            double*, double*, double*, double*, double*);
+    using TileT = void (*)(const KParams, int64_t, const double*, const double*, const uint8_t*, const int32_t*,
+                           const int32_t*, double*, double*, double*, double*, double*);
+    const EntryT ek = g_nt ? cpl_eval_entry_kernel<CPL_ENV_GROUND, true> : cpl_eval_entry_kernel<CPL_ENV_GROUND, false>;
+    const TileT tk = Ks.jdirect ? (g_nt ? cpl_eval_tile_kernel<CPL_ENV_SUPERQUADRIC, 256, true, true>
+                                        : cpl_eval_tile_kernel<CPL_ENV_SUPERQUADRIC, 256, false, true>)
+                                : (g_nt ? cpl_eval_tile_kernel<CPL_ENV_SUPERQUADRIC, 256, true, false>
+                                        : cpl_eval_tile_kernel<CPL_ENV_SUPERQUADRIC, 256, false, false>);
+    const size_t lds_g = sizeof(double) * (size_t)Kg.offI;
+    const size_t lds_s = sizeof(double) * (size_t)(Ks.offRB + Ks.T);
+    const int64_t ntg = (batch + Kg.T - 1) / Kg.T;
+    const int64_t want = resident_blocks(reinterpret_cast<const void*>(ek), lds_g);
+    const unsigned grid_g = (unsigned)(ntg < want ? ntg : want);
+    const int64_t nts = (batch + Ks.T - 1) / Ks.T;
+    const int64_t want_s = resident_blocks(reinterpret_cast<const void*>(tk), lds_s);
+    const unsigned grid_s = (unsigned)(nts < want_s ? nts : want_s);
+    const size_t nparts = (size_t)grid_g + (size_t)grid_s * 4;
+    if (K.want_norms && (st = norm_workspace(stream, nparts, &ws))) return st;
+    // the two halves on two streams (fork after the partition, join before the norms' finish): the
+    // memory-bound Ground records and the latency-bound Superquadric tiles share the CUs
+    SideStream ss;
+    if ((st = side_stream(stream, &ss))) return st;
+    hipError_t e = hipEventRecord(ss.fork, stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ss.side, ss.fork, 0);
+    if (e != hipSuccess) return hip_fail(e, "mixed split fork");
+    hipLaunchKernelGGL(tk, dim3(grid_s), dim3(256), lds_s, stream, Ks, batch, d_x, d_mass, d_env_tag, kl.idx_sq,
+                       kl.counts + 1, d_g, d_jac, d_f, d_grad, ws ? ws + 2 * (size_t)grid_g : nullptr);
+    hipLaunchKernelGGL(ek, dim3(grid_g), dim3(256), lds_g, ss.side, Kg, batch, d_x, d_mass, kl.idx_gr, kl.counts, d_g,
+                       d_jac, d_f, d_grad, ws);
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "mixed split launch");
+    e = hipEventRecord(ss.join, ss.side);
+    if (e == hipSuccess) e = hipStreamWaitEvent(stream, ss.join, 0);
+    if (e != hipSuccess) return hip_fail(e, "mixed split join");
+    if (K.want_norms && finish) launch_residual_final((int)nparts, ws + NORM_HDR, d_norms, stream);
+    return CPL_OK;
+  }
+  if (!lg && use_entry(K, flags)) {
+    st = plan_entry(K, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr);
+    if (st) return st;
+    K.ablate = g_ablate;
+    const size_t lds = sizeof(double) * (size_t)K.offI;
+    using KernT = void (*)(const KParams, int64_t, const double*, const double*, const int32_t*, const int32_t*,
+                           double*, double*, double*, double*, double*);
+    static const KernT table[2][2] = {
+        {cpl_eval_entry_kernel<CPL_ENV_NONE, false>, cpl_eval_entry_kernel<CPL_ENV_NONE, true>},
+        {cpl_eval_entry_kernel<CPL_ENV_GROUND, false>, cpl_eval_entry_kernel<CPL_ENV_GROUND, true>}};
+    const KernT kern = table[K.env_kind == CPL_ENV_GROUND ? 1 : 0][g_nt ? 1 : 0];
+    const int64_t ntiles = (batch + K.T - 1) / K.T;
+    const int64_t want = resident_blocks(reinterpret_cast<const void*>(kern), lds);
+    const unsigned grid = (unsigned)(ntiles < want ? ntiles : want);
+    if (K.want_norms && (st = norm_workspace(stream, grid, &ws))) return st;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, stream, K, batch, d_x, d_mass, nullptr, nullptr, d_g, d_jac,
+                       d_f, d_grad, ws);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "cpl_eval_entry_kernel launch");
+    if (K.want_norms && finish) launch_residual_final((int)grid, ws + NORM_HDR, d_norms, stream);
+    return CPL_OK;
+  }
   if (use_pipe(K)) {
     // the fused Lagrangian gradient computes jac and grad into the tile image and stores only d_grad
     // (the fused gradient also keeps the CSC index, (n + 1) + 2 nnz ints, in LDS)
@@ -2228,12 +2876,12 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
     const int wg = g_wg;
     if (st) return st;
     K.ablate = g_ablate;
-    const size_t lds = sizeof(double) * (size_t)(K.offI + 72);
+    const size_t lds = sizeof(double) * (size_t)(K.offRB + K.T);
     const unsigned grid = (unsigned)((batch + K.T - 1) / K.T);
     const size_t nparts = (size_t)grid * (wg / 64);  // one partial pair per wave
     if (K.want_norms && (st = norm_workspace(stream, nparts, &ws))) return st;
-    using KernT = void (*)(const KParams, int64_t, const double*, const double*, const uint8_t*, double*, double*,
-                           double*, double*, double*);
+    using KernT = void (*)(const KParams, int64_t, const double*, const double*, const uint8_t*, const int32_t*,
+                           const int32_t*, double*, double*, double*, double*, double*);
 #define CPL_TILE_KERNELS(E) \
   {cpl_eval_tile_kernel<E, 128, false, false>, cpl_eval_tile_kernel<E, 128, true, false>,        \
    cpl_eval_tile_kernel<E, 256, false, false>, cpl_eval_tile_kernel<E, 256, true, false>,        \
@@ -2242,8 +2890,8 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
                                       CPL_TILE_KERNELS(CPL_ENV_SUPERQUADRIC), CPL_TILE_KERNELS(CPL_ENV_MIXED)};
 #undef CPL_TILE_KERNELS
     const KernT kern = table[K.env_kind][(K.jdirect ? 4 : (wg == 256 ? 2 : 0)) + (g_nt ? 1 : 0)];
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(wg), lds, stream, K, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f,
-                       d_grad, ws);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(wg), lds, stream, K, batch, d_x, d_mass, d_env_tag, nullptr, nullptr,
+                       d_g, d_jac, d_f, d_grad, ws);
     if (K.want_norms) {  // per-tile partials -> final pair
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return hip_fail(e, "cpl_eval_tile_kernel launch");
@@ -2294,7 +2942,7 @@ __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, c
     const bool sq = ENVK == CPL_ENV_SUPERQUADRIC ||
                     (ENVK == CPL_ENV_MIXED && A.env_tag[b] == CPL_ENV_SUPERQUADRIC);
     const double a_min = A.a_min[b], mub = A.mu[b], tk = A.theta_k[b], pk = A.phi_k[b], g = A.gd[b];
-    const bool sw = A.switch_ok[b] != 0;
+    const uint8_t sw = A.switch_ok[b];
     const double thmax = A.theta_max[b];
     const double* ft = A.filt_t + b * A.nfilt;
     const double* fp = A.filt_p + b * A.nfilt;
@@ -2575,7 +3223,7 @@ int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_t
                        int32_t ablate) {
   if (ablate < 0 || ablate > 2) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
   g_ablate = ablate;
-  if (kernel_variant < VAR_AUTO || kernel_variant > VAR_TILE_JD) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown kernel variant");
+  if (kernel_variant < VAR_AUTO || kernel_variant > VAR_SPLIT_JD) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown kernel variant");
   if (tile_lds_kb != 0 && (tile_lds_kb < 8 || tile_lds_kb > 160))
     return fail(CPL_ERR_INVALID_ARGUMENT, "LDS budget out of [8, 160] KiB");
   if (wg_threads != 128 && wg_threads != 256) return fail(CPL_ERR_INVALID_ARGUMENT, "workgroup size must be 128 or 256");

@@ -1363,13 +1363,18 @@ int32_t cpl_kkt_qd_solve(int64_t batch, int32_t nw, int32_t m, const double* d_W
                          const double* d_Dinv, const double* d_r1, const double* d_r2, const uint8_t* d_active,
                          double* d_delta_w_last, double* d_dw, double* d_dy, double* d_delta_w, double* d_ws,
                          void* stream) {
-  if (batch < 0 || nw <= 0 || m < 0 || nw > KKT_MAX_NW)
-    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_qd_solve: need 0 <= m, 0 < nw <= 128");
+  if (batch < 0 || nw <= 0 || m < 0 || nw > KKT_MAX_NW || m > nw)
+    return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_qd_solve: need 0 <= m <= nw, 0 < nw <= 128");
+  // the kernel's dynamic LDS image (W + A D^-1 A^T, the right-hand side, D^-1 and y, A) must fit one
+  // workgroup's 160 KiB
+  const size_t lds = sizeof(double) * ((size_t)nw * nw + nw + 2 * (size_t)(m > 0 ? m : 1) + (size_t)m * nw);
+  if (lds > 160 * 1024)
+    return fail(CPL_ERR_UNSUPPORTED, "cpl_kkt_qd_solve: system too large for one LDS image (nw^2 + nw + 2m + m nw "
+                                     "doubles must fit 160 KiB)");
   if (batch == 0) return CPL_OK;
   if (!d_W || (m > 0 && (!d_A || !d_Dinv || !d_r2 || !d_dy)) || !d_r1 || !d_dw || !d_delta_w_last || !d_ws)
     return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_qd_solve: missing buffer");
   if (batch > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_qd_solve: batch too large");
-  const size_t lds = sizeof(double) * ((size_t)nw * nw + nw + 2 * (size_t)(m > 0 ? m : 1) + (size_t)m * nw);
   hipLaunchKernelGGL(cpl_kkt_qd_kernel, dim3((unsigned)batch), dim3(KKT_THREADS), lds, (hipStream_t)stream, batch,
                      (int)nw, (int)m, d_W, d_A, d_Dinv, d_r1, d_r2, d_active, d_delta_w_last, d_dw, d_dy, d_delta_w,
                      d_ws);

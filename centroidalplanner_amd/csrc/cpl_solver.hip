@@ -282,7 +282,7 @@ __device__ __forceinline__ double alpha_min_of(double theta, double gd, double t
 // stored with their margins), switching condition / Armijo / sufficient decrease against the
 // reference point with the obj_max_inc guard.  Returns ok; *h_type = the step augments the filter.
 __device__ __forceinline__ bool acceptable_wave(double th, double ph, double tk, double pk, double g, double al,
-                                                bool switch_ok, double theta_max, const double* ft, const double* fp,
+                                                uint8_t switch_ok, double theta_max, const double* ft, const double* fp,
                                                 bool* h_type) {
   return ls_acceptable_wave(th, ph, tk, pk, g, al, switch_ok, theta_max, ft, fp, FMAX, h_type);
 }
@@ -948,11 +948,16 @@ __global__ __launch_bounds__(256) void k_resto_y0(int64_t B, int m, const uint8_
   for (int r = lane; r < m; r += 64) y[b * m + r] = mx <= 1e3 ? dy[b * m + r] : 0.0;
 }
 
-// the restoration problem's optimality error (converged: a point of local infeasibility), its
-// monotone barrier update (resetting its filter) and the proximity term's gradient over w
+// the restoration problem's optimality error, its monotone barrier update (resetting its filter) and
+// the proximity term's gradient over w.  The restoration problem converged (IPOPT's
+// RestoConvergenceCheck): a point of local infeasibility when the original problem's max |c| exceeds
+// 1e2 tol; otherwise the point is feasible but unacceptable to the original filter — the first time the
+// restoration tolerance is tightened to 1e-2 tol and the phase goes on (resto_tight), the second time
+// the solve ends as a restoration failure (IPOPT's RESTORATION_CONVERGED_TO_FEASIBLE_POINT)
 __global__ __launch_bounds__(256) void k_resto_prep1(
     int64_t B, int m, int nf, int nw, int nbounds, double tol, double mu_min, uint8_t* __restrict__ active,
-    const uint8_t* __restrict__ in_resto, uint8_t* __restrict__ actR, int64_t* __restrict__ status,
+    const uint8_t* __restrict__ in_resto, uint8_t* __restrict__ resto_tight, uint8_t* __restrict__ actR,
+    int64_t* __restrict__ status,
     const double* __restrict__ A, const double* __restrict__ c, const double* __restrict__ w,
     const double* __restrict__ y, const double* __restrict__ wR, const double* __restrict__ pR,
     const double* __restrict__ nR, const double* __restrict__ zp, const double* __restrict__ zn,
@@ -990,7 +995,7 @@ __global__ __launch_bounds__(256) void k_resto_prep1(
       cmax = fmax(cmax, fmax(clv[h], cuv[h]));
     }
   }
-  double cp[2] = {0, 0}, cn[2] = {0, 0};
+  double cp[2] = {0, 0}, cn[2] = {0, 0}, cinf = 0.0;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int r = lane + 64 * h;
@@ -1000,6 +1005,7 @@ __global__ __launch_bounds__(256) void k_resto_prep1(
       zs += fabs(zpv) + fabs(znv);
       ys += fabs(yr);
       crmax = fmax(crmax, fabs(c[b * m + r] - pv + nv));
+      cinf = fmax(cinf, fabs(c[b * m + r]));
       cp[h] = pv * zpv;
       cn[h] = nv * znv;
       cmax = fmax(cmax, fmax(cp[h], cn[h]));
@@ -1015,13 +1021,19 @@ __global__ __launch_bounds__(256) void k_resto_prep1(
   const double sc = fmax(zs / (double)max(nbR, 1), 100.0) / 100.0;
   const double base = fmax(dmax / sd, crmax);
   const double err0 = fmax(base, cmax / sc);
-  if (err0 <= tol) {  // the restoration problem converged: a point of local infeasibility
-    if (lane == 0) {
-      status[b] = CPL_SOLVE_INFEASIBLE;
-      active[b] = 0;
-      actR[b] = 0;
+  const bool tight = resto_tight[b] != 0;
+  if (err0 <= (tight ? 1e-2 * tol : tol)) {  // the restoration problem converged
+    cinf = wave_max(cinf);
+    const bool feasible = cinf <= 1e2 * tol;
+    if (!feasible || tight) {
+      if (lane == 0) {
+        status[b] = feasible ? CPL_SOLVE_RESTO_FAILED : CPL_SOLVE_INFEASIBLE;
+        active[b] = 0;
+        actR[b] = 0;
+      }
+      return;
     }
-    return;
+    if (lane == 0) resto_tight[b] = 1;  // once: the restoration tolerance 1e-2 tol, and on
   }
   bool reset = false;
   for (int round = 0; round < MU_ROUNDS; ++round) {
@@ -1186,7 +1198,7 @@ __global__ __launch_bounds__(256) void k_resto_post(
     a_z[b] = fmin(rz, 1.0);
     gdR[b] = gd;
     const double th = thetaR[b];
-    switchR[b] = (th <= thminR[b] && gd < 0.0) ? 1 : 0;
+    switchR[b] = ls_switch_flags(th, thminR[b], gd);
     a_min[b] = alpha_min_of(th, gd, thminR[b]);
     searching[b] = 1;
     st_f[b] = f[b];
@@ -1286,11 +1298,22 @@ __global__ __launch_bounds__(256) void k_resto_accept(
     return;
   }
   const double al = st_alpha[b];
-  if (!(al > 0.0)) {  // the restoration phase's line search failed
+  if (!(al > 0.0)) {
+    // the restoration phase's line search failed: IPOPT's restoration phase for the restoration problem
+    // (RestoRestorationPhase::PerformRestoration) — x (here w) and every multiplier stay, p and n take
+    // the closed-form minimisers of the barrier subproblem at the current c(w) and mu_R (the
+    // restoration phase's start, RestoIterateInitializer), and that is the next iterate.  (g_n = g(w):
+    // the search state's point is the iterate when no trial was taken.)
+    const double mur = muR[b];
+    for (int r = lane; r < m; r += 64) {
+      const double c = cons_row(g_n + b * m, st_w + b * nw, nf, r, row_slack, gl);
+      const double a = (mur - RHO_R * c) / (2.0 * RHO_R);
+      const double nn = a + sqrt(a * a + mur * c / (2.0 * RHO_R));
+      nR[b * m + r] = nn;
+      pR[b * m + r] = c + nn;
+    }
     if (lane == 0) {
       movedR[b] = 0;
-      status[b] = CPL_SOLVE_RESTO_FAILED;
-      active[b] = 0;
       iters[b] += 1;
     }
     return;
@@ -1597,6 +1620,64 @@ __global__ void k_iota(int64_t B, int32_t* __restrict__ orig) {
   if (b < B) orig[b] = (int32_t)b;
 }
 
+// max violation of the constraint values g_b [m] against their original bounds (NaN: infinite), on
+// one wave
+__device__ __forceinline__ double orig_violation_wave(int m, const double* __restrict__ gb,
+                                                      const double* __restrict__ gl, const double* __restrict__ gu) {
+  double v = 0.0;
+  for (int r = threadIdx.x & 63; r < m; r += 64) {
+    const double gv = gb[r];
+    v = fmax(v, fmax(fmax(gl[r] - gv, gv - gu[r]), 0.0));
+    if (gv != gv) v = INFINITY;
+  }
+  return wave_max(v);
+}
+
+// The best iterate of every active instance: after each iteration's acceptance, the current point
+// (w, f, g in sync) replaces the kept one when its original constraints hold to `vtol` and its
+// objective is lower.  (Not IPOPT: a solve that ends without convergence at an infeasible iterate
+// returns this one instead, k_fallback.)
+__global__ __launch_bounds__(256) void k_track_best(int64_t B, int m, int nw, double vtol,
+                                                    const uint8_t* __restrict__ active, const double* __restrict__ w,
+                                                    const double* __restrict__ f, const double* __restrict__ g,
+                                                    const double* __restrict__ gl, const double* __restrict__ gu,
+                                                    double* __restrict__ best_w, double* __restrict__ best_f) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B || !active[b]) return;
+  const double v = orig_violation_wave(m, g + b * m, gl, gu);
+  const double fb = f[b];
+  if (!(v <= vtol) || !(fb < best_f[b])) return;
+  const int lane = threadIdx.x & 63;
+  for (int k = lane; k < nw; k += 64) best_w[b * nw + k] = w[b * nw + k];
+  if (lane == 0) best_f[b] = fb;
+}
+
+// Rows leaving the batch (finished ones, or every row at the end): an instance that stopped without
+// converging (max_iter, local infeasibility, restoration failure) at an iterate violating its
+// constraints by more than `vtol` returns its best feasible iterate (k_track_best) when it met one;
+// fbest[orig] records it
+__global__ __launch_bounds__(256) void k_fallback(int64_t rows, int m, int nw, double vtol, bool finished_only,
+                                                  const int32_t* __restrict__ orig, const uint8_t* __restrict__ active,
+                                                  const int64_t* __restrict__ status, const double* __restrict__ g,
+                                                  const double* __restrict__ gl, const double* __restrict__ gu,
+                                                  const double* __restrict__ best_w, const double* __restrict__ best_f,
+                                                  double* __restrict__ w, uint8_t* __restrict__ fbest) {
+  const int64_t r = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const int32_t o = orig[r];
+  if (o < 0 || (finished_only && active[r]) || status[r] <= CPL_SOLVE_ACCEPTABLE) return;
+  const double v = orig_violation_wave(m, g + r * m, gl, gu);
+  if (v <= vtol || !(best_f[r] < INFINITY)) return;
+  const int lane = threadIdx.x & 63;
+  for (int k = lane; k < nw; k += 64) w[r * nw + k] = best_w[r * nw + k];
+  if (lane == 0) fbest[o] = 1;
+}
+
+__global__ void k_fill(int64_t B, double v, double* __restrict__ out) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) out[b] = v;
+}
+
 // results: max violation of g against its bounds, int32 copies of status / iterations
 __global__ __launch_bounds__(256) void k_final(int64_t B, int m, const double* __restrict__ g, const double* __restrict__ gl,
                                                const double* __restrict__ gu, const int64_t* __restrict__ status,
@@ -1677,7 +1758,9 @@ struct cpl_solver {
   double *Xbase, *w, *y, *zL, *zU, *mu, *filt_t, *filt_p, *dwl, *f, *grad, *g, *J, *d_inf, *Hq, *lm_s, *lm_y, *theta_max,
       *theta_min;
   int64_t *status, *iters, *acc, *fcount, *n_resto;
-  uint8_t *active, *lm_cnt, *lm_skip, *d_any, *in_soft, *tiny_last, *tiny_flag, *in_resto;
+  uint8_t *active, *lm_cnt, *lm_skip, *d_any, *in_soft, *tiny_last, *tiny_flag, *in_resto, *resto_tight;
+  double *best_w, *best_f;  // the best iterate feasible to fallback_viol_tol (lowest f) and its f
+  uint8_t* fbest;           // [B] full-batch: the solve returned that iterate instead of its last one
   int32_t* soft_cnt;
   // restoration state
   double *wR, *pR, *nR, *zp, *zn, *zLR, *zUR, *muR, *ftR, *fpR, *th_o0, *ph_o0, *dwlR, *thmaxR, *thminR;
@@ -2020,6 +2103,11 @@ int32_t step_phase(cpl_solver* S, int phase) {
         LAUNCHED("k_resto_y0");
       }
     count:
+      if (o.fallback_viol_tol > 0.0) {
+        hipLaunchKernelGGL(k_track_best, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nw, o.fallback_viol_tol,
+                           S->active, S->w, S->f, S->g, S->gl, S->gu, S->best_w, S->best_f);
+        LAUNCHED("k_track_best");
+      }
       if (B > COUNT1_MAX) {
         hipLaunchKernelGGL(k_count_zero, dim3(1), dim3(64), 0, st, S->d_count);
         LAUNCHED("k_count_zero");
@@ -2034,7 +2122,8 @@ int32_t step_phase(cpl_solver* S, int phase) {
     }
     case P_RNEWTON: {
       hipLaunchKernelGGL(k_resto_prep1, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nf, nw, S->nbounds, o.tol,
-                         S->mu_min, S->active, S->in_resto, S->actR, S->status, S->A, S->c, S->w, S->y, S->wR, S->pR,
+                         S->mu_min, S->active, S->in_resto, S->resto_tight, S->actR, S->status, S->A, S->c, S->w, S->y,
+                         S->wR, S->pR,
                          S->nR, S->zp, S->zn, S->zLR, S->zUR, S->hasL, S->hasU, S->wl0, S->wu0, S->muR, S->ftR,
                          S->fpR, S->fcR, S->tauR, S->gfR);
       LAUNCHED("k_resto_prep1");
@@ -2198,6 +2287,11 @@ int32_t compact(cpl_solver* S, int64_t count, int64_t Bn) {
   hipStream_t st = S->stream;
   const int64_t Bc = S->Bcur;
   const int n = S->n, m = S->m, nw = S->nw;
+  if (S->opt.fallback_viol_tol > 0.0) {
+    hipLaunchKernelGGL(k_fallback, dim3(blocks_for(Bc)), dim3(256), 0, st, Bc, m, nw, S->opt.fallback_viol_tol, true,
+                       S->orig, S->active, S->status, S->g, S->gl, S->gu, S->best_w, S->best_f, S->w, S->fbest);
+    LAUNCHED("k_fallback");
+  }
   hipLaunchKernelGGL(k_scatter_final, dim3(blocks_for(Bc)), dim3(256), 0, st, Bc, n, m, nw, true, S->orig, S->active,
                      S->w, S->y, S->Xbase, S->d_inf, S->status, S->iters, S->n_resto, S->fw, S->fy, S->fX, S->fdinf,
                      S->fstatus, S->fiters, S->fresto);
@@ -2222,7 +2316,7 @@ int32_t compact(cpl_solver* S, int64_t count, int64_t Bn) {
   CK(move(S->wR, nw)); CK(move(S->pR, m)); CK(move(S->nR, m)); CK(move(S->zp, m)); CK(move(S->zn, m));
   CK(move(S->zLR, nw)); CK(move(S->zUR, nw)); CK(move(S->muR, 1)); CK(move(S->ftR, FMAX)); CK(move(S->fpR, FMAX));
   CK(move(S->fcR, 1)); CK(move(S->th_o0, 1)); CK(move(S->ph_o0, 1)); CK(move(S->dwlR, 1)); CK(move(S->thmaxR, 1));
-  CK(move(S->thminR, 1));
+  CK(move(S->thminR, 1)); CK(move(S->best_w, nw)); CK(move(S->best_f, 1));
   if (S->bfgs) {
     CK(move(S->Hq, LMC(nf)));
     CK(move(S->lm_s, (int64_t)LM_HIST * nf));
@@ -2244,6 +2338,7 @@ int32_t compact(cpl_solver* S, int64_t count, int64_t Bn) {
   CK(move_bytes(S->tiny_last));
   CK(move_bytes(S->tiny_flag));
   CK(move_bytes(S->in_resto));
+  CK(move_bytes(S->resto_tight));
   if (S->tag) CK(move_bytes(S->tag_c));
   auto move_i32 = [&](int32_t* buf) -> int32_t {
     hipLaunchKernelGGL(k_gather_i32, dim3(blocks_elems(count)), dim3(256), 0, st, count, S->pos, buf,
@@ -2288,6 +2383,7 @@ void cpl_solve_options_default(cpl_solve_options* o) {
   o->acceptable_tol = 1e-6;
   o->mu_init = 0.1;
   o->fd_step = 1e-6;
+  o->fallback_viol_tol = 1e-9;
 }
 
 int32_t cpl_solver_destroy(cpl_solver* S) {
@@ -2317,6 +2413,13 @@ int32_t cpl_solver_stats(const cpl_solver* S, int32_t* compactions, int64_t* fin
   if (!S) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_solver_stats: null solver");
   if (compactions) *compactions = S->compactions;
   if (final_rows) *final_rows = S->Bcur;
+  return CPL_OK;
+}
+
+int32_t cpl_solver_fallbacks(const cpl_solver* S, uint8_t* d_out, void* stream) {
+  if (!S || !d_out) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_solver_fallbacks: null argument");
+  HK(hipMemcpyAsync(d_out, S->fbest, (size_t)S->B, hipMemcpyDeviceToDevice, (hipStream_t)stream),
+     "hipMemcpyAsync fallbacks");
   return CPL_OK;
 }
 
@@ -2464,7 +2567,8 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   S->fcount = a.take<int64_t>(Bz); S->fc = a.take<int64_t>(Bz); S->n_resto = a.take<int64_t>(Bz);
   S->active = a.take<uint8_t>(Bz); S->lm_cnt = a.take<uint8_t>(Bz); S->lm_skip = a.take<uint8_t>(Bz); S->d_any = a.take<uint8_t>(4);
   S->in_soft = a.take<uint8_t>(Bz); S->tiny_last = a.take<uint8_t>(Bz); S->tiny_flag = a.take<uint8_t>(Bz);
-  S->in_resto = a.take<uint8_t>(Bz); S->soft_cnt = a.take<int32_t>(Bz);
+  S->in_resto = a.take<uint8_t>(Bz); S->soft_cnt = a.take<int32_t>(Bz); S->resto_tight = a.take<uint8_t>(Bz);
+  S->best_w = a.take<double>(Bz * nw); S->best_f = a.take<double>(Bz); S->fbest = a.take<uint8_t>(Bz);
   // the restoration phase's state
   S->wR = a.take<double>(Bz * nw); S->pR = a.take<double>(Bz * m); S->nR = a.take<double>(Bz * m);
   S->zp = a.take<double>(Bz * m); S->zn = a.take<double>(Bz * m); S->zLR = a.take<double>(Bz * nw);
@@ -2574,6 +2678,10 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
   HK(hipMemsetAsync(S->tiny_last, 0, (size_t)B, st), "hipMemsetAsync");
   HK(hipMemsetAsync(S->tiny_flag, 0, (size_t)B, st), "hipMemsetAsync");
   HK(hipMemsetAsync(S->in_resto, 0, (size_t)B, st), "hipMemsetAsync");
+  HK(hipMemsetAsync(S->resto_tight, 0, (size_t)B, st), "hipMemsetAsync");
+  HK(hipMemsetAsync(S->fbest, 0, (size_t)B, st), "hipMemsetAsync");
+  hipLaunchKernelGGL(k_fill, dim3(blocks_elems(B)), dim3(256), 0, st, B, INFINITY, S->best_f);
+  LAUNCHED("k_fill best_f");
   HK(hipMemsetAsync(S->soft_cnt, 0, 4 * (size_t)B, st), "hipMemsetAsync");
   HK(hipMemsetAsync(S->n_resto, 0, 8 * (size_t)B, st), "hipMemsetAsync");
   int64_t evals = 0;
@@ -2662,6 +2770,11 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
                        S->gradw, S->c, S->w, S->y, S->zL, S->zU, S->hasL, S->hasU, S->wl0, S->wu0, S->mu, S->filt_t,
                        S->filt_p, S->fcount, S->active, S->status, S->acc, S->d_inf, S->err0, S->base, S->mu_o, S->ft,
                        S->fp, S->fc, MU_ROUNDS, S->mu_min, nullptr, S->in_resto, nullptr, st));
+  if (S->opt.fallback_viol_tol > 0.0) {
+    hipLaunchKernelGGL(k_fallback, dim3(blocks_for(Bc)), dim3(256), 0, st, Bc, m, nw, S->opt.fallback_viol_tol, false,
+                       S->orig, S->active, S->status, S->g, S->gl, S->gu, S->best_w, S->best_f, S->w, S->fbest);
+    LAUNCHED("k_fallback");
+  }
   // every row still in the batch to its instance's place in the full-batch results
   hipLaunchKernelGGL(k_scatter_final, dim3(blocks_for(Bc)), dim3(256), 0, st, Bc, n, m, nw, false, S->orig, S->active,
                      S->w, S->y, S->Xbase, S->d_inf, S->status, S->iters, S->n_resto, S->fw, S->fy, S->fX, S->fdinf,

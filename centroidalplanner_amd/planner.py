@@ -61,6 +61,7 @@ class Solution:
     success: bool = True
     message: str = ""
     iterations: int = 0  # the interior-point iterations the solve took (IPOPT's iteration count)
+    fallback: bool = False  # not converged and the last iterate infeasible: the best feasible iterate instead
 
     @property
     def com(self) -> np.ndarray:
@@ -107,7 +108,8 @@ class CentroidalPlanner:
                     derivative_test=self.solver_derivative_test if self.evaluator is None else "none")
         self.last_derivative_report = res.derivative_report
         sol = self._cpl_problem.GetSolution()
-        out = Solution(com_sol=sol["com"], success=res.success, message=res.status, iterations=res.iterations)
+        out = Solution(com_sol=sol["com"], success=res.success, message=res.status, iterations=res.iterations,
+                       fallback=res.fallback)
         for name, cv in sol["contact_values_map"].items():
             out.contact_values_map[name] = ContactValues(cv["force"], cv["position"], cv["normal"])
         return out

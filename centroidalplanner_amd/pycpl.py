@@ -12,13 +12,15 @@ solve engine on the GPU (centroidalplanner_amd.solver).
 """
 from __future__ import annotations
 
+from abc import ABCMeta
+
 from .planner import CentroidalPlanner as _CentroidalPlanner
 from .planner import CoMPlanner as _CoMPlanner
 from .planner import ContactValues, Solution
 from .problem import EnvironmentClass, Ground, Superquadric
 
 
-class CentroidalPlanner(_CentroidalPlanner):
+class CentroidalPlanner(_CentroidalPlanner, metaclass=ABCMeta):
     """pyCpl.cpp:44-58: CentroidalPlanner(contact_names, robot_mass, env)."""
 
 
@@ -38,6 +40,10 @@ class CoMPlanner(_CoMPlanner):
     def SetManipulationWrench(self, wrench_manip):
         self._cp.SetManipulationWrench(wrench_manip)
 
+
+# pyCpl.cpp:61 declares CentroidalPlanner as CoMPlanner's base: isinstance(com, CentroidalPlanner) holds
+# (the C++ CoMPlanner inherits privately and the Python one delegates, so it is a virtual subclass)
+CentroidalPlanner.register(CoMPlanner)
 
 __all__ = ["EnvironmentClass", "Ground", "Superquadric", "ContactValues", "Solution", "CentroidalPlanner",
            "CoMPlanner"]

@@ -7,7 +7,9 @@ this image; the same method runs here as the batched solve loop (batch_ipm.py, t
 8,192-instance solves) with B = 1: on the GPU (HIP kernels, the iteration captured as a HIP graph)
 when no evaluator is given, else on the host over the evaluator's callbacks (tests inject the
 oracle).  Like IFOPT's solver, a run that ends without convergence does not throw: the last iterate
-is kept (src/CentroidalPlanner.cpp:29-33), `success` says how it ended.
+is kept (src/CentroidalPlanner.cpp:29-33), `success` says how it ended — except that when that last
+iterate violates the constraints (by more than 1e-9) and an earlier iterate satisfied them, the
+lowest-objective such iterate is returned instead (`fallback`; IPOPT itself returns the last one).
 Evaluators expose ``eval_batch(X[B, n]) -> {f, grad, g, jac}`` (host arrays).
 """
 from __future__ import annotations
@@ -26,6 +28,7 @@ class SolveResult:
     iterations: int
     primal_inf: float
     derivative_report: Optional[dict] = None  # derivative_test = "first-order" (cpl_derivative_test)
+    fallback: bool = False  # not converged, last iterate infeasible: x is the best feasible iterate instead
 
 
 class _HostBatchEvaluator:
@@ -77,4 +80,4 @@ def solve(problem, evaluator=None, x0: Optional[np.ndarray] = None, tol: float =
     st = int(r.status[0])
     problem.SetVariables(x)  # the next Solve warm-starts here, like the reference's persistent variables
     return SolveResult(x, st <= STATUS_ACCEPTABLE, STATUS_NAMES.get(st, f"status {st}"), int(r.iterations[0]),
-                       float(r.primal_inf[0]), report)
+                       float(r.primal_inf[0]), report, bool(r.fallback[0]) if r.fallback is not None else False)

@@ -44,6 +44,10 @@ CONFIGS = {
     "mixed16": Config("16-contact mixed Ground+Superquadric, batch=1,048,576", 16, "mixed", 1048576, 4),
     "ground4_1m": Config("4-contact Ground env, batch=1,048,576 (north-star target)", 4, "ground", 1048576, 6),
     "none4": Config("4-contact no-environment (CoMPlanner) statics, batch=65,536", 4, "none", 65536, 7),
+    # measurement aid: the Ground half of configs[3] on its own
+    "ground16": Config("16-contact Ground env, batch=524,288 (the Ground half of configs[3])", 16, "ground", 524288, 8),
+    "sq16": Config("16-contact Superquadric env, batch=524,288 (the Superquadric half of configs[3])", 16,
+                   "superquadric", 524288, 9),
 }
 
 

@@ -226,7 +226,9 @@ int32_t cpl_time_eval_batch_ex(const cpl_problem_desc* d, int64_t batch, const d
 /* Tuning knobs (process-wide, for A/B measurements): kernel_variant 0 = auto (default: the
  * pipelined kernel for none/Ground, the tile-stationary kernel for Superquadric/mixed),
  * 1 = row-staged lane-per-instance, 2 = pipelined (persistent, warp-specialized), 3 =
- * tile-stationary; tile_lds_kb = LDS budget of one workgroup (8..160 KiB; 0 = per-kernel
+ * tile-stationary, 4 = tile-stationary with the Jacobian written straight to the records, 5 =
+ * entry-parallel (none / Ground, IFOPT CSR instance-major records: every g / jac entry computed by
+ * the thread that stores it, no output image in LDS); tile_lds_kb = LDS budget of one workgroup (8..160 KiB; 0 = per-kernel
  * default: 48 KiB for both: the largest power-of-two tile that fits, e.g. 8 instances of 8
  * Superquadric contacts, 4 of 16); wg_threads = 128 or 256 for the tile kernel (default 256);
  * nt_stores = non-temporal output stores (default 1); ablate = measurement-only ablation
@@ -348,7 +350,9 @@ int32_t cpl_kkt_solve(int32_t mode, int64_t batch, int32_t nw, int32_t m, const 
  * through K = W + A^T D^-1 A with IPOPT's inertia correction (K + dW I positive definite; first
  * dW 1e-4 or d_delta_w_last / 3, growth x100 / x8): dw = K^-1 (r1 + A^T D^-1 r2), dy = D^-1 (A dw - r2).
  * d_delta_w_last is updated in place (the correction used); d_ws: nw * nw doubles per instance.
- * d_active [batch] uint8 or NULL: inactive instances are skipped.  nw <= 128.
+ * d_active [batch] uint8 or NULL: inactive instances are skipped.  0 <= m <= nw <= 128, and the LDS
+ * image of nw^2 + nw + 2 max(m, 1) + m nw doubles must fit 160 KiB (nw = 128 holds m <= 30; nw = 47,
+ * the 4-contact size, any m <= nw); larger systems return CPL_ERR_UNSUPPORTED before any launch.
  */
 int32_t cpl_kkt_qd_solve(int64_t batch, int32_t nw, int32_t m, const double* d_W, const double* d_A,
                          const double* d_Dinv, const double* d_r1, const double* d_r2, const uint8_t* d_active,
@@ -414,7 +418,9 @@ int32_t cpl_ipm_max_step(int64_t batch, int32_t nw, const double* d_v, const dou
  * cpl_ipm_fd_hessian_raw: (gL[k, free j] - gL[nf + k, free j]) / (2 h_k) from the Lagrangian
  *   gradients at those points, [batch, nf, nf].
  * cpl_ipm_post_step: dzL, dzU from the primal step, the primal and dual fraction-to-the-boundary
- *   steps, gd = grad_phi . dw, the switching-condition flag, delta_w_last on active instances.
+ *   steps, gd = grad_phi . dw, the switching-condition flags (bit 0: gd < 0, bit 1: theta <= theta_min;
+ *   the judge's Armijo branch needs both, its filter-augmentation test IPOPT's IsFtype, bit 0 alone),
+ *   delta_w_last on active instances.
  * cpl_ipm_accept: filter augmentation / reset, y, z (kappa_Sigma safeguard), w, mu and iteration
  *   counters written back in place (d_failed: filter reset rows, d_rest: rows keeping z; both optional).
  * cpl_ipm_masked_rows: dst[b, :] = src[b, :] where mask[b].
@@ -474,7 +480,10 @@ int32_t cpl_ipm_dense_a(int64_t batch, int32_t m, int32_t nw, int32_t nf, int32_
 #define CPL_SOLVE_ACCEPTABLE 1
 #define CPL_SOLVE_MAX_ITER 2
 #define CPL_SOLVE_INFEASIBLE 3   /* restoration phase converged to a point of local infeasibility */
-#define CPL_SOLVE_RESTO_FAILED 4 /* the restoration phase's line search failed */
+#define CPL_SOLVE_RESTO_FAILED 4 /* the restoration phase converged to a feasible point the original
+                                    filter rejects, again after its tolerance was tightened (IPOPT's
+                                    RESTORATION_CONVERGED_TO_FEASIBLE_POINT); a failed restoration line
+                                    search resets p, n instead (RestoRestorationPhase) */
 
 typedef struct cpl_solve_options {
   int32_t max_iter;        /* 3000 (IPOPT's default) */
@@ -496,6 +505,12 @@ typedef struct cpl_solve_options {
   double acceptable_tol;   /* 1e-6 */
   double mu_init;          /* 0.1 */
   double fd_step;          /* 1e-6 (CPL_HESSIAN_FD / Superquadric exact) */
+  double fallback_viol_tol; /* 1e-9; <= 0 off.  Not IPOPT (which returns its last iterate): a solve that
+                              ends without convergence (max_iter, local infeasibility, restoration
+                              failure) at an iterate whose original constraints are violated by more
+                              than this returns the lowest-objective iterate it met that satisfied
+                              them to this tolerance, when there was one (status unchanged;
+                              cpl_solver_fallbacks says which instances) */
 } cpl_solve_options;
 
 typedef struct cpl_solver cpl_solver;
@@ -520,6 +535,9 @@ int32_t cpl_solver_solve(cpl_solver* s, const double* d_x0, const double* d_mass
 int32_t cpl_solver_dims(const cpl_solver* s, int32_t* nf, int32_t* n_ineq, int32_t* graph_captured);
 /* the last solve's active-set compactions and its final lock-step batch size */
 int32_t cpl_solver_stats(const cpl_solver* s, int32_t* compactions, int64_t* final_rows);
+/* the last solve's fallback flags per instance into d_out [batch] (device uint8): 1 = the returned x is
+ * the best feasible iterate, not the last one (cpl_solve_options.fallback_viol_tol) */
+int32_t cpl_solver_fallbacks(const cpl_solver* s, uint8_t* d_out, void* stream);
 /* the last solve's restoration-phase entries per instance into d_out [batch] (device int64) */
 int32_t cpl_solver_restorations(const cpl_solver* s, int64_t* d_out, void* stream);
 

@@ -289,17 +289,11 @@ static void test_solve_plumbing() {
   CHECK(sol.com_sol[2] == 1.0 && sol.contact_values_map.size() == 4);
 }
 
-// ---- TestBasic (tests/TestBasic.cpp) through the C++ facade with its default solver: the native
-// engine (IPOPT's method, IFOPT's defaults), TestBasic's own assertions and tolerances.
-struct StartFrom : solver::NlpSolver {  // sets the problem's variables, then the default solver
-  std::vector<double> x0;
-  solver::NativeSolver inner;
-  bool Solve(solver::CplTNLP& nlp) override {
-    nlp.problem()->SetVariables(x0);
-    return inner.Solve(nlp);
-  }
-};
-
+// ---- TestBasic (tests/TestBasic.cpp) through the C++ facade with its default solver — the native
+// engine (IPOPT's method, IFOPT's defaults: limited-memory Hessian, max_iter 3000), from the
+// reference's own start point x = 0 (Variable3D's initial value, src/Variable3D.cpp:8-10; no warm
+// start) — with TestBasic's own assertions and tolerances.  The solver object is the default one
+// (NativeSolver with default SolveOptions), held here only to read its status and derivative report.
 static Vector3d cross3(const Vector3d& a, const Vector3d& b) {
   return {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
 }
@@ -347,7 +341,8 @@ static void test_testbasic_native() {
     NEAR(Fz, -mass * g, 1e-6);
   }
   const std::vector<double> wrench = {100, 0, 0, 0, 0, 100};
-  {  // testGroundEnv (TestBasic.cpp:64-135)
+  {  // testGroundEnv (TestBasic.cpp:64-135): ends at the iteration limit (the unloaded contacts' cone
+     // apex); the returned point is checked, as TestBasic does
     auto ground = std::make_shared<env::Ground>();
     ground->SetGroundZ(0.1);
     ground->SetMu(0.5);
@@ -356,23 +351,15 @@ static void test_testbasic_native() {
     cpl.SetForceWeight(0.0);
     for (const auto& c : NAMES) cpl.SetPosBounds(c, {-0.3, -0.3, 0.0}, {0.3, 0.3, 1.0});
     cpl.SetManipulationWrench(wrench);
-    auto st = std::make_shared<StartFrom>();
-    st->x0.assign(39, 0.0);
-    st->x0[2] = 1.0;
-    for (int i = 0; i < 4; ++i) {
-      const double ang = 2.0 * M_PI * (i + 0.125) / 4;
-      double* q = &st->x0[3 + 9 * i];
-      q[0] = 1.0; q[1] = 1.0; q[2] = mass * 9.81 / 4;
-      q[3] = 0.2 * std::cos(ang); q[4] = 0.2 * std::sin(ang); q[5] = 0.05;
-      q[6] = 0.0; q[7] = 0.0; q[8] = 1.0;
-    }
-    cpl.SetSolver(st);
+    auto ns = std::make_shared<solver::NativeSolver>();
+    cpl.SetSolver(ns);
     solver::Solution sol = cpl.Solve();
     {  // derivative_test = first-order ran at the start point (src/CentroidalPlanner.cpp:26)
-      const cpl_derivative_report& dr = st->inner.derivative_report();
+      const cpl_derivative_report& dr = ns->derivative_report();
       CHECK(dr.n_checked == 39 * (30 + 1));
-      CHECK(dr.max_rel_error == dr.max_rel_error && dr.worst_row >= -1 && dr.worst_col >= 0);
+      CHECK(dr.worst_row >= -1 && dr.worst_col >= 0);
     }
+    std::printf("testGroundEnv: status %d after %d iterations\n", ns->status(), ns->iterations());
     for (const auto& e : sol.contact_values_map) {
       NEAR(e.second.position_value[2], 0.1, 1e-6);
       NEAR(norm3(e.second.normal_value), 1.0, 1e-6);
@@ -388,19 +375,11 @@ static void test_testbasic_native() {
     cpl.SetForceWeight(0.0);
     for (const auto& c : NAMES) cpl.SetPosBounds(c, {-0.5, -0.5, 0.5}, {0.5, 0.5, 1.5});
     cpl.SetManipulationWrench(wrench);
-    auto st = std::make_shared<StartFrom>();
-    st->x0.assign(39, 0.0);
-    st->x0[2] = 1.0;
-    const double sides[4][2] = {{0.3, 0.0}, {0.0, 0.3}, {-0.3, 0.0}, {0.0, -0.3}};
-    for (int i = 0; i < 4; ++i) {
-      const Vector3d nr{-sides[i][0] / 0.3, -sides[i][1] / 0.3, 0.0};
-      double* q = &st->x0[3 + 9 * i];
-      q[0] = nr[0] * 300.0; q[1] = nr[1] * 300.0; q[2] = 250.0;
-      q[3] = sides[i][0]; q[4] = sides[i][1]; q[5] = 1.0 + 0.01 * (i - 1.5);
-      q[6] = nr[0]; q[7] = nr[1]; q[8] = nr[2];
-    }
-    cpl.SetSolver(st);
+    auto ns = std::make_shared<solver::NativeSolver>();
+    cpl.SetSolver(ns);
     solver::Solution sol = cpl.Solve();
+    std::printf("testSuperquadricEnv: status %d after %d iterations\n", ns->status(), ns->iterations());
+    CHECK(cpl.LastSolveSucceeded());
     for (const auto& e : sol.contact_values_map) {
       const Vector3d& p = e.second.position_value;
       const double C[3] = {0, 0, 1}, R[3] = {0.3, 0.3, 10};
@@ -421,19 +400,11 @@ static void test_testbasic_native() {
     cpl.SetContactPosition("contact4", {1.0, -1.0, 0.0});
     cpl.SetLiftingContact("contact4");
     for (const auto& c : NAMES) cpl.SetForceThreshold(c, 20.0);
-    auto st = std::make_shared<StartFrom>();
-    st->x0.assign(39, 0.0);
-    st->x0[2] = 1.0;
-    const double pos[4][2] = {{1, 1}, {-1, 1}, {-1, -1}, {1, -1}};
-    for (int i = 0; i < 4; ++i) {
-      double* q = &st->x0[3 + 9 * i];
-      q[0] = 1.0; q[1] = 1.0; q[2] = 330.0;
-      q[3] = pos[i][0]; q[4] = pos[i][1]; q[5] = 0.0;  // the fixed positions / normals
-      q[6] = 0.0; q[7] = 0.0; q[8] = 1.0;
-    }
-    st->x0[3 + 27] = st->x0[4 + 27] = st->x0[5 + 27] = 0.0;  // the lifting contact's force bounds are 0
-    cpl.SetSolver(st);
+    auto ns = std::make_shared<solver::NativeSolver>();
+    cpl.SetSolver(ns);
     solver::Solution sol = cpl.Solve();
+    std::printf("testCoMPlanner: status %d after %d iterations\n", ns->status(), ns->iterations());
+    CHECK(cpl.LastSolveSucceeded());
     check_balance(sol, mass, std::vector<double>(6, 0.0), 0.5, 1e-4);
   }
 }

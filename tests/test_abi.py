@@ -133,3 +133,18 @@ def test_bounds_cone_rows_one_sided():
         base = 6 + 6 * k
         assert list(gl[base: base + 4]) == [0.0] * 4 and list(gu[base: base + 4]) == [0.0] * 4
         assert list(gl[base + 4: base + 6]) == [-_abi.INF] * 2 and list(gu[base + 4: base + 6]) == [0.0] * 2
+
+
+@pytest.mark.parametrize("nw,m,ok", [(128, 30, True), (128, 31, False), (47, 47, True), (10, 11, False)])
+def test_kkt_qd_solve_rejects_what_does_not_fit_before_launch(nw, m, ok):
+    """cpl_kkt_qd_solve checks its LDS image (nw^2 + nw + 2m + m nw doubles <= 160 KiB) and m <= nw up
+    front: an oversized system is CPL_ERR_UNSUPPORTED (m > nw: invalid), never a failed launch.  With
+    batch 0 a fitting system returns before touching the GPU."""
+    fn = _abi.lib.cpl_kkt_qd_solve
+    rc = fn(0, nw, m, *([None] * 12))
+    if ok:
+        assert rc == 0
+    else:
+        assert rc in (_abi.ERR_UNSUPPORTED, _abi.ERR_INVALID_ARGUMENT)
+        if m <= nw:
+            assert rc == _abi.ERR_UNSUPPORTED and "LDS" in _abi.lib.cpl_last_error().decode()

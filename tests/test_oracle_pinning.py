@@ -17,9 +17,9 @@ IFOPT's defaults — the limited-memory Hessian, max_iter 3000).
 
 TestBasic's ground scenario (force weight 0) is degenerate: its optimum unloads two contacts, whose
 forces then sit at the apex of the cone |F_t| - mu F.n <= 0, where the constraint is not
-differentiable; neither Hessian mode converges to tol there ("Why TestBasic's ground
-scenario does not converge").  That test pins the
-documented outcome instead of success.
+differentiable; the solve does not converge to tol there ("Why TestBasic's ground
+scenario does not converge") and ends at the iteration limit — TestBasic checks the returned point,
+not the status, and so does that test.
 """
 import numpy as np
 import pytest
@@ -94,16 +94,42 @@ def test_simple_problem(backend):
     assert (gv[~eq] <= 1e-9).all()
 
 
+def _assert_testbasic_point(sol, wrench, robot_mass, g, mu, torque_tol, surface=None):
+    """TestBasic's checks of a returned point (tests/TestBasic.cpp:105-132, 181-220, 267-290): force
+    balance 1e-6, torque balance `torque_tol`, and both friction-cone signs <= 0 (allowing 1e-9 of
+    round-off: IPOPT's bound_relax_factor relaxes the cone rows' bound by 1e-8)."""
+    F_sum, T_sum = np.zeros(3), np.zeros(3)
+    for name, v in sol.contact_values_map.items():
+        F_sum += v.force_value
+        T_sum += np.cross(v.position_value - sol.com_sol, v.force_value)
+        if surface is not None:
+            surface(v)
+        F, n = v.force_value, v.normal_value
+        assert -F.dot(n) <= 1e-9, (name, -F.dot(n))
+        assert np.linalg.norm(F - n.dot(F) * n) - mu * F.dot(n) <= 1e-9, (name, np.linalg.norm(F - n.dot(F) * n) - mu * F.dot(n))
+    assert F_sum[0] == pytest.approx(wrench[0], abs=1e-6)
+    assert F_sum[1] == pytest.approx(wrench[1], abs=1e-6)
+    assert F_sum[2] == pytest.approx(-robot_mass * g + wrench[2], abs=1e-6)
+    assert T_sum[0] == pytest.approx(wrench[3], abs=torque_tol)
+    assert T_sum[1] == pytest.approx(wrench[4], abs=torque_tol)
+    assert T_sum[2] == pytest.approx(wrench[5], abs=torque_tol)
+
+
 @pytest.mark.parametrize("backend", BACKENDS)
 def test_ground_env(backend):
-    """TestBasic.cpp:64-135, from x = 0.  With force weight 0 only the CoM and contact positions are
-    priced: the optimum (objective 0.0665, SLSQP on the oracle) carries the wrench on two contacts and
-    unloads the other two to F = 0, the apex of their friction cones, where |F_t| is not
-    differentiable.  The barrier iterates approach the apex along F_t / F_n -> 0 and the method
-    crawls (IPOPT's theory needs C2 functions at the solution), so the solve ends at the iteration
-    limit.  Pinned: that status; the bounds; the linear constraints (surface height, normals), which
-    every Newton step keeps satisfied once met; the objective an order of magnitude below the start's;
-    a contact unloading towards the optimum's structure."""
+    """TestBasic.cpp:64-135, from x = 0 under IFOPT's defaults (limited-memory Hessian, max_iter 3000),
+    with TestBasic's own assertions and tolerances.
+
+    With force weight 0 only the CoM and contact positions are priced: the optimum (objective 0.0665,
+    SLSQP on the oracle) carries the wrench on two contacts and unloads the other two to F = 0, the
+    apex of their friction cones, where |F_t| is not differentiable.  The interior-point iterates
+    approach the apex along F_t / F_n -> 0 and the method crawls at a fixed barrier parameter (IPOPT's
+    theory needs C2 functions at the solution; the limited-memory model cannot represent the 1/|F_t|
+    curvature): the solve ends at the iteration limit.  Where the crawl stands at iteration 3000
+    depends on the rounding of every step — an accepted filter step may have raised the constraint
+    violation to ~1e-2 there — so the engine returns the best iterate that satisfied the constraints
+    (to 1e-9) when the last one does not (`fallback`; IPOPT returns its last iterate: parity unpinned
+    for this outcome, IPOPT is not in the image).  TestBasic checks no solver status, only the point."""
     robot_mass, g = 100.0, -9.81
     names = ["contact1", "contact2", "contact3", "contact4"]
     ground_z, mu = 0.1, 0.5
@@ -123,22 +149,21 @@ def test_ground_env(backend):
     _use(cpl, backend)
     prob = cpl.GetCplProblem()
     assert not prob.get_starting_point().any()
+    assert cpl.solver_hessian == "limited-memory" and cpl.solver_max_iter == 3000  # IFOPT's IpoptSolver
     sol = cpl.Solve()
-    assert not sol.success and sol.message == "max_iter" and sol.iterations == 3000
+    assert sol.message in ("optimal", "acceptable", "max_iter"), sol.message
+
+    def surface(v):  # TestBasic.cpp:114-116
+        assert v.position_value[2] == pytest.approx(ground_z, abs=1e-6)
+        assert np.linalg.norm(v.normal_value) == pytest.approx(1.0, abs=1e-6)
+        assert v.normal_value[2] == pytest.approx(1.0, abs=1e-6)
+
+    _assert_testbasic_point(sol, wrench, robot_mass, g, mu, 1e-5, surface)
     x = prob.get_starting_point()
     xl, xu, _, _ = prob.get_bounds_info()
     assert (x >= xl).all() and (x <= xu).all()
     f = OracleEvaluator(prob).eval_batch(x[None])["f"][0]
-    # start 1.0002, best known 0.0665; where the crawl stands after 3000 iterations depends on the
-    # rounding of every step (host 0.0678, device 0.078 at the time of writing)
-    assert f <= 0.1
-    Fn = []
-    for name, v in sol.contact_values_map.items():
-        assert v.position_value[2] == pytest.approx(ground_z, abs=1e-6)
-        assert v.normal_value == pytest.approx([0.0, 0.0, 1.0], abs=1e-6)
-        Fn.append(v.force_value[2])
-    # heading for the optimum's structure: the weakest contact carries a small share of the load
-    assert min(Fn) <= 0.05 * max(Fn), Fn
+    assert f <= 0.1  # start 1.0002, best known 0.0665
 
 
 @pytest.mark.parametrize("backend", BACKENDS)
@@ -161,31 +186,21 @@ def test_superquadric_env(backend):
     wrench[5] = 100.0
     cpl.SetManipulationWrench(wrench)
     _use(cpl, backend)
-    # IPOPT's own default Hessian (hessian_approximation = exact; the reference's IpoptSolver can set
-    # it through SetOption): from x = 0 the limited-memory model needs ~2000 iterations on the
-    # exponent-10 surface, the exact Hessian ~300
-    cpl.solver_hessian = "exact"
+    # IFOPT's IpoptSolver default (the reference's configuration): the limited-memory Hessian — from
+    # x = 0 it takes ~2000 iterations on the exponent-10 surface (the exact Hessian ~300)
+    assert cpl.solver_hessian == "limited-memory"
     assert not cpl.GetCplProblem().get_starting_point().any()
     sol = cpl.Solve()
-    assert sol.success and sol.iterations < 1000, (sol.message, sol.iterations)
-    F_sum, T_sum = np.zeros(3), np.zeros(3)
-    for name, v in sol.contact_values_map.items():
-        F_sum += v.force_value
-        T_sum += np.cross(v.position_value - sol.com_sol, v.force_value)
+    assert sol.success and sol.iterations < 3000, (sol.message, sol.iterations)
+
+    def surface(v):  # TestBasic.cpp:192-197, 206-211
         p = v.position_value
         sq = sum(((p[k] - C[k]) / R[k]) ** P[k] for k in range(3))
         assert sq == pytest.approx(1.0, abs=1e-4)
         assert np.linalg.norm(v.normal_value) == pytest.approx(1.0, abs=1e-6)
-        F, n = v.force_value, v.normal_value
-        assert -F.dot(n) <= 1e-9
-        assert np.linalg.norm(F - n.dot(F) * n) - mu * F.dot(n) <= 1e-9
         assert (p - p_lb >= 0.0).all() and (p - p_ub <= 0.0).all()
-    assert F_sum[0] == pytest.approx(wrench[0], abs=1e-6)
-    assert F_sum[1] == pytest.approx(wrench[1], abs=1e-6)
-    assert F_sum[2] == pytest.approx(-robot_mass * g + wrench[2], abs=1e-6)
-    assert T_sum[0] == pytest.approx(wrench[3], abs=1e-4)
-    assert T_sum[1] == pytest.approx(wrench[4], abs=1e-4)
-    assert T_sum[2] == pytest.approx(wrench[5], abs=1e-4)
+
+    _assert_testbasic_point(sol, wrench, robot_mass, g, mu, 1e-4, surface)
 
 
 @pytest.mark.parametrize("backend", BACKENDS)
@@ -212,16 +227,4 @@ def test_com_planner(backend):
     assert not prob.get_starting_point()[:3].any()  # x = 0 (the fixed positions / normals: their bounds)
     sol = cpl.Solve()
     assert sol.success and sol.iterations < 500, (sol.message, sol.iterations)
-    F_sum, T_sum = np.zeros(3), np.zeros(3)
-    for name, v in sol.contact_values_map.items():
-        F_sum += v.force_value
-        T_sum += np.cross(v.position_value - sol.com_sol, v.force_value)
-        F, n = v.force_value, v.normal_value
-        assert -F.dot(n) <= 1e-9
-        assert np.linalg.norm(F - n.dot(F) * n) - mu * F.dot(n) <= 1e-9
-    assert F_sum[0] == pytest.approx(0.0, abs=1e-6)
-    assert F_sum[1] == pytest.approx(0.0, abs=1e-6)
-    assert F_sum[2] == pytest.approx(-robot_mass * g, abs=1e-6)
-    assert T_sum[0] == pytest.approx(0.0, abs=1e-4)
-    assert T_sum[1] == pytest.approx(0.0, abs=1e-4)
-    assert T_sum[2] == pytest.approx(0.0, abs=1e-4)
+    _assert_testbasic_point(sol, np.zeros(6), robot_mass, g, mu, 1e-4)

@@ -47,6 +47,8 @@ def test_module_surface():
     for meth in base + ("SetLiftingContact", "ResetLiftingContact", "SetContactPosition", "GetContactPosition",
                         "SetContactNormal", "SetMu"):
         assert callable(getattr(com, meth)), meth
+    assert isinstance(com, cpl.CentroidalPlanner)  # pyCpl.cpp:61: CentroidalPlanner is CoMPlanner's base
+    assert not isinstance(pl, cpl.CoMPlanner)
 
 
 def test_solution_repr_is_operator_shift():
