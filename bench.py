@@ -30,9 +30,10 @@ Rank 0 prints one JSON line.  Fields beyond the driver contract:
   configs3_mixed16  BASELINE.json configs[3]'s 1,048,576 x 16 mixed batch on one GPU: kernel time, HBM
                 fraction, per-kind checker sample
   configs4_solve5_lbfgs  BASELINE.json configs[4] (8,192 concurrent solves) in the reference's Hessian
-                mode (IPOPT's L-BFGS): solves/s, iterations, a small CPU sample of the same solver;
+                mode (IPOPT's L-BFGS): solves/s, iterations, and the compiled restatement of the same
+                iteration (oracle/cpl_solve_host.c) on one core over a 512-instance sample;
                 .single_solve: one instance solved alone (CentroidalPlanner::Solve()'s batch of one):
-                GPU ms per solve beside the host restatement on one core
+                GPU ms per solve beside that compiled restatement on one core
 """
 from __future__ import annotations
 
@@ -683,24 +684,20 @@ def run_solve5(dev, batch, hessian, steps, warm, max_ls, max_soc, cpu_sample, ra
     if rank == 0 and world == 1 and cpu_sample > 0:
         try:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
-            sys.path.insert(0, os.path.join(ROOT, "tests"))
-            from test_batch_solve import OracleBatchEvaluator
+            import pyoracle
 
             info = host_cpu_info()
-            threads = info["threads"]
-            torch.set_num_threads(threads)
             Bc = min(cpu_sample, batch)
-            tc = time.perf_counter()
-            rc = batch_ipm_solve(prob, torch.tensor(X0[:Bc]), torch.tensor(mass[:Bc]),
-                                 evaluator=OracleBatchEvaluator(prob, nthreads=threads), **opts)
-            tc = time.perf_counter() - tc
-            okc = int((rc.status <= 1).sum().item())
-            cpu = {"value": Bc / tc, "unit": "solves/s", "cores": threads, "kind": "port",
-                   "sample": f"the first {Bc} of the {batch} instances: the same batched solver (hessian={hessian}; "
-                             f"exact = the oracle's restatement of the analytic Hessian kernel) over the oracle's "
-                             f"callbacks on CPU torch, {threads} threads ({rc.iterations_run} iterations, {okc}/{Bc} "
-                             f"solved, {tc:.1f} s)",
-                   **{k: info[k] for k in ("cpu_model", "affinity", "omp_num_threads")}}
+            tc, stc, itc = pyoracle.time_solve(prob.desc(), X0[:Bc], mass[:Bc], max_iter=opts["max_iter"],
+                                               hessian=hessian)
+            okc = int((stc <= 1).sum())
+            cpu = {"value": Bc / tc, "unit": "solves/s", "cores": 1, "kind": "port",
+                   "sample": f"the first {Bc} of the {batch} instances solved one after another on one core by the "
+                             f"compiled restatement of the same iteration (oracle/cpl_solve_host.c, gcc -O2: IPOPT's "
+                             f"method with dense QR / Cholesky KKT solves, hessian={hessian}; IPOPT itself is not in "
+                             f"the image) over the oracle's callbacks ({okc}/{Bc} solved, iterations mean "
+                             f"{float(itc.mean()):.1f}, {tc:.2f} s)",
+                   **{k: info[k] for k in ("cpu_model", "affinity")}}
         except Exception as e:  # noqa: BLE001
             cpu = {"error": str(e)}
     return dt, r, cpu
@@ -725,7 +722,8 @@ def side_single_solve(dev, reps=7):
     """The facade's primary call, CentroidalPlanner::Solve() (src/CentroidalPlanner.cpp:22-34): ONE
     instance of the solve workload solved in IFOPT's limited-memory mode by the native engine (B = 1:
     every kernel of an iteration is launch latency), median of `reps` solves after a warm-up, beside the
-    same solver over the oracle's callbacks on one CPU core (the host restatement, batch_ipm.py)."""
+    compiled restatement of the same iteration over the oracle's callbacks on one CPU core
+    (oracle/cpl_solve_host.c)."""
     import statistics
 
     import torch
@@ -751,22 +749,17 @@ def side_single_solve(dev, reps=7):
            "us_per_iteration": ms * 1e3 / max(1, int(r.iterations_run))}
     try:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        from test_batch_solve import OracleBatchEvaluator
+        import pyoracle
 
-        nt = torch.get_num_threads()
-        torch.set_num_threads(1)
-        try:
-            tc = time.perf_counter()
-            rc = batch_ipm_solve(prob, torch.tensor(X0), torch.tensor(mass), evaluator=OracleBatchEvaluator(prob, nthreads=1),
-                                 **opts)
-            tc = time.perf_counter() - tc
-        finally:
-            torch.set_num_threads(nt)
-        res["cpu_baseline"] = {"value": tc * 1e3, "unit": "ms per solve", "cores": 1, "kind": "port",
-                               "sample": f"the same instance: the host restatement of the solver (batch_ipm.py, CPU "
-                                         f"torch) over the oracle's callbacks, one thread ({int(rc.iterations[0])} "
-                                         f"iterations, status {int(rc.status[0])})"}
+        tcs = []
+        for _ in range(reps):
+            tc, stc, itc = pyoracle.time_solve(prob.desc(), X0, mass, max_iter=opts["max_iter"], hessian=opts["hessian"])
+            tcs.append(tc)
+        res["cpu_baseline"] = {"value": statistics.median(tcs) * 1e3, "unit": "ms per solve", "cores": 1, "kind": "port",
+                               "sample": f"the same instance, median of {reps}: the compiled restatement of the same "
+                                         f"iteration (oracle/cpl_solve_host.c, gcc -O2, dense QR / Cholesky KKT; "
+                                         f"IPOPT itself is not in the image) over the oracle's callbacks, one core "
+                                         f"({int(itc[0])} iterations, status {int(stc[0])})"}
     except Exception as e:  # noqa: BLE001
         res["cpu_baseline"] = {"error": str(e)}
     return res
@@ -777,8 +770,8 @@ def solve_bench(args):
     """BASELINE.json configs[4]: the full solve loop, 8,192 concurrent 4-contact Ground instances on
     one GPU (centroidalplanner_amd/batch_ipm.py).  One step = one complete batched solve from the
     starting points to termination of every instance; every callback of every iteration is one
-    cpl_eval_batch launch.  cpu_baseline = the same solver over the oracle's callbacks on the host
-    (CPU torch), a bounded sample of the instances."""
+    cpl_eval_batch launch.  cpu_baseline = the compiled restatement of the same iteration
+    (oracle/cpl_solve_host.c) over the oracle's callbacks on one core, a bounded sample of the instances."""
     import torch
 
     from centroidalplanner_amd.workload import SOLVE_CONFIG
@@ -1063,7 +1056,7 @@ def main():
         except Exception as e:  # noqa: BLE001
             mixed = {"error": str(e)}
         try:
-            solve5 = side_solve5(dev, 0 if args.no_cpu else 64)
+            solve5 = side_solve5(dev, 0 if args.no_cpu else 512)
         except Exception as e:  # noqa: BLE001
             solve5 = {"error": str(e)}
         try:

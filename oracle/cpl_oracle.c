@@ -706,6 +706,25 @@ int cplo_eval_batch(const cpl_problem_desc* d, int64_t B, const double* x, const
   return CPL_OK;
 }
 
+/* One-instance evaluation with a kept workspace (the solve restatement's callbacks,
+ * cpl_solve_host.c): the structure is built once per solve, not per call. */
+void* cplo_ws_new(const cpl_problem_desc* d) {
+  if (check_desc(d)) return NULL;
+  work_t* w = (work_t*)calloc(1, sizeof(work_t));
+  if (!w) return NULL;
+  if (build_structure(d, w)) { free_work(w); free(w); return NULL; }
+  return w;
+}
+void cplo_ws_eval(const cpl_problem_desc* d, void* ws, const double* x, double mass, double* g, double* jac,
+                  double* f, double* grad) {
+  eval_one(d, (work_t*)ws, x, mass, instance_kind(d, NULL, 0), g, jac, f, grad);
+}
+void cplo_ws_free(void* ws) {
+  if (!ws) return;
+  free_work((work_t*)ws);
+  free(ws);
+}
+
 /* Wall-clock timing of cplo_eval_batch for the bench's cpu_baseline leg. */
 double cplo_time_eval_batch(const cpl_problem_desc* d, int64_t B, const double* x, const double* mass,
                             const uint8_t* tags, double* g, double* jac, double* f, double* grad, int nthreads,

@@ -36,6 +36,11 @@ def _load():
     lib.cplo_time_eval_batch.restype = c_double
     lib.cplo_max_threads.argtypes = []
     lib.cplo_max_threads.restype = c_int
+    lib.cplo_solve.argtypes = [c_void_p, c_void_p, c_double, c_int, c_double, c_int, c_void_p, c_void_p, c_void_p,
+                               c_void_p, c_void_p, c_void_p]
+    lib.cplo_solve.restype = c_int
+    lib.cplo_time_solve.argtypes = [c_void_p, c_int64, c_void_p, c_void_p, c_int, c_double, c_int, c_void_p, c_void_p]
+    lib.cplo_time_solve.restype = c_double
     return lib
 
 
@@ -108,6 +113,44 @@ def time_eval_batch(desc, x, mass=None, env_tag=None, outputs=("g", "jac"), nthr
     if t < 0:
         raise ValueError("oracle timing failed")
     return t
+
+
+STATUS_NAMES = ("optimal", "acceptable", "max_iter", "infeasible", "resto_failed")
+
+
+def solve(desc, x0, mass=None, max_iter=3000, tol=1e-8, hessian="limited-memory"):
+    """One solve on this thread by the compiled restatement of the solve loop (cpl_solve_host.c:
+    IPOPT's iteration with IFOPT's limited-memory Hessian, or hessian="exact": the analytic one;
+    IPOPT itself absent).  Returns a dict:
+    x [n], status (0 optimal .. 4, STATUS_NAMES), iterations, objective, restorations, evaluations."""
+    n, _, _ = dims(desc)
+    x0 = np.ascontiguousarray(x0, dtype=np.float64).reshape(n)
+    x = np.zeros(n)
+    st, it, rs = c_int32(), c_int32(), c_int32()
+    obj, ev = c_double(), c_int64()
+    r = lib.cplo_solve(ctypes.byref(desc), _p(x0), float(desc.mass if mass is None else mass), int(max_iter),
+                       float(tol), int(hessian == "exact"), _p(x), ctypes.byref(st), ctypes.byref(it), ctypes.byref(obj), ctypes.byref(rs),
+                       ctypes.byref(ev))
+    if r:
+        raise ValueError(f"oracle solve failed: {r}")
+    return {"x": x, "status": st.value, "iterations": it.value, "objective": obj.value, "restorations": rs.value,
+            "evaluations": ev.value}
+
+
+def time_solve(desc, x0, mass=None, max_iter=3000, tol=1e-8, hessian="limited-memory"):
+    """Wall-clock seconds of sequential single-thread solves of x0 [count, n] (the CPU baseline of the
+    solve legs); returns (seconds, status [count], iterations [count])."""
+    n, _, _ = dims(desc)
+    x0 = np.ascontiguousarray(x0, dtype=np.float64).reshape(-1, n)
+    cnt = x0.shape[0]
+    mass = None if mass is None else np.ascontiguousarray(mass, dtype=np.float64)
+    st = np.zeros(cnt, dtype=np.int32)
+    it = np.zeros(cnt, dtype=np.int32)
+    t = lib.cplo_time_solve(ctypes.byref(desc), cnt, _p(x0), _p(mass), int(max_iter), float(tol), int(hessian == "exact"),
+                            _p(st), _p(it))
+    if t < 0:
+        raise ValueError("oracle solve timing failed")
+    return t, st, it
 
 
 def max_threads():
