@@ -90,6 +90,14 @@ bool NativeSolver::Solve(CplTNLP& nlp) {
     nlp.get_bounds_info(n, xl.data(), xu.data(), m, gl.data(), gu.data());
     for (int32_t j = 0; j < n; ++j) x0[j] = std::fmin(std::fmax(x0[j], xl[j]), xu[j]);
   }
+  {  // NaN Jacobian entries at the start point (the 0/0 of a cone at F_t = 0): counted and reported
+    int32_t nn = 0, mm = 0, nnz = 0, nh = 0;
+    nlp.get_nlp_info(nn, mm, nnz, nh);
+    std::vector<double> jv((size_t)nnz);
+    _nan_jac_start = 0;
+    if (nnz > 0 && nlp.eval_jac_g(n, x0.data(), true, m, nnz, nullptr, nullptr, jv.data()))
+      for (double v : jv) _nan_jac_start += std::isnan(v) ? 1 : 0;
+  }
   _dreport = cpl_derivative_report{};
   if (_opt.derivative_test) {  // IPOPT checks the first derivatives before it iterates
     double* dx = nullptr;

@@ -62,6 +62,7 @@ class Solution:
     message: str = ""
     iterations: int = 0  # the interior-point iterations the solve took (IPOPT's iteration count)
     fallback: bool = False  # not converged and the last iterate infeasible: the best feasible iterate instead
+    nan_jacobian_at_start: int = 0  # NaN Jacobian entries at the start point, taken as 0 (solver.py)
 
     @property
     def com(self) -> np.ndarray:
@@ -109,7 +110,7 @@ class CentroidalPlanner:
         self.last_derivative_report = res.derivative_report
         sol = self._cpl_problem.GetSolution()
         out = Solution(com_sol=sol["com"], success=res.success, message=res.status, iterations=res.iterations,
-                       fallback=res.fallback)
+                       fallback=res.fallback, nan_jacobian_at_start=res.nan_jacobian_at_start)
         for name, cv in sol["contact_values_map"].items():
             out.contact_values_map[name] = ContactValues(cv["force"], cv["position"], cv["normal"])
         return out

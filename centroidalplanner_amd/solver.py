@@ -10,10 +10,14 @@ oracle).  Like IFOPT's solver, a run that ends without convergence does not thro
 is kept (src/CentroidalPlanner.cpp:29-33), `success` says how it ended — except that when that last
 iterate violates the constraints (by more than 1e-9) and an earlier iterate satisfied them, the
 lowest-objective such iterate is returned instead (`fallback`; IPOPT itself returns the last one).
+Where the start point's constraint Jacobian has NaN entries (FrictionCone's 0/0 at a zero
+tangential force, e.g. x = 0) the loop takes them as 0; the count is returned
+(`nan_jacobian_at_start`) and a RuntimeWarning says so — IPOPT would receive the NaNs.
 Evaluators expose ``eval_batch(X[B, n]) -> {f, grad, g, jac}`` (host arrays).
 """
 from __future__ import annotations
 
+import warnings
 from dataclasses import dataclass
 from typing import Optional
 
@@ -29,6 +33,9 @@ class SolveResult:
     primal_inf: float
     derivative_report: Optional[dict] = None  # derivative_test = "first-order" (cpl_derivative_test)
     fallback: bool = False  # not converged, last iterate infeasible: x is the best feasible iterate instead
+    # Jacobian entries NaN at the start point (FrictionCone's 0/0 where F_t = 0,
+    # src/Constraints/FrictionCone.cpp:85-87, e.g. x = 0): IPOPT would receive NaN, the loop takes 0
+    nan_jacobian_at_start: int = 0
 
 
 class _HostBatchEvaluator:
@@ -67,6 +74,12 @@ def solve(problem, evaluator=None, x0: Optional[np.ndarray] = None, tol: float =
 
     xl, xu, _, _ = problem.get_bounds_info()
     x0 = np.clip(problem.get_starting_point() if x0 is None else np.asarray(x0, dtype=np.float64), xl, xu)
+    jac0 = problem.eval_jac_g(x0) if evaluator is None else np.asarray(evaluator.eval_batch(x0[None])["jac"])[0]
+    nan0 = int(np.isnan(jac0).sum())
+    if nan0:
+        warnings.warn(f"{nan0} constraint Jacobian entries are NaN at the start point (FrictionCone's 0/0 where "
+                      f"a contact's tangential force is 0, src/Constraints/FrictionCone.cpp:85-87); IPOPT would "
+                      f"receive them as NaN, this solve takes them as 0 (a subgradient)", RuntimeWarning, stacklevel=2)
     report = None
     if evaluator is None:
         X0 = torch.as_tensor(x0[None], device=torch.device("cuda", torch.cuda.current_device()))
@@ -80,4 +93,5 @@ def solve(problem, evaluator=None, x0: Optional[np.ndarray] = None, tol: float =
     st = int(r.status[0])
     problem.SetVariables(x)  # the next Solve warm-starts here, like the reference's persistent variables
     return SolveResult(x, st <= STATUS_ACCEPTABLE, STATUS_NAMES.get(st, f"status {st}"), int(r.iterations[0]),
-                       float(r.primal_inf[0]), report, bool(r.fallback[0]) if r.fallback is not None else False)
+                       float(r.primal_inf[0]), report, bool(r.fallback[0]) if r.fallback is not None else False,
+                       nan0)

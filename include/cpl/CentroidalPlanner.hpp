@@ -83,13 +83,17 @@ class NativeSolver : public NlpSolver {
   double primal_inf() const { return _primal_inf; }
   // the derivative checker's report of the last Solve (n_checked == 0 when it did not run)
   const cpl_derivative_report& derivative_report() const { return _dreport; }
+  // Jacobian entries that were NaN at the last Solve's start point (FrictionCone's 0/0 where the
+  // tangential force is 0, src/Constraints/FrictionCone.cpp:85-87 — e.g. at x = 0): IPOPT would
+  // receive them as NaN; the engine takes them as 0 (a subgradient).  0: no substitution happened.
+  int32_t nan_jacobian_at_start() const { return _nan_jac_start; }
 
  private:
   SolveOptions _opt;
   std::unique_ptr<BatchSolver> _bs;  // kept between solves of the same template (_bs_desc)
   const CplProblem* _bs_problem = nullptr;
   cpl_problem_desc _bs_desc{};
-  int32_t _status = -1, _iterations = 0;
+  int32_t _status = -1, _iterations = 0, _nan_jac_start = 0;
   double _primal_inf = 0.0;
   cpl_derivative_report _dreport{};
 };

@@ -7,6 +7,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <random>
 #include <vector>
 
@@ -88,6 +89,19 @@ int main(int argc, char** argv) {
       best = ms < best ? ms : best;
     }
     std::printf("mode %d: %.3f ms for %d systems (nw %d, m %d)\n", mode, best, B, nw, m);
+    {  // FNV-1a of the outputs' bit patterns: variants of the kernel compare bit for bit
+      std::vector<double> ow((size_t)B * nw), oy((size_t)B * m);
+      CK(hipMemcpy(ow.data(), ddw, ow.size() * 8, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(oy.data(), ddy, oy.size() * 8, hipMemcpyDeviceToHost));
+      unsigned long long h = 1469598103934665603ull;
+      for (const auto* v : {&ow, &oy})
+        for (double d : *v) {
+          unsigned long long bits;
+          std::memcpy(&bits, &d, 8);
+          h = (h ^ bits) * 1099511628211ull;
+        }
+      std::printf("  outputs hash %016llx\n", h);
+    }
     if (mode == 0) {
       std::vector<long long> prof((size_t)B * 8);
       CK(hipMemcpy(prof.data(), dprof, prof.size() * 8, hipMemcpyDeviceToHost));

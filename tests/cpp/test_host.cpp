@@ -359,7 +359,10 @@ static void test_testbasic_native() {
       CHECK(dr.n_checked == 39 * (30 + 1));
       CHECK(dr.worst_row >= -1 && dr.worst_col >= 0);
     }
-    std::printf("testGroundEnv: status %d after %d iterations\n", ns->status(), ns->iterations());
+    // x = 0: every cone's Jacobian row is 0/0 (FrictionCone.cpp:85-87), reported as substituted
+    CHECK(ns->nan_jacobian_at_start() > 0);
+    std::printf("testGroundEnv: status %d after %d iterations (%d NaN Jacobian entries at the start)\n", ns->status(),
+                ns->iterations(), ns->nan_jacobian_at_start());
     for (const auto& e : sol.contact_values_map) {
       NEAR(e.second.position_value[2], 0.1, 1e-6);
       NEAR(norm3(e.second.normal_value), 1.0, 1e-6);

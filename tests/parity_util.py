@@ -172,6 +172,61 @@ def plain_rel_off_diagonals(prob, env, x, got, ref, tag=None):
     return out
 
 
+NOISE_ULPS = 8.0  # |ref| at or below this many ulps of the un-cancelled terms' magnitude: rounding noise
+
+
+def plain_rel_diagonals(prob, env, x, got, ref, tag=None):
+    """The three normal-Jacobian diagonals of each Superquadric contact graded on the PLAIN relative
+    error |gpu - ref| / |ref| wherever |ref| is not itself rounding noise of its un-cancelled terms
+    (|ref| > NOISE_ULPS * eps * diag_scale: the expanded (C - p)^2 numerator cancels,
+    src/Superquadric.cpp:98-100, 152-154, 206-208).  Returns {"graded": count, "noise": count of the
+    entries at the noise floor (graded on the scale of check_outputs only), "max": max plain relative
+    error over the graded entries, "outside": graded entries above RTOL, "hist": decades, and
+    "outside_ref_over_scale": |ref| / scale of the entries above RTOL (at most 32)}."""
+    from centroidalplanner_amd import ENV_SUPERQUADRIC
+
+    N = len(prob.contact_names)
+    B = x.shape[0]
+    sq_inst = (np.ones(B, dtype=bool) if env == "superquadric" else
+               (tag == ENV_SUPERQUADRIC) if env == "mixed" else np.zeros(B, dtype=bool))
+    out = {"graded": 0, "noise": 0, "max": 0.0, "outside": 0, "outside_ref_over_scale": [],
+           "hist": {"bitwise": 0, "lt1e-15": 0, "lt1e-13": 0, "lt1e-12": 0, "lt1e-10": 0, "ge1e-10": 0}}
+    if not sq_inst.any():
+        return out
+    ds = diag_scale(x, N, prob.map_order, *sq_params(prob))
+    gv, rv = np.asarray(got["jac"]), np.asarray(ref["jac"])
+    eps = np.finfo(np.float64).eps
+    for kk, (jo, _, _) in enumerate(contact_offsets(N, True, prob.map_order)):
+        for a in range(3):
+            col = jo + 3 + 4 * a + a
+            g, r, s = gv[:, col], rv[:, col], ds[:, kk, a]
+            fin = sq_inst & ~(np.isnan(g) | np.isnan(r)) & np.isfinite(s)
+            with np.errstate(all="ignore"):
+                noise = fin & ~(np.abs(r) > NOISE_ULPS * eps * s)
+                sel = fin & ~noise
+                err = np.where(sel & (g != r), np.abs(g - r), 0.0)
+                rel = np.where(err > 0, err / np.where(np.abs(r) > 0, np.abs(r), 1.0), 0.0)
+            out["noise"] += int(noise.sum())
+            out["graded"] += int(sel.sum())
+            v = rel[sel]
+            if v.size:
+                out["max"] = max(out["max"], float(v.max()))
+            nz = v[v > 0]
+            h = out["hist"]
+            h["bitwise"] += int((v == 0).sum())
+            h["lt1e-15"] += int((nz < 1e-15).sum())
+            h["lt1e-13"] += int(((nz >= 1e-15) & (nz < 1e-13)).sum())
+            h["lt1e-12"] += int(((nz >= 1e-13) & (nz < 1e-12)).sum())
+            h["lt1e-10"] += int(((nz >= 1e-12) & (nz < 1e-10)).sum())
+            h["ge1e-10"] += int((nz >= 1e-10).sum())
+            bad = sel & (rel > RTOL)
+            out["outside"] += int(bad.sum())
+            with np.errstate(all="ignore"):
+                ros = np.abs(r[bad]) / s[bad]
+            out["outside_ref_over_scale"] += [float(t) for t in ros[: 32 - len(out["outside_ref_over_scale"])]]
+    return out
+
+
 def check_outputs(prob, env, x, got, ref, tag=None, raise_on_fail=True):
     """Apply the policy above to every output; returns {output: stats}; raises AssertionError
     (raise_on_fail=False: every output is checked and stats["ok"] says whether it passed)."""

@@ -75,7 +75,11 @@ def test_simple_problem(backend):
     assert not prob.get_starting_point().any()  # x = 0, Variable3D's initial value
     if backend == "oracle":
         cpl.evaluator = OracleEvaluator(prob)
-    sol = cpl.Solve()
+    # at x = 0 the cone's Jacobian row is 0/0 (src/Constraints/FrictionCone.cpp:85-87): the solve
+    # says it took those entries as 0 where IPOPT would receive NaN
+    with pytest.warns(RuntimeWarning, match="NaN at the start point"):
+        sol = cpl.Solve()
+    assert sol.nan_jacobian_at_start > 0
     assert sol.success and sol.iterations < 1000, (sol.message, sol.iterations)
     Fz_tot = 0.0
     for name, v in sol.contact_values_map.items():
