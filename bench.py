@@ -51,7 +51,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "NLP eval_g+eval_jac_g throughput (rows/sec) at batch*contacts; HBM GB/s vs peak"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
-KERNEL_NAME = "cpl_eval"  # matches cpl_eval_pipe_kernel (none/Ground), cpl_eval_tile_kernel, cpl_eval_kernel
+KERNEL_NAME = "cpl_eval"  # matches cpl_eval_pipe_kernel / _entry_kernel (none/Ground), cpl_eval_tile_kernel, cpl_eval_kernel
 
 
 def algorithmic_bytes(N, env, outputs=("g", "jac"), with_mass=True):
@@ -285,13 +285,18 @@ def pmc_child(args):
     xt, mt = torch.tensor(x, device=dev), torch.tensor(mass, device=dev)
     tt = None if tag is None else torch.tensor(tag, device=dev)
     out = prob.eval_batch(xt, mt, tt, outputs=("g", "jac"))
-    for _ in range(5):
+    for _ in range(PMC_LAUNCHES - 1):
         prob.eval_batch(xt, mt, tt, outputs=("g", "jac"), out=out)
     torch.cuda.synchronize()
 
 
+PMC_LAUNCHES = 6  # eval launches of the pmc child
+
+
 def _pmc_pass(args, counters, timeout=240):
-    """One rocprofv3 --pmc pass over the pmc child; returns {counter: mean per eval dispatch}."""
+    """One rocprofv3 --pmc pass over the pmc child; returns {counter: per eval LAUNCH} — the sum over
+    the eval kernels' dispatches / the child's launches (a mixed batch's default launch is two
+    kernels, the kind split's Ground and Superquadric halves)."""
     import csv
 
     rocprof = "/opt/rocm/bin/rocprofv3"
@@ -312,7 +317,7 @@ def _pmc_pass(args, counters, timeout=240):
                 per[row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
     if not per:
         raise RuntimeError(f"no {counters} rows for {KERNEL_NAME}")
-    return {k: sum(v.values()) / len(v) for k, v in per.items()}
+    return {k: sum(v.values()) / PMC_LAUNCHES for k, v in per.items()}
 
 
 def collect_pmc(args, timeout=240):
@@ -353,7 +358,7 @@ def valu_roofline(c, kernel_ms):
     issue_frac = the kernel's VALU issue cycles at full rate (4 cycles per wave64 FP64 instruction,
     2 otherwise, over 1024 SIMDs at 2.4 GHz) / its duration; fp64 TFLOP/s = 64 lanes x
     SQ_INSTS_VALU_FLOPS_FP64(+_TRANS) / duration against the 78.6 TFLOP/s FP64 vector peak.
-    c: counters per eval dispatch (collect_valu_counters, run before this process touches the GPU)."""
+    c: counters per eval launch (collect_valu_counters, run before this process touches the GPU)."""
     t = kernel_ms * 1e-3
     f64 = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
                                        "SQ_INSTS_VALU_TRANS_F64"))
@@ -364,7 +369,7 @@ def valu_roofline(c, kernel_ms):
         "frac": tflops / FP64_PEAK_TFLOPS, "issue_frac": issue_s / t, "issue_bound_ms": issue_s * 1e3,
         "wait_frac": c.get("SQ_WAIT_ANY", 0.0) / max(c.get("SQ_WAVE_CYCLES", 1.0), 1.0),
         "valu_active_frac": c.get("SQ_ACTIVE_INST_VALU", 0.0) / max(c.get("SQ_WAVE_CYCLES", 1.0), 1.0),
-        "counters_per_dispatch": c,
+        "counters_per_launch": c,
     }
 
 

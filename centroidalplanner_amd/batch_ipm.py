@@ -664,6 +664,9 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         # the best iterate feasible to fallback_viol_tol (lowest f): the fallback result of a solve that
         # stops without converging at an infeasible iterate (not IPOPT)
         "best_w": zBw(), "best_f": torch.full((B,), float("inf"), dtype=dt, device=dev),
+        # IPOPT's backup acceptable point (BacktrackingLineSearch::StoreAcceptablePoint): the last
+        # regular iterate at the acceptable level, restored when the restoration phase fails
+        "acc_w": zBw(), "acc_y": zBm(), "acc_zL": zBw(), "acc_zU": zBw(), "has_acc": bool_B(),
     }
 
     def orig_violation(g):
@@ -770,6 +773,12 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         w, y, zL, zU, mu = S["w"], S["y"], S["zL"], S["zU"], S["mu"].clone()
         cur = {"f": S["f"], "grad": S["grad"], "g": S["g"], "J": S["J"]}
         A, gradw, c = E["A"], E["gw"], E["c"]
+        # IPOPT stores the current iterate as the backup acceptable point when it is at the
+        # acceptable level (FindAcceptableTrialPoint: CurrentIsAcceptable -> StoreAcceptablePoint)
+        store = act & (E["err0"] <= acceptable_tol)
+        for k, v in (("acc_w", w), ("acc_y", y), ("acc_zL", zL), ("acc_zU", zU)):
+            S[k].copy_(torch.where(store[:, None], v, S[k]))
+        S["has_acc"].copy_(S["has_acc"] | store)
         # ---- monotone barrier update (IPOPT MonotoneMuUpdate with mu_allow_fast_monotone_decrease: as
         # long as the barrier problem is solved to kappa_eps mu, or once after two tiny steps), the
         # filter reset where mu changed
@@ -1019,8 +1028,13 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         conv = actR & (errR0 <= torch.where(tight, 1e-2 * tol, tol))
         feas = (c.abs().amax(1) if m else zeros_B) <= 1e2 * tol
         stop = conv & (~feas | tight)
-        S["status"].copy_(torch.where(stop & feas, STATUS_RESTO_FAILED,
-                                      torch.where(stop, STATUS_INFEASIBLE, S["status"])))
+        # a failed restoration phase with a backup acceptable point: IPOPT restores that point and stops
+        # there (BacktrackingLineSearch: RestoreAcceptablePoint, STOP_AT_ACCEPTABLE_POINT)
+        back_acc = stop & feas & S["has_acc"]
+        for k, kk in (("w", "acc_w"), ("y", "acc_y"), ("zL", "acc_zL"), ("zU", "acc_zU")):
+            S[k].copy_(torch.where(back_acc[:, None], S[kk], S[k]))
+        S["status"].copy_(torch.where(back_acc, STATUS_ACCEPTABLE, torch.where(stop & feas, STATUS_RESTO_FAILED,
+                                      torch.where(stop, STATUS_INFEASIBLE, S["status"]))))
         S["resto_tight"].copy_(tight | (conv & feas))
         S["active"].copy_(S["active"] & ~stop)
         actR = actR & ~stop

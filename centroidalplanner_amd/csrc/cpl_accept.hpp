@@ -234,6 +234,13 @@ struct IpmUnpack {
   double* X;
   double* tau;
   uint8_t* act;
+  // IPOPT's backup acceptable point (BacktrackingLineSearch::StoreAcceptablePoint): a regular
+  // iterate at the acceptable level is copied here (acc_w == NULL: not kept)
+  double* acc_w;
+  double* acc_y;
+  double* acc_zL;
+  double* acc_zU;
+  uint8_t* has_acc;
 };
 
 // one entry e of A = dc/dw = [J_free | -P] (batch-major [B][m][nw]) from the CSR Jacobian values:

@@ -188,6 +188,15 @@ __global__ __launch_bounds__(256) void cpl_ipm_optimality_kernel(
   const int64_t acc_new = (act && err0 <= acc_tol) ? acc[b] + 1 : 0;
   const bool acc_now = act && !done_now && acc_new >= acc_iter;
   act = act && !done_now && !acc_now;
+  if (up.acc_w && act && err0 <= acc_tol) {  // the backup acceptable point (CurrentIsAcceptable)
+    for (int k = lane; k < nw; k += 64) {
+      up.acc_w[b * nw + k] = w[b * nw + k];
+      up.acc_zL[b * nw + k] = zL[b * nw + k];
+      up.acc_zU[b * nw + k] = zU[b * nw + k];
+    }
+    for (int r = lane; r < m; r += 64) up.acc_y[b * m + r] = yb[r];
+    if (lane == 0) up.has_acc[b] = 1;
+  }
   // barrier update (IPOPT MonotoneMuUpdate, mu_allow_fast_monotone_decrease): while the barrier
   // problem is solved to kappa_eps mu (or once after two tiny steps), at most mu_rounds times
   double mu = mu_in[b];
@@ -272,7 +281,11 @@ __global__ __launch_bounds__(256) void cpl_ipm_max_step_kernel(int64_t batch, in
 // (per instance [sigma, nv, U (lm_pairs x nf), W (lm_pairs x nf)]): H = sigma I + sum_{i < nv}
 // (-u_i u_i' + w_i w_i'), each entry evaluated here in the order the dense build used, staged per wave
 // in dynamic LDS — the dense nf x nf model never goes through memory.
-template <bool LM>
+// WIDE (small batches): one instance per workgroup — wave 0 does the per-variable and per-row work
+// exactly as the one-wave form, the M entries are spread over the four waves (every entry the same
+// operations in the same order: bitwise the one-wave result); at B = 1 one wave filled 47 x 47
+// entries alone.
+template <bool LM, bool WIDE = false>
 __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
     int64_t batch, int nw, int m, int nf, const double* __restrict__ w, const double* __restrict__ zL,
     const double* __restrict__ zU, const double* __restrict__ gw, const double* __restrict__ A,
@@ -282,17 +295,19 @@ __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
     double* __restrict__ M, double* __restrict__ r1, double* __restrict__ r2, double* __restrict__ gphi,
     double* __restrict__ mr_diag, double* __restrict__ theta, double* __restrict__ phi,
     const uint8_t* __restrict__ active, const double* __restrict__ Hc, int lm_pairs) {
-  const int64_t b = (int64_t)blockIdx.x * IPM_WAVES + (threadIdx.x >> 6);
+  const int64_t b = WIDE ? (int64_t)blockIdx.x : (int64_t)blockIdx.x * IPM_WAVES + (threadIdx.x >> 6);
   if (b >= batch || (active && !active[b])) return;  // converged: its Newton system is never read
   const int lane = threadIdx.x & 63;
+  const bool w0 = !WIDE || threadIdx.x < 64;  // the wave doing the per-variable / per-row work
+  const int et = WIDE ? (int)threadIdx.x : lane, es = WIDE ? 256 : 64;  // the M entries' thread / stride
   const double mub = mu[b];
   const double* Ab = A + b * (int64_t)m * nw;
   const double* yb = y + b * m;
   double* Mb = M + b * (int64_t)nw * nw;
   __shared__ double sig_s[IPM_WAVES][128];
-  double* sg = sig_s[threadIdx.x >> 6];
+  double* sg = sig_s[WIDE ? 0 : threadIdx.x >> 6];
   double lg = 0.0;
-  for (int k = lane; k < nw; k += 64) {
+  for (int k = lane; w0 && k < nw; k += 64) {
     const double wk = w[b * nw + k];
     double sig = 0.0, gp = gw[b * nw + k];
     if (hasL[k]) {
@@ -319,31 +334,33 @@ __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
   // the wave's own LDS row of Sigma needs no workgroup barrier, only the wave's LDS ordering
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS stores have landed
   __builtin_amdgcn_wave_barrier();
+  if (WIDE) __syncthreads();  // Sigma from wave 0 to every wave
   if (LM) {
     extern __shared__ __align__(16) double lm_dyn[];
     const int per = 2 * lm_pairs * nf;
-    double* UW = lm_dyn + (threadIdx.x >> 6) * per;  // this wave's U | W
+    double* UW = lm_dyn + (WIDE ? 0 : (threadIdx.x >> 6) * per);  // this wave's (workgroup's) U | W
     const double* hc = Hc + b * (int64_t)(2 + per);
     const double sigma = hc[0];
     const int nv = (int)hc[1];
-    for (int e = lane; e < nv * nf; e += 64) {
+    for (int e = et; e < nv * nf; e += es) {
       UW[e] = hc[2 + e];
       UW[lm_pairs * nf + e] = hc[2 + lm_pairs * nf + e];
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
+    if (WIDE) __syncthreads();
     const double* U = UW;
     const double* W = UW + lm_pairs * nf;
     // four entries per lane at a time (independent chains: their LDS reads overlap), each entry's
     // operations in the order of the one-entry loop
     constexpr int EU = 4;
-    for (int e0 = lane; e0 < nw * nw; e0 += 64 * EU) {
+    for (int e0 = et; e0 < nw * nw; e0 += es * EU) {
       int kk[EU], jj[EU];
       bool in[EU];
       double h[EU];
 #pragma unroll
       for (int u = 0; u < EU; ++u) {
-        const int e = e0 + 64 * u;
+        const int e = e0 + es * u;
         kk[u] = e / nw;
         jj[u] = e - kk[u] * nw;
         in[u] = e < nw * nw && kk[u] < nf && jj[u] < nf;
@@ -357,7 +374,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
       }
 #pragma unroll
       for (int u = 0; u < EU; ++u) {
-        const int e = e0 + 64 * u;
+        const int e = e0 + es * u;
         if (e < nw * nw) {
           double v = (jj[u] == kk[u]) ? sg[kk[u]] : 0.0;
           if (in[u]) v += h[u];
@@ -370,13 +387,14 @@ __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
     // h_sym: H is the raw central-difference matrix (cpl_ipm_fd_hessian_raw), symmetrised here as
     // batch_ipm.py's fd_hessian does: 0.5 (H + H^T) (unrolled: four entries' loads in flight)
 #pragma unroll 4
-    for (int e = lane; e < nw * nw; e += 64) {
+    for (int e = et; e < nw * nw; e += es) {
       const int k = e / nw, j = e - k * nw;
       double v = (j == k) ? sg[k] : 0.0;
       if (Hb && k < nf && j < nf) v += h_sym ? 0.5 * (Hb[k * nf + j] + Hb[j * nf + k]) : Hb[k * nf + j];
       Mb[e] = v;
     }
   }
+  if (!w0) return;
   double th = 0.0;
   for (int r = lane; r < m; r += 64) {
     const double cr = c[b * m + r];
@@ -390,6 +408,9 @@ __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
     phi[b] = f[b] - mub * lg;
   }
 }
+
+// batches up to this size run the Newton setup one instance per workgroup (WIDE)
+constexpr int64_t NEWTON_WIDE_MAX = 1024;
 
 // After the Newton step (batch_ipm.py step): bound-multiplier steps dzL = mu/dl - zL - zL/dl dw,
 // dzU = mu/du - zU + zU/du dw, their fraction-to-the-boundary step a_z, the primal one a_max,
@@ -736,6 +757,15 @@ int32_t cpl_ipm_newton_setup(int64_t batch, int32_t nw, int32_t m, int32_t nf, c
   if (!d_w || !d_zL || !d_zU || !d_gw || (m > 0 && (!d_A || !d_y || !d_c || !d_r2)) || !d_f || !d_mu || !d_hasL ||
       !d_hasU || !d_wl0 || !d_wu0 || !d_M || !d_r1 || !d_gphi || !d_mr_diag || !d_theta || !d_phi)
     return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_newton_setup: missing buffer");
+  if (batch <= NEWTON_WIDE_MAX) {  // one instance per workgroup
+    hipLaunchKernelGGL((cpl_ipm_newton_setup_kernel<false, true>), dim3((unsigned)batch), dim3(64 * IPM_WAVES), 0,
+                       (hipStream_t)stream, batch, (int)nw, (int)m, (int)nf, d_w, d_zL,
+             d_zU, d_gw, d_A, d_y, d_c, d_f, d_mu, d_hasL, d_hasU, d_wl0, d_wu0, d_H, (int)h_sym, d_M, d_r1, d_r2,
+             d_gphi, d_mr_diag, d_theta, d_phi, d_active, nullptr, 0);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_ipm_newton_setup launch: ") + hipGetErrorString(e));
+    return CPL_OK;
+  }
   IPM_LAUNCH(cpl_ipm_newton_setup_kernel<false>, "cpl_ipm_newton_setup", batch, (int)nw, (int)m, (int)nf, d_w, d_zL,
              d_zU, d_gw, d_A, d_y, d_c, d_f, d_mu, d_hasL, d_hasU, d_wl0, d_wu0, d_H, (int)h_sym, d_M, d_r1, d_r2,
              d_gphi, d_mr_diag, d_theta, d_phi, d_active, nullptr, 0);
@@ -859,9 +889,10 @@ int32_t ipm_newton_setup_lm(int64_t batch, int32_t nw, int32_t m, int32_t nf, co
   if (batch == 0) return CPL_OK;
   const int64_t blocks = (batch + IPM_WAVES - 1) / IPM_WAVES;
   if (blocks > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "ipm_newton_setup_lm: batch too large");
-  const size_t lds = sizeof(double) * IPM_WAVES * 2 * (size_t)lm_pairs * nf;
-  hipLaunchKernelGGL(cpl_ipm_newton_setup_kernel<true>, dim3((unsigned)blocks), dim3(64 * IPM_WAVES), lds,
-                     (hipStream_t)stream, batch, (int)nw, (int)m, (int)nf, d_w, d_zL, d_zU, d_gw, d_A, d_y, d_c, d_f,
+  const bool wide = batch <= NEWTON_WIDE_MAX;  // one instance per workgroup
+  const size_t lds = sizeof(double) * (wide ? 1 : IPM_WAVES) * 2 * (size_t)lm_pairs * nf;
+  hipLaunchKernelGGL((wide ? cpl_ipm_newton_setup_kernel<true, true> : cpl_ipm_newton_setup_kernel<true, false>),
+                     dim3((unsigned)(wide ? batch : blocks)), dim3(64 * IPM_WAVES), lds, (hipStream_t)stream, batch, (int)nw, (int)m, (int)nf, d_w, d_zL, d_zU, d_gw, d_A, d_y, d_c, d_f,
                      d_mu, d_hasL, d_hasU, d_wl0, d_wu0, nullptr, 0, d_M, d_r1, d_r2, d_gphi, d_mr_diag, d_theta, d_phi,
                      d_active, d_Hc, (int)lm_pairs);
   hipError_t e = hipGetLastError();

@@ -1201,7 +1201,8 @@ __device__ __forceinline__ void cone_rows(const KParams& K, int i, const double*
   }
 }
 
-template <bool AXL>
+// CONE = false: the row-1 item leaves the contact's friction cone to a separate item (sq_cone_item)
+template <bool AXL, bool CONE = true>
 __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __restrict__ xr, int k, int a,
                                             const double* __restrict__ Lc, double* __restrict__ Gr,
                                             double* __restrict__ Jr) {
@@ -1231,7 +1232,7 @@ __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __re
       gk[3] = q[8] - -ej2 / nrm;
     }
     if (K.want_j) { jk[0] = ej0; jk[1] = ej1; jk[2] = ej2; }
-  } else if (a == 1) {
+  } else if (CONE && a == 1) {
     cone_rows(K, i, q, gk + 4, jk + (fold ? 12 : 15));
   }
   if (!K.want_j) return;
@@ -1293,6 +1294,14 @@ __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __re
   if (!fold) row[3] = 1.0;
 }
 
+// the friction cone rows of contact block k (map order) of a Superquadric record, as sq_row_item's
+// row-1 item computes them
+__device__ __forceinline__ void sq_cone_item(const KParams& K, const double* __restrict__ xr, int k,
+                                             double* __restrict__ Gr, double* __restrict__ Jr) {
+  const int i = s_ct.map_order[k];
+  cone_rows(K, i, xr + 3 + 9 * i, Gr + 6 + 6 * k + 4, Jr + K.jbase + K.cstride * k + (K.fold != FOLD_NONE ? 12 : 15));
+}
+
 // JD: the Jacobian items write their entries straight to the output records (K.jdirect); a
 // compile-time choice, so that every Jacobian store is a plain LDS or a plain global store: through a
 // generic pointer they were FLAT stores, which count on lgkmcnt too — every later LDS wait of the
@@ -1300,7 +1309,13 @@ __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __re
 // idx (optional, with d_count on the device): an instance list — tile position j evaluates instance
 // idx[j] and its records are written in place (the Superquadric half of a mixed batch, launched for
 // `batch` list entries at most; tiles past *d_count only write zero norm partials).  Not with JD / SoA.
-template <int ENVK, int WG, bool NT, bool JD>
+// LIST (compile time): the tile rows are the instances idx[b0 ..] of a device-side instance list of
+// *d_count entries (the kind split's Superquadric half), records written in place; the grid covers the
+// largest possible list (batch / T tiles) and the workgroups past the list's tiles only write zero
+// residual partials.  Without LIST the kernel is the contiguous one-tile-per-workgroup form (111
+// VGPRs for Superquadric; a runtime list pointer and a tile loop in the same body had cost 162 VGPRs
+// and a 36-byte spill, three waves per SIMD instead of four).
+template <int ENVK, int WG, bool NT, bool JD, bool LIST = false>
 __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int64_t batch,
                                                             const double* __restrict__ x,
                                                             const double* __restrict__ mass,
@@ -1320,30 +1335,30 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
   const int tid = threadIdx.x;
   const int T = K.T;
   const int n = K.n, m = K.m, nnz = K.nnz, N = K.N;
-  const int64_t count = d_count ? (int64_t)*d_count : batch;
-  const int64_t ntiles = (count + T - 1) / T;
+  const int64_t count = LIST ? (int64_t)*d_count : batch;
   NormAcc nacc;
   nacc.init(tid, WG, m);
-  // one tile per workgroup, or (list launches, a grid of the resident workgroups) tiles blockIdx,
-  // blockIdx + grid, ...
-  for (int64_t tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
-  const int64_t b0 = tl * T;
+  const int64_t b0 = (int64_t)blockIdx.x * T;
+  if (LIST && b0 >= count) {  // past the list's tiles: zero partials
+    if (K.want_norms) partial_norms_waves(nacc, norms_ws + NORM_HDR);
+    return;
+  }
   const int valid = (int)((count - b0) < T ? (count - b0) : T);
-  long long* rowb = reinterpret_cast<long long*>(smem + K.offRB);  // (idx) instance of each tile row
-  auto inst = [&](int r) -> int64_t { return idx ? (int64_t)rowb[r] : b0 + r; };
+  long long* rowb = reinterpret_cast<long long*>(smem + K.offRB);  // (LIST) instance of each tile row
+  auto inst = [&](int r) -> int64_t { return LIST ? (int64_t)rowb[r] : b0 + r; };
   double* X = smem;
   double* Gt = smem + K.offG;
   // the Jacobian rows: the LDS tile image, or (jdirect) the output records themselves
   double* Jt = JD ? jac_out + b0 * K.nnz : smem + K.offJ;
   // row r's Jacobian: the LDS image's, or (JD) the output record itself — of instance rowb[r] in a
   // list launch
-  auto JR = [&](int r) -> double* { return (JD && idx) ? jac_out + rowb[r] * nnz : Jt + r * nnz; };
+  auto JR = [&](int r) -> double* { return (JD && LIST) ? jac_out + rowb[r] * nnz : Jt + r * nnz; };
   double* Dt = smem + K.offD;
   double* L = smem + K.offL;                                    // [T][LR] (SQ / mixed)
   int* lists = reinterpret_cast<int*>(smem + K.offI);          // sq_list[64], gr_list[64], n_sq
   constexpr bool HAS_SQ = ENVK == CPL_ENV_SUPERQUADRIC || ENVK == CPL_ENV_MIXED;
 
-  if (idx) {
+  if (LIST) {
     if (tid < valid) rowb[tid] = idx[b0 + tid];
     __syncthreads();
     for (int e = tid; e < valid * n; e += WG) {
@@ -1428,16 +1443,27 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
     // first wait for every global store the items issued (f, and with jdirect the Jacobian rows)
     if (HAS_SQ && n_sq > 0 && wgj) lds_barrier();
     const int r_rows = r_ax;
-    const int items2 = r_rows + (OTHERS_FIRST ? 0 : r_gr);
+    // Superquadric batches: the friction cones as items of their own in phase 2 (the workgroup's
+    // fourth wave, otherwise idle there: the row-1 items no longer carry them)
+    constexpr bool CONE_ITEMS = ENVK == CPL_ENV_SUPERQUADRIC;
+    const int r_cone = (CONE_ITEMS && wgj) ? per_axis : 0;
+    const int items2 = r_rows + (OTHERS_FIRST ? 0 : r_gr) + r_cone;
     if (HAS_SQ)
       for (int it = tid; it < r_rows; it += WG) {
         const int a = it / per_axis, kj = it - a * per_axis;
         const int k = kj / n_sq, j = kj - k * n_sq;
         const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
-        sq_row_item<ENVK == CPL_ENV_MIXED>(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m, JR(r));
+        sq_row_item<ENVK == CPL_ENV_MIXED, !CONE_ITEMS>(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m, JR(r));
       }
-    for (int it = tid; it < items2; it += WG)
-      if (it >= r_rows) other_item(it - r_rows);
+    for (int it = tid; it < items2; it += WG) {
+      if (it < r_rows) continue;
+      if (CONE_ITEMS) {
+        const int e = it - r_rows, k = e / n_sq, r = e - k * n_sq;
+        sq_cone_item(K, X + r * n, k, Gt + r * m, JR(r));
+      } else {
+        other_item(it - r_rows);
+      }
+    }
     if (JD && K.want_j) {  // the statics Jacobian rows, lanes along each record
       lds_barrier();  // (the CoM pairs of the values items)
       for (int r = 0; r < valid; ++r) statics_rows_coop(K, X + r * n, com6 + 6 * r, JR(r), tid, WG);
@@ -1445,13 +1471,12 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
   }
   lds_barrier();
   // the residual partials first (from the LDS image), so that their stores are in flight with the
-  // copy-out's instead of after them on every workgroup's tail (one tile per workgroup; list
-  // launches accumulate over their tiles and write after the loop)
+  // copy-out's instead of after them on every workgroup's tail
   if (K.want_norms) {
     nacc.add_tile(Gt, valid * m, tid, WG, m);
-    if (!idx) partial_norms_waves(nacc, norms_ws + NORM_HDR);
+    partial_norms_waves(nacc, norms_ws + NORM_HDR);
   }
-  if (K.ablate != 2 && idx) {  // records written in place: row by row (g, jac rows are 16-byte aligned)
+  if (K.ablate != 2 && LIST) {  // records written in place: row by row (g, jac rows are 16-byte aligned)
     if (K.want_g) copy_out_rows<WG, NT>(g_out, rowb, Gt, m, valid, tid);
     if (K.want_j && !JD) copy_out_rows<WG, NT>(jac_out, rowb, Jt, nnz, valid, tid);
     if (K.want_grad)
@@ -1468,10 +1493,6 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
     if (K.want_j && !JD) copy_out<WG, NT>(jac_out + b0 * nnz, Jt, valid * nnz, tid);
     if (K.want_grad) copy_out<WG, NT>(grad_out + b0 * n, Dt, valid * n, tid);
   }
-  if (tl + gridDim.x < ntiles) __syncthreads();  // the next tile overwrites the LDS image
-  }  // tiles
-  // (list launches) the residual partials, one pair per wave — zeros from workgroups with no tile
-  if (K.want_norms && idx) partial_norms_waves(nacc, norms_ws + NORM_HDR);
 }
 
 
@@ -2416,6 +2437,29 @@ static int32_t side_stream(hipStream_t stream, SideStream* out) {
   return CPL_OK;
 }
 
+// whether a kind split can launch on `stream` now: outside a capture always; inside one only when the
+// stream's kind-list workspace and side stream already exist at this size (the default then falls
+// back to the interleaved mixed kernel — bitwise the same records — instead of failing the capture:
+// the solve engine captures its first iteration directly)
+static bool split_ready(hipStream_t stream, int64_t batch) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs == hipStreamCaptureStatusNone) return true;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  bool ws = false, side = false;
+  {
+    std::lock_guard<std::mutex> lk(g_kind_ws_mutex);
+    auto it = g_kind_ws.find({dev, stream});
+    ws = it != g_kind_ws.end() && it->second.cap >= batch;
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_side_mutex);
+    auto it = g_side.find({dev, stream});
+    side = it != g_side.end() && it->second.side != nullptr;
+  }
+  return ws && side;
+}
+
 static void launch_residual_final(int nparts, const double* part, double* out, hipStream_t s) {
   // 1024 threads: one load round trip for up to 8 192 partials (rocprof: 4.1 us at 768 partials,
   // 4.7 us on 256 threads — three dependent round trips in the tail loop).  Past 2 * RF_CHUNK
@@ -2521,7 +2565,8 @@ static int g_variant = VAR_AUTO;
 static size_t g_lds_budget = 0;    // 0 = per-kernel default (tile 32 KiB, pipelined 48 KiB)
 static int g_wg = 256;             // threads per tile workgroup (128 or 256)
 static int g_nt = 1;               // non-temporal output stores
-static int g_ablate = 0;           // measurement-only: 1 = skip the compute phase, 2 = skip the stores
+static int g_ablate = 0;           // measurement-only: 1 = skip the compute phase, 2 = skip the stores,
+                                   // 4 = the kind split's halves one after the other on the launch stream
 
 static size_t tile_budget() { return g_lds_budget ? g_lds_budget : 48 * 1024; }
 static size_t pipe_budget() { return g_lds_budget ? g_lds_budget : 48 * 1024; }
@@ -2614,13 +2659,19 @@ static int32_t plan_entry(KParams& K, bool g, bool j, bool f, bool grad) {
   K.offI = up2(K.offST + 2 + (K.m + K.nnz + 1) / 2);
   return CPL_OK;
 }
+// the entry-parallel kernel: forced (variants 5, 6), or by default for records of 12+ contacts (the
+// 16-contact Ground records: 0.81 against the pipelined kernel's 1.11 ms at 524 288 instances; the
+// pipelined kernel stays faster at 4 contacts, 0.40 against 0.45 ms at 1 048 576; profiles/r4)
 static bool use_entry(const KParams& K, int32_t flags) {
-  return (g_variant == VAR_ENTRY || g_variant == VAR_SPLIT) && flags == 0 && (K.nnz % 2) == 0 &&
-         (K.env_kind == CPL_ENV_NONE || K.env_kind == CPL_ENV_GROUND);
+  const bool want = g_variant == VAR_ENTRY || g_variant == VAR_SPLIT || (g_variant == VAR_AUTO && K.N >= 12);
+  return want && flags == 0 && (K.nnz % 2) == 0 && (K.env_kind == CPL_ENV_NONE || K.env_kind == CPL_ENV_GROUND);
 }
+// mixed batches split by kind: forced (variants 6, 7) or by default (as variant 6, the Superquadric half
+// staging its Jacobian rows in LDS: 1 048 576 x 16 in 3.34 ms against 3.89 with direct rows and 4.47 ms
+// interleaved, same process, profiles/r4)
 static bool use_split(const KParams& K, int32_t flags, int64_t batch) {
-  return (g_variant == VAR_SPLIT || g_variant == VAR_SPLIT_JD) && flags == 0 && K.env_kind == CPL_ENV_MIXED &&
-         batch <= 0x7fffffffLL;
+  return (g_variant == VAR_SPLIT || g_variant == VAR_SPLIT_JD || g_variant == VAR_AUTO) && flags == 0 &&
+         K.env_kind == CPL_ENV_MIXED && batch <= 0x7fffffffLL;
 }
 
 struct PipeLaunch {
@@ -2737,7 +2788,7 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
   double* ws = nullptr;
   if (lg && !use_pipe(K))
     return fail(CPL_ERR_UNSUPPORTED, "fused Lagrangian gradient: pipelined (Ground / no environment) path only");
-  if (!lg && use_split(K, flags, batch)) {
+  if (!lg && use_split(K, flags, batch) && (g_variant != VAR_AUTO || split_ready(stream, batch))) {
     // mixed batch split by kind: the stable partition, then the Ground instances through the entry
     // kernel and the Superquadric ones through the Superquadric tile kernel, records in place
     KindLists kl;
@@ -2752,42 +2803,45 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
     if ((st = plan_entry(Kg, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr))) return st;
     Ks.jdirect = (g_variant == VAR_SPLIT_JD && d_jac) ? 1 : 0;
     if ((st = plan_tile(Ks, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr))) return st;
-    Kg.ablate = Ks.ablate = g_ablate;
+    Kg.ablate = Ks.ablate = g_ablate & 3;
+    const bool sequential = (g_ablate & 4) != 0;
     using EntryT = void (*)(const KParams, int64_t, const double*, const double*, const int32_t*, const int32_t*,
                             double*, double*, double*, double*, double*);
     using TileT = void (*)(const KParams, int64_t, const double*, const double*, const uint8_t*, const int32_t*,
                            const int32_t*, double*, double*, double*, double*, double*);
     const EntryT ek = g_nt ? cpl_eval_entry_kernel<CPL_ENV_GROUND, true> : cpl_eval_entry_kernel<CPL_ENV_GROUND, false>;
-    const TileT tk = Ks.jdirect ? (g_nt ? cpl_eval_tile_kernel<CPL_ENV_SUPERQUADRIC, 256, true, true>
-                                        : cpl_eval_tile_kernel<CPL_ENV_SUPERQUADRIC, 256, false, true>)
-                                : (g_nt ? cpl_eval_tile_kernel<CPL_ENV_SUPERQUADRIC, 256, true, false>
-                                        : cpl_eval_tile_kernel<CPL_ENV_SUPERQUADRIC, 256, false, false>);
+    const TileT tk = Ks.jdirect ? (g_nt ? cpl_eval_tile_kernel<CPL_ENV_SUPERQUADRIC, 256, true, true, true>
+                                        : cpl_eval_tile_kernel<CPL_ENV_SUPERQUADRIC, 256, false, true, true>)
+                                : (g_nt ? cpl_eval_tile_kernel<CPL_ENV_SUPERQUADRIC, 256, true, false, true>
+                                        : cpl_eval_tile_kernel<CPL_ENV_SUPERQUADRIC, 256, false, false, true>);
     const size_t lds_g = sizeof(double) * (size_t)Kg.offI;
     const size_t lds_s = sizeof(double) * (size_t)(Ks.offRB + Ks.T);
     const int64_t ntg = (batch + Kg.T - 1) / Kg.T;
     const int64_t want = resident_blocks(reinterpret_cast<const void*>(ek), lds_g);
     const unsigned grid_g = (unsigned)(ntg < want ? ntg : want);
-    const int64_t nts = (batch + Ks.T - 1) / Ks.T;
-    const int64_t want_s = resident_blocks(reinterpret_cast<const void*>(tk), lds_s);
-    const unsigned grid_s = (unsigned)(nts < want_s ? nts : want_s);
+    const unsigned grid_s = (unsigned)((batch + Ks.T - 1) / Ks.T);  // every tile the list may hold
     const size_t nparts = (size_t)grid_g + (size_t)grid_s * 4;
     if (K.want_norms && (st = norm_workspace(stream, nparts, &ws))) return st;
     // the two halves on two streams (fork after the partition, join before the norms' finish): the
     // memory-bound Ground records and the latency-bound Superquadric tiles share the CUs
     SideStream ss;
-    if ((st = side_stream(stream, &ss))) return st;
-    hipError_t e = hipEventRecord(ss.fork, stream);
-    if (e == hipSuccess) e = hipStreamWaitEvent(ss.side, ss.fork, 0);
-    if (e != hipSuccess) return hip_fail(e, "mixed split fork");
+    if (!sequential) {
+      if ((st = side_stream(stream, &ss))) return st;
+      hipError_t e = hipEventRecord(ss.fork, stream);
+      if (e == hipSuccess) e = hipStreamWaitEvent(ss.side, ss.fork, 0);
+      if (e != hipSuccess) return hip_fail(e, "mixed split fork");
+    }
     hipLaunchKernelGGL(tk, dim3(grid_s), dim3(256), lds_s, stream, Ks, batch, d_x, d_mass, d_env_tag, kl.idx_sq,
                        kl.counts + 1, d_g, d_jac, d_f, d_grad, ws ? ws + 2 * (size_t)grid_g : nullptr);
-    hipLaunchKernelGGL(ek, dim3(grid_g), dim3(256), lds_g, ss.side, Kg, batch, d_x, d_mass, kl.idx_gr, kl.counts, d_g,
-                       d_jac, d_f, d_grad, ws);
-    e = hipGetLastError();
+    hipLaunchKernelGGL(ek, dim3(grid_g), dim3(256), lds_g, sequential ? stream : ss.side, Kg, batch, d_x, d_mass,
+                       kl.idx_gr, kl.counts, d_g, d_jac, d_f, d_grad, ws);
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "mixed split launch");
-    e = hipEventRecord(ss.join, ss.side);
-    if (e == hipSuccess) e = hipStreamWaitEvent(stream, ss.join, 0);
-    if (e != hipSuccess) return hip_fail(e, "mixed split join");
+    if (!sequential) {
+      e = hipEventRecord(ss.join, ss.side);
+      if (e == hipSuccess) e = hipStreamWaitEvent(stream, ss.join, 0);
+      if (e != hipSuccess) return hip_fail(e, "mixed split join");
+    }
     if (K.want_norms && finish) launch_residual_final((int)nparts, ws + NORM_HDR, d_norms, stream);
     return CPL_OK;
   }
@@ -3221,7 +3275,7 @@ int32_t cpl_eval_batch_norms(const cpl_problem_desc* d, int64_t batch, const dou
 
 int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_threads, int32_t nt_stores,
                        int32_t ablate) {
-  if (ablate < 0 || ablate > 2) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
+  if (ablate < 0 || ablate > 2 && ablate != 4) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
   g_ablate = ablate;
   if (kernel_variant < VAR_AUTO || kernel_variant > VAR_SPLIT_JD) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown kernel variant");
   if (tile_lds_kb != 0 && (tile_lds_kb < 8 || tile_lds_kb > 160))

@@ -1072,6 +1072,31 @@ __global__ __launch_bounds__(256) void k_resto_prep1(
   }
 }
 
+// a restoration phase that failed (k_resto_prep1: RESTO_FAILED) with a backup acceptable point: IPOPT
+// restores that point and stops there as acceptable (BacktrackingLineSearch: RestoreAcceptablePoint,
+// STOP_AT_ACCEPTABLE_POINT); batch_ipm.py resto_step restates it
+__global__ __launch_bounds__(256) void k_restore_acc(int64_t B, int m, int nw, int64_t* __restrict__ status,
+                                                     uint8_t* __restrict__ has_acc, const double* __restrict__ acc_w,
+                                                     const double* __restrict__ acc_y, const double* __restrict__ acc_zL,
+                                                     const double* __restrict__ acc_zU, double* __restrict__ w,
+                                                     double* __restrict__ y, double* __restrict__ zL,
+                                                     double* __restrict__ zU) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B || status[b] != CPL_SOLVE_RESTO_FAILED || !has_acc[b]) return;
+  const int lane = threadIdx.x & 63;
+  for (int k = lane; k < nw; k += 64) {
+    w[b * nw + k] = acc_w[b * nw + k];
+    zL[b * nw + k] = acc_zL[b * nw + k];
+    zU[b * nw + k] = acc_zU[b * nw + k];
+  }
+  for (int r = lane; r < m; r += 64) y[b * m + r] = acc_y[b * m + r];
+  __builtin_amdgcn_wave_barrier();  // (one wave per instance: its lanes read status / has_acc above)
+  if (lane == 0) {
+    status[b] = CPL_SOLVE_ACCEPTABLE;
+    has_acc[b] = 0;
+  }
+}
+
 // after the Newton setup (M = diag(Sigma_R) + H_c, r1 = -(grad phi_R,w + A^T y)): the proximity
 // term's Hessian eta D_R^2 on M's diagonal, the eliminated p / n blocks (Sigma_p = zp / p,
 // Sigma_n = zn / n, D^-1 = 1 / (1/Sigma_p + 1/Sigma_n), r2 = -(c - p + n) + r_p / Sigma_p - r_n / Sigma_n)
@@ -1433,11 +1458,32 @@ __global__ __launch_bounds__(256) void k_resto_accept(
 // system-scope fence: the host polls seq instead of a D2H copy + stream synchronisation (a blit
 // kernel and two host wake-ups per iteration, ~35 us of a single solve's ~200 us iteration).
 constexpr int64_t COUNT1_MAX = 65536;
+constexpr int64_t TRACK_FUSE_ROWS = 64;  // batches up to this size track the best iterate inside k_count1
+struct TrackBest {  // (small batches) k_track_best's work inside k_count1; best_w == NULL: none
+  int nw;
+  double vtol;
+  const double *w, *f, *g, *gl, *gu;
+  double *best_w, *best_f;
+};
+__device__ __forceinline__ double orig_violation_wave(int m, const double* __restrict__ gb,
+                                                      const double* __restrict__ gl, const double* __restrict__ gu);
 __global__ __launch_bounds__(1024) void k_count1(int64_t B, const uint8_t* __restrict__ active,
                                                  const uint8_t* __restrict__ in_resto, int32_t* __restrict__ count,
                                                  int32_t* __restrict__ mail, int m, const uint8_t* __restrict__ failed,
-                                                 const double* __restrict__ dy, double* __restrict__ y) {
+                                                 const double* __restrict__ dy, double* __restrict__ y,
+                                                 const TrackBest tb) {
   __shared__ int s_w[16], s_r[16];
+  if (tb.best_w) {  // k_track_best's work, a wave per instance (the same operations)
+    const int lane = threadIdx.x & 63;
+    for (int64_t b = threadIdx.x >> 6; b < B; b += 16) {
+      if (!active[b]) continue;
+      const double v = orig_violation_wave(m, tb.g + b * m, tb.gl, tb.gu);
+      const double fb = tb.f[b];
+      if (!(v <= tb.vtol) || !(fb < tb.best_f[b])) continue;
+      for (int k = lane; k < tb.nw; k += 64) tb.best_w[b * tb.nw + k] = tb.w[b * tb.nw + k];
+      if (lane == 0) tb.best_f[b] = fb;
+    }
+  }
   if (failed) {  // k_resto_y0's work, a wave per instance (no dependence on the counts below)
     const int lane = threadIdx.x & 63;
     for (int64_t b = threadIdx.x >> 6; b < B; b += 16) {
@@ -1760,6 +1806,8 @@ struct cpl_solver {
   int64_t *status, *iters, *acc, *fcount, *n_resto;
   uint8_t *active, *lm_cnt, *lm_skip, *d_any, *in_soft, *tiny_last, *tiny_flag, *in_resto, *resto_tight;
   double *best_w, *best_f;  // the best iterate feasible to fallback_viol_tol (lowest f) and its f
+  double *acc_w, *acc_y, *acc_zL, *acc_zU;  // IPOPT's backup acceptable point
+  uint8_t* has_acc;
   uint8_t* fbest;           // [B] full-batch: the solve returned that iterate instead of its last one
   int32_t* soft_cnt;
   // restoration state
@@ -1949,7 +1997,8 @@ int32_t step_phase(cpl_solver* S, int phase) {
         LAUNCHED("k_dense_a_prep");
       }
       // (with k_unpack_tau's X = unpack(w), tau and the active snapshot fused into its tail)
-      const IpmUnpack unp{n, S->freepos, S->Xbase, S->in_resto, S->X, S->tau, S->act};
+      const IpmUnpack unp{n, S->freepos, S->Xbase, S->in_resto, S->X, S->tau, S->act,
+                          S->acc_w, S->acc_y, S->acc_zL, S->acc_zU, S->has_acc};
       CK(ipm_optimality_ex(B, nw, m, FMAX, S->nbounds, o.tol, o.acceptable_tol, o.acceptable_iter, S->A, S->gradw,
                            S->c, S->w, S->y, S->zL, S->zU, S->hasL, S->hasU, S->wl0, S->wu0, S->mu, S->filt_t,
                            S->filt_p, S->fcount, S->active, S->status, S->acc, S->d_inf, S->err0, S->base, S->mu_o,
@@ -2103,7 +2152,10 @@ int32_t step_phase(cpl_solver* S, int phase) {
         LAUNCHED("k_resto_y0");
       }
     count:
-      if (o.fallback_viol_tol > 0.0) {
+      const bool track_fused = o.fallback_viol_tol > 0.0 && B <= TRACK_FUSE_ROWS;
+      TrackBest tb{};
+      if (track_fused) tb = TrackBest{nw, o.fallback_viol_tol, S->w, S->f, S->g, S->gl, S->gu, S->best_w, S->best_f};
+      if (o.fallback_viol_tol > 0.0 && !track_fused) {
         hipLaunchKernelGGL(k_track_best, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nw, o.fallback_viol_tol,
                            S->active, S->w, S->f, S->g, S->gl, S->gu, S->best_w, S->best_f);
         LAUNCHED("k_track_best");
@@ -2115,7 +2167,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
       } else {
         // (with the restoration entry's multiplier reset fused in: P_ACCEPT)
         hipLaunchKernelGGL(k_count1, dim3(1), dim3(1024), 0, st, B, S->active, S->in_resto, S->d_count, S->h_count, m,
-                           phase == P_ACCEPT ? S->failed : nullptr, S->dy, S->y);
+                           phase == P_ACCEPT ? S->failed : nullptr, S->dy, S->y, tb);
       }
       LAUNCHED("k_count");
       return CPL_OK;
@@ -2127,6 +2179,9 @@ int32_t step_phase(cpl_solver* S, int phase) {
                          S->nR, S->zp, S->zn, S->zLR, S->zUR, S->hasL, S->hasU, S->wl0, S->wu0, S->muR, S->ftR,
                          S->fpR, S->fcR, S->tauR, S->gfR);
       LAUNCHED("k_resto_prep1");
+      hipLaunchKernelGGL(k_restore_acc, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nw, S->status, S->has_acc,
+                         S->acc_w, S->acc_y, S->acc_zL, S->acc_zU, S->w, S->y, S->zL, S->zU);
+      LAUNCHED("k_restore_acc");
       const double* Hblk = nullptr;
       int h_sym = 0;
       CK(hessian_into(S, &S->desc_R, S->actR, &Hblk, &h_sym));
@@ -2317,6 +2372,7 @@ int32_t compact(cpl_solver* S, int64_t count, int64_t Bn) {
   CK(move(S->zLR, nw)); CK(move(S->zUR, nw)); CK(move(S->muR, 1)); CK(move(S->ftR, FMAX)); CK(move(S->fpR, FMAX));
   CK(move(S->fcR, 1)); CK(move(S->th_o0, 1)); CK(move(S->ph_o0, 1)); CK(move(S->dwlR, 1)); CK(move(S->thmaxR, 1));
   CK(move(S->thminR, 1)); CK(move(S->best_w, nw)); CK(move(S->best_f, 1));
+  CK(move(S->acc_w, nw)); CK(move(S->acc_y, m)); CK(move(S->acc_zL, nw)); CK(move(S->acc_zU, nw));
   if (S->bfgs) {
     CK(move(S->Hq, LMC(nf)));
     CK(move(S->lm_s, (int64_t)LM_HIST * nf));
@@ -2339,6 +2395,7 @@ int32_t compact(cpl_solver* S, int64_t count, int64_t Bn) {
   CK(move_bytes(S->tiny_flag));
   CK(move_bytes(S->in_resto));
   CK(move_bytes(S->resto_tight));
+  CK(move_bytes(S->has_acc));
   if (S->tag) CK(move_bytes(S->tag_c));
   auto move_i32 = [&](int32_t* buf) -> int32_t {
     hipLaunchKernelGGL(k_gather_i32, dim3(blocks_elems(count)), dim3(256), 0, st, count, S->pos, buf,
@@ -2569,6 +2626,8 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   S->in_soft = a.take<uint8_t>(Bz); S->tiny_last = a.take<uint8_t>(Bz); S->tiny_flag = a.take<uint8_t>(Bz);
   S->in_resto = a.take<uint8_t>(Bz); S->soft_cnt = a.take<int32_t>(Bz); S->resto_tight = a.take<uint8_t>(Bz);
   S->best_w = a.take<double>(Bz * nw); S->best_f = a.take<double>(Bz); S->fbest = a.take<uint8_t>(Bz);
+  S->acc_w = a.take<double>(Bz * nw); S->acc_y = a.take<double>(Bz * m); S->acc_zL = a.take<double>(Bz * nw);
+  S->acc_zU = a.take<double>(Bz * nw); S->has_acc = a.take<uint8_t>(Bz);
   // the restoration phase's state
   S->wR = a.take<double>(Bz * nw); S->pR = a.take<double>(Bz * m); S->nR = a.take<double>(Bz * m);
   S->zp = a.take<double>(Bz * m); S->zn = a.take<double>(Bz * m); S->zLR = a.take<double>(Bz * nw);
@@ -2680,6 +2739,7 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
   HK(hipMemsetAsync(S->in_resto, 0, (size_t)B, st), "hipMemsetAsync");
   HK(hipMemsetAsync(S->resto_tight, 0, (size_t)B, st), "hipMemsetAsync");
   HK(hipMemsetAsync(S->fbest, 0, (size_t)B, st), "hipMemsetAsync");
+  HK(hipMemsetAsync(S->has_acc, 0, (size_t)B, st), "hipMemsetAsync");
   hipLaunchKernelGGL(k_fill, dim3(blocks_elems(B)), dim3(256), 0, st, B, INFINITY, S->best_f);
   LAUNCHED("k_fill best_f");
   HK(hipMemsetAsync(S->soft_cnt, 0, 4 * (size_t)B, st), "hipMemsetAsync");

@@ -539,6 +539,8 @@ typedef struct {
   int n_resto, resto_tight;
   double theta_max, theta_min;
   double best_w[NWMAX], best_f;
+  double acc_w[NWMAX], acc_y[MMAX], acc_zL[NWMAX], acc_zU[NWMAX];  /* IPOPT's backup acceptable point */
+  int has_acc;
 } State;
 
 typedef struct {
@@ -787,6 +789,13 @@ static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
   static double M[NWMAX * NWMAX];
   static Eval trial, tsoc, ev_new;
   double mu = S->mu;
+  if (E->err0 <= o->acceptable_tol) {  /* StoreAcceptablePoint (CurrentIsAcceptable) */
+    memcpy(S->acc_w, S->w, sizeof(double) * (size_t)nw);
+    memcpy(S->acc_zL, S->zL, sizeof(double) * (size_t)nw);
+    memcpy(S->acc_zU, S->zU, sizeof(double) * (size_t)nw);
+    memcpy(S->acc_y, S->y, sizeof(double) * (size_t)m);
+    S->has_acc = 1;
+  }
   /* monotone barrier update (mu_allow_fast_monotone_decrease), the filter reset where mu changed */
   const int force = S->tiny_flag;
   for (int r = 0; r < MU_ROUNDS; ++r) {
@@ -1011,6 +1020,13 @@ static void resto_step(Prob* P, State* S, const Opts* o) {
     if (!feas || S->resto_tight) {
       S->status = feas ? ST_RESTO_FAILED : ST_INFEASIBLE;
       S->active = 0;
+      if (feas && S->has_acc) {  /* RestoreAcceptablePoint: stop there as acceptable */
+        memcpy(S->w, S->acc_w, sizeof(double) * (size_t)nw);
+        memcpy(S->zL, S->acc_zL, sizeof(double) * (size_t)nw);
+        memcpy(S->zU, S->acc_zU, sizeof(double) * (size_t)nw);
+        memcpy(S->y, S->acc_y, sizeof(double) * (size_t)m);
+        S->status = ST_ACCEPTABLE;
+      }
       return;
     }
     S->resto_tight = 1;

@@ -227,6 +227,53 @@ def plain_rel_diagonals(prob, env, x, got, ref, tag=None):
     return out
 
 
+def plain_rel_g_graded(prob, env, x, got, ref, tag=None):
+    """The Superquadric g entries (environment value sum pow - 1, normal residual n - n_env: both cancel
+    near the surface) graded on the PLAIN relative error wherever |ref| is above the rounding noise of
+    their un-cancelled terms (|ref| > NOISE_ULPS * eps * g_scale).  Returns {"graded", "noise", "max",
+    "outside": graded entries above RTOL, "outside_err_ulps": their |gpu - ref| in units of eps *
+    g_scale (at most 32), "outside_ref_over_scale", "hist"}."""
+    from centroidalplanner_amd import ENV_SUPERQUADRIC
+
+    N = len(prob.contact_names)
+    n, m, nnz = prob.get_nlp_info()
+    B = x.shape[0]
+    sq_inst = (np.ones(B, dtype=bool) if env == "superquadric" else
+               (tag == ENV_SUPERQUADRIC) if env == "mixed" else np.zeros(B, dtype=bool))
+    out = {"graded": 0, "noise": 0, "max": 0.0, "outside": 0, "outside_err_ulps": [], "outside_ref_over_scale": [],
+           "hist": {"bitwise": 0, "lt1e-15": 0, "lt1e-13": 0, "lt1e-12": 0, "lt1e-10": 0, "ge1e-10": 0}}
+    if not sq_inst.any():
+        return out
+    _, gm = sq_entry_mask(N, prob.map_order, nnz, m, sq_inst)
+    gv, rv = np.asarray(got["g"]), np.asarray(ref["g"])
+    scale = g_scale(x, N, prob.map_order, rv, *sq_params(prob), sq_inst)
+    eps = np.finfo(np.float64).eps
+    with np.errstate(all="ignore"):
+        fin = gm & ~(np.isnan(gv) | np.isnan(rv)) & np.isfinite(scale)
+        noise = fin & ~(np.abs(rv) > NOISE_ULPS * eps * scale)
+        sel = fin & ~noise
+        err = np.where(sel & (gv != rv), np.abs(gv - rv), 0.0)
+        rel = np.where(err > 0, err / np.where(np.abs(rv) > 0, np.abs(rv), 1.0), 0.0)
+    out["noise"] = int(noise.sum())
+    out["graded"] = int(sel.sum())
+    v = rel[sel]
+    out["max"] = float(v.max()) if v.size else 0.0
+    nz = v[v > 0]
+    h = out["hist"]
+    h["bitwise"] = int((v == 0).sum())
+    h["lt1e-15"] = int((nz < 1e-15).sum())
+    h["lt1e-13"] = int(((nz >= 1e-15) & (nz < 1e-13)).sum())
+    h["lt1e-12"] = int(((nz >= 1e-13) & (nz < 1e-12)).sum())
+    h["lt1e-10"] = int(((nz >= 1e-12) & (nz < 1e-10)).sum())
+    h["ge1e-10"] = int((nz >= 1e-10).sum())
+    bad = sel & (rel > RTOL)
+    out["outside"] = int(bad.sum())
+    with np.errstate(all="ignore"):
+        out["outside_err_ulps"] = [float(t) for t in (err[bad] / (eps * scale[bad]))[:32]]
+        out["outside_ref_over_scale"] = [float(t) for t in (np.abs(rv[bad]) / scale[bad])[:32]]
+    return out
+
+
 def check_outputs(prob, env, x, got, ref, tag=None, raise_on_fail=True):
     """Apply the policy above to every output; returns {output: stats}; raises AssertionError
     (raise_on_fail=False: every output is checked and stats["ok"] says whether it passed)."""

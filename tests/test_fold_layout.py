@@ -111,7 +111,11 @@ def test_soa_is_transposed_aos(variant, env, N, folded):
         assert soa[k].shape == (aos[k].shape[1], B)
         assert torch.equal(soa[k], aos[k].t())
     assert torch.equal(soa["f"], aos["f"])
-    assert torch.equal(soa["norms"], aos["norms"])
+    # [max violation, sum of squares]: the max exactly; the sum is summed per kernel tile, and by default
+    # a mixed AoS batch runs the kind split (two kernels' partials) where the SoA one runs the interleaved
+    # kernel — the same terms in another order, equal to rounding
+    assert soa["norms"][0] == aos["norms"][0]
+    assert float(soa["norms"][1]) == pytest.approx(float(aos["norms"][1]), rel=1e-12, abs=1e-300)
 
 
 @pytest.mark.gpu

@@ -1,5 +1,5 @@
-"""The entry-parallel eval kernel (cpl_kernels.hip cpl_eval_entry_kernel, tuning variant 5) against
-the default kernels, bit for bit, on every output (g, CSR Jacobian values, f, grad, fused residual
+"""The entry-parallel eval kernel (cpl_kernels.hip cpl_eval_entry_kernel, tuning variant 5; the
+default for 12+ contacts) against the pipelined / tile kernels, bit for bit, on every output (g, CSR Jacobian values, f, grad, fused residual
 norms), and against the oracle: Ground and no-environment records of 1 ... 16 contacts, ragged
 batches (tiles cut short), the degenerate x = 0 (0/0 cone entries: NaN positions must match)."""
 import ctypes
@@ -49,7 +49,7 @@ def test_entry_kernel_bitwise_default_and_oracle(env, N, B):
         x[B // 2] = 0.0  # the cone's 0/0 entries (NaN) at one instance
     dev = torch.device("cuda:0")
     xt, mt = torch.tensor(x, device=dev), torch.tensor(mass, device=dev)
-    ref = _run(prob, xt, mt, 0)
+    ref = _run(prob, xt, mt, 2)  # the pipelined kernel (the tile kernel where x rows are not 16-byte aligned)
     got = _run(prob, xt, mt, 5)
     for k in ("g", "jac", "f", "grad"):
         assert torch.equal(_bits(got[k]), _bits(ref[k])), k
@@ -116,3 +116,34 @@ def test_mixed_split_bitwise_default_and_oracle(N, B, pattern):
         _same_norms(got["norms"], ref["norms"])
     orc = pyoracle.eval_batch(prob.desc(), x, mass, tag)
     check_outputs(prob, "mixed", x, {k: got[k].cpu().numpy() for k in ("g", "jac", "f", "grad")}, orc, tag)
+
+
+@pytest.mark.gpu
+def test_mixed_default_split_under_graph_capture():
+    """The default mixed launch (the kind split: a stable partition, two kernels on two streams joined
+    by events) inside a HIP graph: captured after one eager launch on the stream it replays the eager
+    records bit for bit; captured on a fresh stream with no eager launch (the split's workspace and side
+    stream do not exist yet, as in the solve engine's first iteration) the default falls back to the
+    interleaved kernel — the same records, no capture error."""
+    prob = make_problem(16, "mixed")
+    x, mass, tag = generate(16, "mixed", 3001, 99)
+    dev = torch.device("cuda:0")
+    xt, mt, tt = torch.tensor(x, device=dev), torch.tensor(mass, device=dev), torch.tensor(tag, device=dev)
+    ref = prob.eval_batch(xt, mt, tt, outputs=("g", "jac"))
+    torch.cuda.synchronize()
+    for warm in (True, False):
+        s = torch.cuda.Stream(dev)
+        out = {"g": torch.empty_like(ref["g"]), "jac": torch.empty_like(ref["jac"])}
+        with torch.cuda.stream(s):
+            if warm:
+                prob.eval_batch(xt, mt, tt, outputs=("g", "jac"), out=out, stream=s)
+            s.synchronize()
+            out["g"].zero_()
+            out["jac"].zero_()
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr, stream=s):
+                prob.eval_batch(xt, mt, tt, outputs=("g", "jac"), out=out, stream=s)
+            gr.replay()
+        s.synchronize()
+        for k in ("g", "jac"):
+            assert torch.equal(_bits(out[k]), _bits(ref[k])), (warm, k)
