@@ -28,11 +28,20 @@ ap.add_argument("--outputs", default="g,jac")
 ap.add_argument("--norms", action="store_true", help="fused residual norms (cpl_eval_batch_norms)")
 ap.add_argument("--folded", action="store_true", help="values-only Jacobian records (CPL_EVAL_JAC_FOLDED)")
 ap.add_argument("--soa", action="store_true", help="entry-major outputs (CPL_EVAL_SOA)")
+ap.add_argument("--tags", default="", help="mixed configs: all_sq | all_ground (every instance of one kind)")
 args = ap.parse_args()
 
 cfg = CONFIGS[args.config]
 B = args.batch or cfg.batch
 prob, x, mass, tag = config_inputs(cfg, B)
+if args.tags:  # one kind only, through the mixed launch (the kind split's halves alone)
+    import numpy as np
+
+    from centroidalplanner_amd.workload import generate
+
+    kind = "superquadric" if args.tags == "all_sq" else "ground"
+    x, _, _ = generate(cfg.n_contacts, kind, B, 4242)
+    tag = np.full(B, 2 if kind == "superquadric" else 1, np.uint8)
 dev = torch.device("cuda:0")
 xt, mt = torch.tensor(x, device=dev), torch.tensor(mass, device=dev)
 tt = None if tag is None else torch.tensor(tag, device=dev)
