@@ -162,7 +162,12 @@ def spawn_ranks(world, argv=None, poll_s=0.5):
         codes = [p.poll() for p in procs]
         bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
         if bad:
-            failed = bad[0]
+            # a rank's failure usually takes its peers' collectives down with it: give them a moment to
+            # exit on their own so that every rank that failed by itself is named, not just the lowest
+            t_end = time.time() + 3.0
+            while time.time() < t_end and any(p.poll() is None for p in procs):
+                time.sleep(poll_s)
+            failed = [(r, p.poll()) for r, p in enumerate(procs) if p.poll() not in (None, 0)]
             break
         if all(c == 0 for c in codes):
             break
@@ -190,7 +195,8 @@ def spawn_ranks(world, argv=None, poll_s=0.5):
             sys.stderr.write(ln)
     sys.stdout.flush()
     if failed is not None:
-        print(f"bench.py: rank {failed[0]} exited with {failed[1]}", file=sys.stderr)
+        for r, c in failed:
+            print(f"bench.py: rank {r} exited with {c}", file=sys.stderr)
         return 1
     return 0
 

@@ -1338,11 +1338,11 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
   const int64_t count = LIST ? (int64_t)*d_count : batch;
   NormAcc nacc;
   nacc.init(tid, WG, m);
-  const int64_t b0 = (int64_t)blockIdx.x * T;
-  if (LIST && b0 >= count) {  // past the list's tiles: zero partials
-    if (K.want_norms) partial_norms_waves(nacc, norms_ws + NORM_HDR);
-    return;
-  }
+  // LIST: a persistent grid (the resident workgroups) walking the list's tiles blockIdx, + grid, ...
+  // (the list's length is known on the device only); otherwise this workgroup's tile, once
+  const int64_t ntiles = (count + T - 1) / T;
+  for (int64_t tl = blockIdx.x; !LIST || tl < ntiles; tl += gridDim.x) {
+  const int64_t b0 = tl * T;
   const int valid = (int)((count - b0) < T ? (count - b0) : T);
   long long* rowb = reinterpret_cast<long long*>(smem + K.offRB);  // (LIST) instance of each tile row
   auto inst = [&](int r) -> int64_t { return LIST ? (int64_t)rowb[r] : b0 + r; };
@@ -1361,9 +1361,27 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
   if (LIST) {
     if (tid < valid) rowb[tid] = idx[b0 + tid];
     __syncthreads();
-    for (int e = tid; e < valid * n; e += WG) {
-      const int r = e / n;
-      X[e] = x[rowb[r] * n + (e - r * n)];
+    // the tile's rows gathered through the list, eight loads in flight per thread before their LDS
+    // stores (one load per iteration waited an HBM round trip each); element e = (row r, column c)
+    // advanced by the workgroup size without a division
+    constexpr int U = 8;
+    const int cnt = valid * n, dr = WG / n, dc = WG - dr * n;
+    int r = tid / n, c = tid - r * n;
+    for (int e0 = tid; e0 < cnt; e0 += U * WG) {
+      double v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        v[u] = e0 + u * WG < cnt ? x[rowb[r] * n + c] : 0.0;
+        c += dc;
+        r += dr;
+        if (c >= n) {
+          c -= n;
+          ++r;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (e0 + u * WG < cnt) X[e0 + u * WG] = v[u];
     }
   } else {
     copy_in<WG>(X, x + b0 * n, valid * n, tid, K.x_aligned16 != 0);
@@ -1474,7 +1492,7 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
   // copy-out's instead of after them on every workgroup's tail
   if (K.want_norms) {
     nacc.add_tile(Gt, valid * m, tid, WG, m);
-    partial_norms_waves(nacc, norms_ws + NORM_HDR);
+    if (!LIST) partial_norms_waves(nacc, norms_ws + NORM_HDR);
   }
   if (K.ablate != 2 && LIST) {  // records written in place: row by row (g, jac rows are 16-byte aligned)
     if (K.want_g) copy_out_rows<WG, NT>(g_out, rowb, Gt, m, valid, tid);
@@ -1493,6 +1511,11 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
     if (K.want_j && !JD) copy_out<WG, NT>(jac_out + b0 * nnz, Jt, valid * nnz, tid);
     if (K.want_grad) copy_out<WG, NT>(grad_out + b0 * n, Dt, valid * n, tid);
   }
+  if (!LIST) break;
+  if (tl + gridDim.x < ntiles) __syncthreads();  // the next tile overwrites the LDS image
+  }  // tiles
+  // (LIST) the residual partials after the tiles, one pair per wave (zeros from workgroups with none)
+  if (LIST && K.want_norms) partial_norms_waves(nacc, norms_ws + NORM_HDR);
 }
 
 
@@ -1825,6 +1848,19 @@ __device__ __forceinline__ unsigned entry_op_j(int q, int N, int S0) {
   return OP_S | (unsigned)(S0 + ENT_PC * i + EPC_ROW1 + (w - 6));   // row 1 (:82-101)
 }
 
+// loader wave: one row of `count` doubles from a 16-byte aligned source into LDS (dst 16-byte aligned):
+// 16-byte DMA granules for the pairs (1 KiB per instruction), the odd last double as two dwords
+__device__ __forceinline__ void dma_row16(double* dst, const double* src, int count, int lane) {
+  const int pairs = count >> 1;
+  for (int q = 0; q < pairs; q += 64)
+    if (q + lane < pairs)
+      __builtin_amdgcn_global_load_lds((glb_void_t*)(src + 2 * (q + lane)), (lds_void_t*)(dst + 2 * q), 16, 0, 0);
+  if (count & 1) {
+    const unsigned* s4 = reinterpret_cast<const unsigned*>(src + count - 1);
+    if (lane < 2) __builtin_amdgcn_global_load_lds((glb_void_t*)(s4 + lane), (lds_void_t*)(dst + count - 1), 4, 0, 0);
+  }
+}
+
 // loader wave: one row of `count` doubles (8-byte aligned source) into LDS with 4-byte DMA granules
 __device__ __forceinline__ void dma_row4(double* dst, const double* src, int count, int lane) {
   const unsigned* s4 = reinterpret_cast<const unsigned*>(src);
@@ -1880,6 +1916,9 @@ __global__ __launch_bounds__(256) void cpl_eval_entry_kernel(const KParams K, in
   const int64_t count = d_count ? (int64_t)*d_count : batch;
   const int64_t ntiles = (count + T - 1) / T;
   const bool contiguous = idx == nullptr && K.x_aligned16;
+  // LDS row stride of x: n for contiguous tiles (one DMA stream), even for lists (every row slot 16-byte
+  // aligned, so the rows whose source is aligned too take 16-byte granules)
+  const int xs = contiguous ? n : (n + 1) & ~1;
   double mass_def = K.mass_default;  // a value (see cpl_eval_pipe_kernel)
   asm volatile("" : "+v"(mass_def));
   NormAcc acc;
@@ -1889,21 +1928,41 @@ __global__ __launch_bounds__(256) void cpl_eval_entry_kernel(const KParams K, in
   if (loader) {
     double st_mass = 0.0, st_tail = 0.0;
     long long st_b = 0;
+    // (lists) the instances and masses of the tile staged next, loaded one tile ahead: the rows' DMA
+    // then issues at once instead of after two dependent round trips (the list entry, then its mass)
+    long long pf_b = 0;
+    double pf_mass = 0.0;
+    auto ids = [&](int64_t tt, long long& bo, double& mo) {
+      const int64_t j0 = tt * T;
+      const int vs = (int)((count - j0) < T ? (count - j0) : T);
+      if (lane < vs) {
+        const int b = idx ? idx[j0 + lane] : (int)(j0 + lane);
+        bo = b;
+        mo = mass ? mass[b] : mass_def;
+      }
+    };
     auto stage = [&](int64_t tt, int bi) {
       const int64_t j0 = tt * T;
       const int vs = (int)((count - j0) < T ? (count - j0) : T);
-      int b = 0;
-      if (lane < vs) {
-        b = idx ? idx[j0 + lane] : (int)(j0 + lane);
-        st_b = b;
-        st_mass = mass ? mass[b] : mass_def;
-      }
       if (contiguous) {
+        ids(tt, st_b, st_mass);
         const int cnt = vs * n;
         dma_tile(XB(bi), x + j0 * n, cnt, lane);
         if ((cnt & 1) && lane == 0) st_tail = x[j0 * n + cnt - 1];
       } else {
-        for (int r = 0; r < vs; ++r) dma_row4(XB(bi) + r * n, x + (int64_t)__builtin_amdgcn_readlane(b, r) * n, n, lane);
+        st_b = pf_b;
+        st_mass = pf_mass;
+        const int b = (int)st_b;
+        // rows whose source and LDS slot are both 16-byte aligned take 16-byte granules (every row when n
+        // is even; the even instances' rows when n is odd), the others 4-byte ones
+        for (int r = 0; r < vs; ++r) {
+          const int64_t br = (int64_t)__builtin_amdgcn_readlane(b, r);
+          double* d = XB(bi) + r * xs;
+          const double* src = x + br * n;
+          if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(d)) & 15) == 0) dma_row16(d, src, n, lane);
+          else dma_row4(d, src, n, lane);
+        }
+        if (tt + gridDim.x < ntiles) ids(tt + gridDim.x, pf_b, pf_mass);
       }
     };
     auto finish_stage = [&](int64_t tt, int bi) {
@@ -1918,6 +1977,7 @@ __global__ __launch_bounds__(256) void cpl_eval_entry_kernel(const KParams K, in
       }
     };
     if (t < ntiles) {
+      if (!contiguous) ids(t, pf_b, pf_mass);
       stage(t, 0);
       finish_stage(t, 0);
     }
@@ -1949,7 +2009,7 @@ __global__ __launch_bounds__(256) void cpl_eval_entry_kernel(const KParams K, in
       for (int it = tid; it < items; it += CT) {
         if (it < pc) {
           const int r = it / N, i = it - r * N;  // (vector order)
-          const double* xr = X + r * n;
+          const double* xr = X + r * xs;
           const double* q = xr + 3 + 9 * i;
           const double F0 = q[0], F1 = q[1], F2 = q[2], p0 = q[3], p1 = q[4], p2 = q[5];
           const double n0 = q[6], n1 = q[7], n2 = q[8];
@@ -1987,7 +2047,7 @@ __global__ __launch_bounds__(256) void cpl_eval_entry_kernel(const KParams K, in
           // CentroidalStatics::GetValues (src/Constraints/CentroidalStatics.cpp:37-61) and the torque
           // rows' CoM pairs (:119-136), both in map order — statics_values_item's arithmetic
           const int r = it - pc;
-          const double* xr = X + r * n;
+          const double* xr = X + r * xs;
           double* st = SC + r * S;
           const double c0 = xr[0], c1 = xr[1], c2 = xr[2];
           double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0, v4 = 0.0, v5 = 0.0;
@@ -2013,7 +2073,7 @@ __global__ __launch_bounds__(256) void cpl_eval_entry_kernel(const KParams K, in
           for (int u = 0; u < 6; ++u) st[6 + u] = a[u];
         } else {
           const int r = it - pc - valid;
-          f_out[Rb[r]] = cost_value(K, X + r * n);
+          f_out[Rb[r]] = cost_value(K, X + r * xs);
         }
       }
       lds_barrier();
@@ -2025,7 +2085,7 @@ __global__ __launch_bounds__(256) void cpl_eval_entry_kernel(const KParams K, in
         int r = tid / h2, q2 = tid - r * h2;
         for (int e = tid; e < total; e += CT) {
           const uint2 o = reinterpret_cast<const uint2*>(op)[q2];
-          const double* Xr = X + r * n;
+          const double* Xr = X + r * xs;
           const double* Sr = SC + r * S;
           const double v0 = entry_value(o.x, Xr, Sr, CN), v1 = entry_value(o.y, Xr, Sr, CN);
           if (norms) {
@@ -2053,7 +2113,7 @@ __global__ __launch_bounds__(256) void cpl_eval_entry_kernel(const KParams K, in
         const int total = valid * n;
         int r = tid / n, q = tid - r * n;
         for (int e = tid; e < total; e += CT) {
-          const double* xr = X + r * n;
+          const double* xr = X + r * xs;
           double v;
           if (q < 3) {
             v = K.W_com * (xr[q] - K.com_ref[q]);
@@ -2566,7 +2626,8 @@ static size_t g_lds_budget = 0;    // 0 = per-kernel default (tile 32 KiB, pipel
 static int g_wg = 256;             // threads per tile workgroup (128 or 256)
 static int g_nt = 1;               // non-temporal output stores
 static int g_ablate = 0;           // measurement-only: 1 = skip the compute phase, 2 = skip the stores,
-                                   // 4 = the kind split's halves one after the other on the launch stream
+                                   // 4 = the kind split's halves one after the other on the launch stream,
+                                   // 8 = the split's halves sized to share every CU
 
 static size_t tile_budget() { return g_lds_budget ? g_lds_budget : 48 * 1024; }
 static size_t pipe_budget() { return g_lds_budget ? g_lds_budget : 48 * 1024; }
@@ -2638,21 +2699,23 @@ static int32_t plan_pipe(KParams& K, bool g, bool j, bool f, bool grad, size_t e
 // Entry kernel layout (doubles): x double buffer, masses [2][T], row bases [2][T] (int64), the cone
 // scratch [T][N][ENT_CS], the statics scratch [T][12]; T even, at most 64, the largest that fits the
 // LDS budget (no output image: 16-contact records keep 12-instance tiles in 48 KiB)
-static int32_t plan_entry(KParams& K, bool g, bool j, bool f, bool grad) {
+static int32_t plan_entry(KParams& K, bool g, bool j, bool f, bool grad, bool list = false) {
   K.want_g = g; K.want_j = j; K.want_f = f; K.want_grad = grad;
-  const size_t per = sizeof(double) * (size_t)(2 * K.n + 4 + K.N * ENT_PC + 12);
+  const size_t per = sizeof(double) * (size_t)(2 * ((K.n + 1) & ~1) + 4 + K.N * ENT_PC + 12);
   const size_t fixed = sizeof(double) * (size_t)(8 + 2 + (K.m + K.nnz + 1) / 2) + sizeof(CTab);
   // default budget: 80 KiB for records of 12+ contacts (two workgroups per CU with ~18-instance
   // tiles: 16-contact Ground 0.81 ms against 0.88 / 1.05 ms at 64 / 48 KiB, profiles/r4), else 48 KiB
-  const size_t budget = g_lds_budget ? g_lds_budget : (K.N >= 12 ? 80 * 1024 : 48 * 1024);
+  // (instance lists, the kind split's Ground half: 48 KiB — three loader waves per CU instead of two)
+  const size_t budget = g_lds_budget ? g_lds_budget : (K.N >= 12 && !list ? 80 * 1024 : 48 * 1024);
   int T = 64;
   while (T > 2 && (size_t)T * per + fixed > budget) T -= 2;
   if ((size_t)T * per + fixed > 160 * 1024) return fail(CPL_ERR_UNSUPPORTED, "problem too large for one LDS tile");
   K.T = T;
   K.logT = 0;
   auto up2 = [](int v) { return (v + 1) & ~1; };
-  K.offX1 = up2(T * K.n);
-  K.offMB = K.offX1 + up2(T * K.n);
+  const int xs = (K.n + 1) & ~1;  // (instance lists) even row stride
+  K.offX1 = up2(T * xs);
+  K.offMB = K.offX1 + up2(T * xs);
   K.offRB = K.offMB + 2 * T;
   K.offCS = K.offRB + 2 * T;                          // scratch [T][12 + ENT_PC N]
   K.offST = K.offCS + T * (12 + ENT_PC * K.N);        // constants (2), then the opcode tables
@@ -2666,9 +2729,9 @@ static bool use_entry(const KParams& K, int32_t flags) {
   const bool want = g_variant == VAR_ENTRY || g_variant == VAR_SPLIT || (g_variant == VAR_AUTO && K.N >= 12);
   return want && flags == 0 && (K.nnz % 2) == 0 && (K.env_kind == CPL_ENV_NONE || K.env_kind == CPL_ENV_GROUND);
 }
-// mixed batches split by kind: forced (variants 6, 7) or by default (as variant 6, the Superquadric half
-// staging its Jacobian rows in LDS: 1 048 576 x 16 in 3.34 ms against 3.89 with direct rows and 4.47 ms
-// interleaved, same process, profiles/r4)
+// mixed batches split by kind: forced (variants 6, 7) or by default (as variant 7, the Superquadric half
+// writing its Jacobian rows straight to the records, both halves on 48 KiB tiles: 1 048 576 x 16 in
+// 2.64 ms against 3.28 with LDS-staged rows and 4.49 ms interleaved, same process, profiles/r4)
 static bool use_split(const KParams& K, int32_t flags, int64_t batch) {
   return (g_variant == VAR_SPLIT || g_variant == VAR_SPLIT_JD || g_variant == VAR_AUTO) && flags == 0 &&
          K.env_kind == CPL_ENV_MIXED && batch <= 0x7fffffffLL;
@@ -2800,8 +2863,8 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
     hipLaunchKernelGGL(k_kind_write, dim3(nblk), dim3(PART_BLOCK), 0, stream, batch, d_env_tag, kl.blk_off, kl.idx_gr,
                        kl.idx_sq);
     KParams Kg = K, Ks = K;
-    if ((st = plan_entry(Kg, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr))) return st;
-    Ks.jdirect = (g_variant == VAR_SPLIT_JD && d_jac) ? 1 : 0;
+    if ((st = plan_entry(Kg, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr, true))) return st;
+    Ks.jdirect = ((g_variant == VAR_SPLIT_JD || g_variant == VAR_AUTO) && d_jac) ? 1 : 0;
     if ((st = plan_tile(Ks, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr))) return st;
     Kg.ablate = Ks.ablate = g_ablate & 3;
     const bool sequential = (g_ablate & 4) != 0;
@@ -2818,8 +2881,19 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
     const size_t lds_s = sizeof(double) * (size_t)(Ks.offRB + Ks.T);
     const int64_t ntg = (batch + Kg.T - 1) / Kg.T;
     const int64_t want = resident_blocks(reinterpret_cast<const void*>(ek), lds_g);
-    const unsigned grid_g = (unsigned)(ntg < want ? ntg : want);
-    const unsigned grid_s = (unsigned)((batch + Ks.T - 1) / Ks.T);  // every tile the list may hold
+    unsigned grid_g = (unsigned)(ntg < want ? ntg : want);
+    const int64_t nts = (batch + Ks.T - 1) / Ks.T;  // the most tiles the list may hold
+    int64_t want_s = resident_blocks(reinterpret_cast<const void*>(tk), lds_s);
+    if (g_ablate & 8) {  // (measurement) co-resident halves: one workgroup per CU left for the Ground half
+      int cus = 256;
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      const int64_t per = want_s / (cus > 0 ? cus : 256);
+      want_s = (int64_t)cus * (per > 1 ? per - 1 : 1);
+      if (ntg > cus) grid_g = (unsigned)cus;
+    }
+    const unsigned grid_s = (unsigned)(nts < want_s ? nts : want_s);
     const size_t nparts = (size_t)grid_g + (size_t)grid_s * 4;
     if (K.want_norms && (st = norm_workspace(stream, nparts, &ws))) return st;
     // the two halves on two streams (fork after the partition, join before the norms' finish): the
@@ -2966,7 +3040,10 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
 // cpl_ipm_judge_take judges the first trial.  The whole search runs in the kernel: the engine's
 // iteration no longer waits for the host between trials (one trial per graph launch and a flag read
 // back per trial cost ~55 us each; the lock-step batch makes as many trials as its slowest instance).
-template <int ENVK, bool RESTO, bool FIRST>
+// GF (with FIRST): the second-order corrections' re-solves read the KKT factors from the workspace in
+// global memory (kkt_wave_resolve_gg) — large batches, where the factors' LDS image bounded the waves
+// per CU; small batches keep the LDS copy (their re-solve latency is the iteration's)
+template <int ENVK, bool RESTO, bool FIRST, bool GF = false>
 __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, const LsBacktrackArgs A) {
   extern __shared__ __align__(16) double smem[];
   __shared__ double s_f;
@@ -3105,9 +3182,14 @@ __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, c
       if (FIRST && !RESTO && stage == S_SOC) {
         if (q > 0 && lane < m) csoc = a_soc * csoc + cons();
         double dwv, dyv;
-        kkt_wave_resolve_g<KNW, KM>(A.M + b * KNW * KNW, A.kkt_ws + b * kkt_ws_per(KNW, KM),
-                                    lane < KNW ? A.r1[b * KNW + lane] : 0.0, lane < KM ? -csoc : 0.0, kk, &dwv,
-                                    &dyv);
+        if (GF)
+          kkt_wave_resolve_gg<KNW, KM>(A.M + b * KNW * KNW, A.kkt_ws + b * kkt_ws_per(KNW, KM),
+                                       lane < KNW ? A.r1[b * KNW + lane] : 0.0, lane < KM ? -csoc : 0.0, kk, &dwv,
+                                       &dyv);
+        else
+          kkt_wave_resolve_g<KNW, KM>(A.M + b * KNW * KNW, A.kkt_ws + b * kkt_ws_per(KNW, KM),
+                                      lane < KNW ? A.r1[b * KNW + lane] : 0.0, lane < KM ? -csoc : 0.0, kk, &dwv,
+                                      &dyv);
         if (lane < nw) Dv[lane] = dwv;
         double r = INFINITY;  // cpl_ipm_max_step (primal)
         const double t = A.tau[b];
@@ -3175,6 +3257,8 @@ __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, c
   }
 }
 
+constexpr int64_t LS_GF_MIN = 2048;  // batches from this size re-solve from the factors in global memory
+
 int32_t ls_backtrack(const cpl_problem_desc* d, const LsBacktrackArgs& a, hipStream_t stream) {
   if (a.batch <= 0) return CPL_OK;
   if (a.batch > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "ls_backtrack: batch too large");
@@ -3193,18 +3277,21 @@ int32_t ls_backtrack(const cpl_problem_desc* d, const LsBacktrackArgs& a, hipStr
     return fail(CPL_ERR_INVALID_ARGUMENT, "ls_backtrack: the fused first trial needs a 47 x 30 system and its buffers");
   const size_t nL = sq ? (size_t)K.N * SQ_L : 0;
   size_t lds = sizeof(double) * ((size_t)a.n + a.m + a.nw + nL + 2);
-  if (first) lds = sizeof(double) * ((((size_t)a.n + a.m + 2 * (size_t)a.nw + nL + 1) & ~(size_t)1) + KktWave<47, 30>::LDS);
+  const bool gf = first && a.batch >= LS_GF_MIN;  // the re-solves' factors from global memory
+  if (first)
+    lds = sizeof(double) * ((((size_t)a.n + a.m + 2 * (size_t)a.nw + nL + 1) & ~(size_t)1) +
+                            (gf ? 2 * 47 : KktWave<47, 30>::LDS));
   using KernT = void (*)(const KParams, const LsBacktrackArgs);
-#define CPL_LS_KERNELS(R, F)                                                                                   \
-  {cpl_ls_backtrack_kernel<CPL_ENV_NONE, R, F>, cpl_ls_backtrack_kernel<CPL_ENV_GROUND, R, F>,                 \
-   cpl_ls_backtrack_kernel<CPL_ENV_SUPERQUADRIC, R, F>, cpl_ls_backtrack_kernel<CPL_ENV_MIXED, R, F>}
-  static const KernT table[3][4] = {CPL_LS_KERNELS(false, false), CPL_LS_KERNELS(true, false),
-                                    CPL_LS_KERNELS(false, true)};
+#define CPL_LS_KERNELS(R, F, G)                                                                                \
+  {cpl_ls_backtrack_kernel<CPL_ENV_NONE, R, F, G>, cpl_ls_backtrack_kernel<CPL_ENV_GROUND, R, F, G>,           \
+   cpl_ls_backtrack_kernel<CPL_ENV_SUPERQUADRIC, R, F, G>, cpl_ls_backtrack_kernel<CPL_ENV_MIXED, R, F, G>}
+  static const KernT table[4][4] = {CPL_LS_KERNELS(false, false, false), CPL_LS_KERNELS(true, false, false),
+                                    CPL_LS_KERNELS(false, true, false), CPL_LS_KERNELS(false, true, true)};
 #undef CPL_LS_KERNELS
   if (a.resto && (!a.pR || !a.nR || !a.dp || !a.dn || !a.wR || !a.st_p || !a.st_n))
     return fail(CPL_ERR_INVALID_ARGUMENT, "ls_backtrack: restoration search without its buffers");
-  hipLaunchKernelGGL(table[first ? 2 : (a.resto ? 1 : 0)][K.env_kind], dim3((unsigned)a.batch), dim3(64), lds, stream,
-                     K, a);
+  hipLaunchKernelGGL(table[first ? (gf ? 3 : 2) : (a.resto ? 1 : 0)][K.env_kind], dim3((unsigned)a.batch), dim3(64), lds,
+                     stream, K, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "cpl_ls_backtrack_kernel launch");
   return CPL_OK;
@@ -3275,7 +3362,7 @@ int32_t cpl_eval_batch_norms(const cpl_problem_desc* d, int64_t batch, const dou
 
 int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_threads, int32_t nt_stores,
                        int32_t ablate) {
-  if (ablate < 0 || ablate > 2 && ablate != 4) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
+  if (ablate < 0 || (ablate > 2 && ablate != 4 && ablate != 8)) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
   g_ablate = ablate;
   if (kernel_variant < VAR_AUTO || kernel_variant > VAR_SPLIT_JD) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown kernel variant");
   if (tile_lds_kb != 0 && (tile_lds_kb < 8 || tile_lds_kb > 160))

@@ -365,4 +365,26 @@ __device__ __forceinline__ void kkt_wave_resolve_g(const double* __restrict__ M,
                              dW, q1v, q2v, s1, s2, dwv, dyv);
 }
 
+// kkt_wave_resolve_g reading the factors straight from the instance's workspace (global memory, an L2
+// hit after the factorisation) instead of an LDS copy: the same operations on the same values (bitwise
+// the same step), with only the two NW-double scratch vectors in LDS (`scratch`) — for the line-search
+// kernel at large batches, whose 22 KiB LDS image of the factors bounded its waves per CU
+template <int NW, int MM>
+__device__ __forceinline__ void kkt_wave_resolve_gg(const double* __restrict__ M, const double* __restrict__ wsb,
+                                                    double q1v, double q2v, double* scratch, double* dwv,
+                                                    double* dyv) {
+  using W = KktWave<NW, MM>;
+  constexpr int NZ = W::NZ, ZS = W::ZS, NFAC = W::NFAC;
+  const double* QR = wsb;
+  const double* Z = QR + MM * NW;
+  const double* L = Z + NW * ZS;
+  const double* beta = L + NZ * NZ;
+  const double* cp = beta + MM;
+  double* s1 = scratch;
+  double* s2 = s1 + NW;
+  const double dW = wsb[NFAC];
+  wave_null_solve_mv<NW, MM>(QR, Z, L, beta, cp, [&](const double* xs, double* ys) { return mfma_matvec_g<NW>(M, xs, ys); },
+                             dW, q1v, q2v, s1, s2, dwv, dyv);
+}
+
 }  // namespace cpl

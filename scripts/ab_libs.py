@@ -27,6 +27,7 @@ ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--libs", default="centroidalplanner_amd/libcpl_mi355x.so,build/libcpl_old.so")
 ap.add_argument("--tuning", default="", help="variant:lds_kb:wg:nt passed to every library's cpl_set_tuning")
 ap.add_argument("--no-norms", action="store_true", help="time the eval kernel without the fused residual norms")
+ap.add_argument("--tags", default="", help="mixed configs: all_sq | all_ground (every instance of one kind)")
 args = ap.parse_args()
 
 libs = {}
@@ -46,6 +47,14 @@ for tag in args.libs.split(","):
 cfg = CONFIGS[args.config]
 B = args.batch or cfg.batch
 prob, x, mass, tag = config_inputs(cfg, B)
+if args.tags:  # one kind only, through the mixed launch (the kind split's halves alone)
+    import numpy as np
+
+    from centroidalplanner_amd.workload import generate
+
+    kind = "superquadric" if args.tags == "all_sq" else "ground"
+    x, _, _ = generate(cfg.n_contacts, kind, B, 4242)
+    tag = np.full(B, 2 if kind == "superquadric" else 1, np.uint8)
 dev = torch.device("cuda:0")
 xt, mt = torch.tensor(x, device=dev), torch.tensor(mass, device=dev)
 tt = None if tag is None else torch.tensor(tag, device=dev)
