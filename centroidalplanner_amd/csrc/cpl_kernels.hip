@@ -1338,11 +1338,14 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
   const int64_t count = LIST ? (int64_t)*d_count : batch;
   NormAcc nacc;
   nacc.init(tid, WG, m);
-  // LIST: a persistent grid (the resident workgroups) walking the list's tiles blockIdx, + grid, ...
-  // (the list's length is known on the device only); otherwise this workgroup's tile, once
-  const int64_t ntiles = (count + T - 1) / T;
-  for (int64_t tl = blockIdx.x; !LIST || tl < ntiles; tl += gridDim.x) {
-  const int64_t b0 = tl * T;
+  // LIST: one workgroup per tile the list may hold (the list's length is known on the device only; a
+  // persistent walk over the list's tiles measured slower: 149-155 VGPRs against 114, three waves per
+  // SIMD instead of four — profiles/r4/ab_split5)
+  const int64_t b0 = (int64_t)blockIdx.x * T;
+  if (LIST && b0 >= count) {  // past the list's tiles: zero partials
+    if (K.want_norms) partial_norms_waves(nacc, norms_ws + NORM_HDR);
+    return;
+  }
   const int valid = (int)((count - b0) < T ? (count - b0) : T);
   long long* rowb = reinterpret_cast<long long*>(smem + K.offRB);  // (LIST) instance of each tile row
   auto inst = [&](int r) -> int64_t { return LIST ? (int64_t)rowb[r] : b0 + r; };
@@ -1492,7 +1495,7 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
   // copy-out's instead of after them on every workgroup's tail
   if (K.want_norms) {
     nacc.add_tile(Gt, valid * m, tid, WG, m);
-    if (!LIST) partial_norms_waves(nacc, norms_ws + NORM_HDR);
+    partial_norms_waves(nacc, norms_ws + NORM_HDR);
   }
   if (K.ablate != 2 && LIST) {  // records written in place: row by row (g, jac rows are 16-byte aligned)
     if (K.want_g) copy_out_rows<WG, NT>(g_out, rowb, Gt, m, valid, tid);
@@ -1511,11 +1514,6 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
     if (K.want_j && !JD) copy_out<WG, NT>(jac_out + b0 * nnz, Jt, valid * nnz, tid);
     if (K.want_grad) copy_out<WG, NT>(grad_out + b0 * n, Dt, valid * n, tid);
   }
-  if (!LIST) break;
-  if (tl + gridDim.x < ntiles) __syncthreads();  // the next tile overwrites the LDS image
-  }  // tiles
-  // (LIST) the residual partials after the tiles, one pair per wave (zeros from workgroups with none)
-  if (LIST && K.want_norms) partial_norms_waves(nacc, norms_ws + NORM_HDR);
 }
 
 
@@ -2627,7 +2625,7 @@ static int g_wg = 256;             // threads per tile workgroup (128 or 256)
 static int g_nt = 1;               // non-temporal output stores
 static int g_ablate = 0;           // measurement-only: 1 = skip the compute phase, 2 = skip the stores,
                                    // 4 = the kind split's halves one after the other on the launch stream,
-                                   // 8 = the split's halves sized to share every CU
+                                   // 8 = the split's Ground half issued before the Superquadric half
 
 static size_t tile_budget() { return g_lds_budget ? g_lds_budget : 48 * 1024; }
 static size_t pipe_budget() { return g_lds_budget ? g_lds_budget : 48 * 1024; }
@@ -2881,19 +2879,8 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
     const size_t lds_s = sizeof(double) * (size_t)(Ks.offRB + Ks.T);
     const int64_t ntg = (batch + Kg.T - 1) / Kg.T;
     const int64_t want = resident_blocks(reinterpret_cast<const void*>(ek), lds_g);
-    unsigned grid_g = (unsigned)(ntg < want ? ntg : want);
-    const int64_t nts = (batch + Ks.T - 1) / Ks.T;  // the most tiles the list may hold
-    int64_t want_s = resident_blocks(reinterpret_cast<const void*>(tk), lds_s);
-    if (g_ablate & 8) {  // (measurement) co-resident halves: one workgroup per CU left for the Ground half
-      int cus = 256;
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      const int64_t per = want_s / (cus > 0 ? cus : 256);
-      want_s = (int64_t)cus * (per > 1 ? per - 1 : 1);
-      if (ntg > cus) grid_g = (unsigned)cus;
-    }
-    const unsigned grid_s = (unsigned)(nts < want_s ? nts : want_s);
+    const unsigned grid_g = (unsigned)(ntg < want ? ntg : want);
+    const unsigned grid_s = (unsigned)((batch + Ks.T - 1) / Ks.T);  // every tile the list may hold
     const size_t nparts = (size_t)grid_g + (size_t)grid_s * 4;
     if (K.want_norms && (st = norm_workspace(stream, nparts, &ws))) return st;
     // the two halves on two streams (fork after the partition, join before the norms' finish): the
@@ -2905,10 +2892,15 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
       if (e == hipSuccess) e = hipStreamWaitEvent(ss.side, ss.fork, 0);
       if (e != hipSuccess) return hip_fail(e, "mixed split fork");
     }
-    hipLaunchKernelGGL(tk, dim3(grid_s), dim3(256), lds_s, stream, Ks, batch, d_x, d_mass, d_env_tag, kl.idx_sq,
-                       kl.counts + 1, d_g, d_jac, d_f, d_grad, ws ? ws + 2 * (size_t)grid_g : nullptr);
+    const bool ground_first = (g_ablate & 8) != 0;  // (measurement) the Ground half's launch issued first
+    auto launch_s = [&]() {
+      hipLaunchKernelGGL(tk, dim3(grid_s), dim3(256), lds_s, stream, Ks, batch, d_x, d_mass, d_env_tag, kl.idx_sq,
+                         kl.counts + 1, d_g, d_jac, d_f, d_grad, ws ? ws + 2 * (size_t)grid_g : nullptr);
+    };
+    if (!ground_first) launch_s();
     hipLaunchKernelGGL(ek, dim3(grid_g), dim3(256), lds_g, sequential ? stream : ss.side, Kg, batch, d_x, d_mass,
                        kl.idx_gr, kl.counts, d_g, d_jac, d_f, d_grad, ws);
+    if (ground_first) launch_s();
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "mixed split launch");
     if (!sequential) {
@@ -3362,7 +3354,7 @@ int32_t cpl_eval_batch_norms(const cpl_problem_desc* d, int64_t batch, const dou
 
 int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_threads, int32_t nt_stores,
                        int32_t ablate) {
-  if (ablate < 0 || (ablate > 2 && ablate != 4 && ablate != 8)) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
+  if (ablate < 0 || (ablate > 2 && ablate != 4 && ablate != 8 && ablate != 12)) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
   g_ablate = ablate;
   if (kernel_variant < VAR_AUTO || kernel_variant > VAR_SPLIT_JD) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown kernel variant");
   if (tile_lds_kb != 0 && (tile_lds_kb < 8 || tile_lds_kb > 160))

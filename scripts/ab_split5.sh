@@ -10,4 +10,3 @@ python -u scripts/ab_libs.py --config mixed16 --rounds 3 --reps 5 --tuning 7:48:
 python -u scripts/ab_libs.py --config mixed16 --batch 524288 --tags all_ground --rounds 3 --reps 5 --tuning 7:48:256:1 --libs $L > "$out/allground_7_48.jsonl" || exit $?
 python -u scripts/ab_libs.py --config mixed16 --batch 524288 --tags all_sq --rounds 3 --reps 5 --tuning 7:48:256:1 --libs $L > "$out/allsq_7_48.jsonl" || exit $?
 python -u scripts/ab_kernels.py --config mixed16 --rounds 3 --reps 5 --variants 0:0:256:1,7:48:256:1,6:48:256:1,3:0:256:1 --norms > "$out/mixed16_default.jsonl"
-python -u scripts/ab_kernels.py --config mixed16 --rounds 3 --reps 5 --variants 7:48:256:1,7:48:256:1:8,7:48:256:1:4 --norms > "$out/mixed16_coresident.jsonl"

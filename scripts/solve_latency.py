@@ -22,6 +22,7 @@ ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--only", default="", help="run one case, e.g. limited-memory:1 (for a kernel trace)")
 ap.add_argument("--ls-kernel", type=int, default=2, help="the engine's ls_kernel option (0 / 1 / 2)")
 ap.add_argument("--variant", type=int, default=0, help="eval kernel variant (cpl_set_tuning), 0 = auto")
+ap.add_argument("--no-graph", action="store_true", help="launch the iteration's kernels directly (no HIP graph)")
 args = ap.parse_args()
 if args.variant:
     from centroidalplanner_amd import _abi  # noqa: E402
@@ -39,11 +40,13 @@ if args.only:
 for hessian, B in cases:
     if True:
         Xt, mt = torch.tensor(X0[:B], device=dev), torch.tensor(mass[:B], device=dev)
-        r = batch_ipm_solve(prob, Xt, mt, max_iter=1000, hessian=hessian, ls_kernel=args.ls_kernel)  # warm: engine + graphs
+        r = batch_ipm_solve(prob, Xt, mt, max_iter=1000, hessian=hessian, ls_kernel=args.ls_kernel,
+                            graph=not args.no_graph)  # warm: engine + graphs
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.reps):
-            r = batch_ipm_solve(prob, Xt, mt, max_iter=1000, hessian=hessian, ls_kernel=args.ls_kernel)
+            r = batch_ipm_solve(prob, Xt, mt, max_iter=1000, hessian=hessian, ls_kernel=args.ls_kernel,
+                            graph=not args.no_graph)
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / args.reps
         its = r.iterations.double()
