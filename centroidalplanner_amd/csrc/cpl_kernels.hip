@@ -2625,7 +2625,9 @@ static int g_wg = 256;             // threads per tile workgroup (128 or 256)
 static int g_nt = 1;               // non-temporal output stores
 static int g_ablate = 0;           // measurement-only: 1 = skip the compute phase, 2 = skip the stores,
                                    // 4 = the kind split's halves one after the other on the launch stream,
-                                   // 8 = the split's Ground half issued before the Superquadric half
+                                   // 8 = the split's Ground half issued before the Superquadric half,
+                                   // 16 = the split's Ground list at 48 KiB (default 40), 32 = its
+                                   // Superquadric tiles at 40 KiB (default 48)
 
 static size_t tile_budget() { return g_lds_budget ? g_lds_budget : 48 * 1024; }
 static size_t pipe_budget() { return g_lds_budget ? g_lds_budget : 48 * 1024; }
@@ -2639,7 +2641,9 @@ static bool use_pipe(const KParams& K) {
 // size_without_j: the tile size is chosen as if the Jacobian were written straight to the records
 // (the layouts that cannot, SoA, then stage it in a larger LDS image) so that every layout of a batch
 // runs the same tiles and the fused per-tile residual partials reduce in the same order
-static int32_t plan_tile(KParams& K, bool g, bool j, bool f, bool grad, int t_max = 64, bool size_without_j = false) {
+static int32_t plan_tile(KParams& K, bool g, bool j, bool f, bool grad, int t_max = 64, bool size_without_j = false,
+                         size_t budget = 0) {
+  if (!budget) budget = tile_budget();
   K.want_g = g; K.want_j = j; K.want_f = f; K.want_grad = grad;
   const bool sq = K.env_kind == CPL_ENV_SUPERQUADRIC || K.env_kind == CPL_ENV_MIXED;
   K.LR = K.N * SQ_L + 1;  // odd instance stride of the SQ scratch: conflict-free LDS banks
@@ -2649,7 +2653,7 @@ static int32_t plan_tile(KParams& K, bool g, bool j, bool f, bool grad, int t_ma
   const size_t fixed = sizeof(double) * 72 + sizeof(CTab);  // index lists + parameter table
   int T = 64, logT = 6;
   while (T > t_max) { T >>= 1; --logT; }
-  while (T > 2 && (size_t)T * per_t + fixed > tile_budget()) { T >>= 1; --logT; }
+  while (T > 2 && (size_t)T * per_t + fixed > budget) { T >>= 1; --logT; }
   // (T >= 2 is even, so every tile of every record array starts on a 16-byte boundary; below 8 the
   // tile boundaries no longer fall on 128-byte lines — the price of more resident workgroups for
   // the large VALU-bound records)
@@ -2697,14 +2701,15 @@ static int32_t plan_pipe(KParams& K, bool g, bool j, bool f, bool grad, size_t e
 // Entry kernel layout (doubles): x double buffer, masses [2][T], row bases [2][T] (int64), the cone
 // scratch [T][N][ENT_CS], the statics scratch [T][12]; T even, at most 64, the largest that fits the
 // LDS budget (no output image: 16-contact records keep 12-instance tiles in 48 KiB)
-static int32_t plan_entry(KParams& K, bool g, bool j, bool f, bool grad, bool list = false) {
+static int32_t plan_entry(KParams& K, bool g, bool j, bool f, bool grad, bool list = false, size_t list_budget = 0) {
   K.want_g = g; K.want_j = j; K.want_f = f; K.want_grad = grad;
   const size_t per = sizeof(double) * (size_t)(2 * ((K.n + 1) & ~1) + 4 + K.N * ENT_PC + 12);
   const size_t fixed = sizeof(double) * (size_t)(8 + 2 + (K.m + K.nnz + 1) / 2) + sizeof(CTab);
   // default budget: 80 KiB for records of 12+ contacts (two workgroups per CU with ~18-instance
   // tiles: 16-contact Ground 0.81 ms against 0.88 / 1.05 ms at 64 / 48 KiB, profiles/r4), else 48 KiB
-  // (instance lists, the kind split's Ground half: 48 KiB — three loader waves per CU instead of two)
-  const size_t budget = g_lds_budget ? g_lds_budget : (K.N >= 12 && !list ? 80 * 1024 : 48 * 1024);
+  // (instance lists, the kind split's Ground half: list_budget, 40 KiB — more loader waves per CU)
+  const size_t budget = g_lds_budget ? g_lds_budget
+                                     : (list && list_budget ? list_budget : (K.N >= 12 && !list ? 80 * 1024 : 48 * 1024));
   int T = 64;
   while (T > 2 && (size_t)T * per + fixed > budget) T -= 2;
   if ((size_t)T * per + fixed > 160 * 1024) return fail(CPL_ERR_UNSUPPORTED, "problem too large for one LDS tile");
@@ -2861,9 +2866,15 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
     hipLaunchKernelGGL(k_kind_write, dim3(nblk), dim3(PART_BLOCK), 0, stream, batch, d_env_tag, kl.blk_off, kl.idx_gr,
                        kl.idx_sq);
     KParams Kg = K, Ks = K;
-    if ((st = plan_entry(Kg, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr, true))) return st;
+    // the Ground list at 40 KiB (1 048 576 x 16 mixed: 2.600 against 2.626 ms at 48 KiB, profiles/r4/
+    // split_lds; measurement: ablation 16 gives it 48 KiB, 32 the Superquadric tiles 40 KiB)
+    if ((st = plan_entry(Kg, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr, true,
+                         (g_ablate & 16) ? 48 * 1024 : 40 * 1024)))
+      return st;
     Ks.jdirect = ((g_variant == VAR_SPLIT_JD || g_variant == VAR_AUTO) && d_jac) ? 1 : 0;
-    if ((st = plan_tile(Ks, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr))) return st;
+    if ((st = plan_tile(Ks, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr, 64, false,
+                        (g_ablate & 32) ? 40 * 1024 : 0)))
+      return st;
     Kg.ablate = Ks.ablate = g_ablate & 3;
     const bool sequential = (g_ablate & 4) != 0;
     using EntryT = void (*)(const KParams, int64_t, const double*, const double*, const int32_t*, const int32_t*,
@@ -3354,7 +3365,7 @@ int32_t cpl_eval_batch_norms(const cpl_problem_desc* d, int64_t batch, const dou
 
 int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_threads, int32_t nt_stores,
                        int32_t ablate) {
-  if (ablate < 0 || (ablate > 2 && ablate != 4 && ablate != 8 && ablate != 12)) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
+  if (ablate < 0 || (ablate > 2 && (ablate & ~(4 | 8 | 16 | 32)))) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
   g_ablate = ablate;
   if (kernel_variant < VAR_AUTO || kernel_variant > VAR_SPLIT_JD) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown kernel variant");
   if (tile_lds_kb != 0 && (tile_lds_kb < 8 || tile_lds_kb > 160))

@@ -759,13 +759,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   if (b >= batch) return;
   double* QR = sm;                 // [MM][NW]
   double* Z = QR + MM * NW;        // [NW][ZS]
-  double* L = Z + NW * ZS;         // [NZ][NZ]
-  double* beta = L + NZ * NZ;      // [MM]
+  double* L = Z + NW * ZS;         // [NLP]: the lower triangle packed by rows
+  double* beta = L + W::NLP;       // [MM]
   double* cp = beta + MM;          // [NP + 1]
   double* s1 = sm + NFAC;          // [NW] scratch
   double* s2 = s1 + NW;            // [NW] scratch
-  double* dwl = s2 + NW;           // [NW] dw (broadcast copy)
-  double* dyl = dwl + NW;          // [MM] dy (broadcast copy)
+  // the refinement's broadcast copies of dw and dy share the scratch slots (dy is read before the M dw
+  // product writes s1, dw is not written by it)
+  double* dwl = s2;                // [NW] dw (broadcast copy)
+  double* dyl = s1;                // [MM] dy (broadcast copy)
   const double* M = Mg + b * NW * NW;
   const double* Ab = Ag + b * MM * NW;
   double* wsb = ws + b * kkt_ws_per(NW, MM);
@@ -1011,7 +1013,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     __builtin_amdgcn_wave_barrier();
   }
   // ---- reduced Hessian Hr = Z^T (M Z): M Z a lane per row through the global workspace (L2),
-  // Hr's upper triangle a lane per entry, mirrored into L; the Cholesky keeps the unshifted rows in
+  // Hr's upper triangle a lane per entry, into L's packed lower triangle; the Cholesky keeps the unshifted rows in
   // registers for its delta_w retries
   double dW = 0.0;
   int32_t inf = 0;
@@ -1022,7 +1024,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     // [k = l >> 4], B lane l = B[k = l >> 4][l & 15], D lane l reg q = D[(l >> 4) + 4q][l & 15]),
     // padded to 16-row / 16-column tiles and 4-deep k-steps.  W's accumulator register q of row
     // block kb / 4 is exactly Hr's B fragment of k-step kb, so W never leaves the registers; Z^T's
-    // A fragment of k-step kb is Z's B fragment.  Hr's upper triangle is mirrored into L.
+    // A fragment of k-step kb is Z's B fragment.  Hr's upper triangle goes to L's packed lower triangle.
     static_assert(NW <= 48 && NZ <= 32, "MFMA tiling of Z^T M Z: nw <= 48, nz <= 32");
     constexpr int KB = (NW + 3) / 4;    // k-steps
     constexpr int RB = (NW + 15) / 16;  // row blocks of W
@@ -1059,10 +1061,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int ar = 16 * ab + lk + 4 * q, c = 16 * cb + li;
-          if (ar < NZ && c < NZ && ar <= c) {
-            L[ar * NZ + c] = h[q];
-            L[c * NZ + ar] = h[q];
-          }
+          if (ar < NZ && c < NZ && ar <= c) L[c * (c + 1) / 2 + ar] = h[q];  // Hr(c, ar), c >= ar
         }
       }
     __threadfence_block();
@@ -1077,7 +1076,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     const int lr = lane < NZ ? lane : 0;
     double hs[NZ], a[NZ];
 #pragma unroll
-    for (int c = 0; c < NZ; ++c) hs[c] = L[lr * NZ + c];
+    for (int c = 0; c < NZ; ++c) hs[c] = c <= lr ? L[lr * (lr + 1) / 2 + c] : L[c * (c + 1) / 2 + lr];
     #pragma unroll 1
     for (int attempt = 0; attempt < 64; ++attempt) {
 #pragma unroll
@@ -1090,7 +1089,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     __builtin_amdgcn_wave_barrier();
     if (lane < NZ) {
 #pragma unroll
-      for (int c = 0; c < NZ; ++c) L[lane * NZ + c] = a[c];
+      for (int c = 0; c < NZ; ++c)
+        if (c <= lane) L[lane * (lane + 1) / 2 + c] = a[c];
     }
     __builtin_amdgcn_wave_barrier();
   }

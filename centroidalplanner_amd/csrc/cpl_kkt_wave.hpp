@@ -11,8 +11,8 @@
 
 namespace cpl {
 
-// Workspace layout per instance (doubles): Q [nw*nw] | QR [m*nw] (R's diagonal on its diagonal) |
-// L [nz*nz] | scalars [4]
+// Workspace size per instance (doubles): Q [nw*nw] | QR [m*nw] (R's diagonal on its diagonal) |
+// L [nz*nz] | scalars [4] (the one-wave kernel's factor image, smaller, fits inside it)
 __host__ __device__ inline int64_t kkt_ws_per(int nw, int m) {
   const int nz = nw - m;
   return (int64_t)nw * nw + (int64_t)m * nw + (int64_t)nz * nz + 4;
@@ -34,22 +34,24 @@ __host__ __device__ inline int64_t kkt_ws_per(int nw, int m) {
 //   * W = M Z and Z^T W on the FP64 matrix cores (v_mfma_f64_16x16x4f64), W's accumulators reused
 //     as Z^T W's B fragments; M's fragments stay in registers for every later M product;
 //   * the inertia-correcting Cholesky and the triangular sweeps with the rows in registers.
-// LDS image QR | Z | L | beta | cp | 3 nw + m vector slots: 21.7 KiB at nw = 47, m = 30, i.e.
-// seven systems per CU.  Factor workspace (mode 1): QR | Z | L | beta | cp | dW, dC.
+// LDS image QR | Z | L (the lower triangle, packed by rows) | beta | cp | 2 nw vector slots: 19.5 KiB
+// at nw = 47, m = 30, i.e. eight systems per CU — as many as its registers allow (21.7 KiB and seven
+// with the full square L and 3 nw + m slots).  Factor workspace (mode 1): the image's factors, dW, dC.
 // ==========================================================================================
 template <int NW, int MM>
 struct KktWave {
   static constexpr int NZ = NW - MM;
   static constexpr int ZS = NZ + (NZ & 1);          // Z row stride: even, so rows are 16-byte aligned
   static constexpr int NP = MM / 2;                 // reflector pairs (a lone last one when MM is odd)
-  static constexpr int NFAC = MM * NW + NW * ZS + NZ * NZ + MM + NP + 1;
-  static constexpr int LDS = ((NFAC + 3 * NW + MM) + 1) & ~1;
+  static constexpr int NLP = NZ * (NZ + 1) / 2;     // L's packed lower triangle: L(r, c) at r (r + 1) / 2 + c
+  static constexpr int NFAC = MM * NW + NW * ZS + NLP + MM + NP + 1;
+  static constexpr int LDS = ((NFAC + 2 * NW) + 1) & ~1;
   static_assert(NW <= 64 && MM <= NW, "one wave per system: nw <= 64");
 };
 
 __host__ __device__ inline int kktw_lds_doubles(int nw, int m) {
   const int nz = nw - m, zs = nz + (nz & 1);
-  return ((m * nw + nw * zs + nz * nz + m + m / 2 + 1 + 3 * nw + m) + 1) & ~1;
+  return ((m * nw + nw * zs + nz * (nz + 1) / 2 + m + m / 2 + 1 + 2 * nw) + 1) & ~1;
 }
 
 // two wave sums, their DPP chains interleaved (the result in every lane)
@@ -145,6 +147,29 @@ __device__ __forceinline__ double wave_trsv_reg(const double* T, int si, int sk,
 #pragma unroll
   for (int k = 0; k < N; ++k) t[k] = T[lr * si + k * sk];
   const double inv = act ? 1.0 / D[lr * sd] : 0.0;
+#pragma unroll
+  for (int s = 0; s < N; ++s) {
+    const int i = LOWER ? s : N - 1 - s;
+    const double xi = wave_bcast(x, i) * wave_bcast(inv, i);
+    if (lane == i) x = xi;
+    if (LOWER ? (act && lane > i) : (lane < i)) x -= t[i] * xi;
+  }
+  return act ? x : 0.0;
+}
+
+// wave_trsv_reg over a lower triangle packed by rows (Lp: L(r, c) at r (r + 1) / 2 + c, c <= r):
+// L x = b (LOWER) or L^T x = b.  The same operands in the same order as wave_trsv_reg over the full
+// square (bitwise the same x); the entries a lane loads past its row's triangle stay inside the
+// array and are never used (the masked updates).
+template <int N, bool LOWER>
+__device__ __forceinline__ double wave_trsv_packed(const double* Lp, double x) {
+  const int lane = threadIdx.x & 63;
+  const bool act = lane < N;
+  const int lr = act ? lane : 0;
+  double t[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) t[k] = LOWER ? Lp[lr * (lr + 1) / 2 + k] : Lp[k * (k + 1) / 2 + lr];
+  const double inv = act ? 1.0 / Lp[lr * (lr + 1) / 2 + lr] : 0.0;
 #pragma unroll
   for (int s = 0; s < N; ++s) {
     const int i = LOWER ? s : N - 1 - s;
@@ -283,8 +308,8 @@ __device__ __forceinline__ void wave_null_solve_mv(const double* QR, const doubl
       for (int r = 0; r < NW; ++r) a[r & 3] += Z[r * ZS + lane] * s1[r];
       rz = (a[0] + a[1]) + (a[2] + a[3]);
     }
-    const double yz = wave_trsv_reg<NZ, true>(L, NZ, 1, L, NZ + 1, rz);   // L y = rz
-    const double pz = wave_trsv_reg<NZ, false>(L, 1, NZ, L, NZ + 1, yz);  // L^T p_z = y
+    const double yz = wave_trsv_packed<NZ, true>(L, rz);   // L y = rz
+    const double pz = wave_trsv_packed<NZ, false>(L, yz);  // L^T p_z = y
     __builtin_amdgcn_wave_barrier();
     if (lane < NZ) s2[lane] = pz;
     __builtin_amdgcn_wave_barrier();
@@ -331,7 +356,7 @@ __device__ __forceinline__ void kkt_wave_resolve(const double* __restrict__ M, c
   double* QR = sm;
   double* Z = QR + MM * NW;
   double* L = Z + NW * ZS;
-  double* beta = L + NZ * NZ;
+  double* beta = L + W::NLP;
   double* cp = beta + MM;
   double* s1 = sm + NFAC;
   double* s2 = s1 + NW;
@@ -354,7 +379,7 @@ __device__ __forceinline__ void kkt_wave_resolve_g(const double* __restrict__ M,
   double* QR = sm;
   double* Z = QR + MM * NW;
   double* L = Z + NW * ZS;
-  double* beta = L + NZ * NZ;
+  double* beta = L + W::NLP;
   double* cp = beta + MM;
   double* s1 = sm + NFAC;
   double* s2 = s1 + NW;
@@ -378,7 +403,7 @@ __device__ __forceinline__ void kkt_wave_resolve_gg(const double* __restrict__ M
   const double* QR = wsb;
   const double* Z = QR + MM * NW;
   const double* L = Z + NW * ZS;
-  const double* beta = L + NZ * NZ;
+  const double* beta = L + W::NLP;
   const double* cp = beta + MM;
   double* s1 = scratch;
   double* s2 = s1 + NW;

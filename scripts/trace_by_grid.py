@@ -13,7 +13,8 @@ from collections import defaultdict
 rows = list(csv.DictReader(open(sys.argv[1])))
 agg = defaultdict(list)
 for r in rows:
-    key = (r["Kernel_Name"].split("(")[0], int(r["Grid_Size_X"]), int(r["Workgroup_Size_X"]))
+    key = (r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0], int(r["Grid_Size_X"]),
+           int(r["Workgroup_Size_X"]))
     agg[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 out = [("kernel", "grid_x", "workgroup_x", "calls", "mean_us", "min_us", "max_us", "total_ms")]
 for (k, g, w), d in sorted(agg.items(), key=lambda t: -sum(t[1])):
