@@ -820,6 +820,200 @@ __global__ __launch_bounds__(256) void k_lbfgs(int64_t B, int m, int nf, int nw,
   }
 }
 
+// k_lbfgs for nf <= 64 with one wave per instance (four instances per workgroup) and the pair vectors
+// in registers (lane k holds entry k of every stored pair): the same operations in the same order as
+// k_lbfgs (the workgroup form, NFX = 64) — the J^T y row partials in its four row groups summed in its order, its block dots as
+// 0 + the wave sum, its recursion — so bitwise the same model, without its barriers and idle waves
+// (that form ran its recursion on one wave of four and kept 15.5 KiB of LDS per instance).
+constexpr int LBW_WAVES = 4;
+__global__ __launch_bounds__(64 * LBW_WAVES) void k_lbfgs_wave(
+    int64_t B, int m, int nf, int nw, int nnz_rec, const int32_t* __restrict__ amap, const uint8_t* __restrict__ act,
+    const double* __restrict__ w_old, const double* __restrict__ w_new, const double* __restrict__ y,
+    const double* __restrict__ dy, const double* __restrict__ alpha, const double* __restrict__ gw_old,
+    const double* __restrict__ J_old, const double* __restrict__ grad_new, const int32_t* __restrict__ free_idx, int n,
+    const double* __restrict__ J_new, double* __restrict__ lm_s, double* __restrict__ lm_y, uint8_t* __restrict__ lm_cnt,
+    uint8_t* __restrict__ lm_skip, const uint8_t* __restrict__ failed, double* __restrict__ Hq) {
+  extern __shared__ double ynw[];  // [LBW_WAVES][m]
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t b = (int64_t)blockIdx.x * LBW_WAVES + wv;
+  if (b >= B || !act[b]) return;
+  double* yn = ynw + (size_t)wv * m;
+  const double al = alpha[b];
+  for (int r = lane; r < m; r += 64) yn[r] = y[b * m + r] + al * dy[b * m + r];
+  const int cnt = lm_cnt[b], skipped = lm_skip[b] + 1;
+  __builtin_amdgcn_wave_barrier();
+  const int shift = cnt == LM_HIST ? 1 : 0, last = cnt - shift;
+  double* gs = lm_s + b * (int64_t)LM_HIST * nf;
+  double* gy = lm_y + b * (int64_t)LM_HIST * nf;
+  const int k = lane;
+  const bool hk = k < nf;
+  double Ps[LM_HIST], Py[LM_HIST];
+  {  // J_free^T y at both points: the workgroup form's four row groups (rows part, part + 4, ...), each in its
+     // eight-row batches, the group partials summed in order
+    constexpr int PARTS = 4;
+    const double* jnb = J_new + b * (int64_t)nnz_rec;
+    const double* job = J_old + b * (int64_t)nnz_rec;
+    double pn[PARTS], po[PARTS];
+#pragma unroll
+    for (int part = 0; part < PARTS; ++part) {
+      double jn = 0.0, jo = 0.0;
+      const int R = m > part ? (m - part + PARTS - 1) / PARTS : 0;
+      if (hk) {
+        for (int t0 = 0; t0 < R; t0 += 8) {
+          int qv[8];
+          double anv[8], aov[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) qv[u] = t0 + u < R ? amap[(part + (t0 + u) * PARTS) * nf + k] : -1;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            anv[u] = qv[u] >= 0 ? jnb[qv[u]] : 1.0;
+            aov[u] = qv[u] >= 0 ? job[qv[u]] : 1.0;
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            if (qv[u] == -1) continue;
+            double an = anv[u], ao = aov[u];
+            if (qv[u] >= 0) {
+              an = an == an ? an : 0.0;
+              ao = ao == ao ? ao : 0.0;
+            }
+            const int r = part + (t0 + u) * PARTS;
+            jn += an * yn[r];
+            jo += ao * yn[r];
+          }
+        }
+      }
+      pn[part] = jn;
+      po[part] = jo;
+    }
+    double jn = pn[0], jo = po[0];
+#pragma unroll
+    for (int q = 1; q < PARTS; ++q) {
+      jn += pn[q];
+      jo += po[q];
+    }
+#pragma unroll
+    for (int j = 0; j < LM_HIST; ++j) {
+      Ps[j] = 0.0;
+      Py[j] = 0.0;
+      if (hk && j < last) {
+        Ps[j] = gs[(j + shift) * nf + k];
+        Py[j] = gy[(j + shift) * nf + k];
+      }
+    }
+    if (hk) {
+      const double sl = w_new[b * nw + k] - w_old[b * nw + k];
+      const double gn = grad_new ? grad_new[b * n + free_idx[k]] : 0.0;
+      const double yl = (gn + jn) - (gw_old[b * nw + k] + jo);
+#pragma unroll
+      for (int j = 0; j < LM_HIST; ++j)
+        if (j == last) {
+          Ps[j] = sl;
+          Py[j] = yl;
+        }
+    }
+  }
+  // the newest pair (slot `last`, wave-uniform) and the three dots as the workgroup form's block_dot: 0 + the
+  // wave sum of the lanes' products (lanes >= nf contribute 0)
+  double sL = 0.0, yL = 0.0;
+#pragma unroll
+  for (int j = 0; j < LM_HIST; ++j)
+    if (j == last) {
+      sL = Ps[j];
+      yL = Py[j];
+    }
+  auto wdot = [&](double a, double c) {
+    double v = 0.0;
+    if (hk) v += a * c;
+    return 0.0 + wave_sum(v);
+  };
+  const double sy = wdot(sL, yL);
+  const double ss = wdot(sL, sL);
+  const double yy = wdot(yL, yL);
+  double* hc = Hq + b * (int64_t)LMC(nf);
+  const bool skip = !(sy > sqrt(DBL_EPSILON) * sqrt(ss) * sqrt(yy));
+  if (skip || failed[b]) {
+    if (!failed[b] && skipped <= LM_MAX_SKIP) {
+      if (lane == 0) lm_skip[b] = (uint8_t)skipped;
+      return;
+    }
+    if (lane == 0) {
+      hc[0] = 1.0;
+      hc[1] = 0.0;
+      lm_skip[b] = 0;
+      lm_cnt[b] = 0;
+    }
+    return;
+  }
+  const int nc = last + 1;
+  if (hk) {
+#pragma unroll
+    for (int j = 0; j < LM_HIST; ++j)
+      if (j < nc) {
+        gs[j * nf + k] = Ps[j];
+        gy[j * nf + k] = Py[j];
+      }
+  }
+  if (lane == 0) {
+    lm_skip[b] = 0;
+    lm_cnt[b] = (uint8_t)nc;
+  }
+  const double sigma = fmin(fmax(sy / ss, 1e-8), 1e8);
+  // the recursion (the workgroup form's, lane k0 = k; its second entry k1 = k + 64 >= nf contributes zeros)
+  double Pa[LM_HIST], s_sa[LM_HIST], s_sy[LM_HIST];
+#pragma unroll
+  for (int j = 0; j < LM_HIST; ++j) {
+    Pa[j] = 0.0;
+    s_sa[j] = 0.0;
+    s_sy[j] = 0.0;
+  }
+#pragma unroll
+  for (int j = 0; j < LM_HIST; ++j) {
+    if (j >= nc) break;
+    const double s0 = hk ? Ps[j] : 0.0, s1 = 0.0;
+    double v0 = sigma * s0, v1 = sigma * s1;
+#pragma unroll
+    for (int i = 0; i < j; ++i) {
+      if (!(s_sa[i] > 0.0)) continue;
+      const double a0 = hk ? Pa[i] : 0.0, a1 = 0.0;
+      const double y0 = hk ? Py[i] : 0.0, y1 = 0.0;
+      const double as = wave_sum(a0 * s0 + a1 * s1) / s_sa[i];
+      const double ys = wave_sum(y0 * s0 + y1 * s1) / s_sy[i];
+      v0 = (v0 - a0 * as) + y0 * ys;
+      v1 = (v1 - a1 * as) + y1 * ys;
+    }
+    if (hk) Pa[j] = v0;
+    const double y0 = hk ? Py[j] : 0.0, y1 = 0.0;
+    s_sa[j] = wave_sum(s0 * v0 + s1 * v1);
+    s_sy[j] = wave_sum(s0 * y0 + s1 * y1);
+  }
+#pragma unroll
+  for (int i = 0; i < LM_HIST; ++i) {
+    if (i >= nc) break;
+    if (!(s_sa[i] > 0.0)) continue;
+    const double qa = sqrt(s_sa[i]), qy = sqrt(s_sy[i]);
+    if (hk) {
+      Pa[i] /= qa;
+      Py[i] /= qy;
+    }
+  }
+  int pos = 0;
+#pragma unroll
+  for (int i = 0; i < LM_HIST; ++i) {
+    if (i >= nc) break;
+    if (!(s_sa[i] > 0.0)) continue;
+    if (hk) {
+      hc[2 + pos * nf + k] = Pa[i];
+      hc[2 + LM_HIST * nf + pos * nf + k] = Py[i];
+    }
+    ++pos;
+  }
+  if (lane == 0) {
+    hc[0] = sigma;
+    hc[1] = (double)pos;
+  }
+}
+
 // ---- the restoration phase (IPOPT MinC_1NrmRestorationPhase; batch_ipm.py enter_resto /
 // resto_step / leave_resto restate these kernels) -------------------------------------------
 // The restoration problem of an instance whose line search failed at w_R:
@@ -2122,9 +2316,15 @@ int32_t step_phase(cpl_solver* S, int phase) {
       }
       CK(eval_full(S, S->Xn, S->f_n, S->grad_n, S->g_n, S->J_n));
       if (S->bfgs) {
-        hipLaunchKernelGGL(nf <= 64 ? k_lbfgs<64> : k_lbfgs<128>, dim3((unsigned)B), dim3(256), 0, st, B, m, nf, nw, S->nnz_rec, S->amap, S->moved,
-                           S->w, S->st_w, S->y, S->dy, S->st_alpha, S->gradw, S->J, S->grad_n, S->free32, n, S->J_n, S->lm_s,
-                           S->lm_y, S->lm_cnt, S->lm_skip, S->zeros_u8, S->Hq);
+        if (nf <= 64)
+          hipLaunchKernelGGL(k_lbfgs_wave, dim3((unsigned)((B + LBW_WAVES - 1) / LBW_WAVES)), dim3(64 * LBW_WAVES),
+                             sizeof(double) * LBW_WAVES * (size_t)m, st, B, m, nf, nw, S->nnz_rec, S->amap, S->moved,
+                             S->w, S->st_w, S->y, S->dy, S->st_alpha, S->gradw, S->J, S->grad_n, S->free32, n, S->J_n,
+                             S->lm_s, S->lm_y, S->lm_cnt, S->lm_skip, S->zeros_u8, S->Hq);
+        else
+          hipLaunchKernelGGL(k_lbfgs<128>, dim3((unsigned)B), dim3(256), 0, st, B, m, nf, nw, S->nnz_rec, S->amap, S->moved,
+                             S->w, S->st_w, S->y, S->dy, S->st_alpha, S->gradw, S->J, S->grad_n, S->free32, n, S->J_n,
+                             S->lm_s, S->lm_y, S->lm_cnt, S->lm_skip, S->zeros_u8, S->Hq);
         LAUNCHED("k_lbfgs");
       }
       CK(cpl_ipm_accept(B, nw, m, FMAX, S->moved, S->st_aug, nullptr, nullptr, S->st_alpha, S->a_z, S->theta_k,
@@ -2237,9 +2437,15 @@ int32_t step_phase(cpl_solver* S, int phase) {
       if (S->bfgs) {  // the restoration phase's own model: pairs from J^T y (its constraint curvature)
         hipLaunchKernelGGL(k_moved_r, dim3(blocks_elems(B)), dim3(256), 0, st, B, S->actR, S->st_alpha, S->movedR);
         LAUNCHED("k_moved_r");
-        hipLaunchKernelGGL(nf <= 64 ? k_lbfgs<64> : k_lbfgs<128>, dim3((unsigned)B), dim3(256), 0, st, B, m, nf, nw, S->nnz_rec, S->amap, S->movedR,
-                           S->w, S->st_w, S->y, S->dy, S->st_alpha, S->zeros_w, S->J, nullptr, S->free32, n, S->J_n, S->lm_s,
-                           S->lm_y, S->lm_cnt, S->lm_skip, S->zeros_u8, S->Hq);
+        if (nf <= 64)
+          hipLaunchKernelGGL(k_lbfgs_wave, dim3((unsigned)((B + LBW_WAVES - 1) / LBW_WAVES)), dim3(64 * LBW_WAVES),
+                             sizeof(double) * LBW_WAVES * (size_t)m, st, B, m, nf, nw, S->nnz_rec, S->amap, S->movedR,
+                             S->w, S->st_w, S->y, S->dy, S->st_alpha, S->zeros_w, S->J, nullptr, S->free32, n, S->J_n,
+                             S->lm_s, S->lm_y, S->lm_cnt, S->lm_skip, S->zeros_u8, S->Hq);
+        else
+          hipLaunchKernelGGL(k_lbfgs<128>, dim3((unsigned)B), dim3(256), 0, st, B, m, nf, nw, S->nnz_rec, S->amap,
+                             S->movedR, S->w, S->st_w, S->y, S->dy, S->st_alpha, S->zeros_w, S->J, nullptr, S->free32, n,
+                             S->J_n, S->lm_s, S->lm_y, S->lm_cnt, S->lm_skip, S->zeros_u8, S->Hq);
         LAUNCHED("k_lbfgs (resto)");
       }
       hipLaunchKernelGGL(k_resto_accept, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nf, nw, S->actR, S->movedR,

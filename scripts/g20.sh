@@ -1,0 +1,14 @@
+#!/bin/bash
+# the one-wave L-BFGS update: bitwise digests of the solve5 workload against build/libcpl_kkt.so (the
+# workgroup form), the solve tests, the solve loop A/B; the split's default (Ground list at 40 KiB)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+out=${1:-gpurun_out/g20}
+mkdir -p "$out"
+for B in 64 8192; do
+  CPL_LIB=build/libcpl_kkt.so timeout -k 10 120 python -u scripts/solve_digest.py --batch $B > "$out/digest_A_B$B.jsonl" || exit $?
+  timeout -k 10 120 python -u scripts/solve_digest.py --batch $B > "$out/digest_B_B$B.jsonl" || exit $?
+done
+timeout -k 10 400 python -u -m pytest -q --timeout 240 --timeout-method thread tests/test_gpu_solve_engine.py tests/test_batch_solve.py tests/test_oracle_pinning.py -m gpu > "$out/tests.log" 2>&1
+rc=$?; [ $rc -ge 124 ] && exit $rc
+bash scripts/ab_solve.sh "$out/ab_solve" build/libcpl_kkt.so centroidalplanner_amd/libcpl_mi355x.so || exit $?
+timeout -k 10 200 python -u scripts/ab_kernels.py --config mixed16 --rounds 3 --reps 5 --variants 0:0:256:1,7:0:256:1,7:0:256:1:16 --norms > "$out/mixed16_default.jsonl"
