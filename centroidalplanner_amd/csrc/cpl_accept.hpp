@@ -19,6 +19,64 @@ constexpr double LS_ETA_PHI = 1e-8, LS_OBJ_MAX_INC = 5.0;
 constexpr int LS_MAX_SOFT_RESTO = 10;  // max_soft_resto_iters
 constexpr double LS_KAPPA_SOC = 0.99;  // kappa_soc
 
+// The accepted step's state commit for instance b on one wave (cpl_ipm_accept_kernel; the solve
+// engine's k_resto_enter runs it in its launch): the filter (augmented / reset), y, z with the
+// kappa_Sigma safeguard, w, mu and the iteration count.
+struct IpmAcceptArgs {
+  int nw, m, nfilt;
+  const uint8_t *active, *aug, *failed, *rest;
+  const double *alpha, *a_z, *theta, *phi, *filt_t_in, *filt_p_in;
+  const int64_t* fcount_in;
+  const double *w_new, *dy, *dzL, *dzU, *mu;
+  const uint8_t *hasL, *hasU;
+  const double *wl0, *wu0;
+  double *w, *y, *zL, *zU, *mu_state;
+  int64_t* iters;
+  double *filt_t, *filt_p;
+  int64_t* fcount;
+};
+__device__ __forceinline__ void ipm_accept_one(const IpmAcceptArgs& a, int64_t b, int lane) {
+  const int nw = a.nw, m = a.m, nfilt = a.nfilt;
+  const bool act = a.active[b] != 0;
+  const bool addm = act && a.aug[b];
+  const bool fail = a.failed && a.failed[b] != 0;
+  const int64_t fc = a.fcount_in[b];
+  const int slot = (int)(fc % nfilt);
+  const double tk = a.theta[b], pk = a.phi[b];
+  for (int k = lane; k < nfilt; k += 64) {
+    double ft = a.filt_t_in[b * nfilt + k], fp = a.filt_p_in[b * nfilt + k];
+    if (addm && k == slot) {
+      ft = (1.0 - 1e-5) * tk;
+      fp = pk - 1e-8 * tk;
+    }
+    if (fail) ft = fp = INFINITY;
+    a.filt_t[b * nfilt + k] = ft;
+    a.filt_p[b * nfilt + k] = fp;
+  }
+  const double al = a.alpha[b], az = (a.rest && a.rest[b]) ? 0.0 : a.a_z[b], mub = a.mu[b];
+  for (int r = lane; r < m; r += 64)
+    if (act) a.y[b * m + r] += al * a.dy[b * m + r];
+  for (int k = lane; k < nw; k += 64) {
+    const double wn = a.w_new[b * nw + k];
+    if (act) {
+      if (a.hasL[k]) {
+        const double dl = wn - a.wl0[k];
+        a.zL[b * nw + k] = fmin(fmax(a.zL[b * nw + k] + az * a.dzL[b * nw + k], mub / (1e10 * dl)), 1e10 * mub / dl);
+      }
+      if (a.hasU[k]) {
+        const double du = a.wu0[k] - wn;
+        a.zU[b * nw + k] = fmin(fmax(a.zU[b * nw + k] + az * a.dzU[b * nw + k], mub / (1e10 * du)), 1e10 * mub / du);
+      }
+      a.w[b * nw + k] = wn;
+    }
+  }
+  if (lane == 0) {
+    a.fcount[b] = fail ? 0 : fc + (addm ? 1 : 0);
+    a.mu_state[b] = mub;
+    if (act) a.iters[b] += 1;
+  }
+}
+
 // theta_max; the filter (entries stored with their margins ((1 - gamma_theta) theta, phi - gamma_phi
 // theta): acceptable when, for every entry, theta or phi is not larger — IPOPT's Filter::Acceptable);
 // the switching condition; Armijo on the barrier objective for an f-type step at a reference point

@@ -468,58 +468,10 @@ __global__ __launch_bounds__(256) void cpl_ipm_post_step_kernel(
 // z += a_z dz with the kappa_Sigma = 1e10 safeguard at the new point, w <- w_new, mu, iters.
 // a_z is taken as 0 where rest (the feasibility step keeps the multipliers).  failed / rest may be
 // NULL (no filter resets / no multiplier-keeping rows: the solve engine's restoration phase).
-__global__ __launch_bounds__(256) void cpl_ipm_accept_kernel(
-    int64_t batch, int nw, int m, int nfilt, const uint8_t* __restrict__ active, const uint8_t* __restrict__ aug,
-    const uint8_t* __restrict__ failed, const uint8_t* __restrict__ rest, const double* __restrict__ alpha,
-    const double* __restrict__ a_z, const double* __restrict__ theta, const double* __restrict__ phi,
-    const double* __restrict__ filt_t_in, const double* __restrict__ filt_p_in, const int64_t* __restrict__ fcount_in,
-    const double* __restrict__ w_new, const double* __restrict__ dy, const double* __restrict__ dzL,
-    const double* __restrict__ dzU, const double* __restrict__ mu, const uint8_t* __restrict__ hasL,
-    const uint8_t* __restrict__ hasU, const double* __restrict__ wl0, const double* __restrict__ wu0,
-    double* __restrict__ w, double* __restrict__ y, double* __restrict__ zL, double* __restrict__ zU,
-    double* __restrict__ mu_state, int64_t* __restrict__ iters, double* __restrict__ filt_t,
-    double* __restrict__ filt_p, int64_t* __restrict__ fcount) {
+__global__ __launch_bounds__(256) void cpl_ipm_accept_kernel(const IpmAcceptArgs a, int64_t batch) {
   const int64_t b = (int64_t)blockIdx.x * IPM_WAVES + (threadIdx.x >> 6);
   if (b >= batch) return;
-  const int lane = threadIdx.x & 63;
-  const bool act = active[b] != 0;
-  const bool addm = act && aug[b];
-  const bool fail = failed && failed[b] != 0;
-  const int64_t fc = fcount_in[b];
-  const int slot = (int)(fc % nfilt);
-  const double tk = theta[b], pk = phi[b];
-  for (int k = lane; k < nfilt; k += 64) {
-    double ft = filt_t_in[b * nfilt + k], fp = filt_p_in[b * nfilt + k];
-    if (addm && k == slot) {
-      ft = (1.0 - 1e-5) * tk;
-      fp = pk - 1e-8 * tk;
-    }
-    if (fail) ft = fp = INFINITY;
-    filt_t[b * nfilt + k] = ft;
-    filt_p[b * nfilt + k] = fp;
-  }
-  const double al = alpha[b], az = (rest && rest[b]) ? 0.0 : a_z[b], mub = mu[b];
-  for (int r = lane; r < m; r += 64)
-    if (act) y[b * m + r] += al * dy[b * m + r];
-  for (int k = lane; k < nw; k += 64) {
-    const double wn = w_new[b * nw + k];
-    if (act) {
-      if (hasL[k]) {
-        const double dl = wn - wl0[k];
-        zL[b * nw + k] = fmin(fmax(zL[b * nw + k] + az * dzL[b * nw + k], mub / (1e10 * dl)), 1e10 * mub / dl);
-      }
-      if (hasU[k]) {
-        const double du = wu0[k] - wn;
-        zU[b * nw + k] = fmin(fmax(zU[b * nw + k] + az * dzU[b * nw + k], mub / (1e10 * du)), 1e10 * mub / du);
-      }
-      w[b * nw + k] = wn;
-    }
-  }
-  if (lane == 0) {
-    fcount[b] = fail ? 0 : fc + (addm ? 1 : 0);
-    mu_state[b] = mub;
-    if (act) iters[b] += 1;
-  }
+  ipm_accept_one(a, b, threadIdx.x & 63);
 }
 
 // dst[b] = src[b] for the rows with mask[b] (row length len doubles), 16-byte accesses when aligned.
@@ -804,10 +756,11 @@ int32_t cpl_ipm_accept(int64_t batch, int32_t nw, int32_t m, int32_t nfilt, cons
       !d_hasL || !d_hasU || !d_wl0 || !d_wu0 || !d_w || !d_zL || !d_zU || !d_mu_state || !d_iters || !d_filt_t ||
       !d_filt_p || !d_fcount)
     return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_ipm_accept: missing buffer");
-  IPM_LAUNCH(cpl_ipm_accept_kernel, "cpl_ipm_accept", batch, (int)nw, (int)m, (int)nfilt, d_active, d_aug, d_failed,
-             d_rest, d_alpha, d_a_z, d_theta, d_phi, d_filt_t_in, d_filt_p_in, d_fcount_in, d_w_new, d_dy, d_dzL,
-             d_dzU, d_mu, d_hasL, d_hasU, d_wl0, d_wu0, d_w, d_y, d_zL, d_zU, d_mu_state, d_iters, d_filt_t, d_filt_p,
-             d_fcount);
+  const IpmAcceptArgs a{(int)nw, (int)m, (int)nfilt, d_active, d_aug, d_failed, d_rest, d_alpha, d_a_z, d_theta,
+                        d_phi, d_filt_t_in, d_filt_p_in, d_fcount_in, d_w_new, d_dy, d_dzL, d_dzU, d_mu, d_hasL,
+                        d_hasU, d_wl0, d_wu0, d_w, d_y, d_zL, d_zU, d_mu_state, d_iters, d_filt_t, d_filt_p,
+                        d_fcount};
+  IPM_LAUNCH(cpl_ipm_accept_kernel, "cpl_ipm_accept", a, batch);
 }
 
 int32_t cpl_ipm_masked_rows(int64_t batch, int64_t row_len, const uint8_t* d_mask, const double* d_src, double* d_dst,

@@ -1060,10 +1060,15 @@ __global__ __launch_bounds__(256) void k_resto_enter(
     int64_t* __restrict__ fcR, double* __restrict__ thmaxR, double* __restrict__ thminR,
     double* __restrict__ th_o0, double* __restrict__ ph_o0, double* __restrict__ dwlR, uint8_t* __restrict__ lm_cnt,
     uint8_t* __restrict__ lm_skip, double* __restrict__ Hq, int64_t lmc, double* __restrict__ Mw,
-    double* __restrict__ r1, double* __restrict__ r2, double* __restrict__ Dinv, const AcceptRows ar) {
+    double* __restrict__ r1, double* __restrict__ r2, double* __restrict__ Dinv, const AcceptRows ar,
+    const IpmAcceptArgs acc, bool with_accept) {
   const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
   if (b >= B) return;
   const int lane = threadIdx.x & 63;
+  if (with_accept) {  // (cpl_ipm_accept for this instance first, in the same launch)
+    ipm_accept_one(acc, b, lane);
+    __threadfence_block();  // its filter / count stores before the entry's loads of them
+  }
   if (ar.moved && ar.moved[b]) {  // (k_accept_rows for the instances that moved, in the same launch)
     const int64_t L = 1 + ar.n + ar.m + ar.nnz;
     for (int64_t q = lane; q < L; q += 64) accept_row_entry(ar, b, q);
@@ -2327,12 +2332,16 @@ int32_t step_phase(cpl_solver* S, int phase) {
                              S->lm_s, S->lm_y, S->lm_cnt, S->lm_skip, S->zeros_u8, S->Hq);
         LAUNCHED("k_lbfgs");
       }
-      CK(cpl_ipm_accept(B, nw, m, FMAX, S->moved, S->st_aug, nullptr, nullptr, S->st_alpha, S->a_z, S->theta_k,
-                        S->phi_k, S->ft, S->fp, S->fc, S->st_w, S->dy, S->dzL, S->dzU, S->mu_o, S->hasL, S->hasU,
-                        S->wl0, S->wu0, S->w, S->y, S->zL, S->zU, S->mu, S->iters, S->filt_t, S->filt_p, S->fcount,
-                        st));
+      const IpmAcceptArgs acc{nw, m, FMAX, S->moved, S->st_aug, nullptr, nullptr, S->st_alpha, S->a_z, S->theta_k,
+                              S->phi_k, S->ft, S->fp, S->fc, S->st_w, S->dy, S->dzL, S->dzU, S->mu_o, S->hasL,
+                              S->hasU, S->wl0, S->wu0, S->w, S->y, S->zL, S->zU, S->mu, S->iters, S->filt_t,
+                              S->filt_p, S->fcount};
       AcceptRows ar{S->moved, n, m, S->nnz_rec, S->f_n, S->grad_n, S->g_n, S->J_n, S->f, S->grad, S->g, S->J};
       if (phase == P_ACCEPT_NR) {  // no instance can have failed its search: no entry
+        CK(cpl_ipm_accept(B, nw, m, FMAX, S->moved, S->st_aug, nullptr, nullptr, S->st_alpha, S->a_z, S->theta_k,
+                          S->phi_k, S->ft, S->fp, S->fc, S->st_w, S->dy, S->dzL, S->dzU, S->mu_o, S->hasL, S->hasU,
+                          S->wl0, S->wu0, S->w, S->y, S->zL, S->zU, S->mu, S->iters, S->filt_t, S->filt_p, S->fcount,
+                          st));
         hipLaunchKernelGGL(k_accept_rows, dim3(blocks_elems(B * (1 + n + m + S->nnz_rec))), dim3(256), 0, st, B, n,
                            m, S->nnz_rec, S->moved, S->f_n, S->grad_n, S->g_n, S->J_n, S->f, S->grad, S->g, S->J);
         LAUNCHED("k_accept_rows");
@@ -2343,8 +2352,8 @@ int32_t step_phase(cpl_solver* S, int phase) {
                          S->zU, S->mu_o, S->theta_k, S->phi_k, S->hasL, S->hasU, S->filt_t, S->filt_p, S->fcount,
                          S->iters, S->in_resto, S->n_resto, S->wR, S->pR, S->nR, S->zp, S->zn, S->zLR, S->zUR, S->muR,
                          S->ftR, S->fpR, S->fcR, S->thmaxR, S->thminR, S->th_o0, S->ph_o0, S->dwlR, S->lm_cnt,
-                         S->lm_skip, S->bfgs ? S->Hq : nullptr, lmc, S->M, S->r1, S->r2, S->Dinv, ar);
-      LAUNCHED("k_resto_enter (+ the accepted rows)");
+                         S->lm_skip, S->bfgs ? S->Hq : nullptr, lmc, S->M, S->r1, S->r2, S->Dinv, ar, acc, true);
+      LAUNCHED("k_resto_enter (+ the accept, the accepted rows)");
       CK(cpl_kkt_qd_solve(B, nw, m, S->M, S->A, S->Dinv, S->r1, S->r2, S->failed, S->dwlR, S->dw, S->dy, S->scr1,
                           S->Kqd, st));
       if (B > COUNT1_MAX) {
