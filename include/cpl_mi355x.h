@@ -228,11 +228,15 @@ int32_t cpl_time_eval_batch_ex(const cpl_problem_desc* d, int64_t batch, const d
  * 1 = row-staged lane-per-instance, 2 = pipelined (persistent, warp-specialized), 3 =
  * tile-stationary, 4 = tile-stationary with the Jacobian written straight to the records, 5 =
  * entry-parallel (none / Ground, IFOPT CSR instance-major records: every g / jac entry computed by
- * the thread that stores it, no output image in LDS); tile_lds_kb = LDS budget of one workgroup (8..160 KiB; 0 = per-kernel
+ * the thread that stores it, no output image in LDS), 6 / 7 = mixed batches split by kind (the
+ * Superquadric half LDS-staged / Jacobian-direct; the default for mixed is 7's form);
+ * tile_lds_kb = LDS budget of one workgroup (8..160 KiB; 0 = per-kernel
  * default: 48 KiB for both: the largest power-of-two tile that fits, e.g. 8 instances of 8
  * Superquadric contacts, 4 of 16); wg_threads = 128 or 256 for the tile kernel (default 256);
  * nt_stores = non-temporal output stores (default 1); ablate = measurement-only ablation
- * (0 = off, 1 = skip the compute phase, 2 = skip the output stores: results are then garbage).
+ * (0 = off, 1 = skip the compute phase, 2 = skip the output stores: results are then garbage; for
+ * the kind split, bits 4 = its halves one after the other on one stream, 8 = the Ground half issued
+ * first, 16 = the Ground list at 48 KiB instead of 40, 32 = the Superquadric tiles at 40 KiB).
  * Every variant computes bit-identical results.  Not thread-safe against concurrent launches. */
 int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_threads, int32_t nt_stores,
                        int32_t ablate);
