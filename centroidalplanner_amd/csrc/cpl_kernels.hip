@@ -2377,48 +2377,43 @@ __global__ __launch_bounds__(PART_BLOCK) void k_kind_count(int64_t batch, const 
     blk_sq[blockIdx.x] = t;
   }
 }
-// exclusive scan of the per-block Superquadric counts (one workgroup, chunks of PART_BLOCK) and the
-// two list lengths: counts[0] Ground, counts[1] Superquadric
-__global__ __launch_bounds__(PART_BLOCK) void k_kind_scan(int64_t batch, int nblk, const int32_t* __restrict__ blk_sq,
-                                                          int32_t* __restrict__ blk_off, int32_t* __restrict__ counts) {
-  __shared__ int sh[PART_BLOCK];
-  int carry = 0;
-  for (int base = 0; base < nblk; base += PART_BLOCK) {
-    const int i = base + (int)threadIdx.x;
-    const int v = i < nblk ? blk_sq[i] : 0;
-    sh[threadIdx.x] = v;
-    __syncthreads();
-    for (int o = 1; o < PART_BLOCK; o <<= 1) {  // Hillis-Steele inclusive scan
-      const int u = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0;
-      __syncthreads();
-      sh[threadIdx.x] += u;
-      __syncthreads();
-    }
-    if (i < nblk) blk_off[i] = carry + sh[threadIdx.x] - v;
-    carry += sh[PART_BLOCK - 1];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    counts[1] = carry;
-    counts[0] = (int32_t)(batch - carry);
-  }
-}
-__global__ __launch_bounds__(PART_BLOCK) void k_kind_write(int64_t batch, const uint8_t* __restrict__ tag,
-                                                           const int32_t* __restrict__ blk_off,
-                                                           int32_t* __restrict__ idx_gr, int32_t* __restrict__ idx_sq) {
+// The lists written in place of a scan kernel: each block sums the Superquadric counts of the blocks
+// before it (its exclusive offset, an integer sum: any order gives the same value), and the last block
+// sums them all for the two list lengths (counts[0] Ground, counts[1] Superquadric) — one launch and
+// one single-workgroup Hillis-Steele pass fewer than a separate scan.
+__global__ __launch_bounds__(PART_BLOCK) void k_kind_write(int64_t batch, int nblk, const uint8_t* __restrict__ tag,
+                                                           const int32_t* __restrict__ blk_sq,
+                                                           int32_t* __restrict__ idx_gr, int32_t* __restrict__ idx_sq,
+                                                           int32_t* __restrict__ counts) {
   __shared__ int wsum[PART_BLOCK / 64];
+  __shared__ long long wpre[PART_BLOCK / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool last = (int)blockIdx.x == nblk - 1;
+  const int upto = last ? nblk : (int)blockIdx.x;  // the last block also sums its own count
+  long long pre = 0;
+  for (int i = (int)threadIdx.x; i < upto; i += PART_BLOCK)
+    if (i < (int)blockIdx.x || last) pre += blk_sq[i];
+  for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
   const int64_t b = (int64_t)blockIdx.x * PART_BLOCK + threadIdx.x;
   const bool in = b < batch;
   const bool sq = in && tag[b] == CPL_ENV_SUPERQUADRIC;
   const unsigned long long msk = __ballot(sq);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) wsum[wave] = __popcll(msk);
+  if (lane == 0) {
+    wsum[wave] = __popcll(msk);
+    wpre[wave] = pre;
+  }
   __syncthreads();
+  long long tot = 0;  // (the last block: every block's count, its own included)
+  for (int w = 0; w < PART_BLOCK / 64; ++w) tot += wpre[w];
+  const int64_t off_sq = last ? tot - (blk_sq[blockIdx.x]) : tot;
+  if (last && threadIdx.x == 0) {
+    counts[1] = (int32_t)tot;
+    counts[0] = (int32_t)(batch - tot);
+  }
   int before = 0;  // Superquadric instances of the block before this wave
   for (int w = 0; w < wave; ++w) before += wsum[w];
   const int sq_rank = before + __popcll(msk & ((1ull << lane) - 1ull));
   const int local = (int)threadIdx.x;
-  const int64_t off_sq = blk_off[blockIdx.x];
   const int64_t off_gr = (int64_t)blockIdx.x * PART_BLOCK - off_sq;
   if (sq) idx_sq[off_sq + sq_rank] = (int32_t)b;
   else if (in) idx_gr[off_gr + (local - sq_rank)] = (int32_t)b;
@@ -2626,8 +2621,8 @@ static int g_nt = 1;               // non-temporal output stores
 static int g_ablate = 0;           // measurement-only: 1 = skip the compute phase, 2 = skip the stores,
                                    // 4 = the kind split's halves one after the other on the launch stream,
                                    // 8 = the split's Ground half issued before the Superquadric half,
-                                   // 16 = the split's Ground list at 48 KiB (default 40), 32 = its
-                                   // Superquadric tiles at 40 KiB (default 48)
+                                   // 16 / 64 / 128 = the split's Ground list at 48 / 36 / 32 KiB
+                                   // (default 40), 32 = its Superquadric tiles at 40 KiB (default 48)
 
 static size_t tile_budget() { return g_lds_budget ? g_lds_budget : 48 * 1024; }
 static size_t pipe_budget() { return g_lds_budget ? g_lds_budget : 48 * 1024; }
@@ -2861,15 +2856,14 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
     if ((st = kind_workspace(stream, batch, &kl))) return st;
     const unsigned nblk = (unsigned)((batch + PART_BLOCK - 1) / PART_BLOCK);
     hipLaunchKernelGGL(k_kind_count, dim3(nblk), dim3(PART_BLOCK), 0, stream, batch, d_env_tag, kl.blk_sq);
-    hipLaunchKernelGGL(k_kind_scan, dim3(1), dim3(PART_BLOCK), 0, stream, batch, (int)nblk, kl.blk_sq, kl.blk_off,
-                       kl.counts);
-    hipLaunchKernelGGL(k_kind_write, dim3(nblk), dim3(PART_BLOCK), 0, stream, batch, d_env_tag, kl.blk_off, kl.idx_gr,
-                       kl.idx_sq);
+    hipLaunchKernelGGL(k_kind_write, dim3(nblk), dim3(PART_BLOCK), 0, stream, batch, (int)nblk, d_env_tag, kl.blk_sq,
+                       kl.idx_gr, kl.idx_sq, kl.counts);
     KParams Kg = K, Ks = K;
     // the Ground list at 40 KiB (1 048 576 x 16 mixed: 2.600 against 2.626 ms at 48 KiB, profiles/r4/
     // split_lds; measurement: ablation 16 gives it 48 KiB, 32 the Superquadric tiles 40 KiB)
+    const size_t list_kb = (g_ablate & 16) ? 48 : (g_ablate & 64) ? 36 : (g_ablate & 128) ? 32 : 40;
     if ((st = plan_entry(Kg, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr, true,
-                         (g_ablate & 16) ? 48 * 1024 : 40 * 1024)))
+                         list_kb * 1024)))
       return st;
     Ks.jdirect = ((g_variant == VAR_SPLIT_JD || g_variant == VAR_AUTO) && d_jac) ? 1 : 0;
     if ((st = plan_tile(Ks, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr, 64, false,
@@ -3365,7 +3359,7 @@ int32_t cpl_eval_batch_norms(const cpl_problem_desc* d, int64_t batch, const dou
 
 int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_threads, int32_t nt_stores,
                        int32_t ablate) {
-  if (ablate < 0 || (ablate > 2 && (ablate & ~(4 | 8 | 16 | 32)))) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
+  if (ablate < 0 || (ablate > 2 && (ablate & ~(4 | 8 | 16 | 32 | 64 | 128)))) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
   g_ablate = ablate;
   if (kernel_variant < VAR_AUTO || kernel_variant > VAR_SPLIT_JD) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown kernel variant");
   if (tile_lds_kb != 0 && (tile_lds_kb < 8 || tile_lds_kb > 160))
