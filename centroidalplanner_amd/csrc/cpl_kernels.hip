@@ -81,6 +81,8 @@ struct KParams {
   int32_t contact_rows;  // constraint rows per contact: 6 (environment) or 2
   int32_t ablate;        // measurement-only ablation (cpl_set_tuning), 0 in production
   int32_t sq_ladder;     // every P_a is an integer in [2, 64]: double-double power ladders
+  int32_t grid_cap;      // (entry kernel, the kind split's Ground half) the workgroups that walk the
+                         // tiles while the Superquadric list is non-empty (0: every workgroup)
   // fused Lagrangian gradient (cpl_eval_lagrangian_grad): grad f + J^T y of every instance from the
   // LDS tile image, through a CSC index of the fixed structure; instance b takes y[b / y_repeat]
   int32_t want_lgrad, y_repeat;
@@ -1920,7 +1922,14 @@ __global__ __launch_bounds__(256) void cpl_eval_entry_kernel(const KParams K, in
   double mass_def = K.mass_default;  // a value (see cpl_eval_pipe_kernel)
   asm volatile("" : "+v"(mass_def));
   NormAcc acc;
-  int64_t t = blockIdx.x;
+  // the grid that walks the tiles: every workgroup, or (the kind split's Ground half beside a non-empty
+  // Superquadric list, whose tiles the other slots of each CU take) the first grid_cap; the others
+  // only write zero residual partials.  d_count[1] is the Superquadric list's length (the split's
+  // counts), the same value in every workgroup.
+  const int64_t G = (K.grid_cap > 0 && d_count && d_count[1] > 0 && (int64_t)gridDim.x > K.grid_cap)
+                        ? (int64_t)K.grid_cap
+                        : (int64_t)gridDim.x;
+  int64_t t = (int64_t)blockIdx.x < G ? (int64_t)blockIdx.x : ntiles;
   __syncthreads();  // (the table)
 
   if (loader) {
@@ -1960,7 +1969,7 @@ __global__ __launch_bounds__(256) void cpl_eval_entry_kernel(const KParams K, in
           if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(d)) & 15) == 0) dma_row16(d, src, n, lane);
           else dma_row4(d, src, n, lane);
         }
-        if (tt + gridDim.x < ntiles) ids(tt + gridDim.x, pf_b, pf_mass);
+        if (tt + G < ntiles) ids(tt + G, pf_b, pf_mass);
       }
     };
     auto finish_stage = [&](int64_t tt, int bi) {
@@ -1981,8 +1990,8 @@ __global__ __launch_bounds__(256) void cpl_eval_entry_kernel(const KParams K, in
     }
     lds_barrier();
     int cur = 0;
-    for (; t < ntiles; t += gridDim.x) {
-      const int64_t tn = t + gridDim.x;
+    for (; t < ntiles; t += G) {
+      const int64_t tn = t + G;
       if (tn < ntiles) stage(tn, cur ^ 1);
       lds_barrier();  // (the compute waves' prologue)
       if (tn < ntiles) finish_stage(tn, cur ^ 1);
@@ -1994,7 +2003,7 @@ __global__ __launch_bounds__(256) void cpl_eval_entry_kernel(const KParams K, in
     lds_barrier();
     int cur = 0;
     const double mu = K.mu;
-    for (; t < ntiles; t += gridDim.x) {
+    for (; t < ntiles; t += G) {
       const int64_t j0 = t * T;
       const int valid = (int)((count - j0) < T ? (count - j0) : T);
       const double* X = XB(cur);
@@ -2622,7 +2631,9 @@ static int g_ablate = 0;           // measurement-only: 1 = skip the compute pha
                                    // 4 = the kind split's halves one after the other on the launch stream,
                                    // 8 = the split's Ground half issued before the Superquadric half,
                                    // 16 / 64 / 128 = the split's Ground list at 48 / 36 / 32 KiB
-                                   // (default 40), 32 = its Superquadric tiles at 40 KiB (default 48)
+                                   // (default 40), 32 = its Superquadric tiles at 40 KiB (default 48),
+                                   // 256 / 512 = every Ground workgroup walking / two per CU
+                                   // (default one per CU while the Superquadric list is non-empty)
 
 static size_t tile_budget() { return g_lds_budget ? g_lds_budget : 48 * 1024; }
 static size_t pipe_budget() { return g_lds_budget ? g_lds_budget : 48 * 1024; }
@@ -2866,6 +2877,9 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
                          list_kb * 1024)))
       return st;
     Ks.jdirect = ((g_variant == VAR_SPLIT_JD || g_variant == VAR_AUTO) && d_jac) ? 1 : 0;
+    // (measurement: ablation 32 = the Superquadric tiles at 40 KiB instead of 48 — within the noise beside
+    // the capped Ground walkers below: 2.603 / 2.552 against 2.540 / 2.579 ms in two runs,
+    // profiles/r4/split_grid)
     if ((st = plan_tile(Ks, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr, 64, false,
                         (g_ablate & 32) ? 40 * 1024 : 0)))
       return st;
@@ -2884,7 +2898,20 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
     const size_t lds_s = sizeof(double) * (size_t)(Ks.offRB + Ks.T);
     const int64_t ntg = (batch + Kg.T - 1) / Kg.T;
     const int64_t want = resident_blocks(reinterpret_cast<const void*>(ek), lds_g);
-    const unsigned grid_g = (unsigned)(ntg < want ? ntg : want);
+    // the Ground half's persistent grid at full residency, of which one workgroup per CU walks the tiles
+    // while the Superquadric list is non-empty (the other slots left to its tiles on the other stream:
+    // 1 048 576 x 16 mixed 2.54-2.58 against 2.61 ms with every workgroup walking, profiles/r4/split_grid);
+    // all of it when the batch is all Ground (the cap decided on the device, from the partition's
+    // counts: 1.31 ms for 524 288 all-Ground mixed instances, as uncapped; a cap fixed at launch had
+    // cost 2.37).  Measurement: ablation 256 = no cap, 512 = two per CU.
+    const int64_t want_g = want;
+    if (!(g_ablate & 256)) {
+      int dev = 0, cus = 256;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      Kg.grid_cap = (int32_t)((g_ablate & 512) ? 2 * cus : cus);
+    }
+    const unsigned grid_g = (unsigned)(ntg < want_g ? ntg : want_g);
     const unsigned grid_s = (unsigned)((batch + Ks.T - 1) / Ks.T);  // every tile the list may hold
     const size_t nparts = (size_t)grid_g + (size_t)grid_s * 4;
     if (K.want_norms && (st = norm_workspace(stream, nparts, &ws))) return st;
@@ -3359,7 +3386,7 @@ int32_t cpl_eval_batch_norms(const cpl_problem_desc* d, int64_t batch, const dou
 
 int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_threads, int32_t nt_stores,
                        int32_t ablate) {
-  if (ablate < 0 || (ablate > 2 && (ablate & ~(4 | 8 | 16 | 32 | 64 | 128)))) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
+  if (ablate < 0 || (ablate > 2 && (ablate & ~(4 | 8 | 16 | 32 | 64 | 128 | 256 | 512)))) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
   g_ablate = ablate;
   if (kernel_variant < VAR_AUTO || kernel_variant > VAR_SPLIT_JD) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown kernel variant");
   if (tile_lds_kb != 0 && (tile_lds_kb < 8 || tile_lds_kb > 160))

@@ -236,7 +236,9 @@ int32_t cpl_time_eval_batch_ex(const cpl_problem_desc* d, int64_t batch, const d
  * nt_stores = non-temporal output stores (default 1); ablate = measurement-only ablation
  * (0 = off, 1 = skip the compute phase, 2 = skip the output stores: results are then garbage; for
  * the kind split, bits 4 = its halves one after the other on one stream, 8 = the Ground half issued
- * first, 16 = the Ground list at 48 KiB instead of 40, 32 = the Superquadric tiles at 40 KiB).
+ * first, 16 / 64 / 128 = the Ground list at 48 / 36 / 32 KiB instead of 40, 32 = the Superquadric tiles
+ * at 40 KiB instead of 48, 256 / 512 = every Ground workgroup walking the tiles / two per CU instead of
+ * one per CU while the Superquadric list is non-empty).
  * Every variant computes bit-identical results.  Not thread-safe against concurrent launches. */
 int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_threads, int32_t nt_stores,
                        int32_t ablate);
