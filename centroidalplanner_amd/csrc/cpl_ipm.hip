@@ -285,6 +285,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_max_step_kernel(int64_t batch, in
 // exactly as the one-wave form, the M entries are spread over the four waves (every entry the same
 // operations in the same order: bitwise the one-wave result); at B = 1 one wave filled 47 x 47
 // entries alone.
+constexpr int LM_REG_PAIRS = 8;  // the column build's largest limited-memory history
 template <bool LM, bool WIDE = false>
 __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
     int64_t batch, int nw, int m, int nf, const double* __restrict__ w, const double* __restrict__ zL,
@@ -351,6 +352,48 @@ __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
     if (WIDE) __syncthreads();
     const double* U = UW;
     const double* W = UW + lm_pairs * nf;
+    if (nw <= 64 && lm_pairs <= LM_REG_PAIRS) {
+      // lane j builds column j: its pair entries u_i[j], w_i[j] in registers, the row's u_i[k], w_i[k]
+      // LDS broadcasts (one address per wave), four rows in flight; each entry the same operations in
+      // the same order as the entry loop below (bitwise its M)
+      const int jj = lane;
+      const bool cj = jj < nf;
+      double Uj[LM_REG_PAIRS], Wj[LM_REG_PAIRS];
+#pragma unroll
+      for (int i = 0; i < LM_REG_PAIRS; ++i) {
+        Uj[i] = (cj && i < nv) ? U[i * nf + jj] : 0.0;
+        Wj[i] = (cj && i < nv) ? W[i * nf + jj] : 0.0;
+      }
+      const int r0 = WIDE ? (int)(threadIdx.x >> 6) : 0, rs = WIDE ? IPM_WAVES : 1;
+      constexpr int RU = 4;
+      for (int k0 = r0; k0 < nw; k0 += rs * RU) {
+        double h[RU];
+        int kr[RU];
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+          kr[u] = k0 + rs * u;
+          h[u] = jj == kr[u] ? sigma : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < LM_REG_PAIRS; ++i) {
+          if (i >= nv) break;
+#pragma unroll
+          for (int u = 0; u < RU; ++u) {
+            const int kk = kr[u] < nf ? kr[u] : 0;
+            h[u] = (h[u] - U[i * nf + kk] * Uj[i]) + W[i * nf + kk] * Wj[i];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+          const int kk = kr[u];
+          if (kk < nw && jj < nw) {
+            double v = (jj == kk) ? sg[kk] : 0.0;
+            if (kk < nf && cj) v += h[u];
+            Mb[kk * nw + jj] = v;
+          }
+        }
+      }
+    } else {
     // four entries per lane at a time (independent chains: their LDS reads overlap), each entry's
     // operations in the order of the one-entry loop
     constexpr int EU = 4;
@@ -382,6 +425,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_newton_setup_kernel(
         }
       }
     }
+    }  // (nw > 64)
   } else {
     const double* Hb = H ? H + b * (int64_t)nf * nf : nullptr;
     // h_sym: H is the raw central-difference matrix (cpl_ipm_fd_hessian_raw), symmetrised here as
