@@ -11,6 +11,8 @@
 #include <cmath>
 #include <cstdint>
 
+#include "cpl_wave.hpp"
+
 namespace cpl {
 
 // gamma_theta, gamma_phi, delta, s_theta, s_phi, eta_phi, obj_max_inc [IPOPT defaults]
@@ -111,6 +113,35 @@ __device__ __forceinline__ bool ls_acceptable_wave(double th, double ph, double 
   return fin && th <= theta_max && in_filter && (ftype ? armijo : suff);
 }
 
+// The line search's per-instance setup after the Newton step (ls_setup_wave below)
+struct LsSetupArgs {
+  int32_t m;
+  const uint8_t* act;
+  const double *w, *dw, *dy, *c, *f, *g, *theta_k, *theta_min;
+  uint8_t* in_soft;
+  int32_t* soft_cnt;
+  uint8_t *tiny_last, *tiny_flag, *tiny_now, *soft_now;
+  double* a_min;
+  uint8_t* searching;
+  double *st_f, *st_g, *st_w, *st_alpha;
+  uint8_t* st_aug;
+  double* alpha;
+  uint8_t* any;
+};
+
+// The post-step quantities (cpl_ipm.hip's post-step kernel; the fused line-search kernel runs it as
+// its prologue: ipm_post_step_one below)
+struct PostStepArgs {
+  int32_t nw;
+  const double *w, *dw, *zL, *zU, *gphi, *mu, *tau;
+  const uint8_t *hasL, *hasU;
+  const double *wl0, *wu0, *theta, *theta_min;
+  const uint8_t* active;
+  const double* delta_w;
+  double *dwl, *dzL, *dzU, *a_max, *a_z, *gd_out;
+  uint8_t* switch_ok;
+};
+
 // The rest of the regular backtracking line search of every instance still searching after its
 // first trial (and that trial's second-order corrections), in one launch: trials at alpha, alpha / 2,
 // ... until one is acceptable, alpha falls to alpha_min, or max_trials more trials were made
@@ -184,6 +215,11 @@ struct LsBacktrackArgs {
   double* soft_X;
   uint8_t* soft_try;
   double* a_soft;
+  // (FIRST) the post-step quantities and the search's setup of every instance, computed in the
+  // kernel's prologue (with_post) instead of a launch of their own
+  PostStepArgs post;
+  LsSetupArgs setup;
+  int32_t with_post;
 };
 
 // s + sum_{r < m} a[r * stride] * v[r], accumulated in r order exactly as the plain loop
@@ -230,20 +266,6 @@ __device__ __forceinline__ double ls_xor_max(double v) {
 // search state (searching unless tiny or in the soft phase; a tiny step is taken whole: alpha_max).
 // One wave per instance, at the end of cpl_ipm.hip's post-step kernel (am = alpha_max and gd = the
 // directional derivative it has just computed).
-struct LsSetupArgs {
-  int32_t m;
-  const uint8_t* act;
-  const double *w, *dw, *dy, *c, *f, *g, *theta_k, *theta_min;
-  uint8_t* in_soft;
-  int32_t* soft_cnt;
-  uint8_t *tiny_last, *tiny_flag, *tiny_now, *soft_now;
-  double* a_min;
-  uint8_t* searching;
-  double *st_f, *st_g, *st_w, *st_alpha;
-  uint8_t* st_aug;
-  double* alpha;
-  uint8_t* any;
-};
 __device__ __forceinline__ void ls_setup_wave(int64_t b, int nw, const LsSetupArgs& L, double am, double gd) {
   const int m = L.m;
   const int lane = threadIdx.x & 63;
@@ -281,6 +303,48 @@ __device__ __forceinline__ void ls_setup_wave(int64_t b, int nw, const LsSetupAr
   }
 }
 
+// After the Newton step (batch_ipm.py step): bound-multiplier steps dzL = mu/dl - zL - zL/dl dw,
+// dzU = mu/du - zU + zU/du dw, their fraction-to-the-boundary step a_z, the primal one a_max,
+// gd = grad_phi . dw, switch_ok = ls_switch_flags (gd < 0, theta <= theta_min), and delta_w_last <-
+// delta_w on the active instances; then (ls.act != NULL) the line search's setup.  One wave, instance b.
+__device__ __forceinline__ void ipm_post_step_one(const PostStepArgs& P, int64_t b, const LsSetupArgs& ls) {
+  const int nw = P.nw;
+  const int lane = threadIdx.x & 63;
+  const double mub = P.mu[b], t = P.tau[b];
+  double rp = INFINITY, rz = INFINITY, gd = 0.0;
+  for (int k = lane; k < nw; k += 64) {
+    const double wk = P.w[b * nw + k], dk = P.dw[b * nw + k];
+    gd += P.gphi[b * nw + k] * dk;
+    double dzl = 0.0, dzu = 0.0;
+    if (P.hasL[k]) {
+      const double dl = wk - P.wl0[k], zl = P.zL[b * nw + k];
+      dzl = mub / dl - zl - zl / dl * dk;
+      if (dk < 0.0) rp = fmin(rp, -t * dl / dk);
+      if (dzl < 0.0) rz = fmin(rz, -t * zl / dzl);
+    }
+    if (P.hasU[k]) {
+      const double du = P.wu0[k] - wk, zu = P.zU[b * nw + k];
+      dzu = mub / du - zu + zu / du * dk;
+      if (dk > 0.0) rp = fmin(rp, -t * du / -dk);
+      if (dzu < 0.0) rz = fmin(rz, -t * zu / dzu);
+    }
+    P.dzL[b * nw + k] = dzl;
+    P.dzU[b * nw + k] = dzu;
+  }
+  rp = wave_min(rp);
+  rz = wave_min(rz);
+  gd = wave_sum(gd);
+  if (lane == 0) {
+    P.a_max[b] = fmin(rp, 1.0);
+    P.a_z[b] = fmin(rz, 1.0);
+    P.gd_out[b] = gd;
+    P.switch_ok[b] = ls_switch_flags(P.theta[b], P.theta_min[b], gd);
+    if (P.active[b]) P.dwl[b] = P.delta_w[b];
+  }
+  // the line-search setup: no output above is among its inputs except alpha_max and gd (registers)
+  if (ls.act) ls_setup_wave(b, nw, ls, fmin(rp, 1.0), gd);
+}
+
 // The solve loop's per-iteration unpack after the optimality test, fused into that kernel's tail
 // (cpl_ipm.hip; was a launch of its own): X = unpack(w) (free columns from w, fixed ones from
 // Xbase), tau = max(0.99, 1 - mu) and the iteration's snapshot act = active && !in_resto.
@@ -299,6 +363,7 @@ struct IpmUnpack {
   double* acc_zL;
   double* acc_zU;
   uint8_t* has_acc;
+  uint8_t* any_reset;  // (the solve loop's fused search) flags to clear, or NULL
 };
 
 // one entry e of A = dc/dw = [J_free | -P] (batch-major [B][m][nw]) from the CSR Jacobian values:

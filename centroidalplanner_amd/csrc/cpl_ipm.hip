@@ -120,6 +120,8 @@ __global__ __launch_bounds__(256) void cpl_ipm_optimality_kernel(
   const int64_t b = (int64_t)blockIdx.x * IPM_WAVES + (threadIdx.x >> 6);
   if (b >= batch) return;
   const int lane = threadIdx.x & 63;
+  // (the fused line search's flags cleared here, one launch before the search sets them)
+  if (b == 0 && lane == 0 && up.any_reset) up.any_reset[0] = up.any_reset[1] = 0;
   // the solve loop's unpack (IpmUnpack) at the iteration's barrier parameter and active flag
   auto unpack = [&](double mu_v, bool act_v) {
     if (!up.X) return;
@@ -460,51 +462,11 @@ constexpr int64_t NEWTON_WIDE_MAX = 1024;
 // dzU = mu/du - zU + zU/du dw, their fraction-to-the-boundary step a_z, the primal one a_max,
 // gd = grad_phi . dw, switch_ok = ls_switch_flags (gd < 0, theta <= theta_min), and delta_w_last <- delta_w on the
 // active instances.
-__global__ __launch_bounds__(256) void cpl_ipm_post_step_kernel(
-    int64_t batch, int nw, const double* __restrict__ w, const double* __restrict__ dw, const double* __restrict__ zL,
-    const double* __restrict__ zU, const double* __restrict__ gphi, const double* __restrict__ mu,
-    const double* __restrict__ tau, const uint8_t* __restrict__ hasL, const uint8_t* __restrict__ hasU,
-    const double* __restrict__ wl0, const double* __restrict__ wu0, const double* __restrict__ theta,
-    const double* __restrict__ theta_min, const uint8_t* __restrict__ active, const double* __restrict__ delta_w,
-    double* __restrict__ dwl, double* __restrict__ dzL, double* __restrict__ dzU, double* __restrict__ a_max,
-    double* __restrict__ a_z, double* __restrict__ gd_out, uint8_t* __restrict__ switch_ok, const LsSetupArgs ls) {
+__global__ __launch_bounds__(256) void cpl_ipm_post_step_kernel(int64_t batch, const PostStepArgs P,
+                                                                const LsSetupArgs ls) {
   const int64_t b = (int64_t)blockIdx.x * IPM_WAVES + (threadIdx.x >> 6);
   if (b >= batch) return;
-  const int lane = threadIdx.x & 63;
-  const double mub = mu[b], t = tau[b];
-  double rp = INFINITY, rz = INFINITY, gd = 0.0;
-  for (int k = lane; k < nw; k += 64) {
-    const double wk = w[b * nw + k], dk = dw[b * nw + k];
-    gd += gphi[b * nw + k] * dk;
-    double dzl = 0.0, dzu = 0.0;
-    if (hasL[k]) {
-      const double dl = wk - wl0[k], zl = zL[b * nw + k];
-      dzl = mub / dl - zl - zl / dl * dk;
-      if (dk < 0.0) rp = fmin(rp, -t * dl / dk);
-      if (dzl < 0.0) rz = fmin(rz, -t * zl / dzl);
-    }
-    if (hasU[k]) {
-      const double du = wu0[k] - wk, zu = zU[b * nw + k];
-      dzu = mub / du - zu + zu / du * dk;
-      if (dk > 0.0) rp = fmin(rp, -t * du / -dk);
-      if (dzu < 0.0) rz = fmin(rz, -t * zu / dzu);
-    }
-    dzL[b * nw + k] = dzl;
-    dzU[b * nw + k] = dzu;
-  }
-  rp = wave_min(rp);
-  rz = wave_min(rz);
-  gd = ipm_wave_sum(gd);
-  if (lane == 0) {
-    a_max[b] = fmin(rp, 1.0);
-    a_z[b] = fmin(rz, 1.0);
-    gd_out[b] = gd;
-    switch_ok[b] = ls_switch_flags(theta[b], theta_min[b], gd);
-    if (active[b]) dwl[b] = delta_w[b];
-  }
-  // the solve loop's line-search setup (ls.act != NULL; was the next launch): no output of this
-  // kernel is among its inputs except alpha_max and gd, passed in registers
-  if (ls.act) ls_setup_wave(b, nw, ls, fmin(rp, 1.0), gd);
+  ipm_post_step_one(P, b, ls);
 }
 
 // Acceptance (batch_ipm.py step, "accept" + state write-back, in place): filter augmentation after
@@ -615,9 +577,10 @@ int32_t ipm_post_step_ex(int64_t batch, int32_t nw, const double* d_w, const dou
                          double* d_a_z, double* d_gd, uint8_t* d_switch_ok, const LsSetupArgs* ls, void* stream) {
   LsSetupArgs L{};
   if (ls) L = *ls;
-  IPM_LAUNCH(cpl_ipm_post_step_kernel, "cpl_ipm_post_step", batch, (int)nw, d_w, d_dw, d_zL, d_zU, d_gphi, d_mu, d_tau,
-             d_hasL, d_hasU, d_wl0, d_wu0, d_theta, d_theta_min, d_active, d_delta_w, d_dwl, d_dzL, d_dzU, d_a_max,
-             d_a_z, d_gd, d_switch_ok, L);
+  const PostStepArgs P{(int32_t)nw, d_w, d_dw, d_zL, d_zU, d_gphi, d_mu, d_tau, d_hasL, d_hasU, d_wl0, d_wu0,
+                       d_theta, d_theta_min, d_active, d_delta_w, d_dwl, d_dzL, d_dzU, d_a_max, d_a_z, d_gd,
+                       d_switch_ok};
+  IPM_LAUNCH(cpl_ipm_post_step_kernel, "cpl_ipm_post_step", batch, P, L);
 }
 
 // cpl_ipm_optimality with the engine's extras: mu_rounds barrier decreases at most, the floor

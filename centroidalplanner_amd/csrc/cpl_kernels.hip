@@ -3074,6 +3074,10 @@ __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, c
   const int64_t b = blockIdx.x;
   if (b >= A.batch) return;
   const int lane = threadIdx.x;
+  if (FIRST && !GF && A.with_post) {  // the post-step quantities and the search's setup of this instance
+    ipm_post_step_one(A.post, b, A.setup);
+    __threadfence_block();  // (their stores before this wave's loads of them below)
+  }
   const bool act = A.act[b] != 0;
   bool searching = act && A.searching[b] != 0;
   double al = A.alpha[b];
@@ -3282,6 +3286,9 @@ __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, c
 }
 
 constexpr int64_t LS_GF_MIN = 2048;  // batches from this size re-solve from the factors in global memory
+// the fused first-trial kernel takes the post-step prologue (with_post) below LS_GF_MIN only: in the
+// global-factor form it would cost that kernel its second wave per SIMD (238 VGPRs + 24 AGPRs)
+bool ls_post_prologue(int64_t batch) { return batch < LS_GF_MIN; }
 
 int32_t ls_backtrack(const cpl_problem_desc* d, const LsBacktrackArgs& a, hipStream_t stream) {
   if (a.batch <= 0) return CPL_OK;
@@ -3297,6 +3304,8 @@ int32_t ls_backtrack(const cpl_problem_desc* d, const LsBacktrackArgs& a, hipStr
   const bool sq = d->env_kind == CPL_ENV_SUPERQUADRIC || d->env_kind == CPL_ENV_MIXED;
   if (d->env_kind == CPL_ENV_MIXED && !a.env_tag) return fail(CPL_ERR_INVALID_ARGUMENT, "ls_backtrack: mixed needs tags");
   const bool first = a.first != 0;
+  if (a.with_post && (!first || a.batch >= LS_GF_MIN))
+    return fail(CPL_ERR_INVALID_ARGUMENT, "ls_backtrack: the post-step prologue is for the first trial below LS_GF_MIN");
   if (first && (a.resto || a.nw != 47 || a.m != 30 || !a.c || !a.M || !a.r1 || !a.kkt_ws || !a.tau))
     return fail(CPL_ERR_INVALID_ARGUMENT, "ls_backtrack: the fused first trial needs a 47 x 30 system and its buffers");
   const size_t nL = sq ? (size_t)K.N * SQ_L : 0;

@@ -40,6 +40,7 @@ int32_t ipm_newton_setup_lm(int64_t batch, int32_t nw, int32_t m, int32_t nf, co
 // cpl_kernels.hip: the backtracking line search after the first trial, one wave per instance
 int32_t ls_backtrack(const cpl_problem_desc* d, const LsBacktrackArgs& a, hipStream_t stream);
 bool kkt_wave_size(int nw, int m);
+bool ls_post_prologue(int64_t batch);
 // cpl_ipm.hip: the post-step kernel with the line-search setup (LsSetupArgs) as its tail
 int32_t ipm_post_step_ex(int64_t batch, int32_t nw, const double* d_w, const double* d_dw, const double* d_zL,
                          const double* d_zU, const double* d_gphi, const double* d_mu, const double* d_tau,
@@ -2196,8 +2197,14 @@ int32_t step_phase(cpl_solver* S, int phase) {
         LAUNCHED("k_dense_a_prep");
       }
       // (with k_unpack_tau's X = unpack(w), tau and the active snapshot fused into its tail)
+      // the whole search in one launch (first trial, its corrections, the backtracking), the post-step
+      // quantities and the search's setup in that launch's prologue; or the first trial step by step
+      // and the remaining trials in one launch
+      const bool fused = o.ls_kernel == 2 || (o.ls_kernel == 1 && B <= FUSE_ROWS);  // (2: the default)
+      const bool fused_ls = fused && S->ls_fusable;
+      const bool post_in_ls = fused_ls && ls_post_prologue(B);  // (the search kernel's prologue)
       const IpmUnpack unp{n, S->freepos, S->Xbase, S->in_resto, S->X, S->tau, S->act,
-                          S->acc_w, S->acc_y, S->acc_zL, S->acc_zU, S->has_acc};
+                          S->acc_w, S->acc_y, S->acc_zL, S->acc_zU, S->has_acc, post_in_ls ? S->d_any : nullptr};
       CK(ipm_optimality_ex(B, nw, m, FMAX, S->nbounds, o.tol, o.acceptable_tol, o.acceptable_iter, S->A, S->gradw,
                            S->c, S->w, S->y, S->zL, S->zU, S->hasL, S->hasU, S->wl0, S->wu0, S->mu, S->filt_t,
                            S->filt_p, S->fcount, S->active, S->status, S->acc, S->d_inf, S->err0, S->base, S->mu_o,
@@ -2215,21 +2222,22 @@ int32_t step_phase(cpl_solver* S, int phase) {
                                 S->theta_k, S->phi_k, S->act, st));
       CK(cpl_kkt_solve(0, B, nw, m, S->M, S->A, S->r1, S->r2, S->mu_o, S->dwl, S->act, S->dw, S->dy, S->delta_w,
                        S->delta_c, S->info, S->ws, st));
-      {  // the step's multipliers / fraction-to-the-boundary, then (same launch) the search's setup
-        LsSetupArgs ls;
-        ls.m = m; ls.act = S->act; ls.w = S->w; ls.dw = S->dw; ls.dy = S->dy; ls.c = S->c; ls.f = S->f; ls.g = S->g;
-        ls.theta_k = S->theta_k; ls.theta_min = S->theta_min; ls.in_soft = S->in_soft; ls.soft_cnt = S->soft_cnt;
-        ls.tiny_last = S->tiny_last; ls.tiny_flag = S->tiny_flag; ls.tiny_now = S->tiny_now; ls.soft_now = S->soft_now;
-        ls.a_min = S->a_min; ls.searching = S->searching; ls.st_f = S->st_f; ls.st_g = S->st_g; ls.st_w = S->st_w;
-        ls.st_alpha = S->st_alpha; ls.st_aug = S->st_aug; ls.alpha = S->alpha; ls.any = S->d_any;
+      // the step's multipliers / fraction-to-the-boundary, then the search's setup: a launch of their
+      // own, or the fused search kernel's prologue
+      LsSetupArgs ls;
+      ls.m = m; ls.act = S->act; ls.w = S->w; ls.dw = S->dw; ls.dy = S->dy; ls.c = S->c; ls.f = S->f; ls.g = S->g;
+      ls.theta_k = S->theta_k; ls.theta_min = S->theta_min; ls.in_soft = S->in_soft; ls.soft_cnt = S->soft_cnt;
+      ls.tiny_last = S->tiny_last; ls.tiny_flag = S->tiny_flag; ls.tiny_now = S->tiny_now; ls.soft_now = S->soft_now;
+      ls.a_min = S->a_min; ls.searching = S->searching; ls.st_f = S->st_f; ls.st_g = S->st_g; ls.st_w = S->st_w;
+      ls.st_alpha = S->st_alpha; ls.st_aug = S->st_aug; ls.alpha = S->alpha; ls.any = S->d_any;
+      const PostStepArgs post{nw, S->w, S->dw, S->zL, S->zU, S->gphi, S->mu_o, S->tau, S->hasL, S->hasU, S->wl0,
+                              S->wu0, S->theta_k, S->theta_min, S->act, S->delta_w, S->dwl, S->dzL, S->dzU,
+                              S->a_max, S->a_z, S->gd, S->switch_ok};
+      if (!post_in_ls)
         CK(ipm_post_step_ex(B, nw, S->w, S->dw, S->zL, S->zU, S->gphi, S->mu_o, S->tau, S->hasL, S->hasU, S->wl0,
                             S->wu0, S->theta_k, S->theta_min, S->act, S->delta_w, S->dwl, S->dzL, S->dzU, S->a_max,
                             S->a_z, S->gd, S->switch_ok, &ls, st));
-      }
-      // the whole search in one launch (first trial, its corrections, the backtracking), or the
-      // first trial step by step and the remaining trials in one launch
-      const bool fused = o.ls_kernel == 2 || (o.ls_kernel == 1 && B <= FUSE_ROWS);  // (2: the default)
-      if (!(fused && S->ls_fusable)) CK(first_trial());
+      if (!fused_ls) CK(first_trial());
       if (fused && S->ls_fusable) {
         LsBacktrackArgs la;
         la.batch = B; la.n = n; la.m = m; la.nf = nf; la.nw = nw; la.nfilt = FMAX; la.max_trials = o.max_ls - 1;
@@ -2256,6 +2264,10 @@ int32_t step_phase(cpl_solver* S, int phase) {
           la.soft_ws = S->ws_; la.soft_X = S->Xs; la.soft_try = S->soft_try; la.a_soft = S->a_soft;
           S->soft_begun = true;
         }
+        la.post = post;
+        la.setup = ls;
+        la.setup.any = nullptr;  // (cleared by the optimality kernel: other waves set them concurrently)
+        la.with_post = post_in_ls ? 1 : 0;
         CK(ls_backtrack(&S->desc, la, st));
       } else if (o.max_ls > 1) {  // the remaining trials of every instance still searching, in one launch
         HK(hipMemsetAsync(S->d_any, 0, 2, st), "hipMemsetAsync flags");
@@ -2275,6 +2287,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
         la.pR = la.nR = la.dp = la.dn = la.wR = nullptr;
         la.st_p = la.st_n = nullptr;
         la.first = 0; la.max_soc = 0; la.c = la.M = la.r1 = la.kkt_ws = la.tau = nullptr;
+        la.with_post = 0;
         la.a_max = la.a_z = nullptr; la.soft_ws = la.soft_X = la.a_soft = nullptr; la.soft_try = nullptr;
         CK(ls_backtrack(&S->desc, la, st));
       }
@@ -2433,6 +2446,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
         la.pR = S->pR; la.nR = S->nR; la.dp = S->dp; la.dn = S->dn; la.wR = S->wR;
         la.st_p = S->st_p; la.st_n = S->st_n;
         la.first = 0; la.max_soc = 0; la.c = la.M = la.r1 = la.kkt_ws = la.tau = nullptr;
+        la.with_post = 0;
         la.a_max = la.a_z = nullptr; la.soft_ws = la.soft_X = la.a_soft = nullptr; la.soft_try = nullptr;
         CK(ls_backtrack(&S->desc, la, st));
       }
