@@ -171,7 +171,7 @@ class NativeSolver:
 
     def __init__(self, problem, batch, tol=1e-8, max_iter=3000, mu_init=0.1, acceptable_tol=1e-6,
                  acceptable_iter=15, max_ls=40, max_soc=4, hessian="exact", fd_step=1e-6, graph=True, compact=True,
-                 ls_kernel=2, fallback_viol_tol=1e-9):
+                 ls_kernel=2, fallback_viol_tol=0.0):
         o = _abi.SolveOptions()
         _abi.lib.cpl_solve_options_default(ctypes.byref(o))
         o.max_iter, o.max_ls, o.max_soc, o.acceptable_iter = int(max_iter), int(max_ls), int(max_soc), int(acceptable_iter)
@@ -259,7 +259,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                     acceptable_iter: int = 15, max_ls: int = 40, max_soc: int = 4, hessian: str = "exact",
                     fd_step: float = 1e-6, graph: Optional[bool] = None, check_every: int = 4,
                     verbose: int = 0, compact: bool = True, verbose_instance: int = 0,
-                    ls_kernel: int = 2, fallback_viol_tol: float = 1e-9) -> BatchSolveResult:
+                    ls_kernel: int = 2, fallback_viol_tol: float = 0.0) -> BatchSolveResult:
     """Solve B instances of `problem`'s template from the starting points X0 [B, n] (torch float64,
     device tensor), per-instance robot masses `mass` [B] (None: the template's).
 
@@ -274,7 +274,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     ls_kernel (device engine): the whole line search (first trial, its corrections, backtracking) in
     one launch for 47 x 30 systems — 2 (default): always, 1: batches of at most 256 rows, 0: never;
     the same iterates bit for bit.
-    fallback_viol_tol (not IPOPT, which returns its last iterate; <= 0: off): an instance that stops
+    fallback_viol_tol (opt-in, default 0 = off; not IPOPT, which returns its last iterate): an instance that stops
     without converging at an iterate violating its original constraints by more than this returns the
     lowest-objective iterate it met that satisfied them to this tolerance (result.fallback)."""
     if hessian not in ("exact", "fd", "limited-memory"):

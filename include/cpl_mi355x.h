@@ -514,12 +514,14 @@ typedef struct cpl_solve_options {
   double acceptable_tol;   /* 1e-6 */
   double mu_init;          /* 0.1 */
   double fd_step;          /* 1e-6 (CPL_HESSIAN_FD / Superquadric exact) */
-  double fallback_viol_tol; /* 1e-9; <= 0 off.  Not IPOPT (which returns its last iterate): a solve that
-                              ends without convergence (max_iter, local infeasibility, restoration
-                              failure) at an iterate whose original constraints are violated by more
-                              than this returns the lowest-objective iterate it met that satisfied
-                              them to this tolerance, when there was one (status unchanged;
-                              cpl_solver_fallbacks says which instances) */
+  double fallback_viol_tol; /* 0 (off, the default: IPOPT returns its last iterate).  Opt-in, not IPOPT:
+                              > 0 — a solve that ends without convergence (max_iter, local infeasibility,
+                              restoration failure) at an iterate whose original constraints are
+                              violated by more than this returns the lowest-objective iterate it met
+                              that satisfied them to this tolerance, when there was one (status
+                              unchanged; cpl_solver_fallbacks says which instances).  Only x is
+                              replaced: the multipliers and dual_inf of such an instance still belong
+                              to its last iterate. */
 } cpl_solve_options;
 
 typedef struct cpl_solver cpl_solver;

@@ -21,6 +21,9 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #include "../include/cpl_mi355x.h"
 
@@ -146,7 +149,7 @@ static double barrier(const Prob* P, const double* w, double mu) {
 static void lagr_hessian(const Prob* P, const double* X, const double* Y, int zero_cost, double* Hf) {
   const cpl_problem_desc* d = P->d;
   const int N = d->n_contacts, n = P->n;
-  static double H[NMAX * NMAX];
+  static __thread double H[NMAX * NMAX];
   memset(H, 0, sizeof(double) * (size_t)n * n);
   const int crow = (d->env_kind == 1 || d->env_kind == 2 || d->env_kind == 3) ? 6 : 2;
   int pos[CPL_MAX_CONTACTS];
@@ -274,7 +277,7 @@ typedef struct {
 
 /* Householder QR of At (nw x m): Q (nw x nw) and R (m x m) */
 static void householder_qr(const double* At, int nw, int m, double* Q, double* R) {
-  static double Wk[NWMAX * MMAX];
+  static __thread double Wk[NWMAX * MMAX];
   memcpy(Wk, At, sizeof(double) * (size_t)nw * m);
   for (int i = 0; i < nw; ++i)
     for (int j = 0; j < nw; ++j) Q[i * nw + j] = i == j ? 1.0 : 0.0;
@@ -310,7 +313,7 @@ static void householder_qr(const double* At, int nw, int m, double* Q, double* R
 
 /* factorise: QR of A^T, delta_c on R's small diagonal, the reduced Hessian with the inertia test */
 static double kkt_factor(Kkt* k, const double* M, const double* A, int nw, int m, double mu, double dwl) {
-  static double At[NWMAX * MMAX];
+  static __thread double At[NWMAX * MMAX];
   k->nw = nw; k->m = m; k->nz = nw - m;
   memcpy(k->A, A, sizeof(double) * (size_t)m * nw);
   for (int i = 0; i < nw; ++i)
@@ -331,7 +334,7 @@ static double kkt_factor(Kkt* k, const double* M, const double* A, int nw, int m
   double dmx = 0.0;
   for (int i = 0; i < nw; ++i) dmx = dmax(dmx, fabs(M[i * nw + i]));
   /* Hr = Z^T M Z, symmetrised */
-  static double MZ[NWMAX * NWMAX], Hr[NWMAX * NWMAX];
+  static __thread double MZ[NWMAX * NWMAX], Hr[NWMAX * NWMAX];
   for (int i = 0; i < nw; ++i)
     for (int c = 0; c < nz; ++c) {
       double s = 0.0;
@@ -439,7 +442,7 @@ static void kkt_solve(const Kkt* k, const double* q1, const double* q2, double* 
  * correction; dw = K^-1 (r1 + A^T Dinv r2), dy = Dinv (A dw - r2) */
 static double kkt_qd(const double* W, const double* A, const double* Dinv, const double* r1, const double* r2,
                      int nw, int m, double dwl, double* dw, double* dy) {
-  static double K[NWMAX * NWMAX], L[NWMAX * NWMAX];
+  static __thread double K[NWMAX * NWMAX], L[NWMAX * NWMAX];
   for (int i = 0; i < nw; ++i)
     for (int j = 0; j < nw; ++j) {
       double s = 0.0;
@@ -587,7 +590,7 @@ static double err_mu(const Prob* P, const Errors* E, double mu) {
 static double pd_error(const Prob* P, const Eval* o, const double* w, const double* y, const double* zl,
                        const double* zu, double mu) {
   const int nw = P->nw, m = P->m, nf = P->nf;
-  static double A[MMAX * NWMAX];
+  static __thread double A[MMAX * NWMAX];
   double c[MMAX];
   jac_w(P, o->J, A);
   cons(P, o->g, w, c);
@@ -722,7 +725,7 @@ static void enter_resto(const Prob* P, State* S, const double* c, const double* 
     S->wR[k] = S->w[k];
   }
   /* least-squares multipliers: the p / n-eliminated system with W = I, Sigma_p = Sigma_n = 1 */
-  static double Wi[NWMAX * NWMAX];
+  static __thread double Wi[NWMAX * NWMAX];
   double Dinv[MMAX], r1[NWMAX], r2[MMAX], dw[NWMAX], yR[MMAX];
   for (int i = 0; i < nw; ++i)
     for (int j = 0; j < nw; ++j) Wi[i * nw + j] = i == j ? 1.0 : 0.0;
@@ -785,9 +788,9 @@ static void leave_resto(const Prob* P, State* S, const double* w_new) {
 /* One regular iteration (batch_ipm.py regular_step) */
 static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
   const int nw = P->nw, m = P->m, nf = P->nf;
-  static Kkt K;
-  static double M[NWMAX * NWMAX];
-  static Eval trial, tsoc, ev_new;
+  static __thread Kkt K;
+  static __thread double M[NWMAX * NWMAX];
+  static __thread Eval trial, tsoc, ev_new;
   double mu = S->mu;
   if (E->err0 <= o->acceptable_tol) {  /* StoreAcceptablePoint (CurrentIsAcceptable) */
     memcpy(S->acc_w, S->w, sizeof(double) * (size_t)nw);
@@ -910,7 +913,7 @@ static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
   int soft_ok = 0;
   if (soft_try) {
     double wsft[NWMAX], Xsft[NMAX], ys[MMAX], zLs[NWMAX], zUs[NWMAX], cs[MMAX];
-    static Eval os;
+    static __thread Eval os;
     for (int k = 0; k < nw; ++k) wsft[k] = w[k] + a_soft * dw[k];
     unpack(P, wsft, Xsft);
     evaluate(P, Xsft, &os);
@@ -981,8 +984,8 @@ static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
 /* One restoration-phase iteration (batch_ipm.py resto_step) */
 static void resto_step(Prob* P, State* S, const Opts* o) {
   const int nw = P->nw, m = P->m, nf = P->nf;
-  static double A[MMAX * NWMAX], W[NWMAX * NWMAX];
-  static Eval trial, ev_new;
+  static __thread double A[MMAX * NWMAX], W[NWMAX * NWMAX];
+  static __thread Eval trial, ev_new;
   double c[MMAX], DR2[NWMAX];
   const double* w = S->w;
   jac_w(P, S->cur.J, A);
@@ -1174,6 +1177,11 @@ static void resto_step(Prob* P, State* S, const Opts* o) {
   if (isfinite(th_o) && isfinite(ph_o) && th_o <= KAPPA_RESTO * t0 && in_filter && vs_start) leave_resto(P, S, st_w);
 }
 
+/* The best-feasible-iterate fallback (not IPOPT; cpl_solve_options.fallback_viol_tol): off (0) by
+ * default like the engine's; cplo_set_fallback_viol_tol opts in (process-wide). */
+static double g_fallback_viol_tol = 0.0;
+void cplo_set_fallback_viol_tol(double v) { g_fallback_viol_tol = v; }
+
 /* Solve one instance from x0 (IFOPT's IpoptSolver defaults: limited-memory Hessian; exact_hessian:
  * the analytic Lagrangian Hessian, batch_ipm.py's hessian="exact", Ground / no environment).  Returns 0;
  * x_out [n] (projected onto the original bounds), status (0 optimal, 1 acceptable, 2 max_iter,
@@ -1181,9 +1189,10 @@ static void resto_step(Prob* P, State* S, const Opts* o) {
 int cplo_solve(const cpl_problem_desc* d, const double* x0, double mass, int max_iter, double tol, int exact_hessian,
                double* x_out,
                int32_t* status, int32_t* iterations, double* objective, int32_t* restorations, int64_t* evaluations) {
-  static Prob P;
-  static State S;
-  static Errors E;
+  /* per thread (cplo_time_solve_mt solves instances on OpenMP threads): large, so not on the stack */
+  static __thread Prob P;
+  static __thread State S;
+  static __thread Errors E;
   int32_t n, m, nnz;
   if (cplo_dims(d, &n, &m, &nnz) || n > NMAX || m > MMAX || nnz > 4096) return CPL_ERR_UNSUPPORTED;
   memset(&P, 0, sizeof(P));
@@ -1222,7 +1231,7 @@ int cplo_solve(const cpl_problem_desc* d, const double* x0, double mass, int max
   P.ws = cplo_ws_new(d);
   if (!P.ws) return CPL_ERR_RUNTIME;
   for (int j = 0; j < n; ++j) P.Xbase[j] = P.is_fixed[j] ? P.xl[j] : x0[j];
-  Opts o = {tol, 1e-6, dmin(tol, COMPL_INF_TOL) / (BARRIER_TOL_FACTOR + 1.0), 1e-9, 15, 40, 4};
+  Opts o = {tol, 1e-6, dmin(tol, COMPL_INF_TOL) / (BARRIER_TOL_FACTOR + 1.0), g_fallback_viol_tol, 15, 40, 4};
   /* starting point: x pushed into its bounds, slacks = g_I(x) pushed into theirs */
   const int nw = P.nw, nf = P.nf;
   double w0[NWMAX], Xs[NMAX];
@@ -1241,7 +1250,7 @@ int cplo_solve(const cpl_problem_desc* d, const double* x0, double mass, int max
   S.theta_max = 1e4 * dmax(theta0, 1.0);
   S.theta_min = 1e-4 * dmax(theta0, 1.0);
   {  /* least-squares constraint multipliers (constr_mult_init_max = 1e3) */
-    static double A0[MMAX * NWMAX], AAt[MMAX * MMAX];
+    static __thread double A0[MMAX * NWMAX], AAt[MMAX * MMAX];
     double rhs[MMAX];
     jac_w(&P, S.cur.J, A0);
     for (int a = 0; a < m; ++a) {
@@ -1273,7 +1282,7 @@ int cplo_solve(const cpl_problem_desc* d, const double* x0, double mass, int max
       if (S.resto) resto_step(&P, &S, &o);
       else regular_step(&P, &S, &E, &o);
     }
-    if (S.active && orig_violation(&P, S.cur.g) <= o.fallback_viol_tol && S.cur.f < S.best_f) {
+    if (o.fallback_viol_tol > 0.0 && S.active && orig_violation(&P, S.cur.g) <= o.fallback_viol_tol && S.cur.f < S.best_f) {
       memcpy(S.best_w, S.w, sizeof(double) * (size_t)nw);
       S.best_f = S.cur.f;
     }
@@ -1283,7 +1292,8 @@ int cplo_solve(const cpl_problem_desc* d, const double* x0, double mass, int max
     errors(&P, &S.cur, S.w, S.y, S.zL, S.zU, &E);
     check(&S, &E, &o);
   }
-  if (S.status > ST_ACCEPTABLE && orig_violation(&P, S.cur.g) > o.fallback_viol_tol && isfinite(S.best_f))
+  if (o.fallback_viol_tol > 0.0 && S.status > ST_ACCEPTABLE && orig_violation(&P, S.cur.g) > o.fallback_viol_tol &&
+      isfinite(S.best_f))
     memcpy(S.w, S.best_w, sizeof(double) * (size_t)nw);
   double X[NMAX], gfin[MMAX], f = 0.0;
   unpack(&P, S.w, X);
@@ -1312,5 +1322,31 @@ double cplo_time_solve(const cpl_problem_desc* d, int64_t count, const double* x
                    iterations ? iterations + b : NULL, NULL, NULL, NULL))
       return -1.0;
   clock_gettime(CLOCK_MONOTONIC, &t1);
+  return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+/* The same over `threads` OpenMP threads (<= 0: omp_get_max_threads()), instances split statically:
+ * the all-core CPU baseline of the solve legs; wall-clock seconds, -1 on failure */
+double cplo_time_solve_mt(const cpl_problem_desc* d, int64_t count, const double* x0, const double* mass, int max_iter,
+                          double tol, int exact_hessian, int threads, int32_t* status, int32_t* iterations) {
+  int32_t n, m, nnz;
+  if (cplo_dims(d, &n, &m, &nnz)) return -1.0;
+#ifdef _OPENMP
+  if (threads <= 0) threads = omp_get_max_threads();
+#else
+  threads = 1;
+#endif
+  struct timespec t0, t1;
+  int failed = 0;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+#pragma omp parallel for schedule(dynamic, 4) num_threads(threads) reduction(| : failed)
+  for (int64_t b = 0; b < count; ++b) {
+    double xo[NMAX];
+    if (cplo_solve(d, x0 + b * n, mass ? mass[b] : d->mass, max_iter, tol, exact_hessian, xo, status ? status + b : NULL,
+                   iterations ? iterations + b : NULL, NULL, NULL, NULL))
+      failed |= 1;
+  }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  if (failed) return -1.0;
   return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }

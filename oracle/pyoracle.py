@@ -41,6 +41,11 @@ def _load():
     lib.cplo_solve.restype = c_int
     lib.cplo_time_solve.argtypes = [c_void_p, c_int64, c_void_p, c_void_p, c_int, c_double, c_int, c_void_p, c_void_p]
     lib.cplo_time_solve.restype = c_double
+    lib.cplo_time_solve_mt.argtypes = [c_void_p, c_int64, c_void_p, c_void_p, c_int, c_double, c_int, c_int, c_void_p,
+                                       c_void_p]
+    lib.cplo_time_solve_mt.restype = c_double
+    lib.cplo_set_fallback_viol_tol.argtypes = [c_double]
+    lib.cplo_set_fallback_viol_tol.restype = None
     return lib
 
 
@@ -151,6 +156,29 @@ def time_solve(desc, x0, mass=None, max_iter=3000, tol=1e-8, hessian="limited-me
     if t < 0:
         raise ValueError("oracle solve timing failed")
     return t, st, it
+
+
+def time_solve_mt(desc, x0, mass=None, max_iter=3000, tol=1e-8, hessian="limited-memory", threads=0):
+    """time_solve over `threads` OpenMP threads (0: all of OMP_NUM_THREADS / the affinity mask), the
+    instances split dynamically: the all-core CPU baseline of the solve legs.  Every instance takes the
+    iterates of its single-thread solve (the solver state is per thread)."""
+    n, _, _ = dims(desc)
+    x0 = np.ascontiguousarray(x0, dtype=np.float64).reshape(-1, n)
+    cnt = x0.shape[0]
+    mass = None if mass is None else np.ascontiguousarray(mass, dtype=np.float64)
+    st = np.zeros(cnt, dtype=np.int32)
+    it = np.zeros(cnt, dtype=np.int32)
+    t = lib.cplo_time_solve_mt(ctypes.byref(desc), cnt, _p(x0), _p(mass), int(max_iter), float(tol),
+                               int(hessian == "exact"), int(threads), _p(st), _p(it))
+    if t < 0:
+        raise ValueError("oracle solve timing failed")
+    return t, st, it
+
+
+def set_fallback_viol_tol(v):
+    """Opt in to the best-feasible-iterate fallback (not IPOPT) in the compiled restatement: v > 0;
+    0 (the default, like the engine's) returns the last iterate as IPOPT does."""
+    lib.cplo_set_fallback_viol_tol(float(v))
 
 
 def max_threads():

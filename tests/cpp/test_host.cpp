@@ -313,8 +313,8 @@ static void check_balance(const solver::Solution& sol, double mass, const std::v
     const double fn = dot3(v.force_value, v.normal_value);
     Vector3d ft;
     for (int k = 0; k < 3; ++k) ft[k] = v.force_value[k] - fn * v.normal_value[k];
-    CHECK(-fn <= 1e-9);                           // TestBasic.cpp:117-124 (cone signs)
-    CHECK(norm3(ft) - mu * fn <= 1e-9);
+    CHECK(-fn <= 0.0);                            // TestBasic.cpp:122-123 (cone signs, as asserted there)
+    CHECK(norm3(ft) - mu * fn <= 0.0);
   }
   NEAR(F[0], w[0], 1e-6);
   NEAR(F[1], w[1], 1e-6);
