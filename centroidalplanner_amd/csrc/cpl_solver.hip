@@ -2669,7 +2669,7 @@ void cpl_solve_options_default(cpl_solve_options* o) {
   o->acceptable_tol = 1e-6;
   o->mu_init = 0.1;
   o->fd_step = 1e-6;
-  o->fallback_viol_tol = 1e-9;
+  o->fallback_viol_tol = 0.0;  // off: IPOPT returns its last iterate
 }
 
 int32_t cpl_solver_destroy(cpl_solver* S) {

@@ -44,8 +44,20 @@
 /* ---------------------------------------------------------------------------------------- */
 /* Eigen 3.3 fixed-size 3-vector arithmetic as the reference sees it                         */
 /* ---------------------------------------------------------------------------------------- */
+#ifdef CPLO_EIGEN_REDUX_NOVEC
+/* Eigen's reduction WITHOUT packet math for a 3-vector (a build without SSE2 vectorisation, or an AVX
+ * build, whose 4-double packets are longer than a Vector3d): redux_novec_unroller splits the 3 terms
+ * as 1 + 2, i.e. a0 b0 + (a1 b1 + a2 b2).  The reference's Eigen build is unpinned; this variant of the
+ * oracle (oracle/_build/libcpl_oracle_novec.so) quantifies how far the two orders lie apart
+ * (tests/test_eigen_order.py). */
+static double edot(const double* a, const double* b) { return a[0] * b[0] + (a[1] * b[1] + a[2] * b[2]); }
+static double esqn(const double* a) { return a[0] * a[0] + (a[1] * a[1] + a[2] * a[2]); }
+#else
+/* Eigen 3.3 on x86-64 with its default SSE2 packets (2 doubles): the packet (a0 b0, a1 b1) is
+ * reduced first, then the tail a2 b2 is added: (a0 b0 + a1 b1) + a2 b2 */
 static double edot(const double* a, const double* b) { return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]; }
 static double esqn(const double* a) { return (a[0] * a[0] + a[1] * a[1]) + a[2] * a[2]; }
+#endif
 static double enorm(const double* a) { return sqrt(esqn(a)); }
 /* Eigen MatrixBase::cross: (a1 b2 - a2 b1, a2 b0 - a0 b2, a0 b1 - a1 b0) */
 static void ecross(const double* a, const double* b, double* o) {

@@ -13,13 +13,14 @@ from ctypes import POINTER, c_double, c_int, c_int32, c_int64, c_void_p
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "libcpl_oracle.so")
+# CPL_ORACLE_LIB: another build of the same sources (scripts/sanitize.sh points it at the ASan/UBSan one)
+LIB_PATH = os.environ.get("CPL_ORACLE_LIB") or os.path.join(HERE, "_build", "libcpl_oracle.so")
 
 
-def _load():
-    if not os.path.exists(LIB_PATH):
+def _load(path=LIB_PATH):
+    if not os.path.exists(path):
         subprocess.run(["make", "-s", "-C", HERE], check=True)
-    lib = ctypes.CDLL(LIB_PATH)
+    lib = ctypes.CDLL(path)
     IP = POINTER(c_int32)
     DP = POINTER(c_double)
     lib.cplo_dims.argtypes = [c_void_p, IP, IP, IP]
@@ -50,6 +51,15 @@ def _load():
 
 
 lib = _load()
+_variants = {}
+
+
+def variant_lib(name):
+    """The oracle built with a variant switch: "novec" = Eigen's non-vectorised 3-vector reduction
+    order a0 b0 + (a1 b1 + a2 b2) (cpl_oracle.c CPLO_EIGEN_REDUX_NOVEC) instead of SSE2's."""
+    if name not in _variants:
+        _variants[name] = _load(os.path.join(HERE, "_build", f"libcpl_oracle_{name}.so"))
+    return _variants[name]
 
 
 def _p(a):
@@ -86,8 +96,9 @@ def bounds(desc):
     return xl, xu, gl, gu
 
 
-def eval_batch(desc, x, mass=None, env_tag=None, outputs=("g", "jac", "f", "grad"), nthreads=None):
-    """x: float64 [B, n] host array.  Returns dict of host arrays."""
+def eval_batch(desc, x, mass=None, env_tag=None, outputs=("g", "jac", "f", "grad"), nthreads=None, variant=None):
+    """x: float64 [B, n] host array.  Returns dict of host arrays.  variant: see variant_lib."""
+    L = lib if variant is None else variant_lib(variant)
     n, m, nnz = dims(desc)
     x = np.ascontiguousarray(x, dtype=np.float64).reshape(-1, n)
     B = x.shape[0]
@@ -96,8 +107,8 @@ def eval_batch(desc, x, mass=None, env_tag=None, outputs=("g", "jac", "f", "grad
     shapes = {"g": (B, m), "jac": (B, nnz), "f": (B,), "grad": (B, n)}
     out = {k: np.zeros(shapes[k]) for k in outputs}
     if nthreads is None:
-        nthreads = lib.cplo_max_threads()
-    st = lib.cplo_eval_batch(ctypes.byref(desc), B, _p(x), _p(mass), _p(env_tag), _p(out.get("g")),
+        nthreads = L.cplo_max_threads()
+    st = L.cplo_eval_batch(ctypes.byref(desc), B, _p(x), _p(mass), _p(env_tag), _p(out.get("g")),
                              _p(out.get("jac")), _p(out.get("f")), _p(out.get("grad")), int(nthreads))
     if st:
         raise ValueError(f"oracle eval failed: {st}")
