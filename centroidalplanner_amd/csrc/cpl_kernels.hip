@@ -213,11 +213,11 @@ constexpr int NORM_HDR = 128;
 
 // partial pair per WAVE (tile kernel): DPP wave reductions and no barrier, so the reduction adds no
 // synchronisation to a workgroup's critical path (the block reduction with its two barriers cost the
-// latency-bound Superquadric tiles 14 %); pair index blockIdx.x * waves + wave
-__device__ __forceinline__ void partial_norms_waves(const NormAcc& a, double* __restrict__ part) {
+// latency-bound Superquadric tiles 14 %); pair index slot * waves + wave (slot: the tile)
+__device__ __forceinline__ void partial_norms_waves(const NormAcc& a, double* __restrict__ part, int64_t slot) {
   const double bm = wave_max(a.vmax), bs = wave_sum(a.vsum);
   if ((threadIdx.x & 63) == 0) {
-    const int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t i = slot * (blockDim.x >> 6) + (threadIdx.x >> 6);
     part[2 * i] = bm;
     part[2 * i + 1] = bs;
   }
@@ -1338,14 +1338,15 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
   const int T = K.T;
   const int n = K.n, m = K.m, nnz = K.nnz, N = K.N;
   const int64_t count = LIST ? (int64_t)*d_count : batch;
-  NormAcc nacc;
-  nacc.init(tid, WG, m);
   // LIST: one workgroup per tile the list may hold (the list's length is known on the device only; a
   // persistent walk over the list's tiles measured slower: 149-155 VGPRs against 114, three waves per
-  // SIMD instead of four — profiles/r4/ab_split5)
+  // SIMD instead of four — profiles/r4/ab_split5; and again in round 5 with the next tile's x
+  // prefetched into registers, for the contiguous Superquadric tiles too: 149-165 VGPRs, sq8 0.395
+  // against 0.307 ms, profiles/r5/)
   const int64_t b0 = (int64_t)blockIdx.x * T;
   if (LIST && b0 >= count) {  // past the list's tiles: zero partials
-    if (K.want_norms) partial_norms_waves(nacc, norms_ws + NORM_HDR);
+    NormAcc nacc;
+    if (K.want_norms) partial_norms_waves(nacc, norms_ws + NORM_HDR, blockIdx.x);
     return;
   }
   const int valid = (int)((count - b0) < T ? (count - b0) : T);
@@ -1391,41 +1392,48 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
   } else {
     copy_in<WG>(X, x + b0 * n, valid * n, tid, K.x_aligned16 != 0);
   }
-  int n_sq = ENVK == CPL_ENV_SUPERQUADRIC ? valid : 0;
-  if (ENVK == CPL_ENV_MIXED) {
-    // compact the tile's instances by environment kind so that every wave runs one code path
-    if (tid < 64) {
-      const bool is_sq = tid < valid && env_tag[b0 + tid] == CPL_ENV_SUPERQUADRIC;
-      const unsigned long long mask = __ballot(is_sq);
-      if (tid < valid) {
-        const int before = __popcll(mask & ((1ull << tid) - 1ull));
-        if (is_sq) lists[before] = tid;
-        else lists[64 + tid - before] = tid;
+  {
+    int n_sq = ENVK == CPL_ENV_SUPERQUADRIC ? valid : 0;
+    if (ENVK == CPL_ENV_MIXED) {
+      // compact the tile's instances by environment kind so that every wave runs one code path
+      if (tid < 64) {
+        const bool is_sq = tid < valid && env_tag[b0 + tid] == CPL_ENV_SUPERQUADRIC;
+        const unsigned long long mask = __ballot(is_sq);
+        if (tid < valid) {
+          const int before = __popcll(mask & ((1ull << tid) - 1ull));
+          if (is_sq) lists[before] = tid;
+          else lists[64 + tid - before] = tid;
+        }
+        if (tid == 0) lists[128] = __popcll(mask);
       }
-      if (tid == 0) lists[128] = __popcll(mask);
     }
-  }
-  __syncthreads();
-  if (ENVK == CPL_ENV_MIXED) n_sq = lists[128];
-  const int n_gr = valid - n_sq;
-  const bool compute = K.ablate != 1;
+    __syncthreads();
+    if (ENVK == CPL_ENV_MIXED) n_sq = lists[128];
+    const int n_gr = valid - n_sq;
+    const bool compute = K.ablate != 1;
 
-  // ---- phase 1: the Superquadric power ladders (into the LDS scratch); phase 2: the Superquadric
-  // rows.  The items that do not read the scratch (Ground / no-env contacts, statics, cost) join
-  // phase 1 for Superquadric batches, so that the two barrier-separated phases carry comparable work
-  // (sq8 0.347 -> 0.329 ms), and phase 2 for mixed batches, where the tile's Ground contacts then
-  // overlap the Superquadric rows (3.50 -> 3.44 ms for mixed16; profiles/r3/ab_*).  SQ items run
-  // axis-major (item -> (axis, contact, instance)).
-  constexpr bool OTHERS_FIRST = ENVK != CPL_ENV_MIXED;
-  const bool wgj = K.want_g || K.want_j;
-  if (compute) {
-    const int r_ax = (HAS_SQ && wgj) ? 3 * N * n_sq : 0;
+    // ---- phase 1: the Superquadric power ladders (into the LDS scratch); phase 2: the Superquadric
+    // rows.  The items that do not read the scratch (Ground / no-env contacts, statics, cost) join
+    // phase 1 for Superquadric batches, so that the two barrier-separated phases carry comparable work
+    // (sq8 0.347 -> 0.329 ms), and phase 2 for mixed batches, where the tile's Ground contacts then
+    // overlap the Superquadric rows (3.50 -> 3.44 ms for mixed16; profiles/r3/ab_*).  SQ items run
+    // axis-major (item -> (axis, contact, instance)).
+    constexpr bool OTHERS_FIRST = ENVK != CPL_ENV_MIXED;
+    const bool wgj = K.want_g || K.want_j;
+    // Superquadric batches (UAX): the items of one axis are padded to whole waves (PA items, a multiple
+    // of 64), so the axis is wave-uniform — a scalar: the per-axis factors are scalar operands, the
+    // power ladders' exponent loops uniform (with a lane-varying axis every ladder was a divergent loop
+    // and every factor a per-lane select) — and (contact, tile row) = (kj >> logT, kj & (T - 1)) with
+    // the rows past `valid` idle (no divisions).  Mixed tiles keep the ballot-compacted mapping.
+    constexpr bool UAX = ENVK == CPL_ENV_SUPERQUADRIC;
+    const int per_axis = UAX ? (N << K.logT) : N * n_sq;
+    const int PA = UAX ? ((per_axis + 63) & ~63) : per_axis;
+    const int r_ax = (HAS_SQ && wgj) ? 3 * PA : 0;
     const int r_gr = (ENVK != CPL_ENV_SUPERQUADRIC && wgj) ? N * n_gr : 0;
     const int r_st = wgj ? (JD ? 1 : 4) * valid : 0;  // (JD: the statics J rows by statics_rows_coop)
     double* com6 = smem + K.offA;                        // (JD) [T][6]
     const int r_co = K.cost_seg >= 0 ? valid : 0;
     const int r_oth = r_gr + r_st + r_co;
-    const int per_axis = N * n_sq;
     auto other_item = [&](int e) {
       if (e < r_gr) {
         const int j = e % n_gr, k = e / n_gr;
@@ -1453,68 +1461,88 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
     // Each phase as two loops over the same item -> thread mapping (Superquadric items, then the
     // others): one item function per loop body, so the register allocation of the two does not add up.
     const int items1 = r_ax + (OTHERS_FIRST ? r_oth : r_oth - r_gr);
-    if (HAS_SQ)
-      for (int it = tid; it < r_ax; it += WG) {
-        const int a = it / per_axis, kj = it - a * per_axis;
-        const int k = kj / n_sq, j = kj - k * n_sq;
-        const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
-        sq_axis_item<ENVK == CPL_ENV_MIXED>(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m);
-      }
-    for (int it = tid; it < items1; it += WG)
-      if (it >= r_ax) other_item(it - r_ax + (OTHERS_FIRST ? 0 : r_gr));
+    if (compute) {
+      if (HAS_SQ && UAX)
+        for (int it = tid; it < r_ax; it += WG) {
+          const int a = __builtin_amdgcn_readfirstlane(it) / PA, kj = it - a * PA;
+          const int k = kj >> K.logT, r = kj & (T - 1);
+          if (kj < per_axis && r < valid) sq_axis_item<false>(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m);
+        }
+      else if (HAS_SQ)
+        for (int it = tid; it < r_ax; it += WG) {
+          const int a = it / per_axis, kj = it - a * per_axis;
+          const int k = kj / n_sq, j = kj - k * n_sq;
+          const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
+          sq_axis_item<ENVK == CPL_ENV_MIXED>(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m);
+        }
+      for (int it = tid; it < items1; it += WG)
+        if (it >= r_ax) other_item(it - r_ax + (OTHERS_FIRST ? 0 : r_gr));
+    }
     // LDS-only barriers from here on: the phases exchange LDS data only, and a __syncthreads would
     // first wait for every global store the items issued (f, and with jdirect the Jacobian rows)
-    if (HAS_SQ && n_sq > 0 && wgj) lds_barrier();
-    const int r_rows = r_ax;
-    // Superquadric batches: the friction cones as items of their own in phase 2 (the workgroup's
-    // fourth wave, otherwise idle there: the row-1 items no longer carry them)
-    constexpr bool CONE_ITEMS = ENVK == CPL_ENV_SUPERQUADRIC;
-    const int r_cone = (CONE_ITEMS && wgj) ? per_axis : 0;
-    const int items2 = r_rows + (OTHERS_FIRST ? 0 : r_gr) + r_cone;
-    if (HAS_SQ)
-      for (int it = tid; it < r_rows; it += WG) {
-        const int a = it / per_axis, kj = it - a * per_axis;
-        const int k = kj / n_sq, j = kj - k * n_sq;
-        const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
-        sq_row_item<ENVK == CPL_ENV_MIXED, !CONE_ITEMS>(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m, JR(r));
+    if (compute && HAS_SQ && n_sq > 0 && wgj) lds_barrier();
+    if (compute) {
+      const int r_rows = r_ax;
+      // Superquadric batches: the friction cones as items of their own in phase 2 (the workgroup's
+      // fourth wave, otherwise idle there: the row-1 items no longer carry them)
+      constexpr bool CONE_ITEMS = ENVK == CPL_ENV_SUPERQUADRIC;
+      const int r_cone = (CONE_ITEMS && wgj) ? per_axis : 0;
+      const int items2 = r_rows + (OTHERS_FIRST ? 0 : r_gr) + r_cone;
+      if (HAS_SQ && UAX)
+        for (int it = tid; it < r_rows; it += WG) {
+          const int a = __builtin_amdgcn_readfirstlane(it) / PA, kj = it - a * PA;
+          const int k = kj >> K.logT, r = kj & (T - 1);
+          if (kj < per_axis && r < valid)
+            sq_row_item<false, !CONE_ITEMS>(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m, JR(r));
+        }
+      else if (HAS_SQ)
+        for (int it = tid; it < r_rows; it += WG) {
+          const int a = it / per_axis, kj = it - a * per_axis;
+          const int k = kj / n_sq, j = kj - k * n_sq;
+          const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
+          sq_row_item<ENVK == CPL_ENV_MIXED, !CONE_ITEMS>(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m,
+                                                          JR(r));
+        }
+      for (int it = tid; it < items2; it += WG) {
+        if (it < r_rows) continue;
+        if (CONE_ITEMS) {
+          const int e = it - r_rows, k = e >> K.logT, r = e & (T - 1);
+          if (r < valid) sq_cone_item(K, X + r * n, k, Gt + r * m, JR(r));
+        } else {
+          other_item(it - r_rows);
+        }
       }
-    for (int it = tid; it < items2; it += WG) {
-      if (it < r_rows) continue;
-      if (CONE_ITEMS) {
-        const int e = it - r_rows, k = e / n_sq, r = e - k * n_sq;
-        sq_cone_item(K, X + r * n, k, Gt + r * m, JR(r));
-      } else {
-        other_item(it - r_rows);
+      if (JD && K.want_j) {  // the statics Jacobian rows, lanes along each record
+        lds_barrier();  // (the CoM pairs of the values items)
+        for (int r = 0; r < valid; ++r) statics_rows_coop(K, X + r * n, com6 + 6 * r, JR(r), tid, WG);
       }
     }
-    if (JD && K.want_j) {  // the statics Jacobian rows, lanes along each record
-      lds_barrier();  // (the CoM pairs of the values items)
-      for (int r = 0; r < valid; ++r) statics_rows_coop(K, X + r * n, com6 + 6 * r, JR(r), tid, WG);
+    lds_barrier();
+    // the residual partials first (from the LDS image), so that their stores are in flight with the
+    // copy-out's instead of after them on every workgroup's tail; one partial slot per tile
+    if (K.want_norms) {
+      NormAcc nacc;
+      nacc.init(tid, WG, m);
+      nacc.add_tile(Gt, valid * m, tid, WG, m);
+      partial_norms_waves(nacc, norms_ws + NORM_HDR, blockIdx.x);
     }
-  }
-  lds_barrier();
-  // the residual partials first (from the LDS image), so that their stores are in flight with the
-  // copy-out's instead of after them on every workgroup's tail
-  if (K.want_norms) {
-    nacc.add_tile(Gt, valid * m, tid, WG, m);
-    partial_norms_waves(nacc, norms_ws + NORM_HDR);
-  }
-  if (K.ablate != 2 && LIST) {  // records written in place: row by row (g, jac rows are 16-byte aligned)
-    if (K.want_g) copy_out_rows<WG, NT>(g_out, rowb, Gt, m, valid, tid);
-    if (K.want_j && !JD) copy_out_rows<WG, NT>(jac_out, rowb, Jt, nnz, valid, tid);
-    if (K.want_grad)
-      for (int e = tid; e < valid * n; e += WG) {
-        const int r = e / n;
-        grad_out[rowb[r] * n + (e - r * n)] = Dt[e];
-      }
-  } else if (K.ablate != 2 && K.soa) {
-    if (K.want_g) copy_out_soa<WG, NT>(g_out + b0, batch, Gt, m, valid, tid);
-    if (K.want_j) copy_out_soa<WG, NT>(jac_out + b0, batch, Jt, nnz, valid, tid);
-    if (K.want_grad) copy_out_soa<WG, NT>(grad_out + b0, batch, Dt, n, valid, tid);
-  } else if (K.ablate != 2) {
-    if (K.want_g) copy_out<WG, NT>(g_out + b0 * m, Gt, valid * m, tid);
-    if (K.want_j && !JD) copy_out<WG, NT>(jac_out + b0 * nnz, Jt, valid * nnz, tid);
-    if (K.want_grad) copy_out<WG, NT>(grad_out + b0 * n, Dt, valid * n, tid);
+    if (K.ablate != 2 && LIST) {  // records written in place: row by row (g, jac rows are 16-byte aligned)
+      if (K.want_g) copy_out_rows<WG, NT>(g_out, rowb, Gt, m, valid, tid);
+      if (K.want_j && !JD) copy_out_rows<WG, NT>(jac_out, rowb, Jt, nnz, valid, tid);
+      if (K.want_grad)
+        for (int e = tid; e < valid * n; e += WG) {
+          const int r = e / n;
+          grad_out[rowb[r] * n + (e - r * n)] = Dt[e];
+        }
+    } else if (K.ablate != 2 && K.soa) {
+      if (K.want_g) copy_out_soa<WG, NT>(g_out + b0, batch, Gt, m, valid, tid);
+      if (K.want_j) copy_out_soa<WG, NT>(jac_out + b0, batch, Jt, nnz, valid, tid);
+      if (K.want_grad) copy_out_soa<WG, NT>(grad_out + b0, batch, Dt, n, valid, tid);
+    } else if (K.ablate != 2) {
+      if (K.want_g) copy_out<WG, NT>(g_out + b0 * m, Gt, valid * m, tid);
+      if (K.want_j && !JD) copy_out<WG, NT>(jac_out + b0 * nnz, Jt, valid * nnz, tid);
+      if (K.want_grad) copy_out<WG, NT>(grad_out + b0 * n, Dt, valid * n, tid);
+    }
   }
 }
 
@@ -3395,7 +3423,8 @@ int32_t cpl_eval_batch_norms(const cpl_problem_desc* d, int64_t batch, const dou
 
 int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_threads, int32_t nt_stores,
                        int32_t ablate) {
-  if (ablate < 0 || (ablate > 2 && (ablate & ~(4 | 8 | 16 | 32 | 64 | 128 | 256 | 512)))) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
+  if (ablate < 0 || (ablate > 2 && (ablate & ~(4 | 8 | 16 | 32 | 64 | 128 | 256 | 512))))
+    return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
   g_ablate = ablate;
   if (kernel_variant < VAR_AUTO || kernel_variant > VAR_SPLIT_JD) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown kernel variant");
   if (tile_lds_kb != 0 && (tile_lds_kb < 8 || tile_lds_kb > 160))
