@@ -29,9 +29,12 @@ Rank 0 prints one JSON line.  Fields beyond the driver contract:
                 roofline (PMC), checker sample
   configs3_mixed16  BASELINE.json configs[3]'s 1,048,576 x 16 mixed batch on one GPU: kernel time, HBM
                 fraction, per-kind checker sample
+  configs3_mixed16_shard  one rank's shard of configs[3] sharded over 8 GPUs (131,072 x 16 mixed) through
+                the same split launch: kernel time and predicted_strong_speedup_8 = t(1,048,576) / t(131,072)
   configs4_solve5_lbfgs  BASELINE.json configs[4] (8,192 concurrent solves) in the reference's Hessian
                 mode (IPOPT's L-BFGS): solves/s, iterations, and the compiled restatement of the same
-                iteration (oracle/cpl_solve_host.c) on one core over a 512-instance sample;
+                iteration (oracle/cpl_solve_host.c) on all usable host cores (OpenMP over instances) and
+                on one core;
                 .single_solve: one instance solved alone (CentroidalPlanner::Solve()'s batch of one):
                 GPU ms per solve beside that compiled restatement on one core
 """
@@ -654,6 +657,23 @@ def side_mixed16(dev, stream, check_sample=512):
     res = {"workload": cfg.name + " (one GPU)", "kernel_ms": kms, "rows_per_s": B * m / (kms * 1e-3),
            "hbm_gbps": bytes_inst * B / (kms * 1e-3) / 1e9,
            "frac_of_peak": bytes_inst * B / (kms * 1e-3) / 1e9 / HBM_PEAK_GBPS, "bytes_per_instance": bytes_inst}
+    # one rank's shard of the 8-GPU strong-scaled run (distributed.shard: the first B / 8 instances),
+    # timed through the same split launch on this GPU: t(B) / t(B / 8) predicts the 8-GPU speedup
+    # (north_star: >= 6x at 8) — the shard's fixed costs (partition, side-stream fork / join, the norms'
+    # finish) grow relative to its work
+    Bs = B // 8
+    sout = {k: v[:Bs] for k, v in out.items() if k in ("g", "jac")}
+    sn = torch.empty_like(out["norms"])
+    srounds = []
+    for _ in range(5):
+        _abi.check(_abi.lib.cpl_time_eval_batch(ctypes.byref(prob.desc()), Bs, p(xt), p(mt), p(tt), p(sout["g"]),
+                                                p(sout["jac"]), None, None, p(sn),
+                                                ctypes.c_void_p(stream.cuda_stream), 10, ctypes.byref(ms)))
+        srounds.append(ms.value)
+    sms = sorted(srounds)[2]
+    res["shard_of_8"] = {"batch": Bs, "kernel_ms": sms, "rows_per_s": Bs * m / (sms * 1e-3),
+                         "frac_of_peak": bytes_inst * Bs / (sms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                         "predicted_strong_speedup_8": kms / sms}
     try:
         res["check"] = checker_leg(prob, cfg.env, xt, mt, tt, out, B, check_sample)
     except Exception as e:  # noqa: BLE001
@@ -1142,7 +1162,10 @@ def main():
         if sq8:
             res["configs2_sq8"] = sq8
         if mixed is not None:
+            shard = mixed.pop("shard_of_8", None) if isinstance(mixed, dict) else None
             res["configs3_mixed16"] = mixed
+            if shard:
+                res["configs3_mixed16_shard"] = shard
         if solve5:
             res["configs4_solve5_lbfgs"] = solve5
         print(json.dumps(res), flush=True)

@@ -1424,8 +1424,11 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
     // of 64), so the axis is wave-uniform — a scalar: the per-axis factors are scalar operands, the
     // power ladders' exponent loops uniform (with a lane-varying axis every ladder was a divergent loop
     // and every factor a per-lane select) — and (contact, tile row) = (kj >> logT, kj & (T - 1)) with
-    // the rows past `valid` idle (no divisions).  Mixed tiles keep the ballot-compacted mapping.
-    constexpr bool UAX = ENVK == CPL_ENV_SUPERQUADRIC;
+    // the rows past `valid` idle (no divisions).  Mixed tiles keep the ballot-compacted mapping, and so
+    // does the kind split's Superquadric half (LIST): beside the Ground half on the other stream the
+    // uniform-axis form ran the 1 048 576 x 16 mixed batch 7 % slower (2.74 against 2.55 ms, although
+    // an all-Superquadric list alone ran 4 % faster; profiles/r5/ab_uax_list).
+    constexpr bool UAX = ENVK == CPL_ENV_SUPERQUADRIC && !LIST;
     const int per_axis = UAX ? (N << K.logT) : N * n_sq;
     const int PA = UAX ? ((per_axis + 63) & ~63) : per_axis;
     const int r_ax = (HAS_SQ && wgj) ? 3 * PA : 0;
@@ -1486,7 +1489,7 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
       // Superquadric batches: the friction cones as items of their own in phase 2 (the workgroup's
       // fourth wave, otherwise idle there: the row-1 items no longer carry them)
       constexpr bool CONE_ITEMS = ENVK == CPL_ENV_SUPERQUADRIC;
-      const int r_cone = (CONE_ITEMS && wgj) ? per_axis : 0;
+      const int r_cone = (CONE_ITEMS && wgj) ? (N << K.logT) : 0;  // (slots (contact, row) = (e >> logT, e & (T - 1)))
       const int items2 = r_rows + (OTHERS_FIRST ? 0 : r_gr) + r_cone;
       if (HAS_SQ && UAX)
         for (int it = tid; it < r_rows; it += WG) {
