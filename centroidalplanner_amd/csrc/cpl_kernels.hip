@@ -2935,8 +2935,11 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
     // all of it when the batch is all Ground (the cap decided on the device, from the partition's
     // counts: 1.31 ms for 524 288 all-Ground mixed instances, as uncapped; a cap fixed at launch had
     // cost 2.37).  Measurement: ablation 256 = no cap, 512 = two per CU.
+    // Not below 262 144 instances: at the 8-GPU shard of configs[3] (131 072 x 16) the capped walkers ran
+    // ~90 us past the Superquadric half (0.432 ms capped against 0.394 uncapped; 262 144 / 524 288 /
+    // 1 048 576: within noise either way, profiles/r5/split_cap)
     const int64_t want_g = want;
-    if (!(g_ablate & 256)) {
+    if (!(g_ablate & 256) && batch >= (int64_t)1 << 18) {
       int dev = 0, cus = 256;
       (void)hipGetDevice(&dev);
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -3107,7 +3110,10 @@ __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, c
   const int lane = threadIdx.x;
   if (FIRST && !GF && A.with_post) {  // the post-step quantities and the search's setup of this instance
     ipm_post_step_one(A.post, b, A.setup);
-    __threadfence_block();  // (their stores before this wave's loads of them below)
+    // lane 0 stored them to global memory; every lane reloads them below: a workgroup barrier (its
+    // release / acquire fences wait for the stores and order the loads behind them — also if the block
+    // ever holds more than one wave; one wave today, so the barrier itself costs nothing)
+    __syncthreads();
   }
   const bool act = A.act[b] != 0;
   bool searching = act && A.searching[b] != 0;

@@ -2004,6 +2004,19 @@ struct cpl_solver {
   double *Xbase, *w, *y, *zL, *zU, *mu, *filt_t, *filt_p, *dwl, *f, *grad, *g, *J, *d_inf, *Hq, *lm_s, *lm_y, *theta_max,
       *theta_min;
   int64_t *status, *iters, *acc, *fcount, *n_resto;
+  // d_any [4]: batch-wide "any instance" flags the host reads once per phase (h_flag):
+  //   [0] an instance is still searching after its trials, [1] an instance needs the soft restoration
+  //   step (both set by the search kernels, cpl_kernels.hip cpl_ls_backtrack_kernel / cpl_ipm_judge_take),
+  //   [2] an instance is searching inside the restoration phase.  Who clears them, per iteration:
+  //   * fused search with the post-step prologue (post_in_ls): block 0 of the OPTIMALITY kernel clears
+  //     [0..1] (IpmUnpack.any) — several launches before the search kernel sets them.  Invariant: no
+  //     launch between the two (Hessian / FD evaluation, Newton setup, KKT factorisation) reads or
+  //     writes d_any; the search kernel's own prologue cannot clear them (its other blocks set them
+  //     concurrently: setup.any = nullptr there);
+  //   * fused search without the prologue: the post-step kernel's tail clears [0..1] (LsSetup.any);
+  //   * step-by-step search: a memset of [0..1] before the first trial;
+  //   * [2]: a memset before the restoration phase's search, or block 0 of k_resto_post.
+  //   tests/test_gpu_solve_engine.py covers the fused paths on both sides of LS_GF_MIN (B 2047 / 2048).
   uint8_t *active, *lm_cnt, *lm_skip, *d_any, *in_soft, *tiny_last, *tiny_flag, *in_resto, *resto_tight;
   double *best_w, *best_f;  // the best iterate feasible to fallback_viol_tol (lowest f) and its f
   double *acc_w, *acc_y, *acc_zL, *acc_zU;  // IPOPT's backup acceptable point

@@ -75,7 +75,10 @@ def test_entry_kernel_large_batch_matches_pipe():
 
 
 MIXED = [(4, 1001, "alternate"), (16, 777, "alternate"), (8, 515, "random"), (4, 64, "all_ground"),
-         (4, 65, "all_sq"), (2, 1, "random")]
+         (4, 65, "all_sq"), (2, 1, "random"),
+         # several partition blocks (PART_BLOCK = 1 024 instances): k_kind_write's cross-block offsets (the
+         # exclusive prefix over the blocks' counts) and the last block's totals
+         (4, 2049, "random"), (8, 5000, "alternate"), (4, 3073, "all_sq"), (2, 4100, "blocks")]
 
 
 @pytest.mark.gpu
@@ -94,6 +97,8 @@ def test_mixed_split_bitwise_default_and_oracle(N, B, pattern):
         tag = np.full(B, 1, np.uint8)
     elif pattern == "all_sq":
         tag = np.full(B, 2, np.uint8)
+    elif pattern == "blocks":  # runs of one kind across block boundaries: 1 500 Ground, 1 700 SQ, ...
+        tag = np.where((np.arange(B) // 1500 + np.arange(B) // 1700) % 2 == 0, 1, 2).astype(np.uint8)
     x2, _, _ = generate(N, "superquadric", B, 4242 + N)  # Superquadric instances need points near the surface
     x = np.where((tag == 2)[:, None], x2, x)
     dev = torch.device("cuda:0")

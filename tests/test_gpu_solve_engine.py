@@ -103,3 +103,23 @@ def test_fused_line_search_is_bitwise_the_stepwise_search(hessian, max_ls, max_s
         assert torch.equal(getattr(a, k), getattr(b, k)), k
     if max_ls == 40:
         assert bool((a.status <= STATUS_ACCEPTABLE).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [2047, 2048])
+def test_fused_search_around_the_global_factor_threshold(B):
+    """Batches on both sides of LS_GF_MIN (2 048): below it the fused search kernel runs the post-step
+    prologue (the any-flags then cleared by the optimality kernel, several launches before the search
+    sets them), from it on the second-order corrections re-solve from the KKT factors in global memory
+    and the post-step kernel clears the flags.  Either way the iterates are bitwise the step-by-step
+    search's (flag ownership: cpl_solver.hip, d_any)."""
+    prob = solve_problem().GetCplProblem()
+    X0, mass = solve_inputs(prob, B, seed=11)
+    dev = torch.device("cuda:0")
+    X0t, mt = torch.as_tensor(X0, device=dev), torch.as_tensor(mass, device=dev)
+    kw = dict(max_iter=1000, hessian="limited-memory", max_ls=40, max_soc=4)
+    a = batch_ipm_solve(prob, X0t, mt, ls_kernel=2, **kw)
+    b = batch_ipm_solve(prob, X0t, mt, ls_kernel=0, **kw)
+    for k in ("x", "y", "status", "iterations", "objective", "restorations"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    assert bool((a.status <= STATUS_ACCEPTABLE).all())
