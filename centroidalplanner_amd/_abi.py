@@ -91,6 +91,7 @@ class SolveOptions(ctypes.Structure):
         ("mu_init", c_double),
         ("fd_step", c_double),
         ("fallback_viol_tol", c_double),
+        ("nlp_scaling", c_int32),
     ]
 
 

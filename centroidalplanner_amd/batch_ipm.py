@@ -97,6 +97,8 @@ SOFT_RESTO_FACTOR = 0.9999  # soft_resto_pderror_reduction_factor
 MAX_SOFT_RESTO = 10         # max_soft_resto_iters
 
 FMAX = 64  # filter entries kept per instance (a ring)
+SCALING_MAX_GRADIENT = 100.0  # nlp_scaling_max_gradient (nlp_scaling_method = gradient-based, IPOPT's default)
+SCALING_MIN_VALUE = 1e-8      # nlp_scaling_min_value
 
 
 def _ptr(t):
@@ -171,7 +173,7 @@ class NativeSolver:
 
     def __init__(self, problem, batch, tol=1e-8, max_iter=3000, mu_init=0.1, acceptable_tol=1e-6,
                  acceptable_iter=15, max_ls=40, max_soc=4, hessian="exact", fd_step=1e-6, graph=True, compact=True,
-                 ls_kernel=2, fallback_viol_tol=0.0):
+                 ls_kernel=2, fallback_viol_tol=0.0, nlp_scaling="gradient-based"):
         o = _abi.SolveOptions()
         _abi.lib.cpl_solve_options_default(ctypes.byref(o))
         o.max_iter, o.max_ls, o.max_soc, o.acceptable_iter = int(max_iter), int(max_ls), int(max_soc), int(acceptable_iter)
@@ -182,6 +184,7 @@ class NativeSolver:
         o.compact = 1 if compact else 0
         o.ls_kernel = int(ls_kernel)
         o.fallback_viol_tol = float(fallback_viol_tol)
+        o.nlp_scaling = {"gradient-based": 1, "none": 0}[nlp_scaling]
         self.problem, self.batch = problem, int(batch)
         self.desc = problem.desc()
         self.handle = ctypes.c_void_p()
@@ -259,7 +262,8 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                     acceptable_iter: int = 15, max_ls: int = 40, max_soc: int = 4, hessian: str = "exact",
                     fd_step: float = 1e-6, graph: Optional[bool] = None, check_every: int = 4,
                     verbose: int = 0, compact: bool = True, verbose_instance: int = 0,
-                    ls_kernel: int = 2, fallback_viol_tol: float = 0.0) -> BatchSolveResult:
+                    ls_kernel: int = 2, fallback_viol_tol: float = 0.0,
+                    nlp_scaling: str = "gradient-based") -> BatchSolveResult:
     """Solve B instances of `problem`'s template from the starting points X0 [B, n] (torch float64,
     device tensor), per-instance robot masses `mass` [B] (None: the template's).
 
@@ -276,9 +280,21 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     the same iterates bit for bit.
     fallback_viol_tol (opt-in, default 0 = off; not IPOPT, which returns its last iterate): an instance that stops
     without converging at an iterate violating its original constraints by more than this returns the
-    lowest-objective iterate it met that satisfied them to this tolerance (result.fallback)."""
+    lowest-objective iterate it met that satisfied them to this tolerance (result.fallback).
+    nlp_scaling: "gradient-based" (IPOPT's default nlp_scaling_method, which IFOPT's IpoptSolver and the
+    reference leave in place: src/CentroidalPlanner.cpp:26-27 sets only derivative_test and
+    print_timing_statistics) — at the starting point, the objective is scaled by
+    df = max(nlp_scaling_min_value, 100 / max|grad f|) when max|grad f| > 100, and each constraint
+    block (the equality rows; the inequality rows) whose largest row gradient exceeds 100 gets
+    dc_i = max(nlp_scaling_min_value, 100 * (1 / max(100, max_j |J_ij|))) on every row (gradients over
+    the free variables; a NaN entry counts as 0, this solve's NaN policy); the iteration runs on the
+    scaled problem (IPOPT's tol applies there), x is not scaled, the returned multipliers are the
+    unscaled ones (dc y / df).  "none": no scaling.  The constraint bounds here are 0 or infinite, so
+    scaling leaves them unchanged."""
     if hessian not in ("exact", "fd", "limited-memory"):
         raise ValueError("hessian must be 'exact', 'fd' or 'limited-memory'")
+    if nlp_scaling not in ("gradient-based", "none"):
+        raise ValueError("nlp_scaling must be 'gradient-based' or 'none'")
     use_bfgs = hessian == "limited-memory"
     import torch
 
@@ -289,7 +305,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         ns = _native(problem, X0.shape[0], tol=tol, max_iter=max_iter, mu_init=mu_init, acceptable_tol=acceptable_tol,
                      acceptable_iter=acceptable_iter, max_ls=max_ls, max_soc=max_soc, hessian=hessian,
                      fd_step=fd_step, graph=True if graph is None else bool(graph), compact=compact,
-                     ls_kernel=ls_kernel, fallback_viol_tol=fallback_viol_tol)
+                     ls_kernel=ls_kernel, fallback_viol_tol=fallback_viol_tol, nlp_scaling=nlp_scaling)
         r = ns.solve(X0, mass, None if evaluator is None else evaluator.env_tag)
         if evaluator is not None:
             evaluator.calls += r.evaluations
@@ -361,10 +377,36 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     Mass_fd = None if Mass is None else Mass.repeat_interleave(2 * nf).contiguous()
     n_eval = 0
 
+    # IPOPT's gradient-based NLP scaling at the starting point (see the docstring): df [B], dc [B, m]
+    df = torch.ones(B, dtype=dt, device=dev)
+    dc = torch.ones(B, m, dtype=dt, device=dev)
+    if nlp_scaling == "gradient-based":
+        n_eval += 1
+        o0 = ev(Xbase, Mass, outputs=("jac", "grad"))
+        gmax = torch.nan_to_num(o0["grad"][:, free], nan=0.0).abs().amax(1) if nf else zeros_B
+        df = torch.where(gmax > SCALING_MAX_GRADIENT,
+                         torch.clamp(SCALING_MAX_GRADIENT / torch.where(gmax > 0, gmax, 1.0), min=SCALING_MIN_VALUE),
+                         torch.ones_like(gmax))
+        if m:
+            free_col = torch.zeros(n, dtype=torch.bool, device=dev)
+            free_col[free] = True
+            aJ = torch.where(free_col[jCol_t], torch.nan_to_num(o0["jac"], nan=0.0).abs(), 0.0)
+            rmax = torch.zeros(B, m, dtype=dt, device=dev).scatter_reduce(1, iRow_t.expand(B, -1), aJ, "amax")
+            for rows in (torch.as_tensor(np.where(gl_np == gu_np)[0], device=dev), I):
+                if rows.numel() == 0:
+                    continue
+                need = rmax[:, rows].amax(1) > SCALING_MAX_GRADIENT
+                d = torch.clamp(SCALING_MAX_GRADIENT * (1.0 / torch.clamp(rmax[:, rows], min=SCALING_MAX_GRADIENT)),
+                                min=SCALING_MIN_VALUE)
+                dc[:, rows] = torch.where(need[:, None], d, torch.ones_like(d))
+    scaled = bool((df != 1.0).any()) or bool((dc != 1.0).any())
+
     def evaluate_fg(Xe):  # line-search trial points: constraint values and objective only
         nonlocal n_eval
         n_eval += 1
         o = ev(Xe, Mass, outputs=("g", "f"))
+        if scaled:
+            return {"f": o["f"] * df, "g": o["g"] * dc}
         return {"f": o["f"], "g": o["g"]}
 
     def evaluate(Xe):
@@ -373,7 +415,16 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         o = ev(Xe, Mass)
         J = torch.zeros(B, m * n, dtype=dt, device=dev)
         J[:, flat_idx] = torch.nan_to_num(o["jac"], nan=0.0)  # a cone at F_t = 0 has a 0/0 Jacobian
-        return {"f": o["f"], "grad": o["grad"], "g": o["g"], "J": J.view(B, m, n)}
+        J = J.view(B, m, n)
+        if scaled:
+            return {"f": o["f"] * df, "grad": o["grad"] * df[:, None], "g": o["g"] * dc, "J": J * dc[:, :, None]}
+        return {"f": o["f"], "grad": o["grad"], "g": o["g"], "J": J}
+
+    def y_raw(yv):
+        """multipliers of the unscaled callbacks: the scaled problem's Lagrangian df f + (dc y)^T g equals
+        df (f + ((dc y) / df)^T g) — the raw Hessian / Lagrangian gradient of the callbacks at these
+        multipliers, times df"""
+        return (dc * yv) / df[:, None] if scaled else yv
 
     def unpack(wv):
         Xn = Xbase.clone()
@@ -404,10 +455,11 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         n_eval += 1
         o = ev(Xp.view(B * 2 * nf, n), Mass_fd, outputs=("jac", "grad"))
         gL = o["grad"].clone() if with_grad else torch.zeros_like(o["grad"])
-        gL.index_add_(1, jCol_t, torch.nan_to_num(o["jac"], nan=0.0) * yv.repeat_interleave(2 * nf, 0)[:, iRow_t])
+        gL.index_add_(1, jCol_t, torch.nan_to_num(o["jac"], nan=0.0) * y_raw(yv).repeat_interleave(2 * nf, 0)[:, iRow_t])
         gL = gL.view(B, 2 * nf, n)[:, :, free]
         H = (gL[:, :nf] - gL[:, nf:]) / (2.0 * h[:, :, None])
-        return 0.5 * (H + H.transpose(1, 2))
+        H = 0.5 * (H + H.transpose(1, 2))
+        return H * df[:, None, None] if scaled else H
 
     def hessian_blk(wv, yv, constraints_only=False):
         """Hessian of the Lagrangian over x_free at unpack(wv): the evaluator's analytic one when it has
@@ -415,9 +467,10 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         restoration phase: its objective's curvature is the proximity term, added by the caller)."""
         Xc = unpack(wv)
         if hessian == "exact" and hasattr(ev, "hessian"):
-            Hb = ev.hessian(Xc, yv, free, zero_cost=True) if constraints_only else ev.hessian(Xc, yv, free)
+            yr = y_raw(yv)
+            Hb = ev.hessian(Xc, yr, free, zero_cost=True) if constraints_only else ev.hessian(Xc, yr, free)
             if Hb is not None:
-                return Hb
+                return Hb * df[:, None, None] if scaled else Hb
         return fd_hessian(Xc, yv, with_grad=not constraints_only)
 
     def chol_inertia(K, dwl, mask):
@@ -1252,10 +1305,12 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     # IPOPT honor_original_bounds: the final point is projected back into the unrelaxed bounds and
     # its objective / constraint values reported there
     Xf = torch.minimum(torch.maximum(unpack(S["w"]), xl), xu).contiguous()
-    fin = evaluate_fg(Xf)
+    n_eval += 1
+    fin = ev(Xf, Mass, outputs=("g", "f"))  # the unscaled callbacks
     g = fin["g"]
     viol = torch.clamp(torch.maximum(gl - g, g - gu), min=0.0).amax(1) if m else zeros_B
-    res = BatchSolveResult(x=Xf, y=S["y"], status=S["status"], iterations=S["iters"],
+    res = BatchSolveResult(x=Xf, y=y_raw(S["y"]), status=S["status"],
+                           iterations=S["iters"],
                            objective=fin["f"].clone(), primal_inf=viol, dual_inf=S["d_inf"], evaluations=n_eval,
                            iterations_run=it_run, graph=False)
     res.restorations = S["n_resto"]

@@ -220,6 +220,10 @@ struct LsBacktrackArgs {
   PostStepArgs post;
   LsSetupArgs setup;
   int32_t with_post;
+  // IPOPT's NLP scaling (cpl_solve_options.nlp_scaling): the trial's f times df[b], its g times
+  // dc[b, r] (the scaled problem's values, as the solver's k_apply_scaling); nullptr: unscaled
+  const double* df = nullptr;
+  const double* dc = nullptr;
 };
 
 // s + sum_{r < m} a[r * stride] * v[r], accumulated in r order exactly as the plain loop

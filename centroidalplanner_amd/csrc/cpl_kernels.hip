@@ -3171,6 +3171,11 @@ __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, c
         }
       }
       __syncthreads();
+      if (A.dc) {  // the scaled problem's values (LsBacktrackArgs::df / dc)
+        for (int r = lane; r < m; r += 64) G[r] = G[r] * A.dc[b * m + r];
+        if (lane == 0) s_f = s_f * A.df[b];
+        __syncthreads();
+      }
       double th = 0.0;
       for (int r = lane; r < m; r += 64) {
         const int s = A.row_slack[r];

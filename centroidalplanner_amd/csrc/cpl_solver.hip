@@ -180,6 +180,90 @@ __global__ __launch_bounds__(256) void k_init_state(
 }
 
 // least-squares multipliers: kept when |y|max <= 1e3 (IPOPT constr_mult_init_max) and the solve succeeded
+// IPOPT's gradient-based NLP scaling (GradientScaling::DetermineScalingParametersImpl, with
+// nlp_scaling_max_gradient 100 and nlp_scaling_min_value 1e-8; batch_ipm.py nlp_scaling,
+// oracle/cpl_solve_host.c nlp_scaling), from the callbacks at the starting point: one wave per
+// instance.  df = max(1e-8, 100 / max|grad f|) when that maximum exceeds 100; per block of rows (the
+// equalities, the inequalities) whose largest row gradient exceeds 100, dc_r = max(1e-8,
+// 100 * (1 / max(100, max_j |J_rj|))) on each row of the block.  Gradients over the free variables
+// (srp / srq: the free-column records of each row), a NaN entry counting as 0.  any[0] = 1 when an
+// instance has a factor != 1.
+__global__ __launch_bounds__(256) void k_nlp_scaling(int64_t B, int n, int m, int nnz_rec, const uint8_t* __restrict__ is_fixed,
+                                                     const int32_t* __restrict__ row_slack, const int32_t* __restrict__ srp,
+                                                     const int32_t* __restrict__ srq, const double* __restrict__ grad,
+                                                     const double* __restrict__ J, double* __restrict__ df,
+                                                     double* __restrict__ dc, uint8_t* __restrict__ any) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  double gm = 0.0;
+  for (int j = lane; j < n; j += 64)
+    if (!is_fixed[j]) {
+      const double v = grad[b * n + j];
+      gm = fmax(gm, v == v ? fabs(v) : 0.0);
+    }
+  gm = wave_max(gm);
+  const double d = gm > 100.0 ? fmax(100.0 / gm, 1e-8) : 1.0;
+  double rm[2] = {0.0, 0.0}, emax = 0.0, imax = 0.0;  // m <= 128: two rows per lane at most
+  for (int h = 0; h < 2; ++h) {
+    const int r = lane + 64 * h;
+    if (r >= m) break;
+    double v = 0.0;
+    for (int t = srp[r]; t < srp[r + 1]; ++t) {
+      const double a = J[b * nnz_rec + srq[t]];
+      v = fmax(v, a == a ? fabs(a) : 0.0);
+    }
+    rm[h] = v;
+    if (row_slack[r] < 0) emax = fmax(emax, v);
+    else imax = fmax(imax, v);
+  }
+  emax = wave_max(emax);
+  imax = wave_max(imax);
+  bool scaled = d != 1.0;
+  for (int h = 0; h < 2; ++h) {
+    const int r = lane + 64 * h;
+    if (r >= m) break;
+    const double bm = row_slack[r] < 0 ? emax : imax;
+    const double s = bm > 100.0 ? fmax(100.0 * (1.0 / fmax(rm[h], 100.0)), 1e-8) : 1.0;
+    dc[b * m + r] = s;
+    scaled |= s != 1.0;
+  }
+  if (lane == 0) df[b] = d;
+  if (__ballot(scaled) != 0 && lane == 0) any[0] = 1;
+}
+
+// the scaled problem's callback values in place: f, grad f times df; g, J (records, row rrow[q])
+// times dc (any output may be nullptr)
+__global__ __launch_bounds__(256) void k_apply_scaling(int64_t B, int n, int m, int nnz_rec, const int32_t* __restrict__ rrow,
+                                                       const double* __restrict__ df, const double* __restrict__ dc,
+                                                       double* __restrict__ f, double* __restrict__ grad,
+                                                       double* __restrict__ g, double* __restrict__ J) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  const double d = df[b];
+  if (f && lane == 0) f[b] = f[b] * d;
+  if (grad)
+    for (int j = lane; j < n; j += 64) grad[b * n + j] = grad[b * n + j] * d;
+  if (g)
+    for (int r = lane; r < m; r += 64) g[b * m + r] = g[b * m + r] * dc[b * m + r];
+  if (J)
+    for (int q = lane; q < nnz_rec; q += 64) J[b * nnz_rec + q] = J[b * nnz_rec + q] * dc[b * m + rrow[q]];
+}
+
+// the Hessian callbacks' multipliers (dc y) / df [B, m]
+__global__ void k_scale_y(int64_t total, int m, const double* __restrict__ dc, const double* __restrict__ df,
+                          const double* __restrict__ y, double* __restrict__ yt) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < total) yt[e] = (dc[e] * y[e]) / df[e / m];
+}
+
+// v [B, per] times df[b] row by row
+__global__ void k_scale_rows(int64_t total, int64_t per, const double* __restrict__ df, double* __restrict__ v) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < total) v[e] = v[e] * df[e / per];
+}
+
 __global__ __launch_bounds__(256) void k_y0(int64_t B, int m, const double* __restrict__ dy, const int32_t* __restrict__ info,
                                             double* __restrict__ y) {
   const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
@@ -1819,6 +1903,7 @@ __global__ void k_gather_bytes(int64_t k, const int32_t* __restrict__ pos, const
 __global__ __launch_bounds__(256) void k_scatter_final(int64_t rows, int n, int m, int nw, bool finished_only,
                                                        const int32_t* __restrict__ orig, const uint8_t* __restrict__ active,
                                                        const double* __restrict__ w, const double* __restrict__ y,
+                                                       const double* __restrict__ dc, const double* __restrict__ df,
                                                        const double* __restrict__ Xbase, const double* __restrict__ d_inf,
                                                        const int64_t* __restrict__ status, const int64_t* __restrict__ iters,
                                                        const int64_t* __restrict__ n_resto,
@@ -1832,7 +1917,8 @@ __global__ __launch_bounds__(256) void k_scatter_final(int64_t rows, int n, int 
   if (o < 0 || (finished_only && active[r])) return;
   const int lane = threadIdx.x & 63;
   for (int k = lane; k < nw; k += 64) fw[(int64_t)o * nw + k] = w[r * nw + k];
-  for (int k = lane; k < m; k += 64) fy[(int64_t)o * m + k] = y[r * m + k];
+  // the multipliers of the unscaled problem: (dc y) / df (nlp_scaling; dc = nullptr: unscaled)
+  for (int k = lane; k < m; k += 64) fy[(int64_t)o * m + k] = dc ? (dc[r * m + k] * y[r * m + k]) / df[r] : y[r * m + k];
   for (int k = lane; k < n; k += 64) fX[(int64_t)o * n + k] = Xbase[r * n + k];
   if (lane == 0) {
     fdinf[o] = d_inf[r];
@@ -2054,6 +2140,14 @@ struct cpl_solver {
   uint64_t* scratch;
   int64_t scratch_words = 0;
   int32_t compactions = 0;
+  // IPOPT's gradient-based NLP scaling (cpl_solve_options.nlp_scaling): df [B], dc [B, m] (rows
+  // compacted with the batch), the Hessian callbacks' multipliers (dc y) / df [B, m]; the records' row
+  // [nnz_rec]; the free-column records of every row (CSR: srp [m + 1], srq); scaled: this solve has a
+  // factor != 1 (the scaling kernels run; graphs keyed by it)
+  double *df, *dc, *ytil;
+  int32_t *rrow, *srp, *srq;
+  uint8_t* sc_any;
+  bool scaled = false;
 };
 
 namespace cpl {
@@ -2069,12 +2163,22 @@ int32_t hip_err(hipError_t e, const char* what) {
   } while (0)
 #define LAUNCHED(what) HK(hipGetLastError(), what)
 
+// the scaled problem's values (IPOPT's scaled NLP): df f, df grad f, dc g, dc J (one product each)
+int32_t apply_scaling(cpl_solver* S, double* fo, double* grado, double* go, double* jo) {
+  if (!S->scaled) return CPL_OK;
+  hipLaunchKernelGGL(k_apply_scaling, dim3(blocks_for(S->Bcur)), dim3(256), 0, S->stream, S->Bcur, S->n, S->m,
+                     S->nnz_rec, S->rrow, S->df, S->dc, fo, grado, go, jo);
+  LAUNCHED("k_apply_scaling");
+  return CPL_OK;
+}
 int32_t eval_fg(cpl_solver* S, const double* X, double* fo, double* go) {
-  return cpl_eval_batch(&S->desc, S->Bcur, X, S->mass, S->tag, go, nullptr, fo, nullptr, S->stream);
+  CK(cpl_eval_batch(&S->desc, S->Bcur, X, S->mass, S->tag, go, nullptr, fo, nullptr, S->stream));
+  return apply_scaling(S, fo, nullptr, go, nullptr);
 }
 int32_t eval_full(cpl_solver* S, const double* X, double* fo, double* grado, double* go, double* jo) {
-  return cpl_eval_batch_ex(&S->desc, S->Bcur, X, S->mass, S->tag, go, jo, fo, grado, nullptr, CPL_EVAL_JAC_FOLDED,
-                           S->stream);
+  CK(cpl_eval_batch_ex(&S->desc, S->Bcur, X, S->mass, S->tag, go, jo, fo, grado, nullptr, CPL_EVAL_JAC_FOLDED,
+                       S->stream));
+  return apply_scaling(S, fo, grado, go, jo);
 }
 
 // The phases of one lock-step iteration (each graph-capturable, no host synchronisation inside):
@@ -2105,8 +2209,25 @@ int32_t hessian_into(cpl_solver* S, const cpl_problem_desc* d, const uint8_t* ma
   *Hblk = nullptr;
   *h_sym = 0;
   if (S->bfgs) return CPL_OK;  // the compact model is expanded inside the Newton setup
+  // scaled: the callbacks' Hessian at the multipliers (dc y) / df, times df (the scaled Lagrangian
+  // df f + (dc y)^T g is df (f + ((dc y) / df)^T g))
+  const double* yh = S->y;
+  if (S->scaled) {
+    hipLaunchKernelGGL(k_scale_y, dim3(blocks_elems(B * S->m)), dim3(256), 0, st, B * S->m, S->m, S->dc, S->df, S->y,
+                       S->ytil);
+    LAUNCHED("k_scale_y");
+    yh = S->ytil;
+  }
+  auto scale_H = [&]() -> int32_t {
+    if (!S->scaled) return CPL_OK;
+    hipLaunchKernelGGL(k_scale_rows, dim3(blocks_elems(B * nf * nf)), dim3(256), 0, st, B * nf * nf, nf * nf, S->df,
+                       S->H);
+    LAUNCHED("k_scale_rows");
+    return CPL_OK;
+  };
   if (S->analytic_H) {
-    CK(cpl_lagrangian_hessian(d, B, S->X, S->y, mask, S->free32, nf, S->H, st));
+    CK(cpl_lagrangian_hessian(d, B, S->X, yh, mask, S->free32, nf, S->H, st));
+    CK(scale_H());
     *Hblk = S->H;
     return CPL_OK;
   }
@@ -2115,17 +2236,18 @@ int32_t hessian_into(cpl_solver* S, const cpl_problem_desc* d, const uint8_t* ma
   int32_t rc = CPL_ERR_UNSUPPORTED;
   if (S->fd_fused)
     rc = cpl_eval_lagrangian_grad(d, B * 2 * nf, S->Xp, S->mass ? S->mass_fd : nullptr, S->tag ? S->tag_fd : nullptr,
-                                  S->col_ptr, S->csc_k, S->csc_row, S->y, 2 * nf, mask, S->gL, st);
+                                  S->col_ptr, S->csc_k, S->csc_row, yh, 2 * nf, mask, S->gL, st);
   if (rc == CPL_ERR_UNSUPPORTED) {  // Superquadric / mixed: eval + J^T y in two launches
     S->fd_fused = false;
     CK(cpl_eval_batch(d, B * 2 * nf, S->Xp, S->mass ? S->mass_fd : nullptr, S->tag ? S->tag_fd : nullptr, nullptr,
                       S->jac_fd, nullptr, S->grad_fd, st));
-    CK(cpl_lagrangian_grad(B * 2 * nf, n, S->m, S->nnz, S->col_ptr, S->csc_k, S->csc_row, S->grad_fd, S->jac_fd, S->y,
+    CK(cpl_lagrangian_grad(B * 2 * nf, n, S->m, S->nnz, S->col_ptr, S->csc_k, S->csc_row, S->grad_fd, S->jac_fd, yh,
                            2 * nf, S->gL, st));
   } else {
     CK(rc);
   }
   CK(cpl_ipm_fd_hessian_raw(B, n, nf, S->free64, S->gL, S->hfd, S->H, mask, st));
+  CK(scale_H());
   *Hblk = S->H;
   *h_sym = 1;
   return CPL_OK;
@@ -2262,6 +2384,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
         la.mu = S->mu_o; la.theta_k = S->theta_k; la.phi_k = S->phi_k; la.gd = S->gd; la.switch_ok = S->switch_ok;
         la.theta_max = S->theta_max; la.filt_t = S->ft; la.filt_p = S->fp;
         la.mass = S->mass; la.env_tag = S->tag;
+        if (S->scaled) { la.df = S->df; la.dc = S->dc; }
         la.st_f = S->st_f; la.st_g = S->st_g; la.st_w = S->st_w; la.st_alpha = S->st_alpha; la.st_aug = S->st_aug;
         la.any = S->d_any;
         la.resto = 0;
@@ -2293,6 +2416,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
         la.mu = S->mu_o; la.theta_k = S->theta_k; la.phi_k = S->phi_k; la.gd = S->gd; la.switch_ok = S->switch_ok;
         la.theta_max = S->theta_max; la.filt_t = S->ft; la.filt_p = S->fp;
         la.mass = S->mass; la.env_tag = S->tag;
+        if (S->scaled) { la.df = S->df; la.dc = S->dc; }
         la.st_f = S->st_f; la.st_g = S->st_g; la.st_w = S->st_w; la.st_alpha = S->st_alpha; la.st_aug = S->st_aug;
         la.any = S->d_any;
         la.resto = 0;
@@ -2452,6 +2576,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
         la.mu = S->muR; la.theta_k = S->thetaR; la.phi_k = S->phiR; la.gd = S->gdR; la.switch_ok = S->switchR;
         la.theta_max = S->thmaxR; la.filt_t = S->ftR; la.filt_p = S->fpR;
         la.mass = S->mass; la.env_tag = S->tag;
+        if (S->scaled) { la.df = S->df; la.dc = S->dc; }
         la.st_f = S->st_f; la.st_g = S->st_g; la.st_w = S->st_w; la.st_alpha = S->st_alpha; la.st_aug = S->st_aug;
         la.any = S->d_any;
         la.resto = 1;
@@ -2525,7 +2650,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
 // replayed); without graphs the phase is launched directly
 int32_t run_phase(cpl_solver* S, int phase) {
   if (!S->opt.use_graph) return step_phase(S, phase);
-  const int64_t key = ((S->Bcur * 4 + (S->mass ? 2 : 0) + (S->tag ? 1 : 0)) * 16) + phase;
+  const int64_t key = ((S->Bcur * 8 + (S->scaled ? 4 : 0) + (S->mass ? 2 : 0) + (S->tag ? 1 : 0)) * 16) + phase;
   auto it = S->graphs.find(key);
   if (it == S->graphs.end()) {
     HK(hipStreamBeginCapture(S->stream, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
@@ -2590,7 +2715,8 @@ int32_t compact(cpl_solver* S, int64_t count, int64_t Bn) {
     LAUNCHED("k_fallback");
   }
   hipLaunchKernelGGL(k_scatter_final, dim3(blocks_for(Bc)), dim3(256), 0, st, Bc, n, m, nw, true, S->orig, S->active,
-                     S->w, S->y, S->Xbase, S->d_inf, S->status, S->iters, S->n_resto, S->fw, S->fy, S->fX, S->fdinf,
+                     S->w, S->y, S->scaled ? S->dc : nullptr, S->df, S->Xbase, S->d_inf, S->status, S->iters, S->n_resto, S->fw, S->fy,
+                     S->fX, S->fdinf,
                      S->fstatus, S->fiters, S->fresto);
   LAUNCHED("k_scatter_final");
   hipLaunchKernelGGL(k_positions, dim3(1), dim3(1024), 0, st, Bc, S->active, S->pos);
@@ -2615,6 +2741,10 @@ int32_t compact(cpl_solver* S, int64_t count, int64_t Bn) {
   CK(move(S->fcR, 1)); CK(move(S->th_o0, 1)); CK(move(S->ph_o0, 1)); CK(move(S->dwlR, 1)); CK(move(S->thmaxR, 1));
   CK(move(S->thminR, 1)); CK(move(S->best_w, nw)); CK(move(S->best_f, 1));
   CK(move(S->acc_w, nw)); CK(move(S->acc_y, m)); CK(move(S->acc_zL, nw)); CK(move(S->acc_zU, nw));
+  if (S->scaled) {
+    CK(move(S->df, 1));
+    CK(move(S->dc, m));
+  }
   if (S->bfgs) {
     CK(move(S->Hq, LMC(nf)));
     CK(move(S->lm_s, (int64_t)LM_HIST * nf));
@@ -2683,6 +2813,7 @@ void cpl_solve_options_default(cpl_solve_options* o) {
   o->mu_init = 0.1;
   o->fd_step = 1e-6;
   o->fallback_viol_tol = 0.0;  // off: IPOPT returns its last iterate
+  o->nlp_scaling = 1;          // IPOPT's default nlp_scaling_method gradient-based
 }
 
 int32_t cpl_solver_destroy(cpl_solver* S) {
@@ -2739,7 +2870,8 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   cpl_solve_options_default(&opt);
   if (o) opt = *o;
   if (opt.hessian < CPL_HESSIAN_EXACT || opt.hessian > CPL_HESSIAN_FD || opt.max_iter < 0 || opt.max_soc < 0 ||
-      opt.max_ls < 0 || !(opt.tol > 0.0) || opt.ls_kernel < 0 || opt.ls_kernel > 2)
+      opt.max_ls < 0 || !(opt.tol > 0.0) || opt.ls_kernel < 0 || opt.ls_kernel > 2 || opt.nlp_scaling < 0 ||
+      opt.nlp_scaling > 1)
     return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_solver_create: bad options");
   int32_t n, m, nnz;
   CK(cpl_dims(d, &n, &m, &nnz));
@@ -2810,6 +2942,20 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
       csc_k[q] = k;
       csc_row[q] = iRow[k];
     }
+  }
+
+  // nlp_scaling: each record's row, and the free-column records of each row (CSR)
+  std::vector<int32_t> rrow(nnz_rec), srp(m + 1, 0), srq;
+  for (int q = 0; q < nnz_rec; ++q) {
+    rrow[q] = iRow[var_k[q]];
+    if (freepos[jCol[var_k[q]]] >= 0) ++srp[rrow[q] + 1];
+  }
+  for (int r = 0; r < m; ++r) srp[r + 1] += srp[r];
+  srq.resize(srp[m]);
+  {
+    std::vector<int32_t> fill(srp.begin(), srp.end() - 1);
+    for (int q = 0; q < nnz_rec; ++q)
+      if (freepos[jCol[var_k[q]]] >= 0) srq[fill[rrow[q]]++] = q;
   }
 
   cpl_solver* S = new cpl_solver();
@@ -2926,6 +3072,9 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   S->fdinf = a.take<double>(Bz); S->fstatus = a.take<int64_t>(Bz); S->fiters = a.take<int64_t>(Bz);
   S->fresto = a.take<int64_t>(Bz);
   S->scratch = a.take<uint64_t>(Bz * (size_t)S->scratch_words);
+  S->df = a.take<double>(Bz); S->dc = a.take<double>(Bz * m); S->ytil = a.take<double>(S->bfgs ? 0 : Bz * m);
+  S->rrow = a.take<int32_t>(nnz_rec); S->srp = a.take<int32_t>(m + 1); S->srq = a.take<int32_t>(srq.size());
+  S->sc_any = a.take<uint8_t>(4);
   };
   Arena probe;
   carve(probe);
@@ -2943,7 +3092,8 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
       {S->free64, f64.data(), 8 * f64.size()}, {S->fixed64, x64.data(), 8 * x64.size()},
       {S->is_fixed, is_fixed.data(), (size_t)n}, {S->hasL, hasL.data(), (size_t)nw}, {S->hasU, hasU.data(), (size_t)nw},
       {S->xl, xl.data(), 8 * (size_t)n}, {S->xu, xu.data(), 8 * (size_t)n}, {S->gl, gl.data(), 8 * (size_t)m},
-      {S->gu, gu.data(), 8 * (size_t)m}, {S->wl0, wl0.data(), 8 * (size_t)nw}, {S->wu0, wu0.data(), 8 * (size_t)nw}};
+      {S->gu, gu.data(), 8 * (size_t)m}, {S->wl0, wl0.data(), 8 * (size_t)nw}, {S->wu0, wu0.data(), 8 * (size_t)nw},
+      {S->rrow, rrow.data(), 4 * rrow.size()}, {S->srp, srp.data(), 4 * srp.size()}, {S->srq, srq.data(), 4 * srq.size()}};
   for (const Up& u : ups)
     if (u.bytes && (e = hipMemcpy(u.dst, u.src, u.bytes, hipMemcpyHostToDevice)) != hipSuccess) return bad(e, "hipMemcpy");
   if ((e = hipMemset(S->zeros_w, 0, 8 * Bz * nw)) != hipSuccess || (e = hipMemset(S->zeros_B, 0, 8 * Bz)) != hipSuccess ||
@@ -2995,6 +3145,20 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
   // starting point: x pushed into its bounds, slacks = g_I(x) pushed into theirs, least-squares y
   hipLaunchKernelGGL(k_xbase, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, d_x0, S->is_fixed, S->xl, S->Xbase);
   LAUNCHED("k_xbase");
+  // IPOPT's gradient-based NLP scaling from the callbacks at the starting point (fixed variables at
+  // their value); the iteration runs on the scaled problem when any instance has a factor != 1
+  S->scaled = false;
+  if (S->opt.nlp_scaling) {
+    CK(eval_full(S, S->Xbase, S->f, S->grad, S->g, S->J));
+    ++evals;
+    HK(hipMemsetAsync(S->sc_any, 0, 4, st), "hipMemsetAsync");
+    hipLaunchKernelGGL(k_nlp_scaling, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, S->nnz_rec, S->is_fixed,
+                       S->row_slack, S->srp, S->srq, S->grad, S->J, S->df, S->dc, S->sc_any);
+    LAUNCHED("k_nlp_scaling");
+    HK(hipMemcpyAsync(S->h_flag, S->sc_any, 4, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+    HK(hipStreamSynchronize(st), "hipStreamSynchronize");
+    S->scaled = S->h_flag[0] != 0;
+  }
   hipLaunchKernelGGL(k_start_x, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, S->freepos, S->Xbase, S->hasL,
                      S->hasU, S->wl0, S->wu0, S->X);
   LAUNCHED("k_start_x");
@@ -3079,7 +3243,8 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
   }
   // every row still in the batch to its instance's place in the full-batch results
   hipLaunchKernelGGL(k_scatter_final, dim3(blocks_for(Bc)), dim3(256), 0, st, Bc, n, m, nw, false, S->orig, S->active,
-                     S->w, S->y, S->Xbase, S->d_inf, S->status, S->iters, S->n_resto, S->fw, S->fy, S->fX, S->fdinf,
+                     S->w, S->y, S->scaled ? S->dc : nullptr, S->df, S->Xbase, S->d_inf, S->status, S->iters, S->n_resto, S->fw, S->fy,
+                     S->fX, S->fdinf,
                      S->fstatus, S->fiters, S->fresto);
   LAUNCHED("k_scatter_final");
   // IPOPT honor_original_bounds: the final point projected into the original bounds, re-evaluated

@@ -522,6 +522,15 @@ typedef struct cpl_solve_options {
                               unchanged; cpl_solver_fallbacks says which instances).  Only x is
                               replaced: the multipliers and dual_inf of such an instance still belong
                               to its last iterate. */
+  int32_t nlp_scaling;     /* 1 (default): IPOPT's gradient-based NLP scaling (nlp_scaling_method, which
+                              IFOPT's IpoptSolver and the reference leave at its default,
+                              src/CentroidalPlanner.cpp:26-27), computed once at the starting point:
+                              df = max(1e-8, 100 / max|grad f|) when max|grad f| > 100; for each block
+                              of rows (equalities; inequalities) whose largest row gradient exceeds 100,
+                              dc_i = max(1e-8, 100 * (1 / max(100, max_j |J_ij|))) on each of its rows
+                              (gradients over the free variables, a NaN entry counting as 0).  The
+                              iteration and its tolerances run on the scaled problem; x is unscaled, the
+                              returned multipliers are the unscaled ones (dc y / df).  0: no scaling. */
 } cpl_solve_options;
 
 typedef struct cpl_solver cpl_solver;

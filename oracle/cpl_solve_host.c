@@ -79,6 +79,10 @@ typedef struct {
   double jac[4096];
   long evals;
   int exact;
+  /* IPOPT's gradient-based NLP scaling (batch_ipm.py nlp_scaling): objective factor df, constraint
+   * row factors dc; scaled = 0: all 1, the callbacks' values unchanged */
+  int scaled;
+  double df, dc[MMAX];
 } Prob;
 
 typedef struct {
@@ -102,10 +106,58 @@ static void evaluate(Prob* P, const double* X, Eval* o) {
     const double v = P->jac[k];
     o->J[P->iRow[k] * P->n + P->jCol[k]] = v == v ? v : 0.0;  /* a cone at F_t = 0: 0/0 */
   }
+  if (P->scaled) {  /* the scaled problem: df f, df grad f, dc g, dc J (one product per value) */
+    o->f = o->f * P->df;
+    for (int j = 0; j < P->n; ++j) o->grad[j] = o->grad[j] * P->df;
+    for (int r = 0; r < P->m; ++r) {
+      o->g[r] = o->g[r] * P->dc[r];
+      for (int j = 0; j < P->n; ++j) o->J[r * P->n + j] = o->J[r * P->n + j] * P->dc[r];
+    }
+  }
 }
 static void evaluate_fg(Prob* P, const double* X, double* f, double* g) {
   ++P->evals;
   cplo_ws_eval(P->d, P->ws, X, P->mass, g, NULL, f, NULL);
+  if (P->scaled) {
+    *f = *f * P->df;
+    for (int r = 0; r < P->m; ++r) g[r] = g[r] * P->dc[r];
+  }
+}
+/* the multipliers of the unscaled callbacks: (dc y) / df (the scaled Lagrangian df f + (dc y)^T g is
+ * df (f + ((dc y) / df)^T g)) */
+static void y_raw(const Prob* P, const double* y, double* yr) {
+  for (int r = 0; r < P->m; ++r) yr[r] = P->scaled ? (P->dc[r] * y[r]) / P->df : y[r];
+}
+/* IPOPT GradientScaling::DetermineScalingParametersImpl at the starting point X (nlp_scaling_max_gradient
+ * 100, nlp_scaling_min_value 1e-8; gradients over the free variables, NaN entries as 0): df when
+ * max |grad f| > 100; per constraint block (equality rows, inequality rows) whose largest row gradient
+ * exceeds 100, dc_i = max(1e-8, 100 * (1 / max(100, row max))) on every row of the block */
+static void nlp_scaling(Prob* P, const double* X) {
+  double grad[NMAX], g[MMAX], f, rmax[MMAX];
+  ++P->evals;
+  cplo_ws_eval(P->d, P->ws, X, P->mass, g, P->jac, &f, grad);
+  double gmax = 0.0;
+  for (int k = 0; k < P->nf; ++k) {
+    const double v = grad[P->free_idx[k]];
+    gmax = dmax(gmax, v == v ? fabs(v) : 0.0);
+  }
+  P->df = gmax > 100.0 ? dmax(100.0 / gmax, 1e-8) : 1.0;
+  for (int r = 0; r < P->m; ++r) { rmax[r] = 0.0; P->dc[r] = 1.0; }
+  for (int k = 0; k < P->nnz; ++k) {
+    const double v = P->jac[k];
+    if (P->is_fixed[P->jCol[k]] || v != v) continue;
+    rmax[P->iRow[k]] = dmax(rmax[P->iRow[k]], fabs(v));
+  }
+  for (int blk = 0; blk < 2; ++blk) {  /* 0: equality rows, 1: inequality rows */
+    double bmax = 0.0;
+    for (int r = 0; r < P->m; ++r)
+      if ((P->row_slack[r] >= 0) == blk) bmax = dmax(bmax, rmax[r]);
+    if (!(bmax > 100.0)) continue;
+    for (int r = 0; r < P->m; ++r)
+      if ((P->row_slack[r] >= 0) == blk) P->dc[r] = dmax(100.0 * (1.0 / dmax(rmax[r], 100.0)), 1e-8);
+  }
+  P->scaled = P->df != 1.0;
+  for (int r = 0; r < P->m; ++r) P->scaled |= P->dc[r] != 1.0;
 }
 
 static void cons(const Prob* P, const double* g, const double* w, double* c) {
@@ -825,7 +877,11 @@ static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
   if (P->exact) {  /* the analytic Lagrangian Hessian at (w, y) in place of the model */
     double Xc[NMAX];
     unpack(P, w, Xc);
-    lagr_hessian(P, Xc, S->y, 0, S->Hq);
+    double yr[MMAX];
+    y_raw(P, S->y, yr);
+    lagr_hessian(P, Xc, yr, 0, S->Hq);
+    if (P->scaled)
+      for (int q = 0; q < P->nf * P->nf; ++q) S->Hq[q] = S->Hq[q] * P->df;
   }
   for (int i = 0; i < nw; ++i)
     for (int j = 0; j < nw; ++j) M[i * nw + j] = (i == j ? Sig[i] : 0.0) + ((i < nf && j < nf) ? S->Hq[i * nf + j] : 0.0);
@@ -1070,7 +1126,11 @@ static void resto_step(Prob* P, State* S, const Opts* o) {
   if (P->exact) {  /* the constraints' curvature y^T g (the proximity term's is added below) */
     double Xc[NMAX];
     unpack(P, w, Xc);
-    lagr_hessian(P, Xc, S->y, 1, S->Hq);
+    double yr[MMAX];
+    y_raw(P, S->y, yr);
+    lagr_hessian(P, Xc, yr, 1, S->Hq);
+    if (P->scaled)
+      for (int q = 0; q < P->nf * P->nf; ++q) S->Hq[q] = S->Hq[q] * P->df;
   }
   for (int i = 0; i < nw; ++i)
     for (int j = 0; j < nw; ++j)
@@ -1181,6 +1241,9 @@ static void resto_step(Prob* P, State* S, const Opts* o) {
  * default like the engine's; cplo_set_fallback_viol_tol opts in (process-wide). */
 static double g_fallback_viol_tol = 0.0;
 void cplo_set_fallback_viol_tol(double v) { g_fallback_viol_tol = v; }
+/* nlp_scaling_method: 1 gradient-based (IPOPT's default, the reference's), 0 none (process-wide) */
+static int g_nlp_scaling = 1;
+void cplo_set_nlp_scaling(int on) { g_nlp_scaling = on != 0; }
 
 /* Solve one instance from x0 (IFOPT's IpoptSolver defaults: limited-memory Hessian; exact_hessian:
  * the analytic Lagrangian Hessian, batch_ipm.py's hessian="exact", Ground / no environment).  Returns 0;
@@ -1231,6 +1294,8 @@ int cplo_solve(const cpl_problem_desc* d, const double* x0, double mass, int max
   P.ws = cplo_ws_new(d);
   if (!P.ws) return CPL_ERR_RUNTIME;
   for (int j = 0; j < n; ++j) P.Xbase[j] = P.is_fixed[j] ? P.xl[j] : x0[j];
+  P.scaled = 0;
+  if (g_nlp_scaling) nlp_scaling(&P, P.Xbase);
   Opts o = {tol, 1e-6, dmin(tol, COMPL_INF_TOL) / (BARRIER_TOL_FACTOR + 1.0), g_fallback_viol_tol, 15, 40, 4};
   /* starting point: x pushed into its bounds, slacks = g_I(x) pushed into theirs */
   const int nw = P.nw, nf = P.nf;
@@ -1298,6 +1363,7 @@ int cplo_solve(const cpl_problem_desc* d, const double* x0, double mass, int max
   double X[NMAX], gfin[MMAX], f = 0.0;
   unpack(&P, S.w, X);
   for (int j = 0; j < n; ++j) X[j] = dmin(dmax(X[j], P.xl[j]), P.xu[j]);  /* honor_original_bounds */
+  P.scaled = 0;  /* the objective / constraints reported at x_out: the unscaled callbacks */
   evaluate_fg(&P, X, &f, gfin);
   if (x_out) memcpy(x_out, X, sizeof(double) * (size_t)n);
   if (status) *status = S.status;

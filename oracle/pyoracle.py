@@ -47,6 +47,8 @@ def _load(path=LIB_PATH):
     lib.cplo_time_solve_mt.restype = c_double
     lib.cplo_set_fallback_viol_tol.argtypes = [c_double]
     lib.cplo_set_fallback_viol_tol.restype = None
+    lib.cplo_set_nlp_scaling.argtypes = [c_int]
+    lib.cplo_set_nlp_scaling.restype = None
     return lib
 
 
@@ -190,6 +192,12 @@ def set_fallback_viol_tol(v):
     """Opt in to the best-feasible-iterate fallback (not IPOPT) in the compiled restatement: v > 0;
     0 (the default, like the engine's) returns the last iterate as IPOPT does."""
     lib.cplo_set_fallback_viol_tol(float(v))
+
+
+def set_nlp_scaling(method):
+    """nlp_scaling_method of the compiled restatement: "gradient-based" (IPOPT's default, the
+    reference's; the default here too) or "none" (process-wide)."""
+    lib.cplo_set_nlp_scaling(1 if method == "gradient-based" else 0)
 
 
 def max_threads():
