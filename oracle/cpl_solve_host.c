@@ -596,6 +596,12 @@ typedef struct {
   double best_w[NWMAX], best_f;
   double acc_w[NWMAX], acc_y[MMAX], acc_zL[NWMAX], acc_zU[NWMAX];  /* IPOPT's backup acceptable point */
   int has_acc;
+  /* IPOPT's watchdog (cplo_set_watchdog): active, shortened-step count, trial iterations; the watchdog
+   * iterate and its step, its line search's references (theta, barrier objective, grad phi^T dw),
+   * its fraction-to-the-boundary step (alpha_primal_test) and optimality error (its values: g_wd_cur) */
+  int in_wd, wd_cnt, wd_trial;
+  double wd_w[NWMAX], wd_y[MMAX], wd_zL[NWMAX], wd_zU[NWMAX], wd_dw[NWMAX], wd_dy[MMAX], wd_dzL[NWMAX], wd_dzU[NWMAX];
+  double wd_th, wd_ph, wd_gd, wd_alpha;
 } State;
 
 typedef struct {
@@ -838,6 +844,26 @@ static void leave_resto(const Prob* P, State* S, const double* w_new) {
 }
 
 /* One regular iteration (batch_ipm.py regular_step) */
+/* IPOPT's watchdog (BacktrackingLineSearch: watchdog_shortened_iter_trigger 10, watchdog_trial_iter_max 3),
+ * opt-in here (cplo_set_watchdog; the device engine and batch_ipm.py have none): after 10 consecutive
+ * iterations whose step the line search shortened, the iterate and its step are kept and the next
+ * iterations take the full step of their own direction, judged against the kept iterate's references
+ * (theta, barrier objective, grad phi^T dw, its alpha_max as the switching condition's alpha); a full
+ * step acceptable to them ends the watchdog; otherwise the step is taken anyway, up to 3 times, after
+ * which the kept iterate is restored and searched along its own step from alpha_max / 2 (no
+ * second-order correction).  A barrier-parameter change ends the watchdog (the line search's Reset).
+ * IPOPT is absent offline: restated from its published method, parity unpinned. */
+#define WD_TRIGGER 10
+#define WD_TRIAL_MAX 3
+static int g_watchdog = 0;
+void cplo_set_watchdog(int on) { g_watchdog = on != 0; }
+static __thread Eval g_wd_cur;
+/* this thread's watchdog events since the last read: starts, successes, restorations of the kept iterate */
+static __thread long g_wd_events[3];
+void cplo_watchdog_events(long* out) {
+  for (int k = 0; k < 3; ++k) { out[k] = g_wd_events[k]; g_wd_events[k] = 0; }
+}
+
 static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
   const int nw = P->nw, m = P->m, nf = P->nf;
   static __thread Kkt K;
@@ -857,6 +883,8 @@ static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
     if (((err_mu(P, E, mu) <= BARRIER_TOL_FACTOR * mu) || (r == 0 && force)) && mu > o->mu_min) {
       mu = dmax(dmin(0.2 * mu, pow(mu, 1.5)), o->mu_min);
       filter_reset(&S->F);
+      S->in_wd = 0;  /* (the line search's Reset: the watchdog ends, its count restarts) */
+      S->wd_cnt = 0;
     }
   }
   const double tau = dmax(1.0 - mu, 0.99);
@@ -907,7 +935,7 @@ static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
   const int tiny = rel < TINY_STEP_TOL && max_abs(dy, m) < TINY_STEP_Y_TOL && E->c_inf < 1e-4;
   S->tiny_flag = tiny && S->tiny_last;
   S->tiny_last = tiny && !S->tiny_last;
-  const double a_min = alpha_min_of(theta_k, gd, S->theta_min);
+  double a_min = alpha_min_of(theta_k, gd, S->theta_min);
   const int soft_now = S->in_soft && !tiny;
   S->soft_cnt += soft_now;
   int searching = !tiny && !soft_now, found = 0, aug = 0;
@@ -915,7 +943,54 @@ static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
   memcpy(st_w, w, sizeof(double) * (size_t)nw);
   double wt[NWMAX], Xt[NMAX];
   double alpha = a_max;
-  for (int ls = 0; ls < (o->max_ls > 1 ? o->max_ls : 1) && searching; ++ls) {
+  /* the line search's references: this iterate's, or the watchdog iterate's */
+  double th_ref = theta_k, ph_ref = phi_k, gd_ref = gd;
+  int sw_ref = switch_ok, ls0 = 0, n_steps = 0, max_soc = o->max_soc;
+  double a_max_r = a_max, a_z_r = a_z;
+  const int was_wd = g_watchdog && S->in_wd && searching;
+  if (was_wd) {  /* one trial: the full step, judged against the watchdog iterate */
+    th_ref = S->wd_th; ph_ref = S->wd_ph; gd_ref = S->wd_gd;
+    sw_ref = S->wd_th <= S->theta_min;
+    for (int k = 0; k < nw; ++k) wt[k] = w[k] + a_max * dw[k];
+    unpack(P, wt, Xt);
+    evaluate_fg(P, Xt, &trial.f, trial.g);
+    double ct[MMAX];
+    cons(P, trial.g, wt, ct);
+    int h = 0;
+    const int ok = acceptable(sum_abs(ct, m), trial.f + barrier(P, wt, mu), th_ref, ph_ref, gd_ref, S->wd_alpha, sw_ref,
+                              S->theta_max, &S->F, 0, &h);
+    searching = 0;
+    if (ok || ++S->wd_trial <= WD_TRIAL_MAX) {  /* acceptable: the watchdog succeeded; else taken anyway */
+      memcpy(st_w, wt, sizeof(double) * (size_t)nw);
+      st_alpha = a_max; aug = h; found = 1;
+      if (ok) { S->in_wd = 0; ++g_wd_events[1]; }
+    } else {
+      ++g_wd_events[2];  /* StopWatchDog: back to the watchdog iterate, a search along its step without the full one */
+      S->in_wd = 0;
+      S->wd_cnt = 0;
+      memcpy(S->w, S->wd_w, sizeof(double) * (size_t)nw);
+      memcpy(S->y, S->wd_y, sizeof(double) * (size_t)m);
+      memcpy(S->zL, S->wd_zL, sizeof(double) * (size_t)nw);
+      memcpy(S->zU, S->wd_zU, sizeof(double) * (size_t)nw);
+      memcpy(dw, S->wd_dw, sizeof(double) * (size_t)nw);
+      memcpy(dy, S->wd_dy, sizeof(double) * (size_t)m);
+      memcpy(dzL, S->wd_dzL, sizeof(double) * (size_t)nw);
+      memcpy(dzU, S->wd_dzU, sizeof(double) * (size_t)nw);
+      S->cur = g_wd_cur;
+      static __thread Errors Ew;
+      errors(P, &S->cur, S->w, S->y, S->zL, S->zU, &Ew);
+      E = &Ew;
+      memcpy(st_w, w, sizeof(double) * (size_t)nw);
+      for (int k = 0; k < nw; ++k) { mdw[k] = -dw[k]; mw[k] = -w[k]; }
+      a_max_r = dmin(max_step(w, dw, P->hasL, P->wl0, nw, tau), max_step(mw, mdw, P->hasU, mwu, nw, tau));
+      a_z_r = dmin(max_step(S->zL, dzL, P->hasL, NULL, nw, tau), max_step(S->zU, dzU, P->hasU, NULL, nw, tau));
+      a_min = alpha_min_of(th_ref, gd_ref, S->theta_min);
+      alpha = 0.5 * a_max_r;
+      searching = alpha > a_min;
+      ls0 = 1; n_steps = 1; max_soc = 0;
+    }
+  }
+  for (int ls = ls0; ls < (o->max_ls > 1 ? o->max_ls : 1) && searching; ++ls) {
     for (int k = 0; k < nw; ++k) wt[k] = w[k] + alpha * dw[k];
     unpack(P, wt, Xt);
     evaluate_fg(P, Xt, &trial.f, trial.g);
@@ -924,11 +999,11 @@ static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
     double th = sum_abs(ct, m);
     double ph = trial.f + barrier(P, wt, mu);
     int h = 0;
-    if (acceptable(th, ph, theta_k, phi_k, gd, alpha, switch_ok, S->theta_max, &S->F, 0, &h)) {
+    if (acceptable(th, ph, th_ref, ph_ref, gd_ref, alpha, sw_ref, S->theta_max, &S->F, 0, &h)) {
       memcpy(st_w, wt, sizeof(double) * (size_t)nw);
       st_alpha = alpha; aug = h; found = 1; searching = 0;
     }
-    if (ls == 0 && o->max_soc > 0 && searching && th >= theta_k) {  /* second-order corrections */
+    if (ls == 0 && max_soc > 0 && searching && th >= theta_k) {  /* second-order corrections */
       double c_soc[MMAX], a_soc = alpha, th_old = th, dws[NWMAX], dys[MMAX], ws[NWMAX], Xs[NMAX];
       memcpy(c_soc, E->c, sizeof(double) * (size_t)m);
       int soc = 1;
@@ -956,7 +1031,26 @@ static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
       }
     }
     alpha = searching ? 0.5 * alpha : alpha;
+    n_steps += searching;
     searching = searching && alpha > a_min;
+  }
+  if (g_watchdog && found) {  /* the shortened-step count; the watchdog starts at this iterate and step */
+    S->wd_cnt = n_steps == 0 ? 0 : S->wd_cnt + 1;
+    if (!S->in_wd && !soft_now && S->wd_cnt >= WD_TRIGGER) {
+      ++g_wd_events[0];
+      S->in_wd = 1;
+      S->wd_trial = 0;
+      memcpy(S->wd_w, w, sizeof(double) * (size_t)nw);
+      memcpy(S->wd_y, S->y, sizeof(double) * (size_t)m);
+      memcpy(S->wd_zL, S->zL, sizeof(double) * (size_t)nw);
+      memcpy(S->wd_zU, S->zU, sizeof(double) * (size_t)nw);
+      memcpy(S->wd_dw, dw, sizeof(double) * (size_t)nw);
+      memcpy(S->wd_dy, dy, sizeof(double) * (size_t)m);
+      memcpy(S->wd_dzL, dzL, sizeof(double) * (size_t)nw);
+      memcpy(S->wd_dzU, dzU, sizeof(double) * (size_t)nw);
+      g_wd_cur = S->cur;
+      S->wd_th = th_ref; S->wd_ph = ph_ref; S->wd_gd = gd_ref; S->wd_alpha = a_max_r;
+    }
   }
   if (tiny) {
     for (int k = 0; k < nw; ++k) st_w[k] = w[k] + a_max * dw[k];
@@ -965,7 +1059,7 @@ static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
   /* soft restoration step */
   const int bt_failed = !tiny && !soft_now && !found;
   const int soft_try = (soft_now && S->soft_cnt <= MAX_SOFT_RESTO) || bt_failed;
-  const double a_soft = dmin(a_max, a_z);
+  const double a_soft = dmin(a_max_r, a_z_r);
   int soft_ok = 0;
   if (soft_try) {
     double wsft[NWMAX], Xsft[NMAX], ys[MMAX], zLs[NWMAX], zUs[NWMAX], cs[MMAX];
@@ -975,7 +1069,7 @@ static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
     evaluate(P, Xsft, &os);
     cons(P, os.g, wsft, cs);
     const double th_s = sum_abs(cs, m), ph_s = os.f + barrier(P, wsft, mu);
-    const int orig_ok = acceptable(th_s, ph_s, theta_k, phi_k, gd, 0.0, switch_ok, S->theta_max, &S->F, 0, NULL);
+    const int orig_ok = acceptable(th_s, ph_s, th_ref, ph_ref, gd_ref, 0.0, sw_ref, S->theta_max, &S->F, 0, NULL);
     for (int r = 0; r < m; ++r) ys[r] = S->y[r] + a_soft * dy[r];
     for (int k = 0; k < nw; ++k) {
       zLs[k] = P->hasL[k] ? S->zL[k] + a_soft * dzL[k] : S->zL[k];
@@ -1002,12 +1096,12 @@ static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
   if (failed) { S->in_soft = 0; S->soft_cnt = 0; }
   const int moved = !failed;
   const double al = st_alpha;
-  const double az = soft_ok ? a_soft : a_z;
+  const double az = soft_ok ? a_soft : a_z_r;
   if (moved) {
     double Xn[NMAX];
     unpack(P, st_w, Xn);
     evaluate(P, Xn, &ev_new);
-    if (aug) filter_add(&S->F, theta_k, phi_k);
+    if (aug) filter_add(&S->F, th_ref, ph_ref);
     double y_new[MMAX];
     for (int r = 0; r < m; ++r) y_new[r] = S->y[r] + al * dy[r];
     for (int k = 0; k < nw; ++k) {
@@ -1029,7 +1123,9 @@ static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
     memcpy(S->y, y_new, sizeof(double) * (size_t)m);
     S->cur = ev_new;
   } else {
-    filter_add(&S->F, theta_k, phi_k);  /* PrepareRestoPhaseStart */
+    filter_add(&S->F, th_ref, ph_ref);  /* PrepareRestoPhaseStart */
+    S->in_wd = 0;  /* (the restoration phase ends the watchdog) */
+    S->wd_cnt = 0;
     enter_resto(P, S, E->c, E->A, S->cur.f);
   }
   S->mu = mu;

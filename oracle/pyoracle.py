@@ -49,6 +49,10 @@ def _load(path=LIB_PATH):
     lib.cplo_set_fallback_viol_tol.restype = None
     lib.cplo_set_nlp_scaling.argtypes = [c_int]
     lib.cplo_set_nlp_scaling.restype = None
+    lib.cplo_set_watchdog.argtypes = [c_int]
+    lib.cplo_set_watchdog.restype = None
+    lib.cplo_watchdog_events.argtypes = [ctypes.POINTER(ctypes.c_long)]
+    lib.cplo_watchdog_events.restype = None
     return lib
 
 
@@ -198,6 +202,20 @@ def set_nlp_scaling(method):
     """nlp_scaling_method of the compiled restatement: "gradient-based" (IPOPT's default, the
     reference's; the default here too) or "none" (process-wide)."""
     lib.cplo_set_nlp_scaling(1 if method == "gradient-based" else 0)
+
+
+def set_watchdog(on):
+    """IPOPT's watchdog in the compiled restatement (opt-in, process-wide; the engine has none): the
+    measurement of its effect (scripts/watchdog_effect.py)."""
+    lib.cplo_set_watchdog(1 if on else 0)
+
+
+def watchdog_events():
+    """(starts, successes, restorations of the kept iterate) of the watchdog on this thread since the
+    last call (single-thread solves)."""
+    out = (ctypes.c_long * 3)()
+    lib.cplo_watchdog_events(out)
+    return tuple(int(v) for v in out)
 
 
 def max_threads():

@@ -417,3 +417,27 @@ def test_split_small_batch_iterations_are_exact(max_ls, max_soc, hessian):
         assert float((a.status <= STATUS_ACCEPTABLE).double().mean()) >= 0.9
     else:
         assert bool((a.status <= STATUS_ACCEPTABLE).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nlp_scaling", ["gradient-based", "none"])
+def test_device_nlp_scaling_matches_host(nlp_scaling):
+    """The engine's NLP scaling (cpl_solve_options.nlp_scaling) against the host restatement over the
+    oracle's callbacks, scaling on and off: the same outcomes and iteration counts, objectives to
+    1e-8, and the returned multipliers (unscaled: dc y / df) certify the unscaled problem's KKT point."""
+    from centroidalplanner_amd.batch_ipm import KernelEvaluator
+
+    prob = solve_problem().GetCplProblem()
+    B = 8
+    X0, mass = solve_inputs(prob, B, seed=17)
+    dev = torch.device("cuda:0")
+    r = batch_ipm_solve(prob, torch.as_tensor(X0, device=dev), torch.as_tensor(mass, device=dev),
+                        evaluator=KernelEvaluator(prob), max_iter=300, hessian="exact", nlp_scaling=nlp_scaling)
+    h = batch_ipm_solve(prob, torch.as_tensor(X0), torch.as_tensor(mass), evaluator=OracleBatchEvaluator(prob),
+                        max_iter=300, hessian="exact", nlp_scaling=nlp_scaling)
+    assert torch.equal(r.status.cpu(), h.status) and bool((h.status == 0).all())
+    assert torch.equal(r.iterations.cpu(), h.iterations)
+    np.testing.assert_allclose(r.objective.cpu().numpy(), h.objective.numpy(), rtol=1e-8)
+    X, Y = r.x.cpu().numpy(), r.y.cpu().numpy()
+    for b in range(B):
+        _certify(prob, X[b], Y[b], mass[b])

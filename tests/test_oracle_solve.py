@@ -54,3 +54,26 @@ def test_time_solve_reports_per_instance_outcomes():
     X0, mass = solve_inputs(prob, 4)
     t, st, it = pyoracle.time_solve(prob.desc(), X0, mass, max_iter=1000)
     assert t > 0 and st.shape == (4,) and (st == 0).all() and (it > 0).all()
+
+
+@pytest.mark.parametrize("hessian", ["limited-memory", "exact"])
+def test_nlp_scaling_off_switch_and_effect(hessian):
+    """IPOPT's gradient-based scaling is active on the solve workload (its torque rows' gradients reach
+    ~1.3e3 at the start, the cone rows ~3e2): the compiled and the host restatement agree with it off
+    (nlp_scaling "none" on both) as with it on, and switching it changes the trajectory."""
+    prob = solve_problem().GetCplProblem()
+    X0, mass = solve_inputs(prob, 2)
+    for b in range(2):
+        pyoracle.set_nlp_scaling("none")
+        try:
+            c0 = pyoracle.solve(prob.desc(), X0[b], mass[b], max_iter=1000, hessian=hessian)
+        finally:
+            pyoracle.set_nlp_scaling("gradient-based")
+        h0 = batch_ipm_solve(prob, torch.as_tensor(X0[b:b + 1]), torch.as_tensor(mass[b:b + 1]), max_iter=1000,
+                             evaluator=OracleBatchEvaluator(prob, 1), hessian=hessian, nlp_scaling="none")
+        assert c0["status"] == int(h0.status[0]) == 0
+        assert c0["iterations"] == int(h0.iterations[0])
+        np.testing.assert_allclose(c0["x"], h0.x[0].numpy(), rtol=0, atol=1e-9)
+        c1 = pyoracle.solve(prob.desc(), X0[b], mass[b], max_iter=1000, hessian=hessian)
+        assert c1["status"] == 0
+        assert c1["iterations"] != c0["iterations"] or np.abs(c1["x"] - c0["x"]).max() > 1e-12
