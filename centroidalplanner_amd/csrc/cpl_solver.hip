@@ -3182,7 +3182,7 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
   int it = 0;
   const int max_iter = S->opt.max_iter;
   const bool compacting = S->opt.compact != 0 && S->opt.use_graph;
-  const int64_t min_rows = 256;
+  const int64_t min_rows = 256;  // (below it a compaction costs more than its smaller iterations save: profiles/r5/compact_floor)
   int32_t resto_rows = 0;  // instances in the restoration phase after the previous iteration
   // the mailbox's sequence: the device counter restarts with this solve (the previous solve ended
   // with a stream synchronisation, so nothing is still writing the host side)
