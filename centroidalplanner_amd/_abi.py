@@ -214,6 +214,7 @@ SIGNATURES = {
     "cpl_solver_stats": (c_int32, [c_void_p, POINTER(c_int32), POINTER(c_int64)]),
     "cpl_solver_restorations": (c_int32, [c_void_p, c_void_p, c_void_p]),
     "cpl_solver_fallbacks": (c_int32, [c_void_p, c_void_p, c_void_p]),
+    "cpl_solver_nan_jacobian": (c_int32, [c_void_p, c_void_p, c_void_p]),
 }
 
 

@@ -157,6 +157,7 @@ class BatchSolveResult:
     compactions: int = 0  # active-set compactions of the native engine (the batch shrank this often)
     restorations: object = None  # [B] int: restoration-phase entries per instance
     fallback: object = None  # [B] bool: x is the best feasible iterate, not the last (fallback_viol_tol)
+    nan_jacobian: object = None  # [B] int: NaN Jacobian entries at the start point (taken as 0)
 
     @property
     def success(self):
@@ -237,10 +238,13 @@ class NativeSolver:
         fb = torch.empty(B, dtype=torch.uint8, device=dev)
         _abi.check(_abi.lib.cpl_solver_fallbacks(self.handle, _ptr(fb),
                                                  ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+        nanj = torch.empty(B, dtype=torch.int32, device=dev)
+        _abi.check(_abi.lib.cpl_solver_nan_jacobian(self.handle, _ptr(nanj),
+                                                    ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
         return BatchSolveResult(x=x, y=y, status=status.to(torch.int64), iterations=iters.to(torch.int64),
                                 objective=obj, primal_inf=pinf, dual_inf=dinf, evaluations=int(ev.value),
                                 iterations_run=int(it.value), graph=bool(g.value), compactions=int(nc.value),
-                                restorations=resto, fallback=fb.bool())
+                                restorations=resto, fallback=fb.bool(), nan_jacobian=nanj.to(torch.int64))
 
 
 _NATIVE_CACHE = {}
@@ -380,9 +384,11 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     # IPOPT's gradient-based NLP scaling at the starting point (see the docstring): df [B], dc [B, m]
     df = torch.ones(B, dtype=dt, device=dev)
     dc = torch.ones(B, m, dtype=dt, device=dev)
+    # (the callbacks at the start point also give the NaN Jacobian entries there: the cone's 0/0)
+    n_eval += 1
+    o0 = ev(Xbase, Mass, outputs=("jac", "grad"))
+    nan_jacobian = torch.isnan(o0["jac"]).sum(1)
     if nlp_scaling == "gradient-based":
-        n_eval += 1
-        o0 = ev(Xbase, Mass, outputs=("jac", "grad"))
         gmax = torch.nan_to_num(o0["grad"][:, free], nan=0.0).abs().amax(1) if nf else zeros_B
         df = torch.where(gmax > SCALING_MAX_GRADIENT,
                          torch.clamp(SCALING_MAX_GRADIENT / torch.where(gmax > 0, gmax, 1.0), min=SCALING_MIN_VALUE),
@@ -1314,5 +1320,6 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                            objective=fin["f"].clone(), primal_inf=viol, dual_inf=S["d_inf"], evaluations=n_eval,
                            iterations_run=it_run, graph=False)
     res.restorations = S["n_resto"]
+    res.nan_jacobian = nan_jacobian
     res.fallback = fallback
     return res

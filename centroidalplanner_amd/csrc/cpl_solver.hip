@@ -187,15 +187,23 @@ __global__ __launch_bounds__(256) void k_init_state(
 // equalities, the inequalities) whose largest row gradient exceeds 100, dc_r = max(1e-8,
 // 100 * (1 / max(100, max_j |J_rj|))) on each row of the block.  Gradients over the free variables
 // (srp / srq: the free-column records of each row), a NaN entry counting as 0.  any[0] = 1 when an
-// instance has a factor != 1.
-__global__ __launch_bounds__(256) void k_nlp_scaling(int64_t B, int n, int m, int nnz_rec, const uint8_t* __restrict__ is_fixed,
+// instance has a factor != 1.  Also (always) the NaN entries of the instance's Jacobian there — the
+// 0/0 of a cone at F_t = 0, which the iteration takes as 0 — into nan_cnt[b] (scale = 0: that only).
+__global__ __launch_bounds__(256) void k_nlp_scaling(int64_t B, int n, int m, int nnz_rec, int scale,
+                                                     const uint8_t* __restrict__ is_fixed,
                                                      const int32_t* __restrict__ row_slack, const int32_t* __restrict__ srp,
                                                      const int32_t* __restrict__ srq, const double* __restrict__ grad,
                                                      const double* __restrict__ J, double* __restrict__ df,
-                                                     double* __restrict__ dc, uint8_t* __restrict__ any) {
+                                                     double* __restrict__ dc, uint8_t* __restrict__ any,
+                                                     int32_t* __restrict__ nan_cnt) {
   const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
   if (b >= B) return;
   const int lane = threadIdx.x & 63;
+  int nans = 0;
+  for (int q = lane; q < nnz_rec; q += 64) nans += J[b * nnz_rec + q] != J[b * nnz_rec + q];
+  nans = (int)wave_sum((double)nans);
+  if (lane == 0) nan_cnt[b] = nans;
+  if (!scale) return;
   double gm = 0.0;
   for (int j = lane; j < n; j += 64)
     if (!is_fixed[j]) {
@@ -2146,6 +2154,7 @@ struct cpl_solver {
   // factor != 1 (the scaling kernels run; graphs keyed by it)
   double *df, *dc, *ytil;
   int32_t *rrow, *srp, *srq;
+  int32_t* nan_cnt;  // [B] full batch: NaN Jacobian entries at each instance's start point
   uint8_t* sc_any;
   bool scaled = false;
 };
@@ -2853,6 +2862,13 @@ int32_t cpl_solver_fallbacks(const cpl_solver* S, uint8_t* d_out, void* stream) 
   return CPL_OK;
 }
 
+int32_t cpl_solver_nan_jacobian(const cpl_solver* S, int32_t* d_out, void* stream) {
+  if (!S || !d_out) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_solver_nan_jacobian: null argument");
+  HK(hipMemcpyAsync(d_out, S->nan_cnt, 4 * (size_t)S->B, hipMemcpyDeviceToDevice, (hipStream_t)stream),
+     "hipMemcpyAsync nan_jacobian");
+  return CPL_OK;
+}
+
 int32_t cpl_solver_restorations(const cpl_solver* S, int64_t* d_out, void* stream) {
   if (!S || !d_out) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_solver_restorations: null argument");
   HK(hipMemcpyAsync(d_out, S->fresto, 8 * (size_t)S->B, hipMemcpyDeviceToDevice, (hipStream_t)stream),
@@ -3074,7 +3090,7 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   S->scratch = a.take<uint64_t>(Bz * (size_t)S->scratch_words);
   S->df = a.take<double>(Bz); S->dc = a.take<double>(Bz * m); S->ytil = a.take<double>(S->bfgs ? 0 : Bz * m);
   S->rrow = a.take<int32_t>(nnz_rec); S->srp = a.take<int32_t>(m + 1); S->srq = a.take<int32_t>(srq.size());
-  S->sc_any = a.take<uint8_t>(4);
+  S->sc_any = a.take<uint8_t>(4); S->nan_cnt = a.take<int32_t>(Bz);
   };
   Arena probe;
   carve(probe);
@@ -3147,14 +3163,15 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
   LAUNCHED("k_xbase");
   // IPOPT's gradient-based NLP scaling from the callbacks at the starting point (fixed variables at
   // their value); the iteration runs on the scaled problem when any instance has a factor != 1
+  // (and the NaN Jacobian entries there: cpl_solver_nan_jacobian)
   S->scaled = false;
+  CK(eval_full(S, S->Xbase, S->f, S->grad, S->g, S->J));
+  ++evals;
+  HK(hipMemsetAsync(S->sc_any, 0, 4, st), "hipMemsetAsync");
+  hipLaunchKernelGGL(k_nlp_scaling, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, S->nnz_rec, S->opt.nlp_scaling,
+                     S->is_fixed, S->row_slack, S->srp, S->srq, S->grad, S->J, S->df, S->dc, S->sc_any, S->nan_cnt);
+  LAUNCHED("k_nlp_scaling");
   if (S->opt.nlp_scaling) {
-    CK(eval_full(S, S->Xbase, S->f, S->grad, S->g, S->J));
-    ++evals;
-    HK(hipMemsetAsync(S->sc_any, 0, 4, st), "hipMemsetAsync");
-    hipLaunchKernelGGL(k_nlp_scaling, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, S->nnz_rec, S->is_fixed,
-                       S->row_slack, S->srp, S->srq, S->grad, S->J, S->df, S->dc, S->sc_any);
-    LAUNCHED("k_nlp_scaling");
     HK(hipMemcpyAsync(S->h_flag, S->sc_any, 4, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
     HK(hipStreamSynchronize(st), "hipStreamSynchronize");
     S->scaled = S->h_flag[0] != 0;

@@ -80,6 +80,19 @@ void BatchSolver::Solve(const double* x0, const double* mass, double* x, double*
   hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
 }
 
+void BatchSolver::NanJacobian(int32_t* counts) const {
+  const size_t B = (size_t)_batch;
+  int32_t* d = nullptr;
+  hip_check(hipMalloc(&d, 4 * B), "hipMalloc");
+  const hipStream_t s = (hipStream_t)_stream;
+  const int32_t st = cpl_solver_nan_jacobian(_solver, d, s);
+  hipError_t e = st == CPL_OK ? hipMemcpyAsync(counts, d, 4 * B, hipMemcpyDeviceToHost, s) : hipSuccess;
+  if (e == hipSuccess && st == CPL_OK) e = hipStreamSynchronize(s);
+  (void)hipFree(d);
+  engine_check(st);
+  hip_check(e, "hipMemcpyAsync nan_jacobian");
+}
+
 bool NativeSolver::Solve(CplTNLP& nlp) {
   const CplProblem::Ptr& prob = nlp.problem();
   const int32_t n = prob->n(), m = prob->m();
@@ -89,14 +102,6 @@ bool NativeSolver::Solve(CplTNLP& nlp) {
     std::vector<double> xl(n), xu(n), gl(m), gu(m);
     nlp.get_bounds_info(n, xl.data(), xu.data(), m, gl.data(), gu.data());
     for (int32_t j = 0; j < n; ++j) x0[j] = std::fmin(std::fmax(x0[j], xl[j]), xu[j]);
-  }
-  {  // NaN Jacobian entries at the start point (the 0/0 of a cone at F_t = 0): counted and reported
-    int32_t nn = 0, mm = 0, nnz = 0, nh = 0;
-    nlp.get_nlp_info(nn, mm, nnz, nh);
-    std::vector<double> jv((size_t)nnz);
-    _nan_jac_start = 0;
-    if (nnz > 0 && nlp.eval_jac_g(n, x0.data(), true, m, nnz, nullptr, nullptr, jv.data()))
-      for (double v : jv) _nan_jac_start += std::isnan(v) ? 1 : 0;
   }
   _dreport = cpl_derivative_report{};
   if (_opt.derivative_test) {  // IPOPT checks the first derivatives before it iterates
@@ -120,6 +125,9 @@ bool NativeSolver::Solve(CplTNLP& nlp) {
     _bs_desc = prob->Desc();
   }
   _bs->Solve(x0.data(), nullptr, x.data(), nullptr, &_status, &_iterations, nullptr, &_primal_inf);
+  // NaN Jacobian entries at the start point (the 0/0 of a cone at F_t = 0), counted by the engine's
+  // own start-point evaluation
+  _bs->NanJacobian(&_nan_jac_start);
   nlp.finalize_solution(n, x.data());
   return _status == CPL_SOLVE_OPTIMAL || _status == CPL_SOLVE_ACCEPTABLE;
 }

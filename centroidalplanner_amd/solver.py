@@ -7,12 +7,12 @@ this image; the same method runs here as the batched solve loop (batch_ipm.py, t
 8,192-instance solves) with B = 1: on the GPU (HIP kernels, the iteration captured as a HIP graph)
 when no evaluator is given, else on the host over the evaluator's callbacks (tests inject the
 oracle).  Like IFOPT's solver, a run that ends without convergence does not throw: the last iterate
-is kept (src/CentroidalPlanner.cpp:29-33), `success` says how it ended — except that when that last
-iterate violates the constraints (by more than 1e-9) and an earlier iterate satisfied them, the
-lowest-objective such iterate is returned instead (`fallback`; IPOPT itself returns the last one).
-Where the start point's constraint Jacobian has NaN entries (FrictionCone's 0/0 at a zero
-tangential force, e.g. x = 0) the loop takes them as 0; the count is returned
-(`nan_jacobian_at_start`) and a RuntimeWarning says so — IPOPT would receive the NaNs.
+is kept (src/CentroidalPlanner.cpp:29-33) and `success` says how it ended (the engine's opt-in
+best-feasible fallback is off here, as IPOPT returns its last iterate).  IPOPT's gradient-based NLP
+scaling is on, as in the reference.  Where the start point's constraint Jacobian has NaN entries
+(FrictionCone's 0/0 at a zero tangential force, e.g. x = 0) the loop takes them as 0; the solve's own
+start-point evaluation counts them (cpl_solver_nan_jacobian — no extra evaluation), the count is
+returned (`nan_jacobian_at_start`) and a RuntimeWarning says so — IPOPT would receive the NaNs.
 Evaluators expose ``eval_batch(X[B, n]) -> {f, grad, g, jac}`` (host arrays).
 """
 from __future__ import annotations
@@ -74,12 +74,6 @@ def solve(problem, evaluator=None, x0: Optional[np.ndarray] = None, tol: float =
 
     xl, xu, _, _ = problem.get_bounds_info()
     x0 = np.clip(problem.get_starting_point() if x0 is None else np.asarray(x0, dtype=np.float64), xl, xu)
-    jac0 = problem.eval_jac_g(x0) if evaluator is None else np.asarray(evaluator.eval_batch(x0[None])["jac"])[0]
-    nan0 = int(np.isnan(jac0).sum())
-    if nan0:
-        warnings.warn(f"{nan0} constraint Jacobian entries are NaN at the start point (FrictionCone's 0/0 where "
-                      f"a contact's tangential force is 0, src/Constraints/FrictionCone.cpp:85-87); IPOPT would "
-                      f"receive them as NaN, this solve takes them as 0 (a subgradient)", RuntimeWarning, stacklevel=2)
     report = None
     if evaluator is None:
         X0 = torch.as_tensor(x0[None], device=torch.device("cuda", torch.cuda.current_device()))
@@ -89,6 +83,12 @@ def solve(problem, evaluator=None, x0: Optional[np.ndarray] = None, tol: float =
     else:
         r = batch_ipm_solve(problem, torch.as_tensor(x0[None]), None, evaluator=_HostBatchEvaluator(evaluator),
                             tol=tol, max_iter=max_iter, hessian=hessian)
+    # the NaN Jacobian entries the solve's own start-point evaluation met (cpl_solver_nan_jacobian)
+    nan0 = int(r.nan_jacobian[0])
+    if nan0:
+        warnings.warn(f"{nan0} constraint Jacobian entries are NaN at the start point (FrictionCone's 0/0 where "
+                      f"a contact's tangential force is 0, src/Constraints/FrictionCone.cpp:85-87); IPOPT would "
+                      f"receive them as NaN, this solve takes them as 0 (a subgradient)", RuntimeWarning, stacklevel=2)
     x = r.x[0].cpu().numpy()
     st = int(r.status[0])
     problem.SetVariables(x)  # the next Solve warm-starts here, like the reference's persistent variables

@@ -60,6 +60,9 @@ class BatchSolver {
   int64_t batch() const { return _batch; }
   int32_t iterations_run() const { return _iterations_run; }
   bool graph_captured() const;
+  // per instance, the NaN Jacobian entries the last Solve met at its start point (taken as 0):
+  // counts [batch] on the host (cpl_solver_nan_jacobian)
+  void NanJacobian(int32_t* counts) const;
 
  private:
   void release();  // frees every device resource (idempotent: pointers nulled)

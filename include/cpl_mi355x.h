@@ -560,6 +560,10 @@ int32_t cpl_solver_stats(const cpl_solver* s, int32_t* compactions, int64_t* fin
 int32_t cpl_solver_fallbacks(const cpl_solver* s, uint8_t* d_out, void* stream);
 /* the last solve's restoration-phase entries per instance into d_out [batch] (device int64) */
 int32_t cpl_solver_restorations(const cpl_solver* s, int64_t* d_out, void* stream);
+/* the last solve's NaN constraint-Jacobian entries per instance at its start point (x0 with the fixed
+ * variables at their values; the cone's 0/0 at F_t = 0, src/Constraints/FrictionCone.cpp:85-87), which
+ * the iteration takes as 0 where IPOPT would receive NaN, into d_out [batch] (device int32) */
+int32_t cpl_solver_nan_jacobian(const cpl_solver* s, int32_t* d_out, void* stream);
 
 #ifdef __cplusplus
 }
