@@ -1203,11 +1203,13 @@ __device__ __forceinline__ void cone_rows(const KParams& K, int i, const double*
   }
 }
 
-// CONE = false: the row-1 item leaves the contact's friction cone to a separate item (sq_cone_item)
-template <bool AXL, bool CONE = true>
-__device__ __forceinline__ void sq_row_item(const KParams& K, const double* __restrict__ xr, int k, int a,
+// CONE = false: the row-1 item leaves the contact's friction cone to a separate item (sq_cone_item).
+// AF >= 0: the axis a compile-time constant (a == AF): the three entries' chains in one basic block
+template <bool AXL, bool CONE = true, int AF = -1>
+__device__ __forceinline__ void sq_row_item(const KParams& K, const double* __restrict__ xr, int k, int a_arg,
                                             const double* __restrict__ Lc, double* __restrict__ Gr,
                                             double* __restrict__ Jr) {
+  const int a = AF >= 0 ? AF : a_arg;
   const int i = s_ct.map_order[k];
   const double* q = xr + 3 + 9 * i;
   double* gk = Gr + 6 + 6 * k;
@@ -1495,14 +1497,23 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
         for (int it = tid; it < r_rows; it += WG) {
           const int a = __builtin_amdgcn_readfirstlane(it) / PA, kj = it - a * PA;
           const int k = kj >> K.logT, r = kj & (T - 1);
-          if (kj < per_axis && r < valid)
-            sq_row_item<false, !CONE_ITEMS>(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m, JR(r));
+          if (kj < per_axis && r < valid) {  // a wave-uniform: the row item specialised on its axis — the
+            // three entries' chains in one basic block, interleaved (97 -> 127 VGPRs, still four waves
+            // per SIMD; bitwise; sq8 0.316 -> 0.299 ms, profiles/r5/sq_rowaf/)
+            double* const Lr = L + r * K.LR + k * SQ_L;
+            if (a == 0) sq_row_item<false, !CONE_ITEMS, 0>(K, X + r * n, k, a, Lr, Gt + r * m, JR(r));
+            else if (a == 1) sq_row_item<false, !CONE_ITEMS, 1>(K, X + r * n, k, a, Lr, Gt + r * m, JR(r));
+            else sq_row_item<false, !CONE_ITEMS, 2>(K, X + r * n, k, a, Lr, Gt + r * m, JR(r));
+          }
         }
       else if (HAS_SQ)
         for (int it = tid; it < r_rows; it += WG) {
           const int a = it / per_axis, kj = it - a * per_axis;
           const int k = kj / n_sq, j = kj - k * n_sq;
           const int r = ENVK == CPL_ENV_MIXED ? lists[j] : j;
+          // (the list tiles' waves also share one axis, but the axis-specialised row items cost their
+          // kernel 144-149 VGPRs (three waves per SIMD): 2.55 -> 2.84 ms for mixed16, 2.64 capped at
+          // four waves with 8-12 spilled VGPRs; profiles/r5/sq_rowaf/)
           sq_row_item<ENVK == CPL_ENV_MIXED, !CONE_ITEMS>(K, X + r * n, k, a, L + r * K.LR + k * SQ_L, Gt + r * m,
                                                           JR(r));
         }

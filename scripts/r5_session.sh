@@ -1,5 +1,7 @@
-# round-5 GPU session: the GPU suite after the engine-side NaN count, then the plain-double power-ladder A/B
+# round-5 GPU session: uniform-axis row items in the kind split's Superquadric list tiles (with / without a 4-wave cap)
 set -o pipefail
-O=gpurun_out/r5_g11; mkdir -p $O
-timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > $O/tests.log 2>&1 || exit $?
-bash scripts/ab_eval.sh $O/plain centroidalplanner_amd/libcpl_mi355x.so build/libcpl_plain.so sq8 sq16 mixed16
+O=gpurun_out/r5_g14; mkdir -p $O
+L=centroidalplanner_amd/libcpl_mi355x.so,build/libcpl_lu.so,build/libcpl_lu_cap.so
+timeout -k 10 300 python -u scripts/ab_libs.py --config mixed16 --rounds 5 --reps 10 --libs $L > $O/mixed16.jsonl 2> $O/mixed16.err || exit $?
+timeout -k 10 300 python -u scripts/ab_libs.py --config mixed16 --rounds 5 --reps 10 --libs $L --tags all_sq > $O/mixed16_allsq.jsonl 2> $O/allsq.err || exit $?
+timeout -k 10 300 python -u scripts/ab_libs.py --config sq8 --rounds 5 --reps 10 --libs $L > $O/sq8.jsonl 2> $O/sq8.err || exit $?
