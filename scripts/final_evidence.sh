@@ -40,6 +40,7 @@ fi
 step 300 bash -c "python -u bench.py --config sq8 > $out/bench_sq8.json 2> $out/bench_sq8.err"
 step 300 bash -c "python -u bench.py --config mixed16 > $out/bench_mixed16.json 2> $out/bench_mixed16.err"
 step 300 bash -c "python -u bench.py --config solve5 --hessian limited-memory > $out/bench_solve5_lbfgs.json 2> $out/bench_solve5_lbfgs.err"
+step 300 bash -c "python -u bench.py --config solve5 > $out/bench_solve5_exact.json 2> $out/bench_solve5_exact.err"
 step 300 bash -c "python -u scripts/solve_latency.py --reps 10 > $out/solve_latency.json 2> $out/solve_latency.err"
 step 300 bash -c "python -u scripts/testbasic_outcomes.py gpu > $out/testbasic_gpu.jsonl 2> $out/testbasic_gpu.err"
 echo done
