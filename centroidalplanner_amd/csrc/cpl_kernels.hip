@@ -981,10 +981,16 @@ __device__ __forceinline__ void contact_item(const KParams& K, const double* __r
 
 // CentroidalStatics::GetValues (src/Constraints/CentroidalStatics.cpp:37-61) and Jacobian rows 0-2
 // (the I3 of every F_i, :93-95)
+// pairs_j: the torque rows' CoM pairs written straight to their Jacobian entries (row q's first two)
+// instead of com6 — the Superquadric tile, whose cone items write the rows' per-contact entries
 __device__ __forceinline__ void statics_values_item(const KParams& K, const double* __restrict__ xr, double m_i,
                                                     double* __restrict__ Gr, double* __restrict__ Jr,
-                                                    bool with_j = true, double* __restrict__ com6 = nullptr) {
+                                                    bool with_j = true, double* __restrict__ com6 = nullptr,
+                                                    bool pairs_j = false) {
   const int N = K.N;
+  if (pairs_j && K.want_j) {
+    com6 = Jr + (K.fold == FOLD_NONE ? 3 * N : 0);  // row q's pair at com6[q * (2 + 4N) + {0, 1}]
+  }
   if (com6) {  // the torque rows' CoM pairs (statics_row_item's a1, a2 for rows 3, 4, 5), map order
     double a[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     for (int k = 0; k < N; ++k) {
@@ -993,8 +999,13 @@ __device__ __forceinline__ void statics_values_item(const KParams& K, const doub
       a[2] -= -(1.0) * F[2];  a[3] -= -(-1.0) * F[0];  // row 4: (2, +), (0, -)
       a[4] -= -(-1.0) * F[1]; a[5] -= -(1.0) * F[0];   // row 5: (1, -), (0, +)
     }
+    if (pairs_j) {
 #pragma unroll
-    for (int t = 0; t < 6; ++t) com6[t] = a[t];
+      for (int t = 0; t < 6; ++t) com6[(t >> 1) * (2 + 4 * N) + (t & 1)] = a[t];
+    } else {
+#pragma unroll
+      for (int t = 0; t < 6; ++t) com6[t] = a[t];
+    }
   }
   if (K.want_g) {
     const double c0 = xr[0], c1 = xr[1], c2 = xr[2];
@@ -1299,11 +1310,32 @@ __device__ __forceinline__ void sq_row_item(const KParams& K, const double* __re
 }
 
 // the friction cone rows of contact block k (map order) of a Superquadric record, as sq_row_item's
-// row-1 item computes them
+// row-1 item computes them; statics (the Superquadric tile): also contact i's entries of the statics
+// Jacobian — its three ones of the force rows and its four entries in each torque row, the values
+// statics_row_item computes (the rows' CoM pairs: statics_values_item, pairs_j)
 __device__ __forceinline__ void sq_cone_item(const KParams& K, const double* __restrict__ xr, int k,
-                                             double* __restrict__ Gr, double* __restrict__ Jr) {
+                                             double* __restrict__ Gr, double* __restrict__ Jr,
+                                             bool statics = false) {
   const int i = s_ct.map_order[k];
   cone_rows(K, i, xr + 3 + 9 * i, Gr + 6 + 6 * k + 4, Jr + K.jbase + K.cstride * k + (K.fold != FOLD_NONE ? 12 : 15));
+  if (!statics || !K.want_j) return;
+  const int N = K.N;
+  if (K.fold == FOLD_NONE) { Jr[3 * k] = 1.0; Jr[3 * k + 1] = 1.0; Jr[3 * k + 2] = 1.0; }  // (3N ones, any order)
+  const double* F = xr + 3 + 9 * i;
+  const double* p = F + 3;
+  double* rows = Jr + (K.fold == FOLD_NONE ? 3 * N : 0) + 2 + 4 * i;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {  // (e1, e2) and signs as statics_row_item
+    const int e1 = q == 2 ? 1 : 2;
+    const int e2 = q == 0 ? 1 : 0;
+    const double s1 = q == 1 ? 1.0 : -1.0;
+    const double s2 = q == 1 ? -1.0 : 1.0;
+    double* row = rows + q * (2 + 4 * N);
+    row[0] = s1 * (p[e1] - xr[e1]);
+    row[1] = s2 * (p[e2] - xr[e2]);
+    row[2] = -s1 * F[e1];
+    row[3] = -s2 * F[e2];
+  }
 }
 
 // JD: the Jacobian items write their entries straight to the output records (K.jdirect); a
@@ -1435,7 +1467,11 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
     const int PA = UAX ? ((per_axis + 63) & ~63) : per_axis;
     const int r_ax = (HAS_SQ && wgj) ? 3 * PA : 0;
     const int r_gr = (ENVK != CPL_ENV_SUPERQUADRIC && wgj) ? N * n_gr : 0;
-    const int r_st = wgj ? (JD ? 1 : 4) * valid : 0;  // (JD: the statics J rows by statics_rows_coop)
+    // (JD: the statics J rows by statics_rows_coop; Superquadric tiles (SQST): the rows' per-contact
+    // entries by the cone items of phase 2, their CoM pairs by the values item — three serial
+    // 2 + 4N-entry row items had bounded phase 1)
+    constexpr bool SQST = ENVK == CPL_ENV_SUPERQUADRIC && !JD;
+    const int r_st = wgj ? ((JD || SQST) ? 1 : 4) * valid : 0;
     double* com6 = smem + K.offA;                        // (JD) [T][6]
     const int r_co = K.cost_seg >= 0 ? valid : 0;
     const int r_oth = r_gr + r_st + r_co;
@@ -1452,8 +1488,8 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
         const int r = e % valid, sg = e / valid;
         const double* xr = X + r * n;
         if (sg == 0)
-          statics_values_item(K, xr, mass ? mass[inst(r)] : mass_def, Gt + r * m, JR(r), !JD,
-                              JD && K.want_j ? com6 + 6 * r : nullptr);
+          statics_values_item(K, xr, mass ? mass[inst(r)] : mass_def, Gt + r * m, JR(r), !JD && !SQST,
+                              JD && K.want_j ? com6 + 6 * r : nullptr, SQST);
         else if (K.want_j) statics_row_item(K, xr, sg - 1, JR(r));
         return;
       }
@@ -1521,7 +1557,7 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
         if (it < r_rows) continue;
         if (CONE_ITEMS) {
           const int e = it - r_rows, k = e >> K.logT, r = e & (T - 1);
-          if (r < valid) sq_cone_item(K, X + r * n, k, Gt + r * m, JR(r));
+          if (r < valid) sq_cone_item(K, X + r * n, k, Gt + r * m, JR(r), SQST);
         } else {
           other_item(it - r_rows);
         }

@@ -1,7 +1,8 @@
-# round-5 GPU session: uniform-axis row items in the kind split's Superquadric list tiles (with / without a 4-wave cap)
+# round-5 GPU session: the SQST build's GPU tests, then the phase ablations on it (measurement-only build)
 set -o pipefail
-O=gpurun_out/r5_g14; mkdir -p $O
-L=centroidalplanner_amd/libcpl_mi355x.so,build/libcpl_lu.so,build/libcpl_lu_cap.so
-timeout -k 10 300 python -u scripts/ab_libs.py --config mixed16 --rounds 5 --reps 10 --libs $L > $O/mixed16.jsonl 2> $O/mixed16.err || exit $?
-timeout -k 10 300 python -u scripts/ab_libs.py --config mixed16 --rounds 5 --reps 10 --libs $L --tags all_sq > $O/mixed16_allsq.jsonl 2> $O/allsq.err || exit $?
-timeout -k 10 300 python -u scripts/ab_libs.py --config sq8 --rounds 5 --reps 10 --libs $L > $O/sq8.jsonl 2> $O/sq8.err || exit $?
+O=gpurun_out/r5_g19; mkdir -p $O
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > $O/tests.log 2>&1 || exit $?
+V=0:0:256:1:0,0:0:256:1:2048,0:0:256:1:4096,0:0:256:1:8192,0:0:256:1:16384,0:0:256:1:30720,0:0:256:1:1,0:0:256:1:2
+for c in sq8 sq16; do
+CPL_LIB=build/libcpl_abl2.so timeout -k 10 300 python -u scripts/ab_kernels.py --config $c --rounds 5 --reps 10 --variants $V --norms > $O/${c}_phases.jsonl || exit $?
+done
