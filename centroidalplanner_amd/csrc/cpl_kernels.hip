@@ -991,38 +991,57 @@ __device__ __forceinline__ void statics_values_item(const KParams& K, const doub
   if (pairs_j && K.want_j) {
     com6 = Jr + (K.fold == FOLD_NONE ? 3 * N : 0);  // row q's pair at com6[q * (2 + 4N) + {0, 1}]
   }
-  if (com6) {  // the torque rows' CoM pairs (statics_row_item's a1, a2 for rows 3, 4, 5), map order
-    double a[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    for (int k = 0; k < N; ++k) {
-      const double* F = xr + 3 + 9 * s_ct.map_order[k];
-      a[0] -= -(-1.0) * F[2]; a[1] -= -(1.0) * F[1];   // row 3: (e1, s1) = (2, -), (e2, s2) = (1, +)
-      a[2] -= -(1.0) * F[2];  a[3] -= -(-1.0) * F[0];  // row 4: (2, +), (0, -)
-      a[4] -= -(-1.0) * F[1]; a[5] -= -(1.0) * F[0];   // row 5: (1, -), (0, +)
-    }
-    if (pairs_j) {
-#pragma unroll
-      for (int t = 0; t < 6; ++t) com6[(t >> 1) * (2 + 4 * N) + (t & 1)] = a[t];
-    } else {
-#pragma unroll
-      for (int t = 0; t < 6; ++t) com6[t] = a[t];
-    }
-  }
-  if (K.want_g) {
+  const bool pairs = com6 != nullptr, vals = K.want_g != 0;
+  if (pairs || vals) {
+    // com6: the torque rows' CoM pairs (statics_row_item's a1, a2 for rows 3, 4, 5); vals: the six
+    // statics values — every sum over the contacts in map order.  The contacts four at a time, their
+    // map-order indices and x entries loaded before the sums (one contact per trip waited two
+    // dependent LDS round trips each: the item was the longest of a 16-contact Superquadric tile's
+    // first phase); each sum's order unchanged (bitwise)
     const double c0 = xr[0], c1 = xr[1], c2 = xr[2];
     double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0, v4 = 0.0, v5 = 0.0;
-    for (int k = 0; k < N; ++k) {
-      const double* q = xr + 3 + 9 * s_ct.map_order[k];
-      const double F0 = q[0], F1 = q[1], F2 = q[2];
-      const double d0 = q[3] - c0, d1 = q[4] - c1, d2 = q[5] - c2;
-      v0 += F0; v1 += F1; v2 += F2;
-      v3 += d1 * F2 - d2 * F1;
-      v4 += d2 * F0 - d0 * F2;
-      v5 += d0 * F1 - d1 * F0;
+    double a[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int k0 = 0; k0 < N; k0 += 4) {
+      double q[4][6];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const double* qq = xr + 3 + 9 * s_ct.map_order[k0 + u < N ? k0 + u : k0];
+#pragma unroll
+        for (int e = 0; e < 6; ++e) q[u][e] = qq[e];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (k0 + u >= N) break;
+        const double F0 = q[u][0], F1 = q[u][1], F2 = q[u][2];
+        if (pairs) {
+          a[0] -= -(-1.0) * F2; a[1] -= -(1.0) * F1;   // row 3: (e1, s1) = (2, -), (e2, s2) = (1, +)
+          a[2] -= -(1.0) * F2;  a[3] -= -(-1.0) * F0;  // row 4: (2, +), (0, -)
+          a[4] -= -(-1.0) * F1; a[5] -= -(1.0) * F0;   // row 5: (1, -), (0, +)
+        }
+        if (vals) {
+          const double d0 = q[u][3] - c0, d1 = q[u][4] - c1, d2 = q[u][5] - c2;
+          v0 += F0; v1 += F1; v2 += F2;
+          v3 += d1 * F2 - d2 * F1;
+          v4 += d2 * F0 - d0 * F2;
+          v5 += d0 * F1 - d1 * F0;
+        }
+      }
     }
-    v0 -= K.wrench[0]; v1 -= K.wrench[1]; v2 -= K.wrench[2];
-    v3 -= K.wrench[3]; v4 -= K.wrench[4]; v5 -= K.wrench[5];
-    v0 += m_i * K.gravity[0]; v1 += m_i * K.gravity[1]; v2 += m_i * K.gravity[2];
-    Gr[0] = v0; Gr[1] = v1; Gr[2] = v2; Gr[3] = v3; Gr[4] = v4; Gr[5] = v5;
+    if (pairs) {
+      if (pairs_j) {
+#pragma unroll
+        for (int t = 0; t < 6; ++t) com6[(t >> 1) * (2 + 4 * N) + (t & 1)] = a[t];
+      } else {
+#pragma unroll
+        for (int t = 0; t < 6; ++t) com6[t] = a[t];
+      }
+    }
+    if (vals) {
+      v0 -= K.wrench[0]; v1 -= K.wrench[1]; v2 -= K.wrench[2];
+      v3 -= K.wrench[3]; v4 -= K.wrench[4]; v5 -= K.wrench[5];
+      v0 += m_i * K.gravity[0]; v1 += m_i * K.gravity[1]; v2 += m_i * K.gravity[2];
+      Gr[0] = v0; Gr[1] = v1; Gr[2] = v2; Gr[3] = v3; Gr[4] = v4; Gr[5] = v5;
+    }
   }
   if (with_j && K.want_j && K.fold == FOLD_NONE)  // folded layouts skip the constant I3 blocks
     for (int e = 0; e < 3 * N; ++e) Jr[e] = 1.0;
