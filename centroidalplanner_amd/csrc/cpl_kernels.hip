@@ -101,6 +101,11 @@ struct KParams {
                              // output records instead of the LDS tile image (smaller tiles' LDS)
   int32_t offA;              // (jdirect) doubles offset of the statics CoM-pair scratch [T][6]
   int32_t offRB, offCS, offST;  // entry kernel: row bases [2][T] (int64), cone scratch, statics scratch
+  // (the solve engine's NLP scaling, eval_batch_scaled; pipelined kernel only) f, grad times
+  // sc_df[b], g row r times sc_dc[b, r], Jacobian entry q (row sc_row[q]) times sc_dc[b, sc_row[q]]
+  const double* sc_df;
+  const double* sc_dc;
+  const int32_t* sc_row;
 };
 static_assert(sizeof(KParams) < 4096, "kernel parameters must fit the kernarg segment");
 
@@ -1131,10 +1136,10 @@ __device__ __forceinline__ double cost_value(const KParams& K, const double* __r
 }
 
 __device__ __forceinline__ void cost_item(const KParams& K, const double* __restrict__ xr, double* __restrict__ f,
-                                          double* __restrict__ Dr) {
+                                          double* __restrict__ Dr, const double* __restrict__ fscale = nullptr) {
   const int N = K.N;
   const double c0 = xr[0], c1 = xr[1], c2 = xr[2];
-  if (K.want_f) *f = cost_value(K, xr);
+  if (K.want_f) *f = fscale ? cost_value(K, xr) * *fscale : cost_value(K, xr);
   if (K.want_grad) {
     Dr[0] = K.W_com * (c0 - K.com_ref[0]);
     Dr[1] = K.W_com * (c1 - K.com_ref[1]);
@@ -1664,7 +1669,7 @@ __device__ __forceinline__ void copy_out_ct(double* __restrict__ dst, const doub
   }
 }
 
-template <int ENVK, int NCW, bool NT>
+template <int ENVK, int NCW, bool NT, bool SC = false>
 __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KParams K, int64_t batch,
                                                                         const double* __restrict__ x,
                                                                         const double* __restrict__ mass,
@@ -1822,7 +1827,7 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
         }
         e -= r_st;
         if (!HAS_SQ && K.lg_active && !K.lg_active[(b0 + e) / K.y_repeat]) continue;
-        cost_item(K, X + e * n, f_out ? f_out + b0 + e : nullptr, Dt + e * n);
+        cost_item(K, X + e * n, f_out ? f_out + b0 + e : nullptr, Dt + e * n, SC ? K.sc_df + b0 + e : nullptr);
       }
       if (HAS_SQ) {
         lds_barrier();
@@ -1840,6 +1845,20 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
       lds_barrier();
     }
     lds_barrier();  // the tile image is complete
+    if (SC) {  // the scaled problem's values (the solve engine's k_apply_scaling, in the tile image)
+      for (int e = tid; e < valid * m; e += CT) {
+        const int r = e / m;
+        Gt[e] = Gt[e] * K.sc_dc[(b0 + r) * m + (e - r * m)];
+      }
+      if (K.want_j)
+        for (int e = tid; e < valid * nnz; e += CT) {
+          const int r = e / nnz;
+          Jt[e] = Jt[e] * K.sc_dc[(b0 + r) * m + K.sc_row[e - r * nnz]];
+        }
+      if (K.want_grad)
+        for (int e = tid; e < valid * n; e += CT) Dt[e] = Dt[e] * K.sc_df[b0 + e / n];
+      lds_barrier();
+    }
     if (K.want_lgrad) {
       // grad f + J^T y per (instance, column), the operation order of cpl_lagrangian_grad (bitwise
       // the same result) without the Jacobian's round trip through HBM; a 0/0 entry counts as 0
@@ -2918,10 +2937,16 @@ struct LGradArgs {
   const uint8_t* active;
 };
 
+struct EvalScale {
+  const double* df;
+  const double* dc;
+  const int32_t* row;
+};
+
 static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
                            const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
                            double* d_norms, hipStream_t stream, bool finish = true,
-                           const LGradArgs* lg = nullptr, int32_t flags = 0) {
+                           const LGradArgs* lg = nullptr, int32_t flags = 0, const EvalScale* sc = nullptr) {
   int32_t st = validate_desc(d);
   if (st) return st;
   if (flags & ~(CPL_EVAL_JAC_FOLDED | CPL_EVAL_SOA)) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown eval flags");
@@ -2954,7 +2979,12 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
   K.col_ptr = K.csc_k = K.csc_row = nullptr;
   K.ly = nullptr;
   K.lg_active = nullptr;
+  K.sc_df = K.sc_dc = nullptr;
+  K.sc_row = nullptr;
   double* ws = nullptr;
+  // (the scaled evaluation: the pipelined path only; the caller scales the others itself)
+  if (sc && (lg || d_norms || K.soa || !use_pipe(K) || use_split(K, flags, batch) || use_entry(K, flags)))
+    return CPL_ERR_UNSUPPORTED;
   if (lg && !use_pipe(K))
     return fail(CPL_ERR_UNSUPPORTED, "fused Lagrangian gradient: pipelined (Ground / no environment) path only");
   if (!lg && use_split(K, flags, batch) && (g_variant != VAR_AUTO || split_ready(stream, batch))) {
@@ -3091,7 +3121,16 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
         {cpl_eval_pipe_kernel<CPL_ENV_GROUND, 3, false>, cpl_eval_pipe_kernel<CPL_ENV_GROUND, 3, true>},
         {cpl_eval_pipe_kernel<CPL_ENV_SUPERQUADRIC, 3, false>, cpl_eval_pipe_kernel<CPL_ENV_SUPERQUADRIC, 3, true>},
         {cpl_eval_pipe_kernel<CPL_ENV_MIXED, 3, false>, cpl_eval_pipe_kernel<CPL_ENV_MIXED, 3, true>}};
-    const KernT kern = table[K.env_kind][g_nt ? 1 : 0];
+    static const KernT table_sc[2][2] = {
+        {cpl_eval_pipe_kernel<CPL_ENV_NONE, 3, false, true>, cpl_eval_pipe_kernel<CPL_ENV_NONE, 3, true, true>},
+        {cpl_eval_pipe_kernel<CPL_ENV_GROUND, 3, false, true>, cpl_eval_pipe_kernel<CPL_ENV_GROUND, 3, true, true>}};
+    if (sc && K.env_kind != CPL_ENV_NONE && K.env_kind != CPL_ENV_GROUND) return CPL_ERR_UNSUPPORTED;
+    if (sc) {
+      K.sc_df = sc->df;
+      K.sc_dc = sc->dc;
+      K.sc_row = sc->row;
+    }
+    const KernT kern = sc ? table_sc[K.env_kind == CPL_ENV_GROUND ? 1 : 0][g_nt ? 1 : 0] : table[K.env_kind][g_nt ? 1 : 0];
     const int64_t ntiles = (batch + K.T - 1) / K.T;
     const int64_t want = resident_blocks(reinterpret_cast<const void*>(kern), lds);
     unsigned grid = (unsigned)(ntiles < want ? ntiles : want);
@@ -3441,6 +3480,17 @@ int32_t ls_backtrack(const cpl_problem_desc* d, const LsBacktrackArgs& a, hipStr
 // per-device residual workspace (RN_GRID partial pairs), allocated once
 static std::mutex g_ws_mutex;
 static double* g_ws[64] = {nullptr};
+
+// (internal, the solve engine) cpl_eval_batch_ex of the NLP-scaled problem: f, grad times df[b], g, J
+// times dc[b, row]; CPL_ERR_UNSUPPORTED (nothing launched) where the evaluation does not take the
+// pipelined kernel — the caller then scales the outputs itself
+int32_t eval_batch_scaled(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
+                          const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
+                          int32_t flags, const double* df, const double* dc, const int32_t* row, void* stream) {
+  const EvalScale sc{df, dc, row};
+  return launch_eval(d, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f, d_grad, nullptr, (hipStream_t)stream, true,
+                     nullptr, flags, &sc);
+}
 
 }  // namespace cpl
 

@@ -39,6 +39,10 @@ int32_t ipm_newton_setup_lm(int64_t batch, int32_t nw, int32_t m, int32_t nf, co
                             double* d_mr_diag, double* d_theta, double* d_phi, const uint8_t* d_active, void* stream);
 // cpl_kernels.hip: the backtracking line search after the first trial, one wave per instance
 int32_t ls_backtrack(const cpl_problem_desc* d, const LsBacktrackArgs& a, hipStream_t stream);
+// cpl_kernels.hip: the NLP-scaled evaluation (pipelined kernel; CPL_ERR_UNSUPPORTED: not that path)
+int32_t eval_batch_scaled(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
+                          const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
+                          int32_t flags, const double* df, const double* dc, const int32_t* row, void* stream);
 bool kkt_wave_size(int nw, int m);
 bool ls_post_prologue(int64_t batch);
 // cpl_ipm.hip: the post-step kernel with the line-search setup (LsSetupArgs) as its tail
@@ -2157,6 +2161,7 @@ struct cpl_solver {
   int32_t* nan_cnt;  // [B] full batch: NaN Jacobian entries at each instance's start point
   uint8_t* sc_any;
   bool scaled = false;
+  bool sc_fused = true;  // the evaluations apply the scaling themselves (until a path says unsupported)
 };
 
 namespace cpl {
@@ -2180,11 +2185,25 @@ int32_t apply_scaling(cpl_solver* S, double* fo, double* grado, double* go, doub
   LAUNCHED("k_apply_scaling");
   return CPL_OK;
 }
+// (scaled: the pipelined evaluation applies the factors in its tile image — one launch fewer per
+// evaluation; other paths evaluate, then k_apply_scaling)
 int32_t eval_fg(cpl_solver* S, const double* X, double* fo, double* go) {
+  if (S->scaled && S->sc_fused) {
+    const int32_t rc = eval_batch_scaled(&S->desc, S->Bcur, X, S->mass, S->tag, go, nullptr, fo, nullptr, 0, S->df,
+                                         S->dc, S->rrow, S->stream);
+    if (rc != CPL_ERR_UNSUPPORTED) return rc;
+    S->sc_fused = false;
+  }
   CK(cpl_eval_batch(&S->desc, S->Bcur, X, S->mass, S->tag, go, nullptr, fo, nullptr, S->stream));
   return apply_scaling(S, fo, nullptr, go, nullptr);
 }
 int32_t eval_full(cpl_solver* S, const double* X, double* fo, double* grado, double* go, double* jo) {
+  if (S->scaled && S->sc_fused) {
+    const int32_t rc = eval_batch_scaled(&S->desc, S->Bcur, X, S->mass, S->tag, go, jo, fo, grado,
+                                         CPL_EVAL_JAC_FOLDED, S->df, S->dc, S->rrow, S->stream);
+    if (rc != CPL_ERR_UNSUPPORTED) return rc;
+    S->sc_fused = false;
+  }
   CK(cpl_eval_batch_ex(&S->desc, S->Bcur, X, S->mass, S->tag, go, jo, fo, grado, nullptr, CPL_EVAL_JAC_FOLDED,
                        S->stream));
   return apply_scaling(S, fo, grado, go, jo);
