@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "cpl_accept.hpp"
+#include "cpl_kkt_qd.hpp"
 #include "cpl_layout.hpp"
 #include "cpl_status.hpp"
 
@@ -1145,25 +1146,72 @@ __device__ __forceinline__ void accept_row_entry(const AcceptRows& a, int64_t b,
 // point (PrepareRestoPhaseStart); an empty restoration filter; a fresh quasi-Newton model; and the
 // least-squares system of the constraint multipliers (W = I, Sigma_p = Sigma_n = 1) for
 // cpl_kkt_qd_solve: r1 = zLR - zUR, r2 = zp - zn, D^-1 = 1/2.
-__global__ __launch_bounds__(256) void k_resto_enter(
-    int64_t B, int m, int nw, const uint8_t* __restrict__ failed, const double* __restrict__ c,
-    const double* __restrict__ w, const double* __restrict__ zL, const double* __restrict__ zU,
-    const double* __restrict__ mu, const double* __restrict__ theta_k, const double* __restrict__ phi_k,
-    const uint8_t* __restrict__ hasL, const uint8_t* __restrict__ hasU, double* __restrict__ filt_t,
-    double* __restrict__ filt_p, int64_t* __restrict__ fcount, int64_t* __restrict__ iters,
-    uint8_t* __restrict__ in_resto, int64_t* __restrict__ n_resto, double* __restrict__ wR, double* __restrict__ pR,
-    double* __restrict__ nR, double* __restrict__ zp, double* __restrict__ zn, double* __restrict__ zLR,
-    double* __restrict__ zUR, double* __restrict__ muR, double* __restrict__ ftR, double* __restrict__ fpR,
-    int64_t* __restrict__ fcR, double* __restrict__ thmaxR, double* __restrict__ thminR,
-    double* __restrict__ th_o0, double* __restrict__ ph_o0, double* __restrict__ dwlR, uint8_t* __restrict__ lm_cnt,
-    uint8_t* __restrict__ lm_skip, double* __restrict__ Hq, int64_t lmc, double* __restrict__ Mw,
-    double* __restrict__ r1, double* __restrict__ r2, double* __restrict__ Dinv, const AcceptRows ar,
-    const IpmAcceptArgs acc, bool with_accept) {
-  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
-  if (b >= B) return;
-  const int lane = threadIdx.x & 63;
-  if (with_accept) {  // (cpl_ipm_accept for this instance first, in the same launch)
-    ipm_accept_one(acc, b, lane);
+struct RestoEnterArgs {
+  int m, nw;
+  const uint8_t* failed;
+  const double *c, *w, *zL, *zU, *mu, *theta_k, *phi_k;
+  const uint8_t *hasL, *hasU;
+  double *filt_t, *filt_p;
+  int64_t *fcount, *iters;
+  uint8_t* in_resto;
+  int64_t* n_resto;
+  double *wR, *pR, *nR, *zp, *zn, *zLR, *zUR, *muR, *ftR, *fpR;
+  int64_t* fcR;
+  double *thmaxR, *thminR, *th_o0, *ph_o0, *dwlR;
+  uint8_t *lm_cnt, *lm_skip;
+  double* Hq;
+  int64_t lmc;
+  double *Mw, *r1, *r2, *Dinv;
+  AcceptRows ar;
+  IpmAcceptArgs acc;
+  bool with_accept;
+};
+// instance b's entry by one wave (lane = its lane)
+__device__ __forceinline__ void resto_enter_one(const RestoEnterArgs& E, int64_t b, int lane) {
+  const int m = E.m, nw = E.nw;
+  const uint8_t* __restrict__ failed = E.failed;
+  const double* __restrict__ c = E.c;
+  const double* __restrict__ w = E.w;
+  const double* __restrict__ zL = E.zL;
+  const double* __restrict__ zU = E.zU;
+  const double* __restrict__ mu = E.mu;
+  const double* __restrict__ theta_k = E.theta_k;
+  const double* __restrict__ phi_k = E.phi_k;
+  const uint8_t* __restrict__ hasL = E.hasL;
+  const uint8_t* __restrict__ hasU = E.hasU;
+  double* __restrict__ filt_t = E.filt_t;
+  double* __restrict__ filt_p = E.filt_p;
+  int64_t* __restrict__ fcount = E.fcount;
+  int64_t* __restrict__ iters = E.iters;
+  uint8_t* __restrict__ in_resto = E.in_resto;
+  int64_t* __restrict__ n_resto = E.n_resto;
+  double* __restrict__ wR = E.wR;
+  double* __restrict__ pR = E.pR;
+  double* __restrict__ nR = E.nR;
+  double* __restrict__ zp = E.zp;
+  double* __restrict__ zn = E.zn;
+  double* __restrict__ zLR = E.zLR;
+  double* __restrict__ zUR = E.zUR;
+  double* __restrict__ muR = E.muR;
+  double* __restrict__ ftR = E.ftR;
+  double* __restrict__ fpR = E.fpR;
+  int64_t* __restrict__ fcR = E.fcR;
+  double* __restrict__ thmaxR = E.thmaxR;
+  double* __restrict__ thminR = E.thminR;
+  double* __restrict__ th_o0 = E.th_o0;
+  double* __restrict__ ph_o0 = E.ph_o0;
+  double* __restrict__ dwlR = E.dwlR;
+  uint8_t* __restrict__ lm_cnt = E.lm_cnt;
+  uint8_t* __restrict__ lm_skip = E.lm_skip;
+  double* __restrict__ Hq = E.Hq;
+  const int64_t lmc = E.lmc;
+  double* __restrict__ Mw = E.Mw;
+  double* __restrict__ r1 = E.r1;
+  double* __restrict__ r2 = E.r2;
+  double* __restrict__ Dinv = E.Dinv;
+  const AcceptRows& ar = E.ar;
+  if (E.with_accept) {  // (cpl_ipm_accept for this instance first, in the same launch)
+    ipm_accept_one(E.acc, b, lane);
     __threadfence_block();  // its filter / count stores before the entry's loads of them
   }
   if (ar.moved && ar.moved[b]) {  // (k_accept_rows for the instances that moved, in the same launch)
@@ -1230,6 +1278,11 @@ __global__ __launch_bounds__(256) void k_resto_enter(
       Hq[b * lmc + 1] = 0.0;
     }
   }
+}
+__global__ __launch_bounds__(256) void k_resto_enter(int64_t B, const RestoEnterArgs E) {
+  const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (b >= B) return;
+  resto_enter_one(E, b, threadIdx.x & 63);
 }
 
 // the least-squares estimate kept when |y|max <= constr_mult_init_max = 1e3
@@ -1763,35 +1816,46 @@ struct TrackBest {  // (small batches) k_track_best's work inside k_count1; best
 };
 __device__ __forceinline__ double orig_violation_wave(int m, const double* __restrict__ gb,
                                                       const double* __restrict__ gl, const double* __restrict__ gu);
-__global__ __launch_bounds__(1024) void k_count1(int64_t B, const uint8_t* __restrict__ active,
-                                                 const uint8_t* __restrict__ in_resto, int32_t* __restrict__ count,
-                                                 int32_t* __restrict__ mail, int m, const uint8_t* __restrict__ failed,
-                                                 const double* __restrict__ dy, double* __restrict__ y,
-                                                 const TrackBest tb) {
-  __shared__ int s_w[16], s_r[16];
-  if (tb.best_w) {  // k_track_best's work, a wave per instance (the same operations)
-    const int lane = threadIdx.x & 63;
-    for (int64_t b = threadIdx.x >> 6; b < B; b += 16) {
-      if (!active[b]) continue;
-      const double v = orig_violation_wave(m, tb.g + b * m, tb.gl, tb.gu);
-      const double fb = tb.f[b];
-      if (!(v <= tb.vtol) || !(fb < tb.best_f[b])) continue;
-      for (int k = lane; k < tb.nw; k += 64) tb.best_w[b * tb.nw + k] = tb.w[b * tb.nw + k];
-      if (lane == 0) tb.best_f[b] = fb;
-    }
+// k_track_best's work for instance b (one wave)
+__device__ __forceinline__ void track_best_one(const TrackBest& tb, const uint8_t* __restrict__ active, int m,
+                                               int64_t b, int lane) {
+  if (!active[b]) return;
+  const double v = orig_violation_wave(m, tb.g + b * m, tb.gl, tb.gu);
+  const double fb = tb.f[b];
+  if (!(v <= tb.vtol) || !(fb < tb.best_f[b])) return;
+  for (int k = lane; k < tb.nw; k += 64) tb.best_w[b * tb.nw + k] = tb.w[b * tb.nw + k];
+  if (lane == 0) tb.best_f[b] = fb;
+}
+// k_resto_y0's work for a failed instance b (one wave)
+__device__ __forceinline__ void resto_y0_one(int m, const double* __restrict__ dy, double* __restrict__ y, int64_t b,
+                                             int lane) {
+  double mx = 0.0;
+  for (int r = lane; r < m; r += 64) mx = fmax(mx, fabs(dy[b * m + r]));
+  mx = wave_max(mx);
+  for (int r = lane; r < m; r += 64) y[b * m + r] = mx <= 1e3 ? dy[b * m + r] : 0.0;
+}
+// the two counts into count[0..1] and, with a mailbox, to the host behind the sequence number
+__device__ __forceinline__ void post_counts(int t, int tr, int32_t* __restrict__ count, int32_t* __restrict__ mail) {
+  count[0] = t;
+  count[1] = tr;
+  if (mail) {
+    const int32_t seq = count[2] + 1;
+    count[2] = seq;
+    volatile int32_t* mb = mail;
+    mb[0] = t;
+    mb[1] = tr;
+    __threadfence_system();
+    mb[2] = seq;
   }
-  if (failed) {  // k_resto_y0's work, a wave per instance (no dependence on the counts below)
-    const int lane = threadIdx.x & 63;
-    for (int64_t b = threadIdx.x >> 6; b < B; b += 16) {
-      if (!failed[b]) continue;
-      double mx = 0.0;
-      for (int r = lane; r < m; r += 64) mx = fmax(mx, fabs(dy[b * m + r]));
-      mx = wave_max(mx);
-      for (int r = lane; r < m; r += 64) y[b * m + r] = mx <= 1e3 ? dy[b * m + r] : 0.0;
-    }
-  }
+}
+// the counts by the NT threads of one workgroup into count[0..1], and the mailbox post
+template <int NT>
+__device__ __forceinline__ void count_post(int64_t B, const uint8_t* __restrict__ active,
+                                           const uint8_t* __restrict__ in_resto, int32_t* __restrict__ count,
+                                           int32_t* __restrict__ mail) {
+  __shared__ int s_w[NT / 64], s_r[NT / 64];
   int c = 0, cr = 0;
-  for (int64_t b = threadIdx.x; b < B; b += 1024) {
+  for (int64_t b = threadIdx.x; b < B; b += NT) {
     c += active[b] ? 1 : 0;
     cr += (active[b] && in_resto[b]) ? 1 : 0;
   }
@@ -1807,20 +1871,75 @@ __global__ __launch_bounds__(1024) void k_count1(int64_t B, const uint8_t* __res
   __syncthreads();
   if (threadIdx.x == 0) {
     int t = 0, tr = 0;
-    for (int q = 0; q < 16; ++q) {
+    for (int q = 0; q < NT / 64; ++q) {
       t += s_w[q];
       tr += s_r[q];
     }
-    count[0] = t;
-    count[1] = tr;
-    if (mail) {
-      const int32_t seq = count[2] + 1;
-      count[2] = seq;
-      volatile int32_t* mb = mail;
-      mb[0] = t;
-      mb[1] = tr;
-      __threadfence_system();
-      mb[2] = seq;
+    post_counts(t, tr, count, mail);
+  }
+}
+__global__ __launch_bounds__(1024) void k_count1(int64_t B, const uint8_t* __restrict__ active,
+                                                 const uint8_t* __restrict__ in_resto, int32_t* __restrict__ count,
+                                                 int32_t* __restrict__ mail, int m, const uint8_t* __restrict__ failed,
+                                                 const double* __restrict__ dy, double* __restrict__ y,
+                                                 const TrackBest tb) {
+  const int lane = threadIdx.x & 63;
+  if (tb.best_w)  // k_track_best's work, a wave per instance (the same operations)
+    for (int64_t b = threadIdx.x >> 6; b < B; b += 16) track_best_one(tb, active, m, b, lane);
+  if (failed)  // k_resto_y0's work, a wave per instance (no dependence on the counts below)
+    for (int64_t b = threadIdx.x >> 6; b < B; b += 16)
+      if (failed[b]) resto_y0_one(m, dy, y, b, lane);
+  count_post<1024>(B, active, in_resto, count, mail);
+}
+
+// The small-batch iteration's tail (B <= FUSE_ROWS: a single-instance Solve(), every solve's
+// compacted tail) in ONE launch instead of three (k_resto_enter, cpl_kkt_qd_kernel, k_count1: ~4.5
+// us each at B = 1, latency only), one workgroup per instance: k_resto_enter's work (the accept,
+// the accepted rows, the restoration entry) by its first wave; for an instance whose search failed
+// the entry's least-squares multipliers by the workgroup (qd_solve_block, cpl_kkt_qd_kernel's
+// solve) and k_resto_y0's estimate; k_count1's best-iterate tracking.  Per instance these are the
+// three launches' operations in their order (bitwise the same state).  The last workgroup to arrive
+// (a 64-bit arrival word at count + 4 that also carries the counts, reset by that workgroup for the
+// next replay) posts the active / restoration counts: k_count1's counting.
+constexpr int TAIL_THREADS = 256;
+struct QdSolveArgs {
+  int nw, m;
+  const double *W, *A, *Dinv, *r1, *r2;
+  double *dwl, *dw, *dy, *delta_w, *Kws;
+};
+__global__ __launch_bounds__(TAIL_THREADS) void k_tail_small(int64_t B, const RestoEnterArgs E, const QdSolveArgs Q,
+                                                             const uint8_t* __restrict__ active,
+                                                             const uint8_t* __restrict__ in_resto,
+                                                             int32_t* __restrict__ count, int32_t* __restrict__ mail,
+                                                             double* __restrict__ y, const TrackBest tb) {
+  extern __shared__ __align__(16) double qd_lds[];
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (tid < 64) resto_enter_one(E, b, lane);
+  __syncthreads();  // (its global stores before the solve's and the tracking's loads of them)
+  const bool fl = E.failed[b] != 0;
+  if (fl) {
+    qd_solve_block<TAIL_THREADS>(b, Q.nw, Q.m, Q.W, Q.A, Q.Dinv, Q.r1, Q.r2, Q.dwl, Q.dw, Q.dy, Q.delta_w, Q.Kws,
+                                 qd_lds);
+    __syncthreads();  // (dy)
+  }
+  if (tid < 64) {
+    if (tb.best_w) track_best_one(tb, active, E.m, b, lane);
+    if (fl) resto_y0_one(E.m, Q.dy, y, b, lane);
+  }
+  // the arrival: ONE 64-bit atomic carries the instance's counts and the arrival itself (bits 0-20
+  // active, 21-41 in the restoration phase, 42- arrivals; B <= FUSE_ROWS), so the last workgroup
+  // reads the totals from its return value — nothing else crosses workgroups, so no device-scope
+  // fences (each an L2 write-back: with them this launch cost as much as the three it replaces)
+  if (tid == 0) {
+    const unsigned long long a = active[b] ? 1ull : 0ull;
+    const unsigned long long r = (a && in_resto[b]) ? 1ull : 0ull;  // (in_resto[b]: this thread's own store)
+    const unsigned long long mine = (1ull << 42) | (r << 21) | a;
+    unsigned long long* acc = reinterpret_cast<unsigned long long*>(count + 4);
+    const unsigned long long tot = atomicAdd(acc, mine) + mine;
+    if ((tot >> 42) == (unsigned long long)B) {
+      atomicExch(acc, 0ull);  // (every workgroup has arrived: reset for the next launch)
+      post_counts((int)(tot & 0x1fffffull), (int)((tot >> 21) & 0x1fffffull), count, mail);
     }
   }
 }
@@ -2525,18 +2644,31 @@ int32_t step_phase(cpl_solver* S, int phase) {
         LAUNCHED("k_accept_rows");
         goto count;
       }
-      // the restoration phase starts where the line search failed
-      hipLaunchKernelGGL(k_resto_enter, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nw, S->failed, S->c, S->w, S->zL,
-                         S->zU, S->mu_o, S->theta_k, S->phi_k, S->hasL, S->hasU, S->filt_t, S->filt_p, S->fcount,
-                         S->iters, S->in_resto, S->n_resto, S->wR, S->pR, S->nR, S->zp, S->zn, S->zLR, S->zUR, S->muR,
-                         S->ftR, S->fpR, S->fcR, S->thmaxR, S->thminR, S->th_o0, S->ph_o0, S->dwlR, S->lm_cnt,
-                         S->lm_skip, S->bfgs ? S->Hq : nullptr, lmc, S->M, S->r1, S->r2, S->Dinv, ar, acc, true);
+      {  // the restoration phase starts where the line search failed
+      RestoEnterArgs E{m, nw, S->failed, S->c, S->w, S->zL, S->zU, S->mu_o, S->theta_k, S->phi_k, S->hasL, S->hasU,
+                       S->filt_t, S->filt_p, S->fcount, S->iters, S->in_resto, S->n_resto, S->wR, S->pR, S->nR, S->zp,
+                       S->zn, S->zLR, S->zUR, S->muR, S->ftR, S->fpR, S->fcR, S->thmaxR, S->thminR, S->th_o0, S->ph_o0,
+                       S->dwlR, S->lm_cnt, S->lm_skip, S->bfgs ? S->Hq : nullptr, lmc, S->M, S->r1, S->r2, S->Dinv, ar,
+                       acc, true};
+      if (B <= FUSE_ROWS && sizeof(double) * qd_lds_doubles(nw, m) <= 160 * 1024) {
+        // the entry, its least-squares multipliers and the counts in one launch (k_tail_small)
+        const QdSolveArgs Q{nw, m, S->M, S->A, S->Dinv, S->r1, S->r2, S->dwlR, S->dw, S->dy, S->scr1, S->Kqd};
+        TrackBest tb{};
+        if (o.fallback_viol_tol > 0.0)
+          tb = TrackBest{nw, o.fallback_viol_tol, S->w, S->f, S->g, S->gl, S->gu, S->best_w, S->best_f};
+        hipLaunchKernelGGL(k_tail_small, dim3((unsigned)B), dim3(TAIL_THREADS), sizeof(double) * qd_lds_doubles(nw, m),
+                           st, B, E, Q, S->active, S->in_resto, S->d_count, S->h_count, S->y, tb);
+        LAUNCHED("k_tail_small (the entry, its multipliers, the counts)");
+        return CPL_OK;
+      }
+      hipLaunchKernelGGL(k_resto_enter, dim3(blocks_for(B)), dim3(256), 0, st, B, E);
       LAUNCHED("k_resto_enter (+ the accept, the accepted rows)");
       CK(cpl_kkt_qd_solve(B, nw, m, S->M, S->A, S->Dinv, S->r1, S->r2, S->failed, S->dwlR, S->dw, S->dy, S->scr1,
                           S->Kqd, st));
       if (B > COUNT1_MAX) {
         hipLaunchKernelGGL(k_resto_y0, dim3(blocks_for(B)), dim3(256), 0, st, B, m, S->failed, S->dy, S->y);
         LAUNCHED("k_resto_y0");
+      }
       }
     count:
       const bool track_fused = o.fallback_viol_tol > 0.0 && B <= TRACK_FUSE_ROWS;
@@ -3101,7 +3233,7 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   S->Xp = a.take<double>(nfd * n); S->gL = a.take<double>(nfd * n); S->hfd = a.take<double>(Bz * nf);
   S->mass_fd = a.take<double>(nfd); S->jac_fd = a.take<double>(nfd * nnz); S->grad_fd = a.take<double>(nfd * n);
   S->tag_fd = a.take<uint8_t>(nfd);
-  S->orig = a.take<int32_t>(Bz); S->pos = a.take<int32_t>(Bz); S->d_count = a.take<int32_t>(4);
+  S->orig = a.take<int32_t>(Bz); S->pos = a.take<int32_t>(Bz); S->d_count = a.take<int32_t>(6);
   S->mass_c = a.take<double>(Bz); S->tag_c = a.take<uint8_t>(Bz);
   S->fw = a.take<double>(Bz * nw); S->fy = a.take<double>(Bz * m); S->fX = a.take<double>(Bz * n);
   S->fdinf = a.take<double>(Bz); S->fstatus = a.take<int64_t>(Bz); S->fiters = a.take<int64_t>(Bz);
@@ -3224,7 +3356,7 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
   // with a stream synchronisation, so nothing is still writing the host side)
   int32_t seq = 0;
   ((volatile int32_t*)S->h_count)[2] = 0;
-  HK(hipMemsetAsync(S->d_count + 2, 0, sizeof(int32_t), st), "hipMemsetAsync seq");
+  HK(hipMemsetAsync(S->d_count + 2, 0, 4 * sizeof(int32_t), st), "hipMemsetAsync seq");  // (+ k_tail_small's arrivals)
   while (it < max_iter) {
     if (S->Bcur <= FUSE_ROWS && S->opt.use_graph) {  // one graph, one host round trip
       CK(run_phase(S, resto_rows > 0 ? P_FUSED_R : P_FUSED));
