@@ -1,12 +1,12 @@
-# round-5 GPU session: the M products of the second-order-correction re-solves with unconditional loads
-# (mfma_matvec_g) against the build before
+# round-5 GPU session: Superquadric batches through the pipelined kernel on four compute waves + the
+# loader (variant 2 = VAR_PIPE) against the tile kernel (variant 0); in-tree = generic row items,
+# build/libcpl_sqpipe_af.so = axis-specialised row items
 set -o pipefail
-O=gpurun_out/r5_g32; mkdir -p $O/ab
-
-for B in 1 64 8192; do
-  for t in A B; do
-    lib=build/libcpl_pre_kkt.so; [ $t = B ] && lib=centroidalplanner_amd/libcpl_mi355x.so
-    CPL_LIB=$lib timeout -k 10 200 python -u scripts/solve_digest.py --batch $B > $O/digest_${t}_B$B.jsonl || exit $?
+O=gpurun_out/r5_g33; mkdir -p $O
+A=centroidalplanner_amd/libcpl_mi355x.so; B=build/libcpl_sqpipe_af.so
+for tun in 0:0:256:1 2:0:256:1; do
+  for cfg in sq8 sq16; do
+    timeout -k 10 300 python -u scripts/ab_libs.py --config $cfg --rounds 5 --reps 10 --libs "$A,$B" --tuning $tun \
+      > $O/${cfg}_$tun.jsonl 2> $O/${cfg}_$tun.err || exit $?
   done
 done
-bash scripts/ab_solve.sh $O/ab build/libcpl_pre_kkt.so centroidalplanner_amd/libcpl_mi355x.so
