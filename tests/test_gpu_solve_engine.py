@@ -44,6 +44,30 @@ def _zero_start(prob):
 
 
 @pytest.mark.gpu
+def test_small_batch_tail_launch_is_bitwise_the_large_batch_tail():
+    """Above 256 rows the iteration's tail (the accept, the restoration entry with its least-squares
+    multipliers, the counts) runs as three launches (k_resto_enter, cpl_kkt_qd_kernel, k_count1); at
+    most 256 rows as one (k_tail_small).  An instance's iterates must not depend on which: TestBasic's
+    superquadric scenario from x = 0 (the restoration phase from the first iteration) in a batch of
+    300 — the three-launch tail until compaction — against the same instances solved alone."""
+    prob, _, _ = _scenario("superquadric")
+    x0 = _zero_start(prob)
+    B = 300
+    mass = np.linspace(80.0, 150.0, B)
+    dev = torch.device("cuda:0")
+    kw = dict(max_iter=600, hessian=_HESSIAN["superquadric"])
+    full = batch_ipm_solve(prob, torch.as_tensor(np.tile(x0, (B, 1)), device=dev), torch.as_tensor(mass, device=dev),
+                           **kw)
+    assert bool((full.restorations.cpu() > 0).all())  # every instance took the entry (on the 3-launch path)
+    for k in (0, 151, 299):
+        one = batch_ipm_solve(prob, torch.as_tensor(x0[None, :], device=dev), torch.as_tensor(mass[k:k + 1], device=dev),
+                              **kw)
+        assert int(one.status[0]) == int(full.status[k]) and int(one.iterations[0]) == int(full.iterations[k])
+        assert int(one.restorations[0]) == int(full.restorations[k])
+        assert torch.equal(one.x[0], full.x[k]) and torch.equal(one.y[0], full.y[k])
+
+
+@pytest.mark.gpu
 def test_restoration_phase_device_matches_host():
     prob, _, _ = _scenario("superquadric")
     x0 = _zero_start(prob)
