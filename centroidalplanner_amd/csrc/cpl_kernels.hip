@@ -1448,7 +1448,13 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
         if (e0 + u * WG < cnt) X[e0 + u * WG] = v[u];
     }
   } else {
+    // Superquadric tiles of 8+ instances (sq8): the copy-in and the copy-out issued at a raised wave
+    // priority, so that a workgroup's memory phases are not queued behind the other resident
+    // workgroups' VALU chains (sq8 0.296 -> 0.288 ms; the 4-instance tiles of 16-contact records lost
+    // 3 % with it, so they keep the default; profiles/r5/sq_prio/)
+    if (ENVK == CPL_ENV_SUPERQUADRIC && T >= 8) __builtin_amdgcn_s_setprio(2);
     copy_in<WG>(X, x + b0 * n, valid * n, tid, K.x_aligned16 != 0);
+    if (ENVK == CPL_ENV_SUPERQUADRIC && T >= 8) __builtin_amdgcn_s_setprio(0);
   }
   {
     int n_sq = ENVK == CPL_ENV_SUPERQUADRIC ? valid : 0;
@@ -1592,6 +1598,7 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
       }
     }
     lds_barrier();
+    if (ENVK == CPL_ENV_SUPERQUADRIC && !LIST && T >= 8) __builtin_amdgcn_s_setprio(2);
     // the residual partials first (from the LDS image), so that their stores are in flight with the
     // copy-out's instead of after them on every workgroup's tail; one partial slot per tile
     if (K.want_norms) {
