@@ -1429,6 +1429,10 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
     // stores (one load per iteration waited an HBM round trip each); element e = (row r, column c)
     // advanced by the workgroup size without a division
     constexpr int U = 8;
+    // (Superquadric list tiles, the mixed split's Superquadric half: the gather and the copy-out at a
+    // raised wave priority, as the contiguous 8-instance tiles below: all-Superquadric 1 048 576 x 16
+    // through the list 3.33 -> 3.21 ms, the 8-GPU shard of configs[3] -1 %, the 50/50 batch unchanged)
+    if (ENVK == CPL_ENV_SUPERQUADRIC) __builtin_amdgcn_s_setprio(2);
     const int cnt = valid * n, dr = WG / n, dc = WG - dr * n;
     int r = tid / n, c = tid - r * n;
     for (int e0 = tid; e0 < cnt; e0 += U * WG) {
@@ -1447,6 +1451,7 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
       for (int u = 0; u < U; ++u)
         if (e0 + u * WG < cnt) X[e0 + u * WG] = v[u];
     }
+    if (ENVK == CPL_ENV_SUPERQUADRIC) __builtin_amdgcn_s_setprio(0);
   } else {
     // Superquadric tiles of 8+ instances (sq8): the copy-in and the copy-out issued at a raised wave
     // priority, so that a workgroup's memory phases are not queued behind the other resident
@@ -1598,7 +1603,7 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
       }
     }
     lds_barrier();
-    if (ENVK == CPL_ENV_SUPERQUADRIC && !LIST && T >= 8) __builtin_amdgcn_s_setprio(2);
+    if (ENVK == CPL_ENV_SUPERQUADRIC && (LIST || T >= 8)) __builtin_amdgcn_s_setprio(2);
     // the residual partials first (from the LDS image), so that their stores are in flight with the
     // copy-out's instead of after them on every workgroup's tail; one partial slot per tile
     if (K.want_norms) {
