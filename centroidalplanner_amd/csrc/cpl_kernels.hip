@@ -1762,6 +1762,9 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
   // The two roles run separate loops with the same barrier sequence per tile, so the compiler's
   // wait-count analysis never sees a pending LDS-DMA on the compute path (no vmcnt drains there).
   if (loader) {
+    // (the loader at a raised wave priority: its few DMA / gather instructions are not queued behind
+    // the compute waves' VALU chains — mixed16 -1.5 %, the rest neutral; profiles/r5/loader_prio/)
+    __builtin_amdgcn_s_setprio(3);
     stage(t, 0);
     finish_stage(t, 0);
     lds_barrier();
@@ -2061,6 +2064,9 @@ __global__ __launch_bounds__(256) void cpl_eval_entry_kernel(const KParams K, in
   __syncthreads();  // (the table)
 
   if (loader) {
+    // (the loader at a raised wave priority: its few DMA / gather instructions are not queued behind
+    // the compute waves' VALU chains — mixed16 -1.5 %, the rest neutral; profiles/r5/loader_prio/)
+    __builtin_amdgcn_s_setprio(3);
     double st_mass = 0.0, st_tail = 0.0;
     long long st_b = 0;
     // (lists) the instances and masses of the tile staged next, loaded one tile ahead: the rows' DMA
