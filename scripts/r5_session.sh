@@ -1,4 +1,13 @@
-# round-5 GPU session: the loader wave of the pipelined and entry kernels at raised priority
+# round-5 GPU session: the split's Ground walker cap re-measured after the priority changes (ablate 256 =
+# every Ground workgroup walking, 512 = two per CU; default one per CU) + the GPU suite
 set -o pipefail
-O=gpurun_out/r5_g41; mkdir -p $O
-bash scripts/ab_eval.sh $O centroidalplanner_amd/libcpl_mi355x.so build/libcpl_ldr.so ground4_1m ground4 ground16 mixed16 none4 || exit $?
+O=gpurun_out/r5_g42; mkdir -p $O
+A=centroidalplanner_amd/libcpl_mi355x.so; B=build/libcpl_same.so
+for tun in 0:0:256:1:0 0:0:256:1:256 0:0:256:1:512; do
+  for spec in "mixed16" "mixed16 --batch 262144"; do
+    tag=$(echo "$tun $spec" | tr ' :' '__')
+    timeout -k 10 300 python -u scripts/ab_libs.py --config $spec --rounds 5 --reps 10 --libs "$A,$B" --tuning $tun \
+      > $O/$tag.jsonl 2> $O/$tag.err || exit $?
+  done
+done
+timeout -k 10 900 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests -m gpu > $O/gpu_tests.log 2>&1
