@@ -62,8 +62,10 @@ out = prob.eval_batch(xt, mt, tt, outputs=("g", "jac", "norms"))
 stream = torch.cuda.current_stream()
 p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
 times = {k: [] for k in libs}
-for _ in range(args.rounds):
-    for k, lib in libs.items():
+# the libraries' order alternates per round: with a fixed order the second library measured ~2-3 %
+# faster on sq8 even when both were the same build (profiles/r5/sq_prio/order/same)
+for rnd in range(args.rounds):
+    for k, lib in (list(libs.items()) if rnd % 2 == 0 else list(libs.items())[::-1]):
         ms = ctypes.c_double()
         _abi.check(lib.cpl_time_eval_batch(ctypes.byref(prob.desc()), B, p(xt), p(mt), p(tt), p(out["g"]), p(out["jac"]),
                                            None, None, None if args.no_norms else p(out["norms"]),

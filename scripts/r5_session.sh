@@ -1,13 +1,8 @@
-# round-5 GPU session: the split's Ground walker cap re-measured after the priority changes (ablate 256 =
-# every Ground workgroup walking, 512 = two per CU; default one per CU) + the GPU suite
+# round-5 GPU session: the priority changes against the tree before them with the library order swapped
+# (ab_libs' second library measured ~3 % faster on sq8 even when both are the same build)
 set -o pipefail
-O=gpurun_out/r5_g42; mkdir -p $O
-A=centroidalplanner_amd/libcpl_mi355x.so; B=build/libcpl_same.so
-for tun in 0:0:256:1:0 0:0:256:1:256 0:0:256:1:512; do
-  for spec in "mixed16" "mixed16 --batch 262144"; do
-    tag=$(echo "$tun $spec" | tr ' :' '__')
-    timeout -k 10 300 python -u scripts/ab_libs.py --config $spec --rounds 5 --reps 10 --libs "$A,$B" --tuning $tun \
-      > $O/$tag.jsonl 2> $O/$tag.err || exit $?
-  done
-done
-timeout -k 10 900 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests -m gpu > $O/gpu_tests.log 2>&1
+O=gpurun_out/r5_g44; mkdir -p $O/ab $O/ba $O/same
+bash scripts/ab_eval.sh $O/ab build/libcpl_pre_prio.so centroidalplanner_amd/libcpl_mi355x.so sq8 sq16 mixed16 "mixed16:--tags all_sq" || exit $?
+bash scripts/ab_eval.sh $O/ba centroidalplanner_amd/libcpl_mi355x.so build/libcpl_pre_prio.so sq8 sq16 mixed16 "mixed16:--tags all_sq" || exit $?
+cp centroidalplanner_amd/libcpl_mi355x.so /tmp/libcpl_copy.so
+bash scripts/ab_eval.sh $O/same centroidalplanner_amd/libcpl_mi355x.so /tmp/libcpl_copy.so sq8 || exit $?
