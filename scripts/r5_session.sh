@@ -1,8 +1,11 @@
-# round-5 GPU session: the priority changes against the tree before them with the library order swapped
-# (ab_libs' second library measured ~3 % faster on sq8 even when both are the same build)
+# round-5 GPU session: the Ground backtracking kernel held to 128 VGPRs (four waves per SIMD) — digests and
+# the solve A/B
 set -o pipefail
-O=gpurun_out/r5_g44; mkdir -p $O/ab $O/ba $O/same
-bash scripts/ab_eval.sh $O/ab build/libcpl_pre_prio.so centroidalplanner_amd/libcpl_mi355x.so sq8 sq16 mixed16 "mixed16:--tags all_sq" || exit $?
-bash scripts/ab_eval.sh $O/ba centroidalplanner_amd/libcpl_mi355x.so build/libcpl_pre_prio.so sq8 sq16 mixed16 "mixed16:--tags all_sq" || exit $?
-cp centroidalplanner_amd/libcpl_mi355x.so /tmp/libcpl_copy.so
-bash scripts/ab_eval.sh $O/same centroidalplanner_amd/libcpl_mi355x.so /tmp/libcpl_copy.so sq8 || exit $?
+O=gpurun_out/r5_g45; mkdir -p $O/ab
+for B in 1 64 8192; do
+  for t in A B; do
+    lib=centroidalplanner_amd/libcpl_mi355x.so; [ $t = B ] && lib=build/libcpl_ls4.so
+    CPL_LIB=$lib timeout -k 10 200 python -u scripts/solve_digest.py --batch $B > $O/digest_${t}_B$B.jsonl || exit $?
+  done
+done
+bash scripts/ab_solve.sh $O/ab centroidalplanner_amd/libcpl_mi355x.so build/libcpl_ls4.so
