@@ -2625,7 +2625,12 @@ static int32_t side_stream(hipStream_t stream, SideStream* out) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
       return fail(CPL_ERR_RUNTIME, "mixed batch: launch once on this stream before capturing it (side stream)");
-    if ((e = hipStreamCreateWithFlags(&ss.side, hipStreamNonBlocking)) != hipSuccess) return hip_fail(e, "hipStreamCreate");
+    // the side stream (the Ground half) at the greatest stream priority: its walkers are dispatched ahead
+    // of the Superquadric tiles queued on the launch stream (1 048 576 x 16 mixed -0.2 %, 262 144 -2 %;
+    // at the least priority +9 %; profiles/r5/side_prio/)
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
+    if ((e = hipStreamCreateWithPriority(&ss.side, hipStreamNonBlocking, hi)) != hipSuccess) return hip_fail(e, "hipStreamCreate");
     if ((e = hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming)) != hipSuccess) return hip_fail(e, "hipEventCreate");
     if ((e = hipEventCreateWithFlags(&ss.join, hipEventDisableTiming)) != hipSuccess) return hip_fail(e, "hipEventCreate");
   }

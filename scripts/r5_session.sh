@@ -1,11 +1,5 @@
-# round-5 GPU session: the Ground backtracking kernel held to 128 VGPRs (four waves per SIMD) — digests and
-# the solve A/B
+# round-5 GPU session: the committed side-stream priority — split / mixed GPU tests and the A/B
 set -o pipefail
-O=gpurun_out/r5_g45; mkdir -p $O/ab
-for B in 1 64 8192; do
-  for t in A B; do
-    lib=centroidalplanner_amd/libcpl_mi355x.so; [ $t = B ] && lib=build/libcpl_ls4.so
-    CPL_LIB=$lib timeout -k 10 200 python -u scripts/solve_digest.py --batch $B > $O/digest_${t}_B$B.jsonl || exit $?
-  done
-done
-bash scripts/ab_solve.sh $O/ab centroidalplanner_amd/libcpl_mi355x.so build/libcpl_ls4.so
+O=gpurun_out/r5_g47; mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests -m gpu -k "mixed or split or entry or graph" > $O/tests.log 2>&1 || exit $?
+bash scripts/ab_eval.sh $O build/libcpl_pre_prio.so centroidalplanner_amd/libcpl_mi355x.so mixed16 "mixed16:--batch 131072" || exit $?
