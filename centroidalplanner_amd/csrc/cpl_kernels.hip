@@ -2625,12 +2625,10 @@ static int32_t side_stream(hipStream_t stream, SideStream* out) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
       return fail(CPL_ERR_RUNTIME, "mixed batch: launch once on this stream before capturing it (side stream)");
-    // the side stream (the Ground half) at the greatest stream priority: its walkers are dispatched ahead
-    // of the Superquadric tiles queued on the launch stream (1 048 576 x 16 mixed -0.2 %, 262 144 -2 %;
-    // at the least priority +9 %; profiles/r5/side_prio/)
-    int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
-    if ((e = hipStreamCreateWithPriority(&ss.side, hipStreamNonBlocking, hi)) != hipSuccess) return hip_fail(e, "hipStreamCreate");
+    // (default priority: at the greatest stream priority the same-process A/B gained 0.2-2 %, but in the
+    // bench's default line, after the north-star loop, the mixed16 side field went 2.54 -> 3.02 ms and
+    // its 8-GPU shard 0.39 -> 0.55 ms; profiles/r5/side_prio/)
+    if ((e = hipStreamCreateWithFlags(&ss.side, hipStreamNonBlocking)) != hipSuccess) return hip_fail(e, "hipStreamCreate");
     if ((e = hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming)) != hipSuccess) return hip_fail(e, "hipEventCreate");
     if ((e = hipEventCreateWithFlags(&ss.join, hipEventDisableTiming)) != hipSuccess) return hip_fail(e, "hipEventCreate");
   }
