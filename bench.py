@@ -521,6 +521,26 @@ def single_instance_latency(prob, cfg, dev, reps=2000):
     return res
 
 
+def eigen_order_field(prob, env, x, mass, tag, got, ref):
+    """The kernels' outputs against the oracle built in the other plausible Eigen reduction order
+    (a0 b0 + (a1 b1 + a2 b2), tests/eigen_order.py): per output class that differs, the largest
+    deviation in ulps (2^-52) of the un-cancelled terms (cone values, cone Jacobian row 1, normal rows)
+    or of the value itself — DESIGN.md section 3's bounds, carried by every bench line."""
+    from eigen_order import order_deviation
+
+    r = order_deviation(prob, env, x, mass, tag, got={"g": got["g"], "jac": got["jac"]})
+    eps = 2.0 ** -52
+    cls = {}
+    worst = 0.0
+    for k, v in r.items():
+        if not isinstance(v, dict) or not v.get("differ"):
+            continue
+        u = v.get("max_rel_uncancelled", v["max_rel"]) / eps
+        cls[k] = {"differ": v["differ"], "entries": v["entries"], "max_ulps": u}
+        worst = max(worst, u)
+    return {"max_ulps_uncancelled": worst, "classes": cls}
+
+
 def checker_leg(prob, env, xt, mt, tt, out, batch, sample):
     """Checker (outside every timed region): a strided sample of the instances whose g / jac the
     timed steps wrote, recomputed by the oracle from the same device inputs and compared with the
@@ -563,6 +583,11 @@ def checker_leg(prob, env, xt, mt, tt, out, batch, sample):
             rep = check_outputs(prob, env, x, got, ref, tag)
             part["ok"] = True
             part["bitwise_frac"] = {k: v["bitwise_frac"] for k, v in rep.items()}
+            # the entries outside the north-star bound read literally (plain relative 1e-10; the policy's
+            # scaled bound is what `ok` asserts) and the largest plain relative error
+            part["outside_plain_1e-10"] = {k: v["plain_rel_hist"]["ge1e-10"] for k, v in rep.items()}
+            part["max_plain_rel_err"] = {k: v["max_plain_rel_err"] for k, v in rep.items()}
+            part["eigen_order"] = eigen_order_field(prob, env, x, mass, tag, got, ref)
         except AssertionError as e:
             part["ok"] = False
             part["error"] = str(e)[:400]
@@ -623,6 +648,16 @@ def side_sq8(dev, stream, valu_counters, check_sample=1024):
     except Exception as e:  # noqa: BLE001
         res["check"] = {"ok": False, "error": f"checker leg failed: {e}"}
     del out, xt, mt
+    try:  # the stress box of tests/test_gpu_parity.py (contacts near the surface, large P terms): every
+        # instance checked, the plain-1e-10 misses counted
+        xs, ms_, _ = generate(cfg.n_contacts, cfg.env, 20000, 99, stress=True)
+        xst, mst = torch.tensor(xs, device=dev), torch.tensor(ms_, device=dev)
+        so = prob.eval_batch(xst, mst, outputs=("g", "jac"))
+        torch.cuda.synchronize()
+        res["stress_box"] = checker_leg(prob, cfg.env, xst, mst, None, so, xs.shape[0], xs.shape[0])
+        del so, xst, mst
+    except Exception as e:  # noqa: BLE001
+        res["stress_box"] = {"ok": False, "error": f"stress-box leg failed: {e}"}
     torch.cuda.empty_cache()
     return res
 
@@ -730,9 +765,22 @@ def run_solve5(dev, batch, hessian, steps, warm, max_ls, max_soc, cpu_sample, ra
             tc, stc, itc = pyoracle.time_solve(prob.desc(), X0[:Bc], mass[:Bc], max_iter=opts["max_iter"],
                                                hessian=hessian)
             okm, okc = int((stm <= 1).sum()), int((stc <= 1).sum())
-            what = (f"the compiled restatement of the same iteration (oracle/cpl_solve_host.c, gcc -O2: IPOPT's method "
+            what = (f"the compiled restatement of the same method (oracle/cpl_solve_host.c, gcc -O2: IPOPT's method "
                     f"with dense QR / Cholesky KKT solves, hessian={hessian}; IPOPT itself is not in the image) over "
-                    f"the oracle's callbacks")
+                    f"the oracle's callbacks; per-instance agreement with the GPU solves in `agreement`")
+            # per instance: the GPU engine's outcome against the compiled restatement's on the same start
+            # points (the two evaluate in different summation orders; DESIGN.md section 5 says where the
+            # trajectories part)
+            import numpy as np
+
+            gst, git = r.status.cpu().numpy()[:Bm], r.iterations.cpu().numpy()[:Bm]
+            dit = np.abs(git.astype(np.int64) - itm.astype(np.int64))
+            agree = {"instances": int(Bm), "status_equal_frac": float((gst == stm).mean()),
+                     "iterations_equal_frac": float((git == itm).mean()),
+                     "iterations_within_2_frac": float((dit <= 2).mean()),
+                     "iterations_absdiff_max": int(dit.max()), "iterations_absdiff_p99": float(np.percentile(dit, 99)),
+                     "gpu_iterations_max": int(git.max()), "cpu_iterations_max": int(itm.max()),
+                     "gpu_iterations_mean": float(git.mean()), "cpu_iterations_mean": float(itm.mean())}
             cpu = {"value": Bm / tm, "unit": "solves/s", "cores": threads, "kind": "port",
                    "sample": f"the first {Bm} of the {batch} instances over {threads} OpenMP threads (each instance "
                              f"solved on one thread) by {what} ({okm}/{Bm} solved, iterations mean "
@@ -740,6 +788,7 @@ def run_solve5(dev, batch, hessian, steps, warm, max_ls, max_soc, cpu_sample, ra
                    "single_core": {"value": Bc / tc, "unit": "solves/s", "cores": 1,
                                    "sample": f"the first {Bc} instances one after another on one core ({okc}/{Bc} "
                                              f"solved, {tc:.2f} s)"},
+                   "agreement": agree,
                    **{k: info[k] for k in ("cpu_model", "affinity", "omp_num_threads")}}
         except Exception as e:  # noqa: BLE001
             cpu = {"error": str(e)}
@@ -800,7 +849,7 @@ def side_single_solve(dev, reps=7):
             tcs.append(tc)
         res["cpu_baseline"] = {"value": statistics.median(tcs) * 1e3, "unit": "ms per solve", "cores": 1, "kind": "port",
                                "sample": f"the same instance, median of {reps}: the compiled restatement of the same "
-                                         f"iteration (oracle/cpl_solve_host.c, gcc -O2, dense QR / Cholesky KKT; "
+                                         f"method (oracle/cpl_solve_host.c, gcc -O2, dense QR / Cholesky KKT; "
                                          f"IPOPT itself is not in the image) over the oracle's callbacks, one core "
                                          f"({int(itc[0])} iterations, status {int(stc[0])})"}
     except Exception as e:  # noqa: BLE001

@@ -261,6 +261,11 @@ def _native(problem, B, **opts):
     return s
 
 
+# (diagnostics) called with the regular iteration's Newton system and step when set
+_DEBUG_NEWTON = None
+_DEBUG_TRIAL = None
+
+
 def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None, tol: float = 1e-8,
                     max_iter: int = 3000, mu_init: float = 0.1, acceptable_tol: float = 1e-6,
                     acceptable_iter: int = 15, max_ls: int = 40, max_soc: int = 4, hessian: str = "exact",
@@ -729,9 +734,12 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     }
 
     def orig_violation(g):
-        """max violation of g against the original constraint bounds (NaN: infinite)."""
+        """max violation of g against the original constraint bounds (NaN: infinite); g is the scaled
+        problem's dc g when the solve is scaled, so the original constraints' values are g / dc."""
         if not m:
             return zeros_B
+        if scaled:
+            g = g / dc
         v = torch.clamp(torch.maximum(gl - g, g - gu), min=0.0).amax(1)
         return torch.where(torch.isnan(g).any(1), torch.full_like(v, float("inf")), v)
 
@@ -865,6 +873,8 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         theta_k = c.abs().sum(1)
         phi_k = cur["f"] + barrier(w, mu)
         dw, dy, delta_w, solve_primal = kkt_host(M, A, r1, r2, mu, S["dwl"], act)
+        if _DEBUG_NEWTON is not None:  # (diagnostics: scripts/solve_divergence.py)
+            _DEBUG_NEWTON(dict(M=M, A=A, r1=r1, r2=r2, dw=dw, dy=dy, w=w, y=y, it=it_run))
         dwl = torch.where(act, delta_w, S["dwl"])
         dzL = torch.where(hasL, mu[:, None] / dl - zL - zL / dl * dw, torch.zeros_like(w))
         dzU = torch.where(hasU, mu[:, None] / du - zU + zU / du * dw, torch.zeros_like(w))
@@ -897,6 +907,9 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
             sel = st["searching"] & ok_
             if extra_mask is not None:
                 sel = sel & extra_mask
+            if _DEBUG_TRIAL is not None:  # (diagnostics)
+                _DEBUG_TRIAL(dict(alpha=al, th=th_, ph=ph_, ok=ok_, sel=sel, soc=extra_mask is not None, a_min=a_min,
+                                  theta_k=theta_k, phi_k=phi_k, gd=gd))
             take(st, sel, wt_, o_, al, h_)
             return ok_, th_
 

@@ -83,6 +83,8 @@ struct KParams {
   int32_t sq_ladder;     // every P_a is an integer in [2, 64]: double-double power ladders
   int32_t grid_cap;      // (entry kernel, the kind split's Ground half) the workgroups that walk the
                          // tiles while the Superquadric list is non-empty (0: every workgroup)
+  int32_t cw_prio;       // (entry kernel) the compute waves' wave priority (s_setprio; 0 = default)
+  int32_t list_prio;     // (tile kernel, LIST) the gather / copy-out at a raised wave priority (1 = yes)
   // fused Lagrangian gradient (cpl_eval_lagrangian_grad): grad f + J^T y of every instance from the
   // LDS tile image, through a CSC index of the fixed structure; instance b takes y[b / y_repeat]
   int32_t want_lgrad, y_repeat;
@@ -885,21 +887,28 @@ __device__ __forceinline__ void copy_out(double* __restrict__ dst, const double*
 }
 
 // Copy-out of a tile image [valid][rec] to the records of instances rowb[r] (rec even: every record
-// and every pair of it is 16-byte aligned), 16-byte stores, lanes along the records
+// and every pair of it is 16-byte aligned), 16-byte stores: one record per wave at a time, lanes along
+// it, so the record's address is wave-uniform (scalar) and each lane adds only its own offset — the
+// flattened (row, pair) walk over the workgroup had cost a 64-bit index product per pair (the list
+// tiles issued ~30 % more VALU instructions than the contiguous ones)
 template <int WG, bool NT>
 __device__ __forceinline__ void copy_out_rows(double* __restrict__ dst, const long long* __restrict__ rowb,
                                               const double* __restrict__ src, int rec, int valid, int tid) {
   const int r2 = rec >> 1;
+  const int wave = tid >> 6, lane = tid & 63;
   const double2* s2 = reinterpret_cast<const double2*>(src);
-  for (int e = tid; e < valid * r2; e += WG) {
-    const int r = e / r2, q = e - r * r2;
-    const double2 v = s2[e];
-    double2* d = reinterpret_cast<double2*>(dst + rowb[r] * rec) + q;
-    if (NT) {
-      __builtin_nontemporal_store(v.x, &d->x);
-      __builtin_nontemporal_store(v.y, &d->y);
-    } else {
-      *d = v;
+  for (int r = wave; r < valid; r += WG / 64) {
+    const int b = __builtin_amdgcn_readfirstlane((int)rowb[r]);
+    double2* d = reinterpret_cast<double2*>(dst + (int64_t)b * rec);
+    const double2* sr = s2 + r * r2;
+    for (int q = lane; q < r2; q += 64) {
+      const double2 v = sr[q];
+      if (NT) {
+        __builtin_nontemporal_store(v.x, &d[q].x);
+        __builtin_nontemporal_store(v.y, &d[q].y);
+      } else {
+        d[q] = v;
+      }
     }
   }
 }
@@ -1376,7 +1385,8 @@ __device__ __forceinline__ void sq_cone_item(const KParams& K, const double* __r
 // VGPRs for Superquadric; a runtime list pointer and a tile loop in the same body had cost 162 VGPRs
 // and a 36-byte spill, three waves per SIMD instead of four).
 template <int ENVK, int WG, bool NT, bool JD, bool LIST = false>
-__global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int64_t batch,
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(LIST && !JD ? 4 : 1)))
+void cpl_eval_tile_kernel(const KParams K, int64_t batch,
                                                             const double* __restrict__ x,
                                                             const double* __restrict__ mass,
                                                             const uint8_t* __restrict__ env_tag,
@@ -1388,10 +1398,6 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
                                                             double* __restrict__ grad_out,
                                                             double* __restrict__ norms_ws) {
   extern __shared__ __align__(16) double smem[];
-  load_ctab(K);
-  __syncthreads();
-  double mass_def = K.mass_default;  // a value (see cpl_eval_pipe_kernel)
-  asm volatile("" : "+v"(mass_def));
   const int tid = threadIdx.x;
   const int T = K.T;
   const int n = K.n, m = K.m, nnz = K.nnz, N = K.N;
@@ -1400,13 +1406,17 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
   // persistent walk over the list's tiles measured slower: 149-155 VGPRs against 114, three waves per
   // SIMD instead of four — profiles/r4/ab_split5; and again in round 5 with the next tile's x
   // prefetched into registers, for the contiguous Superquadric tiles too: 149-165 VGPRs, sq8 0.395
-  // against 0.307 ms, profiles/r5/)
+  // against 0.307 ms, profiles/r5/).  The workgroups past the list's tiles leave before the table load.
   const int64_t b0 = (int64_t)blockIdx.x * T;
   if (LIST && b0 >= count) {  // past the list's tiles: zero partials
     NormAcc nacc;
     if (K.want_norms) partial_norms_waves(nacc, norms_ws + NORM_HDR, blockIdx.x);
     return;
   }
+  load_ctab(K);
+  __syncthreads();
+  double mass_def = K.mass_default;  // a value (see cpl_eval_pipe_kernel)
+  asm volatile("" : "+v"(mass_def));
   const int valid = (int)((count - b0) < T ? (count - b0) : T);
   long long* rowb = reinterpret_cast<long long*>(smem + K.offRB);  // (LIST) instance of each tile row
   auto inst = [&](int r) -> int64_t { return LIST ? (int64_t)rowb[r] : b0 + r; };
@@ -1423,35 +1433,35 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
   constexpr bool HAS_SQ = ENVK == CPL_ENV_SUPERQUADRIC || ENVK == CPL_ENV_MIXED;
 
   if (LIST) {
-    if (tid < valid) rowb[tid] = idx[b0 + tid];
-    __syncthreads();
-    // the tile's rows gathered through the list, eight loads in flight per thread before their LDS
-    // stores (one load per iteration waited an HBM round trip each); element e = (row r, column c)
-    // advanced by the workgroup size without a division
-    constexpr int U = 8;
+    if (tid < valid) rowb[tid] = idx[b0 + tid];  // (published by the barrier before phase 1)
+    // the tile's rows gathered through the list: one row per wave at a time, its source address
+    // wave-uniform (the list entry a scalar load), lanes along the row, every load of a wave's rows
+    // issued before their LDS stores (a flattened (row, column) walk with a 64-bit index product per
+    // element had cost the list tiles ~30 % more VALU instructions than the contiguous copy-in)
     // (Superquadric list tiles, the mixed split's Superquadric half: the gather and the copy-out at a
-    // raised wave priority, as the contiguous 8-instance tiles below: all-Superquadric 1 048 576 x 16
-    // through the list 3.33 -> 3.21 ms, the 8-GPU shard of configs[3] -1 %, the 50/50 batch unchanged)
-    if (ENVK == CPL_ENV_SUPERQUADRIC) __builtin_amdgcn_s_setprio(2);
-    const int cnt = valid * n, dr = WG / n, dc = WG - dr * n;
-    int r = tid / n, c = tid - r * n;
-    for (int e0 = tid; e0 < cnt; e0 += U * WG) {
-      double v[U];
+    // raised wave priority: mixed16 2.35 -> 2.28 ms with the 4-instance LDS-staged tiles, r6)
+    if (ENVK == CPL_ENV_SUPERQUADRIC && K.list_prio) __builtin_amdgcn_s_setprio(2);
+    const int wave = tid >> 6, lane = tid & 63;
+    constexpr int U = 4;  // (rows of up to 4 * 64 doubles in one pass)
+    for (int r = wave; r < valid; r += WG / 64) {
+      const int b = __builtin_amdgcn_readfirstlane(idx[b0 + r]);
+      const double* src = x + (int64_t)b * n;
+      double* dst = X + r * n;
+      for (int c0 = 0; c0 < n; c0 += U * 64) {
+        double v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        v[u] = e0 + u * WG < cnt ? x[rowb[r] * n + c] : 0.0;
-        c += dc;
-        r += dr;
-        if (c >= n) {
-          c -= n;
-          ++r;
+        for (int u = 0; u < U; ++u) {
+          const int c = c0 + u * 64 + lane;
+          v[u] = src[c < n ? c : n - 1];  // (a clamped address: a guarded load is a branch per element)
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int c = c0 + u * 64 + lane;
+          if (c < n) dst[c] = v[u];
         }
       }
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (e0 + u * WG < cnt) X[e0 + u * WG] = v[u];
     }
-    if (ENVK == CPL_ENV_SUPERQUADRIC) __builtin_amdgcn_s_setprio(0);
+    if (ENVK == CPL_ENV_SUPERQUADRIC && K.list_prio) __builtin_amdgcn_s_setprio(0);
   } else {
     // Superquadric tiles of 8+ instances (sq8): the copy-in and the copy-out issued at a raised wave
     // priority, so that a workgroup's memory phases are not queued behind the other resident
@@ -1497,7 +1507,7 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
     // does the kind split's Superquadric half (LIST): beside the Ground half on the other stream the
     // uniform-axis form ran the 1 048 576 x 16 mixed batch 7 % slower (2.74 against 2.55 ms, although
     // an all-Superquadric list alone ran 4 % faster; profiles/r5/ab_uax_list).
-    constexpr bool UAX = ENVK == CPL_ENV_SUPERQUADRIC && !LIST;
+    constexpr bool UAX = ENVK == CPL_ENV_SUPERQUADRIC && !(LIST && JD);
     const int per_axis = UAX ? (N << K.logT) : N * n_sq;
     const int PA = UAX ? ((per_axis + 63) & ~63) : per_axis;
     const int r_ax = (HAS_SQ && wgj) ? 3 * PA : 0;
@@ -1603,7 +1613,7 @@ __global__ __launch_bounds__(WG) void cpl_eval_tile_kernel(const KParams K, int6
       }
     }
     lds_barrier();
-    if (ENVK == CPL_ENV_SUPERQUADRIC && (LIST || T >= 8)) __builtin_amdgcn_s_setprio(2);
+    if (ENVK == CPL_ENV_SUPERQUADRIC && (LIST ? K.list_prio != 0 : T >= 8)) __builtin_amdgcn_s_setprio(2);
     // the residual partials first (from the LDS image), so that their stores are in flight with the
     // copy-out's instead of after them on every workgroup's tail; one partial slot per tile
     if (K.want_norms) {
@@ -2133,6 +2143,8 @@ __global__ __launch_bounds__(256) void cpl_eval_entry_kernel(const KParams K, in
       cur ^= 1;
     }
   } else {
+    if (K.cw_prio == 1) __builtin_amdgcn_s_setprio(1);
+    else if (K.cw_prio == 2) __builtin_amdgcn_s_setprio(2);
     acc.init(tid, CT, m);
     lds_barrier();
     int cur = 0;
@@ -2770,7 +2782,9 @@ static int g_ablate = 0;           // measurement-only: 1 = skip the compute pha
                                    // 16 / 64 / 128 = the split's Ground list at 48 / 36 / 32 KiB
                                    // (default 40), 32 = its Superquadric tiles at 40 KiB (default 48),
                                    // 256 / 512 = every Ground workgroup walking / two per CU
-                                   // (default one per CU while the Superquadric list is non-empty)
+                                   // (default one per CU while the Superquadric list is non-empty),
+                                   // 1024 / 2048 = the Ground half's compute waves at priority 1 / 2,
+                                   // 4096 = the 4-instance Superquadric list tiles at the default priority
 
 static size_t tile_budget() { return g_lds_budget ? g_lds_budget : 48 * 1024; }
 static size_t pipe_budget() { return g_lds_budget ? g_lds_budget : 48 * 1024; }
@@ -3062,6 +3076,10 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
       Kg.grid_cap = (int32_t)((g_ablate & 512) ? 2 * cus : cus);
     }
+    Kg.cw_prio = (g_ablate & 1024) ? 1 : (g_ablate & 2048) ? 2 : 0;
+    // the Superquadric list tiles' gather / copy-out at a raised wave priority (measurement: ablation
+    // 4096 leaves the 4-instance tiles at the default priority)
+    Ks.list_prio = ((g_ablate & 4096) && Ks.T < 8) ? 0 : 1;
     const unsigned grid_g = (unsigned)(ntg < want_g ? ntg : want_g);
     const unsigned grid_s = (unsigned)((batch + Ks.T - 1) / Ks.T);  // every tile the list may hold
     const size_t nparts = (size_t)grid_g + (size_t)grid_s * 4;
@@ -3574,7 +3592,7 @@ int32_t cpl_eval_batch_norms(const cpl_problem_desc* d, int64_t batch, const dou
 
 int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_threads, int32_t nt_stores,
                        int32_t ablate) {
-  if (ablate < 0 || (ablate > 2 && (ablate & ~(4 | 8 | 16 | 32 | 64 | 128 | 256 | 512))))
+  if (ablate < 0 || (ablate > 2 && (ablate & ~(4 | 8 | 16 | 32 | 64 | 128 | 256 | 512 | 1024 | 2048 | 4096))))
     return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
   g_ablate = ablate;
   if (kernel_variant < VAR_AUTO || kernel_variant > VAR_SPLIT_JD) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown kernel variant");

@@ -1813,14 +1813,16 @@ struct TrackBest {  // (small batches) k_track_best's work inside k_count1; best
   double vtol;
   const double *w, *f, *g, *gl, *gu;
   double *best_w, *best_f;
+  const double* dc;  // (scaled solves) the row factors: the violation is the unscaled g's; else NULL
 };
 __device__ __forceinline__ double orig_violation_wave(int m, const double* __restrict__ gb,
-                                                      const double* __restrict__ gl, const double* __restrict__ gu);
+                                                      const double* __restrict__ gl, const double* __restrict__ gu,
+                                                      const double* __restrict__ dcb);
 // k_track_best's work for instance b (one wave)
 __device__ __forceinline__ void track_best_one(const TrackBest& tb, const uint8_t* __restrict__ active, int m,
                                                int64_t b, int lane) {
   if (!active[b]) return;
-  const double v = orig_violation_wave(m, tb.g + b * m, tb.gl, tb.gu);
+  const double v = orig_violation_wave(m, tb.g + b * m, tb.gl, tb.gu, tb.dc ? tb.dc + b * m : nullptr);
   const double fb = tb.f[b];
   if (!(v <= tb.vtol) || !(fb < tb.best_f[b])) return;
   for (int k = lane; k < tb.nw; k += 64) tb.best_w[b * tb.nw + k] = tb.w[b * tb.nw + k];
@@ -2084,12 +2086,15 @@ __global__ void k_iota(int64_t B, int32_t* __restrict__ orig) {
 }
 
 // max violation of the constraint values g_b [m] against their original bounds (NaN: infinite), on
-// one wave
+// one wave.  dcb (scaled solves: the instance's row factors, else NULL): g_b holds the scaled problem's
+// values dc g, so the original constraint's value is g_b / dc (the bounds, 0 or infinite, are the
+// original ones either way) — fallback_viol_tol applies to the original constraints
 __device__ __forceinline__ double orig_violation_wave(int m, const double* __restrict__ gb,
-                                                      const double* __restrict__ gl, const double* __restrict__ gu) {
+                                                      const double* __restrict__ gl, const double* __restrict__ gu,
+                                                      const double* __restrict__ dcb) {
   double v = 0.0;
   for (int r = threadIdx.x & 63; r < m; r += 64) {
-    const double gv = gb[r];
+    const double gv = dcb ? gb[r] / dcb[r] : gb[r];
     v = fmax(v, fmax(fmax(gl[r] - gv, gv - gu[r]), 0.0));
     if (gv != gv) v = INFINITY;
   }
@@ -2104,10 +2109,11 @@ __global__ __launch_bounds__(256) void k_track_best(int64_t B, int m, int nw, do
                                                     const uint8_t* __restrict__ active, const double* __restrict__ w,
                                                     const double* __restrict__ f, const double* __restrict__ g,
                                                     const double* __restrict__ gl, const double* __restrict__ gu,
-                                                    double* __restrict__ best_w, double* __restrict__ best_f) {
+                                                    double* __restrict__ best_w, double* __restrict__ best_f,
+                                                    const double* __restrict__ dc) {
   const int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
   if (b >= B || !active[b]) return;
-  const double v = orig_violation_wave(m, g + b * m, gl, gu);
+  const double v = orig_violation_wave(m, g + b * m, gl, gu, dc ? dc + b * m : nullptr);
   const double fb = f[b];
   if (!(v <= vtol) || !(fb < best_f[b])) return;
   const int lane = threadIdx.x & 63;
@@ -2124,12 +2130,13 @@ __global__ __launch_bounds__(256) void k_fallback(int64_t rows, int m, int nw, d
                                                   const int64_t* __restrict__ status, const double* __restrict__ g,
                                                   const double* __restrict__ gl, const double* __restrict__ gu,
                                                   const double* __restrict__ best_w, const double* __restrict__ best_f,
-                                                  double* __restrict__ w, uint8_t* __restrict__ fbest) {
+                                                  double* __restrict__ w, uint8_t* __restrict__ fbest,
+                                                  const double* __restrict__ dc) {
   const int64_t r = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
   if (r >= rows) return;
   const int32_t o = orig[r];
   if (o < 0 || (finished_only && active[r]) || status[r] <= CPL_SOLVE_ACCEPTABLE) return;
-  const double v = orig_violation_wave(m, g + r * m, gl, gu);
+  const double v = orig_violation_wave(m, g + r * m, gl, gu, dc ? dc + r * m : nullptr);
   if (v <= vtol || !(best_f[r] < INFINITY)) return;
   const int lane = threadIdx.x & 63;
   for (int k = lane; k < nw; k += 64) w[r * nw + k] = best_w[r * nw + k];
@@ -2655,7 +2662,8 @@ int32_t step_phase(cpl_solver* S, int phase) {
         const QdSolveArgs Q{nw, m, S->M, S->A, S->Dinv, S->r1, S->r2, S->dwlR, S->dw, S->dy, S->scr1, S->Kqd};
         TrackBest tb{};
         if (o.fallback_viol_tol > 0.0)
-          tb = TrackBest{nw, o.fallback_viol_tol, S->w, S->f, S->g, S->gl, S->gu, S->best_w, S->best_f};
+          tb = TrackBest{nw, o.fallback_viol_tol, S->w, S->f, S->g, S->gl, S->gu, S->best_w, S->best_f,
+                         S->scaled ? S->dc : nullptr};
         hipLaunchKernelGGL(k_tail_small, dim3((unsigned)B), dim3(TAIL_THREADS), sizeof(double) * qd_lds_doubles(nw, m),
                            st, B, E, Q, S->active, S->in_resto, S->d_count, S->h_count, S->y, tb);
         LAUNCHED("k_tail_small (the entry, its multipliers, the counts)");
@@ -2673,10 +2681,11 @@ int32_t step_phase(cpl_solver* S, int phase) {
     count:
       const bool track_fused = o.fallback_viol_tol > 0.0 && B <= TRACK_FUSE_ROWS;
       TrackBest tb{};
-      if (track_fused) tb = TrackBest{nw, o.fallback_viol_tol, S->w, S->f, S->g, S->gl, S->gu, S->best_w, S->best_f};
+      if (track_fused) tb = TrackBest{nw, o.fallback_viol_tol, S->w, S->f, S->g, S->gl, S->gu, S->best_w, S->best_f,
+                         S->scaled ? S->dc : nullptr};
       if (o.fallback_viol_tol > 0.0 && !track_fused) {
         hipLaunchKernelGGL(k_track_best, dim3(blocks_for(B)), dim3(256), 0, st, B, m, nw, o.fallback_viol_tol,
-                           S->active, S->w, S->f, S->g, S->gl, S->gu, S->best_w, S->best_f);
+                           S->active, S->w, S->f, S->g, S->gl, S->gu, S->best_w, S->best_f, S->scaled ? S->dc : nullptr);
         LAUNCHED("k_track_best");
       }
       if (B > COUNT1_MAX) {
@@ -2871,7 +2880,8 @@ int32_t compact(cpl_solver* S, int64_t count, int64_t Bn) {
   const int n = S->n, m = S->m, nw = S->nw;
   if (S->opt.fallback_viol_tol > 0.0) {
     hipLaunchKernelGGL(k_fallback, dim3(blocks_for(Bc)), dim3(256), 0, st, Bc, m, nw, S->opt.fallback_viol_tol, true,
-                       S->orig, S->active, S->status, S->g, S->gl, S->gu, S->best_w, S->best_f, S->w, S->fbest);
+                       S->orig, S->active, S->status, S->g, S->gl, S->gu, S->best_w, S->best_f, S->w, S->fbest,
+                       S->scaled ? S->dc : nullptr);
     LAUNCHED("k_fallback");
   }
   hipLaunchKernelGGL(k_scatter_final, dim3(blocks_for(Bc)), dim3(256), 0, st, Bc, n, m, nw, true, S->orig, S->active,
@@ -3406,7 +3416,8 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
                        S->fp, S->fc, MU_ROUNDS, S->mu_min, nullptr, S->in_resto, nullptr, st));
   if (S->opt.fallback_viol_tol > 0.0) {
     hipLaunchKernelGGL(k_fallback, dim3(blocks_for(Bc)), dim3(256), 0, st, Bc, m, nw, S->opt.fallback_viol_tol, false,
-                       S->orig, S->active, S->status, S->g, S->gl, S->gu, S->best_w, S->best_f, S->w, S->fbest);
+                       S->orig, S->active, S->status, S->g, S->gl, S->gu, S->best_w, S->best_f, S->w, S->fbest,
+                       S->scaled ? S->dc : nullptr);
     LAUNCHED("k_fallback");
   }
   // every row still in the batch to its instance's place in the full-batch results

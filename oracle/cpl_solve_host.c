@@ -17,6 +17,7 @@
  */
 #include <float.h>
 #include <math.h>
+#include <stdio.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -746,11 +747,13 @@ typedef struct {
   int acceptable_iter, max_ls, max_soc;
 } Opts;
 
+/* the violation of the ORIGINAL constraints: g holds the scaled values dc g on a scaled solve */
 static double orig_violation(const Prob* P, const double* g) {
   double v = 0.0;
   for (int r = 0; r < P->m; ++r) {
-    if (g[r] != g[r]) return INFINITY;
-    v = dmax(v, dmax(dmax(P->gl[r] - g[r], g[r] - P->gu[r]), 0.0));
+    const double gv = P->scaled ? g[r] / P->dc[r] : g[r];
+    if (gv != gv) return INFINITY;
+    v = dmax(v, dmax(dmax(P->gl[r] - gv, gv - P->gu[r]), 0.0));
   }
   return v;
 }
@@ -856,6 +859,7 @@ static void leave_resto(const Prob* P, State* S, const double* w_new) {
 #define WD_TRIGGER 10
 #define WD_TRIAL_MAX 3
 static int g_watchdog = 0;
+static int g_trace = -1;  /* CPLO_TRACE set: one line per regular iteration on stderr */
 void cplo_set_watchdog(int on) { g_watchdog = on != 0; }
 static __thread Eval g_wd_cur;
 /* this thread's watchdog events since the last read: starts, successes, restorations of the kept iterate */
@@ -918,6 +922,16 @@ static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
   double dw[NWMAX], dy[MMAX];
   const double delta_w = kkt_factor(&K, M, E->A, nw, m, mu, S->dwl);
   kkt_solve(&K, r1, r2, dw, dy);
+  if (g_trace && getenv("CPLO_DUMP") && S->iters == atoi(getenv("CPLO_DUMP"))) {  /* (diagnostics) */
+    FILE* fd = fopen("/tmp/cplo_dump.bin", "wb");
+    if (fd) {
+      fwrite(M, sizeof(double), (size_t)nw * nw, fd); fwrite(E->A, sizeof(double), (size_t)m * nw, fd);
+      fwrite(r1, sizeof(double), (size_t)nw, fd); fwrite(r2, sizeof(double), (size_t)m, fd);
+      fwrite(dw, sizeof(double), (size_t)nw, fd); fwrite(dy, sizeof(double), (size_t)m, fd);
+      fwrite(S->w, sizeof(double), (size_t)nw, fd); fwrite(S->y, sizeof(double), (size_t)m, fd);
+      fclose(fd);
+    }
+  }
   double dzL[NWMAX], dzU[NWMAX];
   for (int k = 0; k < nw; ++k) {
     dzL[k] = P->hasL[k] ? mu / dl[k] - S->zL[k] - S->zL[k] / dl[k] * dw[k] : 0.0;
@@ -1003,6 +1017,9 @@ static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
       memcpy(st_w, wt, sizeof(double) * (size_t)nw);
       st_alpha = alpha; aug = h; found = 1; searching = 0;
     }
+    if (g_trace > 1)
+      fprintf(stderr, "      [C] trial %d alpha=%.17g th=%.17g ph=%.17g found=%d th_k=%.17g ph_k=%.17g gd=%.17g a_min=%.17g\n", ls,
+              alpha, th, ph, found, th_ref, ph_ref, gd_ref, a_min);
     if (ls == 0 && max_soc > 0 && searching && th >= theta_k) {  /* second-order corrections */
       double c_soc[MMAX], a_soc = alpha, th_old = th, dws[NWMAX], dys[MMAX], ws[NWMAX], Xs[NMAX];
       memcpy(c_soc, E->c, sizeof(double) * (size_t)m);
@@ -1021,6 +1038,7 @@ static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
         const double ths = sum_abs(cs, m);
         const double phs = tsoc.f + barrier(P, ws, mu);
         const int oks = acceptable(ths, phs, theta_k, phi_k, gd, alpha, switch_ok, S->theta_max, &S->F, 0, &h);
+        if (g_trace > 1) fprintf(stderr, "      [C] soc %d a_soc=%.17g th=%.17g ph=%.17g ok=%d\n", q, a_soc, ths, phs, oks);
         if (oks) {
           memcpy(st_w, ws, sizeof(double) * (size_t)nw);
           st_alpha = alpha; aug = h; found = 1; searching = 0;
@@ -1094,6 +1112,9 @@ static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
     return;
   }
   if (failed) { S->in_soft = 0; S->soft_cnt = 0; }
+  if (g_trace)  /* (diagnostics: batch_ipm.py's verbose line, scripts/solve_divergence.py) */
+    fprintf(stderr, "   [C] mu=%.2e err0=%.2e a_max=%.2e alpha=%.2e dw=%.2e dy=%.2e dW=%.1e f=%.6e d_inf=%.2e c_inf=%.2e resto_next=%d tiny=%d rank_def=%d\n",
+            mu, E->err0, a_max, st_alpha, max_abs(dw, nw), max_abs(dy, m), delta_w, S->cur.f, E->d_inf, E->c_inf, failed, S->tiny_last, K.rank_def);
   const int moved = !failed;
   const double al = st_alpha;
   const double az = soft_ok ? a_soft : a_z_r;
@@ -1354,6 +1375,7 @@ int cplo_solve(const cpl_problem_desc* d, const double* x0, double mass, int max
   static __thread Errors E;
   int32_t n, m, nnz;
   if (cplo_dims(d, &n, &m, &nnz) || n > NMAX || m > MMAX || nnz > 4096) return CPL_ERR_UNSUPPORTED;
+  if (g_trace < 0) g_trace = getenv("CPLO_TRACE") ? atoi(getenv("CPLO_TRACE")) : 0;
   memset(&P, 0, sizeof(P));
   if (exact_hessian && d->env_kind != CPL_ENV_NONE && d->env_kind != CPL_ENV_GROUND) return CPL_ERR_UNSUPPORTED;
   P.d = d; P.n = n; P.m = m; P.nnz = nnz; P.mass = mass; P.exact = exact_hessian != 0;

@@ -139,7 +139,8 @@ def order_deviation(prob, env, x, mass=None, tag=None, got=None):
         jsel = jcls == c
         res["jac_" + c] = stats(a["jac"][:, jsel], b["jac"][:, jsel],
                                 _jac_cone1_scales(prob, x, env).reshape(x.shape[0], -1) if c == "cone1" else None)
-    res["f"] = stats(a["f"], b["f"])
+    if "f" in a:  # (a caller's outputs may carry g and the Jacobian only)
+        res["f"] = stats(a["f"], b["f"])
     res["instances"] = int(x.shape[0])
     res["contacts"] = N
     return res

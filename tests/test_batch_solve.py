@@ -121,10 +121,16 @@ def test_batch_solve_oracle_cpu():
         assert f == pytest.approx(float(r.objective[b]), rel=1e-12)
         if b < 3:
             # the problem is nonconvex (bilinear torque balance): both points are certified local
-            # optima, neighbouring ones at most 1 % apart (with IPOPT's gradient-based scaling the
-            # interior-point path of instance 2 ends in the neighbouring optimum 0.5 % above SLSQP's;
-            # unscaled it had reached SLSQP's or a better one)
-            assert f <= _slsqp_objective(prob, X0[b], mass[b]) * (1.0 + 1e-2)
+            # optima.  Instances 0 and 1 reach SLSQP's optimum or a better one (0: 2.2 % below, 1: equal);
+            # with IPOPT's gradient-based scaling the interior-point path of instance 2 ends in the
+            # neighbouring optimum 0.53 % above SLSQP's (unscaled it had reached SLSQP's), pinned here
+            # on its own so that a regression of 0 or 1 cannot hide under its tolerance
+            ref = _slsqp_objective(prob, X0[b], mass[b])
+            if b < 2:
+                assert f <= ref * (1.0 + 1e-7)
+            else:
+                assert f == pytest.approx(188518.53629546892, rel=1e-8)
+                assert f <= ref * (1.0 + 6e-3)
 
 
 def test_batch_solve_rejects_host_inputs_without_gpu_callbacks():
@@ -413,8 +419,8 @@ def test_split_small_batch_iterations_are_exact(max_ls, max_soc, hessian):
     for k in ("x", "y", "status", "iterations", "objective"):
         assert torch.equal(getattr(a, k), getattr(b, k)), k
     if max_ls == 1:  # one trial per iteration, no backtracking (a stress setting, not IPOPT's): on the scaled
-        # problem (nlp_scaling, round 5) one instance of the 32 cycles to the iteration limit
-        assert float((a.status <= STATUS_ACCEPTABLE).double().mean()) >= 0.9
+        # problem (nlp_scaling, round 5) one instance of the 32 cycles to the iteration limit: at most that one
+        assert int((a.status > STATUS_ACCEPTABLE).sum()) <= 1
     else:
         assert bool((a.status <= STATUS_ACCEPTABLE).all())
 
