@@ -264,6 +264,7 @@ def _native(problem, B, **opts):
 # (diagnostics) called with the regular iteration's Newton system and step when set
 _DEBUG_NEWTON = None
 _DEBUG_TRIAL = None
+_DEBUG_EVENT = None
 
 
 def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None, tol: float = 1e-8,
@@ -855,6 +856,9 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
             upd = act & ((err_mu(E, mu) <= BARRIER_TOL_FACTOR * mu) | (force if r == 0 else False)) & (mu > mu_min)
             mu = torch.where(upd, torch.clamp(torch.minimum(0.2 * mu, mu ** 1.5), min=mu_min), mu)
             ft, fp, fc = reset_filter(upd, ft, fp, fc)
+            # IPOPT's BacktrackingLineSearch::Reset (MonotoneMuUpdate calls it when mu changes): the
+            # filter reset above and the end of the soft restoration phase
+            S["in_soft"].copy_(S["in_soft"] & ~upd)
         tau = torch.clamp(1.0 - mu, min=0.99)
 
         def primal_step(d):  # fraction to the boundary along d from w
@@ -1103,6 +1107,8 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         # a failed restoration phase with a backup acceptable point: IPOPT restores that point and stops
         # there (BacktrackingLineSearch: RestoreAcceptablePoint, STOP_AT_ACCEPTABLE_POINT)
         back_acc = stop & feas & S["has_acc"]
+        if _DEBUG_EVENT is not None and bool(back_acc.any()):  # (diagnostics / tests)
+            _DEBUG_EVENT("restore_acceptable_point", back_acc.clone())
         for k, kk in (("w", "acc_w"), ("y", "acc_y"), ("zL", "acc_zL"), ("zU", "acc_zU")):
             S[k].copy_(torch.where(back_acc[:, None], S[kk], S[k]))
         S["status"].copy_(torch.where(back_acc, STATUS_ACCEPTABLE, torch.where(stop & feas, STATUS_RESTO_FAILED,

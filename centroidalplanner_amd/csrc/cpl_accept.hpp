@@ -368,6 +368,9 @@ struct IpmUnpack {
   double* acc_zU;
   uint8_t* has_acc;
   uint8_t* any_reset;  // (the solve loop's fused search) flags to clear, or NULL
+  // IPOPT's BacktrackingLineSearch::Reset on a barrier change (MonotoneMuUpdate): the soft restoration
+  // phase ends (in_soft cleared where mu changed; NULL: not kept)
+  uint8_t* in_soft;
 };
 
 // one entry e of A = dc/dw = [J_free | -P] (batch-major [B][m][nw]) from the CSR Jacobian values:

@@ -235,6 +235,7 @@ __global__ __launch_bounds__(256) void cpl_ipm_optimality_kernel(
     base_out[b] = base;
     mu_out[b] = mu;
     fcount_out[b] = reset ? 0 : fcount[b];
+    if (reset && up.in_soft) up.in_soft[b] = 0;  // (the line search's Reset: the soft restoration phase ends)
   }
   unpack(mu, act);
 }

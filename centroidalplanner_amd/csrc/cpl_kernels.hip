@@ -1384,6 +1384,10 @@ __device__ __forceinline__ void sq_cone_item(const KParams& K, const double* __r
 // residual partials.  Without LIST the kernel is the contiguous one-tile-per-workgroup form (111
 // VGPRs for Superquadric; a runtime list pointer and a tile loop in the same body had cost 162 VGPRs
 // and a 36-byte spill, three waves per SIMD instead of four).
+// The LDS-staged list tiles (the split's default Superquadric half) are held to four waves per SIMD:
+// uncapped they took 129 VGPRs — two past the four-wave step — and ran three workgroups per CU where the
+// contiguous tiles run four (127 with 2 spilled: the all-Superquadric 524 288 x 16 list 1.93 -> 1.53 ms,
+// the 8-GPU shard of configs[3] 0.355 -> 0.317 ms, 1 048 576 x 16 50 / 50 +1.6 %; profiles/r6/split/)
 template <int ENVK, int WG, bool NT, bool JD, bool LIST = false>
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(LIST && !JD ? 4 : 1)))
 void cpl_eval_tile_kernel(const KParams K, int64_t batch,
@@ -2889,9 +2893,11 @@ static bool use_entry(const KParams& K, int32_t flags) {
   const bool want = g_variant == VAR_ENTRY || g_variant == VAR_SPLIT || (g_variant == VAR_AUTO && K.N >= 12);
   return want && flags == 0 && (K.nnz % 2) == 0 && (K.env_kind == CPL_ENV_NONE || K.env_kind == CPL_ENV_GROUND);
 }
-// mixed batches split by kind: forced (variants 6, 7) or by default (as variant 7, the Superquadric half
-// writing its Jacobian rows straight to the records, both halves on 48 KiB tiles: 1 048 576 x 16 in
-// 2.64 ms against 3.28 with LDS-staged rows and 4.49 ms interleaved, same process, profiles/r4)
+// mixed batches split by kind: forced (variants 6, 7) or by default (as variant 6 since round 6: the
+// Superquadric half on LDS-staged uniform-axis list tiles — the contiguous kernel's code with the rows
+// gathered through the list —, 1 048 576 x 16 in 2.21-2.41 ms against 2.47-2.62 for variant 7, whose
+// Jacobian rows are written straight to the records; round 4: variant 7 2.64 ms against 3.28 for the
+// then LDS-staged rows and 4.49 ms interleaved; profiles/r6/split/)
 static bool use_split(const KParams& K, int32_t flags, int64_t batch) {
   return (g_variant == VAR_SPLIT || g_variant == VAR_SPLIT_JD || g_variant == VAR_AUTO) && flags == 0 &&
          K.env_kind == CPL_ENV_MIXED && batch <= 0x7fffffffLL;
@@ -3038,7 +3044,7 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
     if ((st = plan_entry(Kg, d_g != nullptr, d_jac != nullptr, d_f != nullptr, d_grad != nullptr, true,
                          list_kb * 1024)))
       return st;
-    Ks.jdirect = ((g_variant == VAR_SPLIT_JD || g_variant == VAR_AUTO) && d_jac) ? 1 : 0;
+    Ks.jdirect = (g_variant == VAR_SPLIT_JD && d_jac) ? 1 : 0;
     // (measurement: ablation 32 = the Superquadric tiles at 40 KiB instead of 48 — within the noise beside
     // the capped Ground walkers below: 2.603 / 2.552 against 2.540 / 2.579 ms in two runs,
     // profiles/r4/split_grid)

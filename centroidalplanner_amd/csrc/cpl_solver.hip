@@ -2493,7 +2493,8 @@ int32_t step_phase(cpl_solver* S, int phase) {
       const bool fused_ls = fused && S->ls_fusable;
       const bool post_in_ls = fused_ls && ls_post_prologue(B);  // (the search kernel's prologue)
       const IpmUnpack unp{n, S->freepos, S->Xbase, S->in_resto, S->X, S->tau, S->act,
-                          S->acc_w, S->acc_y, S->acc_zL, S->acc_zU, S->has_acc, post_in_ls ? S->d_any : nullptr};
+                          S->acc_w, S->acc_y, S->acc_zL, S->acc_zU, S->has_acc, post_in_ls ? S->d_any : nullptr,
+                          S->in_soft};
       CK(ipm_optimality_ex(B, nw, m, FMAX, S->nbounds, o.tol, o.acceptable_tol, o.acceptable_iter, S->A, S->gradw,
                            S->c, S->w, S->y, S->zL, S->zU, S->hasL, S->hasU, S->wl0, S->wu0, S->mu, S->filt_t,
                            S->filt_p, S->fcount, S->active, S->status, S->acc, S->d_inf, S->err0, S->base, S->mu_o,

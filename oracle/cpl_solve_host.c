@@ -887,6 +887,7 @@ static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
     if (((err_mu(P, E, mu) <= BARRIER_TOL_FACTOR * mu) || (r == 0 && force)) && mu > o->mu_min) {
       mu = dmax(dmin(0.2 * mu, pow(mu, 1.5)), o->mu_min);
       filter_reset(&S->F);
+      S->in_soft = 0;  /* BacktrackingLineSearch::Reset (MonotoneMuUpdate): the soft restoration phase ends */
       S->in_wd = 0;  /* (the line search's Reset: the watchdog ends, its count restarts) */
       S->wd_cnt = 0;
     }
