@@ -1412,6 +1412,17 @@ void cpl_eval_tile_kernel(const KParams K, int64_t batch,
   // prefetched into registers, for the contiguous Superquadric tiles too: 149-165 VGPRs, sq8 0.395
   // against 0.307 ms, profiles/r5/).  The workgroups past the list's tiles leave before the table load.
   const int64_t b0 = (int64_t)blockIdx.x * T;
+  // (LIST) the tile's list entries loaded before the list's length is known — the workspace holds
+  // `batch` entries, so b0 + r < batch is in bounds (entries past the length are never used): the
+  // length, then the entries, then the rows had been three dependent HBM round trips before any
+  // compute (~10 % of a list tile's life; the contiguous tiles pay one)
+  const int wave0 = tid >> 6;
+  int spec_b = 0;
+  long long spec_rb = 0;
+  if (LIST) {
+    if (b0 + wave0 < batch) spec_b = idx[b0 + wave0];
+    if (tid < T && b0 + tid < batch) spec_rb = idx[b0 + tid];
+  }
   if (LIST && b0 >= count) {  // past the list's tiles: zero partials
     NormAcc nacc;
     if (K.want_norms) partial_norms_waves(nacc, norms_ws + NORM_HDR, blockIdx.x);
@@ -1437,7 +1448,7 @@ void cpl_eval_tile_kernel(const KParams K, int64_t batch,
   constexpr bool HAS_SQ = ENVK == CPL_ENV_SUPERQUADRIC || ENVK == CPL_ENV_MIXED;
 
   if (LIST) {
-    if (tid < valid) rowb[tid] = idx[b0 + tid];  // (published by the barrier before phase 1)
+    if (tid < valid) rowb[tid] = spec_rb;  // (published by the barrier before phase 1)
     // the tile's rows gathered through the list: one row per wave at a time, its source address
     // wave-uniform (the list entry a scalar load), lanes along the row, every load of a wave's rows
     // issued before their LDS stores (a flattened (row, column) walk with a 64-bit index product per
@@ -1447,8 +1458,10 @@ void cpl_eval_tile_kernel(const KParams K, int64_t batch,
     if (ENVK == CPL_ENV_SUPERQUADRIC && K.list_prio) __builtin_amdgcn_s_setprio(2);
     const int wave = tid >> 6, lane = tid & 63;
     constexpr int U = 4;  // (rows of up to 4 * 64 doubles in one pass)
+    int bnext = spec_b;  // (row `wave`'s entry, loaded at the kernel's start)
     for (int r = wave; r < valid; r += WG / 64) {
-      const int b = __builtin_amdgcn_readfirstlane(idx[b0 + r]);
+      const int b = __builtin_amdgcn_readfirstlane(bnext);
+      if (r + WG / 64 < valid) bnext = idx[b0 + r + WG / 64];
       const double* src = x + (int64_t)b * n;
       double* dst = X + r * n;
       for (int c0 = 0; c0 < n; c0 += U * 64) {
@@ -1570,7 +1583,9 @@ void cpl_eval_tile_kernel(const KParams K, int64_t batch,
     }
     // LDS-only barriers from here on: the phases exchange LDS data only, and a __syncthreads would
     // first wait for every global store the items issued (f, and with jdirect the Jacobian rows)
-    if (compute && HAS_SQ && n_sq > 0 && wgj) lds_barrier();
+    // (measurement only, ablation 8192: the phases' barriers skipped — wrong outputs, the barriers' cost)
+    const bool phase_bar = (K.ablate & 8192) == 0;
+    if (compute && HAS_SQ && n_sq > 0 && wgj && phase_bar) lds_barrier();
     if (compute) {
       const int r_rows = r_ax;
       // Superquadric batches: the friction cones as items of their own in phase 2 (the workgroup's
@@ -1616,7 +1631,7 @@ void cpl_eval_tile_kernel(const KParams K, int64_t batch,
         for (int r = 0; r < valid; ++r) statics_rows_coop(K, X + r * n, com6 + 6 * r, JR(r), tid, WG);
       }
     }
-    lds_barrier();
+    if (phase_bar) lds_barrier();
     if (ENVK == CPL_ENV_SUPERQUADRIC && (LIST ? K.list_prio != 0 : T >= 8)) __builtin_amdgcn_s_setprio(2);
     // the residual partials first (from the LDS image), so that their stores are in flight with the
     // copy-out's instead of after them on every workgroup's tail; one partial slot per tile
@@ -2788,7 +2803,8 @@ static int g_ablate = 0;           // measurement-only: 1 = skip the compute pha
                                    // 256 / 512 = every Ground workgroup walking / two per CU
                                    // (default one per CU while the Superquadric list is non-empty),
                                    // 1024 / 2048 = the Ground half's compute waves at priority 1 / 2,
-                                   // 4096 = the 4-instance Superquadric list tiles at the default priority
+                                   // 4096 = the 4-instance Superquadric list tiles at the default priority,
+                                   // 8192 = the tile kernel's phase barriers skipped (wrong outputs)
 
 static size_t tile_budget() { return g_lds_budget ? g_lds_budget : 48 * 1024; }
 static size_t pipe_budget() { return g_lds_budget ? g_lds_budget : 48 * 1024; }
@@ -3598,7 +3614,7 @@ int32_t cpl_eval_batch_norms(const cpl_problem_desc* d, int64_t batch, const dou
 
 int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_threads, int32_t nt_stores,
                        int32_t ablate) {
-  if (ablate < 0 || (ablate > 2 && (ablate & ~(4 | 8 | 16 | 32 | 64 | 128 | 256 | 512 | 1024 | 2048 | 4096))))
+  if (ablate < 0 || (ablate > 2 && (ablate & ~(4 | 8 | 16 | 32 | 64 | 128 | 256 | 512 | 1024 | 2048 | 4096 | 8192))))
     return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
   g_ablate = ablate;
   if (kernel_variant < VAR_AUTO || kernel_variant > VAR_SPLIT_JD) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown kernel variant");

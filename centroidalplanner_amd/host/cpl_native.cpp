@@ -38,6 +38,7 @@ BatchSolver::BatchSolver(CplProblem::Ptr problem, int64_t batch, const SolveOpti
     hip_check(hipMalloc(&_dpinf, 8 * B), "hipMalloc");
     hip_check(hipMalloc(&_dstatus, 4 * B), "hipMalloc");
     hip_check(hipMalloc(&_diters, 4 * B), "hipMalloc");
+    hip_check(hipMalloc(&_dnan, 4 * B), "hipMalloc");
   } catch (...) {
     release();  // (the destructor does not run for a constructor that throws)
     throw;
@@ -48,10 +49,10 @@ BatchSolver::~BatchSolver() { release(); }
 
 void BatchSolver::release() {
   for (void* p : {(void*)_dx0, (void*)_dmass, (void*)_dx, (void*)_dy, (void*)_dobj, (void*)_dpinf, (void*)_dstatus,
-                  (void*)_diters})
+                  (void*)_diters, (void*)_dnan})
     if (p) (void)hipFree(p);
   _dx0 = _dmass = _dx = _dy = _dobj = _dpinf = nullptr;
-  _dstatus = _diters = nullptr;
+  _dstatus = _diters = _dnan = nullptr;
   if (_stream) (void)hipStreamDestroy((hipStream_t)_stream);
   _stream = nullptr;
   if (_solver) cpl_solver_destroy(_solver);
@@ -81,14 +82,13 @@ void BatchSolver::Solve(const double* x0, const double* mass, double* x, double*
 }
 
 void BatchSolver::NanJacobian(int32_t* counts) const {
+  // (into the buffer allocated with the solver's others: a hipMalloc / hipFree per Solve() sat on the
+  // single-instance latency path, and hipFree can synchronise the device)
   const size_t B = (size_t)_batch;
-  int32_t* d = nullptr;
-  hip_check(hipMalloc(&d, 4 * B), "hipMalloc");
   const hipStream_t s = (hipStream_t)_stream;
-  const int32_t st = cpl_solver_nan_jacobian(_solver, d, s);
-  hipError_t e = st == CPL_OK ? hipMemcpyAsync(counts, d, 4 * B, hipMemcpyDeviceToHost, s) : hipSuccess;
+  const int32_t st = cpl_solver_nan_jacobian(_solver, _dnan, s);
+  hipError_t e = st == CPL_OK ? hipMemcpyAsync(counts, _dnan, 4 * B, hipMemcpyDeviceToHost, s) : hipSuccess;
   if (e == hipSuccess && st == CPL_OK) e = hipStreamSynchronize(s);
-  (void)hipFree(d);
   engine_check(st);
   hip_check(e, "hipMemcpyAsync nan_jacobian");
 }

@@ -72,6 +72,7 @@ class BatchSolver {
   void* _stream = nullptr;
   double *_dx0 = nullptr, *_dmass = nullptr, *_dx = nullptr, *_dy = nullptr, *_dobj = nullptr, *_dpinf = nullptr;
   int32_t *_dstatus = nullptr, *_diters = nullptr;
+  int32_t* _dnan = nullptr;  // [batch] NaN Jacobian counts (NanJacobian), allocated with the others
   int32_t _iterations_run = 0;
 };
 

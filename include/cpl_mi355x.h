@@ -545,7 +545,9 @@ int32_t cpl_solver_destroy(cpl_solver* s);
  * d_env_tag for mixed batches) on `stream`; returns when every instance has stopped.  Outputs
  * (device, any may be NULL): d_x [batch, n] (projected onto the original bounds, IPOPT
  * honor_original_bounds), d_y [batch, m] constraint multipliers, d_status (CPL_SOLVE_*), d_iters
- * (iterations per instance), d_obj (f at d_x), d_primal_inf (max violation at d_x), d_dual_inf.
+ * (iterations per instance), d_obj (f at d_x), d_primal_inf (max violation at d_x), d_dual_inf (the
+ * last iterate's dual infeasibility OF THE SCALED PROBLEM when nlp_scaling is on — IPOPT's scaled
+ * quantity; d_y is returned unscaled, dc y / df).
  * *iterations_run (host, may be NULL): lock-step iterations of the batch; *evaluations: eval launches. */
 int32_t cpl_solver_solve(cpl_solver* s, const double* d_x0, const double* d_mass, const uint8_t* d_env_tag,
                          double* d_x, double* d_y, int32_t* d_status, int32_t* d_iters, double* d_obj,
