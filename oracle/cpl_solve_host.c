@@ -326,7 +326,17 @@ typedef struct {
   double Mw[NWMAX * NWMAX];
   double A[MMAX * NWMAX];
   int rank_def;
+  int aug, nw0;  /* (g_jac_reg) the regularised system of a rank-deficient A, in nw0 + m unknowns */
 } Kkt;
+
+/* IPOPT's regularisation of a rank-deficient Jacobian (PDPerturbationHandler: delta_c =
+ * jacobian_regularization_value 1e-8 * mu^jacobian_regularization_exponent 0.25 on the (2,2) block):
+ * [[W + dW I, A^T], [A, -delta_c I]] — solved by the same null-space method as the augmented system in
+ * (dw, s): W~ = diag(W, I), A~ = [A, -sqrt(delta_c) I] (full row rank), whose KKT conditions are exactly
+ * the regularised system's (s = sqrt(delta_c) dy).  Opt-in (cplo_set_jac_reg): the default keeps the
+ * engine's treatment (delta_c added to R's near-zero pivots). */
+static int g_jac_reg = 0;
+void cplo_set_jac_reg(int on) { g_jac_reg = on != 0; }
 
 /* Householder QR of At (nw x m): Q (nw x nw) and R (m x m) */
 static void householder_qr(const double* At, int nw, int m, double* Q, double* R) {
@@ -367,7 +377,8 @@ static void householder_qr(const double* At, int nw, int m, double* Q, double* R
 /* factorise: QR of A^T, delta_c on R's small diagonal, the reduced Hessian with the inertia test */
 static double kkt_factor(Kkt* k, const double* M, const double* A, int nw, int m, double mu, double dwl) {
   static __thread double At[NWMAX * MMAX];
-  k->nw = nw; k->m = m; k->nz = nw - m;
+  static __thread double Ma[NWMAX * NWMAX];
+  k->nw = nw; k->m = m; k->nz = nw - m; k->aug = 0; k->nw0 = nw;
   memcpy(k->A, A, sizeof(double) * (size_t)m * nw);
   for (int i = 0; i < nw; ++i)
     for (int j = 0; j < m; ++j) At[i * m + j] = A[j * nw + i];
@@ -380,18 +391,33 @@ static double kkt_factor(Kkt* k, const double* M, const double* A, int nw, int m
     double* rd = &k->R[i * m + i];
     if (!(fabs(*rd) >= 1e-10 * rmax) || rmax == 0.0) {
       k->rank_def = 1;
-      *rd += *rd < 0.0 ? -dc : dc;
+      if (!g_jac_reg) *rd += *rd < 0.0 ? -dc : dc;
     }
+  }
+  const double* Mr = M;
+  if (k->rank_def && g_jac_reg && nw + m <= NWMAX) {  /* the regularised system as the augmented one */
+    const int na = nw + m;
+    const double sdc = sqrt(1e-8 * pow(mu, 0.25));
+    for (int i = 0; i < na; ++i)
+      for (int j = 0; j < m; ++j) At[i * m + j] = i < nw ? A[j * nw + i] : (i - nw == j ? -sdc : 0.0);
+    householder_qr(At, na, m, k->Q, k->R);
+    for (int r = 0; r < m; ++r)
+      for (int j = 0; j < na; ++j) k->A[r * na + j] = j < nw ? A[r * nw + j] : (j - nw == r ? -sdc : 0.0);
+    for (int i = 0; i < na; ++i)
+      for (int j = 0; j < na; ++j) Ma[i * na + j] = (i < nw && j < nw) ? M[i * nw + j] : (i == j ? 1.0 : 0.0);
+    k->aug = 1; k->rank_def = 0;
+    nw = na; k->nw = na; k->nz = na - m;
+    Mr = Ma;
   }
   const int nz = k->nz;
   double dmx = 0.0;
-  for (int i = 0; i < nw; ++i) dmx = dmax(dmx, fabs(M[i * nw + i]));
+  for (int i = 0; i < nw; ++i) dmx = dmax(dmx, fabs(Mr[i * nw + i]));
   /* Hr = Z^T M Z, symmetrised */
-  static __thread double MZ[NWMAX * NWMAX], Hr[NWMAX * NWMAX];
+  static __thread double MZ[NWMAX * NWMAX], Hr[NWMAX * NWMAX], Pz[NWMAX * NWMAX];
   for (int i = 0; i < nw; ++i)
     for (int c = 0; c < nz; ++c) {
       double s = 0.0;
-      for (int t = 0; t < nw; ++t) s += M[i * nw + t] * k->Q[t * nw + m + c];
+      for (int t = 0; t < nw; ++t) s += Mr[i * nw + t] * k->Q[t * nw + m + c];
       MZ[i * nz + c] = s;
     }
   for (int a = 0; a < nz; ++a)
@@ -405,19 +431,30 @@ static double kkt_factor(Kkt* k, const double* M, const double* A, int nw, int m
       const double s = 0.5 * (Hr[a * nz + b] + Hr[b * nz + a]);
       Hr[a * nz + b] = Hr[b * nz + a] = s;
     }
+  if (k->aug)  /* dW acts on W only: Z~^T diag(I, 0) Z~ */
+    for (int a = 0; a < nz; ++a)
+      for (int b = 0; b < nz; ++b) {
+        double s = 0.0;
+        for (int t = 0; t < k->nw0; ++t) s += k->Q[t * nw + m + a] * k->Q[t * nw + m + b];
+        Pz[a * nz + b] = s;
+      }
   double delta = 0.0;
   if (nz) {
     const double piv_tol = PIVOT_REL * dmx;
     for (int it = 0; it < 65; ++it) {
       memcpy(k->L, Hr, sizeof(double) * (size_t)nz * nz);
-      for (int i = 0; i < nz; ++i) k->L[i * nz + i] += delta;
+      if (k->aug)
+        for (int a = 0; a < nz; ++a)
+          for (int b = 0; b < nz; ++b) k->L[a * nz + b] += delta * Pz[a * nz + b];
+      else
+        for (int i = 0; i < nz; ++i) k->L[i * nz + i] += delta;
       if (!cholesky(k->L, nz, piv_tol)) break;
       const double first = dwl == 0.0 ? 1e-4 : dmax(dwl / 3.0, 1e-20);
       delta = delta == 0.0 ? first : delta * (dwl == 0.0 ? 100.0 : 8.0);
     }
   }
-  memcpy(k->Mw, M, sizeof(double) * (size_t)nw * nw);
-  for (int i = 0; i < nw; ++i) k->Mw[i * nw + i] += delta;
+  memcpy(k->Mw, Mr, sizeof(double) * (size_t)nw * nw);
+  for (int i = 0; i < (k->aug ? k->nw0 : nw); ++i) k->Mw[i * nw + i] += delta;
   return delta;
 }
 
@@ -470,7 +507,18 @@ static void kkt_solve_once(const Kkt* k, const double* q1, const double* q2, dou
   }
 }
 /* one refinement step when A has full rank */
+static void kkt_solve_full(const Kkt* k, const double* q1, const double* q2, double* dw, double* dy);
 static void kkt_solve(const Kkt* k, const double* q1, const double* q2, double* dw, double* dy) {
+  if (k->aug) {  /* the augmented system: q1~ = [q1; 0], dw = the first nw0 unknowns */
+    double qa[NWMAX], da[NWMAX];
+    for (int i = 0; i < k->nw; ++i) qa[i] = i < k->nw0 ? q1[i] : 0.0;
+    kkt_solve_full(k, qa, q2, da, dy);
+    memcpy(dw, da, sizeof(double) * (size_t)k->nw0);
+    return;
+  }
+  kkt_solve_full(k, q1, q2, dw, dy);
+}
+static void kkt_solve_full(const Kkt* k, const double* q1, const double* q2, double* dw, double* dy) {
   const int nw = k->nw, m = k->m;
   kkt_solve_once(k, q1, q2, dw, dy);
   if (k->rank_def) return;

@@ -53,6 +53,8 @@ def _load(path=LIB_PATH):
     lib.cplo_set_watchdog.restype = None
     lib.cplo_watchdog_events.argtypes = [ctypes.POINTER(ctypes.c_long)]
     lib.cplo_watchdog_events.restype = None
+    lib.cplo_set_jac_reg.argtypes = [c_int]
+    lib.cplo_set_jac_reg.restype = None
     return lib
 
 
@@ -202,6 +204,13 @@ def set_nlp_scaling(method):
     """nlp_scaling_method of the compiled restatement: "gradient-based" (IPOPT's default, the
     reference's; the default here too) or "none" (process-wide)."""
     lib.cplo_set_nlp_scaling(1 if method == "gradient-based" else 0)
+
+
+def set_jac_reg(on):
+    """IPOPT's regularisation of a rank-deficient Jacobian ([[W, A^T], [A, -delta_c I]], delta_c = 1e-8 mu^0.25)
+    in the compiled restatement (opt-in, process-wide): the measurement of what the engine's treatment (delta_c
+    on R's near-zero pivots) costs TestBasic's degenerate starts."""
+    lib.cplo_set_jac_reg(1 if on else 0)
 
 
 def set_watchdog(on):
