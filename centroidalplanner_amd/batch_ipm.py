@@ -155,6 +155,7 @@ class BatchSolveResult:
     iterations_run: int  # lock-step iterations of the batch
     graph: bool          # the iteration ran as a captured HIP graph
     compactions: int = 0  # active-set compactions of the native engine (the batch shrank this often)
+    final_rows: int = 0   # the native engine's lock-step batch size at the end (after compactions)
     restorations: object = None  # [B] int: restoration-phase entries per instance
     fallback: object = None  # [B] bool: x is the best feasible iterate, not the last (fallback_viol_tol)
     nan_jacobian: object = None  # [B] int: NaN Jacobian entries at the start point (taken as 0)
@@ -244,7 +245,7 @@ class NativeSolver:
         return BatchSolveResult(x=x, y=y, status=status.to(torch.int64), iterations=iters.to(torch.int64),
                                 objective=obj, primal_inf=pinf, dual_inf=dinf, evaluations=int(ev.value),
                                 iterations_run=int(it.value), graph=bool(g.value), compactions=int(nc.value),
-                                restorations=resto, fallback=fb.bool(), nan_jacobian=nanj.to(torch.int64))
+                                final_rows=int(rows.value), restorations=resto, fallback=fb.bool(), nan_jacobian=nanj.to(torch.int64))
 
 
 _NATIVE_CACHE = {}
