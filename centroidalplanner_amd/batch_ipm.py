@@ -175,7 +175,7 @@ class NativeSolver:
 
     def __init__(self, problem, batch, tol=1e-8, max_iter=3000, mu_init=0.1, acceptable_tol=1e-6,
                  acceptable_iter=15, max_ls=40, max_soc=4, hessian="exact", fd_step=1e-6, graph=True, compact=True,
-                 ls_kernel=2, fallback_viol_tol=0.0, nlp_scaling="gradient-based"):
+                 ls_kernel=2, fallback_viol_tol=0.0, nlp_scaling="gradient-based", jacobian_regularization="pivot"):
         o = _abi.SolveOptions()
         _abi.lib.cpl_solve_options_default(ctypes.byref(o))
         o.max_iter, o.max_ls, o.max_soc, o.acceptable_iter = int(max_iter), int(max_ls), int(max_soc), int(acceptable_iter)
@@ -187,6 +187,9 @@ class NativeSolver:
         o.ls_kernel = int(ls_kernel)
         o.fallback_viol_tol = float(fallback_viol_tol)
         o.nlp_scaling = {"gradient-based": 1, "none": 0}[nlp_scaling]
+        if jacobian_regularization != "pivot":
+            raise ValueError("the native engine regularises a rank-deficient Jacobian on R's pivots only "
+                             "(jacobian_regularization='pivot')")
         self.problem, self.batch = problem, int(batch)
         self.desc = problem.desc()
         self.handle = ctypes.c_void_p()
@@ -274,7 +277,7 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                     fd_step: float = 1e-6, graph: Optional[bool] = None, check_every: int = 4,
                     verbose: int = 0, compact: bool = True, verbose_instance: int = 0,
                     ls_kernel: int = 2, fallback_viol_tol: float = 0.0,
-                    nlp_scaling: str = "gradient-based") -> BatchSolveResult:
+                    nlp_scaling: str = "gradient-based", jacobian_regularization: str = "pivot") -> BatchSolveResult:
     """Solve B instances of `problem`'s template from the starting points X0 [B, n] (torch float64,
     device tensor), per-instance robot masses `mass` [B] (None: the template's).
 
@@ -306,6 +309,9 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         raise ValueError("hessian must be 'exact', 'fd' or 'limited-memory'")
     if nlp_scaling not in ("gradient-based", "none"):
         raise ValueError("nlp_scaling must be 'gradient-based' or 'none'")
+    if jacobian_regularization not in ("ipopt", "pivot"):
+        raise ValueError("jacobian_regularization must be 'ipopt' or 'pivot'")
+    jac_reg = jacobian_regularization == "ipopt"
     use_bfgs = hessian == "limited-memory"
     import torch
 
@@ -316,7 +322,8 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         ns = _native(problem, X0.shape[0], tol=tol, max_iter=max_iter, mu_init=mu_init, acceptable_tol=acceptable_tol,
                      acceptable_iter=acceptable_iter, max_ls=max_ls, max_soc=max_soc, hessian=hessian,
                      fd_step=fd_step, graph=True if graph is None else bool(graph), compact=compact,
-                     ls_kernel=ls_kernel, fallback_viol_tol=fallback_viol_tol, nlp_scaling=nlp_scaling)
+                     ls_kernel=ls_kernel, fallback_viol_tol=fallback_viol_tol, nlp_scaling=nlp_scaling,
+                     jacobian_regularization=jacobian_regularization)
         r = ns.solve(X0, mass, None if evaluator is None else evaluator.env_tag)
         if evaluator is not None:
             evaluator.calls += r.evaluations
@@ -579,7 +586,75 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
             return torch.where(keep, d1, d1 + c1), torch.where(keep, d2, d2 + c2)
 
         dw, dy = refined(r1, r2)
-        return dw, dy, delta_w, lambda r2v, mask=None: refined(r1, r2v)[0]
+        if not (jac_reg and bool(rank_def.any())):
+            return dw, dy, delta_w, lambda r2v, mask=None: refined(r1, r2v)[0]
+        # IPOPT's regularisation of the rank-deficient systems (jacobian_regularization="ipopt"): the
+        # system [[W + dW I, A^T], [A, -delta_c I]], delta_c = 1e-8 mu^0.25, solved as the augmented one
+        # in (dw, s): W~ = diag(W, I), A~ = [A, -sqrt(delta_c) I] (full row rank), dW on the W block only
+        # — the compiled restatement's kkt_factor with cplo_set_jac_reg (oracle/cpl_solve_host.c)
+        idx = torch.nonzero(rank_def).flatten()
+        k, na = idx.numel(), nw + m
+        sdc = torch.sqrt(1e-8 * mu[idx] ** 0.25)
+        Ma = torch.zeros(k, na, na, dtype=dt)
+        Ma[:, :nw, :nw] = M[idx]
+        Ma[:, nw:, nw:] = torch.eye(m, dtype=dt)
+        Aa = torch.cat([A[idx], -sdc[:, None, None] * torch.eye(m, dtype=dt)], 2)
+        Qa, Ra_ = torch.linalg.qr(Aa.transpose(1, 2), mode="complete")
+        Ya, Za = Qa[:, :, :m], Qa[:, :, m:]
+        Ra = Ra_[:, :m, :m]
+        Hra = Za.transpose(1, 2) @ Ma @ Za
+        Hra = 0.5 * (Hra + Hra.transpose(1, 2))
+        Pz = Za[:, :nw, :].transpose(1, 2) @ Za[:, :nw, :]  # dW acts on W only
+        piv_tol_a = _PIVOT_REL * Ma.diagonal(dim1=1, dim2=2).abs().amax(1)
+        dwl_a = dwl[idx]
+
+        def chol_a(dw_):
+            Lf, inf_ = torch.linalg.cholesky_ex(Hra + dw_[:, None, None] * Pz)
+            inf_ = torch.where((inf_ == 0) & ((Lf.diagonal(dim1=1, dim2=2) ** 2).amin(1) <= piv_tol_a),
+                               torch.ones_like(inf_), inf_)
+            return Lf, inf_
+
+        dwa = torch.zeros(k, dtype=dt)
+        La, infa = chol_a(dwa)
+        for _ in range(64):
+            bad = infa != 0
+            if not bool(bad.any()):
+                break
+            first_dw = torch.where(dwl_a == 0, torch.full_like(dwa, 1e-4), torch.clamp(dwl_a / 3.0, min=1e-20))
+            grow = dwa * torch.where(dwl_a == 0, 100.0, 8.0)
+            dwa = torch.where(bad, torch.where(dwa == 0, first_dw, grow), dwa)
+            Ln, infn = chol_a(dwa)
+            La = torch.where(bad[:, None, None], Ln, La)
+            infa = torch.where(bad, infn, infa)
+        Mwa = Ma.clone()
+        Mwa[:, :nw, :nw] += dwa[:, None, None] * eye_w
+
+        def solve_a(q1, q2):
+            py = torch.linalg.solve_triangular(Ra.transpose(1, 2), q2.unsqueeze(2), upper=False)
+            d = Ya @ py
+            pz = torch.cholesky_solve(Za.transpose(1, 2) @ (q1.unsqueeze(2) - Mwa @ d), La)
+            d = d + Za @ pz
+            dy_ = torch.linalg.solve_triangular(Ra, Ya.transpose(1, 2) @ (q1.unsqueeze(2) - Mwa @ d), upper=True)
+            return d.squeeze(2), dy_.squeeze(2)
+
+        def refined_a(q1, q2):
+            q1a = torch.cat([q1, torch.zeros(k, m, dtype=dt)], 1)
+            d1, d2 = solve_a(q1a, q2)
+            e1 = q1a - (Mwa @ d1.unsqueeze(2)).squeeze(2) - (Aa.transpose(1, 2) @ d2.unsqueeze(2)).squeeze(2)
+            e2 = q2 - (Aa @ d1.unsqueeze(2)).squeeze(2)
+            c1, c2 = solve_a(e1, e2)
+            return (d1 + c1)[:, :nw], d2 + c2
+
+        dwr, dyr = refined_a(r1[idx], r2[idx])
+        dw, dy, delta_w = dw.clone(), dy.clone(), delta_w.clone()
+        dw[idx], dy[idx], delta_w[idx] = dwr, dyr, dwa
+
+        def solve_primal(r2v, mask=None):
+            d = refined(r1, r2v)[0].clone()
+            d[idx] = refined_a(r1[idx], r2v[idx])[0]
+            return d
+
+        return dw, dy, delta_w, solve_primal
 
     def kkt_qd(W, A, Dinv, r1, r2, dwl, mask):
         """The restoration phase's Newton system after p and n are eliminated (as IPOPT's

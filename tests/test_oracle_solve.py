@@ -189,3 +189,10 @@ def test_ipopt_jacobian_regularisation_on_the_simple_problem():
     assert d["status"] == 1 and d["iterations"] == 388
     assert r["status"] == 0 and r["iterations"] <= 20
     assert r["objective"] <= d["objective"] * (1.0 + 1e-12)
+    # the host restatement's opt-in form (batch_ipm_solve(jacobian_regularization="ipopt")): the same
+    # iterations, the same point to rounding
+    h = batch_ipm_solve(prob, torch.as_tensor(x0[None]), torch.as_tensor(np.array([mass])), max_iter=3000,
+                        evaluator=OracleBatchEvaluator(prob, 1), hessian="limited-memory",
+                        jacobian_regularization="ipopt")
+    assert int(h.status[0]) == r["status"] and int(h.iterations[0]) == r["iterations"]
+    np.testing.assert_allclose(h.x[0].numpy(), r["x"], rtol=0, atol=1e-9)
