@@ -2804,7 +2804,8 @@ static int g_ablate = 0;           // measurement-only: 1 = skip the compute pha
                                    // (default one per CU while the Superquadric list is non-empty),
                                    // 1024 / 2048 = the Ground half's compute waves at priority 1 / 2,
                                    // 4096 = the 4-instance Superquadric list tiles at the default priority,
-                                   // 8192 = the tile kernel's phase barriers skipped (wrong outputs)
+                                   // 8192 = the tile kernel's phase barriers skipped (wrong outputs),
+                                   // 16384 = the split's Superquadric grid for half the batch
 
 static size_t tile_budget() { return g_lds_budget ? g_lds_budget : 48 * 1024; }
 static size_t pipe_budget() { return g_lds_budget ? g_lds_budget : 48 * 1024; }
@@ -3103,7 +3104,11 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
     // 4096 leaves the 4-instance tiles at the default priority)
     Ks.list_prio = ((g_ablate & 4096) && Ks.T < 8) ? 0 : 1;
     const unsigned grid_g = (unsigned)(ntg < want_g ? ntg : want_g);
-    const unsigned grid_s = (unsigned)((batch + Ks.T - 1) / Ks.T);  // every tile the list may hold
+    // every tile the list may hold (measurement only, ablation 16384: half of them — correct only for
+    // batches with at most half their instances Superquadric, e.g. the bench's alternating tags — to
+    // price the empty workgroups past the list)
+    const int64_t grid_inst = (g_ablate & 16384) ? (batch + 1) / 2 : batch;
+    const unsigned grid_s = (unsigned)((grid_inst + Ks.T - 1) / Ks.T);
     const size_t nparts = (size_t)grid_g + (size_t)grid_s * 4;
     if (K.want_norms && (st = norm_workspace(stream, nparts, &ws))) return st;
     // the two halves on two streams (fork after the partition, join before the norms' finish): the
@@ -3614,7 +3619,7 @@ int32_t cpl_eval_batch_norms(const cpl_problem_desc* d, int64_t batch, const dou
 
 int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_threads, int32_t nt_stores,
                        int32_t ablate) {
-  if (ablate < 0 || (ablate > 2 && (ablate & ~(4 | 8 | 16 | 32 | 64 | 128 | 256 | 512 | 1024 | 2048 | 4096 | 8192))))
+  if (ablate < 0 || (ablate > 2 && (ablate & ~(4 | 8 | 16 | 32 | 64 | 128 | 256 | 512 | 1024 | 2048 | 4096 | 8192 | 16384))))
     return fail(CPL_ERR_INVALID_ARGUMENT, "unknown ablation");
   g_ablate = ablate;
   if (kernel_variant < VAR_AUTO || kernel_variant > VAR_SPLIT_JD) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown kernel variant");
