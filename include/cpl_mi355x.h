@@ -229,7 +229,8 @@ int32_t cpl_time_eval_batch_ex(const cpl_problem_desc* d, int64_t batch, const d
  * tile-stationary, 4 = tile-stationary with the Jacobian written straight to the records, 5 =
  * entry-parallel (none / Ground, IFOPT CSR instance-major records: every g / jac entry computed by
  * the thread that stores it, no output image in LDS), 6 / 7 = mixed batches split by kind (the
- * Superquadric half LDS-staged / Jacobian-direct; the default for mixed is 7's form);
+ * Superquadric half LDS-staged on the contiguous kernel's uniform-axis tiles / Jacobian-direct; the
+ * default for mixed is 6's form since round 6, 7's before);
  * tile_lds_kb = LDS budget of one workgroup (8..160 KiB; 0 = per-kernel
  * default: 48 KiB for both: the largest power-of-two tile that fits, e.g. 8 instances of 8
  * Superquadric contacts, 4 of 16); wg_threads = 128 or 256 for the tile kernel (default 256);
@@ -238,7 +239,10 @@ int32_t cpl_time_eval_batch_ex(const cpl_problem_desc* d, int64_t batch, const d
  * the kind split, bits 4 = its halves one after the other on one stream, 8 = the Ground half issued
  * first, 16 / 64 / 128 = the Ground list at 48 / 36 / 32 KiB instead of 40, 32 = the Superquadric tiles
  * at 40 KiB instead of 48, 256 / 512 = every Ground workgroup walking the tiles / two per CU instead of
- * one per CU while the Superquadric list is non-empty).
+ * one per CU while the Superquadric list is non-empty, 1024 / 2048 = the Ground half's compute waves at
+ * wave priority 1 / 2, 4096 = the 4-instance Superquadric list tiles' gather / copy-out at the default
+ * priority, 16384 = the Superquadric grid for half the batch (correct only when at most half the
+ * instances are Superquadric); for the tile kernel, 8192 = its phase barriers skipped: garbage results).
  * Every variant computes bit-identical results.  Not thread-safe against concurrent launches. */
 int32_t cpl_set_tuning(int32_t kernel_variant, int32_t tile_lds_kb, int32_t wg_threads, int32_t nt_stores,
                        int32_t ablate);
