@@ -7,7 +7,7 @@ out=${1:?out dir}
 mkdir -p "$out"
 AB="python3 -u scripts/ab_kernels.py"
 V="0:0:256:1,0:0:256:1:16384,0:0:256:1:260,0:0:256:1:8"
-timeout -k 10 200 python3 -u scripts/variant_bitwise.py --config mixed16 --batch 20011 --variants 0:0:256:1:16384 > "$out/bitwise.jsonl" || exit $?
+# (16384 is bitwise on random and all-Ground tags, not all-Superquadric: a pricing probe only)
 timeout -k 10 400 $AB --config mixed16 --rounds 4 --reps 10 --variants $V > "$out/mixed16.jsonl" || exit $?
 timeout -k 10 200 $AB --config mixed16 --batch 131072 --rounds 4 --reps 20 --variants $V > "$out/mixed16_shard.jsonl" || exit $?
 echo done
