@@ -92,6 +92,7 @@ class SolveOptions(ctypes.Structure):
         ("fd_step", c_double),
         ("fallback_viol_tol", c_double),
         ("nlp_scaling", c_int32),
+        ("jacobian_regularization", c_int32),
     ]
 
 

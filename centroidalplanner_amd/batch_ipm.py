@@ -187,9 +187,7 @@ class NativeSolver:
         o.ls_kernel = int(ls_kernel)
         o.fallback_viol_tol = float(fallback_viol_tol)
         o.nlp_scaling = {"gradient-based": 1, "none": 0}[nlp_scaling]
-        if jacobian_regularization != "pivot":
-            raise ValueError("the native engine regularises a rank-deficient Jacobian on R's pivots only "
-                             "(jacobian_regularization='pivot')")
+        o.jacobian_regularization = {"pivot": 0, "ipopt": 1}[jacobian_regularization]
         self.problem, self.batch = problem, int(batch)
         self.desc = problem.desc()
         self.handle = ctypes.c_void_p()
@@ -304,7 +302,11 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     the free variables; a NaN entry counts as 0, this solve's NaN policy); the iteration runs on the
     scaled problem (IPOPT's tol applies there), x is not scaled, the returned multipliers are the
     unscaled ones (dc y / df).  "none": no scaling.  The constraint bounds here are 0 or infinite, so
-    scaling leaves them unchanged."""
+    scaling leaves them unchanged.
+    jacobian_regularization: a rank-deficient A (|R_jj| < 1e-10 |R|max): "pivot" (default) adds
+    delta_c = 1e-8 mu^0.25 |R|max to R's small pivots; "ipopt" solves IPOPT's [[W, A^T], [A, -delta_c I]]
+    (delta_c = 1e-8 mu^0.25) as the augmented system — here and in the engine
+    (cpl_solve_options.jacobian_regularization, csrc/cpl_kkt.hip cpl_kkt_aug_kernel)."""
     if hessian not in ("exact", "fd", "limited-memory"):
         raise ValueError("hessian must be 'exact', 'fd' or 'limited-memory'")
     if nlp_scaling not in ("gradient-based", "none"):

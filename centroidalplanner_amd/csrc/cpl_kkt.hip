@@ -125,10 +125,11 @@ __device__ __forceinline__ void group_dots(int n, int len, const double* A, int 
 // Solve with the factors in LDS: Q [nw][nw] (row-major: Q[r*nw + c]), QR array (row j = column j of
 // A^T after the reflections; R[i][j] = QR[j*nw + i] for i < j, R[j][j] = QR[j*nw + j]), L [nz][nz] the
 // Cholesky of the reduced Hessian, M [nw][nw] (plus delta_w on the diagonal, applied here).
-// Vectors in LDS: q1 [nw], q2 [m] -> dw [nw], dy [m].  tmp: >= 2*nw doubles.
-__device__ __forceinline__ void kkt_solve_lds(int nw, int m, const double* Q, const double* QR, const double* L,
-                              const double* M, double dW, const double* q1, const double* q2, double* dw,
-                              double* dy, double* tmp) {
+// Vectors in LDS: q1 [nw], q2 [m] -> dw [nw], dy [m].  tmp: >= 2*nw doubles.  delta_w acts on the
+// first nw0 unknowns (nw0 = nw but for the augmented system of a regularised Jacobian: its W block).
+__device__ __forceinline__ void kkt_solve_lds(int nw, int m, int nw0, const double* Q, const double* QR,
+                              const double* L, const double* M, double dW, const double* q1, const double* q2,
+                              double* dw, double* dy, double* tmp) {
   const int tid = threadIdx.x;
   const int nz = nw - m;
   double* py = tmp;          // [m]
@@ -142,7 +143,7 @@ __device__ __forceinline__ void kkt_solve_lds(int nw, int m, const double* Q, co
   group_dots<4>(nw, m, Q, nw, 1, py, 1, [&](int r, double d) { dw[r] = d; });
   __syncthreads();
   // t = q1 - (M + dW I) Y p_y
-  group_dots<4>(nw, nw, M, nw, 1, dw, 1, [&](int r, double d) { t[r] = q1[r] - dW * dw[r] - d; });
+  group_dots<4>(nw, nw, M, nw, 1, dw, 1, [&](int r, double d) { t[r] = q1[r] - (r < nw0 ? dW * dw[r] : 0.0) - d; });
   __syncthreads();
   if (nz > 0) {
     // rz = Z^T t into tmp[m .. m+nz) (py still needed) -> p_z by the two triangular solves
@@ -159,7 +160,7 @@ __device__ __forceinline__ void kkt_solve_lds(int nw, int m, const double* Q, co
     __syncthreads();
   }
   // u = q1 - (M + dW I) dw  -> s = Y^T u -> R dy = s
-  group_dots<4>(nw, nw, M, nw, 1, dw, 1, [&](int r, double d) { t[r] = q1[r] - dW * dw[r] - d; });
+  group_dots<4>(nw, nw, M, nw, 1, dw, 1, [&](int r, double d) { t[r] = q1[r] - (r < nw0 ? dW * dw[r] : 0.0) - d; });
   __syncthreads();
   group_dots<4>(m, nw, Q, 1, nw, t, 1, [&](int k, double d) { dy[k] = d; });
   __syncthreads();
@@ -188,37 +189,33 @@ __host__ __device__ inline int kkt_launch_lds_doubles(int nw, int m, int mode) {
   return kkt_lds_doubles(nw, m) + (mode == 0 && kkt_mz_in_lds(nw, m) ? nw * (nw - m) : 0) + 8;
 }
 
-// NW, MM > 0: the kernel specialised for one system size (nw = NW, m = MM; the arguments are
-// ignored) — every stride, trip count and index division becomes a compile-time constant, which
-// the instruction-issue-bound kernel needs (SQ counters: ~75 % of wave cycles parked, the SIMDs'
-// issue near saturation from 4 workgroups per CU); NW = 0: any size.
+// One system on one workgroup (the body of cpl_kkt_kernel and cpl_kkt_aug_kernel): M [nw][nw], A
+// [m][nw], the right-hand sides q1 [nw], q2 [m] in global memory; *mub (mode 0: the barrier parameter),
+// *lastb (the previous delta_w, or none); the outputs dwo [nw0], dyo [m], *dWo, *dCo, *infob; wsb the
+// system's workspace (the factors kept for mode 1).  nw0 = nw but for an augmented system (Pzg set):
+// delta_w then acts on its first nw0 unknowns only — on the reduced Hessian as dW Pz, Pz = Z[:nw0]^T
+// Z[:nw0] (global scratch Pzg [nz][nz]) — and dw is its first nw0 entries.
+// NW, MM > 0: specialised for one system size (nw = NW, m = MM; the arguments are ignored) — every
+// stride, trip count and index division becomes a compile-time constant, which the
+// instruction-issue-bound kernel needs (SQ counters: ~75 % of wave cycles parked, the SIMDs' issue
+// near saturation from 4 workgroups per CU); NW = 0: any size.
 template <int NW, int MM>
-__global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 8))) void cpl_kkt_kernel(
-    int mode, int64_t batch, int nw_arg, int m_arg, const double* __restrict__ Mg, const double* __restrict__ Ag,
-    const double* __restrict__ r1g, const double* __restrict__ r2g, const double* __restrict__ mug,
-    const double* __restrict__ dw_last, const uint8_t* __restrict__ active, double* __restrict__ dwg,
-    double* __restrict__ dyg, double* __restrict__ dWg, double* __restrict__ dCg, int32_t* __restrict__ info,
-    double* __restrict__ ws) {
-  extern __shared__ __align__(16) double sm[];
-  __shared__ KktShared sh;
+__device__ __forceinline__ void kkt_block(int mode, int nw_arg, int m_arg, int nw0, const double* __restrict__ M,
+                                          const double* __restrict__ Ab, const double* __restrict__ q1,
+                                          const double* __restrict__ q2, const double* mub, const double* lastb,
+                                          double* __restrict__ dwo, double* __restrict__ dyo, double* dWo,
+                                          double* dCo, int32_t* infob, double* __restrict__ wsb, double* Pzg,
+                                          double* sm, KktShared& sh) {
   const int nw = NW > 0 ? NW : nw_arg;
   const int m = NW > 0 ? MM : m_arg;
-  const int64_t b = blockIdx.x;
-  if (b >= batch) return;
   const int tid = threadIdx.x;
   const int nz = nw - m;
   double* Q = sm;
   double* QR = Q + nw * nw;
   double* L = QR + m * nw;
-  const double* q1 = r1g + b * nw;  // right-hand sides: global
-  const double* q2 = r2g + b * m;
   double* dw = L + nz * nz;
   double* dy = dw + nw;
   double* tmp = dy + m;  // max(2 nw, 3 m)
-  const double* Mb = Mg + b * nw * nw;
-  const double* M = Mb;  // global
-  const double* Ab = Ag + b * m * nw;
-  double* wsb = ws + b * kkt_ws_per(nw, m);
   // refinement residual and correction: global scratch past M Z in the workspace (overwritten by
   // the factors at the end)
   double* e1 = wsb + nw * nz;
@@ -226,21 +223,14 @@ __global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 
   double* c1 = e2 + m;
   double* c2 = c1 + nw;
 
-  if (active && !active[b]) {
-    for (int i = tid; i < nw; i += KKT_THREADS) dwg[b * nw + i] = 0.0;
-    for (int i = tid; i < m; i += KKT_THREADS) dyg[b * m + i] = 0.0;
-    if (tid == 0 && mode == 0) { dWg[b] = 0.0; dCg[b] = 0.0; info[b] = 0; }
-    return;
-  }
-
   if (mode == 1) {  // re-solve with the kept factors
     const int64_t per = kkt_ws_per(nw, m);
     for (int64_t i = tid; i < per - 4; i += KKT_THREADS) sm[i] = wsb[i];
     if (tid == 0) { sh.delta_w = wsb[per - 4]; sh.delta_c = wsb[per - 3]; }
     __syncthreads();
-    kkt_solve_lds(nw, m, Q, QR, L, M, sh.delta_w, q1, q2, dw, dy, tmp);
-    for (int i = tid; i < nw; i += KKT_THREADS) dwg[b * nw + i] = dw[i];
-    for (int i = tid; i < m; i += KKT_THREADS) dyg[b * m + i] = dy[i];
+    kkt_solve_lds(nw, m, nw0, Q, QR, L, M, sh.delta_w, q1, q2, dw, dy, tmp);
+    for (int i = tid; i < nw0; i += KKT_THREADS) dwo[i] = dw[i];
+    for (int i = tid; i < m; i += KKT_THREADS) dyo[i] = dy[i];
     return;
   }
 
@@ -443,7 +433,7 @@ __global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 
   if (tid == 0) {
     double rmax = 0.0;
     for (int j = 0; j < m; ++j) rmax = fabs(QR[j * nw + j]) > rmax ? fabs(QR[j * nw + j]) : rmax;
-    const double dc = 1e-8 * pow(mug[b], 0.25) * (rmax > 0.0 ? rmax : 1.0);
+    const double dc = 1e-8 * pow(*mub, 0.25) * (rmax > 0.0 ? rmax : 1.0);
     int def = 0;
     for (int j = 0; j < m; ++j)
       if (!(fabs(QR[j * nw + j]) >= 1e-10 * rmax) || rmax == 0.0) {
@@ -454,13 +444,19 @@ __global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 
     sh.rank_def = def;
     sh.delta_c = def ? dc : 0.0;
   }
+  if (Pzg && nz > 0) {  // the augmented system: delta_w's shift of the reduced Hessian, Z[:nw0]^T Z[:nw0]
+    for (int e = tid; e < nz * nz; e += KKT_THREADS) {
+      const int a = e / nz, c = e - a * nz;
+      Pzg[e] = lds_dot(Q + m + a, nw, Q + m + c, nw, nw0);
+    }
+  }
   __syncthreads();
   // ---- reduced Hessian Hr = Z^T (M Z), M Z staged in LDS or the global workspace
   double* Hr0 = L;  // keep the unshifted reduced Hessian in the workspace slot of L first
   if (nz > 0) {
     // LDS after tmp when it fits (kkt_mz_in_lds), else global scratch (the workspace; overwritten
     // at the end)
-    double* MZ = kkt_mz_in_lds(nw, m) ? tmp + (2 * nw > 3 * m ? 2 * nw : 3 * m) : ws + b * kkt_ws_per(nw, m);
+    double* MZ = kkt_mz_in_lds(nw, m) ? tmp + (2 * nw > 3 * m ? 2 * nw : 3 * m) : wsb;
     // MZ = M Z: a thread per (row r, 4 columns), M[r][k] from global once per k, Z[k][c..c+3] from
     // LDS (reads past Z's last column land inside the LDS image and are discarded)
     const int nb = (nz + 3) >> 2;
@@ -539,7 +535,7 @@ __global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 
     // ---- inertia correction: Cholesky of Hr + delta_w I, IPOPT's delta_w schedule — wave 0 alone
     // (no workgroup barriers inside the retry loop; the other waves wait at the next barrier)
     if (tid < 64) {
-      const double last = dw_last ? dw_last[b] : 0.0;
+      const double last = lastb ? *lastb : 0.0;
       double dW = 0.0;
       int32_t inf = 0;
       // a pivot at or below DBL_EPSILON max|M_ii| — the rounding level of Z^T M Z's entries, M
@@ -551,7 +547,8 @@ __global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 
       const double pivot_min = 2.220446049250313e-16 * mmax;
       #pragma unroll 1
       for (int attempt = 0; attempt < 64; ++attempt) {
-        for (int e = tid; e < nz * nz; e += 64) L[e] = Hsave[e] + ((e / nz == e % nz) ? dW : 0.0);
+        for (int e = tid; e < nz * nz; e += 64)
+          L[e] = Hsave[e] + (Pzg ? dW * Pzg[e] : ((e / nz == e % nz) ? dW : 0.0));
         if (wave_cholesky(L, nz, pivot_min)) break;
         if (dW == 0.0) dW = last == 0.0 ? 1e-4 : fmax(1e-20, last / 3.0);
         else dW *= last == 0.0 ? 100.0 : 8.0;
@@ -559,22 +556,22 @@ __global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 
       }
       if (tid == 0) {
         sh.delta_w = dW;
-        if (info) info[b] = inf;
+        if (infob) *infob = inf;
       }
     }
     __syncthreads();
   } else {
-    if (tid == 0) { sh.delta_w = 0.0; if (info) info[b] = 0; }
+    if (tid == 0) { sh.delta_w = 0.0; if (infob) *infob = 0; }
     __syncthreads();
   }
   const double dW = sh.delta_w;
   KKT_MARK(4);
   // ---- solve, then one step of iterative refinement on the unregularised system
-  kkt_solve_lds(nw, m, Q, QR, L, M, dW, q1, q2, dw, dy, tmp);
+  kkt_solve_lds(nw, m, nw0, Q, QR, L, M, dW, q1, q2, dw, dy, tmp);
   KKT_MARK(5);
   if (!sh.rank_def) {
     // e1[r] is written and then updated by the same lane (group assignment depends on r only)
-    group_dots<4>(nw, m, Ab, 1, nw, dy, 1, [&](int r, double d) { e1[r] = q1[r] - dW * dw[r] - d; });
+    group_dots<4>(nw, m, Ab, 1, nw, dy, 1, [&](int r, double d) { e1[r] = q1[r] - (r < nw0 ? dW * dw[r] : 0.0) - d; });
     group_dots<4>(nw, nw, M, nw, 1, dw, 1, [&](int r, double d) { e1[r] -= d; });
     group_dots<4>(m, nw, Ab, nw, 1, dw, 1, [&](int k, double d) { e2[k] = q2[k] - d; });
     __syncthreads();
@@ -590,22 +587,101 @@ __global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 
     __syncthreads();
     if (sh.flag) {
       // the correction (e1, e2) -> (c1, c2), global scratch
-      kkt_solve_lds(nw, m, Q, QR, L, M, dW, e1, e2, c1, c2, tmp);
+      kkt_solve_lds(nw, m, nw0, Q, QR, L, M, dW, e1, e2, c1, c2, tmp);
       for (int r = tid; r < nw; r += KKT_THREADS) dw[r] += c1[r];
       for (int k = tid; k < m; k += KKT_THREADS) dy[k] += c2[k];
       __syncthreads();
     }
   }
   KKT_MARK(6);
-  for (int i = tid; i < nw; i += KKT_THREADS) dwg[b * nw + i] = dw[i];
-  for (int i = tid; i < m; i += KKT_THREADS) dyg[b * m + i] = dy[i];
-  if (tid == 0) { dWg[b] = dW; dCg[b] = sh.delta_c; }
+  for (int i = tid; i < nw0; i += KKT_THREADS) dwo[i] = dw[i];
+  for (int i = tid; i < m; i += KKT_THREADS) dyo[i] = dy[i];
+  if (tid == 0) { *dWo = dW; *dCo = sh.delta_c; }
   // keep the factors for mode 1 (the global scratch use above is finished: barrier first)
   __syncthreads();
   const int64_t per = kkt_ws_per(nw, m);
   for (int64_t i = tid; i < per - 4; i += KKT_THREADS) wsb[i] = sm[i];
   if (tid == 0) { wsb[per - 4] = dW; wsb[per - 3] = sh.delta_c; wsb[per - 2] = 0.0; wsb[per - 1] = 0.0; }
   KKT_MARK(7);
+}
+
+template <int NW, int MM>
+__global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 8))) void cpl_kkt_kernel(
+    int mode, int64_t batch, int nw_arg, int m_arg, const double* __restrict__ Mg, const double* __restrict__ Ag,
+    const double* __restrict__ r1g, const double* __restrict__ r2g, const double* __restrict__ mug,
+    const double* __restrict__ dw_last, const uint8_t* __restrict__ active, double* __restrict__ dwg,
+    double* __restrict__ dyg, double* __restrict__ dWg, double* __restrict__ dCg, int32_t* __restrict__ info,
+    double* __restrict__ ws) {
+  extern __shared__ __align__(16) double sm[];
+  __shared__ KktShared sh;
+  const int nw = NW > 0 ? NW : nw_arg;
+  const int m = NW > 0 ? MM : m_arg;
+  const int64_t b = blockIdx.x;
+  if (b >= batch) return;
+  const int tid = threadIdx.x;
+  if (active && !active[b]) {
+    for (int i = tid; i < nw; i += KKT_THREADS) dwg[b * nw + i] = 0.0;
+    for (int i = tid; i < m; i += KKT_THREADS) dyg[b * m + i] = 0.0;
+    if (tid == 0 && mode == 0) { dWg[b] = 0.0; dCg[b] = 0.0; info[b] = 0; }
+    return;
+  }
+  kkt_block<NW, MM>(mode, nw, m, nw, Mg + b * nw * nw, Ag + b * m * nw, r1g + b * nw, r2g + b * m,
+                    mug ? mug + b : nullptr, dw_last ? dw_last + b : nullptr, dwg + b * nw, dyg + b * m,
+                    dWg ? dWg + b : nullptr, dCg ? dCg + b : nullptr, info ? info + b : nullptr,
+                    ws + b * kkt_ws_per(nw, m), nullptr, sm, sh);
+}
+
+// IPOPT's regularisation of a rank-deficient Jacobian (cpl_solve_options.jacobian_regularization;
+// IpPDPerturbationHandler: delta_c = jacobian_regularization_value 1e-8 * mu^jacobian_regularization_
+// exponent 0.25 on the (2,2) block): [[W + dW I, A^T], [A, -delta_c I]] solved by the same null-space
+// method as the augmented system in (dw, s), W~ = diag(W, I), A~ = [A, -sqrt(delta_c) I] (full row
+// rank), whose KKT conditions are exactly the regularised system's (s = sqrt(delta_c) dy) — the
+// restatements' form (oracle/cpl_solve_host.c kkt_factor with cplo_set_jac_reg, batch_ipm.py kkt_host).
+// Launched after the factorisation kernel of the same call (either kernel marks a rank-deficient
+// system by its delta_c != 0, its R-pivot treatment): the marked systems only, mode 0 re-factorising
+// them in the augmented form and overwriting dw, dy, delta_w (delta_c := IPOPT's), mode 1 re-solving
+// with the augmented factors.  Workspace per system (kkt_aug_ws_per): the augmented factors | W~ | A~ |
+// [q1; 0] | Pz.
+__host__ __device__ inline int64_t kkt_aug_ws_per(int nw, int m) {
+  const int na = nw + m;
+  return kkt_ws_per(na, m) + (int64_t)na * na + (int64_t)m * na + na + (int64_t)nw * nw;
+}
+
+__global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_aug_kernel(
+    int mode, int64_t batch, int nw, int m, const double* __restrict__ Mg, const double* __restrict__ Ag,
+    const double* __restrict__ r1g, const double* __restrict__ r2g, const double* __restrict__ mug,
+    const double* __restrict__ dw_last, const uint8_t* __restrict__ active, double* __restrict__ dwg,
+    double* __restrict__ dyg, double* __restrict__ dWg, double* __restrict__ dCg, int32_t* __restrict__ info,
+    double* __restrict__ wsa) {
+  extern __shared__ __align__(16) double sm[];
+  __shared__ KktShared sh;
+  const int64_t b = blockIdx.x;
+  if (b >= batch || (active && !active[b]) || dCg[b] == 0.0) return;
+  const int na = nw + m, tid = threadIdx.x;
+  double* wsb = wsa + b * kkt_aug_ws_per(nw, m);
+  double* Ma = wsb + kkt_ws_per(na, m);
+  double* Aa = Ma + (int64_t)na * na;
+  double* q1a = Aa + (int64_t)m * na;
+  double* Pz = q1a + na;
+  if (mode == 0) {
+    const double* M = Mg + b * nw * nw;
+    const double* A = Ag + b * m * nw;
+    const double sdc = sqrt(1e-8 * pow(mug[b], 0.25));
+    for (int e = tid; e < na * na; e += KKT_THREADS) {
+      const int r = e / na, c = e - r * na;
+      Ma[e] = (r < nw && c < nw) ? M[r * nw + c] : (r == c ? 1.0 : 0.0);
+    }
+    for (int e = tid; e < m * na; e += KKT_THREADS) {
+      const int r = e / na, c = e - r * na;
+      Aa[e] = c < nw ? A[r * nw + c] : (c - nw == r ? -sdc : 0.0);
+    }
+  }
+  for (int i = tid; i < na; i += KKT_THREADS) q1a[i] = i < nw ? r1g[b * nw + i] : 0.0;
+  __syncthreads();
+  kkt_block<0, 0>(mode, na, m, nw, Ma, Aa, q1a, r2g + b * m, mug ? mug + b : nullptr,
+                  dw_last ? dw_last + b : nullptr, dwg + b * nw, dyg + b * m, dWg ? dWg + b : nullptr, dCg + b,
+                  info ? info + b : nullptr, wsb, Pz, sm, sh);
+  if (mode == 0 && tid == 0) dCg[b] = 1e-8 * pow(mug[b], 0.25);  // (stays != 0: the mark for mode 1)
 }
 
 // grad f + J^T y per instance from the CSR values (the Lagrangian gradient the solve loop
@@ -1108,6 +1184,32 @@ static KktWaveKernel kkt_wave_kernel_for(int nw, int m) {
 // the system size runs the one-wave kernel (whose factors the fused line-search kernel re-solves with)
 namespace cpl {
 bool kkt_wave_size(int nw, int m) { return kkt_wave_kernel_for(nw, m) != nullptr; }
+
+// IPOPT's Jacobian regularisation (cpl_kkt_aug_kernel): its workspace doubles per system, or -1 when
+// the augmented system (nw + m unknowns) exceeds the workgroup kernel (128 unknowns, one LDS image)
+int64_t kkt_aug_workspace_doubles(int nw, int m) {
+  const int na = nw + m;
+  if (nw <= 0 || m < 0 || m > nw || na > KKT_MAX_NW) return -1;
+  if (sizeof(double) * (size_t)kkt_launch_lds_doubles(na, m, 0) > 160 * 1024) return -1;
+  return kkt_aug_ws_per(nw, m);
+}
+
+// the marked (delta_c != 0) systems of the cpl_kkt_solve call just issued with the same arguments,
+// re-factorised (mode 0) or re-solved (mode 1) in IPOPT's regularised form
+int32_t kkt_aug_solve(int mode, int64_t batch, int nw, int m, const double* d_M, const double* d_A, const double* d_r1,
+                      const double* d_r2, const double* d_mu, const double* d_dwl, const uint8_t* d_active, double* d_dw,
+                      double* d_dy, double* d_delta_w, double* d_delta_c, int32_t* d_info, double* d_wsa,
+                      hipStream_t st) {
+  if (batch == 0) return CPL_OK;
+  if (kkt_aug_workspace_doubles(nw, m) < 0 || !d_delta_c || !d_wsa || (mode == 0 && (!d_mu || !d_delta_w)))
+    return fail(CPL_ERR_INVALID_ARGUMENT, "kkt_aug_solve: bad arguments");
+  const size_t lds = sizeof(double) * (size_t)kkt_launch_lds_doubles(nw + m, m, mode);
+  hipLaunchKernelGGL(cpl_kkt_aug_kernel, dim3((unsigned)batch), dim3(KKT_THREADS), lds, st, mode, batch, nw, m, d_M,
+                     d_A, d_r1, d_r2, d_mu, d_dwl, d_active, d_dw, d_dy, d_delta_w, d_delta_c, d_info, d_wsa);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(CPL_ERR_HIP, std::string("cpl_kkt_aug_kernel launch: ") + hipGetErrorString(e));
+  return CPL_OK;
+}
 }  // namespace cpl
 
 extern "C" {

@@ -45,6 +45,11 @@ int32_t eval_batch_scaled(const cpl_problem_desc* d, int64_t batch, const double
                           const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
                           int32_t flags, const double* df, const double* dc, const int32_t* row, void* stream);
 bool kkt_wave_size(int nw, int m);
+int64_t kkt_aug_workspace_doubles(int nw, int m);
+int32_t kkt_aug_solve(int mode, int64_t batch, int nw, int m, const double* d_M, const double* d_A, const double* d_r1,
+                      const double* d_r2, const double* d_mu, const double* d_dwl, const uint8_t* d_active, double* d_dw,
+                      double* d_dy, double* d_delta_w, double* d_delta_c, int32_t* d_info, double* d_wsa,
+                      hipStream_t st);
 bool ls_post_prologue(int64_t batch);
 // cpl_ipm.hip: the post-step kernel with the line-search setup (LsSetupArgs) as its tail
 int32_t ipm_post_step_ex(int64_t batch, int32_t nw, const double* d_w, const double* d_dw, const double* d_zL,
@@ -2211,6 +2216,8 @@ struct cpl_solver {
   int n = 0, m = 0, nnz = 0, nnz_rec = 0, nf = 0, nI = 0, nw = 0, nbounds = 0;
   bool analytic_H = false, bfgs = false, fd = false, fd_fused = true;
   bool ls_fusable = false;  // the one-wave KKT size: the fused line-search kernel can re-solve with its factors
+  bool jreg = false;        // IPOPT's Jacobian regularisation (cpl_kkt_aug_kernel after every KKT call)
+  double* ws_aug = nullptr; // its workspace
   double mu_min = 0.0;
   hipStream_t stream = nullptr;
   bool captured = false;  // an iteration graph exists
@@ -2447,6 +2454,9 @@ int32_t step_phase(cpl_solver* S, int phase) {
         }
         CK(cpl_kkt_solve(1, B, nw, m, S->M, S->A, S->r1, S->r2s, nullptr, nullptr, S->soc, S->dws, S->dys, nullptr,
                          nullptr, nullptr, S->ws, st));
+        if (S->jreg)
+          CK(kkt_aug_solve(1, B, nw, m, S->M, S->A, S->r1, S->r2s, nullptr, nullptr, S->soc, S->dws, S->dys, nullptr,
+                           S->delta_c, nullptr, S->ws_aug, st));
         CK(cpl_ipm_max_step(B, nw, S->w, S->dws, nullptr, nullptr, S->hasL, S->hasU, S->wl0, S->wu0, S->tau, S->a_soc,
                             st));
         CK(cpl_ipm_trial_point(B, n, nf, nw, S->free64, S->fixed64, S->Xbase, S->w, S->dws, S->a_soc, S->soc, S->st_w,
@@ -2512,6 +2522,9 @@ int32_t step_phase(cpl_solver* S, int phase) {
                                 S->theta_k, S->phi_k, S->act, st));
       CK(cpl_kkt_solve(0, B, nw, m, S->M, S->A, S->r1, S->r2, S->mu_o, S->dwl, S->act, S->dw, S->dy, S->delta_w,
                        S->delta_c, S->info, S->ws, st));
+      if (S->jreg)
+        CK(kkt_aug_solve(0, B, nw, m, S->M, S->A, S->r1, S->r2, S->mu_o, S->dwl, S->act, S->dw, S->dy, S->delta_w,
+                         S->delta_c, S->info, S->ws_aug, st));
       // the step's multipliers / fraction-to-the-boundary, then the search's setup: a launch of their
       // own, or the fused search kernel's prologue
       LsSetupArgs ls;
@@ -2985,6 +2998,7 @@ void cpl_solve_options_default(cpl_solve_options* o) {
   o->fd_step = 1e-6;
   o->fallback_viol_tol = 0.0;  // off: IPOPT returns its last iterate
   o->nlp_scaling = 1;          // IPOPT's default nlp_scaling_method gradient-based
+  o->jacobian_regularization = 0;  // R's pivots (the restatements' default); 1: IPOPT's (2,2) block
 }
 
 int32_t cpl_solver_destroy(cpl_solver* S) {
@@ -3049,7 +3063,7 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   if (o) opt = *o;
   if (opt.hessian < CPL_HESSIAN_EXACT || opt.hessian > CPL_HESSIAN_FD || opt.max_iter < 0 || opt.max_soc < 0 ||
       opt.max_ls < 0 || !(opt.tol > 0.0) || opt.ls_kernel < 0 || opt.ls_kernel > 2 || opt.nlp_scaling < 0 ||
-      opt.nlp_scaling > 1)
+      opt.nlp_scaling > 1 || opt.jacobian_regularization < 0 || opt.jacobian_regularization > 1)
     return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_solver_create: bad options");
   int32_t n, m, nnz;
   CK(cpl_dims(d, &n, &m, &nnz));
@@ -3144,7 +3158,14 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   S->opt = opt;
   S->B = batch;
   S->n = n; S->m = m; S->nnz = nnz; S->nnz_rec = nnz_rec; S->nf = nf; S->nI = nI; S->nw = nw; S->nbounds = nbounds;
-  S->ls_fusable = kkt_wave_size(nw, m);
+  S->jreg = opt.jacobian_regularization == 1;
+  if (S->jreg && kkt_aug_workspace_doubles(nw, m) < 0) {
+    delete S;
+    return fail(CPL_ERR_UNSUPPORTED, "cpl_solver_create: jacobian_regularization needs nw + m <= 128");
+  }
+  // (regularised: the second-order corrections re-solve through cpl_kkt_solve + the augmented kernel,
+  // not inside the fused search kernel, whose re-solve knows the one-wave factors only)
+  S->ls_fusable = kkt_wave_size(nw, m) && !S->jreg;
   S->mu_min = ipm_mu_min(opt.tol);
   S->bfgs = opt.hessian == CPL_HESSIAN_LIMITED_MEMORY;
   S->analytic_H = opt.hessian == CPL_HESSIAN_EXACT && cpl_lagrangian_hessian(d, 0, nullptr, nullptr, nullptr, nullptr,
@@ -3212,7 +3233,8 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
   S->phi_k = a.take<double>(Bz); S->dw = a.take<double>(Bz * nw); S->dy = a.take<double>(Bz * m);
   S->delta_w = a.take<double>(Bz); S->delta_c = a.take<double>(Bz); S->dzL = a.take<double>(Bz * nw);
   S->dzU = a.take<double>(Bz * nw); S->a_max = a.take<double>(Bz); S->a_z = a.take<double>(Bz);
-  S->gd = a.take<double>(Bz); S->ws = a.take<double>(Bz * kws); S->info = a.take<int32_t>(Bz);
+  S->gd = a.take<double>(Bz); S->ws = a.take<double>(Bz * kws);
+  S->ws_aug = a.take<double>(S->jreg ? Bz * (size_t)kkt_aug_workspace_doubles(nw, m) : 0); S->info = a.take<int32_t>(Bz);
   S->a_min = a.take<double>(Bz); S->a_soft = a.take<double>(Bz); S->cs_tmp = a.take<double>(Bz * m);
   S->scr1 = a.take<double>(2 * Bz); S->scr2 = a.take<double>(Bz * m);
   S->act = a.take<uint8_t>(Bz); S->switch_ok = a.take<uint8_t>(Bz); S->searching = a.take<uint8_t>(Bz);
@@ -3351,6 +3373,9 @@ int32_t cpl_solver_solve(cpl_solver* S, const double* d_x0, const double* d_mass
   CK(cpl_ipm_dense_a(B, m, nw, nf, S->nnz_rec, S->amap, S->row_slack, S->J, S->A, nullptr, st));
   CK(cpl_kkt_solve(0, B, nw, m, S->M, S->A, S->r1, S->r2, S->mu, S->zeros_B, nullptr, S->dw, S->dy, S->delta_w,
                    S->delta_c, S->info, S->ws, st));
+  if (S->jreg)
+    CK(kkt_aug_solve(0, B, nw, m, S->M, S->A, S->r1, S->r2, S->mu, S->zeros_B, nullptr, S->dw, S->dy, S->delta_w,
+                     S->delta_c, S->info, S->ws_aug, st));
   hipLaunchKernelGGL(k_y0, dim3(blocks_for(B)), dim3(256), 0, st, B, m, S->dy, S->info, S->y);
   LAUNCHED("k_y0");
   if (S->bfgs) {  // model initialised to init_val I (IPOPT's limited_memory_init_val = 1)

@@ -97,6 +97,9 @@ class CentroidalPlanner:
         self.solver_tol = 1e-8
         self.solver_max_iter = 3000
         self.solver_hessian = "limited-memory"
+        # a rank-deficient constraint Jacobian: "pivot" (the engine's default, delta_c on R's small
+        # pivots) or "ipopt" (IPOPT's (2,2)-block regularisation, cpl_solve_options.jacobian_regularization)
+        self.solver_jacobian_regularization = "pivot"
         # src/CentroidalPlanner.cpp:26 SetOption("derivative_test", "first-order"): IPOPT checks the
         # first derivatives at the start point of every solve; the report lands here
         self.solver_derivative_test = "first-order"
@@ -105,7 +108,7 @@ class CentroidalPlanner:
     # ---- Solve (src/CentroidalPlanner.cpp:22-34) ------------------------------------------
     def Solve(self) -> Solution:
         res = solve(self._cpl_problem, evaluator=self.evaluator, tol=self.solver_tol, max_iter=self.solver_max_iter,
-                    hessian=self.solver_hessian,
+                    hessian=self.solver_hessian, jacobian_regularization=self.solver_jacobian_regularization,
                     derivative_test=self.solver_derivative_test if self.evaluator is None else "none")
         self.last_derivative_report = res.derivative_report
         sol = self._cpl_problem.GetSolution()

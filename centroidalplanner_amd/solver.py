@@ -61,11 +61,13 @@ class _HostBatchEvaluator:
 
 
 def solve(problem, evaluator=None, x0: Optional[np.ndarray] = None, tol: float = 1e-8, max_iter: int = 3000,
-          hessian: str = "limited-memory", derivative_test: str = "none") -> SolveResult:
+          hessian: str = "limited-memory", derivative_test: str = "none",
+          jacobian_regularization: str = "pivot") -> SolveResult:
     """One instance through the batched solve loop.  hessian: "limited-memory" (IFOPT's default, as
     the reference runs) or "exact" (the analytic Lagrangian Hessian).  derivative_test:
     "first-order" runs IPOPT's first-order derivative checker at the start point first, as the
-    reference's solver option does (src/CentroidalPlanner.cpp:26); its report is returned."""
+    reference's solver option does (src/CentroidalPlanner.cpp:26); its report is returned.
+    jacobian_regularization: "pivot" (default) or "ipopt" (batch_ipm_solve's option)."""
     if derivative_test not in ("none", "first-order"):
         raise ValueError(f"derivative_test must be 'none' or 'first-order', not {derivative_test!r}")
     import torch
@@ -79,10 +81,12 @@ def solve(problem, evaluator=None, x0: Optional[np.ndarray] = None, tol: float =
         X0 = torch.as_tensor(x0[None], device=torch.device("cuda", torch.cuda.current_device()))
         if derivative_test == "first-order":
             report = problem.derivative_test(X0)
-        r = batch_ipm_solve(problem, X0, None, tol=tol, max_iter=max_iter, hessian=hessian)
+        r = batch_ipm_solve(problem, X0, None, tol=tol, max_iter=max_iter, hessian=hessian,
+                            jacobian_regularization=jacobian_regularization)
     else:
         r = batch_ipm_solve(problem, torch.as_tensor(x0[None]), None, evaluator=_HostBatchEvaluator(evaluator),
-                            tol=tol, max_iter=max_iter, hessian=hessian)
+                            tol=tol, max_iter=max_iter, hessian=hessian,
+                            jacobian_regularization=jacobian_regularization)
     # the NaN Jacobian entries the solve's own start-point evaluation met (cpl_solver_nan_jacobian)
     nan0 = int(r.nan_jacobian[0])
     if nan0:

@@ -535,6 +535,14 @@ typedef struct cpl_solve_options {
                               (gradients over the free variables, a NaN entry counting as 0).  The
                               iteration and its tolerances run on the scaled problem; x is unscaled, the
                               returned multipliers are the unscaled ones (dc y / df).  0: no scaling. */
+  int32_t jacobian_regularization; /* a rank-deficient constraint Jacobian (|R_jj| < 1e-10 |R|max in the QR
+                              of A^T): 0 (default) — delta_c = 1e-8 mu^0.25 |R|max added to R's small
+                              pivots (the three restatements' treatment); 1 — IPOPT's: the (2,2) block
+                              [[W + dW I, A^T], [A, -delta_c I]], delta_c = 1e-8 mu^0.25
+                              (jacobian_regularization_value / _exponent), solved as the augmented system
+                              in (dw, s) with A~ = [A, -sqrt(delta_c) I] on the workgroup KKT kernel;
+                              needs nw + m <= 128.  The restatements carry the same option
+                              (oracle cplo_set_jac_reg, batch_ipm_solve(jacobian_regularization="ipopt")). */
 } cpl_solve_options;
 
 typedef struct cpl_solver cpl_solver;

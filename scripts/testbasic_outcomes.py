@@ -5,7 +5,8 @@ callbacks) the outcome, the iteration count, whether the best-feasible fallback 
 Jacobian entries at the start, the returned point's TestBasic quantities (force / torque balance
 errors, worst cone value) and the wall time.  One JSON line per run.
 
-usage: python scripts/testbasic_outcomes.py [gpu|oracle|both] > out.jsonl
+usage: python scripts/testbasic_outcomes.py [gpu|oracle|both] [pivot|ipopt] > out.jsonl
+(the second argument: the facade's solver_jacobian_regularization, default pivot)
 """
 import json
 import os
@@ -78,8 +79,10 @@ class _Oracle:
         return self.po.eval_batch(self.prob.desc(), np.atleast_2d(X), outputs=("g", "jac", "f", "grad"), nthreads=1)
 
 
-def run(name, make, backend):
+def run(name, make, backend, jac_reg="pivot"):
     cpl, wrench, mu = make()
+    inner = getattr(cpl, "_cp", cpl)  # (CoMPlanner wraps a CentroidalPlanner)
+    inner.solver_jacobian_regularization = jac_reg
     if backend == "oracle":
         cpl.evaluator = _Oracle(cpl.GetCplProblem())
     t0 = time.perf_counter()
@@ -94,7 +97,7 @@ def run(name, make, backend):
         T_sum += np.cross(v.position_value - sol.com_sol, F)
         cone = max(cone, float(-F.dot(n)), float(np.linalg.norm(F - n.dot(F) * n) - mu * F.dot(n)))
     fb = F_sum - np.array([wrench[0], wrench[1], -MASS * G + wrench[2]])
-    return {"scenario": name, "backend": backend, "status": sol.message, "iterations": sol.iterations,
+    return {"scenario": name, "backend": backend, "jacobian_regularization": jac_reg, "status": sol.message, "iterations": sol.iterations,
             "fallback": bool(sol.fallback), "nan_jacobian_at_start": int(sol.nan_jacobian_at_start),
             "force_balance_err": float(np.abs(fb).max()), "torque_balance_err": float(np.abs(T_sum - wrench[3:]).max()),
             "worst_cone_value": cone, "seconds": dt}
@@ -103,10 +106,11 @@ def run(name, make, backend):
 def main():
     which = sys.argv[1] if len(sys.argv) > 1 else "gpu"
     backends = ["gpu", "oracle"] if which == "both" else [which]
+    jac_reg = sys.argv[2] if len(sys.argv) > 2 else "pivot"
     for backend in backends:
         for name, make in (("testSimpleProblem", simple), ("testGroundEnv", ground),
                            ("testSuperquadricEnv", superquadric), ("testCoMPlanner", com_planner)):
-            print(json.dumps(run(name, make, backend)), flush=True)
+            print(json.dumps(run(name, make, backend, jac_reg)), flush=True)
 
 
 if __name__ == "__main__":
