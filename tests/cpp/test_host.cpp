@@ -340,6 +340,23 @@ static void test_testbasic_native() {
     }
     NEAR(Fz, -mass * g, 1e-6);
   }
+  {  // the same with IPOPT's Jacobian regularisation (SolveOptions::jacobian_regularization = 1): every
+     // Newton system here is rank deficient; the regularised form converges
+    auto ground = std::make_shared<env::Ground>();
+    ground->SetGroundZ(0.1);
+    CentroidalPlanner cpl({"contact1"}, mass, ground);
+    solver::SolveOptions opt;
+    opt.jacobian_regularization = 1;
+    auto ns = std::make_shared<solver::NativeSolver>(opt);
+    cpl.SetSolver(ns);
+    solver::Solution sol = cpl.Solve();
+    std::printf("testSimpleProblem (IPOPT's Jacobian regularisation): status %d after %d iterations\n", ns->status(),
+                ns->iterations());
+    CHECK(ns->status() == CPL_SOLVE_OPTIMAL && ns->iterations() <= 20);
+    double Fz = 0.0;
+    for (const auto& e : sol.contact_values_map) Fz += e.second.force_value[2];
+    NEAR(Fz, -mass * g, 1e-6);
+  }
   const std::vector<double> wrench = {100, 0, 0, 0, 0, 100};
   {  // testGroundEnv (TestBasic.cpp:64-135): ends at the iteration limit (the unloaded contacts' cone
      // apex); the returned point is checked, as TestBasic does
