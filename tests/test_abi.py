@@ -148,3 +148,21 @@ def test_kkt_qd_solve_rejects_what_does_not_fit_before_launch(nw, m, ok):
         assert rc in (_abi.ERR_UNSUPPORTED, _abi.ERR_INVALID_ARGUMENT)
         if m <= nw:
             assert rc == _abi.ERR_UNSUPPORTED and "LDS" in _abi.lib.cpl_last_error().decode()
+
+
+def test_solver_rejects_bad_jacobian_regularization_before_any_gpu_call():
+    """cpl_solve_options.jacobian_regularization: 0 / 1 only (CPL_ERR_INVALID_ARGUMENT otherwise), and
+    IPOPT's form needs the augmented system (nw + m unknowns) to fit the workgroup KKT kernel (<= 128):
+    the 8-contact problem's does not — CPL_ERR_UNSUPPORTED, checked before the solver touches the GPU."""
+    from centroidalplanner_amd.workload import solve_problem
+
+    for nc, jr, want in ((4, 2, _abi.ERR_INVALID_ARGUMENT), (8, 1, _abi.ERR_UNSUPPORTED)):
+        prob = solve_problem(nc).GetCplProblem()
+        o = _abi.SolveOptions()
+        _abi.lib.cpl_solve_options_default(ctypes.byref(o))
+        assert o.jacobian_regularization == 0
+        o.jacobian_regularization = jr
+        h = ctypes.c_void_p()
+        d = prob.desc()
+        assert _abi.lib.cpl_solver_create(ctypes.byref(d), 4, ctypes.byref(o), ctypes.byref(h)) == want
+        assert not h.value
