@@ -89,6 +89,8 @@ def parse():
     ap.add_argument("--no-check", action="store_true", help="skip the checker leg")
     ap.add_argument("--check-sample", type=int, default=4096, help="instances in the checker leg's strided sample")
     ap.add_argument("--no-graph", action="store_true", help="launch each step from Python instead of a HIP graph")
+    ap.add_argument("--collective-always", action="store_true",
+                    help="tests: the RCCL process group and the bucketed norms all-gather even at one rank")
     ap.add_argument("--bucket", type=int, default=10,
                     help="steps per HIP-graph replay and per residual-norm all-gather (1 = per step)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -970,7 +972,8 @@ def main():
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
+    dist_on = world > 1 or args.collective_always  # (the latter: the RCCL path exercised on one GPU)
+    if dist_on:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
     from centroidalplanner_amd import _abi
@@ -1006,7 +1009,7 @@ def main():
 
     # the bucketed step loop with its asynchronous all-gather (distributed.BucketedNormGather: the
     # same code the gloo world-2 tests drive on the CPU)
-    runner = BucketedNormGather(world, S, dev, launch, stream=stream)
+    runner = BucketedNormGather(world, S, dev, launch, stream=stream, gather_always=dist_on)
     norms = runner.norms
     sizes = sorted(set(runner.sizes(K) + runner.sizes(W)))
     with torch.cuda.stream(stream):  # warm the launch path (per-stream workspaces) before capture
@@ -1030,7 +1033,7 @@ def main():
             w.wait()
     torch.cuda.synchronize()
     runner.reset()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -1039,12 +1042,12 @@ def main():
         if w is not None:
             w.wait()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     total_batch = batch
-    if world > 1:
+    if dist_on:
         tdt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tdt, op=dist.ReduceOp.MAX)
         dt = float(tdt.item())
@@ -1225,7 +1228,7 @@ def main():
             res["configs4_solve5_lbfgs"] = solve5
         print(json.dumps(res), flush=True)
 
-    if world > 1:
+    if dist_on:
         dist.barrier()  # every rank leaves together (rank 0 ran the checker leg after the timing)
         dist.destroy_process_group()
 

@@ -60,12 +60,15 @@ class BucketedNormGather:
     rows the collective is still reading.
 
     launch(rows, count): writes rows[:count] (a [bucket, 2] float64 tensor); ``replay`` (optional,
-    {(buffer, count): callable}) replaces launch with captured graphs of the same work."""
+    {(buffer, count): callable}) replaces launch with captured graphs of the same work.
+    ``gather_always``: gather at one rank too (a one-rank process group: the RCCL path on one GPU)."""
 
-    def __init__(self, world: int, bucket: int, device, launch, stream=None, replay=None, group=None):
+    def __init__(self, world: int, bucket: int, device, launch, stream=None, replay=None, group=None,
+                 gather_always: bool = False):
         import torch
 
         self.world, self.bucket, self.group = int(world), max(1, int(bucket)), group
+        self.gather = self.world > 1 or bool(gather_always)
         self.launch, self.stream, self.replay = launch, stream, replay or {}
         self.norms = [torch.zeros(self.bucket, 2, dtype=torch.float64, device=device) for _ in range(2)]
         self.pending = [None, None]
@@ -95,7 +98,7 @@ class BucketedNormGather:
                 fn()
             else:
                 self.launch(self.norms[j], count)
-            if self.world > 1:
+            if self.gather:
                 out, work = all_gather_norms(self.norms[j][:count], group=self.group, async_op=True)
                 self.pending[j] = work
                 self.gathered.append((out, count))

@@ -117,3 +117,38 @@ def test_beyond_int32_offsets():
     it = torch.as_tensor(idx, device=dev)
     assert np.array_equal(out["jac"][it].cpu().numpy(), ref["jac"])
     assert np.array_equal(out["g"][it].cpu().numpy(), ref["g"])
+
+
+@pytest.mark.gpu
+def test_bench_rccl_gather_path_on_one_gpu():
+    """The multi-rank bench's collective path on real hardware with the one GPU a box has: a one-rank
+    RCCL ("nccl") process group under torch.distributed.run, the bucketed asynchronous all-gather of
+    the residual norms issued every bucket (`--collective-always`), the barriers and the max-over-ranks
+    reduction — the calls an 8-GPU run makes, minus the peers.  The gathered rows must be the norms the
+    rank computed, and the line must still be one JSON line."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"), "--gpus", "1", "--collective-always",
+           "--config", "ground4", "--batch", "65536", "--steps", "23", "--warmup", "3", "--bucket", "5", "--no-pmc",
+           "--no-cpu", "--no-side", "--no-check"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    ln = json.loads(lines[0])
+    g = ln["residual_gather"]
+    assert ln["n_gpus"] == 1 and ln["steps"] == 23 and g is not None
+    assert g["steps_in_last_bucket"] == 3 and g["local_rows_match"]
+    mx, ss = g["last_step_global_norms"]
+    assert mx >= 0.0 and ss >= 0.0
