@@ -11,7 +11,8 @@
 // has full row rank and the reduced Hessian Z^T M Z is positive definite, so the Cholesky of the
 // reduced Hessian is the inertia test (pivots at the rounding level eps max|M_ii| count as zero) and dW follows IPOPT's schedule (first trial 1e-4, or
 // dW_last / 3; growth x100 without history, x8 with) until it succeeds; a rank-deficient A (|R_jj|
-// tiny) gets dC = 1e-8 mu^(1/4) |R|max on R's diagonal (IPOPT's jacobian_regularization_value).
+// tiny) gets dC = 1e-8 mu^(1/4) |R|max on R's diagonal — or, opt-in (cpl_kkt_aug_kernel below), IPOPT's
+// own (2,2)-block regularisation with jacobian_regularization_value 1e-8 mu^(1/4).
 // One step of iterative refinement against the unregularised system follows when dC = 0.
 // The factors are kept in a per-instance workspace so second-order corrections re-solve with
 // another r2 without refactorising (mode 1).
