@@ -206,7 +206,7 @@ __device__ __forceinline__ void kkt_block(int mode, int nw_arg, int m_arg, int n
                                           const double* __restrict__ q2, const double* mub, const double* lastb,
                                           double* __restrict__ dwo, double* __restrict__ dyo, double* dWo,
                                           double* dCo, int32_t* infob, double* __restrict__ wsb, double* Pzg,
-                                          double* sm, KktShared& sh) {
+                                          double* rscr, double* sm, KktShared& sh) {
   const int nw = NW > 0 ? NW : nw_arg;
   const int m = NW > 0 ? MM : m_arg;
   const int tid = threadIdx.x;
@@ -230,6 +230,33 @@ __device__ __forceinline__ void kkt_block(int mode, int nw_arg, int m_arg, int n
     if (tid == 0) { sh.delta_w = wsb[per - 4]; sh.delta_c = wsb[per - 3]; }
     __syncthreads();
     kkt_solve_lds(nw, m, nw0, Q, QR, L, M, sh.delta_w, q1, q2, dw, dy, tmp);
+    if (rscr) {  // (the augmented system) one step of iterative refinement, as its factorisation's, with
+                 // the residual and correction in rscr: wsb holds the kept factors
+      const double dW = sh.delta_w;
+      double* f1 = rscr;
+      double* f2 = f1 + nw;
+      double* h1 = f2 + m;
+      double* h2 = h1 + nw;
+      group_dots<4>(nw, m, Ab, 1, nw, dy, 1, [&](int r, double d) { f1[r] = q1[r] - (r < nw0 ? dW * dw[r] : 0.0) - d; });
+      group_dots<4>(nw, nw, M, nw, 1, dw, 1, [&](int r, double d) { f1[r] -= d; });
+      group_dots<4>(m, nw, Ab, nw, 1, dw, 1, [&](int k, double d) { f2[k] = q2[k] - d; });
+      __syncthreads();
+      if (tid < 64) {
+        double rmax = 0.0, qmax = 0.0;
+        for (int r = tid; r < nw; r += 64) { rmax = fmax(rmax, fabs(f1[r])); qmax = fmax(qmax, fabs(q1[r])); }
+        for (int k = tid; k < m; k += 64) { rmax = fmax(rmax, fabs(f2[k])); qmax = fmax(qmax, fabs(q2[k])); }
+        rmax = wave_max(rmax);
+        qmax = wave_max(qmax);
+        if (tid == 0) sh.flag = !(rmax <= 1e-13 * qmax);
+      }
+      __syncthreads();
+      if (sh.flag) {
+        kkt_solve_lds(nw, m, nw0, Q, QR, L, M, dW, f1, f2, h1, h2, tmp);
+        for (int r = tid; r < nw; r += KKT_THREADS) dw[r] += h1[r];
+        for (int k = tid; k < m; k += KKT_THREADS) dy[k] += h2[k];
+        __syncthreads();
+      }
+    }
     for (int i = tid; i < nw0; i += KKT_THREADS) dwo[i] = dw[i];
     for (int i = tid; i < m; i += KKT_THREADS) dyo[i] = dy[i];
     return;
@@ -629,7 +656,7 @@ __global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 
   kkt_block<NW, MM>(mode, nw, m, nw, Mg + b * nw * nw, Ag + b * m * nw, r1g + b * nw, r2g + b * m,
                     mug ? mug + b : nullptr, dw_last ? dw_last + b : nullptr, dwg + b * nw, dyg + b * m,
                     dWg ? dWg + b : nullptr, dCg ? dCg + b : nullptr, info ? info + b : nullptr,
-                    ws + b * kkt_ws_per(nw, m), nullptr, sm, sh);
+                    ws + b * kkt_ws_per(nw, m), nullptr, nullptr, sm, sh);
 }
 
 // IPOPT's regularisation of a rank-deficient Jacobian (cpl_solve_options.jacobian_regularization;
@@ -641,11 +668,12 @@ __global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 
 // Launched after the factorisation kernel of the same call (either kernel marks a rank-deficient
 // system by its delta_c != 0, its R-pivot treatment): the marked systems only, mode 0 re-factorising
 // them in the augmented form and overwriting dw, dy, delta_w (delta_c := IPOPT's), mode 1 re-solving
-// with the augmented factors.  Workspace per system (kkt_aug_ws_per): the augmented factors | W~ | A~ |
-// [q1; 0] | Pz.
+// with the augmented factors (and, like the factorisation, one step of iterative refinement — the
+// restatements refine every full-rank re-solve).  Workspace per system (kkt_aug_ws_per): the augmented
+// factors | W~ | A~ | [q1; 0] | Pz | the re-solve's refinement residual and correction.
 __host__ __device__ inline int64_t kkt_aug_ws_per(int nw, int m) {
   const int na = nw + m;
-  return kkt_ws_per(na, m) + (int64_t)na * na + (int64_t)m * na + na + (int64_t)nw * nw;
+  return kkt_ws_per(na, m) + (int64_t)na * na + (int64_t)m * na + na + (int64_t)nw * nw + 2 * (int64_t)(na + m);
 }
 
 __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_aug_kernel(
@@ -664,6 +692,7 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_aug_kernel(
   double* Aa = Ma + (int64_t)na * na;
   double* q1a = Aa + (int64_t)m * na;
   double* Pz = q1a + na;
+  double* rscr = Pz + (int64_t)nw * nw;
   if (mode == 0) {
     const double* M = Mg + b * nw * nw;
     const double* A = Ag + b * m * nw;
@@ -681,7 +710,7 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_aug_kernel(
   __syncthreads();
   kkt_block<0, 0>(mode, na, m, nw, Ma, Aa, q1a, r2g + b * m, mug ? mug + b : nullptr,
                   dw_last ? dw_last + b : nullptr, dwg + b * nw, dyg + b * m, dWg ? dWg + b : nullptr, dCg + b,
-                  info ? info + b : nullptr, wsb, Pz, sm, sh);
+                  info ? info + b : nullptr, wsb, Pz, mode == 1 ? rscr : nullptr, sm, sh);
   if (mode == 0 && tid == 0) dCg[b] = 1e-8 * pow(mug[b], 0.25);  // (stays != 0: the mark for mode 1)
 }
 
