@@ -43,4 +43,5 @@ step 300 bash -c "python -u bench.py --config solve5 --hessian limited-memory > 
 step 300 bash -c "python -u bench.py --config solve5 > $out/bench_solve5_exact.json 2> $out/bench_solve5_exact.err"
 step 300 bash -c "python -u scripts/solve_latency.py --reps 10 > $out/solve_latency.json 2> $out/solve_latency.err"
 step 300 bash -c "python -u scripts/testbasic_outcomes.py gpu > $out/testbasic_gpu.jsonl 2> $out/testbasic_gpu.err"
+step 300 bash -c "python -u scripts/testbasic_outcomes.py gpu ipopt > $out/testbasic_gpu_ipopt.jsonl 2> $out/testbasic_gpu_ipopt.err"
 echo done
