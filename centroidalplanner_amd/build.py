@@ -18,7 +18,8 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libcpl_mi355x.so")
 
 SOURCES = ["cpl_host.cpp", "cpl_kernels.hip", "cpl_kkt.hip", "cpl_ipm.hip", "cpl_solver.hip", "cpl_check.hip"]
-HEADERS = ["cpl_layout.hpp", "cpl_status.hpp", "cpl_wave.hpp"]
+HEADERS = ["cpl_layout.hpp", "cpl_status.hpp", "cpl_wave.hpp", "cpl_accept.hpp", "cpl_kkt_block.hpp", "cpl_kkt_qd.hpp",
+           "cpl_kkt_wave.hpp"]
 
 HIPCC_FLAGS = [
     "--offload-arch=gfx950",

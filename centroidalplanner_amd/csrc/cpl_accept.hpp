@@ -224,6 +224,15 @@ struct LsBacktrackArgs {
   // dc[b, r] (the scaled problem's values, as the solver's k_apply_scaling); nullptr: unscaled
   const double* df = nullptr;
   const double* dc = nullptr;
+  // IPOPT's Jacobian regularisation (cpl_solve_options.jacobian_regularization): a system whose
+  // factorisation marked it rank deficient (aug_dc[b] != 0) re-solves its corrections with the augmented
+  // factors cpl_kkt_aug_kernel kept in aug_ws (cpl_kkt_block.hpp kkt_aug_resolve_wave); nullptr: off
+  const double* aug_dc = nullptr;
+  double* aug_ws = nullptr;
+  // which instances this launch searches (set by ls_backtrack): 0 all; 1 the unmarked (aug_dc == 0),
+  // 2 the marked — large batches run the two in separate instantiations (the default one keeps its
+  // occupancy), small ones all in the AUGR one
+  int32_t aug_sel = 0;
 };
 
 // s + sum_{r < m} a[r * stride] * v[r], accumulated in r order exactly as the plain loop

@@ -33,6 +33,7 @@
 #include <vector>
 
 #include "cpl_accept.hpp"
+#include "cpl_kkt_block.hpp"
 #include "cpl_kkt_wave.hpp"
 #include "cpl_layout.hpp"
 #include "cpl_wave.hpp"
@@ -3271,13 +3272,17 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
 // back per trial cost ~55 us each; the lock-step batch makes as many trials as its slowest instance).
 // GF (with FIRST): the second-order corrections' re-solves read the KKT factors from the workspace in
 // global memory (kkt_wave_resolve_gg) — large batches, where the factors' LDS image bounded the waves
-// per CU; small batches keep the LDS copy (their re-solve latency is the iteration's)
-template <int ENVK, bool RESTO, bool FIRST, bool GF = false>
+// per CU; small batches keep the LDS copy (their re-solve latency is the iteration's).
+// AUGR (with FIRST; IPOPT's Jacobian regularisation on): a system marked rank deficient re-solves its
+// corrections with the augmented factors (kkt_aug_resolve_wave) — its own instantiation, because the
+// call raises the kernel's registers past two waves per SIMD; the default search keeps its occupancy
+template <int ENVK, bool RESTO, bool FIRST, bool GF = false, bool AUGR = false>
 __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, const LsBacktrackArgs A) {
   extern __shared__ __align__(16) double smem[];
   __shared__ double s_f;
   const int64_t b = blockIdx.x;
   if (b >= A.batch) return;
+  if (FIRST && A.aug_sel != 0 && (A.aug_sel == 1) == (A.aug_dc[b] != 0.0)) return;  // (the other launch's)
   const int lane = threadIdx.x;
   if (FIRST && !GF && A.with_post) {  // the post-step quantities and the search's setup of this instance
     ipm_post_step_one(A.post, b, A.setup);
@@ -3423,7 +3428,11 @@ __global__ __launch_bounds__(64) void cpl_ls_backtrack_kernel(const KParams K, c
       if (FIRST && !RESTO && stage == S_SOC) {
         if (q > 0 && lane < m) csoc = a_soc * csoc + cons();
         double dwv, dyv;
-        if (GF)
+        if (AUGR && A.aug_dc[b] != 0.0) {  // a regularised (augmented) system
+          const Dd r = kkt_aug_resolve_wave(KNW, KM, A.aug_ws + b * kkt_aug_ws_per(KNW, KM), lane < KM ? -csoc : 0.0);
+          dwv = r.a;
+          dyv = r.b;
+        } else if (GF)
           kkt_wave_resolve_gg<KNW, KM>(A.M + b * KNW * KNW, A.kkt_ws + b * kkt_ws_per(KNW, KM),
                                        lane < KNW ? A.r1[b * KNW + lane] : 0.0, lane < KM ? -csoc : 0.0, kk, &dwv,
                                        &dyv);
@@ -3528,16 +3537,26 @@ int32_t ls_backtrack(const cpl_problem_desc* d, const LsBacktrackArgs& a, hipStr
     lds = sizeof(double) * ((((size_t)a.n + a.m + 2 * (size_t)a.nw + nL + 1) & ~(size_t)1) +
                             (gf ? 2 * 47 : KktWave<47, 30>::LDS));
   using KernT = void (*)(const KParams, const LsBacktrackArgs);
-#define CPL_LS_KERNELS(R, F, G)                                                                                \
-  {cpl_ls_backtrack_kernel<CPL_ENV_NONE, R, F, G>, cpl_ls_backtrack_kernel<CPL_ENV_GROUND, R, F, G>,           \
-   cpl_ls_backtrack_kernel<CPL_ENV_SUPERQUADRIC, R, F, G>, cpl_ls_backtrack_kernel<CPL_ENV_MIXED, R, F, G>}
-  static const KernT table[4][4] = {CPL_LS_KERNELS(false, false, false), CPL_LS_KERNELS(true, false, false),
-                                    CPL_LS_KERNELS(false, true, false), CPL_LS_KERNELS(false, true, true)};
+#define CPL_LS_KERNELS(R, F, G, AG)                                                                            \
+  {cpl_ls_backtrack_kernel<CPL_ENV_NONE, R, F, G, AG>, cpl_ls_backtrack_kernel<CPL_ENV_GROUND, R, F, G, AG>,   \
+   cpl_ls_backtrack_kernel<CPL_ENV_SUPERQUADRIC, R, F, G, AG>, cpl_ls_backtrack_kernel<CPL_ENV_MIXED, R, F, G, AG>}
+  static const KernT table[6][4] = {CPL_LS_KERNELS(false, false, false, false), CPL_LS_KERNELS(true, false, false, false),
+                                    CPL_LS_KERNELS(false, true, false, false), CPL_LS_KERNELS(false, true, true, false),
+                                    CPL_LS_KERNELS(false, true, false, true), CPL_LS_KERNELS(false, true, true, true)};
 #undef CPL_LS_KERNELS
+  const bool augr = first && a.aug_ws && a.aug_dc;
   if (a.resto && (!a.pR || !a.nR || !a.dp || !a.dn || !a.wR || !a.st_p || !a.st_n))
     return fail(CPL_ERR_INVALID_ARGUMENT, "ls_backtrack: restoration search without its buffers");
-  hipLaunchKernelGGL(table[first ? (gf ? 3 : 2) : (a.resto ? 1 : 0)][K.env_kind], dim3((unsigned)a.batch), dim3(64), lds,
-                     stream, K, a);
+  if (augr && gf) {  // large batches: the unmarked instances in the default instantiation, the marked in AUGR
+    LsBacktrackArgs a1 = a, a2 = a;
+    a1.aug_sel = 1;
+    a2.aug_sel = 2;
+    hipLaunchKernelGGL(table[3][K.env_kind], dim3((unsigned)a.batch), dim3(64), lds, stream, K, a1);
+    hipLaunchKernelGGL(table[5][K.env_kind], dim3((unsigned)a.batch), dim3(64), lds, stream, K, a2);
+  } else {
+    hipLaunchKernelGGL(table[first ? (gf ? 3 : 2) + (augr ? 2 : 0) : (a.resto ? 1 : 0)][K.env_kind],
+                       dim3((unsigned)a.batch), dim3(64), lds, stream, K, a);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "cpl_ls_backtrack_kernel launch");
   return CPL_OK;

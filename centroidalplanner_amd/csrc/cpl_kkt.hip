@@ -33,6 +33,7 @@
 #include "cpl_wave.hpp"
 #include "cpl_kkt_wave.hpp"
 #include "cpl_kkt_qd.hpp"
+#include "cpl_kkt_block.hpp"
 
 namespace cpl {
 
@@ -49,8 +50,6 @@ __device__ long long* g_kkt_prof;
   } while (0)
 #endif
 
-constexpr int KKT_THREADS = 256;
-constexpr int KKT_MAX_NW = 128;
 
 
 struct KktShared {
@@ -85,91 +84,6 @@ __device__ __forceinline__ double glb_dot(const double* a, int sa, const double*
   for (; k < len; ++k) s[0] += a[k * sa] * b[k * sb];
   return ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
 }
-
-// Dot products of n strided vectors with one shared operand, G lanes per vector (G | 64): lane
-// `part` of a group sums k = part, part + G, ... and the group reduces with log2(G) xor shuffles;
-// fin(r, dot) runs on the group's first lane.  Every thread of the workgroup must call it (the
-// shuffles run on all lanes; groups never straddle a wave).  Row r of A starts at A + r * sr, its
-// k-th element at stride sk.
-template <int G, class F>
-__device__ __forceinline__ void group_dots(int n, int len, const double* A, int sr, int sk, const double* x, int sx,
-                                           F fin) {
-  const int part = threadIdx.x % G;
-  for (int base = 0; base < n * G; base += KKT_THREADS) {
-    const int r = (base + (int)threadIdx.x) / G;
-    const bool act = r < n;
-    double s0 = 0.0, s1 = 0.0;
-    if (act) {
-      const double* a = A + (int64_t)r * sr;
-      int k = part;
-      for (; k + G < len; k += 2 * G) {
-        const double p0 = a[k * sk], p1 = a[(k + G) * sk];
-        s0 += p0 * x[k * sx];
-        s1 += p1 * x[(k + G) * sx];
-      }
-      if (k < len) s0 += a[k * sk] * x[k * sx];
-    }
-    double s = s0 + s1;
-    if constexpr (G == 4) {
-      s = group4_sum(s);
-    } else if constexpr (G == 8) {
-      s = group8_sum(s);
-    } else {
-#pragma unroll
-      for (int o = 1; o < G; o <<= 1) s += __shfl_xor(s, o);
-    }
-    if (act && part == 0) fin(r, s);
-  }
-}
-
-
-// Solve with the factors in LDS: Q [nw][nw] (row-major: Q[r*nw + c]), QR array (row j = column j of
-// A^T after the reflections; R[i][j] = QR[j*nw + i] for i < j, R[j][j] = QR[j*nw + j]), L [nz][nz] the
-// Cholesky of the reduced Hessian, M [nw][nw] (plus delta_w on the diagonal, applied here).
-// Vectors in LDS: q1 [nw], q2 [m] -> dw [nw], dy [m].  tmp: >= 2*nw doubles.  delta_w acts on the
-// first nw0 unknowns (nw0 = nw but for the augmented system of a regularised Jacobian: its W block).
-__device__ __forceinline__ void kkt_solve_lds(int nw, int m, int nw0, const double* Q, const double* QR,
-                              const double* L, const double* M, double dW, const double* q1, const double* q2,
-                              double* dw, double* dy, double* tmp) {
-  const int tid = threadIdx.x;
-  const int nz = nw - m;
-  double* py = tmp;          // [m]
-  double* t = tmp + nw;      // [nw]
-  // R^T p_y = q2 (forward substitution; (R^T)[i][k] = R[k][i] = QR[i*nw + k])
-  for (int i = tid; i < m; i += KKT_THREADS) py[i] = q2[i];
-  __syncthreads();
-  if (tid < 64) wave_trsv(m, true, QR, nw, 1, QR, nw + 1, py);
-  __syncthreads();
-  // dw <- Y p_y
-  group_dots<4>(nw, m, Q, nw, 1, py, 1, [&](int r, double d) { dw[r] = d; });
-  __syncthreads();
-  // t = q1 - (M + dW I) Y p_y
-  group_dots<4>(nw, nw, M, nw, 1, dw, 1, [&](int r, double d) { t[r] = q1[r] - (r < nw0 ? dW * dw[r] : 0.0) - d; });
-  __syncthreads();
-  if (nz > 0) {
-    // rz = Z^T t into tmp[m .. m+nz) (py still needed) -> p_z by the two triangular solves
-    double* rz = tmp + m;
-    group_dots<4>(nz, nw, Q + m, 1, nw, t, 1, [&](int c, double d) { rz[c] = d; });
-    __syncthreads();
-    if (tid < 64) {
-      wave_trsv(nz, true, L, nz, 1, L, nz + 1, rz);    // L y = rz
-      wave_trsv(nz, false, L, 1, nz, L, nz + 1, rz);   // L^T z = y
-    }
-    __syncthreads();
-    // dw += Z p_z
-    group_dots<4>(nw, nz, Q + m, nw, 1, rz, 1, [&](int r, double d) { dw[r] += d; });
-    __syncthreads();
-  }
-  // u = q1 - (M + dW I) dw  -> s = Y^T u -> R dy = s
-  group_dots<4>(nw, nw, M, nw, 1, dw, 1, [&](int r, double d) { t[r] = q1[r] - (r < nw0 ? dW * dw[r] : 0.0) - d; });
-  __syncthreads();
-  group_dots<4>(m, nw, Q, 1, nw, t, 1, [&](int k, double d) { dy[k] = d; });
-  __syncthreads();
-  // R dy = s (backward substitution; R[i][k] = QR[k*nw + i])
-  if (tid < 64) wave_trsv(m, false, QR, 1, nw, QR, nw + 1, dy);
-  __syncthreads();
-}
-
 
 // LDS layout (doubles): Q | QR | L | dw | dy | tmp(max(2 nw, 3 m)).  M, the right-hand sides and the
 // refinement's residual / correction stay in global memory (L2-resident while the workgroup runs):
@@ -230,33 +144,9 @@ __device__ __forceinline__ void kkt_block(int mode, int nw_arg, int m_arg, int n
     if (tid == 0) { sh.delta_w = wsb[per - 4]; sh.delta_c = wsb[per - 3]; }
     __syncthreads();
     kkt_solve_lds(nw, m, nw0, Q, QR, L, M, sh.delta_w, q1, q2, dw, dy, tmp);
-    if (rscr) {  // (the augmented system) one step of iterative refinement, as its factorisation's, with
-                 // the residual and correction in rscr: wsb holds the kept factors
-      const double dW = sh.delta_w;
-      double* f1 = rscr;
-      double* f2 = f1 + nw;
-      double* h1 = f2 + m;
-      double* h2 = h1 + nw;
-      group_dots<4>(nw, m, Ab, 1, nw, dy, 1, [&](int r, double d) { f1[r] = q1[r] - (r < nw0 ? dW * dw[r] : 0.0) - d; });
-      group_dots<4>(nw, nw, M, nw, 1, dw, 1, [&](int r, double d) { f1[r] -= d; });
-      group_dots<4>(m, nw, Ab, nw, 1, dw, 1, [&](int k, double d) { f2[k] = q2[k] - d; });
-      __syncthreads();
-      if (tid < 64) {
-        double rmax = 0.0, qmax = 0.0;
-        for (int r = tid; r < nw; r += 64) { rmax = fmax(rmax, fabs(f1[r])); qmax = fmax(qmax, fabs(q1[r])); }
-        for (int k = tid; k < m; k += 64) { rmax = fmax(rmax, fabs(f2[k])); qmax = fmax(qmax, fabs(q2[k])); }
-        rmax = wave_max(rmax);
-        qmax = wave_max(qmax);
-        if (tid == 0) sh.flag = !(rmax <= 1e-13 * qmax);
-      }
-      __syncthreads();
-      if (sh.flag) {
-        kkt_solve_lds(nw, m, nw0, Q, QR, L, M, dW, f1, f2, h1, h2, tmp);
-        for (int r = tid; r < nw; r += KKT_THREADS) dw[r] += h1[r];
-        for (int k = tid; k < m; k += KKT_THREADS) dy[k] += h2[k];
-        __syncthreads();
-      }
-    }
+    if (rscr)  // (the augmented system) one step of iterative refinement, as its factorisation's, with
+               // the residual and correction in rscr: wsb holds the kept factors
+      kkt_resolve_refine(nw, m, nw0, Q, QR, L, M, Ab, sh.delta_w, q1, q2, dw, dy, tmp, rscr, &sh.flag);
     for (int i = tid; i < nw0; i += KKT_THREADS) dwo[i] = dw[i];
     for (int i = tid; i < m; i += KKT_THREADS) dyo[i] = dy[i];
     return;
@@ -669,12 +559,8 @@ __global__ __launch_bounds__(KKT_THREADS) __attribute__((amdgpu_waves_per_eu(5, 
 // system by its delta_c != 0, its R-pivot treatment): the marked systems only, mode 0 re-factorising
 // them in the augmented form and overwriting dw, dy, delta_w (delta_c := IPOPT's), mode 1 re-solving
 // with the augmented factors (and, like the factorisation, one step of iterative refinement — the
-// restatements refine every full-rank re-solve).  Workspace per system (kkt_aug_ws_per): the augmented
-// factors | W~ | A~ | [q1; 0] | Pz | the re-solve's refinement residual and correction.
-__host__ __device__ inline int64_t kkt_aug_ws_per(int nw, int m) {
-  const int na = nw + m;
-  return kkt_ws_per(na, m) + (int64_t)na * na + (int64_t)m * na + na + (int64_t)nw * nw + 2 * (int64_t)(na + m);
-}
+// restatements refine every full-rank re-solve).  Workspace per system: KktAugLayout (cpl_kkt_block.hpp;
+// the fused search kernel re-solves there on one wave, kkt_aug_resolve_wave).
 
 __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_aug_kernel(
     int mode, int64_t batch, int nw, int m, const double* __restrict__ Mg, const double* __restrict__ Ag,
@@ -687,12 +573,13 @@ __global__ __launch_bounds__(KKT_THREADS) void cpl_kkt_aug_kernel(
   const int64_t b = blockIdx.x;
   if (b >= batch || (active && !active[b]) || dCg[b] == 0.0) return;
   const int na = nw + m, tid = threadIdx.x;
-  double* wsb = wsa + b * kkt_aug_ws_per(nw, m);
-  double* Ma = wsb + kkt_ws_per(na, m);
-  double* Aa = Ma + (int64_t)na * na;
-  double* q1a = Aa + (int64_t)m * na;
-  double* Pz = q1a + na;
-  double* rscr = Pz + (int64_t)nw * nw;
+  const KktAugLayout Lo(nw, m);
+  double* wsb = wsa + b * Lo.per;
+  double* Ma = wsb + Lo.Ma;
+  double* Aa = wsb + Lo.Aa;
+  double* q1a = wsb + Lo.q1a;
+  double* Pz = wsb + Lo.Pz;
+  double* rscr = wsb + Lo.rscr;
   if (mode == 0) {
     const double* M = Mg + b * nw * nw;
     const double* A = Ag + b * m * nw;

@@ -2562,6 +2562,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
         la.first = 1;
         la.max_soc = o.max_soc;
         la.c = S->c; la.M = S->M; la.r1 = S->r1; la.kkt_ws = S->ws; la.tau = S->tau;
+        if (S->jreg) { la.aug_dc = S->delta_c; la.aug_ws = S->ws_aug; }  // (the regularised systems' re-solves)
         la.a_max = S->a_max; la.a_z = S->a_z;
         la.soft_ws = la.soft_X = la.a_soft = nullptr; la.soft_try = nullptr;
         if (S->soft_fused) {
@@ -3163,9 +3164,7 @@ int32_t cpl_solver_create(const cpl_problem_desc* d, int64_t batch, const cpl_so
     delete S;
     return fail(CPL_ERR_UNSUPPORTED, "cpl_solver_create: jacobian_regularization needs nw + m <= 128");
   }
-  // (regularised: the second-order corrections re-solve through cpl_kkt_solve + the augmented kernel,
-  // not inside the fused search kernel, whose re-solve knows the one-wave factors only)
-  S->ls_fusable = kkt_wave_size(nw, m) && !S->jreg;
+  S->ls_fusable = kkt_wave_size(nw, m);
   S->mu_min = ipm_mu_min(opt.tol);
   S->bfgs = opt.hessian == CPL_HESSIAN_LIMITED_MEMORY;
   S->analytic_H = opt.hessian == CPL_HESSIAN_EXACT && cpl_lagrangian_hessian(d, 0, nullptr, nullptr, nullptr, nullptr,

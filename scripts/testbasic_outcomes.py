@@ -6,7 +6,7 @@ Jacobian entries at the start, the returned point's TestBasic quantities (force 
 errors, worst cone value) and the wall time.  One JSON line per run.
 
 usage: python scripts/testbasic_outcomes.py [gpu|oracle|both] [pivot|ipopt] > out.jsonl
-(the second argument: the facade's solver_jacobian_regularization, default pivot)
+(the second argument: the facade's solver_jacobian_regularization; default: the facade's own, pivot)
 """
 import json
 import os
@@ -79,10 +79,12 @@ class _Oracle:
         return self.po.eval_batch(self.prob.desc(), np.atleast_2d(X), outputs=("g", "jac", "f", "grad"), nthreads=1)
 
 
-def run(name, make, backend, jac_reg="pivot"):
+def run(name, make, backend, jac_reg=None):
     cpl, wrench, mu = make()
     inner = getattr(cpl, "_cp", cpl)  # (CoMPlanner wraps a CentroidalPlanner)
-    inner.solver_jacobian_regularization = jac_reg
+    if jac_reg is not None:
+        inner.solver_jacobian_regularization = jac_reg
+    jac_reg = inner.solver_jacobian_regularization
     if backend == "oracle":
         cpl.evaluator = _Oracle(cpl.GetCplProblem())
     t0 = time.perf_counter()
@@ -106,7 +108,7 @@ def run(name, make, backend, jac_reg="pivot"):
 def main():
     which = sys.argv[1] if len(sys.argv) > 1 else "gpu"
     backends = ["gpu", "oracle"] if which == "both" else [which]
-    jac_reg = sys.argv[2] if len(sys.argv) > 2 else "pivot"
+    jac_reg = sys.argv[2] if len(sys.argv) > 2 else None
     for backend in backends:
         for name, make in (("testSimpleProblem", simple), ("testGroundEnv", ground),
                            ("testSuperquadricEnv", superquadric), ("testCoMPlanner", com_planner)):

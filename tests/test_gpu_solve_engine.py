@@ -230,3 +230,25 @@ def test_ipopt_jacobian_regularisation_four_contacts_device_matches_host(hessian
         scale = float(h.x.abs().max())
         print(hessian, "iterate", k, "max |x_dev - x_host|", err, "scale", scale)
         assert err <= 1e-10 * max(1.0, scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hessian", ["limited-memory", "exact"])
+def test_regularised_fused_search_is_bitwise_the_stepwise_search(hessian):
+    """With the regularisation on, the fused search kernel re-solves a marked system's second-order
+    corrections on one wave over the augmented factors (kkt_aug_resolve_wave, its own AUGR
+    instantiation), the stepwise search through cpl_kkt_solve + cpl_kkt_aug_kernel on a workgroup: the
+    same arithmetic, so the same iterates bit for bit — on TestBasic's ground scenario from x = 0, whose
+    systems are rank deficient and whose first iteration takes a second-order correction."""
+    from test_oracle_solve import _testbasic
+
+    prob, x0, _ = _testbasic("testGroundEnv")
+    B = 4
+    mass = np.array([100.0, 90.0, 110.0, 125.0])
+    dev = torch.device("cuda:0")
+    args = (prob, torch.as_tensor(np.tile(x0, (B, 1)), device=dev), torch.as_tensor(mass, device=dev))
+    kw = dict(max_iter=40, hessian=hessian, jacobian_regularization="ipopt")
+    fused = batch_ipm_solve(*args, ls_kernel=2, **kw)
+    step = batch_ipm_solve(*args, ls_kernel=0, **kw)
+    assert torch.equal(fused.x, step.x) and torch.equal(fused.y, step.y)
+    assert torch.equal(fused.iterations, step.iterations) and torch.equal(fused.status, step.status)
