@@ -252,3 +252,31 @@ def test_regularised_fused_search_is_bitwise_the_stepwise_search(hessian):
     step = batch_ipm_solve(*args, ls_kernel=0, **kw)
     assert torch.equal(fused.x, step.x) and torch.equal(fused.y, step.y)
     assert torch.equal(fused.iterations, step.iterations) and torch.equal(fused.status, step.status)
+
+
+@pytest.mark.gpu
+def test_regularised_search_split_by_marking_at_large_batches():
+    """From LS_GF_MIN (2 048) on, with the regularisation on, the fused search runs as two launches: the
+    default instantiation over the unmarked instances, the AUGR one over the marked (rank-deficient)
+    ones.  A batch of 2 050 solve-workload instances, every 97th started from x = 0 (every force 0: A
+    rank deficient) — the fused search bitwise the stepwise one over the whole batch; the instances from
+    the workload's own starts (whose systems never lose rank) bitwise the pivot form's; the x = 0 ones
+    not (the regularised step differs there)."""
+    prob = solve_problem().GetCplProblem()
+    B = 2050
+    X0, mass = solve_inputs(prob, B, seed=23)
+    xl, xu, _, _ = prob.get_bounds_info()
+    zero = np.arange(0, B, 97)
+    X0[zero] = np.clip(np.zeros(prob.n), xl, xu)
+    dev = torch.device("cuda:0")
+    args = (prob, torch.as_tensor(X0, device=dev), torch.as_tensor(mass, device=dev))
+    kw = dict(max_iter=200, hessian="limited-memory")
+    fused = batch_ipm_solve(*args, ls_kernel=2, jacobian_regularization="ipopt", **kw)
+    step = batch_ipm_solve(*args, ls_kernel=0, jacobian_regularization="ipopt", **kw)
+    for k in ("x", "y", "status", "iterations"):
+        assert torch.equal(getattr(fused, k), getattr(step, k)), k
+    pivot = batch_ipm_solve(*args, ls_kernel=2, **kw)
+    rest = torch.as_tensor(np.setdiff1d(np.arange(B), zero), device=dev)
+    assert torch.equal(fused.x[rest], pivot.x[rest]) and torch.equal(fused.iterations[rest], pivot.iterations[rest])
+    zi = torch.as_tensor(zero, device=dev)
+    assert not torch.equal(fused.x[zi], pivot.x[zi])
