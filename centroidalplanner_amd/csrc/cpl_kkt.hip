@@ -650,8 +650,13 @@ __device__ __forceinline__ double col_dot_u(const double* a, int stride, const d
 
 
 
-template <int NW, int MM>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void cpl_kkt_wave_kernel(
+// W4: Z's accumulation and the reflector pairs' c_p on the workgroup's four waves (small batches: the
+// GPU is idle but for the few systems) — Z's 16 register-resident columns on wave 0, its 17th (a full
+// wave sum per reflector on the one-wave kernel's critical path) on wave 1, the c_p on waves 2 and 3;
+// the QR before and everything after on wave 0, as the one-wave kernel: the same factors and steps bit
+// for bit (scripts/r6_kkt_w4_probe.sh: one system 63 -> 60 us, Z 28k -> 20k cycles).
+template <int NW, int MM, bool W4 = false>
+__global__ __launch_bounds__(W4 ? 256 : 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void cpl_kkt_wave_kernel(
     int mode, int64_t batch, const double* __restrict__ Mg, const double* __restrict__ Ag,
     const double* __restrict__ r1g, const double* __restrict__ r2g, const double* __restrict__ mug,
     const double* __restrict__ dw_last, const uint8_t* __restrict__ active, double* __restrict__ dwg,
@@ -661,6 +666,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   constexpr int NZ = W::NZ, ZS = W::ZS, NP = W::NP, NFAC = W::NFAC;
   extern __shared__ __align__(16) double sm[];
   const int lane = threadIdx.x & 63;
+  const int wid = W4 ? (int)(threadIdx.x >> 6) : 0;
   const int64_t b = blockIdx.x;
   if (b >= batch) return;
   double* QR = sm;                 // [MM][NW]
@@ -683,12 +689,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const double q2v = lane < MM ? r2g[b * MM + lane] : 0.0;
 
   if (active && !active[b]) {
+    if (wid != 0) return;
     if (rw) dwg[b * NW + lane] = 0.0;
     if (lane < MM) dyg[b * MM + lane] = 0.0;
     if (lane == 0 && mode == 0) { dWg[b] = 0.0; dCg[b] = 0.0; info[b] = 0; }
     return;
   }
   if (mode == 1) {  // re-solve with the kept factors
+    if (wid != 0) return;
     double dwv, dyv;
     kkt_wave_resolve<NW, MM>(M, wsb, q1v, q2v, sm, &dwv, &dyv);
     if (rw) dwg[b * NW + lane] = dwv;
@@ -701,7 +709,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   // the 8 lanes of group j & 7 form the reflector (a group sum, two broadcasts) and publish its
   // entries through a 47-double LDS buffer; every trailing column's dot is a group sum and its
   // update stays in registers — 2 x 6 LDS operations per column instead of ~50.
-  {
+  if (!W4 || wid == 0) {  // (W4: the QR on wave 0 — its column blocks on four waves measured no faster,
+                          // the reflectors' scalar chain is its critical path)
     constexpr int RT = (NW + 7) / 8;  // row blocks per lane
     constexpr int CQ = (MM + 7) / 8;  // column blocks per lane
     const int g = lane >> 3, part = lane & 7;
@@ -805,9 +814,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       }
     __builtin_amdgcn_wave_barrier();
   }
+  if constexpr (W4) __syncthreads();
   KKT_MARK(1);
-  // c_p = v_{2p}^T v_{2p+1} for the paired chains (lane p keeps c_p)
-  {
+  // c_p = v_{2p}^T v_{2p+1} for the paired chains (lane p keeps c_p; W4: waves 2 and 3, beside Z)
+  if constexpr (W4) {
+    if (wid >= 2) {
+      #pragma unroll 1
+      for (int p = wid - 2; p < NP; p += 2) {
+        const double c = wave_sum(refl_entry<NW>(QR, 2 * p) * refl_entry<NW>(QR, 2 * p + 1));
+        if (lane == 0) cp[p] = c;
+      }
+    }
+  } else {
     double cl = 0.0;
     #pragma unroll 1
     for (int p = 0; p < NP; ++p) {
@@ -819,8 +837,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   // ---- Z = H_0 ... H_{m-1} [0; I], register-resident: lane (c = lane >> 2, part = lane & 3) holds
   // Z[i][c] for the rows i = part + 4t of column c < 16, the columns past 16 a row per lane; per
   // reflector (backward) a group-of-4 sum per column, the next reflector's entries loaded one step
-  // ahead.  Rows < j of Z are still zero at step j.
-  {
+  // ahead.  Rows < j of Z are still zero at step j.  (W4: wave 0 the 16 columns, wave 1 the rest.)
+  if (!W4 || wid < 2) {
+    const bool zmain = !W4 || wid == 0, zextra = !W4 || wid == 1;
     constexpr int ZT = (NW + 3) / 4;
     constexpr int NZX = NZ > 16 ? NZ - 16 : 0;
     const int c16 = lane >> 2, part = lane & 3;
@@ -854,19 +873,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         nb = beta[j - 1];
       }
       if (bj != 0.0) {
-        double d0 = 0.0, d1 = 0.0;
+        if (zmain) {
+          double d0 = 0.0, d1 = 0.0;
 #pragma unroll
-        for (int t = JB; t < ZT; t += 2) {
-          d0 += vl[t] * z[t];
-          if (t + 1 < ZT) d1 += vl[t + 1] * z[t + 1];
+          for (int t = JB; t < ZT; t += 2) {
+            d0 += vl[t] * z[t];
+            if (t + 1 < ZT) d1 += vl[t + 1] * z[t + 1];
+          }
+          const double sc = bj * group4_sum(d0 + d1);
+          if (c16 < NZ) {
+#pragma unroll
+            for (int t = JB; t < ZT; ++t) z[t] -= sc * vl[t];
+          }
         }
-        const double sc = bj * group4_sum(d0 + d1);
-        if (c16 < NZ) {
+        if (zextra) {
 #pragma unroll
-          for (int t = JB; t < ZT; ++t) z[t] -= sc * vl[t];
+          for (int c = 0; c < NZX; ++c) zx[c] -= bj * wave_sum(vx * zx[c]) * vx;
         }
-#pragma unroll
-        for (int c = 0; c < NZX; ++c) zx[c] -= bj * wave_sum(vx * zx[c]) * vx;
       }
 #pragma unroll
       for (int t = 0; t < ZT; ++t) vl[t] = j > 0 ? nl[t] : 0.0;
@@ -889,18 +912,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     zblock(std::integral_constant<int, 2>());
     zblock(std::integral_constant<int, 1>());
     zblock(std::integral_constant<int, 0>());
-    if (c16 < NZ && c16 < 16) {
+    if (zmain && c16 < NZ && c16 < 16) {
 #pragma unroll
       for (int t = 0; t < ZT; ++t) {
         const int i = part + 4 * t;
         if (i < NW) Z[i * ZS + c16] = z[t];
       }
     }
-    if (lane < NW) {
+    if (zextra && lane < NW) {
 #pragma unroll
       for (int c = 0; c < NZX; ++c) Z[lane * ZS + 16 + c] = zx[c];
     }
     __builtin_amdgcn_wave_barrier();
+  }
+  if constexpr (W4) {  // Z and c_p complete; wave 0 goes on alone
+    __syncthreads();
+    if (wid != 0) return;
   }
   KKT_MARK(2);
   // ---- rank deficiency: delta_c on R's diagonal
@@ -1086,6 +1113,16 @@ using KktWaveKernel = void (*)(int, int64_t, const double*, const double*, const
 // runs the same kernel and an instance's iterates do not depend on the batch it is solved in
 // (tests/test_gpu_solve_engine.py: B = 1 vs inside B = 64).  CPL_KKT_KERNEL=block or =wave forces
 // one (measurement only).
+// batches up to this size factorise on four waves per system (cpl_kkt_wave_kernel<.., true>): the same
+// factors bit for bit, the QR's column blocks in parallel (CPL_KKT_W4=0 / 1: never / always; measurement)
+constexpr int64_t KKT_W4_MAX = 256;
+static bool kkt_use_w4(int64_t batch) {
+  static const int forced = [] {
+    const char* e = std::getenv("CPL_KKT_W4");
+    return e ? (std::string(e) == "1" ? 1 : 0) + (std::string(e) == "0" ? 2 : 0) : 0;
+  }();
+  return forced == 1 || (forced == 0 && batch <= KKT_W4_MAX);
+}
 static KktWaveKernel kkt_wave_kernel_for(int nw, int m) {
   static const int forced = [] {
     const char* e = std::getenv("CPL_KKT_KERNEL");
@@ -1169,8 +1206,11 @@ int32_t cpl_kkt_solve(int32_t mode, int64_t batch, int32_t nw, int32_t m, const 
   if (batch > 0x7fffffffLL) return fail(CPL_ERR_INVALID_ARGUMENT, "cpl_kkt_solve: batch too large");
   if (KktWaveKernel wk = kkt_wave_kernel_for(nw, m)) {
     const size_t lds = sizeof(double) * (size_t)kktw_lds_doubles(nw, m);
-    hipLaunchKernelGGL(wk, dim3((unsigned)batch), dim3(64), lds, (hipStream_t)stream, (int)mode, batch, d_M, d_A, d_r1,
-                       d_r2, d_mu, d_delta_w_last, d_active, d_dw, d_dy, d_delta_w, d_delta_c, d_info, d_ws);
+    const bool w4 = mode == 0 && kkt_use_w4(batch);
+    const KktWaveKernel k = w4 ? static_cast<KktWaveKernel>(cpl_kkt_wave_kernel<47, 30, true>) : wk;
+    hipLaunchKernelGGL(k, dim3((unsigned)batch), dim3(w4 ? 256 : 64), lds,
+                       (hipStream_t)stream, (int)mode, batch, d_M, d_A, d_r1, d_r2, d_mu, d_delta_w_last, d_active, d_dw,
+                       d_dy, d_delta_w, d_delta_c, d_info, d_ws);
   } else {
     const size_t lds = sizeof(double) * (size_t)kkt_launch_lds_doubles(nw, m, mode);
     if (lds > 160 * 1024) return fail(CPL_ERR_UNSUPPORTED, "cpl_kkt_solve: system too large for one LDS image");
