@@ -109,6 +109,9 @@ struct KParams {
   const double* sc_df;
   const double* sc_dc;
   const int32_t* sc_row;
+  // (the solve engine; pipelined kernel only) a device byte that, when 0, makes the launch a no-op:
+  // the small-batch iteration's soft-restoration evaluation when no instance tries a soft step
+  const uint8_t* gate;
 };
 static_assert(sizeof(KParams) < 4096, "kernel parameters must fit the kernarg segment");
 
@@ -1724,6 +1727,7 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void cpl_eval_pipe_kernel(const KPa
   constexpr int CT = 64 * NCW;  // compute threads
   constexpr bool HAS_SQ = ENVK == CPL_ENV_SUPERQUADRIC || ENVK == CPL_ENV_MIXED;
   extern __shared__ __align__(16) double smem[];
+  if (K.gate && *K.gate == 0) return;  // (every thread of every workgroup: the same byte)
   load_ctab(K);
   // fused Lagrangian gradient: the CSC index of the structure in LDS (read per column, per entry)
   int* s_colp = reinterpret_cast<int*>(smem + K.offC);
@@ -3005,7 +3009,8 @@ struct EvalScale {
 static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
                            const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
                            double* d_norms, hipStream_t stream, bool finish = true,
-                           const LGradArgs* lg = nullptr, int32_t flags = 0, const EvalScale* sc = nullptr) {
+                           const LGradArgs* lg = nullptr, int32_t flags = 0, const EvalScale* sc = nullptr,
+                           const uint8_t* gate = nullptr) {
   int32_t st = validate_desc(d);
   if (st) return st;
   if (flags & ~(CPL_EVAL_JAC_FOLDED | CPL_EVAL_SOA)) return fail(CPL_ERR_INVALID_ARGUMENT, "unknown eval flags");
@@ -3025,6 +3030,7 @@ static int32_t launch_eval(const cpl_problem_desc* d, int64_t batch, const doubl
   if (!d_g && !d_jac && !d_f && !d_grad) return CPL_OK;
   KParams K;
   fill_params(d, K, d_x);
+  K.gate = gate;  // (honoured by the pipelined kernel; the others evaluate regardless)
   if (flags & CPL_EVAL_JAC_FOLDED) {  // values-only Jacobian records (cpl_layout.hpp)
     K.fold = fold_level(d->env_kind);
     K.nnz = folded_nnz(K.N, d->env_kind);
@@ -3571,10 +3577,19 @@ static double* g_ws[64] = {nullptr};
 // pipelined kernel — the caller then scales the outputs itself
 int32_t eval_batch_scaled(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
                           const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
-                          int32_t flags, const double* df, const double* dc, const int32_t* row, void* stream) {
+                          int32_t flags, const double* df, const double* dc, const int32_t* row, void* stream,
+                          const uint8_t* gate) {
   const EvalScale sc{df, dc, row};
   return launch_eval(d, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f, d_grad, nullptr, (hipStream_t)stream, true,
-                     nullptr, flags, &sc);
+                     nullptr, flags, &sc, gate);
+}
+
+// (internal, the solve engine) cpl_eval_batch_ex with a gate byte (KParams::gate)
+int32_t eval_batch_gated(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
+                         const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
+                         int32_t flags, void* stream, const uint8_t* gate) {
+  return launch_eval(d, batch, d_x, d_mass, d_env_tag, d_g, d_jac, d_f, d_grad, nullptr, (hipStream_t)stream, true,
+                     nullptr, flags, nullptr, gate);
 }
 
 }  // namespace cpl

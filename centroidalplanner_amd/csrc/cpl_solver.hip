@@ -43,7 +43,12 @@ int32_t ls_backtrack(const cpl_problem_desc* d, const LsBacktrackArgs& a, hipStr
 // cpl_kernels.hip: the NLP-scaled evaluation (pipelined kernel; CPL_ERR_UNSUPPORTED: not that path)
 int32_t eval_batch_scaled(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
                           const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
-                          int32_t flags, const double* df, const double* dc, const int32_t* row, void* stream);
+                          int32_t flags, const double* df, const double* dc, const int32_t* row, void* stream,
+                          const uint8_t* gate = nullptr);
+// cpl_kernels.hip: cpl_eval_batch_ex whose pipelined-kernel launch is a no-op while *gate == 0
+int32_t eval_batch_gated(const cpl_problem_desc* d, int64_t batch, const double* d_x, const double* d_mass,
+                         const uint8_t* d_env_tag, double* d_g, double* d_jac, double* d_f, double* d_grad,
+                         int32_t flags, void* stream, const uint8_t* gate);
 bool kkt_wave_size(int nw, int m);
 int64_t kkt_aug_workspace_doubles(int nw, int m);
 int32_t kkt_aug_solve(int mode, int64_t batch, int nw, int m, const double* d_M, const double* d_A, const double* d_r1,
@@ -2330,15 +2335,18 @@ int32_t eval_fg(cpl_solver* S, const double* X, double* fo, double* go) {
   CK(cpl_eval_batch(&S->desc, S->Bcur, X, S->mass, S->tag, go, nullptr, fo, nullptr, S->stream));
   return apply_scaling(S, fo, nullptr, go, nullptr);
 }
-int32_t eval_full(cpl_solver* S, const double* X, double* fo, double* grado, double* go, double* jo) {
+// gate (device byte, or nullptr): the evaluation is skipped where the pipelined kernel runs it and the
+// byte is 0 — the outputs are then left as they were, and so are they scaled again (callers gate only
+// an evaluation whose outputs nobody reads when the byte is 0)
+int32_t eval_full(cpl_solver* S, const double* X, double* fo, double* grado, double* go, double* jo,
+                  const uint8_t* gate = nullptr) {
   if (S->scaled && S->sc_fused) {
     const int32_t rc = eval_batch_scaled(&S->desc, S->Bcur, X, S->mass, S->tag, go, jo, fo, grado,
-                                         CPL_EVAL_JAC_FOLDED, S->df, S->dc, S->rrow, S->stream);
+                                         CPL_EVAL_JAC_FOLDED, S->df, S->dc, S->rrow, S->stream, gate);
     if (rc != CPL_ERR_UNSUPPORTED) return rc;
     S->sc_fused = false;
   }
-  CK(cpl_eval_batch_ex(&S->desc, S->Bcur, X, S->mass, S->tag, go, jo, fo, grado, nullptr, CPL_EVAL_JAC_FOLDED,
-                       S->stream));
+  CK(eval_batch_gated(&S->desc, S->Bcur, X, S->mass, S->tag, go, jo, fo, grado, CPL_EVAL_JAC_FOLDED, S->stream, gate));
   return apply_scaling(S, fo, grado, go, jo);
 }
 
@@ -2606,7 +2614,9 @@ int32_t step_phase(cpl_solver* S, int phase) {
                            S->soft_try, S->a_soft, S->ws_, S->Xs);
         LAUNCHED("k_soft_begin");
       }
-      CK(eval_full(S, S->Xs, S->f_n, S->grad_n, S->g_n, S->J_n));
+      // (the fused search kernel raised d_any[1] exactly where it set soft_try: with no soft-step candidate
+      // this evaluation's outputs are read by nobody, and its launch returns at once)
+      CK(eval_full(S, S->Xs, S->f_n, S->grad_n, S->g_n, S->J_n, S->soft_begun ? S->d_any + 1 : nullptr));
       if (S->tail_fused) {
         const FailTail tail{S->freepos, S->Xbase, S->Xn, S->act, S->err0, o.acceptable_tol, S->failed, S->moved,
                             S->status, S->active};
