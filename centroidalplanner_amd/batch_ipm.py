@@ -75,7 +75,8 @@ STATUS_OPTIMAL = 0
 STATUS_ACCEPTABLE = 1
 STATUS_MAX_ITER = 2
 STATUS_INFEASIBLE = 3     # the restoration phase converged: a point of local infeasibility
-STATUS_RESTO_FAILED = 4   # the restoration phase converged twice to a feasible point the filter rejects
+STATUS_RESTO_FAILED = 4   # the restoration phase converged twice to a feasible point the filter rejects, or
+                          # it was called at an almost feasible point without a backup acceptable point
 STATUS_NAMES = {STATUS_OPTIMAL: "optimal", STATUS_ACCEPTABLE: "acceptable", STATUS_MAX_ITER: "max_iter",
                 STATUS_INFEASIBLE: "local_infeasibility", STATUS_RESTO_FAILED: "restoration_failed"}
 
@@ -95,6 +96,7 @@ KAPPA_RESTO = 0.9          # required_infeasibility_reduction
 BOUND_MULT_RESET = 1000.0  # bound_mult_reset_threshold
 SOFT_RESTO_FACTOR = 0.9999  # soft_resto_pderror_reduction_factor
 MAX_SOFT_RESTO = 10         # max_soft_resto_iters
+ALMOST_FEASIBLE = 1e-2      # BacktrackingLineSearch: no restoration phase at theta <= 1e-2 tol
 
 FMAX = 64  # filter entries kept per instance (a ring)
 SCALING_MAX_GRADIENT = 100.0  # nlp_scaling_max_gradient (nlp_scaling_method = gradient-based, IPOPT's default)
@@ -1051,11 +1053,23 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         # IPOPT calls no restoration phase at an acceptable point (BacktrackingLineSearch: "Restoration
         # phase called at acceptable point" -> STOP_AT_ACCEPTABLE_POINT): the solve ends there
         at_acc = failed & (E["err0"] <= acceptable_tol)
-        act_it = act & ~at_acc  # the instances whose iteration counts
-        if bool(at_acc.any()):
-            S["status"].copy_(torch.where(at_acc, STATUS_ACCEPTABLE, S["status"]))
-            S["active"].copy_(S["active"] & ~at_acc)
-            failed = failed & ~at_acc
+        # nor at an almost feasible point (theta <= 1e-2 tol): the backup acceptable point is restored
+        # and the solve stops there as acceptable (RestoreAcceptablePoint), or without one it ends as a
+        # restoration failure ("Restoration phase called, but point is almost feasible")
+        near = failed & ~at_acc & (theta_k <= ALMOST_FEASIBLE * tol)
+        back = near & S["has_acc"]
+        if _DEBUG_EVENT is not None and bool(back.any()):  # (diagnostics / tests)
+            _DEBUG_EVENT("restore_acceptable_point", back.clone())
+        for k, kk in (("w", "acc_w"), ("y", "acc_y"), ("zL", "acc_zL"), ("zU", "acc_zU")):
+            S[k].copy_(torch.where(back[:, None], S[kk], S[k]))
+        at_acc = at_acc | back
+        stop = at_acc | near
+        act_it = act & ~stop  # the instances whose iteration counts
+        if bool(stop.any()):
+            S["status"].copy_(torch.where(at_acc, STATUS_ACCEPTABLE, torch.where(near, STATUS_RESTO_FAILED,
+                                                                                   S["status"])))
+            S["active"].copy_(S["active"] & ~stop)
+            failed = failed & ~stop
         S["in_soft"].copy_(S["in_soft"] & ~failed)
         S["soft_cnt"].copy_(torch.where(failed, 0, S["soft_cnt"]))
         moved = act_it & ~failed

@@ -631,16 +631,41 @@ __global__ __launch_bounds__(256) void k_soft_judge(
 // moved = an accepted one; a failed search leaves the soft phase.  IPOPT calls no restoration phase
 // at an acceptable point (BacktrackingLineSearch: "Restoration phase called at acceptable point" ->
 // STOP_AT_ACCEPTABLE_POINT): an instance whose search failed there ends with status acceptable.
+// Nor at an almost feasible point (theta <= 1e-2 tol): the backup acceptable point is restored and
+// the solve stops there as acceptable (RestoreAcceptablePoint), or without one it ends as a
+// restoration failure ("Restoration phase called, but point is almost feasible").
+struct NearFeasible {
+  const double* theta_k;
+  double near_tol;  // 1e-2 tol
+  int nw, m;
+  uint8_t* has_acc;
+  const double *acc_w, *acc_y, *acc_zL, *acc_zU;
+  double *w, *y, *zL, *zU;
+};
 // The bookkeeping of instance b:
 __device__ __forceinline__ void fail_book(int64_t b, const uint8_t* __restrict__ act,
                                           const double* __restrict__ st_alpha, const double* __restrict__ err0,
                                           double acc_tol, uint8_t* __restrict__ failed, uint8_t* __restrict__ moved,
                                           uint8_t* __restrict__ in_soft, int32_t* __restrict__ soft_cnt,
-                                          int64_t* __restrict__ status, uint8_t* __restrict__ active) {
+                                          int64_t* __restrict__ status, uint8_t* __restrict__ active,
+                                          const NearFeasible& nf) {
   const bool a = act[b] != 0;
   bool f = a && !(st_alpha[b] > 0.0);
-  if (f && err0[b] <= acc_tol) {
-    status[b] = CPL_SOLVE_ACCEPTABLE;
+  const bool at_acc = f && err0[b] <= acc_tol;
+  const bool near = f && !at_acc && nf.theta_k[b] <= nf.near_tol;
+  if (at_acc || near) {
+    const bool back = near && nf.has_acc[b] != 0;
+    if (back) {  // (a rare branch: one thread copies the instance's backup point)
+      const int nw = nf.nw, m = nf.m;
+      for (int k = 0; k < nw; ++k) {
+        nf.w[b * nw + k] = nf.acc_w[b * nw + k];
+        nf.zL[b * nw + k] = nf.acc_zL[b * nw + k];
+        nf.zU[b * nw + k] = nf.acc_zU[b * nw + k];
+      }
+      for (int r = 0; r < m; ++r) nf.y[b * m + r] = nf.acc_y[b * m + r];
+      nf.has_acc[b] = 0;
+    }
+    status[b] = (at_acc || back) ? CPL_SOLVE_ACCEPTABLE : CPL_SOLVE_RESTO_FAILED;
     active[b] = 0;
     failed[b] = 0;
     moved[b] = 0;
@@ -661,7 +686,7 @@ __global__ void k_fail_unpack(int64_t total, int n, int nw, const int32_t* __res
                               const uint8_t* __restrict__ act, const double* __restrict__ st_alpha,
                               const double* __restrict__ err0, double acc_tol, uint8_t* __restrict__ failed,
                               uint8_t* __restrict__ moved, uint8_t* __restrict__ in_soft, int32_t* __restrict__ soft_cnt,
-                              int64_t* __restrict__ status, uint8_t* __restrict__ active) {
+                              int64_t* __restrict__ status, uint8_t* __restrict__ active, const NearFeasible nf) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total) return;
   const int64_t b = e / n;
@@ -669,7 +694,7 @@ __global__ void k_fail_unpack(int64_t total, int n, int nw, const int32_t* __res
   const int k = freepos[j];
   X[e] = k >= 0 ? st_w[b * nw + k] : Xbase[e];
   if (j != 0) return;
-  fail_book(b, act, st_alpha, err0, acc_tol, failed, moved, in_soft, soft_cnt, status, active);
+  fail_book(b, act, st_alpha, err0, acc_tol, failed, moved, in_soft, soft_cnt, status, active, nf);
 }
 
 // The small-batch iteration (P_FUSED) runs the soft step's judge and the end of the search as one
@@ -688,6 +713,7 @@ struct FailTail {
   uint8_t* moved;
   int64_t* status;
   uint8_t* active;
+  NearFeasible nf;
 };
 __global__ __launch_bounds__(256) void k_soft_judge_fail(
     int64_t B, int n, int m, int nf, int nw, int nnz_rec, const uint8_t* __restrict__ soft_try,
@@ -721,7 +747,7 @@ __global__ __launch_bounds__(256) void k_soft_judge_fail(
   }
   if (lane == 0)
     fail_book(b, ft2.act, st_alpha, ft2.err0, ft2.acc_tol, ft2.failed, ft2.moved, in_soft, soft_cnt, ft2.status,
-              ft2.active);
+              ft2.active, ft2.nf);
 }
 
 // IPOPT's limited-memory quasi-Newton model (LimMemQuasiNewtonUpdater [IPOPT] with the defaults
@@ -2422,6 +2448,11 @@ int32_t hessian_into(cpl_solver* S, const cpl_problem_desc* d, const uint8_t* ma
   return CPL_OK;
 }
 
+static NearFeasible near_feasible(cpl_solver* S, const cpl_solve_options& o) {
+  return NearFeasible{S->theta_k, 1e-2 * o.tol, S->nw, S->m, S->has_acc, S->acc_w, S->acc_y, S->acc_zL, S->acc_zU,
+                      S->w, S->y, S->zL, S->zU};
+}
+
 int32_t step_phase(cpl_solver* S, int phase) {
   const int64_t B = S->Bcur;
   const int n = S->n, m = S->m, nf = S->nf, nw = S->nw;
@@ -2619,7 +2650,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
       CK(eval_full(S, S->Xs, S->f_n, S->grad_n, S->g_n, S->J_n, S->soft_begun ? S->d_any + 1 : nullptr));
       if (S->tail_fused) {
         const FailTail tail{S->freepos, S->Xbase, S->Xn, S->act, S->err0, o.acceptable_tol, S->failed, S->moved,
-                            S->status, S->active};
+                            S->status, S->active, near_feasible(S, o)};
         hipLaunchKernelGGL(k_soft_judge_fail, dim3(blocks_for(B)), dim3(256), 0, st, B, n, m, nf, nw, S->nnz_rec,
                            S->soft_try, S->soft_now, S->a_soft, S->amap, S->row_slack, S->free32, S->gl, S->hasL,
                            S->hasU, S->wl0, S->wu0, S->ws_, S->f_n, S->grad_n, S->g_n, S->J_n, S->A, S->gradw, S->c,
@@ -2645,7 +2676,7 @@ int32_t step_phase(cpl_solver* S, int phase) {
       if (!S->tail_fused) {
         hipLaunchKernelGGL(k_fail_unpack, dim3(blocks_elems(B * n)), dim3(256), 0, st, B * n, n, nw, S->freepos,
                            S->Xbase, S->st_w, S->Xn, S->act, S->st_alpha, S->err0, o.acceptable_tol, S->failed,
-                           S->moved, S->in_soft, S->soft_cnt, S->status, S->active);
+                           S->moved, S->in_soft, S->soft_cnt, S->status, S->active, near_feasible(S, o));
         LAUNCHED("k_fail_unpack");
       }
       CK(eval_full(S, S->Xn, S->f_n, S->grad_n, S->g_n, S->J_n));

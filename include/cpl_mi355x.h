@@ -493,10 +493,11 @@ int32_t cpl_ipm_dense_a(int64_t batch, int32_t m, int32_t nw, int32_t nf, int32_
 #define CPL_SOLVE_RESTO_FAILED 4 /* the restoration phase converged to a feasible point the original
                                     filter rejects, again after its tolerance was tightened (IPOPT's
                                     RESTORATION_CONVERGED_TO_FEASIBLE_POINT); a failed restoration line
-                                    search resets p, n instead (RestoRestorationPhase).  When an earlier
-                                    regular iterate was at the acceptable level, that point is restored
-                                    and the status is CPL_SOLVE_ACCEPTABLE instead (IPOPT's backup
-                                    acceptable point) */
+                                    search resets p, n instead (RestoRestorationPhase); or the line search
+                                    failed at an almost feasible point (theta <= 1e-2 tol), where IPOPT
+                                    calls no restoration phase.  When an earlier regular iterate was at
+                                    the acceptable level, that point is restored and the status is
+                                    CPL_SOLVE_ACCEPTABLE instead (IPOPT's backup acceptable point) */
 
 typedef struct cpl_solve_options {
   int32_t max_iter;        /* 3000 (IPOPT's default) */

@@ -59,6 +59,7 @@ int cplo_bounds(const cpl_problem_desc* d, double* xl, double* xu, double* gl, d
 #define KAPPA_RESTO 0.9
 #define BOUND_MULT_RESET 1000.0
 #define SOFT_RESTO_FACTOR 0.9999
+#define ALMOST_FEASIBLE 1e-2   /* BacktrackingLineSearch: no restoration phase at theta <= 1e-2 tol */
 #define MAX_SOFT_RESTO 10
 #define FMAX 64
 #define PIVOT_REL DBL_EPSILON
@@ -912,6 +913,7 @@ void cplo_set_watchdog(int on) { g_watchdog = on != 0; }
 static __thread Eval g_wd_cur;
 /* this thread's watchdog events since the last read: starts, successes, restorations of the kept iterate */
 static __thread long g_wd_events[3];
+static __thread long g_resto_fail_events[2];  /* (cplo_resto_fail_events) */
 void cplo_watchdog_events(long* out) {
   for (int k = 0; k < 3; ++k) { out[k] = g_wd_events[k]; g_wd_events[k] = 0; }
 }
@@ -1160,6 +1162,23 @@ static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
     S->mu = mu;
     return;
   }
+  if (failed && theta_k <= ALMOST_FEASIBLE * o->tol) {
+    /* nor at an almost feasible point (BacktrackingLineSearch: theta <= 1e-2 tol): the backup acceptable
+     * point is restored and the solve stops there as acceptable (RestoreAcceptablePoint), or without
+     * one it ends as a restoration failure ("Restoration phase called, but point is almost feasible") */
+    S->active = 0;
+    S->mu = mu;
+    S->status = S->has_acc ? ST_ACCEPTABLE : ST_RESTO_FAILED;
+    g_resto_fail_events[0] += 1;
+    if (S->has_acc) {
+      g_resto_fail_events[1] += 1;
+      memcpy(S->w, S->acc_w, sizeof(double) * (size_t)nw);
+      memcpy(S->zL, S->acc_zL, sizeof(double) * (size_t)nw);
+      memcpy(S->zU, S->acc_zU, sizeof(double) * (size_t)nw);
+      memcpy(S->y, S->acc_y, sizeof(double) * (size_t)m);
+    }
+    return;
+  }
   if (failed) { S->in_soft = 0; S->soft_cnt = 0; }
   if (g_trace)  /* (diagnostics: batch_ipm.py's verbose line, scripts/solve_divergence.py) */
     fprintf(stderr, "   [C] mu=%.2e err0=%.2e a_max=%.2e alpha=%.2e dw=%.2e dy=%.2e dW=%.1e f=%.6e d_inf=%.2e c_inf=%.2e resto_next=%d tiny=%d rank_def=%d\n",
@@ -1245,7 +1264,9 @@ static void resto_step(Prob* P, State* S, const Opts* o) {
     if (!feas || S->resto_tight) {
       S->status = feas ? ST_RESTO_FAILED : ST_INFEASIBLE;
       S->active = 0;
+      if (feas) g_resto_fail_events[0] += 1;
       if (feas && S->has_acc) {  /* RestoreAcceptablePoint: stop there as acceptable */
+        g_resto_fail_events[1] += 1;
         memcpy(S->w, S->acc_w, sizeof(double) * (size_t)nw);
         memcpy(S->zL, S->acc_zL, sizeof(double) * (size_t)nw);
         memcpy(S->zU, S->acc_zU, sizeof(double) * (size_t)nw);
@@ -1407,6 +1428,15 @@ static void resto_step(Prob* P, State* S, const Opts* o) {
  * default like the engine's; cplo_set_fallback_viol_tol opts in (process-wide). */
 static double g_fallback_viol_tol = 0.0;
 void cplo_set_fallback_viol_tol(double v) { g_fallback_viol_tol = v; }
+/* IPOPT's acceptable_tol (default 1e-6, process-wide) and the count of failed restoration phases on this
+ * thread (feasible end points; those with a backup acceptable point second): the search for the
+ * RestoreAcceptablePoint branch (scripts/resto_acc_search.py). */
+static double g_acceptable_tol = 1e-6;
+void cplo_set_acceptable_tol(double v) { g_acceptable_tol = v; }
+void cplo_resto_fail_events(long* out) {
+  out[0] = g_resto_fail_events[0]; out[1] = g_resto_fail_events[1];
+  g_resto_fail_events[0] = g_resto_fail_events[1] = 0;
+}
 /* nlp_scaling_method: 1 gradient-based (IPOPT's default, the reference's), 0 none (process-wide) */
 static int g_nlp_scaling = 1;
 void cplo_set_nlp_scaling(int on) { g_nlp_scaling = on != 0; }
@@ -1463,7 +1493,7 @@ int cplo_solve(const cpl_problem_desc* d, const double* x0, double mass, int max
   for (int j = 0; j < n; ++j) P.Xbase[j] = P.is_fixed[j] ? P.xl[j] : x0[j];
   P.scaled = 0;
   if (g_nlp_scaling) nlp_scaling(&P, P.Xbase);
-  Opts o = {tol, 1e-6, dmin(tol, COMPL_INF_TOL) / (BARRIER_TOL_FACTOR + 1.0), g_fallback_viol_tol, 15, 40, 4};
+  Opts o = {tol, g_acceptable_tol, dmin(tol, COMPL_INF_TOL) / (BARRIER_TOL_FACTOR + 1.0), g_fallback_viol_tol, 15, 40, 4};
   /* starting point: x pushed into its bounds, slacks = g_I(x) pushed into theirs */
   const int nw = P.nw, nf = P.nf;
   double w0[NWMAX], Xs[NMAX];

@@ -51,8 +51,12 @@ def _load(path=LIB_PATH):
     lib.cplo_set_nlp_scaling.restype = None
     lib.cplo_set_watchdog.argtypes = [c_int]
     lib.cplo_set_watchdog.restype = None
+    lib.cplo_set_acceptable_tol.argtypes = [c_double]
+    lib.cplo_set_acceptable_tol.restype = None
     lib.cplo_watchdog_events.argtypes = [ctypes.POINTER(ctypes.c_long)]
     lib.cplo_watchdog_events.restype = None
+    lib.cplo_resto_fail_events.argtypes = [ctypes.POINTER(ctypes.c_long)]
+    lib.cplo_resto_fail_events.restype = None
     lib.cplo_set_jac_reg.argtypes = [c_int]
     lib.cplo_set_jac_reg.restype = None
     return lib
@@ -224,6 +228,19 @@ def watchdog_events():
     last call (single-thread solves)."""
     out = (ctypes.c_long * 3)()
     lib.cplo_watchdog_events(out)
+    return tuple(int(v) for v in out)
+
+
+def set_acceptable_tol(v):
+    """IPOPT's acceptable_tol in the compiled restatement (process-wide; default 1e-6)."""
+    lib.cplo_set_acceptable_tol(float(v))
+
+
+def resto_fail_events():
+    """(failed restoration phases ending at a feasible point, those of them that restored the backup
+    acceptable point) on this thread since the last call (single-thread solves)."""
+    out = (ctypes.c_long * 2)()
+    lib.cplo_resto_fail_events(out)
     return tuple(int(v) for v in out)
 
 
