@@ -283,29 +283,30 @@ def test_regularised_search_split_by_marking_at_large_batches():
 
 
 @pytest.mark.gpu
-def test_restoration_called_at_an_almost_feasible_point_device():
+@pytest.mark.parametrize("k", [0, 1])
+def test_restoration_called_at_an_almost_feasible_point_device(k):
     """The engine's end of a failed line search (cpl_solver.hip fail_book): at an almost feasible point
     (theta <= 1e-2 tol) no restoration phase — the backup acceptable point restored and the solve
     stopped as acceptable there (RestoreAcceptablePoint), or without one a restoration failure.  The
-    case of test_oracle_solve.py (tests/golden/resto_acc_cases.json), where both CPU restatements reach
-    the branch: under the default acceptable_tol the device solve ends as a restoration failure; with
-    acceptable_tol 1.78e-5 the same iteration restores an earlier iterate and ends as acceptable
-    (measured: iteration 183 on the device, 129 / 176 in the compiled / host restatements — the
-    degenerate trajectory parts them by rounding; scripts/resto_acc_gpu_probe.py)."""
+    cases of test_oracle_solve.py (tests/golden/resto_acc_cases.json), where both CPU restatements reach
+    the branch: without a backup point the device solve ends as a restoration failure; with one (case 1:
+    IPOPT's default acceptable_tol) the same iteration restores an earlier iterate and ends as acceptable
+    (measured: iteration 183 / 680 on the device, 129 / 1 414 and 176 / 903 in the compiled / host
+    restatements — the degenerate trajectories part them by rounding; scripts/resto_acc_gpu_probe.py)."""
     from test_oracle_solve import _resto_case
 
-    prob, x0, c = _resto_case()
+    prob, x0, c = _resto_case(k)
     dev = torch.device("cuda:0")
     kw = dict(tol=c["tol"], max_iter=3000, hessian=c["hessian"])
     X0 = torch.as_tensor(x0[None], device=dev)
     mass = torch.as_tensor(np.array([prob.desc().mass]), device=dev)
-    fail = batch_ipm_solve(prob, X0, mass, acceptable_tol=1e-6, **kw)
+    fail = batch_ipm_solve(prob, X0, mass, acceptable_tol=c["no_backup_tol"], **kw)
     back = batch_ipm_solve(prob, X0, mass, acceptable_tol=c["acceptable_tol"], **kw)
     assert int(fail.status[0]) == 4 and int(back.status[0]) == STATUS_ACCEPTABLE
     assert int(back.iterations[0]) == int(fail.iterations[0])
     assert not torch.equal(back.x, fail.x) and float(back.objective[0]) != float(fail.objective[0])
-    # the same instance in a batch of 64 (with the workload's other starts around it) takes the branch
-    # at the same iteration to the same point: the restore is per instance
+    # the same instance in a batch of 64 (perturbed starts around it) takes the branch at the same
+    # iteration to the same point: the restore is per instance
     Xb = X0.repeat(64, 1)
     Xb[1:] += torch.as_tensor(np.random.default_rng(5).normal(0.0, 1e-3, (63, x0.size)), device=dev)
     batch = batch_ipm_solve(prob, Xb, mass.repeat(64), acceptable_tol=c["acceptable_tol"], **kw)

@@ -200,58 +200,63 @@ def test_ipopt_jacobian_regularisation_on_the_simple_problem():
     np.testing.assert_allclose(h.x[0].numpy(), r["x"], rtol=0, atol=1e-9)
 
 
-def _resto_case():
+def _resto_case(k=0):
     import json
     import os
 
     from resto_cases import make
 
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "resto_acc_cases.json")
-    c = json.load(open(path))["cases"][0]
+    c = json.load(open(path))["cases"][k]
     with warnings.catch_warnings():
         warnings.simplefilter("ignore", RuntimeWarning)
         prob = make(c["params"]).GetCplProblem()
     return prob, np.array(c["x0"]), c
 
 
-def test_restoration_called_at_an_almost_feasible_point():
+@pytest.mark.parametrize("k", [0, 1])
+def test_restoration_called_at_an_almost_feasible_point(k):
     """IPOPT's BacktrackingLineSearch calls no restoration phase at an almost feasible point (theta <=
     1e-2 tol): it restores the backup acceptable point and stops there as acceptable
     (RestoreAcceptablePoint), or without one the solve ends as a restoration failure ("Restoration phase
-    called, but point is almost feasible").  A ground scenario found by scripts/resto_acc_search.py
-    (tests/golden/resto_acc_cases.json): under the default acceptable_tol (1e-6) no iterate is acceptable,
-    and both restatements end as a restoration failure; with acceptable_tol 1.78e-5 an earlier iterate is
-    stored, and the same iteration restores it and ends as acceptable at that point.  (The degenerate
-    trajectory parts the two restatements by rounding: the compiled one reaches the branch at iteration
-    129, the host one at 176; what is asserted is the branch and its outcome, per restatement.)"""
+    called, but point is almost feasible").  Cases found by scripts/resto_acc_search.py
+    (tests/golden/resto_acc_cases.json), where both restatements (and the engine,
+    test_gpu_solve_engine.py) reach the branch: 0 — a ground scenario at tol 1e-6, where IPOPT's
+    acceptable_tol 1e-6 stores no iterate (a restoration failure) and 1.78e-5 stores one (restored); 1 —
+    a Superquadric scenario under IPOPT's defaults (tol 1e-8, acceptable_tol 1e-6: restored; with no
+    backup point possible, a restoration failure).  The same iteration ends either way, at a different
+    point.  (The degenerate trajectories part the restatements by rounding: the compiled one reaches the
+    branch at iteration 129 / 1 414, the host one at 176 / 903, the device at 183 / 680; what is asserted
+    is the branch and its outcome, per restatement.)"""
     import centroidalplanner_amd.batch_ipm as bi
 
-    prob, x0, c = _resto_case()
+    prob, x0, c = _resto_case(k)
     mass = prob.desc().mass
+    nb, at = c["no_backup_tol"], c["acceptable_tol"]
     out = {}
     try:
-        for at in (1e-6, c["acceptable_tol"]):
-            pyoracle.set_acceptable_tol(at)
+        for a in (nb, at):
+            pyoracle.set_acceptable_tol(a)
             pyoracle.resto_fail_events()
-            out[at] = (pyoracle.solve(prob.desc(), x0, mass, tol=c["tol"], hessian=c["hessian"]),
-                       pyoracle.resto_fail_events())
+            out[a] = (pyoracle.solve(prob.desc(), x0, mass, tol=c["tol"], hessian=c["hessian"]),
+                      pyoracle.resto_fail_events())
     finally:
         pyoracle.set_acceptable_tol(1e-6)
-    (fail, ev0), (back, ev1) = out[1e-6], out[c["acceptable_tol"]]
+    (fail, ev0), (back, ev1) = out[nb], out[at]
     assert pyoracle.STATUS_NAMES[fail["status"]] == "resto_failed" and ev0 == (1, 0)
     assert pyoracle.STATUS_NAMES[back["status"]] == "acceptable" and ev1 == (1, 1)
     assert back["iterations"] == fail["iterations"] and back["objective"] != fail["objective"]
     hs = {}
-    for at in (1e-6, c["acceptable_tol"]):
+    for a in (nb, at):
         log = []
         bi._DEBUG_EVENT = lambda name, mask: log.append(name)
         try:
             h = batch_ipm_solve(prob, torch.as_tensor(x0[None]), torch.as_tensor(np.array([mass])), tol=c["tol"],
                                 max_iter=3000, evaluator=OracleBatchEvaluator(prob, 1), hessian=c["hessian"],
-                                acceptable_tol=at)
+                                acceptable_tol=a)
         finally:
             bi._DEBUG_EVENT = None
-        hs[at] = (int(h.status[0]), int(h.iterations[0]), float(h.objective[0]), "restore_acceptable_point" in log)
-    (hst0, hit0, hobj0, hr0), (hst1, hit1, hobj1, hr1) = hs[1e-6], hs[c["acceptable_tol"]]
+        hs[a] = (int(h.status[0]), int(h.iterations[0]), float(h.objective[0]), "restore_acceptable_point" in log)
+    (hst0, hit0, hobj0, hr0), (hst1, hit1, hobj1, hr1) = hs[nb], hs[at]
     assert hst0 == 4 and not hr0
     assert hst1 == 1 and hr1 and hit1 == hit0 and hobj1 != hobj0
