@@ -277,7 +277,9 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                     fd_step: float = 1e-6, graph: Optional[bool] = None, check_every: int = 4,
                     verbose: int = 0, compact: bool = True, verbose_instance: int = 0,
                     ls_kernel: int = 2, fallback_viol_tol: float = 0.0,
-                    nlp_scaling: str = "gradient-based", jacobian_regularization: str = "pivot") -> BatchSolveResult:
+                    nlp_scaling: str = "gradient-based", jacobian_regularization: str = "pivot",
+                    watchdog: bool = False, watchdog_trigger: int = 10,
+                    watchdog_trial_max: int = 3) -> BatchSolveResult:
     """Solve B instances of `problem`'s template from the starting points X0 [B, n] (torch float64,
     device tensor), per-instance robot masses `mass` [B] (None: the template's).
 
@@ -308,7 +310,14 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     jacobian_regularization: a rank-deficient A (|R_jj| < 1e-10 |R|max): "pivot" (default) adds
     delta_c = 1e-8 mu^0.25 |R|max to R's small pivots; "ipopt" solves IPOPT's [[W, A^T], [A, -delta_c I]]
     (delta_c = 1e-8 mu^0.25) as the augmented system — here and in the engine
-    (cpl_solve_options.jacobian_regularization, csrc/cpl_kkt.hip cpl_kkt_aug_kernel)."""
+    (cpl_solve_options.jacobian_regularization, csrc/cpl_kkt.hip cpl_kkt_aug_kernel).
+    watchdog (host path only, opt-in; the engine has none): IPOPT's watchdog procedure
+    (BacktrackingLineSearch, watchdog_shortened_iter_trigger 10, watchdog_trial_iter_max 3) as the
+    compiled restatement has it (oracle/cpl_solve_host.c, cplo_set_watchdog): after `watchdog_trigger`
+    consecutive shortened steps the iterate and its step are kept; the next iterations take their full
+    step judged against the kept iterate's references, a success ends it, the (trial_max + 1)-th failure
+    restores the kept iterate and backtracks along its step from alpha_max / 2; a barrier change or the
+    restoration phase ends it."""
     if hessian not in ("exact", "fd", "limited-memory"):
         raise ValueError("hessian must be 'exact', 'fd' or 'limited-memory'")
     if nlp_scaling not in ("gradient-based", "none"):
@@ -318,6 +327,9 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
     jac_reg = jacobian_regularization == "ipopt"
     use_bfgs = hessian == "limited-memory"
     import torch
+
+    if watchdog and X0.is_cuda:
+        raise ValueError("watchdog: the host restatement only (the device engine has no watchdog)")
 
     if X0.is_cuda:  # device tensors: the native engine (csrc/cpl_solver.hip) with the product callbacks
         if evaluator is not None and not isinstance(evaluator, KernelEvaluator):
@@ -813,6 +825,13 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         # regular iterate at the acceptable level, restored when the restoration phase fails
         "acc_w": zBw(), "acc_y": zBm(), "acc_zL": zBw(), "acc_zU": zBw(), "has_acc": bool_B(),
     }
+    if watchdog:  # IPOPT's watchdog: its state, the kept iterate, its step, evaluation and references
+        S.update({"in_wd": bool_B(), "wd_cnt": torch.zeros(B, dtype=torch.int64, device=dev),
+                  "wd_trial": torch.zeros(B, dtype=torch.int64, device=dev), "wd_w": zBw(), "wd_y": zBm(),
+                  "wd_zL": zBw(), "wd_zU": zBw(), "wd_dw": zBw(), "wd_dy": zBm(), "wd_dzL": zBw(), "wd_dzU": zBw(),
+                  "wd_f": torch.zeros_like(S["f"]), "wd_grad": torch.zeros_like(S["grad"]),
+                  "wd_g": torch.zeros_like(S["g"]), "wd_J": torch.zeros_like(S["J"]), "wd_th": zB(), "wd_ph": zB(),
+                  "wd_gd": zB(), "wd_alpha": zB()})
 
     def orig_violation(g):
         """max violation of g against the original constraint bounds (NaN: infinite); g is the scaled
@@ -937,8 +956,11 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
             mu = torch.where(upd, torch.clamp(torch.minimum(0.2 * mu, mu ** 1.5), min=mu_min), mu)
             ft, fp, fc = reset_filter(upd, ft, fp, fc)
             # IPOPT's BacktrackingLineSearch::Reset (MonotoneMuUpdate calls it when mu changes): the
-            # filter reset above and the end of the soft restoration phase
+            # filter reset above and the end of the soft restoration phase (and of the watchdog)
             S["in_soft"].copy_(S["in_soft"] & ~upd)
+            if watchdog:
+                S["in_wd"].copy_(S["in_wd"] & ~upd)
+                S["wd_cnt"].copy_(torch.where(upd, 0, S["wd_cnt"]))
         tau = torch.clamp(1.0 - mu, min=0.99)
 
         def primal_step(d):  # fraction to the boundary along d from w
@@ -997,15 +1019,62 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
             take(st, sel, wt_, o_, al, h_)
             return ok_, th_
 
-        alpha = a_max.clone()
+        R = bool_B()  # (watchdog: the instances whose kept iterate is restored this iteration)
+        if watchdog and bool((S["in_wd"] & st["searching"]).any()):
+            # IPOPT's watchdog iteration: one trial, the full step, judged against the kept iterate's
+            # references; acceptable ends the watchdog, else the step is taken anyway up to trial_max
+            # times, after which the kept iterate is restored (StopWatchDog) and searched along its step
+            wd = S["in_wd"] & st["searching"]
+            theta_k = torch.where(wd, S["wd_th"], theta_k)
+            phi_k = torch.where(wd, S["wd_ph"], phi_k)
+            gd = torch.where(wd, S["wd_gd"], gd)
+            switch_ok = torch.where(wd, S["wd_th"] <= theta_min, switch_ok)
+            wt, o = trial_ls(w, dw, a_max, wd, st)
+            th_ = cons(o["g"], wt[:, nf:]).abs().sum(1)
+            ok_, h_ = acceptable(th_, o["f"] + barrier(wt, mu), theta_k, phi_k, gd, S["wd_alpha"], switch_ok,
+                                 theta_max, ft, fp)
+            trial = torch.where(wd & ~ok_, S["wd_trial"] + 1, S["wd_trial"])
+            S["wd_trial"].copy_(trial)
+            tk = wd & (ok_ | (trial <= watchdog_trial_max))
+            take(st, tk, wt, o, a_max, h_)
+            st["searching"] = st["searching"] & ~wd
+            if _DEBUG_EVENT is not None:  # (diagnostics / tests)
+                _DEBUG_EVENT("watchdog_success", wd & ok_)
+                _DEBUG_EVENT("watchdog_restore", wd & ~tk)
+            S["in_wd"].copy_(S["in_wd"] & ~(wd & ok_))
+            R = wd & ~tk
+            if bool(R.any()):
+                S["in_wd"].copy_(S["in_wd"] & ~R)
+                S["wd_cnt"].copy_(torch.where(R, 0, S["wd_cnt"]))
+                for k in ("w", "y", "zL", "zU", "f", "grad", "g", "J"):  # (w, y, zL, zU, cur alias these)
+                    v = S[k]
+                    v.copy_(torch.where(R.view(-1, *([1] * (v.dim() - 1))), S["wd_" + k], v))
+                dw = torch.where(R[:, None], S["wd_dw"], dw)
+                dy = torch.where(R[:, None], S["wd_dy"], dy)
+                dzL = torch.where(R[:, None], S["wd_dzL"], dzL)
+                dzU = torch.where(R[:, None], S["wd_dzU"], dzU)
+                E = errors(cur, w, y, zL, zU)
+                A, gradw, c = E["A"], E["gw"], E["c"]
+                a_max = torch.where(R, primal_step(dw), a_max)
+                a_z = torch.where(R, torch.minimum(max_step(zL, dzL, hasL, 0.0, tau), max_step(zU, dzU, hasU, 0.0, tau)),
+                                  a_z)
+                a_min = torch.where(R, alpha_min_of(theta_k, gd, theta_min), a_min)
+                st["w"] = torch.where(R[:, None], w, st["w"])
+                st["f"] = torch.where(R, cur["f"], st["f"])
+                st["g"] = torch.where(R[:, None], cur["g"], st["g"])
+                st["searching"] = st["searching"] | (R & (0.5 * a_max > a_min))
+        alpha = torch.where(R, 0.5 * a_max, a_max)
+        n_steps = R.to(torch.int64)  # (the watchdog's shortened-step count: halvings before acceptance)
         for ls in range(max(1, max_ls)):
+            if watchdog:  # a restored instance searches from its second trial on (no full step, no SOC)
+                st["searching"] = st["searching"] & ~(R & (ls >= max(1, max_ls) - 1))
             if not bool(st["searching"].any()):
                 break
             wt, o = trial_ls(w, dw, alpha, st["searching"], st)
             ok, th = judge_take(wt, o, alpha)
             if ls == 0:
                 if max_soc > 0:
-                    soc = st["searching"] & (th >= theta_k)
+                    soc = st["searching"] & (th >= theta_k) & ~R
                     c_soc, a_soc, th_old = c, alpha, th
                     ct = cons(o["g"], wt[:, nf:])
                     for _ in range(max_soc):
@@ -1020,7 +1089,21 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
                         th_old = ths
                         ct = cons(os_["g"], ws[:, nf:])
             alpha = torch.where(st["searching"], 0.5 * alpha, alpha)
+            n_steps = n_steps + st["searching"].to(torch.int64)
             st["searching"] = st["searching"] & (alpha > a_min)  # IPOPT: the next trial only above alpha_min
+        if watchdog:  # the shortened-step count; the watchdog starts at this iterate and its step
+            fnd = st["found"]
+            S["wd_cnt"].copy_(torch.where(fnd, torch.where(n_steps == 0, 0, S["wd_cnt"] + 1), S["wd_cnt"]))
+            start = fnd & ~S["in_wd"] & ~soft_now & (S["wd_cnt"] >= watchdog_trigger)
+            if bool(start.any()):
+                if _DEBUG_EVENT is not None:
+                    _DEBUG_EVENT("watchdog_start", start.clone())
+                for k, v in (("w", w), ("y", y), ("zL", zL), ("zU", zU), ("dw", dw), ("dy", dy), ("dzL", dzL),
+                             ("dzU", dzU), ("f", cur["f"]), ("grad", cur["grad"]), ("g", cur["g"]), ("J", cur["J"]),
+                             ("th", theta_k), ("ph", phi_k), ("gd", gd), ("alpha", a_max)):
+                    S["wd_" + k].copy_(torch.where(start.view(-1, *([1] * (v.dim() - 1))), v, S["wd_" + k]))
+                S["in_wd"].copy_(S["in_wd"] | start)
+                S["wd_trial"].copy_(torch.where(start, 0, S["wd_trial"]))
         # tiny steps: the whole fraction-to-the-boundary step
         w_tiny = w + a_max[:, None] * dw
         st["w"] = torch.where(tiny[:, None], w_tiny, st["w"])
@@ -1100,6 +1183,9 @@ def batch_ipm_solve(problem, X0, mass=None, evaluator: Optional[Callable] = None
         ft, fp, fc = augment_filter(failed, ft, fp, fc, theta_k, phi_k)
         if bool(failed.any()):
             enter_resto(failed, w, mu, c, A, zL, zU, cur["f"])
+            if watchdog:  # (the restoration phase ends the watchdog)
+                S["in_wd"].copy_(S["in_wd"] & ~failed)
+                S["wd_cnt"].copy_(torch.where(failed, 0, S["wd_cnt"]))
         S["w"].copy_(torch.where(mv, w_new, w))
         S["y"].copy_(torch.where(failed[:, None], S["y"], y_new))
         S["zL"].copy_(zL_new)

@@ -905,11 +905,11 @@ static void leave_resto(const Prob* P, State* S, const double* w_new) {
  * which the kept iterate is restored and searched along its own step from alpha_max / 2 (no
  * second-order correction).  A barrier-parameter change ends the watchdog (the line search's Reset).
  * IPOPT is absent offline: restated from its published method, parity unpinned. */
-#define WD_TRIGGER 10
-#define WD_TRIAL_MAX 3
+static int WD_TRIGGER = 10, WD_TRIAL_MAX = 3;  /* (cplo_set_watchdog_params: a lower trigger in the tests) */
 static int g_watchdog = 0;
 static int g_trace = -1;  /* CPLO_TRACE set: one line per regular iteration on stderr */
 void cplo_set_watchdog(int on) { g_watchdog = on != 0; }
+void cplo_set_watchdog_params(int trigger, int trial_max) { WD_TRIGGER = trigger; WD_TRIAL_MAX = trial_max; }
 static __thread Eval g_wd_cur;
 /* this thread's watchdog events since the last read: starts, successes, restorations of the kept iterate */
 static __thread long g_wd_events[3];
@@ -1162,7 +1162,7 @@ static void regular_step(Prob* P, State* S, const Errors* E, const Opts* o) {
     S->mu = mu;
     return;
   }
-  if (failed && theta_k <= ALMOST_FEASIBLE * o->tol) {
+  if (failed && th_ref <= ALMOST_FEASIBLE * o->tol) {  /* (th_ref: the current iterate's theta, the kept one after a watchdog restore) */
     /* nor at an almost feasible point (BacktrackingLineSearch: theta <= 1e-2 tol): the backup acceptable
      * point is restored and the solve stops there as acceptable (RestoreAcceptablePoint), or without
      * one it ends as a restoration failure ("Restoration phase called, but point is almost feasible") */

@@ -52,6 +52,8 @@ def _load(path=LIB_PATH):
     lib.cplo_set_watchdog.argtypes = [c_int]
     lib.cplo_set_watchdog.restype = None
     lib.cplo_set_acceptable_tol.argtypes = [c_double]
+    lib.cplo_set_watchdog_params.argtypes = [c_int, c_int]
+    lib.cplo_set_watchdog_params.restype = None
     lib.cplo_set_acceptable_tol.restype = None
     lib.cplo_watchdog_events.argtypes = [ctypes.POINTER(ctypes.c_long)]
     lib.cplo_watchdog_events.restype = None
@@ -221,6 +223,12 @@ def set_watchdog(on):
     """IPOPT's watchdog in the compiled restatement (opt-in, process-wide; the engine has none): the
     measurement of its effect (scripts/watchdog_effect.py)."""
     lib.cplo_set_watchdog(1 if on else 0)
+
+
+def set_watchdog_params(trigger=10, trial_max=3):
+    """The watchdog's watchdog_shortened_iter_trigger / watchdog_trial_iter_max (IPOPT: 10 / 3;
+    process-wide; the tests lower the trigger to compare the restatements where it starts)."""
+    lib.cplo_set_watchdog_params(int(trigger), int(trial_max))
 
 
 def watchdog_events():

@@ -260,3 +260,56 @@ def test_restoration_called_at_an_almost_feasible_point(k):
     (hst0, hit0, hobj0, hr0), (hst1, hit1, hobj1, hr1) = hs[nb], hs[at]
     assert hst0 == 4 and not hr0
     assert hst1 == 1 and hr1 and hit1 == hit0 and hobj1 != hobj0
+
+
+def _watchdog_run(prob, X0, mass, hessian, trigger):
+    """(compiled [(status, iterations, events)], host result, host events [B, 3]) with IPOPT's watchdog at
+    `trigger` shortened steps (IPOPT: 10) in both restatements."""
+    import centroidalplanner_amd.batch_ipm as bi
+
+    B = X0.shape[0]
+    pyoracle.set_watchdog(True)
+    pyoracle.set_watchdog_params(trigger, 3)
+    try:
+        C = []
+        for b in range(B):
+            pyoracle.watchdog_events()
+            r = pyoracle.solve(prob.desc(), X0[b], mass[b], max_iter=3000, hessian=hessian)
+            C.append((r["status"], r["iterations"], pyoracle.watchdog_events(), r["x"]))
+    finally:
+        pyoracle.set_watchdog(False)
+        pyoracle.set_watchdog_params(10, 3)
+    ev = {k: np.zeros(B, dtype=np.int64) for k in ("watchdog_start", "watchdog_success", "watchdog_restore")}
+
+    def dbg(name, mask):
+        if name in ev:
+            ev[name] += mask.numpy().astype(np.int64)
+
+    bi._DEBUG_EVENT = dbg
+    try:
+        h = batch_ipm_solve(prob, torch.as_tensor(X0), torch.as_tensor(mass), evaluator=OracleBatchEvaluator(prob, 4),
+                            max_iter=3000, hessian=hessian, watchdog=True, watchdog_trigger=trigger)
+    finally:
+        bi._DEBUG_EVENT = None
+    return C, h, np.stack([ev["watchdog_start"], ev["watchdog_success"], ev["watchdog_restore"]], 1)
+
+
+def test_watchdog_host_restatement_matches_compiled():
+    """IPOPT's watchdog (BacktrackingLineSearch: watchdog_shortened_iter_trigger, watchdog_trial_iter_max 3)
+    in the host restatement (batch_ipm_solve(watchdog=True), opt-in) against the compiled one
+    (cplo_set_watchdog): at IPOPT's trigger of 10 it never starts on the solve workload (DESIGN.md section
+    5), so the trigger is lowered to 1 here to exercise it.  Exact Hessian, 64 instances: the same status,
+    iteration count and watchdog events (starts, successes, restorations of the kept iterate) per instance.
+    L-BFGS instance 46 (the sample's one restore path: 6 starts, 2 successes, 4 restorations of the kept
+    iterate and backtracking along its step): the same 59 iterations, events and point in both."""
+    prob = solve_problem().GetCplProblem()
+    X0, mass = solve_inputs(prob, 64, seed=21)
+    C, h, ev = _watchdog_run(prob, X0, mass, "exact", 1)
+    assert ev[:, 0].sum() >= 1
+    for b in range(64):
+        assert (int(h.status[b]), int(h.iterations[b])) == C[b][:2], b
+        assert tuple(int(v) for v in ev[b]) == C[b][2], b
+    C, h, ev = _watchdog_run(prob, X0[46:47], mass[46:47], "limited-memory", 1)
+    assert C[0][2] == (6, 2, 4) and tuple(int(v) for v in ev[0]) == (6, 2, 4)
+    assert int(h.status[0]) == C[0][0] == 0 and int(h.iterations[0]) == C[0][1] == 59
+    np.testing.assert_allclose(h.x[0].numpy(), C[0][3], rtol=0, atol=1e-8)
